@@ -1,0 +1,177 @@
+// Python bindings of the gale native library (module gale._C).
+//
+// Kernels take raw device pointers (torch tensors' data_ptr()) and a hipStream_t handle
+// (torch.cuda.current_stream().cuda_stream), so they interoperate with PyTorch-ROCm tensors
+// without linking libtorch. Long-running calls release the GIL.
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include "gale/executor.h"
+#include "gale/kernels.h"
+
+namespace py = pybind11;
+
+namespace gale {
+void bind_host(py::module_& m);  // codec / kafka / engine bindings (host_bindings.cpp)
+}
+
+namespace {
+
+using gale::ConvDesc;
+
+template <typename T>
+T get_or(const py::dict& d, const char* k, T dflt) {
+  return d.contains(k) ? d[k].cast<T>() : dflt;
+}
+
+ConvDesc desc_from_dict(const py::dict& d) {
+  ConvDesc c{};
+  c.H = d["H"].cast<int>();
+  c.W = d["W"].cast<int>();
+  c.Cin = d["Cin"].cast<int>();
+  c.Ho = d["Ho"].cast<int>();
+  c.Wo = d["Wo"].cast<int>();
+  c.Cout = d["Cout"].cast<int>();
+  c.KH = d["KH"].cast<int>();
+  c.KW = d["KW"].cast<int>();
+  c.stride = d["stride"].cast<int>();
+  c.pad = d["pad"].cast<int>();
+  c.K = d["K"].cast<int>();
+  c.Kpad = d["Kpad"].cast<int>();
+  c.Npad = d["Npad"].cast<int>();
+  c.relu = get_or<int>(d, "relu", 0);
+  c.has_res = get_or<int>(d, "has_res", 0);
+  c.res_H = get_or<int>(d, "res_H", c.Ho);
+  c.res_W = get_or<int>(d, "res_W", c.Wo);
+  c.res_C = get_or<int>(d, "res_C", c.Cout);
+  c.res_stride = get_or<int>(d, "res_stride", 1);
+  c.in_f32 = get_or<int>(d, "in_f32", 0);
+  c.out_f32 = get_or<int>(d, "out_f32", 0);
+  c.fp8 = get_or<int>(d, "fp8", 0);
+  c.act_scale = get_or<float>(d, "act_scale", 1.0f);
+  return c;
+}
+
+inline hipStream_t S(uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
+inline void* P(uintptr_t p) { return reinterpret_cast<void*>(p); }
+
+void chk(hipError_t e, const char* what) { gale::check_hip(e, what); }
+
+gale::PlanOp op_from_dict(const py::dict& d) {
+  gale::PlanOp op;
+  op.kind = d["kind"].cast<int>();
+  if (d.contains("conv")) op.conv = desc_from_dict(d["conv"].cast<py::dict>());
+  if (d.contains("p")) {
+    auto v = d["p"].cast<std::vector<int>>();
+    for (size_t i = 0; i < v.size() && i < 8; ++i) op.p[i] = v[i];
+  }
+  op.in = d["in"].cast<int>();
+  op.out = d["out"].cast<int>();
+  op.res = get_or<int>(d, "res", -1);
+  op.w = P(get_or<uintptr_t>(d, "w", 0));
+  op.bias = static_cast<const float*>(P(get_or<uintptr_t>(d, "bias", 0)));
+  op.wscale = static_cast<const float*>(P(get_or<uintptr_t>(d, "wscale", 0)));
+  return op;
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_C, m) {
+  m.doc() = "gale native library: gfx950 kernels, plan executor, host runtime";
+
+  m.def("conv2d",
+        [](py::dict desc, int batch, uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t wscale,
+           uintptr_t res, uintptr_t y, uintptr_t stream) {
+          ConvDesc d = desc_from_dict(desc);
+          chk(gale::conv2d(d, batch, P(x), P(w), static_cast<const float*>(P(bias)),
+                           static_cast<const float*>(P(wscale)), P(res), P(y), S(stream)),
+              "conv2d");
+        },
+        py::arg("desc"), py::arg("batch"), py::arg("x"), py::arg("w"), py::arg("bias"),
+        py::arg("wscale"), py::arg("res"), py::arg("y"), py::arg("stream"));
+  m.def("maxpool2d",
+        [](int batch, int H, int W, int C, int k, int s, int p, int Ho, int Wo, uintptr_t x,
+           uintptr_t y, uintptr_t stream) {
+          chk(gale::maxpool2d(batch, H, W, C, k, s, p, Ho, Wo, P(x), P(y), S(stream)), "maxpool2d");
+        });
+  m.def("avgpool_global", [](int batch, int HW, int C, uintptr_t x, uintptr_t y, uintptr_t stream) {
+    chk(gale::avgpool_global(batch, HW, C, P(x), P(y), S(stream)), "avgpool_global");
+  });
+  m.def("head_pool_dense_softmax",
+        [](int batch, int HW, int C, int N, uintptr_t x, uintptr_t w, uintptr_t b, uintptr_t out,
+           uintptr_t stream) {
+          chk(gale::head_pool_dense_softmax(batch, HW, C, N, P(x),
+                                            static_cast<const float*>(P(w)),
+                                            static_cast<const float*>(P(b)),
+                                            static_cast<float*>(P(out)), S(stream)),
+              "head_pool_dense_softmax");
+        });
+  m.def("softmax_rows", [](int batch, int N, int ld, uintptr_t x, uintptr_t out, uintptr_t stream) {
+    chk(gale::softmax_rows(batch, N, ld, static_cast<const float*>(P(x)),
+                           static_cast<float*>(P(out)), S(stream)),
+        "softmax_rows");
+  });
+  m.def("cast_f32_bf16",
+        [](int64_t n, float scale, float shift, uintptr_t x, uintptr_t y, uintptr_t stream) {
+          chk(gale::cast_f32_bf16(n, scale, shift, static_cast<const float*>(P(x)), P(y),
+                                  S(stream)),
+              "cast_f32_bf16");
+        });
+  m.def("json_parse_instances",
+        [](int nrec, uintptr_t recs, uintptr_t bytes, int per_image, uintptr_t out,
+           uintptr_t stream) {
+          chk(gale::json_parse_instances(nrec, static_cast<const gale::JsonRecord*>(P(recs)),
+                                         static_cast<const uint8_t*>(P(bytes)), per_image,
+                                         static_cast<float*>(P(out)), S(stream)),
+              "json_parse_instances");
+        });
+  m.attr("JSON_RECORD_BYTES") = (int)sizeof(gale::JsonRecord);
+  m.def("memcpy_async",
+        [](uintptr_t dst, uintptr_t src, size_t n, uintptr_t stream) {
+          chk(hipMemcpyAsync(P(dst), P(src), n, hipMemcpyDefault, S(stream)), "memcpy_async");
+        });
+  m.def("stream_sync", [](uintptr_t stream) {
+    py::gil_scoped_release nogil;
+    chk(hipStreamSynchronize(S(stream)), "stream_sync");
+  });
+
+  py::class_<gale::Executor, std::shared_ptr<gale::Executor>>(m, "Executor")
+      .def(py::init([](int device, py::list ops, std::vector<long long> buf_bytes, int max_batch,
+                       int slots, std::vector<int> buckets) {
+             gale::PlanSpec spec;
+             for (auto o : ops) spec.ops.push_back(op_from_dict(o.cast<py::dict>()));
+             spec.buf_bytes_per_image = std::move(buf_bytes);
+             spec.max_batch = max_batch;
+             spec.slots = slots;
+             spec.buckets = std::move(buckets);
+             return std::make_shared<gale::Executor>(device, std::move(spec));
+           }),
+           py::arg("device"), py::arg("ops"), py::arg("buf_bytes"), py::arg("max_batch"),
+           py::arg("slots") = 2, py::arg("buckets") = std::vector<int>{})
+      .def("run",
+           [](gale::Executor& e, int slot, int batch, uintptr_t stream, bool use_graph) {
+             py::gil_scoped_release nogil;
+             e.run(slot, batch, S(stream), use_graph);
+           },
+           py::arg("slot"), py::arg("batch"), py::arg("stream"), py::arg("use_graph") = true)
+      .def("run_on",
+           [](gale::Executor& e, int batch, uintptr_t in, uintptr_t out, uintptr_t stream) {
+             py::gil_scoped_release nogil;
+             e.run_on(batch, P(in), P(out), S(stream));
+           })
+      .def("capture_all",
+           [](gale::Executor& e, uintptr_t stream) {
+             py::gil_scoped_release nogil;
+             e.capture_all(S(stream));
+           })
+      .def("input_ptr", [](gale::Executor& e, int slot) { return (uintptr_t)e.input(slot); })
+      .def("output_ptr", [](gale::Executor& e, int slot) { return (uintptr_t)e.output(slot); })
+      .def("bucket_for", &gale::Executor::bucket_for)
+      .def_property_readonly("buckets", &gale::Executor::buckets)
+      .def_property_readonly("max_batch", &gale::Executor::max_batch)
+      .def_property_readonly("slots", &gale::Executor::slots)
+      .def_property_readonly("device", &gale::Executor::device)
+      .def_property_readonly("graphs_captured", &gale::Executor::graphs_captured);
+
+  gale::bind_host(m);
+}

@@ -1,0 +1,91 @@
+// Model plan executor: runs a flat list of gale kernels on one device/stream and replays each
+// (batch bucket, I/O slot) pair from a captured hipGraph.
+//
+// Replaces the reference's per-tuple `sess.runner().feed("input:0").fetch("output/Softmax:0")
+// .run()` (InferenceBolt.java:81-85): the model is a static plan built once (R6 prepare,
+// InferenceBolt.java:43-62) and every micro-batch is one graph launch.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "gale/kernels.h"
+
+namespace gale {
+
+enum OpKind : int {
+  OP_CONV = 0,      // conv2d (also dense layers as 1x1 convs)
+  OP_MAXPOOL = 1,   // p[0..6] = H, W, C, k, s, pad, Ho ; p[7] = Wo
+  OP_AVGPOOL = 2,   // p[0] = HW, p[1] = C
+  OP_HEAD = 3,      // p[0] = HW, p[1] = C, p[2] = N   (pool + dense(fp32 w) + softmax)
+  OP_SOFTMAX = 4,   // p[0] = N, p[1] = ld
+};
+
+// Buffer ids: 0 = network input (fp32 NHWC), 1 = network output (fp32 [B, classes]),
+// >= 2 = activation workspace.
+struct PlanOp {
+  int kind = 0;
+  ConvDesc conv{};
+  int p[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  int in = 0, out = 0, res = -1;
+  const void* w = nullptr;
+  const float* bias = nullptr;
+  const float* wscale = nullptr;
+};
+
+struct PlanSpec {
+  std::vector<PlanOp> ops;
+  std::vector<long long> buf_bytes_per_image;  // indexed by buffer id (ids 0 and 1 included)
+  int max_batch = 256;
+  int slots = 2;                               // independent I/O buffer sets (pipelining depth)
+  std::vector<int> buckets;                    // graph batch buckets (ascending); empty = powers of 2
+};
+
+class Executor {
+ public:
+  Executor(int device, PlanSpec spec);
+  ~Executor();
+  Executor(const Executor&) = delete;
+  Executor& operator=(const Executor&) = delete;
+
+  int device() const { return device_; }
+  int max_batch() const { return spec_.max_batch; }
+  int slots() const { return spec_.slots; }
+  const std::vector<int>& buckets() const { return buckets_; }
+  int bucket_for(int batch) const;
+
+  // Device I/O buffers of a slot (input fp32 [max_batch, ...], output fp32 [max_batch, classes]).
+  void* input(int slot) const { return bufs_[slot][0]; }
+  void* output(int slot) const { return bufs_[slot][1]; }
+  long long input_bytes_per_image() const { return spec_.buf_bytes_per_image[0]; }
+  long long output_bytes_per_image() const { return spec_.buf_bytes_per_image[1]; }
+
+  // Enqueue the forward for `batch` images of `slot` on `stream`. use_graph replays (capturing on
+  // first use) the graph of the smallest bucket >= batch; otherwise launches kernels eagerly.
+  void run(int slot, int batch, hipStream_t stream, bool use_graph);
+  // Eager forward on caller-provided device buffers (tests / ops API; no graph).
+  void run_on(int batch, const void* in, void* out, hipStream_t stream);
+  void capture_all(hipStream_t stream);  // pre-capture every (bucket, slot) graph
+  int graphs_captured() const;
+
+ private:
+  void launch_all(int batch, void* const* bufs, hipStream_t stream);
+  int device_;
+  PlanSpec spec_;
+  std::vector<int> buckets_;
+  std::vector<std::vector<void*>> bufs_;  // [slot][buffer id]
+  void* shared_ws_ = nullptr;             // activation buffers shared by every slot
+  std::map<std::pair<int, int>, hipGraphExec_t> graphs_;
+  mutable std::mutex mu_;
+  std::mutex capture_mu_;
+  hipStream_t capture_stream_ = nullptr;
+};
+
+void check_hip(hipError_t e, const char* what);
+
+}  // namespace gale

@@ -1,0 +1,79 @@
+// Host-visible declarations of the gale CDNA4 (gfx950) kernels.
+//
+// Every tensor is NHWC. Activations are bf16, the network input is fp32 (as parsed from the
+// InstObj JSON contract, /root/reference/src/main/java/dke/model/data/InstObj.java:8) and the
+// network output is the fp32 softmax (the reference fetches "output/Softmax:0",
+// /root/reference/src/main/java/dke/model/InferenceBolt.java:83).
+//
+// These launchers never allocate or synchronise, so they can be captured into a hipGraph.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace gale {
+
+// Geometry of one convolution (or fully connected layer expressed as a 1x1 convolution over a
+// 1x1 image). Independent of the batch size, which is a launch argument so one descriptor serves
+// every hipGraph batch bucket.
+struct ConvDesc {
+  int H, W, Cin;        // input spatial size and channel count (channel stride of the input)
+  int Ho, Wo, Cout;     // output spatial size; Cout = stored output channels (channel stride of y)
+  int KH, KW, stride, pad;
+  int K;                // true reduction length KH*KW*Cin
+  int Kpad;             // K rounded up to 32 (row stride of the packed weights)
+  int Npad;             // rows of the packed weight matrix (multiple of the n-block)
+  int relu;             // apply ReLU in the epilogue
+  // residual added before the ReLU (ResNet shortcut). res_C < Cout zero-pads the extra channels
+  // and res_stride > 1 subsamples: together they are the parameter-free "option A" shortcut.
+  int has_res, res_H, res_W, res_C, res_stride;
+  int in_f32;           // input tensor is fp32 (network input; converted to bf16 while staging)
+  int out_f32;          // output tensor is fp32 (classifier logits)
+  int fp8;              // weights are OCP e4m3 (fp8 MFMA path); activations quantised per tensor
+  float act_scale;      // fp8 path: activation quantisation scale (x_q = x * act_scale)
+};
+
+// y[B,Ho,Wo,Cout] = act(conv(x, w) + bias (+ residual)).
+// w: [Npad][Kpad] (bf16 or e4m3), k = (kh*KW + kw)*Cin + ci, zero padded.
+// bias: [Npad] fp32 (BatchNorm already folded in). wscale: [Npad] fp32 per-output-channel weight
+// dequant scale (fp8 path only; nullptr otherwise).
+hipError_t conv2d(const ConvDesc& d, int batch, const void* x, const void* w, const float* bias,
+                  const float* wscale, const void* res, void* y, hipStream_t stream);
+
+// Max pooling, NHWC bf16, window k, stride s, symmetric zero... (-inf) padding p.
+hipError_t maxpool2d(int batch, int H, int W, int C, int k, int s, int p, int Ho, int Wo,
+                     const void* x, void* y, hipStream_t stream);
+
+// Global average pooling, NHWC bf16 [B,H,W,C] -> bf16 [B,C].
+hipError_t avgpool_global(int batch, int HW, int C, const void* x, void* y, hipStream_t stream);
+
+// Fused classifier head: optional global average pool over HW, dense layer with fp32 weights
+// w[N][C] + bias[N], then row softmax. x: bf16 [B,HW,C]; out: fp32 [B,N]. One workgroup per image.
+hipError_t head_pool_dense_softmax(int batch, int HW, int C, int N, const void* x, const float* w,
+                                   const float* bias, float* out, hipStream_t stream);
+
+// Row softmax, fp32 [B, ld] -> fp32 [B, N] (first N columns of each row).
+hipError_t softmax_rows(int batch, int N, int ld, const float* x, float* out, hipStream_t stream);
+
+// fp32 -> bf16 cast with optional affine normalisation y = x*scale + shift (n elements).
+hipError_t cast_f32_bf16(int64_t n, float scale, float shift, const float* x, void* y,
+                         hipStream_t stream);
+
+// Quantise fp32 -> OCP e4m3 with a per-tensor scale (used to pack fp8 weights on device).
+hipError_t quant_f32_e4m3(int64_t n, const float* x, const float* row_scale, int row_len, void* y,
+                          hipStream_t stream);
+
+// GPU JSON tokenizer for the InstObj contract: parses every number of each record's value into
+// the fp32 input tensor. recs: [nrec] {byte offset, byte length, first image slot, images}.
+// Host validation has already proven each record rectangular with the model's H*W*C per image,
+// so the kernel only finds number boundaries (block prefix sum) and converts them.
+struct JsonRecord {
+  int64_t off;      // byte offset of the record value inside the staged byte buffer
+  int32_t len;      // value length in bytes
+  int32_t slot;     // first image slot of this record inside the batch
+  int32_t images;   // images in this record
+  int32_t status;   // 0 = ok; written by the kernel: 1 = number count mismatch, 2 = bad number
+};
+hipError_t json_parse_instances(int nrec, const JsonRecord* recs, const uint8_t* bytes,
+                                int per_image, float* out, hipStream_t stream);
+
+}  // namespace gale

@@ -1,0 +1,203 @@
+// Pooling, classifier head and elementwise kernels (NHWC, gfx950).
+//
+// These cover the MaxPool / AvgPool / MatMul+BiasAdd / Softmax ops of the CNN classifiers the
+// reference serves (README.md:16; output tensor "output/Softmax:0", InferenceBolt.java:83).
+// All of them are memory-bound: bf16 traffic is vectorised 16 B per lane (8 channels).
+#include "common.cuh"
+#include "gale/kernels.h"
+
+namespace gale {
+namespace {
+
+__global__ __launch_bounds__(256) void maxpool_kernel(int total, int H, int W, int C8, int k, int s,
+                                                      int p, int Ho, int Wo, const bf16* x,
+                                                      bf16* y) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= total) return;
+  const int cg = i % C8;
+  const int pix = i / C8;
+  const int wo = pix % Wo;
+  const int t = pix / Wo;
+  const int ho = t % Ho;
+  const int n = t / Ho;
+  const int C = C8 * 8;
+  float m[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) m[j] = -3.0e38f;
+  for (int kh = 0; kh < k; ++kh) {
+    const int hi = ho * s - p + kh;
+    if ((unsigned)hi >= (unsigned)H) continue;
+    for (int kw = 0; kw < k; ++kw) {
+      const int wi = wo * s - p + kw;
+      if ((unsigned)wi >= (unsigned)W) continue;
+      const bf16x8 v = ld_bf16x8(x + ((size_t)(n * H + hi) * W + wi) * C + cg * 8);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) m[j] = fmaxf(m[j], (float)v[j]);
+    }
+  }
+  bf16x8 o;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o[j] = (bf16)m[j];
+  *reinterpret_cast<uint4*>(y + (size_t)pix * C + cg * 8) = __builtin_bit_cast(uint4, o);
+}
+
+__global__ __launch_bounds__(256) void avgpool_kernel(int total, int HW, int C8, const bf16* x,
+                                                      bf16* y) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= total) return;
+  const int cg = i % C8;
+  const int n = i / C8;
+  const int C = C8 * 8;
+  float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const bf16* base = x + (size_t)n * HW * C + cg * 8;
+  for (int q = 0; q < HW; ++q) {
+    const bf16x8 v = ld_bf16x8(base + (size_t)q * C);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s[j] += (float)v[j];
+  }
+  const float inv = 1.f / (float)HW;
+  bf16x8 o;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o[j] = (bf16)(s[j] * inv);
+  *reinterpret_cast<uint4*>(y + (size_t)n * C + cg * 8) = __builtin_bit_cast(uint4, o);
+}
+
+// One workgroup per image: pooled[C] -> logits[N] -> softmax, all fp32 in LDS.
+__global__ __launch_bounds__(256) void head_kernel(int HW, int C, int N, const bf16* x,
+                                                   const float* w, const float* bias,
+                                                   float* out) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int C8 = C >> 3;
+  const int nps = 256 / C8 > 0 ? 256 / C8 : 1;  // pixel slices summed in parallel
+  float* part = reinterpret_cast<float*>(smem);            // [nps][C]
+  float* pooled = part + (size_t)nps * C;                  // [C]
+  float* logits = pooled + C;                              // [N]
+  const int n = blockIdx.x;
+  const bf16* img = x + (size_t)n * HW * C;
+  for (int t = threadIdx.x; t < nps * C8; t += 256) {
+    const int cg = t % C8, ps = t / C8;
+    float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int q = ps; q < HW; q += nps) {
+      const bf16x8 v = ld_bf16x8(img + (size_t)q * C + cg * 8);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s[j] += (float)v[j];
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) part[ps * C + cg * 8 + j] = s[j];
+  }
+  __syncthreads();
+  const float inv = 1.f / (float)HW;
+  for (int c = threadIdx.x; c < C; c += 256) {
+    float s = 0.f;
+    for (int ps = 0; ps < nps; ++ps) s += part[ps * C + c];
+    pooled[c] = s * inv;
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int o = wave; o < N; o += 4) {
+    const float* wr = w + (size_t)o * C;
+    float s = 0.f;
+    for (int c = lane; c < C; c += 64) s += wr[c] * pooled[c];
+    s = wave_sum(s);
+    if (lane == 0) logits[o] = s + bias[o];
+  }
+  __syncthreads();
+  if (wave == 0) {
+    float mx = -3.0e38f;
+    for (int o = lane; o < N; o += 64) mx = fmaxf(mx, logits[o]);
+    mx = wave_max(mx);
+    float sum = 0.f;
+    for (int o = lane; o < N; o += 64) {
+      const float e = __expf(logits[o] - mx);
+      logits[o] = e;
+      sum += e;
+    }
+    sum = wave_sum(sum);
+    const float r = 1.f / sum;
+    for (int o = lane; o < N; o += 64) out[(size_t)n * N + o] = logits[o] * r;
+  }
+}
+
+// One wave per row.
+__global__ __launch_bounds__(256) void softmax_kernel(int B, int N, int ld, const float* x,
+                                                      float* out) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= B) return;
+  const float* xr = x + (size_t)row * ld;
+  float mx = -3.0e38f;
+  for (int o = lane; o < N; o += 64) mx = fmaxf(mx, xr[o]);
+  mx = wave_max(mx);
+  float sum = 0.f;
+  for (int o = lane; o < N; o += 64) sum += __expf(xr[o] - mx);
+  sum = wave_sum(sum);
+  const float r = 1.f / sum;
+  for (int o = lane; o < N; o += 64) out[(size_t)row * N + o] = __expf(xr[o] - mx) * r;
+}
+
+__global__ __launch_bounds__(256) void cast_kernel(int64_t n4, float scale, float shift,
+                                                   const float* x, bf16* y) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n4) return;
+  const float4 v = reinterpret_cast<const float4*>(x)[i];
+  bf16x4 o;
+  o[0] = (bf16)(v.x * scale + shift);
+  o[1] = (bf16)(v.y * scale + shift);
+  o[2] = (bf16)(v.z * scale + shift);
+  o[3] = (bf16)(v.w * scale + shift);
+  reinterpret_cast<uint2*>(y)[i] = __builtin_bit_cast(uint2, o);
+}
+
+}  // namespace
+
+hipError_t maxpool2d(int batch, int H, int W, int C, int k, int s, int p, int Ho, int Wo,
+                     const void* x, void* y, hipStream_t stream) {
+  if (batch <= 0) return hipSuccess;
+  if (C % 8) return hipErrorInvalidValue;
+  const int total = batch * Ho * Wo * (C / 8);
+  hipLaunchKernelGGL(maxpool_kernel, dim3((total + 255) / 256), dim3(256), 0, stream, total, H, W,
+                     C / 8, k, s, p, Ho, Wo, reinterpret_cast<const bf16*>(x),
+                     reinterpret_cast<bf16*>(y));
+  return hipGetLastError();
+}
+
+hipError_t avgpool_global(int batch, int HW, int C, const void* x, void* y, hipStream_t stream) {
+  if (batch <= 0) return hipSuccess;
+  if (C % 8) return hipErrorInvalidValue;
+  const int total = batch * (C / 8);
+  hipLaunchKernelGGL(avgpool_kernel, dim3((total + 255) / 256), dim3(256), 0, stream, total, HW,
+                     C / 8, reinterpret_cast<const bf16*>(x), reinterpret_cast<bf16*>(y));
+  return hipGetLastError();
+}
+
+hipError_t head_pool_dense_softmax(int batch, int HW, int C, int N, const void* x, const float* w,
+                                   const float* bias, float* out, hipStream_t stream) {
+  if (batch <= 0) return hipSuccess;
+  if (C % 8 || C > 4096 || N > 4096) return hipErrorInvalidValue;
+  const int C8 = C / 8;
+  const int nps = 256 / C8 > 0 ? 256 / C8 : 1;
+  const size_t lds = ((size_t)nps * C + C + N) * sizeof(float);
+  if (lds > 160 * 1024) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(head_kernel, dim3(batch), dim3(256), lds, stream, HW, C, N,
+                     reinterpret_cast<const bf16*>(x), w, bias, out);
+  return hipGetLastError();
+}
+
+hipError_t softmax_rows(int batch, int N, int ld, const float* x, float* out, hipStream_t stream) {
+  if (batch <= 0) return hipSuccess;
+  hipLaunchKernelGGL(softmax_kernel, dim3((batch + 3) / 4), dim3(256), 0, stream, batch, N, ld, x,
+                     out);
+  return hipGetLastError();
+}
+
+hipError_t cast_f32_bf16(int64_t n, float scale, float shift, const float* x, void* y,
+                         hipStream_t stream) {
+  if (n <= 0) return hipSuccess;
+  if (n % 4) return hipErrorInvalidValue;
+  const int64_t n4 = n / 4;
+  hipLaunchKernelGGL(cast_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, stream, n4,
+                     scale, shift, x, reinterpret_cast<bf16*>(y));
+  return hipGetLastError();
+}
+
+}  // namespace gale

@@ -1,0 +1,160 @@
+// Plan executor (see gale/executor.h).
+#include "gale/executor.h"
+
+#include <algorithm>
+#include <stdexcept>
+
+namespace gale {
+
+void check_hip(hipError_t e, const char* what) {
+  if (e != hipSuccess) {
+    throw std::runtime_error(std::string("HIP error in ") + what + ": " + hipGetErrorString(e));
+  }
+}
+
+Executor::Executor(int device, PlanSpec spec) : device_(device), spec_(std::move(spec)) {
+  if (spec_.buf_bytes_per_image.size() < 2) throw std::invalid_argument("plan needs >= 2 buffers");
+  if (spec_.max_batch <= 0 || spec_.slots <= 0) throw std::invalid_argument("bad max_batch/slots");
+  buckets_ = spec_.buckets;
+  if (buckets_.empty()) {
+    for (int b = 1; b < spec_.max_batch; b *= 2) buckets_.push_back(b);
+    buckets_.push_back(spec_.max_batch);
+  }
+  std::sort(buckets_.begin(), buckets_.end());
+  buckets_.erase(std::unique(buckets_.begin(), buckets_.end()), buckets_.end());
+  if (buckets_.back() < spec_.max_batch) buckets_.push_back(spec_.max_batch);
+
+  check_hip(hipSetDevice(device_), "hipSetDevice");
+  const size_t nb = spec_.buf_bytes_per_image.size();
+  // activation workspace (ids >= 2) shared by all slots: one compute stream per executor
+  size_t ws_total = 0;
+  std::vector<size_t> ws_off(nb, 0);
+  for (size_t i = 2; i < nb; ++i) {
+    ws_off[i] = ws_total;
+    const size_t bytes = (size_t)spec_.buf_bytes_per_image[i] * spec_.max_batch;
+    ws_total += (bytes + 255) & ~size_t(255);
+  }
+  if (ws_total) check_hip(hipMalloc(&shared_ws_, ws_total), "hipMalloc(workspace)");
+  check_hip(hipStreamCreateWithFlags(&capture_stream_, hipStreamNonBlocking), "capture stream");
+  bufs_.resize(spec_.slots);
+  for (int s = 0; s < spec_.slots; ++s) {
+    bufs_[s].assign(nb, nullptr);
+    for (int i = 0; i < 2; ++i) {
+      const size_t bytes = (size_t)spec_.buf_bytes_per_image[i] * spec_.max_batch;
+      check_hip(hipMalloc(&bufs_[s][i], bytes ? bytes : 256), "hipMalloc(io)");
+      check_hip(hipMemset(bufs_[s][i], 0, bytes ? bytes : 256), "hipMemset(io)");
+    }
+    for (size_t i = 2; i < nb; ++i) bufs_[s][i] = static_cast<char*>(shared_ws_) + ws_off[i];
+  }
+}
+
+Executor::~Executor() {
+  hipSetDevice(device_);
+  for (auto& kv : graphs_) hipGraphExecDestroy(kv.second);
+  for (auto& s : bufs_) {
+    if (s.size() >= 2) {
+      hipFree(s[0]);
+      hipFree(s[1]);
+    }
+  }
+  if (shared_ws_) hipFree(shared_ws_);
+  if (capture_stream_) hipStreamDestroy(capture_stream_);
+}
+
+int Executor::bucket_for(int batch) const {
+  for (int b : buckets_)
+    if (b >= batch) return b;
+  return -1;
+}
+
+void Executor::launch_all(int batch, void* const* bufs, hipStream_t stream) {
+  for (const PlanOp& op : spec_.ops) {
+    const void* in = bufs[op.in];
+    void* out = bufs[op.out];
+    hipError_t e = hipSuccess;
+    switch (op.kind) {
+      case OP_CONV:
+        e = conv2d(op.conv, batch, in, op.w, op.bias, op.wscale, op.res >= 0 ? bufs[op.res] : nullptr,
+                   out, stream);
+        break;
+      case OP_MAXPOOL:
+        e = maxpool2d(batch, op.p[0], op.p[1], op.p[2], op.p[3], op.p[4], op.p[5], op.p[6], op.p[7],
+                      in, out, stream);
+        break;
+      case OP_AVGPOOL:
+        e = avgpool_global(batch, op.p[0], op.p[1], in, out, stream);
+        break;
+      case OP_HEAD:
+        e = head_pool_dense_softmax(batch, op.p[0], op.p[1], op.p[2], in,
+                                    static_cast<const float*>(op.w), op.bias,
+                                    static_cast<float*>(out), stream);
+        break;
+      case OP_SOFTMAX:
+        e = softmax_rows(batch, op.p[0], op.p[1], static_cast<const float*>(in),
+                         static_cast<float*>(out), stream);
+        break;
+      default:
+        throw std::invalid_argument("unknown plan op kind");
+    }
+    check_hip(e, "plan op launch");
+  }
+}
+
+void Executor::run_on(int batch, const void* in, void* out, hipStream_t stream) {
+  if (batch > spec_.max_batch) throw std::invalid_argument("batch > max_batch");
+  std::vector<void*> b = bufs_[0];
+  b[0] = const_cast<void*>(in);
+  b[1] = out;
+  launch_all(batch, b.data(), stream);
+}
+
+void Executor::run(int slot, int batch, hipStream_t stream, bool use_graph) {
+  if (slot < 0 || slot >= spec_.slots) throw std::invalid_argument("bad slot");
+  if (batch <= 0) return;
+  if (batch > spec_.max_batch) throw std::invalid_argument("batch > max_batch");
+  if (!use_graph) {
+    launch_all(batch, bufs_[slot].data(), stream);
+    return;
+  }
+  const int bucket = bucket_for(batch);
+  hipGraphExec_t exec = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    auto it = graphs_.find({bucket, slot});
+    if (it != graphs_.end()) exec = it->second;
+  }
+  if (!exec) {
+    // capture on a private non-blocking stream (the legacy null stream cannot capture); the
+    // instantiated graph is then launched on the caller's stream
+    std::lock_guard<std::mutex> cap(capture_mu_);
+    hipGraph_t graph = nullptr;
+    check_hip(hipStreamBeginCapture(capture_stream_, hipStreamCaptureModeThreadLocal),
+              "BeginCapture");
+    try {
+      launch_all(bucket, bufs_[slot].data(), capture_stream_);
+    } catch (...) {
+      hipStreamEndCapture(capture_stream_, &graph);
+      if (graph) hipGraphDestroy(graph);
+      throw;
+    }
+    check_hip(hipStreamEndCapture(capture_stream_, &graph), "EndCapture");
+    check_hip(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0), "GraphInstantiate");
+    hipGraphDestroy(graph);
+    std::lock_guard<std::mutex> lk(mu_);
+    graphs_[{bucket, slot}] = exec;
+  }
+  check_hip(hipGraphLaunch(exec, stream), "hipGraphLaunch");
+}
+
+void Executor::capture_all(hipStream_t stream) {
+  for (int s = 0; s < spec_.slots; ++s)
+    for (int b : buckets_) run(s, b, stream, true);
+  check_hip(hipStreamSynchronize(stream), "capture_all sync");
+}
+
+int Executor::graphs_captured() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  return (int)graphs_.size();
+}
+
+}  // namespace gale

@@ -1,0 +1,404 @@
+"""Network IR for the gale model zoo, parameter packing and plan building.
+
+The reference serves an opaque TF SavedModel (``model/saved_model.pb``, InferenceBolt.java:49-58)
+whose only pinned contract is ``input:0`` (NHWC float) -> ``output/Softmax:0`` (float[N][10],
+:82-86). gale instead describes each supported CNN as a small static layer list. From it we get:
+
+* seeded random initialisation (``init_params``) with BatchNorm statistics calibrated on synthetic
+  data, so random-init networks keep unit-scale activations like trained ones do;
+* BatchNorm folding into conv weight/bias (``fold_params``);
+* one flat packed parameter buffer (``pack_params``) whose layout (``param_layout``) depends only
+  on the architecture, so rank 0 can fill it and RCCL-broadcast it to every other GPU;
+* the executor plan (``build_plan``): a flat list of gfx950 kernels with buffer ids.
+"""
+
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Tuple, Union
+
+import torch
+
+ALIGN = 256  # byte alignment of every packed parameter
+
+
+def round_up(x: int, m: int) -> int:
+    return (x + m - 1) // m * m
+
+
+def stored_channels(c: int) -> int:
+    """Channel stride of an activation tensor in memory (16-B vector loads need multiples of 8)."""
+    return round_up(c, 8)
+
+
+def conv_n_tiles(cout_stored: int) -> int:
+    """Mirror of ``gale::conv_n_tiles`` (csrc/kernels/conv_mfma.hip): 16-channel tiles per n-block."""
+    if cout_stored <= 16:
+        return 1
+    if cout_stored <= 32:
+        return 2
+    if cout_stored <= 64:
+        return 4
+    return 8
+
+
+@dataclass
+class Conv:
+    name: str
+    inp: str
+    out: str
+    cin: int
+    cout: int
+    k: int
+    stride: int = 1
+    pad: int = 0
+    bn: bool = True
+    bias: bool = False
+    relu: bool = True
+    residual: Optional[str] = None
+    res_mode: str = "identity"  # "identity" | "pad" (ResNet option A: subsample + zero channels)
+    out_f32: bool = False  # fp32 output (classifier logits)
+
+
+@dataclass
+class MaxPool:
+    name: str
+    inp: str
+    out: str
+    k: int
+    s: int
+    p: int = 0
+
+
+@dataclass
+class AvgPool:
+    name: str
+    inp: str
+    out: str
+
+
+@dataclass
+class Head:
+    """Global average pool (if spatial) + dense (fp32 weights) + softmax -> network output."""
+
+    name: str
+    inp: str
+    classes: int
+
+
+@dataclass
+class Softmax:
+    name: str
+    inp: str
+    classes: int
+
+
+Layer = Union[Conv, MaxPool, AvgPool, Head, Softmax]
+
+
+@dataclass
+class Network:
+    name: str
+    input_shape: Tuple[int, int, int]  # H, W, C of one image (InstObj.instances[i])
+    classes: int
+    layers: List[Layer]
+    dataset: str = ""
+    shapes: Dict[str, Tuple[int, int, int]] = field(default_factory=dict)
+
+    def __post_init__(self):
+        self.shapes = infer_shapes(self)
+
+    @property
+    def per_image(self) -> int:
+        h, w, c = self.input_shape
+        return h * w * c
+
+    def macs_per_image(self) -> int:
+        total = 0
+        for L in self.layers:
+            if isinstance(L, Conv):
+                ho, wo, _ = self.shapes[L.out]
+                total += ho * wo * L.cout * L.cin * L.k * L.k
+            elif isinstance(L, Head):
+                _, _, c = self.shapes[L.inp]
+                total += c * L.classes
+        return total
+
+
+def infer_shapes(net: Network) -> Dict[str, Tuple[int, int, int]]:
+    shapes = {"input": tuple(net.input_shape)}
+    for L in net.layers:
+        h, w, c = shapes[L.inp]
+        if isinstance(L, Conv):
+            if c != L.cin:
+                raise ValueError(f"{L.name}: input has {c} channels, layer expects {L.cin}")
+            ho = (h + 2 * L.pad - L.k) // L.stride + 1
+            wo = (w + 2 * L.pad - L.k) // L.stride + 1
+            shapes[L.out] = (ho, wo, L.cout)
+            if L.residual is not None:
+                rh, rw, rc = shapes[L.residual]
+                if L.res_mode == "identity" and (rh, rw, rc) != (ho, wo, L.cout):
+                    raise ValueError(f"{L.name}: identity residual shape mismatch")
+                if L.res_mode == "pad" and (rh != ho * 2 or rw != wo * 2 or rc > L.cout):
+                    raise ValueError(f"{L.name}: option-A residual shape mismatch")
+        elif isinstance(L, MaxPool):
+            ho = (h + 2 * L.p - L.k) // L.s + 1
+            wo = (w + 2 * L.p - L.k) // L.s + 1
+            shapes[L.out] = (ho, wo, c)
+        elif isinstance(L, AvgPool):
+            shapes[L.out] = (1, 1, c)
+        elif isinstance(L, (Head, Softmax)):
+            shapes["output"] = (1, 1, L.classes)
+    return shapes
+
+
+# --------------------------------------------------------------------------------------------
+# parameters
+# --------------------------------------------------------------------------------------------
+
+BN_EPS = 1e-5
+
+
+def init_params(net: Network, seed: int = 0, calibrate: bool = True,
+                calib_batch: int = 8) -> Dict[str, torch.Tensor]:
+    """Seeded random init (Kaiming convs, U(0,1)-input BN calibration). fp32 CPU tensors."""
+    g = torch.Generator().manual_seed(seed)
+    p: Dict[str, torch.Tensor] = {}
+    for L in net.layers:
+        if isinstance(L, Conv):
+            fan_in = L.cin * L.k * L.k
+            std = math.sqrt(2.0 / fan_in)
+            p[f"{L.name}.weight"] = torch.randn(L.cout, L.cin, L.k, L.k, generator=g) * std
+            if L.bias or not L.bn:
+                p[f"{L.name}.bias"] = (torch.rand(L.cout, generator=g) - 0.5) * 0.1
+            if L.bn:
+                p[f"{L.name}.bn.gamma"] = 0.5 + torch.rand(L.cout, generator=g) * 0.5
+                p[f"{L.name}.bn.beta"] = (torch.rand(L.cout, generator=g) - 0.5) * 0.2
+                p[f"{L.name}.bn.mean"] = torch.zeros(L.cout)
+                p[f"{L.name}.bn.var"] = torch.ones(L.cout)
+        elif isinstance(L, Head):
+            _, _, c = net.shapes[L.inp]
+            p[f"{L.name}.weight"] = torch.randn(L.classes, c, generator=g) * math.sqrt(1.0 / c) * 2.0
+            p[f"{L.name}.bias"] = (torch.rand(L.classes, generator=g) - 0.5) * 0.1
+    if calibrate and any(isinstance(L, Conv) and L.bn for L in net.layers):
+        from gale.models.reference import calibrate_bn
+
+        x = torch.rand((calib_batch,) + tuple(net.input_shape), generator=g)
+        calibrate_bn(net, p, x)
+    return p
+
+
+def fold_params(net: Network, p: Dict[str, torch.Tensor]) -> Dict[str, torch.Tensor]:
+    """Fold inference BatchNorm into the preceding conv: w' = w*s, b' = beta + (b - mean)*s."""
+    f: Dict[str, torch.Tensor] = {}
+    for L in net.layers:
+        if isinstance(L, Conv):
+            w = p[f"{L.name}.weight"].float()
+            b = p.get(f"{L.name}.bias", torch.zeros(L.cout)).float()
+            if L.bn:
+                s = p[f"{L.name}.bn.gamma"] / torch.sqrt(p[f"{L.name}.bn.var"] + BN_EPS)
+                w = w * s.view(-1, 1, 1, 1)
+                b = p[f"{L.name}.bn.beta"] + (b - p[f"{L.name}.bn.mean"]) * s
+            f[f"{L.name}.weight"] = w.contiguous()
+            f[f"{L.name}.bias"] = b.contiguous()
+        elif isinstance(L, Head):
+            f[f"{L.name}.weight"] = p[f"{L.name}.weight"].float().contiguous()
+            f[f"{L.name}.bias"] = p[f"{L.name}.bias"].float().contiguous()
+    return f
+
+
+# --------------------------------------------------------------------------------------------
+# packing: one flat byte buffer, architecture-determined layout
+# --------------------------------------------------------------------------------------------
+
+
+@dataclass
+class PackedEntry:
+    offset: int
+    nbytes: int
+    dtype: torch.dtype
+    shape: Tuple[int, ...]
+
+
+def _conv_geometry(net: Network, L: Conv) -> Dict[str, int]:
+    h, w, _ = net.shapes[L.inp]
+    ho, wo, _ = net.shapes[L.out]
+    cin_s = L.cin if L.inp == "input" else stored_channels(L.cin)
+    cout_s = stored_channels(L.cout)
+    K = L.k * L.k * cin_s
+    Kpad = round_up(K, 32)
+    nt = conv_n_tiles(cout_s)
+    Npad = round_up(cout_s, nt * 16)
+    return dict(H=h, W=w, Cin=cin_s, Ho=ho, Wo=wo, Cout=cout_s, KH=L.k, KW=L.k, stride=L.stride,
+                pad=L.pad, K=K, Kpad=Kpad, Npad=Npad)
+
+
+def param_layout(net: Network, wdtype: str = "bf16") -> Tuple[Dict[str, PackedEntry], int]:
+    """Byte layout of the packed parameter buffer (depends only on the architecture)."""
+    wbytes = {"bf16": 2, "fp8": 1}[wdtype]
+    layout: Dict[str, PackedEntry] = {}
+    off = 0
+
+    def add(name, nbytes, dtype, shape):
+        nonlocal off
+        layout[name] = PackedEntry(off, nbytes, dtype, tuple(shape))
+        off = round_up(off + nbytes, ALIGN)
+
+    for L in net.layers:
+        if isinstance(L, Conv):
+            gm = _conv_geometry(net, L)
+            wdt = torch.bfloat16 if wdtype == "bf16" else torch.uint8
+            add(f"{L.name}.w", gm["Npad"] * gm["Kpad"] * wbytes, wdt, (gm["Npad"], gm["Kpad"]))
+            add(f"{L.name}.b", gm["Npad"] * 4, torch.float32, (gm["Npad"],))
+            if wdtype == "fp8":
+                add(f"{L.name}.s", gm["Npad"] * 4, torch.float32, (gm["Npad"],))
+        elif isinstance(L, Head):
+            _, _, c = net.shapes[L.inp]
+            cs = stored_channels(c)
+            add(f"{L.name}.w", L.classes * cs * 4, torch.float32, (L.classes, cs))
+            add(f"{L.name}.b", L.classes * 4, torch.float32, (L.classes,))
+    return layout, round_up(off, ALIGN)
+
+
+def pack_conv_weight(w: torch.Tensor, cin_s: int, Npad: int, Kpad: int) -> torch.Tensor:
+    """[cout, cin, kh, kw] fp32 -> [Npad, Kpad] with k = (kh*KW + kw)*cin_s + ci (zero padded)."""
+    cout, cin, kh, kw = w.shape
+    wp = torch.zeros(cout, kh, kw, cin_s, dtype=torch.float32)
+    wp[..., :cin] = w.permute(0, 2, 3, 1)
+    flat = torch.zeros(Npad, Kpad, dtype=torch.float32)
+    flat[:cout, : kh * kw * cin_s] = wp.reshape(cout, -1)
+    return flat
+
+
+def pack_params(net: Network, folded: Dict[str, torch.Tensor], wdtype: str = "bf16") -> torch.Tensor:
+    """Fill the flat packed buffer (uint8 CPU tensor) from folded fp32 parameters."""
+    layout, total = param_layout(net, wdtype)
+    buf = torch.zeros(total, dtype=torch.uint8)
+
+    def put(name: str, t: torch.Tensor):
+        e = layout[name]
+        raw = t.contiguous().view(torch.uint8).reshape(-1)
+        assert raw.numel() == e.nbytes, (name, raw.numel(), e.nbytes)
+        buf[e.offset : e.offset + e.nbytes] = raw
+
+    for L in net.layers:
+        if isinstance(L, Conv):
+            gm = _conv_geometry(net, L)
+            w = pack_conv_weight(folded[f"{L.name}.weight"], gm["Cin"], gm["Npad"], gm["Kpad"])
+            b = torch.zeros(gm["Npad"])
+            b[: L.cout] = folded[f"{L.name}.bias"]
+            if wdtype == "bf16":
+                put(f"{L.name}.w", w.to(torch.bfloat16))
+            else:
+                from gale.models.quant import quantize_rows_e4m3
+
+                q, s = quantize_rows_e4m3(w)
+                put(f"{L.name}.w", q)
+                put(f"{L.name}.s", s)
+            put(f"{L.name}.b", b)
+        elif isinstance(L, Head):
+            _, _, c = net.shapes[L.inp]
+            cs = stored_channels(c)
+            w = torch.zeros(L.classes, cs)
+            w[:, :c] = folded[f"{L.name}.weight"]
+            put(f"{L.name}.w", w)
+            put(f"{L.name}.b", folded[f"{L.name}.bias"])
+    return buf
+
+
+# --------------------------------------------------------------------------------------------
+# executor plan
+# --------------------------------------------------------------------------------------------
+
+OP_CONV, OP_MAXPOOL, OP_AVGPOOL, OP_HEAD, OP_SOFTMAX = 0, 1, 2, 3, 4
+
+
+def _tensor_bytes(net: Network, name: str) -> int:
+    h, w, c = net.shapes[name]
+    if name == "input":
+        return h * w * c * 4
+    return h * w * stored_channels(c) * 2
+
+
+def build_plan(net: Network, base_ptr: int, wdtype: str = "bf16") -> Tuple[List[dict], List[int]]:
+    """Executor plan for a packed parameter buffer living at device address ``base_ptr``.
+
+    Returns (ops, buf_bytes_per_image). Buffer 0 = fp32 input, 1 = fp32 softmax output, >= 2 =
+    bf16 activations assigned by liveness so concurrently-live tensors never share a buffer.
+    """
+    layout, _ = param_layout(net, wdtype)
+    # liveness: last layer index reading each tensor
+    last_use: Dict[str, int] = {}
+    for i, L in enumerate(net.layers):
+        last_use[L.inp] = i
+        if isinstance(L, Conv) and L.residual is not None:
+            last_use[L.residual] = i
+    buf_of: Dict[str, int] = {"input": 0}
+    buf_bytes: List[int] = [_tensor_bytes(net, "input"), net.classes * 4]
+    free: List[int] = []
+    ops: List[dict] = []
+    # fp32 logits tensors (Conv.out_f32) get their own dedicated buffers
+    for i, L in enumerate(net.layers):
+        out_name = getattr(L, "out", "output")
+        if isinstance(L, (Head, Softmax)):
+            buf_of["output"] = 1
+        else:
+            need = _tensor_bytes(net, out_name)
+            if isinstance(L, Conv) and L.out_f32:
+                h, w, c = net.shapes[out_name]
+                need = h * w * stored_channels(c) * 4
+            bid = None
+            for j, b in enumerate(free):
+                bid = b
+                free.pop(j)
+                break
+            if bid is None:
+                bid = len(buf_bytes)
+                buf_bytes.append(0)
+            buf_bytes[bid] = max(buf_bytes[bid], need)
+            buf_of[out_name] = bid
+        if isinstance(L, Conv):
+            gm = _conv_geometry(net, L)
+            d = dict(gm)
+            d["relu"] = int(L.relu)
+            d["in_f32"] = int(L.inp == "input")
+            d["out_f32"] = int(L.out_f32)
+            d["fp8"] = int(wdtype == "fp8")
+            res = -1
+            if L.residual is not None:
+                rh, rw, rc = net.shapes[L.residual]
+                d.update(has_res=1, res_H=rh, res_W=rw, res_C=stored_channels(rc),
+                         res_stride=2 if L.res_mode == "pad" else 1)
+                res = buf_of[L.residual]
+            op = dict(kind=OP_CONV, conv=d, **{"in": buf_of[L.inp]}, out=buf_of[out_name], res=res,
+                      w=base_ptr + layout[f"{L.name}.w"].offset,
+                      bias=base_ptr + layout[f"{L.name}.b"].offset)
+            if wdtype == "fp8":
+                op["wscale"] = base_ptr + layout[f"{L.name}.s"].offset
+            ops.append(op)
+        elif isinstance(L, MaxPool):
+            h, w, c = net.shapes[L.inp]
+            ho, wo, _ = net.shapes[L.out]
+            ops.append(dict(kind=OP_MAXPOOL, p=[h, w, stored_channels(c), L.k, L.s, L.p, ho, wo],
+                            **{"in": buf_of[L.inp]}, out=buf_of[L.out]))
+        elif isinstance(L, AvgPool):
+            h, w, c = net.shapes[L.inp]
+            ops.append(dict(kind=OP_AVGPOOL, p=[h * w, stored_channels(c)],
+                            **{"in": buf_of[L.inp]}, out=buf_of[L.out]))
+        elif isinstance(L, Head):
+            h, w, c = net.shapes[L.inp]
+            ops.append(dict(kind=OP_HEAD, p=[h * w, stored_channels(c), L.classes],
+                            **{"in": buf_of[L.inp]}, out=1,
+                            w=base_ptr + layout[f"{L.name}.w"].offset,
+                            bias=base_ptr + layout[f"{L.name}.b"].offset))
+        elif isinstance(L, Softmax):
+            h, w, c = net.shapes[L.inp]
+            ops.append(dict(kind=OP_SOFTMAX, p=[L.classes, stored_channels(c)],
+                            **{"in": buf_of[L.inp]}, out=1))
+        # release buffers whose tensors die here
+        for t, lu in list(last_use.items()):
+            if lu == i and t in buf_of and buf_of[t] >= 2:
+                free.append(buf_of[t])
+                del last_use[t]
+    return ops, buf_bytes

@@ -1,0 +1,127 @@
+"""PyTorch-facing wrappers of the gale gfx950 kernels (``gale._C``).
+
+Each op takes device tensors, launches the hand-written HIP kernel on the current torch stream
+and returns a new tensor. There is deliberately no eager-PyTorch fallback: if the native library
+is missing or the tensor is not on a GPU the call fails loudly (the serving path must never run
+silently on a non-native implementation).
+"""
+
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from gale._native import native
+from gale.models.graph import conv_n_tiles, pack_conv_weight, round_up
+
+
+def _stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _check(t: torch.Tensor, dtype: torch.dtype, name: str) -> None:
+    if not t.is_cuda:
+        raise RuntimeError(f"gale op: {name} must be a GPU tensor (no CPU fallback)")
+    if t.dtype != dtype:
+        raise TypeError(f"gale op: {name} must be {dtype}, got {t.dtype}")
+    if not t.is_contiguous():
+        raise ValueError(f"gale op: {name} must be contiguous")
+
+
+def pack_conv(w_oihw: torch.Tensor, bias: torch.Tensor, cin_stored: Optional[int] = None,
+              device=None):
+    """Pack an fp32 [Cout, Cin, KH, KW] conv weight for the MFMA kernel.
+
+    Returns (w_packed bf16 [Npad, Kpad], bias fp32 [Npad], desc-geometry dict).
+    """
+    cout, cin, kh, kw = w_oihw.shape
+    cin_s = cin if cin_stored is None else cin_stored
+    cout_s = round_up(cout, 4)
+    K = kh * kw * cin_s
+    Kpad = round_up(K, 32)
+    Npad = round_up(cout_s, conv_n_tiles(cout_s) * 16)
+    wp = pack_conv_weight(w_oihw.float().cpu(), cin_s, Npad, Kpad).to(torch.bfloat16)
+    bp = torch.zeros(Npad)
+    bp[:cout] = bias.float().cpu()
+    dev = device if device is not None else torch.device("cuda")
+    return wp.to(dev), bp.to(dev), dict(Cin=cin_s, Cout=cout_s, KH=kh, KW=kw, K=K, Kpad=Kpad,
+                                        Npad=Npad)
+
+
+def conv2d(x: torch.Tensor, w_packed: torch.Tensor, bias: torch.Tensor, geom: dict, stride: int = 1,
+           pad: int = 0, relu: bool = False, residual: Optional[torch.Tensor] = None,
+           res_mode: str = "identity", out_f32: bool = False) -> torch.Tensor:
+    """NHWC conv on MFMA. x: [B,H,W,Cin] bf16 (or fp32 for the network input)."""
+    B, H, W, C = x.shape
+    if C != geom["Cin"]:
+        raise ValueError(f"x has {C} channels, packed weight expects {geom['Cin']}")
+    _check(w_packed, torch.bfloat16, "w_packed")
+    _check(bias, torch.float32, "bias")
+    if x.dtype not in (torch.bfloat16, torch.float32):
+        raise TypeError("x must be bf16 or fp32")
+    _check(x, x.dtype, "x")
+    kh, kw = geom["KH"], geom["KW"]
+    Ho = (H + 2 * pad - kh) // stride + 1
+    Wo = (W + 2 * pad - kw) // stride + 1
+    cout = geom["Cout"]
+    y = torch.empty(B, Ho, Wo, cout, device=x.device,
+                    dtype=torch.float32 if out_f32 else torch.bfloat16)
+    d = dict(geom, H=H, W=W, Ho=Ho, Wo=Wo, stride=stride, pad=pad, relu=int(relu),
+             in_f32=int(x.dtype == torch.float32), out_f32=int(out_f32))
+    res_ptr = 0
+    if residual is not None:
+        _check(residual, torch.bfloat16, "residual")
+        _, rh, rw, rc = residual.shape
+        d.update(has_res=1, res_H=rh, res_W=rw, res_C=rc, res_stride=2 if res_mode == "pad" else 1)
+        res_ptr = residual.data_ptr()
+    native().conv2d(d, B, x.data_ptr(), w_packed.data_ptr(), bias.data_ptr(), 0, res_ptr,
+                    y.data_ptr(), _stream())
+    return y
+
+
+def maxpool2d(x: torch.Tensor, k: int, s: int, p: int = 0) -> torch.Tensor:
+    _check(x, torch.bfloat16, "x")
+    B, H, W, C = x.shape
+    Ho = (H + 2 * p - k) // s + 1
+    Wo = (W + 2 * p - k) // s + 1
+    y = torch.empty(B, Ho, Wo, C, device=x.device, dtype=torch.bfloat16)
+    native().maxpool2d(B, H, W, C, k, s, p, Ho, Wo, x.data_ptr(), y.data_ptr(), _stream())
+    return y
+
+
+def avgpool_global(x: torch.Tensor) -> torch.Tensor:
+    _check(x, torch.bfloat16, "x")
+    B, H, W, C = x.shape
+    y = torch.empty(B, C, device=x.device, dtype=torch.bfloat16)
+    native().avgpool_global(B, H * W, C, x.data_ptr(), y.data_ptr(), _stream())
+    return y
+
+
+def head(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """Global avg pool + dense(fp32 w [N, C]) + softmax. x: [B,H,W,C] bf16 -> [B,N] fp32."""
+    _check(x, torch.bfloat16, "x")
+    _check(w, torch.float32, "w")
+    _check(b, torch.float32, "b")
+    B, H, W, C = x.shape
+    N = w.shape[0]
+    out = torch.empty(B, N, device=x.device, dtype=torch.float32)
+    native().head_pool_dense_softmax(B, H * W, C, N, x.data_ptr(), w.data_ptr(), b.data_ptr(),
+                                     out.data_ptr(), _stream())
+    return out
+
+
+def softmax(x: torch.Tensor, n: Optional[int] = None) -> torch.Tensor:
+    _check(x, torch.float32, "x")
+    B, ld = x.shape
+    n = ld if n is None else n
+    out = torch.empty(B, n, device=x.device, dtype=torch.float32)
+    native().softmax_rows(B, n, ld, x.data_ptr(), out.data_ptr(), _stream())
+    return out
+
+
+def cast_bf16(x: torch.Tensor, scale: float = 1.0, shift: float = 0.0) -> torch.Tensor:
+    _check(x, torch.float32, "x")
+    y = torch.empty(x.shape, device=x.device, dtype=torch.bfloat16)
+    native().cast_f32_bf16(x.numel(), scale, shift, x.data_ptr(), y.data_ptr(), _stream())
+    return y

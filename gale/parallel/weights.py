@@ -1,0 +1,39 @@
+"""Weight materialisation for data-parallel replicas.
+
+The reference has every InferenceBolt task copy ``model/saved_model.pb`` out of the jar and load
+its own copy (InferenceBolt.java:48-58). gale initialises (or loads) the packed parameter buffer
+once on the source rank and broadcasts it over RCCL (xGMI) to every other GPU in ONE collective:
+the buffer layout depends only on the architecture (``param_layout``), so receivers allocate it
+without knowing any values.
+"""
+
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+from gale.models.graph import Network, fold_params, init_params, pack_params, param_layout
+
+
+def host_packed_params(net: Network, seed: int = 0, wdtype: str = "bf16",
+                       params: Optional[dict] = None) -> torch.Tensor:
+    if params is None:
+        params = init_params(net, seed=seed)
+    return pack_params(net, fold_params(net, params), wdtype)
+
+
+def materialize_weights(net: Network, device: torch.device, seed: int = 0, wdtype: str = "bf16",
+                        src: int = 0, group=None, params: Optional[dict] = None) -> torch.Tensor:
+    """Return the packed parameter buffer on ``device``, identical on every rank of ``group``."""
+    _, total = param_layout(net, wdtype)
+    distributed = dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1
+    rank = dist.get_rank() if distributed else src
+    if rank == src:
+        buf = host_packed_params(net, seed, wdtype, params).to(device)
+    else:
+        buf = torch.empty(total, dtype=torch.uint8, device=device)
+    if distributed:
+        dist.broadcast(buf, src=src, group=group)  # RCCL over xGMI with the "nccl" backend
+    return buf

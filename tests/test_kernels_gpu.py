@@ -1,0 +1,149 @@
+"""Numerics of the hand-written gfx950 kernels against plain PyTorch fp32 references.
+
+Operands are asymmetric random data (cdna_hip_programming.md §3: a symmetric operand hides a
+transposed C-write). Tolerances are bf16-level: inputs/weights are rounded to bf16 and the
+reference uses the same rounded values, so the remaining error is fp32-accumulation order plus
+the bf16 rounding of the output.
+"""
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from gale import ops
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _ref_conv(x_nhwc, w, b, stride, pad, relu, res=None, res_mode="identity"):
+    x = x_nhwc.float().permute(0, 3, 1, 2)
+    y = F.conv2d(x, w.float(), b.float(), stride=stride, padding=pad)
+    if res is not None:
+        r = res.float().permute(0, 3, 1, 2)
+        if res_mode == "pad":
+            r = r[:, :, ::2, ::2]
+            r = F.pad(r, (0, 0, 0, 0, 0, y.shape[1] - r.shape[1]))
+        y = y + r
+    if relu:
+        y = F.relu(y)
+    return y.permute(0, 2, 3, 1)
+
+
+CONV_CASES = [
+    # B, H, W, Cin, Cout, k, stride, pad, in_f32
+    (3, 32, 32, 3, 16, 3, 1, 1, True),      # ResNet-20 stem (gather, fp32 input)
+    (2, 28, 28, 1, 8, 5, 1, 2, True),       # LeNet conv1
+    (4, 32, 32, 16, 16, 3, 1, 1, False),    # ResNet-20 stage 1
+    (4, 32, 32, 16, 32, 3, 2, 1, False),    # stage 2 downsample
+    (3, 16, 16, 32, 32, 3, 1, 1, False),
+    (5, 8, 8, 64, 64, 3, 1, 1, False),      # stage 3
+    (2, 5, 5, 16, 120, 5, 1, 0, False),     # LeNet fc1 as a 5x5 valid conv
+    (3, 14, 14, 64, 256, 1, 1, 0, False),   # ResNet-50 1x1 expand (n-blocks > 1)
+    (2, 14, 14, 256, 128, 1, 2, 0, False),  # 1x1 stride-2 projection
+    (2, 7, 7, 512, 512, 3, 1, 1, False),    # K = 4608: K-chunked (non weight-stationary)
+    (1, 56, 56, 64, 64, 3, 1, 1, False),
+]
+
+
+@pytest.mark.parametrize("case", CONV_CASES)
+@pytest.mark.parametrize("relu", [False, True])
+def test_conv2d_matches_torch(case, relu):
+    B, H, W, Cin, Cout, k, s, p, in_f32 = case
+    g = torch.Generator().manual_seed(1234 + Cin * 7 + Cout)
+    x = torch.randn(B, H, W, Cin, generator=g)
+    w = torch.randn(Cout, Cin, k, k, generator=g) / (Cin * k * k) ** 0.5
+    b = torch.randn(Cout, generator=g) * 0.1
+    xq = x if in_f32 else x.to(torch.bfloat16)
+    wq = w.to(torch.bfloat16).float()
+    wp, bp, geom = ops.pack_conv(w, b)
+    y = ops.conv2d(xq.to(DEV), wp, bp, geom, stride=s, pad=p, relu=relu)
+    ref = _ref_conv(xq.to(torch.bfloat16).float(), wq, b, s, p, relu)
+    torch.cuda.synchronize()
+    got = y.float().cpu()[..., :Cout]
+    err = (got - ref).abs().max().item()
+    scale = ref.abs().max().item() + 1e-6
+    assert err <= 2e-2 * scale + 1e-2, f"max err {err} (scale {scale})"
+
+
+@pytest.mark.parametrize("mode", ["identity", "pad"])
+def test_conv2d_residual(mode):
+    g = torch.Generator().manual_seed(7)
+    B, H, Cin, Cout = 3, 16, 16 if mode == "pad" else 32, 32
+    s = 2 if mode == "pad" else 1
+    Hin = H * s
+    x = torch.randn(B, Hin, Hin, Cin, generator=g).to(torch.bfloat16)
+    w = torch.randn(Cout, Cin, 3, 3, generator=g) / (Cin * 9) ** 0.5
+    b = torch.randn(Cout, generator=g) * 0.1
+    res_c = Cin if mode == "pad" else Cout
+    res = torch.randn(B, Hin if mode == "pad" else H, Hin if mode == "pad" else H, res_c,
+                      generator=g).to(torch.bfloat16)
+    wp, bp, geom = ops.pack_conv(w, b)
+    y = ops.conv2d(x.to(DEV), wp, bp, geom, stride=s, pad=1, relu=True, residual=res.to(DEV),
+                   res_mode=mode)
+    ref = _ref_conv(x.float(), w.to(torch.bfloat16).float(), b, s, 1, True, res=res, res_mode=mode)
+    err = (y.float().cpu() - ref).abs().max().item()
+    assert err <= 2e-2 * ref.abs().max().item() + 1e-2
+
+
+def test_conv2d_identity_weight_asymmetric():
+    """A = I check: a 1x1 conv with identity weights must reproduce an asymmetric input exactly."""
+    B, H, C = 2, 8, 64
+    x = (torch.arange(B * H * H * C, dtype=torch.float32).reshape(B, H, H, C) % 97) / 8.0
+    x = x.to(torch.bfloat16)
+    w = torch.eye(C).reshape(C, C, 1, 1)
+    wp, bp, geom = ops.pack_conv(w, torch.zeros(C))
+    y = ops.conv2d(x.to(DEV), wp, bp, geom)
+    assert torch.equal(y.cpu(), x)
+
+
+def test_conv2d_fc_out_f32():
+    g = torch.Generator().manual_seed(3)
+    B, K, N = 9, 2048, 1000
+    x = torch.randn(B, 1, 1, K, generator=g).to(torch.bfloat16)
+    w = torch.randn(N, K, 1, 1, generator=g) / K ** 0.5
+    b = torch.randn(N, generator=g)
+    wp, bp, geom = ops.pack_conv(w, b)
+    y = ops.conv2d(x.to(DEV), wp, bp, geom, out_f32=True)
+    assert y.dtype == torch.float32
+    ref = x.float().reshape(B, K) @ w.reshape(N, K).to(torch.bfloat16).float().t() + b
+    err = (y.cpu().reshape(B, N) - ref).abs().max().item()
+    assert err < 1e-2 * ref.abs().max().item() + 1e-3
+
+
+@pytest.mark.parametrize("k,s,p", [(2, 2, 0), (3, 2, 1)])
+def test_maxpool(k, s, p):
+    x = torch.randn(3, 28, 28, 16).to(torch.bfloat16)
+    y = ops.maxpool2d(x.to(DEV), k, s, p).cpu()
+    ref = F.max_pool2d(x.float().permute(0, 3, 1, 2), k, s, p).permute(0, 2, 3, 1)
+    assert torch.equal(y.float(), ref)
+
+
+def test_avgpool_and_head_and_softmax():
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(6, 8, 8, 64, generator=g).to(torch.bfloat16)
+    pooled = ops.avgpool_global(x.to(DEV)).float().cpu()
+    ref_pool = x.float().mean(dim=(1, 2))
+    assert (pooled - ref_pool).abs().max().item() < 1e-2
+    w = torch.randn(10, 64, generator=g) * 0.3
+    b = torch.randn(10, generator=g) * 0.1
+    probs = ops.head(x.to(DEV), w.to(DEV), b.to(DEV)).cpu()
+    ref = torch.softmax(ref_pool @ w.t() + b, dim=1)
+    assert (probs - ref).abs().max().item() < 1e-4
+    assert torch.allclose(probs.sum(1), torch.ones(6), atol=1e-5)
+    logits = torch.randn(5, 1000, generator=g) * 3
+    sm = ops.softmax(logits.to(DEV)).cpu()
+    assert (sm - torch.softmax(logits, 1)).abs().max().item() < 1e-6
+
+
+def test_cast():
+    x = torch.randn(1024)
+    y = ops.cast_bf16(x.to(DEV), 2.0, 0.5).cpu()
+    assert torch.equal(y, (x * 2.0 + 0.5).to(torch.bfloat16))
+
+
+def test_no_cpu_fallback():
+    w, b, geom = ops.pack_conv(torch.randn(16, 16, 3, 3), torch.zeros(16))
+    with pytest.raises(RuntimeError):
+        ops.conv2d(torch.randn(1, 8, 8, 16).to(torch.bfloat16), w, b, geom)

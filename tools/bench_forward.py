@@ -1,0 +1,52 @@
+"""GPU-only forward throughput of a model replica (hipGraph replay), for kernel work.
+
+Not the headline metric (that is bench.py: end-to-end Kafka -> JSON -> GPU -> JSON -> Kafka).
+"""
+
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+from gale.models import get_model  # noqa: E402
+from gale.parallel.weights import materialize_weights  # noqa: E402
+from gale.runtime.replica import ModelReplica  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--model", default="resnet20")
+    ap.add_argument("--batches", default="1,64,256,1024,4096")
+    ap.add_argument("--iters", type=int, default=50)
+    ap.add_argument("--eager", action="store_true")
+    a = ap.parse_args()
+    net = get_model(a.model)
+    dev = torch.device("cuda", 0)
+    packed = materialize_weights(net, dev)
+    bs = [int(b) for b in a.batches.split(",")]
+    rep = ModelReplica(net, packed, max_batch=max(bs), slots=1, buckets=bs)
+    s = torch.cuda.current_stream().cuda_stream
+    res = []
+    for b in bs:
+        for _ in range(3):
+            rep.executor.run(0, b, s, not a.eager)
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        for _ in range(a.iters):
+            rep.executor.run(0, b, s, not a.eager)
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t) / a.iters
+        flops = 2 * net.macs_per_image() * b
+        r = dict(model=a.model, batch=b, ms=dt * 1e3, img_s=b / dt, tflops=flops / dt / 1e12,
+                 graph=not a.eager)
+        res.append(r)
+        print(json.dumps(r), flush=True)
+
+
+if __name__ == "__main__":
+    main()
