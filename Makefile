@@ -13,7 +13,7 @@ HIP_FLAGS := --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 -Icsrc/include -Icsrc/k
              -Wno-unused-result
 CXX_FLAGS := -O3 -fPIC -std=c++17 -D__HIP_PLATFORM_AMD__ -I$(ROCM)/include -Icsrc/include \
              -I$(PY_INC) -I$(PYBIND_INC) -mavx2 -mfma -msse4.2 -mpclmul -mbmi2 -pthread \
-             -fvisibility=hidden -Wall -Wno-unused-function
+             -fvisibility=hidden -Wall -Wno-unused-function -Wno-unused-result
 
 HIP_SRC   := $(wildcard csrc/kernels/*.hip)
 CXX_SRC   := $(wildcard csrc/runtime/*.cpp) $(wildcard csrc/codec/*.cpp) \

@@ -1,0 +1,175 @@
+#!/usr/bin/env python3
+"""Headline benchmark (BASELINE.json): whole-node images/s + p50 latency of the streaming
+inference topology, CIFAR-10 ResNet-20 bf16, one data-parallel replica per GPU.
+
+What one rank (= one GPU, launched by torch.distributed.run for N > 1) does:
+
+* starts an embedded Kafka-protocol broker on 127.0.0.1 (one Kafka partition per replica,
+  BASELINE config 3) and preloads its input topic with synthetic InstObj records
+  ``{"instances": [[[[...32x32x3 Java-formatted floats...]]]]}`` (~35 KB of JSON per image);
+* initialises ResNet-20 weights on rank 0 (seeded random init) and RCCL-broadcasts the packed
+  buffer over xGMI to every other rank;
+* runs the full gale engine: Kafka Fetch over TCP -> envelope scan -> micro-batcher -> pinned
+  staging -> H2D -> GPU JSON parse -> hipGraph ResNet-20 forward -> D2H softmax ->
+  {"predictions": ...} encode -> Kafka Produce (acks=1) -> ack.
+
+A "step" is ``--batch`` images completing that whole path (acknowledged by the broker). W warmup
+steps run first (graphs are captured before that), then exactly K timed steps, bracketed by a
+barrier + ``torch.cuda.synchronize()``. ``value`` is the whole-job aggregate images/s (sum over
+ranks of timed images / the slowest rank's time). p50 latency = median time from a record's
+fetch to its output record's produce-ack, over all timed records of rank 0 (queue included).
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "images/sec (whole node) + p50 latency, CIFAR-10 ResNet-20 at 1/2/4/8 GPUs"
+
+
+def parse_args():
+    ap = argparse.ArgumentParser(description=__doc__.split("\n\n")[0])
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--model", default="resnet20", choices=["lenet5", "resnet20", "resnet50"])
+    ap.add_argument("--batch", type=int, default=256, help="images per step per GPU")
+    ap.add_argument("--images-per-record", type=int, default=1)
+    ap.add_argument("--distinct", type=int, default=1024, help="distinct synthetic images")
+    ap.add_argument("--source-parallelism", type=int, default=2)
+    ap.add_argument("--sink-parallelism", type=int, default=2)
+    ap.add_argument("--replicas-per-gpu", type=int, default=1)
+    ap.add_argument("--max-wait-us", type=int, default=2000)
+    ap.add_argument("--queue-batches", type=int, default=4,
+                    help="records buffered in the engine, in units of --batch")
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp8"])
+    ap.add_argument("--stub", action="store_true", help="CPU stub replicas (no GPU)")
+    ap.add_argument("--timeout", type=float, default=600.0)
+    return ap.parse_args()
+
+
+def main() -> int:
+    a = parse_args()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    import torch.distributed as dist
+
+    use_gpu = not a.stub
+    if use_gpu and not torch.cuda.is_available():
+        raise SystemExit("bench.py: no GPU visible (use --stub for the CPU plumbing run)")
+    if use_gpu:
+        torch.cuda.set_device(local_rank)
+    if world > 1:
+        dist.init_process_group(backend="nccl" if use_gpu else "gloo",
+                                device_id=torch.device("cuda", local_rank) if use_gpu else None)
+
+    from gale._native import native
+    from gale.config import GaleConfig
+    from gale.data import encode_batches, encode_records, preload, synthetic_images
+    from gale.engine import Engine
+    from gale.models import get_model
+
+    net = get_model(a.model)
+    K = native().kafka
+    ipr = a.images_per_record
+    rpb = 64  # records per preloaded RecordBatch
+    broker = K.Broker(max_message_bytes=256 << 20, retention_bytes=1 << 62)
+    broker.start()
+    broker.create_topic("gale-in", 1)
+    broker.create_topic("gale-out", 1)
+    # slack: the warm-up engine drains everything it fetched (queue + in-flight fetches)
+    per_rank_images = (a.warmup + a.steps + 4) * a.batch + 8192 * ipr + 4 * a.queue_batches * a.batch
+    n_records = -(-per_rank_images // ipr)
+    distinct = max(rpb, (a.distinct // (ipr * rpb)) * rpb) * ipr
+    imgs = synthetic_images(distinct, net.input_shape, seed=1234 + rank)
+    batches = encode_batches(encode_records(imgs, ipr), rpb)
+    preload(broker, "gale-in", 0, batches, n_records, rpb)
+    del imgs
+
+    cfg = GaleConfig(topology_name=f"bench-r{rank}", input_topic="gale-in",
+                     output_topic="gale-out", bootstrap=f"127.0.0.1:{broker.port}",
+                     group_id="bench", start_offset="earliest", model=a.model, dtype=a.dtype,
+                     max_batch=a.batch, max_wait_us=a.max_wait_us,
+                     queue_depth=max(1, a.queue_batches * a.batch // ipr),
+                     source_parallelism=a.source_parallelism,
+                     sink_parallelism=a.sink_parallelism, replicas=a.replicas_per_gpu,
+                     stub=a.stub, commit_interval_ms=500)
+    devices = [local_rank] if use_gpu else None
+    warm_records = -(-a.warmup * a.batch // ipr)
+    eng = Engine(cfg, devices=devices, max_records=max(1, warm_records))  # weights: RCCL bcast
+    eng.start()
+    eng.wait(a.timeout)
+    eng.stop()
+    warm_done = eng.completed
+
+    timed_records = -(-a.steps * a.batch // ipr)
+    cfg.start_offset = "committed"
+    eng2 = Engine(cfg, devices=devices, max_records=timed_records,
+                  model_replicas=eng.model_replicas if use_gpu else None)
+    if world > 1:
+        dist.barrier()
+    if use_gpu:
+        torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    eng2.start()
+    reached = eng2.wait(a.timeout)
+    if use_gpu:
+        torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+    st = eng2.stats()
+    eng2.stop()
+    broker.stop()
+    if not reached:
+        raise SystemExit(f"rank {rank}: timed out after {elapsed:.1f}s "
+                         f"({eng2.completed}/{timed_records} records)")
+    images = timed_records * ipr
+    t = torch.tensor([elapsed, float(images)], dtype=torch.float64)
+    if world > 1:
+        tt = t.cuda() if use_gpu else t
+        mx = tt.clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        sm = tt.clone()
+        dist.all_reduce(sm, op=dist.ReduceOp.SUM)
+        elapsed_max, total_images = float(mx[0]), float(sm[1])
+    else:
+        elapsed_max, total_images = elapsed, float(images)
+    if rank == 0:
+        value = total_images / elapsed_max
+        out = {
+            "metric": METRIC, "value": round(value, 1), "unit": "images/s", "n_gpus": world,
+            "steps": a.steps, "warmup": a.warmup,
+            "ms_per_step": round(elapsed_max / a.steps * 1e3, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": a.dtype,
+            "data": "synthetic (uniform [0,1) CIFAR-shaped InstObj JSON records, Java float "
+                    "format, preloaded into an embedded Kafka-protocol broker); random-init "
+                    "weights (seed 0) RCCL-broadcast from rank 0",
+            "config": {"model": a.model, "global_batch": a.batch * world, "seq_len": None,
+                       "parallelism": f"dp{world}", "images_per_record": ipr,
+                       "max_wait_us": a.max_wait_us, "replicas_per_gpu": a.replicas_per_gpu,
+                       "path": "kafka-fetch->gpu-json-parse->hipgraph-forward->kafka-produce"},
+            "p50_latency_ms": round(st["e2e_us_p50"] / 1e3, 3),
+            "p99_latency_ms": round(st["e2e_us_p99"] / 1e3, 3),
+            "device_ms_p50": round(st["device_us_p50"] / 1e3, 3),
+            "batch_images_mean": round(st["batch_images_mean"], 1),
+            "json_mb_per_s_rank0": round(st["bytes_in"] / elapsed / 1e6, 1),
+            "warmup_records": warm_done,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

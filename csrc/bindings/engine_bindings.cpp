@@ -1,0 +1,111 @@
+// Python bindings of the serving engine (gale._C.Engine).
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include "../runtime/engine.h"
+#include "gale/executor.h"
+
+namespace py = pybind11;
+
+namespace gale {
+
+namespace {
+
+template <typename T>
+void opt(const py::dict& d, const char* k, T& dst) {
+  if (d.contains(k) && !d[k].is_none()) dst = d[k].cast<T>();
+}
+
+EngineConfig config_from_dict(const py::dict& d) {
+  EngineConfig c;
+  opt(d, "bootstrap", c.bootstrap);
+  opt(d, "input_topic", c.input_topic);
+  opt(d, "output_topic", c.output_topic);
+  opt(d, "group_id", c.group_id);
+  opt(d, "client_id", c.client_id);
+  opt(d, "partitions", c.partitions);
+  opt(d, "source_parallelism", c.source_parallelism);
+  opt(d, "start_offset", c.start_offset);
+  opt(d, "fetch_max_wait_ms", c.fetch_max_wait_ms);
+  opt(d, "fetch_max_bytes", c.fetch_max_bytes);
+  opt(d, "partition_max_bytes", c.partition_max_bytes);
+  opt(d, "check_crcs", c.check_crcs);
+  opt(d, "commit_interval_ms", c.commit_interval_ms);
+  opt(d, "sink_parallelism", c.sink_parallelism);
+  opt(d, "acks", c.acks);
+  opt(d, "sink_mode", c.sink_mode);
+  opt(d, "linger_ms", c.linger_ms);
+  opt(d, "batch_size", c.batch_size);
+  opt(d, "value_format", c.value_format);
+  opt(d, "type_id_header", c.type_id_header);
+  opt(d, "on_error", c.on_error);
+  opt(d, "H", c.H);
+  opt(d, "W", c.W);
+  opt(d, "C", c.C);
+  opt(d, "classes", c.classes);
+  opt(d, "max_batch", c.max_batch);
+  opt(d, "max_wait_us", c.max_wait_us);
+  opt(d, "queue_depth", c.queue_depth);
+  opt(d, "watchdog_ms", c.watchdog_ms);
+  opt(d, "fault", c.fault);
+  opt(d, "max_records", c.max_records);
+  opt(d, "seed", c.seed);
+  return c;
+}
+
+}  // namespace
+
+void bind_engine(py::module_& m) {
+  py::class_<Engine, std::shared_ptr<Engine>>(m, "Engine")
+      .def(py::init([](py::dict cfg) { return std::make_shared<Engine>(config_from_dict(cfg)); }))
+      .def("add_stub_replica",
+           [](Engine& e, int max_images, int delay_us) {
+             const EngineConfig& c = e.config();
+             e.add_replica(
+                 std::make_shared<StubReplica>(c.H, c.W, c.C, c.classes, max_images, delay_us));
+           },
+           py::arg("max_images") = 256, py::arg("delay_us") = 0)
+      .def("add_gpu_replica",
+           [](Engine& e, std::shared_ptr<Executor> exec, bool use_graph) {
+             const EngineConfig& c = e.config();
+             e.add_replica(std::make_shared<GpuReplica>(std::move(exec), c.H, c.W, c.C,
+                                                        c.classes, use_graph));
+           },
+           py::arg("executor"), py::arg("use_graph") = true)
+      .def("start",
+           [](Engine& e) {
+             py::gil_scoped_release nogil;
+             e.start();
+           })
+      .def("stop",
+           [](Engine& e) {
+             py::gil_scoped_release nogil;
+             e.stop();
+           })
+      .def("wait",
+           [](Engine& e, int64_t timeout_ms) {
+             py::gil_scoped_release nogil;
+             return e.wait(timeout_ms);
+           },
+           py::arg("timeout_ms") = -1)
+      .def_property_readonly("running", &Engine::running)
+      .def_property_readonly("completed", &Engine::completed)
+      .def("stats", &Engine::stats)
+      .def("reset_stats", &Engine::reset_stats)
+      .def("replica_stats", [](Engine& e) {
+        py::list out;
+        for (const ReplicaStats& s : e.replica_stats()) {
+          py::dict d;
+          d["name"] = s.name;
+          d["device"] = s.device;
+          d["alive"] = s.alive;
+          d["batches"] = s.batches;
+          d["images"] = s.images;
+          d["records"] = s.records;
+          out.append(d);
+        }
+        return out;
+      });
+}
+
+}  // namespace gale

@@ -1,8 +1,517 @@
-// Host-runtime bindings (codec, Kafka, engine) — filled in as those subsystems land.
+// Python bindings of the host runtime: JSON codec, Kafka wire protocol / broker / client.
+#include <pybind11/functional.h>
+#include <pybind11/numpy.h>
 #include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include "../codec/json_codec.h"
+#include "../kafka/broker.h"
+#include "../kafka/client.h"
+#include "../kafka/protocol.h"
+#include "../kafka/wire.h"
 
 namespace py = pybind11;
 
 namespace gale {
-void bind_host(py::module_& m) { (void)m; }
+
+void bind_engine(py::module_& m);  // engine_bindings.cpp
+
+namespace {
+
+using namespace gale::kafka;
+
+std::string_view view(const py::bytes& b) {
+  char* p;
+  Py_ssize_t n;
+  PyBytes_AsStringAndSize(b.ptr(), &p, &n);
+  return std::string_view(p, (size_t)n);
+}
+
+py::object opt_bytes(const uint8_t* base, int64_t off, int32_t len) {
+  if (len < 0) return py::none();
+  return py::bytes(reinterpret_cast<const char*>(base + off), (size_t)len);
+}
+
+py::list records_to_py(const uint8_t* base, const std::vector<RecordRef>& recs) {
+  py::list out;
+  for (const RecordRef& r : recs) {
+    py::dict d;
+    d["partition"] = r.partition;
+    d["offset"] = r.offset;
+    d["timestamp"] = r.timestamp;
+    d["key"] = opt_bytes(base, r.key_off, r.key_len);
+    d["value"] = opt_bytes(base, r.value_off, r.value_len);
+    py::list hs;
+    for (const Header& h : decode_headers(base, r))
+      hs.append(py::make_tuple(h.key, h.value_null ? py::object(py::none())
+                                                   : py::object(py::bytes(h.value))));
+    d["headers"] = hs;
+    out.append(d);
+  }
+  return out;
+}
+
+std::vector<Header> headers_from_py(const py::object& o) {
+  std::vector<Header> hs;
+  if (o.is_none()) return hs;
+  for (auto item : o) {
+    auto t = item.cast<py::tuple>();
+    Header h;
+    h.key = t[0].cast<std::string>();
+    if (t[1].is_none()) h.value_null = true;
+    else h.value = std::string(view(t[1].cast<py::bytes>()));
+    hs.push_back(std::move(h));
+  }
+  return hs;
+}
+
+// Batch encode from python: records = [(key|None, value|None, timestamp, headers|None), ...]
+py::bytes py_encode_batch(py::list records, int64_t base_offset, int64_t base_ts) {
+  std::vector<std::string> keys(records.size()), vals(records.size());
+  std::vector<std::vector<Header>> hdrs(records.size());
+  std::vector<RecordIn> ins(records.size());
+  for (size_t i = 0; i < records.size(); ++i) {
+    auto t = records[i].cast<py::tuple>();
+    if (!t[0].is_none()) {
+      keys[i] = std::string(view(t[0].cast<py::bytes>()));
+      ins[i].key = keys[i];
+      ins[i].key_null = false;
+    }
+    if (t[1].is_none()) {
+      ins[i].value_null = true;
+    } else {
+      vals[i] = std::string(view(t[1].cast<py::bytes>()));
+      ins[i].value = vals[i];
+    }
+    ins[i].timestamp = t.size() > 2 ? t[2].cast<int64_t>() : -1;
+    if (t.size() > 3) {
+      hdrs[i] = headers_from_py(t[3]);
+      if (!hdrs[i].empty()) ins[i].headers = &hdrs[i];
+    }
+  }
+  Writer w;
+  encode_batch(w, ins.data(), ins.size(), base_offset, base_ts);
+  return py::bytes(w.buf);
+}
+
+std::vector<std::string> strs(const py::handle& o) { return o.cast<std::vector<std::string>>(); }
+
+// Encode a request body by message name (golden-byte tests of the protocol layer).
+py::bytes py_encode(const std::string& name, py::dict d) {
+  Writer w;
+  if (name == "request_header") {
+    RequestHeader h;
+    h.api_key = d["api_key"].cast<int16_t>();
+    h.api_version = d["api_version"].cast<int16_t>();
+    h.correlation_id = d["correlation_id"].cast<int32_t>();
+    h.client_id = d["client_id"].cast<std::string>();
+    encode_request_header(w, h);
+  } else if (name == "metadata_request") {
+    MetadataRequest m;
+    if (d["topics"].is_none()) m.all_topics = true;
+    else m.topics = strs(d["topics"]);
+    m.allow_auto_topic_creation = d["allow_auto_topic_creation"].cast<bool>();
+    encode_metadata_request(w, m);
+  } else if (name == "fetch_request") {
+    FetchRequest m;
+    m.max_wait_ms = d["max_wait_ms"].cast<int32_t>();
+    m.min_bytes = d["min_bytes"].cast<int32_t>();
+    m.max_bytes = d["max_bytes"].cast<int32_t>();
+    FetchTopic t;
+    t.name = d["topic"].cast<std::string>();
+    for (auto p : d["partitions"].cast<py::list>()) {
+      auto tp = p.cast<py::tuple>();
+      t.partitions.push_back({tp[0].cast<int32_t>(), tp[1].cast<int64_t>(), tp[2].cast<int32_t>()});
+    }
+    m.topics.push_back(t);
+    encode_fetch_request(w, m);
+  } else if (name == "produce_request") {
+    ProduceRequest m;
+    m.acks = d["acks"].cast<int16_t>();
+    m.timeout_ms = d["timeout_ms"].cast<int32_t>();
+    ProduceTopic t;
+    t.name = d["topic"].cast<std::string>();
+    ProducePartition pp;
+    pp.index = d["partition"].cast<int32_t>();
+    pp.records = std::string(view(d["records"].cast<py::bytes>()));
+    t.partitions.push_back(pp);
+    m.topics.push_back(t);
+    encode_produce_request(w, m);
+  } else if (name == "list_offsets_request") {
+    ListOffsetsRequest m;
+    m.topics.push_back({d["topic"].cast<std::string>(),
+                        {{d["partition"].cast<int32_t>(), d["timestamp"].cast<int64_t>()}}});
+    encode_list_offsets_request(w, m);
+  } else if (name == "offset_commit_request") {
+    OffsetCommitRequest m;
+    m.group_id = d["group_id"].cast<std::string>();
+    CommitTopic t;
+    t.name = d["topic"].cast<std::string>();
+    CommitPartition cp;
+    cp.index = d["partition"].cast<int32_t>();
+    cp.offset = d["offset"].cast<int64_t>();
+    t.partitions.push_back(cp);
+    m.topics.push_back(t);
+    encode_offset_commit_request(w, m);
+  } else {
+    throw std::invalid_argument("unknown message " + name);
+  }
+  return py::bytes(w.buf);
+}
+
+py::dict py_decode(const std::string& name, py::bytes b) {
+  const std::string_view s = view(b);
+  Reader r(s);
+  py::dict d;
+  if (name == "metadata_response") {
+    const MetadataResponse m = decode_metadata_response(r);
+    py::list brokers;
+    for (auto& n : m.brokers) brokers.append(py::make_tuple(n.node_id, n.host, n.port));
+    d["brokers"] = brokers;
+    d["cluster_id"] = m.cluster_id;
+    d["controller_id"] = m.controller_id;
+    py::dict topics;
+    for (auto& t : m.topics) {
+      py::list parts;
+      for (auto& p : t.partitions) parts.append(py::make_tuple(p.index, p.leader, p.error));
+      topics[py::str(t.name)] = py::make_tuple(t.error, parts);
+    }
+    d["topics"] = topics;
+  } else if (name == "produce_response") {
+    const ProduceResponse m = decode_produce_response(r);
+    py::list parts;
+    for (auto& t : m.topics)
+      for (auto& p : t.partitions)
+        parts.append(py::make_tuple(t.name, p.index, p.error, p.base_offset));
+    d["partitions"] = parts;
+    d["throttle_ms"] = m.throttle_ms;
+  } else if (name == "fetch_response") {
+    const FetchResponse m = decode_fetch_response(r);
+    py::list parts;
+    for (auto& t : m.topics)
+      for (auto& p : t.partitions) {
+        std::vector<RecordRef> recs;
+        if (p.records_len > 0)
+          decode_records(reinterpret_cast<const uint8_t*>(s.data()), p.records_off,
+                         (size_t)p.records_len, 0, true, recs);
+        parts.append(py::make_tuple(t.name, p.index, p.error, p.high_watermark,
+                                    records_to_py(reinterpret_cast<const uint8_t*>(s.data()), recs)));
+      }
+    d["partitions"] = parts;
+  } else if (name == "api_versions_response") {
+    const ApiVersionsResponse m = decode_api_versions_response(r);
+    d["error"] = m.error;
+    py::dict apis;
+    for (auto& a : m.apis) apis[py::int_(a.key)] = py::make_tuple(a.min_version, a.max_version);
+    d["apis"] = apis;
+  } else {
+    throw std::invalid_argument("unknown message " + name);
+  }
+  return d;
+}
+
+// Python callables held by C++ must be released with the GIL held.
+std::shared_ptr<py::object> hold(py::object o) {
+  return std::shared_ptr<py::object>(new py::object(std::move(o)), [](py::object* p) {
+    py::gil_scoped_acquire g;
+    delete p;
+  });
+}
+
+}  // namespace
+
+void bind_host(py::module_& m) {
+  // ---- JSON codec ----
+  m.def("status_name", &codec::status_name);
+  m.def("scan_instances", [](py::bytes b, int H, int W, int C) {
+    const std::string_view s = view(b);
+    const codec::Scan sc =
+        codec::scan_instances(reinterpret_cast<const uint8_t*>(s.data()), s.size(), H, W, C);
+    return py::make_tuple(sc.status, sc.arr_off, sc.arr_len, sc.images);
+  });
+  m.def("parse_instances_host", [](py::bytes b, int H, int W, int C, int max_images) {
+    const std::string_view s = view(b);
+    const codec::Scan sc =
+        codec::scan_instances(reinterpret_cast<const uint8_t*>(s.data()), s.size(), H, W, C);
+    const int n = sc.status == codec::OK ? sc.images : 0;
+    py::array_t<float> out({(py::ssize_t)n, (py::ssize_t)H, (py::ssize_t)W, (py::ssize_t)C});
+    int images = 0;
+    int st = sc.status;
+    if (st == codec::OK)
+      st = codec::parse_instances_host(reinterpret_cast<const uint8_t*>(s.data()), s.size(), H, W,
+                                       C, out.mutable_data(), max_images, &images);
+    return py::make_tuple(st, out);
+  }, py::arg("data"), py::arg("H"), py::arg("W"), py::arg("C"), py::arg("max_images") = -1);
+  m.def("format_float_java", [](float v) {
+    char buf[48];
+    return std::string(buf, (size_t)codec::format_float_java(v, buf));
+  });
+  m.def("encode_predictions", [](py::array_t<float, py::array::c_style | py::array::forcecast> p,
+                                 bool json_string) {
+    if (p.ndim() != 2) throw std::invalid_argument("predictions must be [N, classes]");
+    std::string out;
+    codec::encode_predictions(p.data(), (int)p.shape(0), (int)p.shape(1), json_string, out);
+    return py::bytes(out);
+  }, py::arg("probs"), py::arg("json_string") = false);
+  m.def("encode_instances", [](py::array_t<float, py::array::c_style | py::array::forcecast> x) {
+    if (x.ndim() != 4) throw std::invalid_argument("instances must be [N, H, W, C]");
+    std::string out;
+    {
+      py::gil_scoped_release nogil;
+      codec::encode_instances(x.data(), (int)x.shape(0), (int)x.shape(1), (int)x.shape(2),
+                              (int)x.shape(3), out);
+    }
+    return py::bytes(out);
+  });
+  m.def("encode_error", [](int status, const std::string& detail, bool json_string) {
+    std::string out;
+    codec::encode_error(status, detail.c_str(), json_string, out);
+    return py::bytes(out);
+  });
+
+  // ---- Kafka wire ----
+  py::module_ k = m.def_submodule("kafka", "Kafka wire protocol, embedded broker and client");
+  k.def("crc32c", [](py::bytes b) {
+    const std::string_view s = view(b);
+    return crc32c(reinterpret_cast<const uint8_t*>(s.data()), s.size());
+  });
+  k.def("murmur2", [](py::bytes b) {
+    const std::string_view s = view(b);
+    return murmur2(reinterpret_cast<const uint8_t*>(s.data()), s.size());
+  });
+  k.def("encode_batch", &py_encode_batch, py::arg("records"), py::arg("base_offset") = 0,
+        py::arg("base_timestamp") = 0);
+  k.def("decode_records", [](py::bytes b, int64_t min_offset, bool check_crc) {
+    const std::string_view s = view(b);
+    std::vector<RecordRef> recs;
+    decode_records(reinterpret_cast<const uint8_t*>(s.data()), 0, s.size(), min_offset, check_crc,
+                   recs);
+    return records_to_py(reinterpret_cast<const uint8_t*>(s.data()), recs);
+  }, py::arg("data"), py::arg("min_offset") = 0, py::arg("check_crc") = true);
+  k.def("encode", &py_encode);
+  k.def("decode", &py_decode);
+  k.def("api_version", [](int key) { return kVersion((ApiKey)key); });
+  k.def("error_name", &error_name);
+
+  py::class_<Broker, std::shared_ptr<Broker>>(k, "Broker")
+      .def(py::init([](const std::string& host, int port, int node_id, int default_partitions,
+                       bool auto_create, int64_t max_message_bytes, int64_t retention_bytes,
+                       bool check_crcs) {
+             BrokerConfig c;
+             c.host = host;
+             c.port = port;
+             c.node_id = node_id;
+             c.default_partitions = default_partitions;
+             c.auto_create_topics = auto_create;
+             c.max_message_bytes = max_message_bytes;
+             c.retention_bytes = retention_bytes;
+             c.check_crcs = check_crcs;
+             return std::make_shared<Broker>(c);
+           }),
+           py::arg("host") = "127.0.0.1", py::arg("port") = 0, py::arg("node_id") = 0,
+           py::arg("default_partitions") = 1, py::arg("auto_create_topics") = true,
+           py::arg("max_message_bytes") = 64ll << 20, py::arg("retention_bytes") = 4ll << 30,
+           py::arg("check_crcs") = true)
+      .def("start", &Broker::start)
+      .def("stop", [](Broker& b) {
+        py::gil_scoped_release nogil;
+        b.stop();
+      })
+      .def_property_readonly("port", &Broker::port)
+      .def_property_readonly("node_id", &Broker::node_id)
+      .def_property_readonly("host", [](Broker& b) { return b.config().host; })
+      .def("set_cluster", [](Broker& b, py::list nodes) {
+        std::vector<BrokerNode> v;
+        for (auto n : nodes) {
+          auto t = n.cast<py::tuple>();
+          v.push_back({t[0].cast<int32_t>(), t[1].cast<std::string>(), t[2].cast<int32_t>()});
+        }
+        b.set_cluster(v);
+      })
+      .def("leads", &Broker::leads)
+      .def("create_topic", &Broker::create_topic)
+      .def("topics", &Broker::topics)
+      .def("partitions", &Broker::partitions)
+      .def("append", [](Broker& b, const std::string& topic, int partition, py::list values,
+                        py::object keys) {
+        std::vector<std::string> vals(values.size()), ks(values.size());
+        std::vector<RecordIn> ins(values.size());
+        for (size_t i = 0; i < values.size(); ++i) {
+          if (values[i].is_none()) {
+            ins[i].value_null = true;
+          } else {
+            vals[i] = std::string(view(values[i].cast<py::bytes>()));
+            ins[i].value = vals[i];
+          }
+          if (!keys.is_none() && !keys.cast<py::list>()[i].is_none()) {
+            ks[i] = std::string(view(keys.cast<py::list>()[i].cast<py::bytes>()));
+            ins[i].key = ks[i];
+            ins[i].key_null = false;
+          }
+        }
+        py::gil_scoped_release nogil;
+        return b.append(topic, partition, ins);
+      }, py::arg("topic"), py::arg("partition"), py::arg("values"), py::arg("keys") = py::none())
+      .def("append_batch_repeated", [](Broker& b, const std::string& topic, int partition,
+                                       py::bytes batch, int64_t times) {
+        // append one pre-encoded batch `times` times, sharing its bytes (bench preloading)
+        auto s = std::make_shared<const std::string>(view(batch));
+        py::gil_scoped_release nogil;
+        int64_t first = -1;
+        for (int64_t i = 0; i < times; ++i) {
+          const int64_t o = b.append_shared(topic, partition, s);
+          if (i == 0) first = o;
+        }
+        return first;
+      })
+      .def("log_start", &Broker::log_start)
+      .def("log_end", &Broker::log_end)
+      .def("committed", &Broker::committed)
+      .def("read", [](Broker& b, const std::string& topic, int partition, int64_t offset,
+                      int64_t max_bytes) {
+        const std::string raw = b.read_raw(topic, partition, offset, max_bytes);
+        std::vector<RecordRef> recs;
+        decode_records(reinterpret_cast<const uint8_t*>(raw.data()), 0, raw.size(), offset, true,
+                       recs);
+        for (auto& r : recs) r.partition = partition;
+        return records_to_py(reinterpret_cast<const uint8_t*>(raw.data()), recs);
+      }, py::arg("topic"), py::arg("partition"), py::arg("offset") = 0,
+         py::arg("max_bytes") = 64ll << 20)
+      .def("stats", [](Broker& b) {
+        const BrokerStats s = b.stats();
+        py::dict d;
+        d["requests"] = s.requests;
+        d["produce_requests"] = s.produce_requests;
+        d["fetch_requests"] = s.fetch_requests;
+        d["bytes_in"] = s.bytes_in;
+        d["bytes_out"] = s.bytes_out;
+        d["records_in"] = s.records_in;
+        d["connections"] = s.connections;
+        return d;
+      });
+
+  py::class_<Producer, std::shared_ptr<Producer>>(k, "Producer")
+      .def(py::init([](const std::string& bootstrap, int acks, int linger_ms, int batch_size,
+                       const std::string& client_id, int request_timeout_ms, int max_in_flight) {
+             ProducerConfig c;
+             c.bootstrap = bootstrap;
+             c.acks = acks;
+             c.linger_ms = linger_ms;
+             c.batch_size = batch_size;
+             c.client_id = client_id;
+             c.request_timeout_ms = request_timeout_ms;
+             c.max_in_flight = max_in_flight;
+             py::gil_scoped_release nogil;
+             return std::make_shared<Producer>(c);
+           }),
+           py::arg("bootstrap"), py::arg("acks") = 1, py::arg("linger_ms") = 0,
+           py::arg("batch_size") = 16384, py::arg("client_id") = "gale-producer",
+           py::arg("request_timeout_ms") = 30000, py::arg("max_in_flight") = 5)
+      .def("send", [](Producer& p, const std::string& topic, py::object value, py::object key,
+                      int partition, py::object headers, int64_t timestamp, py::object callback) {
+        std::string v;
+        bool vnull = value.is_none();
+        if (!vnull) v = std::string(view(value.cast<py::bytes>()));
+        std::string ks;
+        const bool has_key = !key.is_none();
+        if (has_key) ks = std::string(view(key.cast<py::bytes>()));
+        SendCallback cb;
+        if (!callback.is_none()) {
+          auto held = hold(callback);
+          cb = [held](const SendResult& r) {
+            py::gil_scoped_acquire g;
+            try {
+              (*held)(r.error, r.partition, r.offset);
+            } catch (py::error_already_set& e) {
+              e.discard_as_unraisable(__func__);
+            }
+          };
+        }
+        auto hs = headers_from_py(headers);
+        py::gil_scoped_release nogil;
+        p.send(topic, partition, has_key ? &ks : nullptr, std::move(v), vnull, std::move(hs),
+               timestamp, std::move(cb));
+      }, py::arg("topic"), py::arg("value"), py::arg("key") = py::none(),
+         py::arg("partition") = -1, py::arg("headers") = py::none(), py::arg("timestamp") = -1,
+         py::arg("callback") = py::none())
+      .def("flush", [](Producer& p) {
+        py::gil_scoped_release nogil;
+        p.flush();
+      })
+      .def("close", [](Producer& p) {
+        py::gil_scoped_release nogil;
+        p.close();
+      })
+      .def("partitions_for", [](Producer& p, const std::string& t) {
+        py::gil_scoped_release nogil;
+        return p.partitions_for(t);
+      })
+      .def("stats", [](Producer& p) {
+        const ProducerStats s = p.stats();
+        py::dict d;
+        d["records_sent"] = s.records_sent;
+        d["records_acked"] = s.records_acked;
+        d["records_failed"] = s.records_failed;
+        d["requests"] = s.requests;
+        d["bytes"] = s.bytes;
+        return d;
+      });
+
+  py::class_<Consumer, std::shared_ptr<Consumer>>(k, "Consumer")
+      .def(py::init([](const std::string& bootstrap, const std::string& group_id, int max_wait_ms,
+                       int fetch_max_bytes, int partition_max_bytes, bool check_crcs,
+                       const std::string& auto_offset_reset, const std::string& client_id) {
+             ConsumerConfig c;
+             c.bootstrap = bootstrap;
+             c.group_id = group_id;
+             c.max_wait_ms = max_wait_ms;
+             c.fetch_max_bytes = fetch_max_bytes;
+             c.partition_max_bytes = partition_max_bytes;
+             c.check_crcs = check_crcs;
+             c.auto_offset_reset = auto_offset_reset;
+             c.client_id = client_id;
+             return std::make_shared<Consumer>(c);
+           }),
+           py::arg("bootstrap"), py::arg("group_id") = "", py::arg("max_wait_ms") = 100,
+           py::arg("fetch_max_bytes") = 64 << 20, py::arg("partition_max_bytes") = 16 << 20,
+           py::arg("check_crcs") = true, py::arg("auto_offset_reset") = "latest",
+           py::arg("client_id") = "gale-consumer")
+      .def("assign", [](Consumer& c, const std::string& topic, std::vector<int> parts) {
+        py::gil_scoped_release nogil;
+        c.assign(topic, parts);
+      }, py::arg("topic"), py::arg("partitions") = std::vector<int>{})
+      .def("assignment", &Consumer::assignment)
+      .def("seek_to", [](Consumer& c, const std::string& w) {
+        py::gil_scoped_release nogil;
+        c.seek_to(w);
+      })
+      .def("seek", &Consumer::seek)
+      .def("position", &Consumer::position)
+      .def("poll", [](Consumer& c) {
+        std::vector<Fetched> fs;
+        {
+          py::gil_scoped_release nogil;
+          fs = c.poll();
+        }
+        py::list out;
+        for (auto& f : fs)
+          for (auto item : records_to_py(f.buf.get(), f.records)) out.append(item);
+        return out;
+      })
+      .def("commit", [](Consumer& c, std::map<int, int64_t> offs) {
+        py::gil_scoped_release nogil;
+        c.commit(offs);
+      })
+      .def("committed", [](Consumer& c, int p) {
+        py::gil_scoped_release nogil;
+        return c.committed(p);
+      })
+      .def("high_watermarks", &Consumer::high_watermarks);
+
+  py::register_exception<KafkaError>(k, "KafkaError");
+  py::register_exception<ProtocolError>(k, "ProtocolError");
+
+  bind_engine(m);
+}
+
 }  // namespace gale

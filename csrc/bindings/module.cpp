@@ -118,10 +118,10 @@ PYBIND11_MODULE(_C, m) {
               "cast_f32_bf16");
         });
   m.def("json_parse_instances",
-        [](int nrec, uintptr_t recs, uintptr_t bytes, int per_image, uintptr_t out,
+        [](int nrec, uintptr_t recs, uintptr_t bytes, int H, int W, int C, uintptr_t out,
            uintptr_t stream) {
           chk(gale::json_parse_instances(nrec, static_cast<const gale::JsonRecord*>(P(recs)),
-                                         static_cast<const uint8_t*>(P(bytes)), per_image,
+                                         static_cast<const uint8_t*>(P(bytes)), H, W, C,
                                          static_cast<float*>(P(out)), S(stream)),
               "json_parse_instances");
         });

@@ -62,18 +62,19 @@ hipError_t cast_f32_bf16(int64_t n, float scale, float shift, const float* x, vo
 hipError_t quant_f32_e4m3(int64_t n, const float* x, const float* row_scale, int row_len, void* y,
                           hipStream_t stream);
 
-// GPU JSON tokenizer for the InstObj contract: parses every number of each record's value into
-// the fp32 input tensor. recs: [nrec] {byte offset, byte length, first image slot, images}.
-// Host validation has already proven each record rectangular with the model's H*W*C per image,
-// so the kernel only finds number boundaries (block prefix sum) and converts them.
+// GPU decoder for the InstObj JSON contract: parses every number of each record's instances
+// array into the fp32 NHWC batch tensor and validates the rectangular [N][H][W][C] structure.
+// recs: [nrec] {byte offset (16-aligned), length, first image slot, images}. The kernel writes
+// each record's status: 0 ok, 1 number-count mismatch, 2 malformed number / element, 3 bad
+// structure (ragged / wrong rank).
 struct JsonRecord {
-  int64_t off;      // byte offset of the record value inside the staged byte buffer
-  int32_t len;      // value length in bytes
+  int64_t off;      // byte offset of the instances array inside the staged byte buffer
+  int32_t len;      // array length in bytes
   int32_t slot;     // first image slot of this record inside the batch
-  int32_t images;   // images in this record
-  int32_t status;   // 0 = ok; written by the kernel: 1 = number count mismatch, 2 = bad number
+  int32_t images;   // images in this record (from the host '[' count)
+  int32_t status;   // written by the kernel
 };
-hipError_t json_parse_instances(int nrec, const JsonRecord* recs, const uint8_t* bytes,
-                                int per_image, float* out, hipStream_t stream);
+hipError_t json_parse_instances(int nrec, const JsonRecord* recs, const uint8_t* bytes, int H,
+                                int W, int C, float* out, hipStream_t stream);
 
 }  // namespace gale

@@ -1,0 +1,807 @@
+// Embedded Kafka-protocol broker (see broker.h).
+#include "broker.h"
+
+#include <arpa/inet.h>
+#include <errno.h>
+#include <fcntl.h>
+#include <netinet/in.h>
+#include <netinet/tcp.h>
+#include <poll.h>
+#include <sys/eventfd.h>
+#include <sys/socket.h>
+#include <sys/uio.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <chrono>
+#include <deque>
+#include <stdexcept>
+
+namespace gale {
+namespace kafka {
+
+namespace {
+
+int64_t now_ms() {
+  return std::chrono::duration_cast<std::chrono::milliseconds>(
+             std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+
+int64_t wall_ms() {
+  return std::chrono::duration_cast<std::chrono::milliseconds>(
+             std::chrono::system_clock::now().time_since_epoch())
+      .count();
+}
+
+bool valid_topic(const std::string& t) {
+  if (t.empty() || t.size() > 249 || t == "." || t == "..") return false;
+  for (char c : t)
+    if (!(isalnum((unsigned char)c) || c == '.' || c == '_' || c == '-')) return false;
+  return true;
+}
+
+void set_sock_opts(int fd) {
+  int one = 1;
+  setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
+  int sz = 8 << 20;
+  setsockopt(fd, SOL_SOCKET, SO_SNDBUF, &sz, sizeof(sz));
+  setsockopt(fd, SOL_SOCKET, SO_RCVBUF, &sz, sizeof(sz));
+  fcntl(fd, F_SETFL, fcntl(fd, F_GETFL) | O_NONBLOCK);
+}
+
+std::string offset_key(const std::string& g, const std::string& t, int p) {
+  std::string k = g;
+  k.push_back('\0');
+  k += t;
+  k.push_back('\0');
+  k += std::to_string(p);
+  return k;
+}
+
+}  // namespace
+
+struct Broker::Chunk {
+  std::string own;
+  std::shared_ptr<const std::string> shared;
+  size_t off = 0, len = 0;
+  const char* data() const { return (shared ? shared->data() : own.data()) + off; }
+};
+
+struct Broker::Conn {
+  int fd = -1;
+  std::string in;
+  size_t in_off = 0;
+  std::deque<Chunk> out;
+  bool parked = false;
+  bool closed = false;
+  FetchRequest fetch;
+  int32_t fetch_corr = 0;
+  int64_t deadline = 0;
+};
+
+// Response under construction: owned bytes interleaved with zero-copy references.
+struct ResponseBuilder {
+  Writer w;
+  size_t total = 0;
+  std::vector<Broker::Chunk> chunks;
+  void cut() {
+    if (w.buf.empty()) return;
+    Broker::Chunk c;
+    c.own = std::move(w.buf);
+    c.len = c.own.size();
+    total += c.len;
+    chunks.push_back(std::move(c));
+    w.buf = std::string();
+  }
+  void shared(std::shared_ptr<const std::string> s, size_t off, size_t len) {
+    cut();
+    Broker::Chunk c;
+    c.shared = std::move(s);
+    c.off = off;
+    c.len = len;
+    total += len;
+    chunks.push_back(std::move(c));
+  }
+  void finish() {
+    cut();
+    // frame size excludes the 4-byte size field at the front of chunk 0
+    const int32_t sz = (int32_t)(total - 4);
+    Writer::put_be(&chunks[0].own[0], &sz, 4);
+  }
+};
+
+Broker::Broker(BrokerConfig cfg) : cfg_(std::move(cfg)) {}
+
+Broker::~Broker() { stop(); }
+
+BrokerNode Broker::self_node() const {
+  BrokerNode n;
+  n.node_id = cfg_.node_id;
+  n.host = cfg_.host;
+  n.port = port_;
+  return n;
+}
+
+void Broker::set_cluster(const std::vector<BrokerNode>& nodes) {
+  std::lock_guard<std::mutex> lk(mu_);
+  cluster_ = nodes;
+}
+
+std::vector<BrokerNode> Broker::cluster() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  if (cluster_.empty()) return {self_node()};
+  return cluster_;
+}
+
+int32_t Broker::leader_of(int partition) const {  // mu_ held
+  if (cluster_.empty()) return cfg_.node_id;
+  return cluster_[(size_t)partition % cluster_.size()].node_id;
+}
+
+bool Broker::leads(int partition) const {
+  std::lock_guard<std::mutex> lk(mu_);
+  return leader_of(partition) == cfg_.node_id;
+}
+
+void Broker::start() {
+  if (running_) return;
+  listen_fd_ = socket(AF_INET, SOCK_STREAM, 0);
+  if (listen_fd_ < 0) throw std::runtime_error("broker: socket() failed");
+  int one = 1;
+  setsockopt(listen_fd_, SOL_SOCKET, SO_REUSEADDR, &one, sizeof(one));
+  sockaddr_in a{};
+  a.sin_family = AF_INET;
+  a.sin_port = htons((uint16_t)cfg_.port);
+  if (inet_pton(AF_INET, cfg_.host.c_str(), &a.sin_addr) != 1)
+    throw std::runtime_error("broker: bad host " + cfg_.host);
+  if (bind(listen_fd_, reinterpret_cast<sockaddr*>(&a), sizeof(a)) != 0) {
+    close(listen_fd_);
+    listen_fd_ = -1;
+    throw std::runtime_error("broker: bind failed on " + cfg_.host + ":" +
+                             std::to_string(cfg_.port) + ": " + strerror(errno));
+  }
+  listen(listen_fd_, 128);
+  socklen_t len = sizeof(a);
+  getsockname(listen_fd_, reinterpret_cast<sockaddr*>(&a), &len);
+  port_ = ntohs(a.sin_port);
+  fcntl(listen_fd_, F_SETFL, fcntl(listen_fd_, F_GETFL) | O_NONBLOCK);
+  wake_fd_ = eventfd(0, EFD_NONBLOCK);
+  running_ = true;
+  thread_ = std::thread([this] { run(); });
+}
+
+void Broker::stop() {
+  if (!running_.exchange(false)) return;
+  wake();
+  if (thread_.joinable()) thread_.join();
+  for (auto& c : conns_)
+    if (c->fd >= 0) close(c->fd);
+  conns_.clear();
+  if (listen_fd_ >= 0) close(listen_fd_);
+  if (wake_fd_ >= 0) close(wake_fd_);
+  listen_fd_ = wake_fd_ = -1;
+}
+
+void Broker::wake() {
+  if (wake_fd_ >= 0) {
+    uint64_t one = 1;
+    ssize_t r = write(wake_fd_, &one, 8);
+    (void)r;
+  }
+}
+
+bool Broker::create_topic(const std::string& topic, int partitions) {
+  if (!valid_topic(topic)) throw std::invalid_argument("invalid topic name: " + topic);
+  if (partitions <= 0) throw std::invalid_argument("partitions must be > 0");
+  std::lock_guard<std::mutex> lk(mu_);
+  if (topics_.count(topic)) return false;
+  topics_[topic].resize((size_t)partitions);
+  return true;
+}
+
+std::vector<std::string> Broker::topics() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  std::vector<std::string> v;
+  for (auto& kv : topics_) v.push_back(kv.first);
+  return v;
+}
+
+int Broker::partitions(const std::string& topic) const {
+  std::lock_guard<std::mutex> lk(mu_);
+  auto it = topics_.find(topic);
+  return it == topics_.end() ? -1 : (int)it->second.size();
+}
+
+Broker::PartitionLog* Broker::find_log(const std::string& topic, int partition) {
+  auto it = topics_.find(topic);
+  if (it == topics_.end() || partition < 0 || (size_t)partition >= it->second.size())
+    return nullptr;
+  return &it->second[(size_t)partition];
+}
+
+const Broker::PartitionLog* Broker::find_log(const std::string& topic, int partition) const {
+  auto it = topics_.find(topic);
+  if (it == topics_.end() || partition < 0 || (size_t)partition >= it->second.size())
+    return nullptr;
+  return &it->second[(size_t)partition];
+}
+
+int64_t Broker::append_locked(PartitionLog& log, std::shared_ptr<const std::string> batch,
+                              const BatchInfo& bi) {
+  Segment s;
+  s.base = log.end;
+  s.next = log.end + bi.last_offset_delta + 1;
+  s.max_ts = bi.max_timestamp;
+  s.bytes = std::move(batch);
+  log.bytes += (int64_t)s.bytes->size();
+  log.end = s.next;
+  log.segs.push_back(std::move(s));
+  stats_.records_in += bi.records;
+  // byte retention: drop the oldest segments (never the newest)
+  while (log.bytes > cfg_.retention_bytes && log.first + 1 < log.segs.size()) {
+    log.bytes -= (int64_t)log.segs[log.first].bytes->size();
+    log.segs[log.first].bytes.reset();
+    ++log.first;
+    log.start = log.segs[log.first].base;
+  }
+  if (log.first > 4096 && log.first * 2 > log.segs.size()) {
+    log.segs.erase(log.segs.begin(), log.segs.begin() + (long)log.first);
+    log.first = 0;
+  }
+  return s.next - (bi.last_offset_delta + 1);
+}
+
+int64_t Broker::append(const std::string& topic, int partition, const std::vector<RecordIn>& recs) {
+  if (recs.empty()) return log_end(topic, partition);
+  Writer w;
+  encode_batch(w, recs.data(), recs.size(), 0, wall_ms());
+  auto bytes = std::make_shared<const std::string>(std::move(w.buf));
+  const BatchInfo bi =
+      peek_batch(reinterpret_cast<const uint8_t*>(bytes->data()), bytes->size(), false);
+  int64_t base;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    PartitionLog* log = find_log(topic, partition);
+    if (!log) throw std::invalid_argument("unknown topic/partition " + topic);
+    base = append_locked(*log, std::move(bytes), bi);
+  }
+  wake();
+  return base;
+}
+
+int64_t Broker::append_shared(const std::string& topic, int partition,
+                              std::shared_ptr<const std::string> batch) {
+  const BatchInfo bi =
+      peek_batch(reinterpret_cast<const uint8_t*>(batch->data()), batch->size(), false);
+  int64_t base;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    PartitionLog* log = find_log(topic, partition);
+    if (!log) throw std::invalid_argument("unknown topic/partition " + topic);
+    base = append_locked(*log, std::move(batch), bi);
+  }
+  wake();
+  return base;
+}
+
+int64_t Broker::log_start(const std::string& topic, int partition) const {
+  std::lock_guard<std::mutex> lk(mu_);
+  const PartitionLog* log = find_log(topic, partition);
+  return log ? log->start : -1;
+}
+
+int64_t Broker::log_end(const std::string& topic, int partition) const {
+  std::lock_guard<std::mutex> lk(mu_);
+  const PartitionLog* log = find_log(topic, partition);
+  return log ? log->end : -1;
+}
+
+int64_t Broker::committed(const std::string& group, const std::string& topic, int partition) const {
+  std::lock_guard<std::mutex> lk(mu_);
+  auto it = offsets_.find(offset_key(group, topic, partition));
+  return it == offsets_.end() ? -1 : it->second;
+}
+
+BrokerStats Broker::stats() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  return stats_;
+}
+
+std::string Broker::read_raw(const std::string& topic, int partition, int64_t offset,
+                             int64_t max_bytes) const {
+  std::lock_guard<std::mutex> lk(mu_);
+  const PartitionLog* log = find_log(topic, partition);
+  std::string out;
+  if (!log) return out;
+  for (size_t i = log->first; i < log->segs.size(); ++i) {
+    const Segment& s = log->segs[i];
+    if (s.next <= offset) continue;
+    if (!out.empty() && (int64_t)(out.size() + s.bytes->size()) > max_bytes) break;
+    const size_t at = out.size();
+    out += *s.bytes;
+    Writer::put_be(&out[at], &s.base, 8);
+  }
+  return out;
+}
+
+// ------------------------------------------------------------------------------------------
+// I/O loop
+// ------------------------------------------------------------------------------------------
+
+void Broker::run() {
+  std::vector<pollfd> pfds;
+  while (running_) {
+    pfds.clear();
+    pfds.push_back({listen_fd_, POLLIN, 0});
+    pfds.push_back({wake_fd_, POLLIN, 0});
+    int64_t next_deadline = now_ms() + 200;
+    for (auto& c : conns_) {
+      short ev = POLLIN;
+      if (!c->out.empty()) ev |= POLLOUT;
+      pfds.push_back({c->fd, ev, 0});
+      if (c->parked) next_deadline = std::min(next_deadline, c->deadline);
+    }
+    const int timeout = (int)std::max<int64_t>(0, next_deadline - now_ms());
+    const int nready = poll(pfds.data(), pfds.size(), timeout);
+    if (!running_) break;
+    if (nready < 0 && errno != EINTR) break;
+    bool appended = false;
+    if (pfds[1].revents & POLLIN) {
+      uint64_t v;
+      while (read(wake_fd_, &v, 8) == 8) {
+      }
+      appended = true;
+    }
+    if (pfds[0].revents & POLLIN) accept_all();
+    const size_t nconn = std::min(conns_.size(), pfds.size() - 2);
+    for (size_t i = 0; i < nconn; ++i) {
+      Conn& c = *conns_[i];
+      const short re = pfds[i + 2].revents;
+      if (re & (POLLERR | POLLNVAL)) {
+        c.closed = true;
+        continue;
+      }
+      if (re & (POLLIN | POLLHUP)) {
+        const int64_t before = stats_.produce_requests;
+        if (!handle_readable(c)) c.closed = true;
+        if (stats_.produce_requests != before) appended = true;
+      }
+      if (!c.closed && !c.out.empty() && !flush(c)) c.closed = true;
+    }
+    const int64_t t = now_ms();
+    for (auto& cp : conns_) {
+      Conn& c = *cp;
+      if (c.closed || !c.parked) continue;
+      if (appended || t >= c.deadline) {
+        if (try_fetch(c, t >= c.deadline)) {
+          // the fetch completed: continue with any pipelined requests of this connection
+          if (!process_frames(c)) c.closed = true;
+          if (!c.closed && !flush(c)) c.closed = true;
+        }
+      }
+    }
+    for (size_t i = 0; i < conns_.size();) {
+      if (conns_[i]->closed) {
+        close(conns_[i]->fd);
+        conns_.erase(conns_.begin() + (long)i);
+      } else {
+        ++i;
+      }
+    }
+  }
+}
+
+void Broker::accept_all() {
+  for (;;) {
+    const int fd = accept(listen_fd_, nullptr, nullptr);
+    if (fd < 0) return;
+    set_sock_opts(fd);
+    auto c = std::make_unique<Conn>();
+    c->fd = fd;
+    conns_.push_back(std::move(c));
+    std::lock_guard<std::mutex> lk(mu_);
+    ++stats_.connections;
+  }
+}
+
+bool Broker::handle_readable(Conn& c) {
+  char buf[1 << 16];
+  for (;;) {
+    const ssize_t r = recv(c.fd, buf, sizeof(buf), 0);
+    if (r > 0) {
+      c.in.append(buf, (size_t)r);
+      {
+        std::lock_guard<std::mutex> lk(mu_);
+        stats_.bytes_in += r;
+      }
+      if (r < (ssize_t)sizeof(buf)) break;
+      continue;
+    }
+    if (r == 0) return false;
+    if (errno == EAGAIN || errno == EWOULDBLOCK) break;
+    if (errno == EINTR) continue;
+    return false;
+  }
+  return process_frames(c);
+}
+
+bool Broker::process_frames(Conn& c) {
+  while (!c.parked) {
+    const size_t avail = c.in.size() - c.in_off;
+    if (avail < 4) break;
+    int32_t sz;
+    {
+      Reader r(reinterpret_cast<const uint8_t*>(c.in.data()) + c.in_off, 4);
+      sz = r.i32();
+    }
+    if (sz < 0 || sz > (int32_t)std::min<int64_t>(cfg_.max_message_bytes + (16 << 20), 1 << 30))
+      return false;
+    if (avail < 4 + (size_t)sz) break;
+    const uint8_t* p = reinterpret_cast<const uint8_t*>(c.in.data()) + c.in_off + 4;
+    bool ok;
+    try {
+      ok = handle_request(c, p, (size_t)sz);
+    } catch (const ProtocolError&) {
+      ok = false;
+    }
+    if (!ok) return false;
+    c.in_off += 4 + (size_t)sz;
+  }
+  if (c.in_off > 0 && (c.in_off == c.in.size() || c.in_off > (1 << 20))) {
+    c.in.erase(0, c.in_off);
+    c.in_off = 0;
+  }
+  return true;
+}
+
+bool Broker::flush(Conn& c) {
+  while (!c.out.empty()) {
+    iovec iov[64];
+    int n = 0;
+    for (auto it = c.out.begin(); it != c.out.end() && n < 64; ++it, ++n) {
+      iov[n].iov_base = const_cast<char*>(it->data());
+      iov[n].iov_len = it->len;
+    }
+    const ssize_t w = writev(c.fd, iov, n);
+    if (w < 0) {
+      if (errno == EAGAIN || errno == EWOULDBLOCK) return true;
+      if (errno == EINTR) continue;
+      return false;
+    }
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stats_.bytes_out += w;
+    }
+    size_t left = (size_t)w;
+    while (left && !c.out.empty()) {
+      Chunk& f = c.out.front();
+      if (left >= f.len) {
+        left -= f.len;
+        c.out.pop_front();
+      } else {
+        f.off += left;
+        f.len -= left;
+        left = 0;
+      }
+    }
+  }
+  return true;
+}
+
+namespace {
+void frame_into(std::deque<Broker::Chunk>& out, Writer& w) {
+  const int32_t sz = (int32_t)(w.buf.size() - 4);
+  Writer::put_be(&w.buf[0], &sz, 4);
+  Broker::Chunk c;
+  c.own = std::move(w.buf);
+  c.len = c.own.size();
+  out.push_back(std::move(c));
+}
+}  // namespace
+
+bool Broker::handle_request(Conn& c, const uint8_t* p, size_t n) {
+  Reader r(p, n);
+  const RequestHeader h = decode_request_header(r);
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    ++stats_.requests;
+  }
+  Writer w;
+  w.i32(0);
+  w.i32(h.correlation_id);
+  const ApiKey key = (ApiKey)h.api_key;
+  if (key == API_VERSIONS) {
+    ApiVersionsResponse resp;
+    resp.error = h.api_version == 0 ? NONE : UNSUPPORTED_VERSION;
+    for (ApiKey k : {PRODUCE, FETCH, LIST_OFFSETS, METADATA, OFFSET_COMMIT, OFFSET_FETCH,
+                     FIND_COORDINATOR, API_VERSIONS, CREATE_TOPICS})
+      resp.apis.push_back({(int16_t)k, kVersion(k), kVersion(k)});
+    encode_api_versions_response(w, resp);
+    frame_into(c.out, w);
+    return true;
+  }
+  if (kVersion(key) < 0 || h.api_version != kVersion(key)) return false;  // unsupported: close
+
+  switch (key) {
+    case METADATA: {
+      const MetadataRequest req = decode_metadata_request(r);
+      MetadataResponse resp;
+      std::lock_guard<std::mutex> lk(mu_);
+      resp.brokers = cluster_.empty() ? std::vector<BrokerNode>{self_node()} : cluster_;
+      resp.cluster_id = cfg_.cluster_id;
+      resp.controller_id = resp.brokers[0].node_id;
+      std::vector<std::string> names;
+      if (req.all_topics) {
+        for (auto& kv : topics_) names.push_back(kv.first);
+      } else {
+        names = req.topics;
+      }
+      for (const std::string& t : names) {
+        TopicMetadata tm;
+        tm.name = t;
+        auto it = topics_.find(t);
+        if (it == topics_.end()) {
+          if (!valid_topic(t)) {
+            tm.error = INVALID_TOPIC_EXCEPTION;
+          } else if (cfg_.auto_create_topics && req.allow_auto_topic_creation) {
+            topics_[t].resize((size_t)cfg_.default_partitions);
+            it = topics_.find(t);
+          } else {
+            tm.error = UNKNOWN_TOPIC_OR_PARTITION;
+          }
+        }
+        if (it != topics_.end()) {
+          for (size_t pi = 0; pi < it->second.size(); ++pi) {
+            PartitionMetadata pm;
+            pm.index = (int32_t)pi;
+            pm.leader = leader_of((int)pi);
+            pm.replicas = {pm.leader};
+            pm.isr = {pm.leader};
+            tm.partitions.push_back(pm);
+          }
+        }
+        resp.topics.push_back(std::move(tm));
+      }
+      encode_metadata_response(w, resp);
+      break;
+    }
+    case PRODUCE: {
+      const ProduceRequest req = decode_produce_request(r);
+      ProduceResponse resp;
+      const int16_t ack_err = (req.acks == 0 || req.acks == 1 || req.acks == -1)
+                                  ? (int16_t)NONE : (int16_t)INVALID_REQUIRED_ACKS;
+      {
+        std::lock_guard<std::mutex> lk(mu_);
+        ++stats_.produce_requests;
+        for (const ProduceTopic& t : req.topics) {
+          ProduceTopicResponse tr;
+          tr.name = t.name;
+          for (const ProducePartition& pp : t.partitions) {
+            ProducePartitionResponse pr;
+            pr.index = pp.index;
+            PartitionLog* log = find_log(t.name, pp.index);
+            if (ack_err) {
+              pr.error = ack_err;
+            } else if (!log) {
+              pr.error = UNKNOWN_TOPIC_OR_PARTITION;
+            } else if (leader_of(pp.index) != cfg_.node_id) {
+              pr.error = NOT_LEADER_FOR_PARTITION;
+            } else if (pp.records_len <= 0) {
+              pr.error = CORRUPT_MESSAGE;
+            } else {
+              // validate every batch first: a partition's append is all-or-nothing
+              std::vector<std::pair<size_t, BatchInfo>> bs;
+              size_t pos = 0;
+              const uint8_t* blob = p + pp.records_off;
+              try {
+                while (pos < (size_t)pp.records_len) {
+                  const BatchInfo bi =
+                      peek_batch(blob + pos, (size_t)pp.records_len - pos, cfg_.check_crcs);
+                  if (bi.length > cfg_.max_message_bytes) {
+                    pr.error = MESSAGE_TOO_LARGE;
+                    break;
+                  }
+                  bs.push_back({pos, bi});
+                  pos += (size_t)bi.length;
+                }
+              } catch (const ProtocolError&) {
+                pr.error = CORRUPT_MESSAGE;
+              }
+              if (pr.error == NONE) {
+                for (size_t k = 0; k < bs.size(); ++k) {
+                  auto copy = std::make_shared<std::string>(
+                      reinterpret_cast<const char*>(blob + bs[k].first), (size_t)bs[k].second.length);
+                  const int64_t base = log->end;
+                  Writer::put_be(&(*copy)[0], &base, 8);
+                  append_locked(*log, std::move(copy), bs[k].second);
+                  if (k == 0) pr.base_offset = base;
+                }
+              }
+            }
+            tr.partitions.push_back(pr);
+          }
+          resp.topics.push_back(std::move(tr));
+        }
+      }
+      if (req.acks == 0) return true;  // Kafka sends no response for acks=0
+      encode_produce_response(w, resp);
+      break;
+    }
+    case FETCH: {
+      c.fetch = decode_fetch_request(r);
+      c.fetch_corr = h.correlation_id;
+      c.parked = true;
+      c.deadline = now_ms() + std::max(0, c.fetch.max_wait_ms);
+      {
+        std::lock_guard<std::mutex> lk(mu_);
+        ++stats_.fetch_requests;
+      }
+      try_fetch(c, c.fetch.max_wait_ms <= 0);
+      return true;
+    }
+    case LIST_OFFSETS: {
+      const ListOffsetsRequest req = decode_list_offsets_request(r);
+      ListOffsetsResponse resp;
+      std::lock_guard<std::mutex> lk(mu_);
+      for (const ListOffsetsTopic& t : req.topics) {
+        ListOffsetsTopicResponse tr;
+        tr.name = t.name;
+        for (const ListOffsetsPartition& lp : t.partitions) {
+          ListOffsetsPartitionResponse pr;
+          pr.index = lp.index;
+          const PartitionLog* log = find_log(t.name, lp.index);
+          if (!log) {
+            pr.error = UNKNOWN_TOPIC_OR_PARTITION;
+          } else if (leader_of(lp.index) != cfg_.node_id) {
+            pr.error = NOT_LEADER_FOR_PARTITION;
+          } else if (lp.timestamp == kLatest) {
+            pr.offset = log->end;
+          } else if (lp.timestamp == kEarliest) {
+            pr.offset = log->start;
+          } else {
+            pr.offset = log->end;
+            for (size_t i = log->first; i < log->segs.size(); ++i) {
+              if (log->segs[i].max_ts >= lp.timestamp) {
+                pr.offset = log->segs[i].base;
+                pr.timestamp = log->segs[i].max_ts;
+                break;
+              }
+            }
+          }
+          tr.partitions.push_back(pr);
+        }
+        resp.topics.push_back(std::move(tr));
+      }
+      encode_list_offsets_response(w, resp);
+      break;
+    }
+    case FIND_COORDINATOR: {
+      const FindCoordinatorRequest req = decode_find_coordinator_request(r);
+      FindCoordinatorResponse resp;
+      std::lock_guard<std::mutex> lk(mu_);
+      if (cluster_.empty()) {
+        resp.node = self_node();
+      } else {
+        resp.node = cluster_[std::hash<std::string>()(req.key) % cluster_.size()];
+      }
+      encode_find_coordinator_response(w, resp);
+      break;
+    }
+    case OFFSET_COMMIT: {
+      OffsetCommitRequest req = decode_offset_commit_request(r);
+      std::lock_guard<std::mutex> lk(mu_);
+      for (CommitTopic& t : req.topics)
+        for (CommitPartition& cp : t.partitions) {
+          offsets_[offset_key(req.group_id, t.name, cp.index)] = cp.offset;
+          cp.error = NONE;
+        }
+      encode_offset_commit_response(w, req.topics);
+      break;
+    }
+    case OFFSET_FETCH: {
+      OffsetFetchRequest req = decode_offset_fetch_request(r);
+      std::lock_guard<std::mutex> lk(mu_);
+      for (CommitTopic& t : req.topics)
+        for (CommitPartition& cp : t.partitions) {
+          auto it = offsets_.find(offset_key(req.group_id, t.name, cp.index));
+          cp.offset = it == offsets_.end() ? -1 : it->second;
+          cp.error = NONE;
+        }
+      encode_offset_fetch_response(w, req.topics);
+      break;
+    }
+    case CREATE_TOPICS: {
+      CreateTopicsRequest req = decode_create_topics_request(r);
+      std::lock_guard<std::mutex> lk(mu_);
+      for (CreateTopic& t : req.topics) {
+        if (!valid_topic(t.name)) {
+          t.error = INVALID_TOPIC_EXCEPTION;
+        } else if (t.partitions <= 0 && t.partitions != -1) {
+          t.error = INVALID_PARTITIONS;
+        } else if (topics_.count(t.name)) {
+          t.error = TOPIC_ALREADY_EXISTS;
+        } else if (!req.validate_only) {
+          topics_[t.name].resize((size_t)(t.partitions == -1 ? cfg_.default_partitions
+                                                             : t.partitions));
+        }
+      }
+      encode_create_topics_response(w, req.topics);
+      break;
+    }
+    default:
+      return false;
+  }
+  frame_into(c.out, w);
+  return true;
+}
+
+bool Broker::try_fetch(Conn& c, bool final_attempt) {
+  const FetchRequest& req = c.fetch;
+  ResponseBuilder rb;
+  rb.w.i32(0);
+  rb.w.i32(c.fetch_corr);
+  rb.w.i32(0);  // throttle
+  int64_t data_bytes = 0;
+  bool any_error = false;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    int64_t budget = req.max_bytes > 0 ? req.max_bytes : INT64_MAX;
+    bool first_data = true;
+    rb.w.array_len((int32_t)req.topics.size());
+    for (const FetchTopic& t : req.topics) {
+      rb.w.str(t.name);
+      rb.w.array_len((int32_t)t.partitions.size());
+      for (const FetchPartition& fp : t.partitions) {
+        const PartitionLog* log = find_log(t.name, fp.index);
+        int16_t err = NONE;
+        if (!log) err = UNKNOWN_TOPIC_OR_PARTITION;
+        else if (leader_of(fp.index) != cfg_.node_id) err = NOT_LEADER_FOR_PARTITION;
+        else if (fp.fetch_offset < log->start || fp.fetch_offset > log->end)
+          err = OFFSET_OUT_OF_RANGE;
+        rb.w.i32(fp.index);
+        rb.w.i16(err);
+        rb.w.i64(log ? log->end : -1);
+        rb.w.i64(log ? log->end : -1);
+        rb.w.array_len(-1);  // aborted transactions: null
+        if (err != NONE) {
+          any_error = true;
+          rb.w.i32(-1);
+          continue;
+        }
+        // segments covering [fetch_offset, end)
+        std::vector<const Segment*> sel;
+        int64_t pbytes = 0;
+        auto it = std::upper_bound(
+            log->segs.begin() + (long)log->first, log->segs.end(), fp.fetch_offset,
+            [](int64_t off, const Segment& s) { return off < s.base; });
+        if (it != log->segs.begin() + (long)log->first) --it;
+        for (; it != log->segs.end(); ++it) {
+          if (it->next <= fp.fetch_offset) continue;
+          const int64_t sz = (int64_t)it->bytes->size();
+          const bool forced = first_data && sel.empty();  // KIP-74: first batch always fits
+          if (!forced && (pbytes + sz > fp.max_bytes || sz > budget)) break;
+          sel.push_back(&*it);
+          pbytes += sz;
+          budget -= sz;
+          if (budget <= 0) break;
+        }
+        if (!sel.empty()) first_data = false;
+        rb.w.i32((int32_t)pbytes);
+        for (const Segment* s : sel) {
+          rb.w.i64(s->base);
+          rb.shared(s->bytes, 8, s->bytes->size() - 8);
+        }
+        data_bytes += pbytes;
+      }
+    }
+  }
+  if (!final_attempt && !any_error && data_bytes < std::max(1, req.min_bytes)) return false;
+  rb.finish();
+  for (auto& ch : rb.chunks) c.out.push_back(std::move(ch));
+  c.parked = false;
+  return true;
+}
+
+}  // namespace kafka
+}  // namespace gale

@@ -1,0 +1,131 @@
+// Embedded Kafka-protocol broker.
+//
+// Plays the role that an embedded Kafka / Storm LocalCluster plays for the reference's topology
+// ("an embedded in-process Kafka-protocol broker"): tests, benchmarks and the
+// GPU boxes (which have no network) get real Kafka topics on 127.0.0.1 that any Kafka-protocol
+// client can talk to, with the reference's external contract unchanged (INPUT_TOPIC records in,
+// OUTPUT_TOPIC records out, MainTopology.java:36-38).
+//
+// * One poll() I/O thread; in-memory partition logs of RecordBatch v2 segments with byte-based
+//   retention; zero-copy Fetch responses (writev straight from the stored batches).
+// * Long-poll Fetch (max_wait_ms / min_bytes), acks 0/1/-1 Produce, ListOffsets, consumer-group
+//   offset storage (FindCoordinator / OffsetCommit / OffsetFetch), CreateTopics, ApiVersions.
+// * Multi-broker clusters: set_cluster() makes partition p of every topic led by node
+//   nodes[p % n]; Metadata advertises the whole cluster (one broker per GPU rank in bench.py).
+#pragma once
+#include <stdint.h>
+
+#include <atomic>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "protocol.h"
+#include "wire.h"
+
+namespace gale {
+namespace kafka {
+
+struct BrokerConfig {
+  std::string host = "127.0.0.1";
+  int port = 0;                       // 0 = ephemeral
+  int node_id = 0;
+  int default_partitions = 1;         // num.partitions for auto-created topics
+  bool auto_create_topics = true;
+  int64_t max_message_bytes = 64ll << 20;  // message.max.bytes (per record batch)
+  int64_t retention_bytes = 4ll << 30;     // per partition; oldest segments dropped beyond it
+  bool check_crcs = true;             // validate produced batches
+  std::string cluster_id = "gale-embedded";
+};
+
+struct BrokerStats {
+  int64_t requests = 0, produce_requests = 0, fetch_requests = 0;
+  int64_t bytes_in = 0, bytes_out = 0, records_in = 0, connections = 0;
+};
+
+class Broker {
+ public:
+  explicit Broker(BrokerConfig cfg);
+  ~Broker();
+  Broker(const Broker&) = delete;
+  Broker& operator=(const Broker&) = delete;
+
+  void start();
+  void stop();
+  int port() const { return port_; }
+  int node_id() const { return cfg_.node_id; }
+  const BrokerConfig& config() const { return cfg_; }
+
+  void set_cluster(const std::vector<BrokerNode>& nodes);
+  std::vector<BrokerNode> cluster() const;
+  bool leads(int partition) const;
+
+  // Returns false if the topic already existed (partition count unchanged).
+  bool create_topic(const std::string& topic, int partitions);
+  std::vector<std::string> topics() const;
+  int partitions(const std::string& topic) const;  // -1 if unknown
+
+  // Local (in-process) producer: appends one batch; returns its base offset.
+  int64_t append(const std::string& topic, int partition, const std::vector<RecordIn>& recs);
+  // Append a pre-encoded batch shared by reference (bench preloading of repeated payloads).
+  int64_t append_shared(const std::string& topic, int partition,
+                        std::shared_ptr<const std::string> batch);
+  int64_t log_start(const std::string& topic, int partition) const;
+  int64_t log_end(const std::string& topic, int partition) const;
+  // Concatenated batches (base offsets patched) covering [offset, ...) up to ~max_bytes.
+  std::string read_raw(const std::string& topic, int partition, int64_t offset,
+                       int64_t max_bytes) const;
+  int64_t committed(const std::string& group, const std::string& topic, int partition) const;
+  BrokerStats stats() const;
+
+ public:
+  struct Chunk;  // one piece of a response (owned bytes or a zero-copy slice of a stored batch)
+
+ private:
+  struct Segment {
+    int64_t base;
+    int64_t next;  // base + lastOffsetDelta + 1
+    int64_t max_ts;
+    std::shared_ptr<const std::string> bytes;
+  };
+  struct PartitionLog {
+    std::vector<Segment> segs;
+    size_t first = 0;  // index of the first retained segment
+    int64_t start = 0, end = 0;
+    int64_t bytes = 0;
+  };
+  struct Conn;
+
+  void run();
+  void wake();
+  void accept_all();
+  bool handle_readable(Conn& c);
+  bool process_frames(Conn& c);
+  bool handle_request(Conn& c, const uint8_t* p, size_t n);
+  bool try_fetch(Conn& c, bool final_attempt);
+  bool flush(Conn& c);
+  int64_t append_locked(PartitionLog& log, std::shared_ptr<const std::string> batch,
+                        const BatchInfo& bi);
+  PartitionLog* find_log(const std::string& topic, int partition);
+  const PartitionLog* find_log(const std::string& topic, int partition) const;
+  BrokerNode self_node() const;
+  int32_t leader_of(int partition) const;
+
+  BrokerConfig cfg_;
+  int listen_fd_ = -1, wake_fd_ = -1;
+  int port_ = 0;
+  std::thread thread_;
+  std::atomic<bool> running_{false};
+  mutable std::mutex mu_;  // topics_, offsets_, cluster_, stats_
+  std::map<std::string, std::vector<PartitionLog>> topics_;
+  std::map<std::string, int64_t> offsets_;  // "group\0topic\0partition" -> offset
+  std::vector<BrokerNode> cluster_;
+  BrokerStats stats_;
+  std::vector<std::unique_ptr<Conn>> conns_;
+};
+
+}  // namespace kafka
+}  // namespace gale

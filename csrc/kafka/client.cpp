@@ -1,0 +1,761 @@
+// Kafka-protocol client: connections, metadata, producer, consumer (see client.h).
+#include "client.h"
+
+#include <arpa/inet.h>
+#include <errno.h>
+#include <fcntl.h>
+#include <netdb.h>
+#include <netinet/in.h>
+#include <netinet/tcp.h>
+#include <poll.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <chrono>
+#include <sstream>
+
+namespace gale {
+namespace kafka {
+
+namespace {
+
+int64_t wall_ms() {
+  return std::chrono::duration_cast<std::chrono::milliseconds>(
+             std::chrono::system_clock::now().time_since_epoch())
+      .count();
+}
+int64_t mono_ms() {
+  return std::chrono::duration_cast<std::chrono::milliseconds>(
+             std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+
+std::vector<std::pair<std::string, int>> parse_bootstrap(const std::string& s) {
+  std::vector<std::pair<std::string, int>> out;
+  std::stringstream ss(s);
+  std::string item;
+  while (std::getline(ss, item, ',')) {
+    while (!item.empty() && isspace((unsigned char)item.back())) item.pop_back();
+    while (!item.empty() && isspace((unsigned char)item.front())) item.erase(0, 1);
+    if (item.empty()) continue;
+    const size_t c = item.rfind(':');
+    if (c == std::string::npos) {
+      out.push_back({item, 9092});
+    } else {
+      out.push_back({item.substr(0, c), std::stoi(item.substr(c + 1))});
+    }
+  }
+  if (out.empty()) throw std::invalid_argument("empty bootstrap server list");
+  return out;
+}
+
+}  // namespace
+
+std::shared_ptr<uint8_t> heap_alloc(size_t bytes) {
+  return std::shared_ptr<uint8_t>(new uint8_t[bytes + 64], std::default_delete<uint8_t[]>());
+}
+
+// ---------------------------------------------------------------------------------------------
+// Connection
+// ---------------------------------------------------------------------------------------------
+
+Connection::Connection(const std::string& host, int port, const ClientConfig& cfg)
+    : host_(host), port_(port), client_id_(cfg.client_id) {
+  addrinfo hints{}, *res = nullptr;
+  hints.ai_family = AF_INET;
+  hints.ai_socktype = SOCK_STREAM;
+  const std::string ps = std::to_string(port);
+  if (getaddrinfo(host.c_str(), ps.c_str(), &hints, &res) != 0 || !res)
+    throw KafkaError(-1, "cannot resolve " + host);
+  fd_ = socket(AF_INET, SOCK_STREAM, 0);
+  fcntl(fd_, F_SETFL, fcntl(fd_, F_GETFL) | O_NONBLOCK);
+  int rc = connect(fd_, res->ai_addr, res->ai_addrlen);
+  freeaddrinfo(res);
+  if (rc != 0 && errno != EINPROGRESS) {
+    close(fd_);
+    throw KafkaError(-1, "connect to " + host + ":" + ps + " failed: " + strerror(errno));
+  }
+  if (rc != 0) {
+    pollfd p{fd_, POLLOUT, 0};
+    int err = 0;
+    socklen_t el = sizeof(err);
+    if (poll(&p, 1, cfg.connect_timeout_ms) != 1 ||
+        getsockopt(fd_, SOL_SOCKET, SO_ERROR, &err, &el) != 0 || err != 0) {
+      close(fd_);
+      throw KafkaError(-1, "connect to " + host + ":" + ps + " failed: " +
+                               (err ? strerror(err) : "timeout"));
+    }
+  }
+  fcntl(fd_, F_SETFL, fcntl(fd_, F_GETFL) & ~O_NONBLOCK);
+  int one = 1;
+  setsockopt(fd_, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
+  int sz = 8 << 20;
+  setsockopt(fd_, SOL_SOCKET, SO_RCVBUF, &sz, sizeof(sz));
+  setsockopt(fd_, SOL_SOCKET, SO_SNDBUF, &sz, sizeof(sz));
+  timeval tv{cfg.request_timeout_ms / 1000, (cfg.request_timeout_ms % 1000) * 1000};
+  setsockopt(fd_, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof(tv));
+  setsockopt(fd_, SOL_SOCKET, SO_SNDTIMEO, &tv, sizeof(tv));
+}
+
+Connection::~Connection() {
+  if (fd_ >= 0) close(fd_);
+}
+
+void Connection::send_all(const char* p, size_t n) {
+  while (n) {
+    const ssize_t w = ::send(fd_, p, n, MSG_NOSIGNAL);
+    if (w < 0) {
+      if (errno == EINTR) continue;
+      throw KafkaError(-1, std::string("send failed: ") + strerror(errno));
+    }
+    p += w;
+    n -= (size_t)w;
+  }
+}
+
+void Connection::recv_all(uint8_t* p, size_t n) {
+  while (n) {
+    const ssize_t r = ::recv(fd_, p, n, 0);
+    if (r == 0) throw KafkaError(-1, "connection closed by broker " + host_);
+    if (r < 0) {
+      if (errno == EINTR) continue;
+      if (errno == EAGAIN || errno == EWOULDBLOCK)
+        throw KafkaError(REQUEST_TIMED_OUT, "request timed out on " + host_);
+      throw KafkaError(-1, std::string("recv failed: ") + strerror(errno));
+    }
+    p += r;
+    n -= (size_t)r;
+  }
+}
+
+int32_t Connection::send(ApiKey key, const Writer& body) {
+  Writer w;
+  w.reserve(body.size() + 64);
+  w.i32(0);
+  RequestHeader h;
+  h.api_key = key;
+  h.api_version = kVersion(key);
+  h.correlation_id = next_corr_++;
+  h.client_id = client_id_;
+  encode_request_header(w, h);
+  w.raw(body.buf.data(), body.buf.size());
+  w.patch_i32(0, (int32_t)(w.size() - 4));
+  send_all(w.buf.data(), w.buf.size());
+  return h.correlation_id;
+}
+
+std::shared_ptr<uint8_t> Connection::recv(int32_t corr, size_t* size, const BufferAlloc& alloc) {
+  uint8_t hdr[8];
+  recv_all(hdr, 8);
+  Reader r(hdr, 8);
+  const int32_t sz = r.i32();
+  const int32_t got = r.i32();
+  if (sz < 4) throw KafkaError(-1, "bad response size");
+  if (got != corr)
+    throw KafkaError(-1, "correlation id mismatch (" + std::to_string(got) + " != " +
+                             std::to_string(corr) + ")");
+  const size_t n = (size_t)sz - 4;
+  std::shared_ptr<uint8_t> buf = alloc(n);
+  recv_all(buf.get(), n);
+  *size = n;
+  return buf;
+}
+
+std::string Connection::request(ApiKey key, const Writer& body) {
+  const int32_t corr = send(key, body);
+  size_t n = 0;
+  auto buf = recv(corr, &n, heap_alloc);
+  return std::string(reinterpret_cast<const char*>(buf.get()), n);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Cluster
+// ---------------------------------------------------------------------------------------------
+
+Cluster::Cluster(ClientConfig cfg) : cfg_(std::move(cfg)) {}
+
+void Cluster::check_versions(Connection& c) {
+  Writer w;
+  const std::string resp = c.request(API_VERSIONS, w);
+  Reader r(resp);
+  const ApiVersionsResponse av = decode_api_versions_response(r);
+  if (av.error != NONE) throw KafkaError(av.error, "ApiVersions failed");
+  for (ApiKey k : {PRODUCE, FETCH, LIST_OFFSETS, METADATA, OFFSET_COMMIT, OFFSET_FETCH,
+                   FIND_COORDINATOR}) {
+    bool ok = false;
+    for (const auto& a : av.apis)
+      if (a.key == k && a.min_version <= kVersion(k) && kVersion(k) <= a.max_version) ok = true;
+    if (!ok)
+      throw KafkaError(UNSUPPORTED_VERSION, "broker " + c.host() + " does not support api " +
+                                                std::to_string(k) + " v" +
+                                                std::to_string(kVersion(k)));
+  }
+}
+
+Connection& Cluster::any() {
+  if (!conns_.empty()) return *conns_.begin()->second;
+  if (bootstrap_) return *bootstrap_;
+  std::string errs;
+  for (auto& hp : parse_bootstrap(cfg_.bootstrap)) {
+    try {
+      auto c = std::make_unique<Connection>(hp.first, hp.second, cfg_);
+      check_versions(*c);
+      bootstrap_ = std::move(c);
+      return *bootstrap_;
+    } catch (const KafkaError& e) {
+      errs += std::string(e.what()) + "; ";
+    }
+  }
+  throw KafkaError(-1, "no bootstrap broker reachable: " + errs);
+}
+
+void Cluster::refresh(const std::vector<std::string>& topics, bool auto_create) {
+  for (int attempt = 0;; ++attempt) {
+    MetadataRequest req;
+    req.topics = topics;
+    req.allow_auto_topic_creation = auto_create;
+    Writer w;
+    encode_metadata_request(w, req);
+    const std::string resp = any().request(METADATA, w);
+    Reader r(resp);
+    const MetadataResponse m = decode_metadata_response(r);
+    for (const BrokerNode& b : m.brokers) nodes_[b.node_id] = b;
+    bool retry = false;
+    for (const TopicMetadata& t : m.topics) {
+      if (t.error == LEADER_NOT_AVAILABLE) {
+        retry = true;
+        continue;
+      }
+      if (t.error != NONE) {
+        topics_.erase(t.name);
+        continue;
+      }
+      std::vector<int32_t> leaders(t.partitions.size(), -1);
+      for (const PartitionMetadata& p : t.partitions)
+        if ((size_t)p.index < leaders.size()) leaders[(size_t)p.index] = p.leader;
+      topics_[t.name] = leaders;
+    }
+    if (!retry || attempt >= 20) return;
+    usleep(50000);
+  }
+}
+
+int Cluster::partitions(const std::string& topic) {
+  auto it = topics_.find(topic);
+  if (it == topics_.end()) {
+    refresh({topic});
+    it = topics_.find(topic);
+    if (it == topics_.end()) return -1;
+  }
+  return (int)it->second.size();
+}
+
+int32_t Cluster::leader(const std::string& topic, int partition) {
+  if (partitions(topic) <= partition) throw KafkaError(UNKNOWN_TOPIC_OR_PARTITION, topic);
+  const int32_t l = topics_[topic][(size_t)partition];
+  if (l < 0) throw KafkaError(LEADER_NOT_AVAILABLE, topic);
+  return l;
+}
+
+Connection& Cluster::node(int32_t node_id) {
+  auto it = conns_.find(node_id);
+  if (it != conns_.end()) return *it->second;
+  auto nit = nodes_.find(node_id);
+  if (nit == nodes_.end()) throw KafkaError(-1, "unknown broker node " + std::to_string(node_id));
+  auto c = std::make_unique<Connection>(nit->second.host, nit->second.port, cfg_);
+  check_versions(*c);
+  Connection& ref = *c;
+  conns_[node_id] = std::move(c);
+  return ref;
+}
+
+Connection& Cluster::coordinator(const std::string& group) {
+  auto it = coordinators_.find(group);
+  if (it == coordinators_.end()) {
+    FindCoordinatorRequest req;
+    req.key = group;
+    Writer w;
+    encode_find_coordinator_request(w, req);
+    const std::string resp = any().request(FIND_COORDINATOR, w);
+    Reader r(resp);
+    const FindCoordinatorResponse m = decode_find_coordinator_response(r);
+    if (m.error != NONE) throw KafkaError(m.error, "FindCoordinator: " + std::string(error_name(m.error)));
+    nodes_[m.node.node_id] = m.node;
+    it = coordinators_.emplace(group, m.node.node_id).first;
+  }
+  return node(it->second);
+}
+
+std::vector<BrokerNode> Cluster::brokers() const {
+  std::vector<BrokerNode> v;
+  for (auto& kv : nodes_) v.push_back(kv.second);
+  return v;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Producer
+// ---------------------------------------------------------------------------------------------
+
+int32_t murmur2(const uint8_t* data, size_t n) {
+  const uint32_t m = 0x5bd1e995;
+  const int r = 24;
+  uint32_t h = 0x9747b28cu ^ (uint32_t)n;
+  const size_t n4 = n / 4;
+  for (size_t i = 0; i < n4; ++i) {
+    uint32_t k = (uint32_t)data[4 * i] | ((uint32_t)data[4 * i + 1] << 8) |
+                 ((uint32_t)data[4 * i + 2] << 16) | ((uint32_t)data[4 * i + 3] << 24);
+    k *= m;
+    k ^= k >> r;
+    k *= m;
+    h *= m;
+    h ^= k;
+  }
+  const size_t t = n & ~(size_t)3;
+  switch (n % 4) {
+    case 3: h ^= (uint32_t)data[t + 2] << 16; [[fallthrough]];
+    case 2: h ^= (uint32_t)data[t + 1] << 8; [[fallthrough]];
+    case 1: h ^= (uint32_t)data[t]; h *= m;
+  }
+  h ^= h >> 13;
+  h *= m;
+  h ^= h >> 15;
+  return (int32_t)h;
+}
+
+Producer::Producer(ProducerConfig cfg)
+    : cfg_(std::move(cfg)), cluster_(cfg_), meta_(cfg_) {
+  if (cfg_.acks != 0 && cfg_.acks != 1 && cfg_.acks != -1)
+    throw std::invalid_argument("acks must be 0, 1 or -1");
+  thread_ = std::thread([this] { run(); });
+}
+
+Producer::~Producer() {
+  try {
+    close();
+  } catch (...) {
+  }
+}
+
+int Producer::partitions_for(const std::string& topic) {
+  std::lock_guard<std::mutex> lk(mu_);
+  auto it = nparts_.find(topic);
+  if (it != nparts_.end()) return it->second;
+  const int n = meta_.partitions(topic);
+  if (n > 0) nparts_[topic] = n;
+  return n;
+}
+
+int Producer::choose_partition(const std::string& topic, const std::string* key) {  // mu_ held
+  auto it = nparts_.find(topic);
+  int n;
+  if (it == nparts_.end()) {
+    n = meta_.partitions(topic);
+    if (n <= 0) throw KafkaError(UNKNOWN_TOPIC_OR_PARTITION, "unknown topic " + topic);
+    nparts_[topic] = n;
+  } else {
+    n = it->second;
+  }
+  if (key)
+    return (int)((uint32_t)murmur2(reinterpret_cast<const uint8_t*>(key->data()), key->size()) &
+                 0x7fffffffu) % n;
+  return (int)((rr_++ & 0x7fffffffu) % (uint32_t)n);
+}
+
+void Producer::send(const std::string& topic, int partition, const std::string* key,
+                    std::string value, bool value_null, std::vector<Header> headers,
+                    int64_t timestamp, SendCallback cb) {
+  std::unique_lock<std::mutex> lk(mu_);
+  if (closing_) throw std::runtime_error("producer is closed");
+  if (partition < 0) partition = choose_partition(topic, key);
+  done_cv_.wait(lk, [&] { return unsent_bytes_ < cfg_.buffer_memory || closing_; });
+  Pending p;
+  if (key) {
+    p.key = *key;
+    p.key_null = false;
+  }
+  p.value = std::move(value);
+  p.value_null = value_null;
+  p.headers = std::move(headers);
+  p.ts = timestamp >= 0 ? timestamp : wall_ms();
+  p.cb = std::move(cb);
+  const size_t sz = p.value.size() + p.key.size() + 32;
+  PartBatch& b = acc_[{topic, partition}];
+  if (b.recs.empty()) b.first_ms = mono_ms();
+  b.bytes += sz;
+  b.recs.push_back(std::move(p));
+  unsent_bytes_ += (int64_t)sz;
+  ++outstanding_;
+  ++stats_.records_sent;
+  if (b.bytes >= (size_t)cfg_.batch_size || cfg_.linger_ms <= 0) cv_.notify_one();
+}
+
+void Producer::flush() {
+  std::unique_lock<std::mutex> lk(mu_);
+  flush_req_ = true;
+  cv_.notify_one();
+  done_cv_.wait(lk, [&] { return outstanding_ == 0; });
+  flush_req_ = false;
+}
+
+void Producer::close() {
+  {
+    std::unique_lock<std::mutex> lk(mu_);
+    if (closing_ && !thread_.joinable()) return;
+  }
+  flush();
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    closing_ = true;
+  }
+  cv_.notify_all();
+  done_cv_.notify_all();
+  if (thread_.joinable()) thread_.join();
+}
+
+ProducerStats Producer::stats() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  return stats_;
+}
+
+void Producer::run() {
+  std::deque<InFlight> inflight;
+  auto complete = [&](std::vector<Pending>& recs, int16_t err, int part, int64_t base) {
+    for (size_t i = 0; i < recs.size(); ++i) {
+      SendResult r;
+      r.error = err;
+      r.partition = part;
+      r.offset = (err == NONE && base >= 0) ? base + (int64_t)i : -1;
+      if (recs[i].cb) {
+        try {
+          recs[i].cb(r);
+        } catch (...) {
+        }
+      }
+    }
+    std::lock_guard<std::mutex> lk(mu_);
+    outstanding_ -= (int64_t)recs.size();
+    if (err == NONE) stats_.records_acked += (int64_t)recs.size();
+    else stats_.records_failed += (int64_t)recs.size();
+    done_cv_.notify_all();
+  };
+  auto read_one = [&]() {
+    InFlight f = std::move(inflight.front());
+    inflight.pop_front();
+    size_t n = 0;
+    std::shared_ptr<uint8_t> buf;
+    try {
+      buf = cluster_.node(f.node).recv(f.corr, &n, heap_alloc);
+    } catch (const std::exception&) {
+      for (auto& b : f.batches) complete(b.second, REQUEST_TIMED_OUT, b.first.second, -1);
+      cluster_.invalidate();
+      return;
+    }
+    Reader r(buf.get(), n);
+    const ProduceResponse resp = decode_produce_response(r);
+    for (auto& b : f.batches) {
+      int16_t err = UNKNOWN_SERVER_ERROR;
+      int64_t base = -1;
+      for (const auto& t : resp.topics)
+        if (t.name == b.first.first)
+          for (const auto& p : t.partitions)
+            if (p.index == b.first.second) {
+              err = p.error;
+              base = p.base_offset;
+            }
+      if (err != NONE) cluster_.invalidate();
+      complete(b.second, err, b.first.second, base);
+    }
+  };
+
+  for (;;) {
+    std::vector<std::pair<std::pair<std::string, int>, std::vector<Pending>>> ready;
+    bool stop = false;
+    {
+      std::unique_lock<std::mutex> lk(mu_);
+      for (;;) {
+        const int64_t now = mono_ms();
+        int64_t next = INT64_MAX;
+        for (auto it = acc_.begin(); it != acc_.end();) {
+          PartBatch& b = it->second;
+          if (b.recs.empty()) {
+            it = acc_.erase(it);
+            continue;
+          }
+          if (flush_req_ || closing_ || b.bytes >= (size_t)cfg_.batch_size ||
+              now - b.first_ms >= cfg_.linger_ms) {
+            for (auto& p : b.recs) unsent_bytes_ -= (int64_t)(p.value.size() + p.key.size() + 32);
+            ready.push_back({it->first, std::move(b.recs)});
+            it = acc_.erase(it);
+          } else {
+            next = std::min(next, b.first_ms + cfg_.linger_ms);
+            ++it;
+          }
+        }
+        if (!ready.empty()) {
+          done_cv_.notify_all();
+          break;
+        }
+        if (!inflight.empty()) break;
+        if (closing_) {
+          stop = true;
+          break;
+        }
+        if (next == INT64_MAX) cv_.wait(lk);
+        else cv_.wait_for(lk, std::chrono::milliseconds(std::max<int64_t>(1, next - now)));
+      }
+    }
+    if (stop) return;
+    // group by leader and send (one request per node, split at max_request_size)
+    std::map<int32_t, std::vector<size_t>> by_node;
+    for (size_t i = 0; i < ready.size(); ++i) {
+      try {
+        by_node[cluster_.leader(ready[i].first.first, ready[i].first.second)].push_back(i);
+      } catch (const KafkaError& e) {
+        complete(ready[i].second, (int16_t)e.code, ready[i].first.second, -1);
+        cluster_.invalidate();
+      }
+    }
+    for (auto& kv : by_node) {
+      size_t k = 0;
+      while (k < kv.second.size()) {
+        ProduceRequest req;
+        req.acks = (int16_t)cfg_.acks;
+        req.timeout_ms = cfg_.request_timeout_ms;
+        InFlight f;
+        f.node = kv.first;
+        size_t bytes = 0;
+        for (; k < kv.second.size(); ++k) {
+          auto& item = ready[kv.second[k]];
+          std::vector<RecordIn> ins(item.second.size());
+          for (size_t j = 0; j < item.second.size(); ++j) {
+            const Pending& p = item.second[j];
+            ins[j].key = p.key;
+            ins[j].key_null = p.key_null;
+            ins[j].value = p.value;
+            ins[j].value_null = p.value_null;
+            ins[j].timestamp = p.ts;
+            ins[j].headers = p.headers.empty() ? nullptr : &p.headers;
+          }
+          Writer bw;
+          encode_batch(bw, ins.data(), ins.size(), 0, item.second.front().ts);
+          if (bytes && bytes + bw.size() > (size_t)cfg_.max_request_size) break;
+          bytes += bw.size();
+          ProduceTopic* pt = nullptr;
+          for (auto& t : req.topics)
+            if (t.name == item.first.first) pt = &t;
+          if (!pt) {
+            req.topics.push_back(ProduceTopic{item.first.first, {}});
+            pt = &req.topics.back();
+          }
+          ProducePartition pp;
+          pp.index = item.first.second;
+          pp.records = std::move(bw.buf);
+          pt->partitions.push_back(std::move(pp));
+          f.batches.push_back({item.first, std::move(item.second)});
+        }
+        Writer w;
+        encode_produce_request(w, req);
+        try {
+          Connection& c = cluster_.node(kv.first);
+          f.corr = c.send(PRODUCE, w);
+          {
+            std::lock_guard<std::mutex> lk(mu_);
+            ++stats_.requests;
+            stats_.bytes += (int64_t)w.size();
+          }
+        } catch (const std::exception&) {
+          for (auto& b : f.batches) complete(b.second, REQUEST_TIMED_OUT, b.first.second, -1);
+          cluster_.invalidate();
+          continue;
+        }
+        if (cfg_.acks == 0) {
+          for (auto& b : f.batches) complete(b.second, NONE, b.first.second, -1);
+        } else {
+          inflight.push_back(std::move(f));
+          if ((int)inflight.size() >= cfg_.max_in_flight) read_one();
+        }
+      }
+    }
+    // read responses when there is nothing new to send
+    bool more;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      more = false;
+      for (auto& kv : acc_)
+        if (!kv.second.recs.empty() &&
+            (flush_req_ || closing_ || kv.second.bytes >= (size_t)cfg_.batch_size ||
+             cfg_.linger_ms <= 0))
+          more = true;
+    }
+    if (!more) {
+      while (!inflight.empty()) read_one();
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Consumer
+// ---------------------------------------------------------------------------------------------
+
+Consumer::Consumer(ConsumerConfig cfg, BufferAlloc alloc)
+    : cfg_(std::move(cfg)), alloc_(std::move(alloc)), cluster_(cfg_) {}
+
+void Consumer::assign(const std::string& topic, const std::vector<int>& partitions) {
+  topic_ = topic;
+  const int n = cluster_.partitions(topic);
+  if (n < 0) throw KafkaError(UNKNOWN_TOPIC_OR_PARTITION, "unknown topic " + topic);
+  parts_.clear();
+  if (partitions.empty()) {
+    for (int p = 0; p < n; ++p) parts_.push_back(p);
+  } else {
+    for (int p : partitions) {
+      if (p < 0 || p >= n)
+        throw KafkaError(UNKNOWN_TOPIC_OR_PARTITION,
+                         "partition " + std::to_string(p) + " not in " + topic);
+      parts_.push_back(p);
+    }
+  }
+  pos_.clear();
+}
+
+int64_t Consumer::list_offset(int partition, int64_t ts) {
+  ListOffsetsRequest req;
+  req.topics.push_back({topic_, {{partition, ts}}});
+  Writer w;
+  encode_list_offsets_request(w, req);
+  const std::string resp = cluster_.node(cluster_.leader(topic_, partition)).request(LIST_OFFSETS, w);
+  Reader r(resp);
+  const ListOffsetsResponse m = decode_list_offsets_response(r);
+  for (auto& t : m.topics)
+    for (auto& p : t.partitions)
+      if (p.index == partition) {
+        if (p.error != NONE) throw KafkaError(p.error, "ListOffsets: " + std::string(error_name(p.error)));
+        return p.offset;
+      }
+  throw KafkaError(-1, "ListOffsets: partition missing from response");
+}
+
+void Consumer::seek(int partition, int64_t offset) { pos_[partition] = offset; }
+
+int64_t Consumer::position(int partition) const {
+  auto it = pos_.find(partition);
+  return it == pos_.end() ? -1 : it->second;
+}
+
+void Consumer::seek_to(const std::string& where) {
+  for (int p : parts_) {
+    if (where == "latest") {
+      pos_[p] = list_offset(p, kLatest);
+    } else if (where == "earliest") {
+      pos_[p] = list_offset(p, kEarliest);
+    } else if (where == "committed") {
+      const int64_t c = cfg_.group_id.empty() ? -1 : committed(p);
+      pos_[p] = c >= 0 ? c : list_offset(p, cfg_.auto_offset_reset == "earliest" ? kEarliest : kLatest);
+    } else {
+      throw std::invalid_argument("seek_to: expected latest|earliest|committed, got " + where);
+    }
+  }
+}
+
+std::vector<Fetched> Consumer::poll() {
+  std::vector<Fetched> out;
+  for (int p : parts_)
+    if (!pos_.count(p)) pos_[p] = list_offset(p, cfg_.auto_offset_reset == "earliest" ? kEarliest : kLatest);
+  std::map<int32_t, std::vector<int>> by_leader;
+  for (int p : parts_) {
+    try {
+      by_leader[cluster_.leader(topic_, p)].push_back(p);
+    } catch (const KafkaError&) {
+      cluster_.invalidate();
+    }
+  }
+  // issue every leader's fetch first (long polls run concurrently), then collect
+  std::vector<std::pair<int32_t, int32_t>> sent;  // node, corr
+  for (auto& kv : by_leader) {
+    FetchRequest req;
+    req.max_wait_ms = cfg_.max_wait_ms;
+    req.min_bytes = cfg_.min_bytes;
+    req.max_bytes = cfg_.fetch_max_bytes;
+    FetchTopic ft;
+    ft.name = topic_;
+    for (int p : kv.second) ft.partitions.push_back({p, pos_[p], cfg_.partition_max_bytes});
+    req.topics.push_back(std::move(ft));
+    Writer w;
+    encode_fetch_request(w, req);
+    sent.push_back({kv.first, cluster_.node(kv.first).send(FETCH, w)});
+  }
+  bool stale = false;
+  for (auto& s : sent) {
+    Fetched f;
+    f.buf = cluster_.node(s.first).recv(s.second, &f.size, alloc_);
+    Reader r(f.buf.get(), f.size);
+    const FetchResponse m = decode_fetch_response(r);
+    for (auto& t : m.topics)
+      for (auto& p : t.partitions) {
+        if (p.error == OFFSET_OUT_OF_RANGE) {
+          pos_[p.index] = list_offset(p.index, cfg_.auto_offset_reset == "earliest" ? kEarliest : kLatest);
+          continue;
+        }
+        if (p.error != NONE) {
+          stale = true;
+          continue;
+        }
+        hw_[p.index] = p.high_watermark;
+        if (p.records_len <= 0) continue;
+        const size_t before = f.records.size();
+        decode_records(f.buf.get(), p.records_off, (size_t)p.records_len, pos_[p.index],
+                       cfg_.check_crcs, f.records);
+        for (size_t i = before; i < f.records.size(); ++i) f.records[i].partition = p.index;
+        if (f.records.size() > before) pos_[p.index] = f.records.back().offset + 1;
+      }
+    if (!f.records.empty()) out.push_back(std::move(f));
+  }
+  if (stale) cluster_.invalidate();
+  return out;
+}
+
+void Consumer::commit(const std::map<int, int64_t>& offsets) {
+  if (cfg_.group_id.empty()) throw std::invalid_argument("commit needs a group_id");
+  if (offsets.empty()) return;
+  OffsetCommitRequest req;
+  req.group_id = cfg_.group_id;
+  CommitTopic t;
+  t.name = topic_;
+  for (auto& kv : offsets) {
+    CommitPartition cp;
+    cp.index = kv.first;
+    cp.offset = kv.second;
+    t.partitions.push_back(cp);
+  }
+  req.topics.push_back(std::move(t));
+  Writer w;
+  encode_offset_commit_request(w, req);
+  const std::string resp = cluster_.coordinator(cfg_.group_id).request(OFFSET_COMMIT, w);
+  Reader r(resp);
+  for (auto& ct : decode_offset_commit_response(r))
+    for (auto& cp : ct.partitions)
+      if (cp.error != NONE) throw KafkaError(cp.error, "OffsetCommit failed");
+}
+
+int64_t Consumer::committed(int partition) {
+  OffsetFetchRequest req;
+  req.group_id = cfg_.group_id;
+  CommitTopic t;
+  t.name = topic_;
+  CommitPartition cp;
+  cp.index = partition;
+  t.partitions.push_back(cp);
+  req.topics.push_back(std::move(t));
+  Writer w;
+  encode_offset_fetch_request(w, req);
+  const std::string resp = cluster_.coordinator(cfg_.group_id).request(OFFSET_FETCH, w);
+  Reader r(resp);
+  for (auto& ct : decode_offset_fetch_response(r))
+    for (auto& p : ct.partitions)
+      if (p.index == partition) return p.offset;
+  return -1;
+}
+
+}  // namespace kafka
+}  // namespace gale

@@ -1,0 +1,224 @@
+// Kafka-protocol client: cluster metadata, producer and consumer.
+//
+// Replaces the two Kafka libraries of the reference:
+//   * Consumer  <- storm-kafka KafkaSpout (E1): partition discovery via Metadata, start position
+//     latest / earliest / committed (ListOffsets / OffsetFetch; the reference hard-wires
+//     LatestTime + ignoreZkOffsets, MainTopology.java:101-103), long-poll Fetch, offset commits
+//     (the spout's periodic ZK commits, X3), lag metrics (the spout's kafkaOffset metric).
+//   * Producer  <- kafka-clients 0.11 KafkaProducer (E7, KafkaBolt.java:111-113,144): async send
+//     with per-record callbacks on the sender thread, acks 0/1/-1 (MainTopology.java:113),
+//     batch.size / linger.ms accumulation per partition, pipelined in-flight requests, the
+//     DefaultPartitioner (murmur2 for keyed records, round-robin for null keys, E7/E9).
+// Fetch response bodies are received straight into caller-provided buffers (pinned host memory in
+// the serving engine), so record values are staged for the GPU without another copy.
+#pragma once
+#include <stdint.h>
+
+#include <atomic>
+#include <condition_variable>
+#include <deque>
+#include <functional>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "protocol.h"
+#include "wire.h"
+
+namespace gale {
+namespace kafka {
+
+struct KafkaError : std::runtime_error {
+  int code;
+  KafkaError(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+struct ClientConfig {
+  std::string bootstrap = "127.0.0.1:9092";  // host:port[,host:port...]
+  std::string client_id = "gale";
+  int request_timeout_ms = 30000;
+  int connect_timeout_ms = 10000;
+};
+
+// Response buffers: the body of a response frame (after the 4-byte size) is received into
+// memory obtained from this allocator. The shared_ptr's deleter returns it to its pool.
+using BufferAlloc = std::function<std::shared_ptr<uint8_t>(size_t bytes)>;
+std::shared_ptr<uint8_t> heap_alloc(size_t bytes);
+
+class Connection {
+ public:
+  Connection(const std::string& host, int port, const ClientConfig& cfg);
+  ~Connection();
+  Connection(const Connection&) = delete;
+  Connection& operator=(const Connection&) = delete;
+
+  int32_t send(ApiKey key, const Writer& body);  // returns the correlation id
+  // Receive the response for `corr` (responses arrive in request order on one connection).
+  // The returned buffer starts AFTER the correlation id.
+  std::shared_ptr<uint8_t> recv(int32_t corr, size_t* size, const BufferAlloc& alloc);
+  std::string request(ApiKey key, const Writer& body);  // send + recv into a string
+  const std::string& host() const { return host_; }
+  int port() const { return port_; }
+
+ private:
+  void send_all(const char* p, size_t n);
+  void recv_all(uint8_t* p, size_t n);
+  int fd_ = -1;
+  std::string host_;
+  int port_;
+  int32_t next_corr_ = 1;
+  std::string client_id_;
+};
+
+// Metadata cache + per-node connections (one Cluster per client thread; not thread-safe).
+class Cluster {
+ public:
+  explicit Cluster(ClientConfig cfg);
+  const ClientConfig& config() const { return cfg_; }
+  // Refresh metadata for `topics` (auto-creating them when the broker allows).
+  void refresh(const std::vector<std::string>& topics, bool auto_create = true);
+  int partitions(const std::string& topic);  // refreshes when unknown; -1 if absent
+  int32_t leader(const std::string& topic, int partition);
+  Connection& node(int32_t node_id);
+  Connection& any();
+  Connection& coordinator(const std::string& group);
+  std::vector<BrokerNode> brokers() const;
+  void invalidate() { topics_.clear(); }
+
+ private:
+  void check_versions(Connection& c);
+  ClientConfig cfg_;
+  std::map<int32_t, BrokerNode> nodes_;
+  std::map<int32_t, std::unique_ptr<Connection>> conns_;
+  std::unique_ptr<Connection> bootstrap_;
+  std::map<std::string, std::vector<int32_t>> topics_;  // topic -> leader per partition
+  std::map<std::string, int32_t> coordinators_;
+};
+
+// Java Kafka's murmur2 (Utils.murmur2), for keyed-record partitioning compatibility.
+int32_t murmur2(const uint8_t* data, size_t n);
+
+struct ProducerConfig : ClientConfig {
+  int acks = 1;                    // MainTopology.java:113
+  int linger_ms = 0;               // kafka-clients 0.11 default
+  int batch_size = 16384;          // kafka-clients 0.11 default (bytes per partition batch)
+  int max_request_size = 64 << 20;
+  int max_in_flight = 5;
+  int64_t buffer_memory = 1ll << 30;  // send() blocks while more than this is unsent
+};
+
+struct SendResult {
+  int16_t error = 0;
+  int32_t partition = -1;
+  int64_t offset = -1;
+};
+using SendCallback = std::function<void(const SendResult&)>;
+
+struct ProducerStats {
+  int64_t records_sent = 0, records_acked = 0, records_failed = 0, requests = 0, bytes = 0;
+};
+
+class Producer {
+ public:
+  explicit Producer(ProducerConfig cfg);
+  ~Producer();
+  Producer(const Producer&) = delete;
+  Producer& operator=(const Producer&) = delete;
+
+  // Asynchronous send. partition < 0 selects the partitioner. value_null sends a null record
+  // (tombstone) - what the reference's JsonSerializer does for a failed tuple.
+  void send(const std::string& topic, int partition, const std::string* key, std::string value,
+            bool value_null, std::vector<Header> headers, int64_t timestamp, SendCallback cb);
+  void flush();  // blocks until every record sent so far is acked or failed
+  void close();
+  int partitions_for(const std::string& topic);
+  ProducerStats stats() const;
+
+ private:
+  struct Pending {
+    std::string key;
+    bool key_null = true;
+    std::string value;
+    bool value_null = false;
+    std::vector<Header> headers;
+    int64_t ts = -1;
+    SendCallback cb;
+  };
+  struct PartBatch {
+    std::vector<Pending> recs;
+    size_t bytes = 0;
+    int64_t first_ms = 0;
+  };
+  struct InFlight {
+    int32_t corr;
+    int32_t node;
+    std::vector<std::pair<std::pair<std::string, int>, std::vector<Pending>>> batches;
+  };
+  void run();
+  int choose_partition(const std::string& topic, const std::string* key);
+
+  ProducerConfig cfg_;
+  Cluster cluster_;  // sender thread only
+  Cluster meta_;     // partition counts for send(), under mu_
+  mutable std::mutex mu_;
+  std::condition_variable cv_, done_cv_;
+  std::map<std::pair<std::string, int>, PartBatch> acc_;
+  std::map<std::string, int> nparts_;
+  int64_t unsent_bytes_ = 0;
+  int64_t outstanding_ = 0;
+  bool flush_req_ = false, closing_ = false;
+  uint32_t rr_ = 0;
+  std::thread thread_;
+  ProducerStats stats_;
+};
+
+struct ConsumerConfig : ClientConfig {
+  std::string group_id;            // empty: no offset commits
+  int max_wait_ms = 100;           // fetch long-poll
+  int min_bytes = 1;
+  int fetch_max_bytes = 64 << 20;
+  int partition_max_bytes = 16 << 20;
+  bool check_crcs = true;
+  std::string auto_offset_reset = "latest";  // on OFFSET_OUT_OF_RANGE / no committed offset
+};
+
+// One fetch round: records point into `buf` (the response body).
+struct Fetched {
+  std::shared_ptr<uint8_t> buf;
+  size_t size = 0;
+  std::vector<RecordRef> records;
+};
+
+class Consumer {
+ public:
+  Consumer(ConsumerConfig cfg, BufferAlloc alloc = heap_alloc);
+  void assign(const std::string& topic, const std::vector<int>& partitions);
+  const std::vector<int>& assignment() const { return parts_; }
+  const std::string& topic() const { return topic_; }
+  // "latest" | "earliest" | "committed" (committed falls back to auto_offset_reset)
+  void seek_to(const std::string& where);
+  void seek(int partition, int64_t offset);
+  int64_t position(int partition) const;
+  // One fetch round over all assigned partitions (grouped by leader). Empty when nothing arrived
+  // within max_wait_ms.
+  std::vector<Fetched> poll();
+  void commit(const std::map<int, int64_t>& offsets);  // next offset to read, per partition
+  int64_t committed(int partition);
+  std::map<int, int64_t> high_watermarks() const { return hw_; }
+  Cluster& cluster() { return cluster_; }
+
+ private:
+  int64_t list_offset(int partition, int64_t ts);
+  ConsumerConfig cfg_;
+  BufferAlloc alloc_;
+  Cluster cluster_;
+  std::string topic_;
+  std::vector<int> parts_;
+  std::map<int, int64_t> pos_, hw_;
+};
+
+}  // namespace kafka
+}  // namespace gale

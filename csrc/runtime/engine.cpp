@@ -1,0 +1,634 @@
+// The gale serving engine (see engine.h).
+#include "engine.h"
+
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+
+#include <algorithm>
+#include <sstream>
+
+#include "../codec/json_codec.h"
+
+namespace gale {
+
+// ---------------------------------------------------------------------------------------------
+// Batcher: bounded record queue + continuous micro-batch formation
+// ---------------------------------------------------------------------------------------------
+
+class Engine::Batcher {
+ public:
+  explicit Batcher(size_t cap) : cap_(cap) {}
+
+  // Blocks while the queue is full (backpressure to the Kafka consumer). False once closed.
+  bool push_many(std::vector<InRecord>& recs, const std::atomic<bool>& stop) {
+    size_t i = 0;
+    std::unique_lock<std::mutex> lk(mu_);
+    while (i < recs.size()) {
+      while (q_.size() >= cap_ && !closed_ && !stop)
+        cv_space_.wait_for(lk, std::chrono::milliseconds(20));
+      if (closed_ || (stop && q_.size() >= cap_)) return false;
+      while (i < recs.size() && q_.size() < cap_) {
+        images_ += recs[i].images;
+        q_.push_back(std::move(recs[i++]));
+      }
+      cv_items_.notify_all();
+    }
+    return true;
+  }
+
+  void requeue(std::vector<InRecord>&& recs) {
+    std::lock_guard<std::mutex> lk(mu_);
+    for (auto it = recs.rbegin(); it != recs.rend(); ++it) {
+      images_ += it->images;
+      q_.push_front(std::move(*it));
+    }
+    cv_items_.notify_all();
+  }
+
+  // Continuous batching: a full batch (max_images) is taken at once; a partial one when its
+  // oldest record has waited max_wait_ns, or immediately once the queue is closed (drain).
+  // With a batch already in flight on the caller's replica, a partial batch is not taken early
+  // (returns true with `out` empty) so the device work accumulates a fuller next batch.
+  bool take(int max_images, int64_t max_wait_ns, bool have_inflight, std::vector<InRecord>& out,
+            int& images) {
+    out.clear();
+    images = 0;
+    std::unique_lock<std::mutex> lk(mu_);
+    for (;;) {
+      if (q_.empty()) {
+        if (closed_) return false;
+        if (have_inflight) return true;
+        cv_items_.wait_for(lk, std::chrono::milliseconds(20));
+        continue;
+      }
+      const int64_t deadline = q_.front().t_fetch_ns + max_wait_ns;
+      const int64_t now = mono_ns();
+      if (images_ >= max_images || now >= deadline || closed_) {
+        while (!q_.empty() && (images == 0 || images + q_.front().images <= max_images)) {
+          images += q_.front().images;
+          images_ -= q_.front().images;
+          out.push_back(std::move(q_.front()));
+          q_.pop_front();
+        }
+        cv_space_.notify_all();
+        return true;
+      }
+      if (have_inflight) return true;
+      cv_items_.wait_for(lk, std::chrono::nanoseconds(std::max<int64_t>(deadline - now, 1000)));
+    }
+  }
+
+  void close() {
+    std::lock_guard<std::mutex> lk(mu_);
+    closed_ = true;
+    cv_items_.notify_all();
+    cv_space_.notify_all();
+  }
+  size_t size() {
+    std::lock_guard<std::mutex> lk(mu_);
+    return q_.size();
+  }
+
+ private:
+  std::mutex mu_;
+  std::condition_variable cv_items_, cv_space_;
+  std::deque<InRecord> q_;
+  int64_t images_ = 0;
+  size_t cap_;
+  bool closed_ = false;
+};
+
+struct Engine::ReplicaSlot {
+  std::shared_ptr<Replica> rep;
+  int index = 0;
+  std::atomic<bool> alive{true};
+  std::mutex mu;  // inflight
+  std::deque<std::shared_ptr<Batch>> inflight;
+  std::atomic<int64_t> batches{0}, images{0}, records{0};
+};
+
+// ---------------------------------------------------------------------------------------------
+
+Engine::Engine(EngineConfig cfg) : cfg_(std::move(cfg)), rng_(cfg_.seed) {
+  if (cfg_.input_topic.empty() || cfg_.output_topic.empty())
+    throw std::invalid_argument("engine: input and output topics are required");
+  if (cfg_.sink_mode != "async" && cfg_.sink_mode != "sync" && cfg_.sink_mode != "fire-and-forget")
+    throw std::invalid_argument("engine: sink_mode must be async|sync|fire-and-forget");
+  if (cfg_.on_error != "null" && cfg_.on_error != "error-json" && cfg_.on_error != "drop")
+    throw std::invalid_argument("engine: on_error must be null|error-json|drop");
+  if (cfg_.value_format != "json" && cfg_.value_format != "json-string")
+    throw std::invalid_argument("engine: value_format must be json|json-string");
+  if (cfg_.max_batch <= 0 || cfg_.source_parallelism <= 0 || cfg_.sink_parallelism <= 0)
+    throw std::invalid_argument("engine: max_batch / parallelism must be positive");
+  // fault injection spec: comma separated kind@value
+  std::stringstream ss(cfg_.fault);
+  std::string item;
+  while (std::getline(ss, item, ',')) {
+    if (item.empty()) continue;
+    const size_t at = item.find('@');
+    if (at == std::string::npos) throw std::invalid_argument("engine: bad fault spec " + item);
+    const std::string kind = item.substr(0, at), val = item.substr(at + 1);
+    if (kind == "replica_crash") crash_at_batch_ = std::stoll(val);
+    else if (kind == "parse_error") parse_error_p_ = std::stod(val);
+    else if (kind == "producer_fail") producer_fail_p_ = std::stod(val);
+    else throw std::invalid_argument("engine: unknown fault kind " + kind);
+  }
+  batcher_ = std::make_unique<Batcher>((size_t)std::max(1, cfg_.queue_depth));
+}
+
+Engine::~Engine() {
+  try {
+    stop();
+  } catch (...) {
+  }
+}
+
+void Engine::add_replica(std::shared_ptr<Replica> r) {
+  if (running_) throw std::logic_error("engine: add_replica after start");
+  if (r->max_images() < cfg_.max_batch)
+    throw std::invalid_argument("engine: replica " + r->name() + " max batch " +
+                                std::to_string(r->max_images()) + " < engine max_batch " +
+                                std::to_string(cfg_.max_batch));
+  auto s = std::make_shared<ReplicaSlot>();
+  s->rep = std::move(r);
+  s->index = (int)replicas_.size();
+  replicas_.push_back(std::move(s));
+}
+
+kafka::Producer* Engine::producer_for(int i) {
+  return producers_[(size_t)i % producers_.size()].get();
+}
+
+bool Engine::fault_hit(double p) {
+  if (p <= 0) return false;
+  std::lock_guard<std::mutex> lk(rng_mu_);
+  return std::uniform_real_distribution<double>(0, 1)(rng_) < p;
+}
+
+void Engine::start() {
+  if (running_) return;
+  if (replicas_.empty()) throw std::logic_error("engine: no replicas");
+  for (int i = 0; i < cfg_.sink_parallelism; ++i) {
+    kafka::ProducerConfig pc;
+    pc.bootstrap = cfg_.bootstrap;
+    pc.client_id = cfg_.client_id + "-sink-" + std::to_string(i);
+    pc.acks = cfg_.acks;
+    pc.linger_ms = cfg_.linger_ms;
+    pc.batch_size = cfg_.batch_size;
+    producers_.push_back(std::make_unique<kafka::Producer>(pc));
+  }
+  // resolve the input partitions and split them over the source threads
+  std::vector<int> parts = cfg_.partitions;
+  if (parts.empty()) {
+    kafka::Cluster cl(kafka::ClientConfig{cfg_.bootstrap, cfg_.client_id, 30000, 10000});
+    const int n = cl.partitions(cfg_.input_topic);
+    if (n <= 0) throw kafka::KafkaError(kafka::UNKNOWN_TOPIC_OR_PARTITION,
+                                        "input topic " + cfg_.input_topic + " not found");
+    for (int p = 0; p < n; ++p) parts.push_back(p);
+  }
+  const int ns = std::min<int>(cfg_.source_parallelism, (int)parts.size());
+  std::vector<std::vector<int>> split((size_t)ns);
+  for (size_t i = 0; i < parts.size(); ++i) split[i % (size_t)ns].push_back(parts[i]);
+  running_ = true;
+  stopping_ = false;
+  sources_done_ = false;
+  sources_active_ = ns;
+  for (auto& rs : replicas_) workers_.emplace_back([this, rs] { worker_loop(rs.get()); });
+  for (int i = 0; i < ns; ++i)
+    sources_.emplace_back([this, i, p = split[(size_t)i]] { source_loop(i, p); });
+  watchdog_ = std::thread([this] { watchdog_loop(); });
+}
+
+void Engine::stop() {
+  if (!running_) return;
+  stopping_ = true;
+  {
+    // wait for the sources to stop fetching
+    std::unique_lock<std::mutex> lk(done_mu_);
+    done_cv_.wait_for(lk, std::chrono::seconds(30), [&] { return sources_active_ == 0; });
+  }
+  batcher_->close();
+  for (size_t i = 0; i < workers_.size(); ++i) {
+    if (replicas_[i]->alive) {
+      workers_[i].join();
+    } else {
+      workers_[i].detach();  // may be stuck on a dead device; its batches were re-queued
+    }
+  }
+  workers_.clear();
+  for (auto& p : producers_) p->flush();
+  sources_done_ = true;  // sources may now commit their final offsets
+  done_cv_.notify_all();
+  for (auto& t : sources_) t.join();
+  sources_.clear();
+  running_ = false;
+  done_cv_.notify_all();
+  if (watchdog_.joinable()) watchdog_.join();
+  for (auto& p : producers_) p->close();
+  producers_.clear();
+}
+
+bool Engine::wait(int64_t timeout_ms) {
+  std::unique_lock<std::mutex> lk(done_mu_);
+  auto pred = [&] {
+    return !running_ || stopping_ ||
+           (cfg_.max_records > 0 && completed_.load() >= cfg_.max_records);
+  };
+  if (timeout_ms < 0) done_cv_.wait(lk, pred);
+  else done_cv_.wait_for(lk, std::chrono::milliseconds(timeout_ms), pred);
+  return cfg_.max_records > 0 && completed_.load() >= cfg_.max_records;
+}
+
+// ---------------------------------------------------------------------------------------------
+// source
+// ---------------------------------------------------------------------------------------------
+
+void Engine::commit(kafka::Consumer& c, const std::vector<int>& parts) {
+  if (cfg_.group_id.empty()) return;
+  std::map<int, int64_t> offs;
+  {
+    std::lock_guard<std::mutex> lk(pend_mu_);
+    for (int p : parts) {
+      auto it = pending_.find(p);
+      if (it != pending_.end() && !it->second.empty()) offs[p] = it->second.begin()->first;
+      else if (next_fetch_.count(p)) offs[p] = next_fetch_[p];
+    }
+  }
+  try {
+    c.commit(offs);
+    ++commits_;
+  } catch (const std::exception& e) {
+    fprintf(stderr, "[gale source] offset commit failed: %s\n", e.what());
+  }
+}
+
+void Engine::source_loop(int idx, std::vector<int> parts) {
+  kafka::ConsumerConfig cc;
+  cc.bootstrap = cfg_.bootstrap;
+  cc.client_id = cfg_.client_id + "-source-" + std::to_string(idx);
+  cc.group_id = cfg_.group_id;
+  cc.max_wait_ms = cfg_.fetch_max_wait_ms;
+  cc.fetch_max_bytes = cfg_.fetch_max_bytes;
+  cc.partition_max_bytes = cfg_.partition_max_bytes;
+  cc.check_crcs = cfg_.check_crcs;
+  cc.auto_offset_reset = cfg_.start_offset == "earliest" ? "earliest" : "latest";
+  std::unique_ptr<kafka::Consumer> cons;
+  try {
+    cons = std::make_unique<kafka::Consumer>(cc);
+    cons->assign(cfg_.input_topic, parts);
+    cons->seek_to(cfg_.start_offset);
+    std::lock_guard<std::mutex> lk(pend_mu_);
+    for (int p : parts) next_fetch_[p] = cons->position(p);
+  } catch (const std::exception& e) {
+    fprintf(stderr, "[gale source %d] failed to start: %s\n", idx, e.what());
+    cons.reset();
+  }
+  int64_t last_commit = mono_ns();
+  std::vector<InRecord> good;
+  kafka::Producer* prod = producer_for(idx);
+  while (cons && !stopping_) {
+    std::vector<kafka::Fetched> fs;
+    try {
+      fs = cons->poll();
+    } catch (const std::exception& e) {
+      fprintf(stderr, "[gale source %d] fetch failed: %s\n", idx, e.what());
+      std::this_thread::sleep_for(std::chrono::milliseconds(100));
+      continue;
+    }
+    const int64_t now = mono_ns();
+    good.clear();
+    std::vector<InRecord> bad;
+    {
+      std::lock_guard<std::mutex> lk(pend_mu_);
+      for (auto& f : fs)
+        for (const kafka::RecordRef& rr : f.records) pending_[rr.partition][rr.offset] = 1;
+      for (int p : parts) next_fetch_[p] = cons->position(p);
+    }
+    for (auto& f : fs) {
+      for (const kafka::RecordRef& rr : f.records) {
+        InRecord r;
+        r.buf = f.buf;
+        r.value = rr.value_len >= 0 ? f.buf.get() + rr.value_off : nullptr;
+        r.len = rr.value_len;
+        r.partition = rr.partition;
+        r.offset = rr.offset;
+        r.timestamp_ms = rr.timestamp;
+        r.t_fetch_ns = now;
+        r.source = idx;
+        ++records_in_;
+        if (r.len < 0) {
+          r.status = codec::BAD_ENVELOPE;  // null value (Jackson would throw)
+        } else {
+          bytes_in_ += r.len;
+          const codec::Scan s = codec::scan_instances(r.value, (size_t)r.len, cfg_.H, cfg_.W, cfg_.C);
+          r.status = s.status;
+          r.arr_off = s.arr_off;
+          r.arr_len = s.arr_len;
+          r.images = s.images;
+          if (r.status == codec::OK && r.images > cfg_.max_batch) r.status = codec::TOO_LARGE;
+          if (r.status == codec::OK && fault_hit(parse_error_p_)) r.status = codec::BAD_ENVELOPE;
+        }
+        if (r.status == codec::OK) {
+          images_in_ += r.images;
+          good.push_back(std::move(r));
+        } else {
+          bad.push_back(std::move(r));
+        }
+      }
+    }
+    if (!fs.empty()) {
+      int64_t z = 0;
+      t_first_ns_.compare_exchange_strong(z, now);
+    }
+    for (InRecord& r : bad) emit_error(r, r.status, prod);
+    // when stopping with a full queue the rest stays pending (never committed, so a restart
+    // with start_offset=committed re-reads it)
+    if (!good.empty()) batcher_->push_many(good, stopping_);
+    if (mono_ns() - last_commit > (int64_t)cfg_.commit_interval_ms * 1000000) {
+      commit(*cons, parts);
+      last_commit = mono_ns();
+    }
+  }
+  {
+    std::lock_guard<std::mutex> lk(done_mu_);
+    --sources_active_;
+  }
+  done_cv_.notify_all();
+  if (cons) {
+    std::unique_lock<std::mutex> lk(done_mu_);
+    done_cv_.wait_for(lk, std::chrono::seconds(60), [&] { return sources_done_.load(); });
+    lk.unlock();
+    commit(*cons, parts);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// replicas
+// ---------------------------------------------------------------------------------------------
+
+void Engine::worker_loop(ReplicaSlot* rs) {
+  Replica& rep = *rs->rep;
+  if (rep.device() >= 0) hipSetDevice(rep.device());
+  const int64_t max_wait_ns = (int64_t)cfg_.max_wait_us * 1000;
+  const size_t depth = (size_t)std::max(1, rep.depth());
+  std::deque<std::shared_ptr<Batch>> mine;
+  auto fail = [&](const char* what, const std::string& msg) {
+    fprintf(stderr, "[gale replica %d %s] %s: %s -> replica marked dead, batches re-queued\n",
+            rs->index, rep.name().c_str(), what, msg.c_str());
+    std::vector<InRecord> back;
+    {
+      std::lock_guard<std::mutex> lk(rs->mu);
+      if (rs->alive.exchange(false)) {
+        for (auto& b : rs->inflight)
+          for (const InRecord& r : b->recs) back.push_back(r);
+        rs->inflight.clear();
+      }
+    }
+    ++replica_failures_;
+    requeued_ += (int64_t)back.size();
+    if (!back.empty()) batcher_->requeue(std::move(back));
+  };
+  while (rs->alive) {
+    if (mine.size() < depth) {
+      auto b = std::make_shared<Batch>();
+      int images = 0;
+      if (!batcher_->take(cfg_.max_batch, max_wait_ns, !mine.empty(), b->recs, images)) {
+        if (mine.empty()) break;  // closed and drained
+      } else if (!b->recs.empty()) {
+        b->images = images;
+        b->t_take_ns = mono_ns();
+        for (const InRecord& r : b->recs) h_queue_us_.add((b->t_take_ns - r.t_fetch_ns) / 1000);
+        const int64_t nb = ++batches_total_;
+        {
+          std::lock_guard<std::mutex> lk(rs->mu);
+          rs->inflight.push_back(b);
+        }
+        try {
+          if (crash_at_batch_ > 0 && nb == crash_at_batch_)
+            throw std::runtime_error("injected replica crash (fault replica_crash@" +
+                                     std::to_string(crash_at_batch_) + ")");
+          b->t_submit_ns = mono_ns();
+          rep.submit(*b);
+        } catch (const std::exception& e) {
+          fail("submit", e.what());
+          break;
+        }
+        mine.push_back(b);
+        continue;
+      }
+    }
+    if (mine.empty()) continue;
+    std::shared_ptr<Batch> f = mine.front();
+    try {
+      rep.wait(*f);
+    } catch (const std::exception& e) {
+      fail("wait", e.what());
+      break;
+    }
+    f->t_done_ns = mono_ns();
+    {
+      std::lock_guard<std::mutex> lk(rs->mu);
+      if (!rs->alive) break;  // the watchdog re-queued it already
+      rs->inflight.pop_front();
+    }
+    mine.pop_front();
+    finish_batch(rs, *f);
+  }
+}
+
+void Engine::watchdog_loop() {
+  while (running_ && !(stopping_ && workers_.empty())) {
+    std::this_thread::sleep_for(std::chrono::milliseconds(50));
+    const int64_t now = mono_ns();
+    for (auto& rs : replicas_) {
+      std::vector<InRecord> back;
+      {
+        std::lock_guard<std::mutex> lk(rs->mu);
+        if (!rs->alive || rs->inflight.empty()) continue;
+        const int64_t t0 = rs->inflight.front()->t_submit_ns;
+        if (t0 == 0 || now - t0 < (int64_t)cfg_.watchdog_ms * 1000000) continue;
+        rs->alive = false;
+        for (auto& b : rs->inflight)
+          for (const InRecord& r : b->recs) back.push_back(r);
+        rs->inflight.clear();
+      }
+      fprintf(stderr, "[gale watchdog] replica %d (%s) exceeded %d ms: marked dead, %zu records "
+              "re-queued\n", rs->index, rs->rep->name().c_str(), cfg_.watchdog_ms, back.size());
+      ++replica_failures_;
+      requeued_ += (int64_t)back.size();
+      batcher_->requeue(std::move(back));
+    }
+  }
+}
+
+void Engine::finish_batch(ReplicaSlot* rs, Batch& b) {
+  h_device_us_.add((b.t_done_ns - b.t_submit_ns) / 1000);
+  h_batch_images_.add(b.images);
+  rs->batches++;
+  rs->images += b.images;
+  rs->records += (int64_t)b.recs.size();
+  kafka::Producer* prod = producer_for(rs->index);
+  const bool js = cfg_.value_format == "json-string";
+  int img = 0;
+  std::string out;
+  for (size_t i = 0; i < b.recs.size(); ++i) {
+    InRecord& r = b.recs[i];
+    if (r.status == codec::OK && i < b.dev_status.size()) r.status = b.dev_status[i];
+    if (r.status != codec::OK) {
+      emit_error(r, r.status, prod);
+    } else {
+      codec::encode_predictions(b.probs + (size_t)img * cfg_.classes, r.images, cfg_.classes, js,
+                                out);
+      emit(r, out, false, prod);
+    }
+    img += r.images;
+  }
+  if (cfg_.sink_mode == "sync") prod->flush();
+}
+
+// ---------------------------------------------------------------------------------------------
+// sink
+// ---------------------------------------------------------------------------------------------
+
+void Engine::complete_record(const InRecord& r, bool ok) {
+  {
+    std::lock_guard<std::mutex> lk(pend_mu_);
+    auto it = pending_.find(r.partition);
+    if (it != pending_.end()) it->second.erase(r.offset);
+  }
+  const int64_t now = mono_ns();
+  if (ok) {
+    ++records_out_;
+    images_out_ += r.images;
+    h_engine_e2e_us_.add((now - r.t_fetch_ns) / 1000);
+    if (r.timestamp_ms > 0) h_record_e2e_ms_.add(wall_ms_now() - r.timestamp_ms);
+  } else {
+    ++produce_failures_;
+  }
+  t_last_ns_ = now;
+  const int64_t c = ++completed_;
+  if (cfg_.max_records > 0 && c >= cfg_.max_records) {
+    std::lock_guard<std::mutex> lk(done_mu_);
+    done_cv_.notify_all();
+  }
+}
+
+void Engine::emit(InRecord& r, std::string value, bool null_value, kafka::Producer* prod) {
+  std::vector<kafka::Header> hs;
+  if (cfg_.type_id_header) hs.push_back({"__TypeId__", "java.lang.String", false});
+  // the callback keeps only what completion needs (not the fetch buffer)
+  InRecord meta;
+  meta.partition = r.partition;
+  meta.offset = r.offset;
+  meta.timestamp_ms = r.timestamp_ms;
+  meta.t_fetch_ns = r.t_fetch_ns;
+  meta.images = r.status == codec::OK ? r.images : 0;
+  const bool ff = cfg_.sink_mode == "fire-and-forget";
+  kafka::SendCallback cb;
+  if (!ff) {
+    cb = [this, meta](const kafka::SendResult& res) {
+      const bool ok = res.error == 0 && !fault_hit(producer_fail_p_);
+      complete_record(meta, ok);
+    };
+  }
+  try {
+    prod->send(cfg_.output_topic, -1, nullptr, std::move(value), null_value, std::move(hs), -1,
+               std::move(cb));
+  } catch (const std::exception& e) {
+    fprintf(stderr, "[gale sink] send failed: %s\n", e.what());
+    complete_record(meta, false);
+    return;
+  }
+  if (ff) complete_record(meta, true);  // KafkaBolt fire-and-forget acks immediately
+}
+
+void Engine::emit_error(InRecord& r, int status, kafka::Producer* prod) {
+  ++errors_;
+  err_by_status_[status & 7]++;
+  if (cfg_.on_error == "drop") {
+    ++dropped_;
+    InRecord meta = r;
+    meta.images = 0;
+    complete_record(meta, true);
+    return;
+  }
+  if (cfg_.on_error == "null") {
+    emit(r, std::string(), true, prod);
+    return;
+  }
+  std::string v;
+  codec::encode_error(status, "", cfg_.value_format == "json-string", v);
+  emit(r, std::move(v), false, prod);
+}
+
+// ---------------------------------------------------------------------------------------------
+// metrics
+// ---------------------------------------------------------------------------------------------
+
+std::map<std::string, double> Engine::stats() const {
+  std::map<std::string, double> s;
+  s["records_in"] = (double)records_in_;
+  s["images_in"] = (double)images_in_;
+  s["bytes_in"] = (double)bytes_in_;
+  s["records_out"] = (double)records_out_;
+  s["images_out"] = (double)images_out_;
+  s["completed"] = (double)completed_;
+  s["errors"] = (double)errors_;
+  s["produce_failures"] = (double)produce_failures_;
+  s["dropped"] = (double)dropped_;
+  s["requeued"] = (double)requeued_;
+  s["replica_failures"] = (double)replica_failures_;
+  s["commits"] = (double)commits_;
+  s["batches"] = (double)batches_total_;
+  s["queue_records"] = (double)const_cast<Batcher*>(batcher_.get())->size();
+  for (int i = 1; i < 8; ++i)
+    s[std::string("err_") + codec::status_name(i)] = (double)err_by_status_[i];
+  const double el = (double)(t_last_ns_ - t_first_ns_) * 1e-9;
+  s["elapsed_s"] = el > 0 ? el : 0;
+  s["images_per_s"] = el > 0 ? (double)images_out_ / el : 0;
+  auto q = [&](const char* n, const Histogram& h) {
+    s[std::string(n) + "_p50"] = h.quantile(0.5);
+    s[std::string(n) + "_p90"] = h.quantile(0.9);
+    s[std::string(n) + "_p99"] = h.quantile(0.99);
+    s[std::string(n) + "_max"] = (double)h.max();
+    s[std::string(n) + "_mean"] = h.mean();
+  };
+  q("queue_us", h_queue_us_);
+  q("device_us", h_device_us_);
+  q("e2e_us", h_engine_e2e_us_);
+  q("record_e2e_ms", h_record_e2e_ms_);
+  q("batch_images", h_batch_images_);
+  int alive = 0;
+  for (auto& r : replicas_) alive += r->alive ? 1 : 0;
+  s["replicas_alive"] = alive;
+  return s;
+}
+
+std::vector<ReplicaStats> Engine::replica_stats() const {
+  std::vector<ReplicaStats> v;
+  for (auto& r : replicas_) {
+    ReplicaStats s;
+    s.name = r->rep->name();
+    s.device = r->rep->device();
+    s.alive = r->alive;
+    s.batches = r->batches;
+    s.images = r->images;
+    s.records = r->records;
+    v.push_back(s);
+  }
+  return v;
+}
+
+void Engine::reset_stats() {
+  h_queue_us_.reset();
+  h_device_us_.reset();
+  h_engine_e2e_us_.reset();
+  h_record_e2e_ms_.reset();
+  h_batch_images_.reset();
+  images_out_ = 0;
+  records_out_ = 0;
+  t_first_ns_ = mono_ns();
+  t_last_ns_ = t_first_ns_.load();
+}
+
+}  // namespace gale

@@ -1,0 +1,160 @@
+// The gale serving engine: Kafka source -> micro-batcher -> model replicas -> Kafka sink.
+//
+// This is the whole Storm topology of the reference (MainTopology.java:52-92) collapsed into one
+// process per GPU with native threads and bounded in-memory queues instead of Storm executors,
+// Netty/Kryo tuple transport and ackers:
+//
+//   source threads  (KafkaSpout x KAFKA_SPOUT_PARAL, MainTopology.java:26,61)
+//      Consumer.poll -> codec::scan_instances (envelope check + image count, AVX2)
+//      -> Batcher (bounded: backpressure to the consumer)
+//   replica workers (InferenceBolt x INFERENCE_BOLT_PARAL, :27,62; shuffle grouping :62 -> pull)
+//      Batcher.take: continuous micro-batching (max_batch images or max_wait_us since the oldest
+//      record; an idle replica pulls first, which is least-loaded dispatch) -> Replica.submit /
+//      wait (depth-deep pipelining) -> encode {"predictions": ...} per record
+//   sink            (KafkaBolt x KAFKA_BOLT_PARAL, :28,63)
+//      Producer.send async | sync | fire-and-forget (KafkaBolt.java:129-155), acks (:113)
+//
+// Delivery: offsets of a partition are committed up to the first record whose output has not
+// been acknowledged (at-least-once when start_offset=committed). The reference is at-most-once,
+// latest-only; start_offset=latest reproduces that default.
+// Failure handling: a replica that throws or exceeds the watchdog deadline is
+// marked dead and its in-flight batches are re-queued to the surviving replicas; malformed input
+// follows on_error = null (reference: a null record, InferenceBolt.java:92-99) | error-json |
+// drop.
+#pragma once
+#include <stdint.h>
+
+#include <atomic>
+#include <condition_variable>
+#include <deque>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <random>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../kafka/client.h"
+#include "metrics.h"
+#include "replica.h"
+
+namespace gale {
+
+struct EngineConfig {
+  // source (R4, E1)
+  std::string bootstrap = "127.0.0.1:9092";
+  std::string input_topic, output_topic;
+  std::string group_id;            // offsets committed under this group (empty: no commits)
+  std::string client_id = "gale";
+  std::vector<int> partitions;     // empty = every partition of input_topic
+  int source_parallelism = 2;      // KAFKA_SPOUT_PARAL (MainTopology.java:26)
+  std::string start_offset = "latest";  // latest | earliest | committed
+  int fetch_max_wait_ms = 20;
+  int fetch_max_bytes = 64 << 20;
+  int partition_max_bytes = 16 << 20;
+  bool check_crcs = true;
+  int commit_interval_ms = 2000;   // storm-kafka's ZK commit period
+  // sink (R5, R9, E7-E9)
+  int sink_parallelism = 2;        // KAFKA_BOLT_PARAL (MainTopology.java:28)
+  int acks = 1;                    // MainTopology.java:113
+  std::string sink_mode = "async"; // async | sync | fire-and-forget (KafkaBolt.java:186-197)
+  int linger_ms = 0;
+  int batch_size = 1 << 20;
+  std::string value_format = "json";  // json | json-string (spring JsonSerializer, E8)
+  bool type_id_header = false;     // __TypeId__: java.lang.String header (E8)
+  std::string on_error = "null";   // null | error-json | drop
+  // model I/O contract (InstObj [N][H][W][C] -> PredObj [N][classes])
+  int H = 32, W = 32, C = 3, classes = 10;
+  // batching (P7)
+  int max_batch = 256;             // images per micro-batch (<= every replica's max)
+  int max_wait_us = 2000;          // latency bound on batch formation
+  int queue_depth = 8192;          // records buffered between source and replicas
+  // robustness
+  int watchdog_ms = 30000;         // a batch longer than this on a replica marks it dead
+  std::string fault;               // "replica_crash@N,parse_error@P,producer_fail@P"
+  int64_t max_records = -1;        // stop once this many records are completed (bench/tests)
+  uint64_t seed = 0;
+};
+
+struct ReplicaStats {
+  std::string name;
+  int device = -1;
+  bool alive = true;
+  int64_t batches = 0, images = 0, records = 0;
+};
+
+class Engine {
+ public:
+  explicit Engine(EngineConfig cfg);
+  ~Engine();
+  Engine(const Engine&) = delete;
+  Engine& operator=(const Engine&) = delete;
+
+  void add_replica(std::shared_ptr<Replica> r);
+  void start();
+  // Graceful stop: sources stop fetching, queued records drain through the replicas, the sink
+  // is flushed and offsets are committed.
+  void stop();
+  // Block until max_records completed, stop() was called, or timeout (ms; <0 = forever).
+  // Returns true when the record target was reached.
+  bool wait(int64_t timeout_ms);
+  bool running() const { return running_; }
+  int64_t completed() const { return completed_.load(); }
+
+  // counters and latency quantiles for the metrics reporter
+  std::map<std::string, double> stats() const;
+  std::vector<ReplicaStats> replica_stats() const;
+  void reset_stats();
+  const EngineConfig& config() const { return cfg_; }
+
+ private:
+  struct Pending;    // per-partition outstanding offsets
+  struct ReplicaSlot;
+  class Batcher;
+
+  void source_loop(int idx, std::vector<int> parts);
+  void worker_loop(ReplicaSlot* rs);
+  void watchdog_loop();
+  void finish_batch(ReplicaSlot* rs, Batch& b);
+  void emit(InRecord& r, std::string value, bool null_value, kafka::Producer* prod);
+  void emit_error(InRecord& r, int status, kafka::Producer* prod);
+  void complete_record(const InRecord& r, bool ok);
+  void commit(kafka::Consumer& c, const std::vector<int>& parts);
+  kafka::Producer* producer_for(int i);
+  bool fault_hit(double p);
+
+  EngineConfig cfg_;
+  std::vector<std::shared_ptr<ReplicaSlot>> replicas_;
+  std::unique_ptr<Batcher> batcher_;
+  std::vector<std::unique_ptr<kafka::Producer>> producers_;
+  std::vector<std::thread> sources_, workers_;
+  std::thread watchdog_;
+  std::atomic<bool> running_{false}, stopping_{false}, sources_done_{false};
+  std::atomic<int> sources_active_{0};
+
+  std::mutex pend_mu_;
+  std::map<int, std::map<int64_t, int>> pending_;  // partition -> offset -> 1
+  std::map<int, int64_t> next_fetch_;              // partition -> next offset to fetch
+
+  std::mutex done_mu_;
+  std::condition_variable done_cv_;
+  std::atomic<int64_t> completed_{0};
+
+  // fault injection
+  int64_t crash_at_batch_ = -1;
+  double parse_error_p_ = 0, producer_fail_p_ = 0;
+  std::atomic<int64_t> batches_total_{0};
+  std::mutex rng_mu_;
+  std::mt19937_64 rng_;
+
+  // metrics
+  std::atomic<int64_t> records_in_{0}, images_in_{0}, records_out_{0}, images_out_{0};
+  std::atomic<int64_t> bytes_in_{0}, errors_{0}, produce_failures_{0}, dropped_{0};
+  std::atomic<int64_t> requeued_{0}, replica_failures_{0}, commits_{0};
+  std::atomic<int64_t> err_by_status_[8] = {};
+  Histogram h_queue_us_, h_device_us_, h_engine_e2e_us_, h_record_e2e_ms_, h_batch_images_;
+  std::atomic<int64_t> t_first_ns_{0}, t_last_ns_{0};
+};
+
+}  // namespace gale

@@ -1,0 +1,177 @@
+// Inference replicas (see replica.h).
+#include "replica.h"
+
+#include <math.h>
+#include <string.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <stdexcept>
+
+#include "../codec/json_codec.h"
+
+namespace gale {
+
+// ---------------------------------------------------------------------------------------------
+// StubReplica
+// ---------------------------------------------------------------------------------------------
+
+StubReplica::StubReplica(int H, int W, int C, int classes, int max_images, int delay_us)
+    : H_(H), W_(W), C_(C), classes_(classes), max_images_(max_images), delay_us_(delay_us) {
+  x_.resize((size_t)max_images * H * W * C);
+  probs_.resize((size_t)max_images * classes);
+}
+
+void StubReplica::submit(Batch& b) {
+  const size_t per = (size_t)H_ * W_ * C_;
+  int slot = 0;
+  b.dev_status.assign(b.recs.size(), codec::OK);
+  for (size_t ri = 0; ri < b.recs.size(); ++ri) {
+    InRecord& r = b.recs[ri];
+    int n = 0;
+    const int st = codec::parse_instances_host(r.value, (size_t)r.len, H_, W_, C_,
+                                               x_.data() + (size_t)slot * per,
+                                               max_images_ - slot, &n);
+    if (st != codec::OK) b.dev_status[ri] = st;
+    for (int i = 0; i < r.images; ++i) {
+      const float* img = x_.data() + (size_t)(slot + i) * per;
+      float* out = probs_.data() + (size_t)(slot + i) * classes_;
+      if (st != codec::OK) {
+        std::fill(out, out + classes_, 0.f);
+        continue;
+      }
+      double mx = -1e300;
+      for (int k = 0; k < classes_; ++k) {
+        double s = 0;
+        for (size_t p = (size_t)(k % C_); p < per; p += (size_t)C_) s += img[p];
+        const double logit = (k + 1) * s / (double)(per / (size_t)C_);
+        out[k] = (float)logit;
+        mx = std::max(mx, logit);
+      }
+      double sum = 0;
+      for (int k = 0; k < classes_; ++k) sum += exp((double)out[k] - mx);
+      for (int k = 0; k < classes_; ++k) out[k] = (float)(exp((double)out[k] - mx) / sum);
+    }
+    slot += r.images;
+  }
+  if (delay_us_ > 0) usleep((useconds_t)delay_us_);
+  b.probs = probs_.data();
+}
+
+void StubReplica::wait(Batch& b) { (void)b; }
+
+// ---------------------------------------------------------------------------------------------
+// GpuReplica
+// ---------------------------------------------------------------------------------------------
+
+GpuReplica::GpuReplica(std::shared_ptr<Executor> exec, int H, int W, int C, int classes,
+                       bool use_graph)
+    : exec_(std::move(exec)), H_(H), W_(W), C_(C), classes_(classes), use_graph_(use_graph) {
+  if (exec_->input_bytes_per_image() != (long long)H * W * C * 4)
+    throw std::invalid_argument("GpuReplica: executor input is not fp32 [H, W, C]");
+  if (exec_->output_bytes_per_image() != (long long)classes * 4)
+    throw std::invalid_argument("GpuReplica: executor output is not fp32 [classes]");
+  check_hip(hipSetDevice(exec_->device()), "hipSetDevice");
+  check_hip(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "hipStreamCreate");
+  const int mb = exec_->max_batch();
+  slots_.resize((size_t)exec_->slots());
+  for (Slot& s : slots_) {
+    check_hip(hipHostMalloc(reinterpret_cast<void**>(&s.h_recs), sizeof(JsonRecord) * mb),
+              "hipHostMalloc(recs)");
+    check_hip(hipMalloc(reinterpret_cast<void**>(&s.d_recs), sizeof(JsonRecord) * mb),
+              "hipMalloc(recs)");
+    check_hip(hipHostMalloc(reinterpret_cast<void**>(&s.h_out), sizeof(float) * mb * classes),
+              "hipHostMalloc(out)");
+    check_hip(hipEventCreateWithFlags(&s.done, hipEventDisableTiming), "hipEventCreate");
+    // initial text capacity: ~12 bytes per number (Java Float.toString + ", ") x a full batch
+    ensure_capacity(s, (size_t)mb * H * W * C * 12 + 4096);
+  }
+}
+
+GpuReplica::~GpuReplica() {
+  hipSetDevice(exec_->device());
+  if (stream_) hipStreamSynchronize(stream_);
+  for (Slot& s : slots_) {
+    if (s.h_bytes) hipHostFree(s.h_bytes);
+    if (s.d_bytes) hipFree(s.d_bytes);
+    if (s.h_recs) hipHostFree(s.h_recs);
+    if (s.d_recs) hipFree(s.d_recs);
+    if (s.h_out) hipHostFree(s.h_out);
+    if (s.done) hipEventDestroy(s.done);
+  }
+  if (stream_) hipStreamDestroy(stream_);
+}
+
+std::string GpuReplica::name() const { return "gpu" + std::to_string(exec_->device()); }
+
+void GpuReplica::ensure_capacity(Slot& s, size_t bytes) {
+  if (bytes <= s.cap) return;
+  size_t cap = std::max(bytes, s.cap * 2);
+  cap = (cap + 4095) & ~(size_t)4095;
+  if (s.h_bytes) {
+    check_hip(hipEventSynchronize(s.done), "hipEventSynchronize");
+    hipHostFree(s.h_bytes);
+    hipFree(s.d_bytes);
+  }
+  check_hip(hipHostMalloc(reinterpret_cast<void**>(&s.h_bytes), cap), "hipHostMalloc(bytes)");
+  check_hip(hipMalloc(reinterpret_cast<void**>(&s.d_bytes), cap), "hipMalloc(bytes)");
+  s.cap = cap;
+}
+
+void GpuReplica::submit(Batch& b) {
+  const int slot = next_slot_;
+  next_slot_ = (next_slot_ + 1) % (int)slots_.size();
+  b.slot = slot;
+  Slot& s = slots_[(size_t)slot];
+  size_t total = 16;
+  for (const InRecord& r : b.recs) total += ((size_t)r.arr_len + 15) & ~(size_t)15;
+  ensure_capacity(s, total);
+  size_t off = 0;
+  int nrec = 0, img = 0;
+  for (const InRecord& r : b.recs) {
+    memcpy(s.h_bytes + off, r.value + r.arr_off, (size_t)r.arr_len);
+    JsonRecord& jr = s.h_recs[nrec++];
+    jr.off = (int64_t)off;
+    jr.len = (int32_t)r.arr_len;
+    jr.slot = img;
+    jr.images = r.images;
+    jr.status = 0;
+    const size_t padded = ((size_t)r.arr_len + 15) & ~(size_t)15;
+    memset(s.h_bytes + off + r.arr_len, ' ', padded - (size_t)r.arr_len);
+    off += padded;
+    img += r.images;
+  }
+  memset(s.h_bytes + off, ' ', 16);
+  if (img > exec_->max_batch()) throw std::logic_error("GpuReplica: batch exceeds max_batch");
+  b.images = img;
+  check_hip(hipMemcpyAsync(s.d_bytes, s.h_bytes, off + 16, hipMemcpyHostToDevice, stream_),
+            "H2D bytes");
+  check_hip(hipMemcpyAsync(s.d_recs, s.h_recs, sizeof(JsonRecord) * nrec, hipMemcpyHostToDevice,
+                           stream_),
+            "H2D recs");
+  check_hip(json_parse_instances(nrec, s.d_recs, s.d_bytes, H_, W_, C_,
+                                 static_cast<float*>(exec_->input(slot)), stream_),
+            "json_parse_instances");
+  exec_->run(slot, img, stream_, use_graph_);
+  check_hip(hipMemcpyAsync(s.h_out, exec_->output(slot), sizeof(float) * img * classes_,
+                           hipMemcpyDeviceToHost, stream_),
+            "D2H probs");
+  check_hip(hipMemcpyAsync(s.h_recs, s.d_recs, sizeof(JsonRecord) * nrec, hipMemcpyDeviceToHost,
+                           stream_),
+            "D2H status");
+  check_hip(hipEventRecord(s.done, stream_), "hipEventRecord");
+}
+
+void GpuReplica::wait(Batch& b) {
+  Slot& s = slots_[(size_t)b.slot];
+  check_hip(hipEventSynchronize(s.done), "hipEventSynchronize(batch)");
+  b.dev_status.assign(b.recs.size(), codec::OK);
+  for (size_t i = 0; i < b.recs.size(); ++i) {
+    const int st = s.h_recs[i].status;
+    if (st == 1 || st == 3) b.dev_status[i] = codec::BAD_SHAPE;
+    else if (st == 2) b.dev_status[i] = codec::BAD_NUMBER;
+  }
+  b.probs = s.h_out;
+}
+
+}  // namespace gale

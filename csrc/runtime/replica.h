@@ -1,0 +1,106 @@
+// Inference replicas driven by the serving engine.
+//
+// A replica is the InferenceBolt's model + session (InferenceBolt.java:43-62) and its per-tuple
+// execute (:70-99), generalised to micro-batches: the engine hands it a Batch of Kafka records
+// (already envelope-validated by codec::scan_instances), the replica turns their JSON text into
+// softmax rows. Replicas are asynchronous with a fixed depth so that host staging of batch k+1
+// overlaps device work on batch k:
+//   submit(b)  — enqueue (returns immediately for the GPU replica)
+//   wait(b)    — block until b's outputs and per-record statuses are on the host
+#pragma once
+#include <stdint.h>
+
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "gale/executor.h"
+#include "gale/kernels.h"
+
+namespace gale {
+
+struct InRecord {
+  std::shared_ptr<uint8_t> buf;  // keeps the fetch buffer alive
+  const uint8_t* value = nullptr;
+  int32_t len = -1;              // -1 = null value
+  int32_t partition = -1;
+  int64_t offset = -1;
+  int64_t timestamp_ms = -1;     // Kafka record CreateTime
+  int64_t t_fetch_ns = 0;        // host receive time
+  int64_t arr_off = 0, arr_len = 0;  // instances array inside the value (scan result)
+  int32_t images = 0;
+  int32_t status = 0;            // codec::Status (scan, then device parse)
+  int32_t source = 0;
+};
+
+struct Batch {
+  std::vector<InRecord> recs;
+  int images = 0;
+  int slot = 0;
+  const float* probs = nullptr;  // [images, classes] after wait()
+  std::vector<int32_t> dev_status;  // per-record codec::Status found by the replica's parser
+  int64_t t_take_ns = 0, t_submit_ns = 0, t_done_ns = 0;
+};
+
+class Replica {
+ public:
+  virtual ~Replica() = default;
+  virtual std::string name() const = 0;
+  virtual int max_images() const = 0;
+  virtual int depth() const = 0;  // batches that may be in flight
+  virtual void submit(Batch& b) = 0;
+  virtual void wait(Batch& b) = 0;
+  virtual int device() const { return -1; }
+};
+
+// CPU stub (SURVEY.md §4 "stub replica for plumbing tests on GPU-less hosts"): parses on the
+// host and computes a fixed deterministic classifier, logits[k] = (k+1) * mean(x[..., k % C]),
+// followed by softmax. An optional per-batch delay emulates device time.
+class StubReplica : public Replica {
+ public:
+  StubReplica(int H, int W, int C, int classes, int max_images, int delay_us);
+  std::string name() const override { return "stub"; }
+  int max_images() const override { return max_images_; }
+  int depth() const override { return 1; }
+  void submit(Batch& b) override;
+  void wait(Batch& b) override;
+
+ private:
+  int H_, W_, C_, classes_, max_images_, delay_us_;
+  std::vector<float> x_, probs_;
+};
+
+// One model replica on one GPU: staged JSON bytes -> GPU JSON parser -> hipGraph forward ->
+// softmax rows, all on the replica's own stream. `slots` I/O buffer sets pipeline host staging
+// with device work (the executor's per-slot graphs, csrc/runtime/executor.cpp).
+class GpuReplica : public Replica {
+ public:
+  GpuReplica(std::shared_ptr<Executor> exec, int H, int W, int C, int classes, bool use_graph);
+  ~GpuReplica() override;
+  std::string name() const override;
+  int max_images() const override { return exec_->max_batch(); }
+  int depth() const override { return exec_->slots(); }
+  int device() const override { return exec_->device(); }
+  void submit(Batch& b) override;
+  void wait(Batch& b) override;
+
+ private:
+  struct Slot {
+    uint8_t* h_bytes = nullptr;  // pinned staging of the JSON text
+    uint8_t* d_bytes = nullptr;
+    size_t cap = 0;
+    JsonRecord* h_recs = nullptr;
+    JsonRecord* d_recs = nullptr;
+    float* h_out = nullptr;      // pinned softmax rows
+    hipEvent_t done = nullptr;
+  };
+  void ensure_capacity(Slot& s, size_t bytes);
+  std::shared_ptr<Executor> exec_;
+  int H_, W_, C_, classes_;
+  bool use_graph_;
+  hipStream_t stream_ = nullptr;
+  std::vector<Slot> slots_;
+  int next_slot_ = 0;
+};
+
+}  // namespace gale

@@ -1,0 +1,160 @@
+"""One configuration object for a gale topology.
+
+The reference spreads its configuration over three layers: compiled-in constants
+(``NUM_WORKERS=8, KAFKA_SPOUT_PARAL=2, INFERENCE_BOLT_PARAL=4, KAFKA_BOLT_PARAL=2``,
+MainTopology.java:25-28), hard-coded ``zkHosts`` / ``bootstrap`` strings that must be edited in
+source (:33-34, README.md:38) and three positional CLI args (:36-38). gale keeps the positional
+``<TOPOLOGY_NAME> <INPUT_TOPIC> <OUTPUT_TOPIC>`` contract and turns every knob into a field with
+precedence
+
+    CLI flag  >  environment (GALE_<FIELD>)  >  TOML file (--config)  >  default.
+"""
+
+from __future__ import annotations
+
+import dataclasses
+import os
+from dataclasses import dataclass, field, fields
+from typing import Any, Dict, List, Optional
+
+CHOICES = {
+    "sink_mode": ("async", "sync", "fire-and-forget"),
+    "start_offset": ("latest", "earliest", "committed"),
+    "value_format": ("json", "json-string"),
+    "on_error": ("null", "error-json", "drop"),
+    "dtype": ("fp32", "bf16", "fp8"),
+    "model": ("lenet5", "resnet20", "resnet50"),
+}
+
+
+@dataclass
+class GaleConfig:
+    # positional contract (MainTopology.java:36-38)
+    topology_name: str = "gale"
+    input_topic: str = ""
+    output_topic: str = ""
+    # Kafka (R4, R5; the reference's zkHosts/bootstrap strings, MainTopology.java:33-34)
+    bootstrap: str = "127.0.0.1:9092"
+    embedded_broker: bool = False      # run an in-process broker on the bootstrap address
+    broker_partitions: int = 1         # partitions of auto-created topics (embedded broker)
+    group_id: str = ""                 # default: the topology name
+    start_offset: str = "latest"       # reference: LatestTime + ignoreZkOffsets (:101-102)
+    commit_interval_ms: int = 2000
+    # parallelism (R3)
+    workers: int = 8                   # NUM_WORKERS: placement only (one process per GPU here)
+    source_parallelism: int = 2        # KAFKA_SPOUT_PARAL
+    replicas: int = 0                  # INFERENCE_BOLT_PARAL; 0 = one per visible GPU
+    sink_parallelism: int = 2          # KAFKA_BOLT_PARAL
+    gpus: int = 0                      # GPUs to use (0 = all visible)
+    # sink (R9, E7-E9)
+    acks: int = 1                      # MainTopology.java:113
+    sink_mode: str = "async"           # KafkaBolt async / sync / fire-and-forget
+    value_format: str = "json"         # json-string = spring JsonSerializer double encoding
+    type_id_header: bool = False       # add __TypeId__: java.lang.String (spring JsonSerializer)
+    linger_ms: int = 0
+    on_error: str = "null"             # reference: malformed input -> null record
+    # lifetime (reference: sleep 1 h then kill, MainTopology.java:71-77)
+    duration: float = 3600.0
+    # model / compute
+    model: str = "resnet20"
+    dtype: str = "bf16"
+    weights: str = ""                  # .npz / .safetensors (torch layout); empty = seeded init
+    seed: int = 0
+    max_batch: int = 256
+    max_wait_us: int = 2000
+    queue_depth: int = 8192
+    use_graph: bool = True
+    stub: bool = False                 # CPU stub replicas (plumbing without a GPU)
+    # robustness / observability
+    watchdog_ms: int = 30000
+    fault: str = ""                    # replica_crash@N,parse_error@P,producer_fail@P
+    metrics_interval: float = 10.0
+    metrics_file: str = ""             # JSON lines; empty = stderr
+    log_level: str = "INFO"
+    registry_dir: str = field(default_factory=lambda: os.path.join(
+        os.path.expanduser("~"), ".gale", "topologies"))
+
+    def validate(self) -> "GaleConfig":
+        for k, allowed in CHOICES.items():
+            v = getattr(self, k)
+            if v not in allowed:
+                raise ValueError(f"{k}={v!r}: expected one of {allowed}")
+        if self.acks not in (0, 1, -1):
+            raise ValueError("acks must be 0, 1 or -1")
+        for k in ("source_parallelism", "sink_parallelism", "max_batch", "queue_depth"):
+            if getattr(self, k) <= 0:
+                raise ValueError(f"{k} must be positive")
+        if self.replicas < 0 or self.gpus < 0:
+            raise ValueError("replicas/gpus must be >= 0")
+        if not self.topology_name:
+            raise ValueError("topology name is required")
+        return self
+
+    @property
+    def effective_group(self) -> str:
+        return self.group_id or self.topology_name
+
+    def engine_dict(self, H: int, W: int, C: int, classes: int) -> Dict[str, Any]:
+        """Keyword dict for the native ``gale._C.Engine``."""
+        return dict(
+            bootstrap=self.bootstrap, input_topic=self.input_topic, output_topic=self.output_topic,
+            group_id=self.effective_group, client_id=self.topology_name,
+            source_parallelism=self.source_parallelism, start_offset=self.start_offset,
+            commit_interval_ms=self.commit_interval_ms, sink_parallelism=self.sink_parallelism,
+            acks=self.acks, sink_mode=self.sink_mode, linger_ms=self.linger_ms,
+            value_format=self.value_format, type_id_header=self.type_id_header,
+            on_error=self.on_error, H=H, W=W, C=C, classes=classes, max_batch=self.max_batch,
+            max_wait_us=self.max_wait_us, queue_depth=self.queue_depth,
+            watchdog_ms=self.watchdog_ms, fault=self.fault, seed=self.seed)
+
+
+def _coerce(f: dataclasses.Field, raw: Any) -> Any:
+    t = f.type if isinstance(f.type, str) else getattr(f.type, "__name__", str(f.type))
+    if t == "bool":
+        if isinstance(raw, bool):
+            return raw
+        s = str(raw).strip().lower()
+        if s in ("1", "true", "yes", "on"):
+            return True
+        if s in ("0", "false", "no", "off", ""):
+            return False
+        raise ValueError(f"{f.name}: not a boolean: {raw!r}")
+    if t == "int":
+        return int(raw)
+    if t == "float":
+        return float(raw)
+    return str(raw)
+
+
+def from_sources(cli: Optional[Dict[str, Any]] = None, env: Optional[Dict[str, str]] = None,
+                 toml_path: Optional[str] = None) -> GaleConfig:
+    """Merge defaults < TOML < env (GALE_*) < CLI (only keys explicitly given)."""
+    env = os.environ if env is None else env
+    values: Dict[str, Any] = {}
+    known = {f.name: f for f in fields(GaleConfig)}
+    if toml_path:
+        import tomli
+
+        with open(toml_path, "rb") as fh:
+            data = tomli.load(fh)
+        data = data.get("gale", data)
+        for k, v in data.items():
+            k = k.replace("-", "_")
+            if k not in known:
+                raise ValueError(f"{toml_path}: unknown key {k!r}")
+            values[k] = _coerce(known[k], v)
+    for name, f in known.items():
+        ev = env.get("GALE_" + name.upper())
+        if ev is not None:
+            values[name] = _coerce(f, ev)
+    for k, v in (cli or {}).items():
+        if v is None:
+            continue
+        if k not in known:
+            raise ValueError(f"unknown option {k!r}")
+        values[k] = _coerce(known[k], v)
+    return GaleConfig(**values).validate()
+
+
+def field_names() -> List[str]:
+    return [f.name for f in fields(GaleConfig)]

@@ -1,0 +1,111 @@
+"""Python face of the native serving engine (csrc/runtime/engine.cpp).
+
+Builds the replicas a topology asks for and hands them to ``gale._C.Engine``:
+
+* GPU replicas — one ``ModelReplica`` (packed weights + hipGraph plan executor) per replica,
+  placed round-robin over the process's GPUs. Weights are materialised once per device: on the
+  source rank from the seed (or a weights file) and RCCL-broadcast over xGMI to every other rank
+  of the default process group (``gale.parallel.weights``); inside one process they are copied
+  device-to-device. This replaces every InferenceBolt task loading its own SavedModel copy
+  (InferenceBolt.java:48-58).
+* stub replicas — the CPU plumbing replica (``--stub``), no GPU needed.
+
+The hot path never returns to Python: source threads, micro-batcher, replica workers and sink
+threads all run natively; Python only starts/stops the engine and reads its metrics.
+"""
+
+from __future__ import annotations
+
+from typing import Dict, List, Optional, Sequence
+
+from gale._native import native
+from gale.config import GaleConfig
+from gale.models import get_model
+
+
+def replica_devices(n_replicas: int, devices: Sequence[int]) -> List[int]:
+    if not devices:
+        raise ValueError("no devices to place replicas on")
+    return [devices[i % len(devices)] for i in range(n_replicas)]
+
+
+class Engine:
+    def __init__(self, cfg: GaleConfig, devices: Optional[Sequence[int]] = None,
+                 max_records: int = -1, params: Optional[dict] = None,
+                 model_replicas: Optional[list] = None):
+        self.cfg = cfg
+        self.net = get_model(cfg.model)
+        H, W, C = self.net.input_shape
+        d = cfg.engine_dict(H, W, C, self.net.classes)
+        d["max_records"] = max_records
+        self._native = native().Engine(d)
+        self.model_replicas: list = []
+        self.devices: List[int] = []
+        if cfg.stub:
+            for _ in range(max(1, cfg.replicas)):
+                self._native.add_stub_replica(cfg.max_batch, 0)
+            return
+        if model_replicas is not None:
+            reps = list(model_replicas)
+        else:
+            reps = self._build_gpu_replicas(devices, params)
+        for rep in reps:
+            self._native.add_gpu_replica(rep.executor, cfg.use_graph)
+            self.model_replicas.append(rep)
+            self.devices.append(rep.device.index or 0)
+
+    def _build_gpu_replicas(self, devices: Optional[Sequence[int]], params: Optional[dict]):
+        import torch
+
+        from gale.parallel.weights import materialize_weights
+        from gale.runtime.replica import ModelReplica
+
+        if not torch.cuda.is_available():
+            raise RuntimeError("no GPU visible: run with --stub for CPU plumbing replicas")
+        if devices is None:
+            n = torch.cuda.device_count()
+            devices = list(range(n if self.cfg.gpus <= 0 else min(self.cfg.gpus, n)))
+        n_rep = self.cfg.replicas if self.cfg.replicas > 0 else len(devices)
+        wdtype = "fp8" if self.cfg.dtype == "fp8" else "bf16"
+        packed: Dict[int, "torch.Tensor"] = {}
+        reps = []
+        for dev in replica_devices(n_rep, devices):
+            if dev not in packed:
+                if not packed:
+                    packed[dev] = materialize_weights(self.net, torch.device("cuda", dev),
+                                                      seed=self.cfg.seed, wdtype=wdtype,
+                                                      params=params)
+                else:  # same process: device-to-device copy over xGMI
+                    packed[dev] = next(iter(packed.values())).to(torch.device("cuda", dev))
+            reps.append(ModelReplica(self.net, packed[dev], max_batch=self.cfg.max_batch,
+                                     slots=2, wdtype=wdtype))
+        for r in reps:
+            r.capture()
+        return reps
+
+    # -- lifecycle ---------------------------------------------------------------------------
+    def start(self) -> None:
+        self._native.start()
+
+    def stop(self) -> None:
+        self._native.stop()
+
+    def wait(self, timeout_s: Optional[float] = None) -> bool:
+        return self._native.wait(-1 if timeout_s is None else int(timeout_s * 1000))
+
+    @property
+    def running(self) -> bool:
+        return self._native.running
+
+    @property
+    def completed(self) -> int:
+        return self._native.completed
+
+    def stats(self) -> Dict[str, float]:
+        return dict(self._native.stats())
+
+    def replica_stats(self) -> List[dict]:
+        return list(self._native.replica_stats())
+
+    def reset_stats(self) -> None:
+        self._native.reset_stats()

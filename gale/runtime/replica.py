@@ -34,6 +34,12 @@ class ModelReplica:
     def max_batch(self) -> int:
         return self.executor.max_batch
 
+    def capture(self) -> int:
+        """Pre-capture the hipGraph of every (batch bucket, I/O slot); returns the graph count."""
+        with torch.cuda.device(self.device):
+            self.executor.capture_all(torch.cuda.current_stream().cuda_stream)
+        return self.executor.graphs_captured
+
     def infer(self, x: torch.Tensor, use_graph: bool = True, slot: int = 0) -> torch.Tensor:
         """x: [B,H,W,C] fp32 (any device) -> softmax [B, classes] fp32 on this replica's GPU."""
         B = x.shape[0]
