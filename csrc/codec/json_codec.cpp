@@ -104,6 +104,32 @@ size_t parse_json_number(const uint8_t* p, size_t n, float* out) {
   return i;
 }
 
+// Decimal digits (trailing zeros dropped) and exponent of a > 0: a = d1.d2d3.. x 10^e.
+// precision < 0: shortest round-trip digits; otherwise `precision` digits after the first.
+void sci_digits(float a, int precision, char* dig, int* nd, int* e) {
+  char buf[48];
+  auto r = precision < 0
+               ? std::to_chars(buf, buf + sizeof(buf), a, std::chars_format::scientific)
+               : std::to_chars(buf, buf + sizeof(buf), a, std::chars_format::scientific, precision);
+  int n = 0;
+  const char* c = buf;
+  while (c < r.ptr && *c != 'e') {
+    if (*c != '.') dig[n++] = *c;
+    ++c;
+  }
+  int x = 0;
+  if (c < r.ptr) {
+    ++c;
+    bool neg = false;
+    if (*c == '-' || *c == '+') { neg = *c == '-'; ++c; }
+    while (c < r.ptr) x = x * 10 + (*c++ - '0');
+    if (neg) x = -x;
+  }
+  while (n > 1 && dig[n - 1] == '0') --n;
+  *nd = n;
+  *e = x;
+}
+
 }  // namespace
 
 Scan scan_instances(const uint8_t* p, size_t n, int H, int W, int C) {
@@ -230,25 +256,13 @@ int format_float_java(float v, char* out) {
   const float a = fabsf(v);
   if (isinf(a)) { memcpy(o, "Infinity", 8); return (int)(o - out) + 8; }
   if (a == 0.f) { memcpy(o, "0.0", 3); return (int)(o - out) + 3; }
-  char buf[32];
-  auto r = std::to_chars(buf, buf + sizeof(buf), a, std::chars_format::scientific);
-  // buf = d[.ddd]e(+|-)xx
+  // shortest round-trip digits (std::to_chars, Ryu); JDK 19+ spec: when the shortest decimal
+  // has one digit, take the decimal of length 1 or 2 closest to the value instead
+  // (Float.MIN_VALUE -> "1.4E-45", not "1.0E-45"), i.e. the correctly rounded 2-digit form.
   char dig[16];
-  int nd = 0;
-  const char* c = buf;
-  while (c < r.ptr && *c != 'e') {
-    if (*c != '.') dig[nd++] = *c;
-    ++c;
-  }
-  int e = 0;
-  if (c < r.ptr) {
-    ++c;
-    bool neg = false;
-    if (*c == '-' || *c == '+') { neg = *c == '-'; ++c; }
-    while (c < r.ptr) e = e * 10 + (*c++ - '0');
-    if (neg) e = -e;
-  }
-  while (nd > 1 && dig[nd - 1] == '0') --nd;
+  int nd = 0, e = 0;
+  sci_digits(a, -1, dig, &nd, &e);
+  if (nd == 1) sci_digits(a, 1, dig, &nd, &e);
   const int dec_exp = e + 1;  // value = 0.d1d2.. x 10^dec_exp (Java FloatingDecimal decExponent)
   if (dec_exp > 0 && dec_exp < 8) {
     if (nd <= dec_exp) {

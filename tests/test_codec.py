@@ -1,0 +1,126 @@
+"""Host JSON codec: the InstObj/PredObj contract (InstObj.java:8, PredObj.java:9) and Jackson
+compatibility (FAIL_ON_UNKNOWN_PROPERTIES, Java Float.toString output)."""
+
+import json
+
+import numpy as np
+import pytest
+from hypothesis import given, settings
+from hypothesis import strategies as st
+
+from gale._native import native
+
+C = native()
+OK, BAD_ENVELOPE, UNKNOWN_KEY, BAD_SHAPE, EMPTY, BAD_NUMBER, NULL_INSTANCES = range(7)
+
+
+def rec(arr):
+    return json.dumps({"instances": arr}).encode()
+
+
+def img(h, w, c, base=0.0):
+    return [[[base + (i * w + j) * c + k for k in range(c)] for j in range(w)] for i in range(h)]
+
+
+@pytest.mark.parametrize("n", [1, 2, 5])
+def test_scan_counts_images(n):
+    data = rec([img(4, 3, 2, base=i) for i in range(n)])
+    st_, off, ln, images = C.scan_instances(data, 4, 3, 2)
+    assert st_ == OK and images == n
+    assert data[off:off + 1] == b"[" and data[off + ln - 1:off + ln] == b"]"
+
+
+@pytest.mark.parametrize("data,expected", [
+    (b'{"instances": [[[[1,2]]]], "extra": 1}', UNKNOWN_KEY),      # Jackson FAIL_ON_UNKNOWN
+    (b'{"other": [[[[1,2]]]]}', UNKNOWN_KEY),
+    (b'{"instances": null}', NULL_INSTANCES),
+    (b'{}', NULL_INSTANCES),
+    (b'{"instances": []}', EMPTY),
+    (b'not json', BAD_ENVELOPE),
+    (b'[1,2,3]', BAD_ENVELOPE),
+    (b'{"instances": [[[[1,2]]]]', BAD_ENVELOPE),                  # unterminated object
+    (b'{"instances": [[["a","b"]]]}', BAD_NUMBER),
+    (b'  {  "instances" :  [[[[1,2]]]]  }  ', OK),                  # whitespace everywhere
+])
+def test_scan_statuses(data, expected):
+    st_ = C.scan_instances(data, 1, 1, 2)[0]
+    assert st_ == expected, C.status_name(st_)
+
+
+def test_parse_host_matches_json():
+    rng = np.random.default_rng(0)
+    x = rng.standard_normal((3, 4, 5, 2)).astype(np.float32)
+    data = rec(x.tolist())
+    st_, out = C.parse_instances_host(data, 4, 5, 2)
+    assert st_ == OK
+    np.testing.assert_array_equal(out, x)  # float64 repr -> float32 rounds back exactly
+
+
+@pytest.mark.parametrize("bad", [
+    [[[[1, 2]], [[3]]]],          # ragged innermost
+    [[[[1, 2], [3, 4]]]],         # W=2 where the model expects W=1
+    [[[1, 2]]],                   # rank 3
+    [[[[1, 2, 3]]]],              # C=3
+])
+def test_parse_host_rejects_bad_shapes(bad):
+    st_, _ = C.parse_instances_host(rec(bad), 1, 1, 2)
+    assert st_ in (BAD_SHAPE, EMPTY), C.status_name(st_)
+
+
+@pytest.mark.parametrize("num", ["01", "1.", ".5", "+1", "1e", "--1", "0x10", "1.2.3", "NaN"])
+def test_parse_host_rejects_bad_numbers(num):
+    data = b'{"instances": [[[[' + num.encode() + b', 1]]]]}'
+    st_, _ = C.parse_instances_host(data, 1, 1, 2)
+    assert st_ in (BAD_NUMBER, BAD_SHAPE), C.status_name(st_)
+
+
+# Java Float.toString (JDK >= 19 shortest-digit spec; identical to JDK 8 for these values)
+@pytest.mark.parametrize("v,s", [
+    (0.0, "0.0"), (-0.0, "-0.0"), (1.0, "1.0"), (0.1, "0.1"), (0.5, "0.5"), (3.0, "3.0"),
+    (100.0, "100.0"), (0.001, "0.001"), (0.0001, "1.0E-4"), (1e-5, "1.0E-5"),
+    (1.25e-5, "1.25E-5"), (9999999.0, "9999999.0"), (1e7, "1.0E7"), (1.5e7, "1.5E7"),
+    (123456.7, "123456.7"), (-2.5, "-2.5"), (float("inf"), "Infinity"),
+    (float("-inf"), "-Infinity"), (float("nan"), "NaN"), (0.3, "0.3"),
+    (0.09874, "0.09874"), (3.4028235e38, "3.4028235E38"), (1.4e-45, "1.4E-45"),
+])
+def test_format_float_java(v, s):
+    assert C.format_float_java(v) == s
+
+
+@settings(max_examples=300, deadline=None)
+@given(st.floats(width=32, allow_nan=False, allow_infinity=False))
+def test_format_float_java_roundtrips(v):
+    s = C.format_float_java(v)
+    assert np.float32(float(s)) == np.float32(v)
+
+
+def test_encode_predictions_json_and_json_string():
+    p = np.array([[0.5, 0.25, 1e-5], [0.1, 0.2, 0.7]], dtype=np.float32)
+    out = C.encode_predictions(p, False)
+    assert out == b'{"predictions":[[0.5,0.25,1.0E-5],[0.1,0.2,0.7]]}'
+    d = json.loads(out)
+    np.testing.assert_allclose(np.array(d["predictions"], dtype=np.float32), p)
+    s = C.encode_predictions(p[:1], True)  # spring JsonSerializer double encoding (E8)
+    assert json.loads(json.loads(s)) == {"predictions": [[0.5, 0.25, 1e-5]]}
+
+
+def test_encode_error_record():
+    e = json.loads(C.encode_error(UNKNOWN_KEY, 'bad "key"', False))
+    assert e == {"error": "unknown_key", "detail": 'bad "key"'}
+    e2 = json.loads(json.loads(C.encode_error(BAD_SHAPE, "", True)))
+    assert e2 == {"error": "bad_shape"}
+
+
+@settings(max_examples=40, deadline=None)
+@given(st.integers(1, 3), st.integers(1, 4), st.integers(1, 4), st.integers(1, 3),
+       st.integers(0, 2**31 - 1))
+def test_instances_roundtrip(n, h, w, c, seed):
+    rng = np.random.default_rng(seed)
+    x = (rng.standard_normal((n, h, w, c)) * 10.0 ** rng.integers(-6, 6)).astype(np.float32)
+    data = C.encode_instances(x)
+    assert json.loads(data)["instances"] is not None
+    st_, off, ln, images = C.scan_instances(data, h, w, c)
+    assert st_ == OK and images == n
+    st2, y = C.parse_instances_host(data, h, w, c)
+    assert st2 == OK
+    np.testing.assert_array_equal(y, x)

@@ -1,0 +1,169 @@
+"""The serving engine end to end on CPU: embedded broker -> native engine with stub replicas ->
+output topic (SURVEY.md §7.3 "reduced first milestone ... stub replica on CPU"). Covers the
+reference's semantics (one output record per input record, unkeyed, null record on malformed
+input, InferenceBolt.java:70-99) and the new capabilities (micro-batching, error policies,
+fault injection, offset commits / resume)."""
+
+import json
+
+import numpy as np
+import pytest
+
+from gale._native import native
+from gale.config import GaleConfig
+from gale.engine import Engine
+
+C = native()
+K = C.kafka
+H, W, CH, CLASSES = 32, 32, 3, 10
+
+
+def stub_probs(x):
+    """The StubReplica classifier: logits[k] = (k+1) * mean(x[..., k % C])."""
+    means = x.reshape(x.shape[0], -1, x.shape[-1]).astype(np.float64).mean(axis=1)
+    logits = np.stack([(k + 1) * means[:, k % x.shape[-1]] for k in range(CLASSES)], axis=1)
+    e = np.exp(logits - logits.max(axis=1, keepdims=True))
+    return e / e.sum(axis=1, keepdims=True)
+
+
+@pytest.fixture()
+def broker():
+    b = K.Broker()
+    b.start()
+    b.create_topic("in", 2)
+    b.create_topic("out", 1)
+    yield b
+    b.stop()
+
+
+def make_cfg(broker, **kw):
+    base = dict(topology_name="t", input_topic="in", output_topic="out",
+                bootstrap=f"127.0.0.1:{broker.port}", start_offset="earliest", stub=True,
+                max_batch=16, max_wait_us=500, queue_depth=64, commit_interval_ms=100)
+    base.update(kw)
+    return GaleConfig(**base)
+
+
+def run(broker, n_records, **kw):
+    eng = Engine(make_cfg(broker, **kw), max_records=n_records)
+    eng.start()
+    assert eng.wait(30), eng.stats()
+    eng.stop()
+    return eng, broker.read("out", 0)
+
+
+def produce_images(broker, counts, seed=0):
+    rng = np.random.default_rng(seed)
+    imgs = []
+    for i, n in enumerate(counts):
+        x = rng.random((n, H, W, CH), dtype=np.float32)
+        imgs.append(x)
+        broker.append("in", i % 2, [C.encode_instances(x)])
+    return imgs
+
+
+def test_predictions_match_stub_and_one_output_per_record(broker):
+    counts = [1, 3, 1, 2, 5, 1, 1, 4] * 3
+    imgs = produce_images(broker, counts)
+    eng, out = run(broker, len(counts))
+    assert len(out) == len(counts)
+    assert all(r["key"] is None for r in out)  # unkeyed, like FieldNameBasedTupleToKafkaMapper
+    preds = [np.array(json.loads(r["value"])["predictions"]) for r in out]
+    expected = {tuple(np.round(stub_probs(x).ravel(), 5)) for x in imgs}
+    got = {tuple(np.round(p.ravel(), 5)) for p in preds}
+    assert got == expected
+    st = eng.stats()
+    assert st["images_out"] == sum(counts) and st["errors"] == 0
+    assert st["batch_images_max"] <= 16
+
+
+@pytest.mark.parametrize("policy", ["null", "error-json", "drop"])
+def test_error_policies(broker, policy):
+    produce_images(broker, [1, 1])
+    broker.append("in", 0, [b'{"instances": [[1,2]], "extra": 0}', b"garbage", None,
+                            b'{"instances": [[[[1.0, 2.0]]]]}'])  # wrong shape for 32x32x3
+    eng, out = run(broker, 6, on_error=policy)
+    vals = [r["value"] for r in out]
+    good = [v for v in vals if v is not None and b"predictions" in v]
+    assert len(good) == 2
+    bad = [v for v in vals if v is None or b"predictions" not in v]
+    if policy == "null":
+        assert bad == [None] * 4
+    elif policy == "error-json":
+        assert sorted(json.loads(v)["error"] for v in bad) == [
+            "bad_envelope", "bad_envelope", "bad_shape", "unknown_key"]
+    else:
+        assert bad == []
+    assert eng.stats()["errors"] == 4
+
+
+def test_json_string_value_and_type_header(broker):
+    produce_images(broker, [2])
+    _, out = run(broker, 1, value_format="json-string", type_id_header=True)
+    v = json.loads(json.loads(out[0]["value"]))  # spring JsonSerializer double encoding
+    assert len(v["predictions"]) == 2
+    assert out[0]["headers"] == [("__TypeId__", b"java.lang.String")]
+
+
+def test_replica_crash_requeues_without_loss(broker):
+    counts = [1] * 120
+    produce_images(broker, counts)
+    eng, out = run(broker, len(counts), replicas=2, fault="replica_crash@3")
+    st = eng.stats()
+    assert st["replica_failures"] == 1 and st["replicas_alive"] == 1
+    assert len([r for r in out if r["value"] is not None]) == 120
+    rs = eng.replica_stats()
+    assert sum(r["images"] for r in rs) == 120 and sum(not r["alive"] for r in rs) == 1
+
+
+@pytest.mark.parametrize("mode", ["sync", "fire-and-forget"])
+def test_sink_modes(broker, mode):
+    produce_images(broker, [1] * 20)
+    eng, out = run(broker, 20, sink_mode=mode)
+    assert len(out) == 20
+
+
+def test_commit_and_resume(broker):
+    produce_images(broker, [1] * 40)
+    run(broker, 40, group_id="grp")
+    assert broker.committed("grp", "in", 0) + broker.committed("grp", "in", 1) == 40
+    produce_images(broker, [1] * 10, seed=5)
+    eng, out = run(broker, 10, group_id="grp", start_offset="committed")
+    assert eng.stats()["records_in"] == 10  # resumed exactly after the committed offsets
+    assert len(out) == 50
+
+
+def test_latest_only_skips_backlog(broker):
+    # reference default: LatestTime + ignoreZkOffsets -> only records produced after start
+    produce_images(broker, [1] * 5)
+    eng = Engine(make_cfg(broker, start_offset="latest"), max_records=3)
+    eng.start()
+    import time
+
+    time.sleep(0.5)
+    produce_images(broker, [1] * 3, seed=9)
+    assert eng.wait(20)
+    eng.stop()
+    assert eng.stats()["records_in"] == 3
+
+
+def test_parse_error_and_producer_fault_injection(broker):
+    produce_images(broker, [1] * 60)
+    eng, out = run(broker, 60, fault="parse_error@0.5,producer_fail@0.2", seed=3)
+    st = eng.stats()
+    assert 10 < st["errors"] < 50
+    assert st["produce_failures"] > 0
+    assert len(out) == 60
+
+
+def test_backpressure_small_queue(broker):
+    produce_images(broker, [1] * 100)
+    eng, out = run(broker, 100, queue_depth=4, max_batch=4)
+    assert len(out) == 100 and eng.stats()["batch_images_max"] <= 4
+
+
+def test_bad_config_is_rejected(broker):
+    with pytest.raises(ValueError):
+        GaleConfig(sink_mode="bogus").validate()
+    with pytest.raises(Exception):
+        C.Engine(dict(input_topic="in", output_topic="out", on_error="explode"))

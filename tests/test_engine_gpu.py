@@ -1,0 +1,157 @@
+"""GPU serving path: the gfx950 JSON parser kernel against the host decoder, and the full
+engine (Kafka -> GPU JSON parse -> hipGraph forward -> Kafka) against the fp32 torch oracle."""
+
+import json
+
+import numpy as np
+import pytest
+import torch
+
+from gale._native import native
+from gale.config import GaleConfig
+from gale.engine import Engine
+from gale.models import fold_params, get_model, init_params
+from gale.models.reference import forward
+
+pytestmark = pytest.mark.gpu
+
+C = native()
+K = C.kafka
+REC = np.dtype([("off", "<i8"), ("len", "<i4"), ("slot", "<i4"), ("images", "<i4"),
+                ("status", "<i4")])
+
+
+def stage(arrays):
+    """Pack JSON array texts 16-byte aligned (+16 slack) and their JsonRecord table."""
+    buf = bytearray()
+    recs = np.zeros(len(arrays), dtype=REC)
+    slot = 0
+    for i, (txt, images) in enumerate(arrays):
+        recs[i] = (len(buf), len(txt), slot, images, 0)
+        buf += txt + b" " * ((-len(txt)) % 16)
+        slot += images
+    buf += b" " * 16
+    return np.frombuffer(bytes(buf), dtype=np.uint8), recs, slot
+
+
+def gpu_parse(arrays, H, Wd, Cc):
+    raw, recs, total = stage(arrays)
+    d_raw = torch.from_numpy(raw.copy()).cuda()
+    d_recs = torch.from_numpy(recs.view(np.uint8).copy()).cuda()
+    out = torch.full((max(total, 1), H, Wd, Cc), -7.0, device="cuda")
+    C.json_parse_instances(len(arrays), d_recs.data_ptr(), d_raw.data_ptr(), H, Wd, Cc,
+                           out.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    st = d_recs.cpu().numpy().view(REC)["status"]
+    return out.cpu().numpy(), st
+
+
+def array_text(record: bytes, H, Wd, Cc):
+    s, off, ln, n = C.scan_instances(record, H, Wd, Cc)
+    assert s == 0
+    return record[off:off + ln], n
+
+
+def test_gpu_json_parse_matches_host():
+    rng = np.random.default_rng(0)
+    H, Wd, Cc = 5, 4, 3
+    recs, xs = [], []
+    for n in (1, 3, 2):
+        x = (rng.standard_normal((n, H, Wd, Cc)) * 10.0 ** rng.integers(-8, 8, (n, H, Wd, Cc))
+             ).astype(np.float32)
+        xs.append(x)
+        recs.append(array_text(C.encode_instances(x), H, Wd, Cc))
+    # python's json.dumps formatting (doubles, spaces) must parse too
+    x4 = rng.random((2, H, Wd, Cc)).astype(np.float32)
+    xs.append(x4)
+    recs.append(array_text(json.dumps({"instances": x4.astype(np.float64).tolist()},
+                                      indent=1).encode(), H, Wd, Cc))
+    out, st = gpu_parse(recs, H, Wd, Cc)
+    assert list(st) == [0, 0, 0, 0]
+    ref = np.concatenate(xs)
+    np.testing.assert_allclose(out, ref, rtol=1e-6, atol=0)
+
+
+@pytest.mark.parametrize("txt,status", [
+    (b"[[[[1,2,3],[4,5,6]],[[1,2,3],[4,5,6]]]]", 0),
+    (b"[[[[1,2,3],[4,5,6]],[[1,2,3],[4,5]]]]", 1),        # one number short
+    (b"[[[[1,2,3],[4,5,6]],[[1,2,3,4],[5,6]]]]", 3),      # ragged: counts match, structure not
+    (b"[[[[1,2,3],[4,5,6],[1,2,3],[4,5,6]]]]", 3),        # 1x4 instead of 2x2
+    (b"[[[[1,2,3],[4,5,x6]],[[1,2,3],[4,5,6]]]]", 2),     # bad element
+    (b"[[[[1,2,3],[4,5,06]],[[1,2,3],[4,5,6]]]]", 2),     # leading zero
+    (b"[[[[1,2,3],[4,5,6]],[[1,2,3],[4,5,6]]]],[]", 3),   # trailing junk
+])
+def test_gpu_json_parse_validates_structure(txt, status):
+    _, st = gpu_parse([(txt, 1)], 2, 2, 3)
+    assert st[0] == status
+
+
+@pytest.fixture()
+def broker():
+    b = K.Broker()
+    b.start()
+    b.create_topic("in", 1)
+    b.create_topic("out", 1)
+    yield b
+    b.stop()
+
+
+def run_engine(broker, n, **kw):
+    cfg = GaleConfig(topology_name="g", input_topic="in", output_topic="out",
+                     bootstrap=f"127.0.0.1:{broker.port}", start_offset="earliest",
+                     max_batch=32, max_wait_us=500, **kw)
+    eng = Engine(cfg, devices=[0], max_records=n)
+    eng.start()
+    assert eng.wait(120), eng.stats()
+    eng.stop()
+    return eng, broker.read("out", 0)
+
+
+@pytest.mark.parametrize("model", ["resnet20", "lenet5"])
+def test_gpu_engine_matches_oracle(broker, model):
+    net = get_model(model)
+    params = init_params(net, seed=0, calib_batch=16)
+    rng = np.random.default_rng(1)
+    counts = [1, 2, 1, 3, 1, 1, 4, 1, 2, 1] * 3
+    xs = []
+    for n in counts:
+        x = rng.random((n,) + net.input_shape, dtype=np.float32)
+        xs.append(x)
+        broker.append("in", 0, [C.encode_instances(x)])
+    broker.append("in", 0, [b'{"instances": [[[[0.5]]]]}'])  # wrong shape -> null record
+    cfg = GaleConfig(topology_name="g", input_topic="in", output_topic="out", model=model,
+                     bootstrap=f"127.0.0.1:{broker.port}", start_offset="earliest",
+                     max_batch=32, max_wait_us=500)
+    eng = Engine(cfg, devices=[0], max_records=len(counts) + 1, params=params)
+    eng.start()
+    assert eng.wait(120), eng.stats()
+    eng.stop()
+    out = broker.read("out", 0)
+    assert len(out) == len(counts) + 1
+    assert sum(r["value"] is None for r in out) == 1
+    folded = fold_params(net, params)
+    # outputs arrive in an engine-defined order: match each to its closest reference
+    refs = [forward(net, folded, torch.from_numpy(x)).numpy() for x in xs]
+    got = [np.array(json.loads(r["value"])["predictions"]) for r in out if r["value"]]
+    used = set()
+    for g in got:
+        best = min((i for i in range(len(refs)) if i not in used and refs[i].shape == g.shape),
+                   key=lambda i: np.abs(refs[i] - g).max())
+        used.add(best)
+        assert np.abs(refs[best] - g).max() < 3e-2
+    assert len(used) == len(refs)
+    st = eng.stats()
+    assert st["errors"] == 1 and st["images_out"] == sum(counts)
+
+
+def test_gpu_engine_two_replicas_on_one_gpu_and_crash(broker):
+    x = np.random.default_rng(2).random((1, 32, 32, 3), dtype=np.float32)
+    rec = C.encode_instances(x)
+    for _ in range(300):
+        broker.append("in", 0, [rec])
+    eng, out = run_engine(broker, 300, replicas=2, fault="replica_crash@4")
+    assert len(out) == 300 and all(r["value"] is not None for r in out)
+    st = eng.stats()
+    assert st["replica_failures"] == 1 and st["replicas_alive"] == 1
+    vals = {r["value"] for r in out}
+    assert len(vals) == 1  # identical input -> identical output on both replicas
