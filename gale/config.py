@@ -38,6 +38,7 @@ class GaleConfig:
     embedded_broker: bool = False      # run an in-process broker on the bootstrap address
     broker_partitions: int = 1         # partitions of auto-created topics (embedded broker)
     group_id: str = ""                 # default: the topology name
+    partitions: str = ""               # comma-separated input partitions (empty = all)
     start_offset: str = "latest"       # reference: LatestTime + ignoreZkOffsets (:101-102)
     commit_interval_ms: int = 2000
     # parallelism (R3)
@@ -99,6 +100,7 @@ class GaleConfig:
         return dict(
             bootstrap=self.bootstrap, input_topic=self.input_topic, output_topic=self.output_topic,
             group_id=self.effective_group, client_id=self.topology_name,
+            partitions=[int(p) for p in self.partitions.split(",") if p.strip()],
             source_parallelism=self.source_parallelism, start_offset=self.start_offset,
             commit_interval_ms=self.commit_interval_ms, sink_parallelism=self.sink_parallelism,
             acks=self.acks, sink_mode=self.sink_mode, linger_ms=self.linger_ms,

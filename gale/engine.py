@@ -67,6 +67,10 @@ class Engine:
             devices = list(range(n if self.cfg.gpus <= 0 else min(self.cfg.gpus, n)))
         n_rep = self.cfg.replicas if self.cfg.replicas > 0 else len(devices)
         wdtype = "fp8" if self.cfg.dtype == "fp8" else "bf16"
+        if params is None and self.cfg.weights:
+            from gale.models.weights_io import load_params
+
+            params = load_params(self.cfg.weights, self.net)
         packed: Dict[int, "torch.Tensor"] = {}
         reps = []
         for dev in replica_devices(n_rep, devices):

@@ -1,0 +1,66 @@
+"""Multi-process paths on CPU (gloo, world_size 2): the weight broadcast that replaces every
+InferenceBolt loading its own model copy (InferenceBolt.java:48-58; RCCL over xGMI on GPUs) and
+bench.py's one-process-per-GPU launch contract (torch.distributed.run, max-over-ranks timing)."""
+
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _bcast_worker(rank, world, port, q):
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from gale.models import get_model
+    from gale.parallel.weights import materialize_weights
+
+    net = get_model("resnet20")
+    # only rank 0's seed matters: every other rank receives rank 0's buffer
+    buf = materialize_weights(net, torch.device("cpu"), seed=0 if rank == 0 else 99)
+    q.put((rank, int(buf.sum().item()), buf.numel()))
+    dist.destroy_process_group()
+
+
+def test_weight_broadcast_gloo_world2():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bcast_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(60)
+    assert res[0][1:] == res[1][1:]
+
+
+def test_bench_stub_torchrun_world2():
+    port = _free_port()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "2",
+           "--stub", "--steps", "4", "--warmup", "1", "--batch", "32", "--distinct", "64",
+           "--timeout", "120"]
+    out = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=300,
+                         env=dict(os.environ, OMP_NUM_THREADS="1"))
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [json.loads(x) for x in out.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1  # rank 0 only
+    r = lines[0]
+    assert r["n_gpus"] == 2 and r["steps"] == 4 and r["value"] > 0
+    assert r["config"]["parallelism"] == "dp2" and r["config"]["global_batch"] == 64
