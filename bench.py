@@ -43,14 +43,20 @@ def parse_args():
     ap.add_argument("--batch", type=int, default=256, help="images per step per GPU")
     ap.add_argument("--images-per-record", type=int, default=1)
     ap.add_argument("--distinct", type=int, default=1024, help="distinct synthetic images")
-    ap.add_argument("--source-parallelism", type=int, default=2)
+    ap.add_argument("--partitions", type=int, default=0,
+                    help="input partitions per GPU (default: one per replica, BASELINE config 3)")
+    ap.add_argument("--source-parallelism", type=int, default=0,
+                    help="consumer threads (default: one per partition)")
     ap.add_argument("--sink-parallelism", type=int, default=2)
+    ap.add_argument("--decode-threads", type=int, default=2)
     ap.add_argument("--replicas-per-gpu", type=int, default=1)
     ap.add_argument("--max-wait-us", type=int, default=2000)
     ap.add_argument("--queue-batches", type=int, default=4,
                     help="records buffered in the engine, in units of --batch")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp8"])
     ap.add_argument("--stub", action="store_true", help="CPU stub replicas (no GPU)")
+    ap.add_argument("--stub-null", action="store_true",
+                    help="stub replicas skip parsing (measures the host Kafka/codec path only)")
     ap.add_argument("--timeout", type=float, default=600.0)
     return ap.parse_args()
 
@@ -84,7 +90,8 @@ def main() -> int:
     rpb = 64  # records per preloaded RecordBatch
     broker = K.Broker(max_message_bytes=256 << 20, retention_bytes=1 << 62)
     broker.start()
-    broker.create_topic("gale-in", 1)
+    parts = a.partitions or a.replicas_per_gpu
+    broker.create_topic("gale-in", parts)
     broker.create_topic("gale-out", 1)
     # slack: the warm-up engine drains everything it fetched (queue + in-flight fetches)
     per_rank_images = (a.warmup + a.steps + 4) * a.batch + 8192 * ipr + 4 * a.queue_batches * a.batch
@@ -92,7 +99,8 @@ def main() -> int:
     distinct = max(rpb, (a.distinct // (ipr * rpb)) * rpb) * ipr
     imgs = synthetic_images(distinct, net.input_shape, seed=1234 + rank)
     batches = encode_batches(encode_records(imgs, ipr), rpb)
-    preload(broker, "gale-in", 0, batches, n_records, rpb)
+    for p in range(parts):
+        preload(broker, "gale-in", p, batches, -(-n_records // parts), rpb)
     del imgs
 
     cfg = GaleConfig(topology_name=f"bench-r{rank}", input_topic="gale-in",
@@ -100,9 +108,10 @@ def main() -> int:
                      group_id="bench", start_offset="earliest", model=a.model, dtype=a.dtype,
                      max_batch=a.batch, max_wait_us=a.max_wait_us,
                      queue_depth=max(1, a.queue_batches * a.batch // ipr),
-                     source_parallelism=a.source_parallelism,
+                     source_parallelism=a.source_parallelism or parts,
                      sink_parallelism=a.sink_parallelism, replicas=a.replicas_per_gpu,
-                     stub=a.stub, commit_interval_ms=500)
+                     decode_threads=a.decode_threads,
+                     stub=a.stub, stub_null=a.stub_null, commit_interval_ms=500)
     devices = [local_rank] if use_gpu else None
     warm_records = -(-a.warmup * a.batch // ipr)
     eng = Engine(cfg, devices=devices, max_records=max(1, warm_records))  # weights: RCCL bcast
@@ -164,6 +173,8 @@ def main() -> int:
             "batch_images_mean": round(st["batch_images_mean"], 1),
             "json_mb_per_s_rank0": round(st["bytes_in"] / elapsed / 1e6, 1),
             "warmup_records": warm_done,
+            "rank0_thread_s": {k[9:]: round(v, 3) for k, v in st.items()
+                               if k.startswith("thread_s_")},
         }
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -30,6 +30,8 @@ EngineConfig config_from_dict(const py::dict& d) {
   opt(d, "fetch_max_bytes", c.fetch_max_bytes);
   opt(d, "partition_max_bytes", c.partition_max_bytes);
   opt(d, "check_crcs", c.check_crcs);
+  opt(d, "decode_threads", c.decode_threads);
+  opt(d, "pinned_fetch_bytes", c.pinned_fetch_bytes);
   opt(d, "commit_interval_ms", c.commit_interval_ms);
   opt(d, "sink_parallelism", c.sink_parallelism);
   opt(d, "acks", c.acks);
@@ -59,12 +61,12 @@ void bind_engine(py::module_& m) {
   py::class_<Engine, std::shared_ptr<Engine>>(m, "Engine")
       .def(py::init([](py::dict cfg) { return std::make_shared<Engine>(config_from_dict(cfg)); }))
       .def("add_stub_replica",
-           [](Engine& e, int max_images, int delay_us) {
+           [](Engine& e, int max_images, int delay_us, bool compute) {
              const EngineConfig& c = e.config();
-             e.add_replica(
-                 std::make_shared<StubReplica>(c.H, c.W, c.C, c.classes, max_images, delay_us));
+             e.add_replica(std::make_shared<StubReplica>(c.H, c.W, c.C, c.classes, max_images,
+                                                         delay_us, compute));
            },
-           py::arg("max_images") = 256, py::arg("delay_us") = 0)
+           py::arg("max_images") = 256, py::arg("delay_us") = 0, py::arg("compute") = true)
       .def("add_gpu_replica",
            [](Engine& e, std::shared_ptr<Executor> exec, bool use_graph) {
              const EngineConfig& c = e.config();

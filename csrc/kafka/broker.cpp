@@ -6,8 +6,6 @@
 #include <fcntl.h>
 #include <netinet/in.h>
 #include <netinet/tcp.h>
-#include <poll.h>
-#include <sys/eventfd.h>
 #include <sys/socket.h>
 #include <sys/uio.h>
 #include <unistd.h>
@@ -70,11 +68,8 @@ struct Broker::Chunk {
 
 struct Broker::Conn {
   int fd = -1;
-  std::string in;
-  size_t in_off = 0;
   std::deque<Chunk> out;
   bool parked = false;
-  bool closed = false;
   FetchRequest fetch;
   int32_t fetch_corr = 0;
   int64_t deadline = 0;
@@ -165,30 +160,33 @@ void Broker::start() {
   socklen_t len = sizeof(a);
   getsockname(listen_fd_, reinterpret_cast<sockaddr*>(&a), &len);
   port_ = ntohs(a.sin_port);
-  fcntl(listen_fd_, F_SETFL, fcntl(listen_fd_, F_GETFL) | O_NONBLOCK);
-  wake_fd_ = eventfd(0, EFD_NONBLOCK);
   running_ = true;
-  thread_ = std::thread([this] { run(); });
+  thread_ = std::thread([this] { accept_loop(); });
 }
 
 void Broker::stop() {
   if (!running_.exchange(false)) return;
-  wake();
+  shutdown(listen_fd_, SHUT_RDWR);  // unblocks accept()
   if (thread_.joinable()) thread_.join();
-  for (auto& c : conns_)
-    if (c->fd >= 0) close(c->fd);
-  conns_.clear();
-  if (listen_fd_ >= 0) close(listen_fd_);
-  if (wake_fd_ >= 0) close(wake_fd_);
-  listen_fd_ = wake_fd_ = -1;
+  close(listen_fd_);
+  listen_fd_ = -1;
+  {
+    std::lock_guard<std::mutex> lk(conn_mu_);
+    for (int fd : conn_fds_) shutdown(fd, SHUT_RDWR);  // unblocks recv()/writev()
+  }
+  wake();
+  for (auto& t : conn_threads_) t.join();
+  conn_threads_.clear();
+  conn_fds_.clear();
 }
 
+// Signals new data to long-polling fetches.
 void Broker::wake() {
-  if (wake_fd_ >= 0) {
-    uint64_t one = 1;
-    ssize_t r = write(wake_fd_, &one, 8);
-    (void)r;
+  {
+    std::lock_guard<std::mutex> lk(append_mu_);
+    ++append_seq_;
   }
+  append_cv_.notify_all();
 }
 
 bool Broker::create_topic(const std::string& topic, int partitions) {
@@ -329,130 +327,95 @@ std::string Broker::read_raw(const std::string& topic, int partition, int64_t of
 // I/O loop
 // ------------------------------------------------------------------------------------------
 
-void Broker::run() {
-  std::vector<pollfd> pfds;
+void Broker::accept_loop() {
   while (running_) {
-    pfds.clear();
-    pfds.push_back({listen_fd_, POLLIN, 0});
-    pfds.push_back({wake_fd_, POLLIN, 0});
-    int64_t next_deadline = now_ms() + 200;
-    for (auto& c : conns_) {
-      short ev = POLLIN;
-      if (!c->out.empty()) ev |= POLLOUT;
-      pfds.push_back({c->fd, ev, 0});
-      if (c->parked) next_deadline = std::min(next_deadline, c->deadline);
-    }
-    const int timeout = (int)std::max<int64_t>(0, next_deadline - now_ms());
-    const int nready = poll(pfds.data(), pfds.size(), timeout);
-    if (!running_) break;
-    if (nready < 0 && errno != EINTR) break;
-    bool appended = false;
-    if (pfds[1].revents & POLLIN) {
-      uint64_t v;
-      while (read(wake_fd_, &v, 8) == 8) {
-      }
-      appended = true;
-    }
-    if (pfds[0].revents & POLLIN) accept_all();
-    const size_t nconn = std::min(conns_.size(), pfds.size() - 2);
-    for (size_t i = 0; i < nconn; ++i) {
-      Conn& c = *conns_[i];
-      const short re = pfds[i + 2].revents;
-      if (re & (POLLERR | POLLNVAL)) {
-        c.closed = true;
-        continue;
-      }
-      if (re & (POLLIN | POLLHUP)) {
-        const int64_t before = stats_.produce_requests;
-        if (!handle_readable(c)) c.closed = true;
-        if (stats_.produce_requests != before) appended = true;
-      }
-      if (!c.closed && !c.out.empty() && !flush(c)) c.closed = true;
-    }
-    const int64_t t = now_ms();
-    for (auto& cp : conns_) {
-      Conn& c = *cp;
-      if (c.closed || !c.parked) continue;
-      if (appended || t >= c.deadline) {
-        if (try_fetch(c, t >= c.deadline)) {
-          // the fetch completed: continue with any pipelined requests of this connection
-          if (!process_frames(c)) c.closed = true;
-          if (!c.closed && !flush(c)) c.closed = true;
-        }
-      }
-    }
-    for (size_t i = 0; i < conns_.size();) {
-      if (conns_[i]->closed) {
-        close(conns_[i]->fd);
-        conns_.erase(conns_.begin() + (long)i);
-      } else {
-        ++i;
-      }
-    }
-  }
-}
-
-void Broker::accept_all() {
-  for (;;) {
     const int fd = accept(listen_fd_, nullptr, nullptr);
-    if (fd < 0) return;
-    set_sock_opts(fd);
-    auto c = std::make_unique<Conn>();
-    c->fd = fd;
-    conns_.push_back(std::move(c));
-    std::lock_guard<std::mutex> lk(mu_);
+    if (fd < 0) {
+      if (errno == EINTR) continue;
+      if (!running_) return;
+      std::this_thread::sleep_for(std::chrono::milliseconds(10));
+      continue;
+    }
+    int one = 1;
+    setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
+    int sz = 8 << 20;
+    setsockopt(fd, SOL_SOCKET, SO_SNDBUF, &sz, sizeof(sz));
+    setsockopt(fd, SOL_SOCKET, SO_RCVBUF, &sz, sizeof(sz));
+    std::lock_guard<std::mutex> lk(conn_mu_);
+    if (!running_) {
+      close(fd);
+      return;
+    }
+    conn_fds_.push_back(fd);
+    conn_threads_.emplace_back([this, fd] { serve(fd); });
+    std::lock_guard<std::mutex> lk2(mu_);
     ++stats_.connections;
   }
 }
 
-bool Broker::handle_readable(Conn& c) {
-  char buf[1 << 16];
-  for (;;) {
-    const ssize_t r = recv(c.fd, buf, sizeof(buf), 0);
-    if (r > 0) {
-      c.in.append(buf, (size_t)r);
-      {
-        std::lock_guard<std::mutex> lk(mu_);
-        stats_.bytes_in += r;
-      }
-      if (r < (ssize_t)sizeof(buf)) break;
-      continue;
-    }
+namespace {
+bool read_exact(int fd, char* p, size_t n) {
+  while (n) {
+    const ssize_t r = recv(fd, p, n, 0);
     if (r == 0) return false;
-    if (errno == EAGAIN || errno == EWOULDBLOCK) break;
-    if (errno == EINTR) continue;
-    return false;
-  }
-  return process_frames(c);
-}
-
-bool Broker::process_frames(Conn& c) {
-  while (!c.parked) {
-    const size_t avail = c.in.size() - c.in_off;
-    if (avail < 4) break;
-    int32_t sz;
-    {
-      Reader r(reinterpret_cast<const uint8_t*>(c.in.data()) + c.in_off, 4);
-      sz = r.i32();
-    }
-    if (sz < 0 || sz > (int32_t)std::min<int64_t>(cfg_.max_message_bytes + (16 << 20), 1 << 30))
+    if (r < 0) {
+      if (errno == EINTR) continue;
       return false;
-    if (avail < 4 + (size_t)sz) break;
-    const uint8_t* p = reinterpret_cast<const uint8_t*>(c.in.data()) + c.in_off + 4;
+    }
+    p += r;
+    n -= (size_t)r;
+  }
+  return true;
+}
+}  // namespace
+
+// One thread per client connection: blocking reads, requests answered in order, long-poll
+// Fetch waits on append_cv_ (so concurrent consumers are served by concurrent threads).
+void Broker::serve(int fd) {
+  Conn c;
+  c.fd = fd;
+  std::string frame;
+  while (running_) {
+    char hdr[4];
+    if (!read_exact(fd, hdr, 4)) break;
+    Reader hr(reinterpret_cast<const uint8_t*>(hdr), 4);
+    const int32_t sz = hr.i32();
+    if (sz < 0 || sz > (int32_t)std::min<int64_t>(cfg_.max_message_bytes + (16 << 20), 1 << 30))
+      break;
+    frame.resize((size_t)sz);
+    if (!read_exact(fd, &frame[0], (size_t)sz)) break;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stats_.bytes_in += 4 + sz;
+    }
     bool ok;
     try {
-      ok = handle_request(c, p, (size_t)sz);
+      ok = handle_request(c, reinterpret_cast<const uint8_t*>(frame.data()), frame.size());
     } catch (const ProtocolError&) {
       ok = false;
     }
-    if (!ok) return false;
-    c.in_off += 4 + (size_t)sz;
+    if (!ok) break;
+    if (c.parked) {
+      uint64_t seq;
+      {
+        std::lock_guard<std::mutex> lk(append_mu_);
+        seq = append_seq_;
+      }
+      bool final_attempt = c.fetch.max_wait_ms <= 0;
+      while (!try_fetch(c, final_attempt)) {
+        std::unique_lock<std::mutex> lk(append_mu_);
+        append_cv_.wait_until(
+            lk, std::chrono::steady_clock::time_point(std::chrono::milliseconds(c.deadline)),
+            [&] { return append_seq_ != seq || !running_; });
+        seq = append_seq_;
+        final_attempt = now_ms() >= c.deadline || !running_;
+      }
+    }
+    if (!flush(c)) break;
   }
-  if (c.in_off > 0 && (c.in_off == c.in.size() || c.in_off > (1 << 20))) {
-    c.in.erase(0, c.in_off);
-    c.in_off = 0;
-  }
-  return true;
+  close(fd);
+  std::lock_guard<std::mutex> lk(conn_mu_);
+  conn_fds_.erase(std::remove(conn_fds_.begin(), conn_fds_.end(), fd), conn_fds_.end());
 }
 
 bool Broker::flush(Conn& c) {
@@ -465,7 +428,6 @@ bool Broker::flush(Conn& c) {
     }
     const ssize_t w = writev(c.fd, iov, n);
     if (w < 0) {
-      if (errno == EAGAIN || errno == EWOULDBLOCK) return true;
       if (errno == EINTR) continue;
       return false;
     }
@@ -624,6 +586,7 @@ bool Broker::handle_request(Conn& c, const uint8_t* p, size_t n) {
           resp.topics.push_back(std::move(tr));
         }
       }
+      wake();
       if (req.acks == 0) return true;  // Kafka sends no response for acks=0
       encode_produce_response(w, resp);
       break;
@@ -637,8 +600,7 @@ bool Broker::handle_request(Conn& c, const uint8_t* p, size_t n) {
         std::lock_guard<std::mutex> lk(mu_);
         ++stats_.fetch_requests;
       }
-      try_fetch(c, c.fetch.max_wait_ms <= 0);
-      return true;
+      return true;  // serve() completes it (long poll)
     }
     case LIST_OFFSETS: {
       const ListOffsetsRequest req = decode_list_offsets_request(r);

@@ -6,8 +6,9 @@
 // client can talk to, with the reference's external contract unchanged (INPUT_TOPIC records in,
 // OUTPUT_TOPIC records out, MainTopology.java:36-38).
 //
-// * One poll() I/O thread; in-memory partition logs of RecordBatch v2 segments with byte-based
-//   retention; zero-copy Fetch responses (writev straight from the stored batches).
+// * One thread per client connection (blocking I/O, so concurrent consumers are served in
+//   parallel); in-memory partition logs of RecordBatch v2 segments with byte-based retention;
+//   zero-copy Fetch responses (writev straight from the stored batches).
 // * Long-poll Fetch (max_wait_ms / min_bytes), acks 0/1/-1 Produce, ListOffsets, consumer-group
 //   offset storage (FindCoordinator / OffsetCommit / OffsetFetch), CreateTopics, ApiVersions.
 // * Multi-broker clusters: set_cluster() makes partition p of every topic led by node
@@ -16,6 +17,7 @@
 #include <stdint.h>
 
 #include <atomic>
+#include <condition_variable>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -99,11 +101,9 @@ class Broker {
   };
   struct Conn;
 
-  void run();
+  void accept_loop();
+  void serve(int fd);
   void wake();
-  void accept_all();
-  bool handle_readable(Conn& c);
-  bool process_frames(Conn& c);
   bool handle_request(Conn& c, const uint8_t* p, size_t n);
   bool try_fetch(Conn& c, bool final_attempt);
   bool flush(Conn& c);
@@ -115,16 +115,21 @@ class Broker {
   int32_t leader_of(int partition) const;
 
   BrokerConfig cfg_;
-  int listen_fd_ = -1, wake_fd_ = -1;
+  int listen_fd_ = -1;
   int port_ = 0;
-  std::thread thread_;
+  std::thread thread_;  // acceptor
+  std::mutex conn_mu_;
+  std::vector<std::thread> conn_threads_;
+  std::vector<int> conn_fds_;
+  std::mutex append_mu_;  // long-poll wakeups
+  std::condition_variable append_cv_;
+  uint64_t append_seq_ = 0;
   std::atomic<bool> running_{false};
   mutable std::mutex mu_;  // topics_, offsets_, cluster_, stats_
   std::map<std::string, std::vector<PartitionLog>> topics_;
   std::map<std::string, int64_t> offsets_;  // "group\0topic\0partition" -> offset
   std::vector<BrokerNode> cluster_;
   BrokerStats stats_;
-  std::vector<std::unique_ptr<Conn>> conns_;
 };
 
 }  // namespace kafka

@@ -688,6 +688,7 @@ std::vector<Fetched> Consumer::poll() {
   bool stale = false;
   for (auto& s : sent) {
     Fetched f;
+    f.crc_checked = cfg_.check_crcs;
     f.buf = cluster_.node(s.first).recv(s.second, &f.size, alloc_);
     Reader r(f.buf.get(), f.size);
     const FetchResponse m = decode_fetch_response(r);
@@ -705,7 +706,7 @@ std::vector<Fetched> Consumer::poll() {
         if (p.records_len <= 0) continue;
         const size_t before = f.records.size();
         decode_records(f.buf.get(), p.records_off, (size_t)p.records_len, pos_[p.index],
-                       cfg_.check_crcs, f.records);
+                       cfg_.check_crcs, f.records, &f.batches);
         for (size_t i = before; i < f.records.size(); ++i) f.records[i].partition = p.index;
         if (f.records.size() > before) pos_[p.index] = f.records.back().offset + 1;
       }

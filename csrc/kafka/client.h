@@ -190,6 +190,8 @@ struct Fetched {
   std::shared_ptr<uint8_t> buf;
   size_t size = 0;
   std::vector<RecordRef> records;
+  std::vector<BatchSpan> batches;  // record batches (for deferred CRC checks)
+  bool crc_checked = false;
 };
 
 class Consumer {

@@ -6,27 +6,114 @@
 namespace gale {
 namespace kafka {
 
+namespace {
+
+// CRC32C with three independent crc32q streams (the instruction has 3-cycle latency and 1-cycle
+// throughput, so one serial chain runs at a third of the unit's rate). The partial CRCs are
+// combined with precomputed "append N zero bytes" operators in GF(2) (Mark Adler's crc32c
+// method): crc(A|B) = shift(crc(A), |B|) ^ crc(B).
+constexpr uint32_t kPoly = 0x82f63b78u;
+constexpr size_t kLong = 8192, kShort = 256;
+
+uint32_t gf2_times(const uint32_t* mat, uint32_t vec) {
+  uint32_t sum = 0;
+  while (vec) {
+    if (vec & 1) sum ^= *mat;
+    vec >>= 1;
+    ++mat;
+  }
+  return sum;
+}
+
+void gf2_square(uint32_t* square, const uint32_t* mat) {
+  for (int n = 0; n < 32; ++n) square[n] = gf2_times(mat, mat[n]);
+}
+
+// operator for appending len (a power of two) zero bytes
+void zeros_op(uint32_t* even, size_t len) {
+  uint32_t odd[32];
+  odd[0] = kPoly;
+  uint32_t row = 1;
+  for (int n = 1; n < 32; ++n) {
+    odd[n] = row;
+    row <<= 1;
+  }
+  gf2_square(even, odd);  // 2 zero bits
+  gf2_square(odd, even);  // 4 zero bits
+  do {
+    gf2_square(even, odd);
+    len >>= 1;
+    if (len == 0) return;
+    gf2_square(odd, even);
+    len >>= 1;
+  } while (len);
+  for (int n = 0; n < 32; ++n) even[n] = odd[n];
+}
+
+struct ShiftTable {
+  uint32_t t[4][256];
+  explicit ShiftTable(size_t len) {
+    uint32_t op[32];
+    zeros_op(op, len);
+    for (uint32_t n = 0; n < 256; ++n) {
+      t[0][n] = gf2_times(op, n);
+      t[1][n] = gf2_times(op, n << 8);
+      t[2][n] = gf2_times(op, n << 16);
+      t[3][n] = gf2_times(op, n << 24);
+    }
+  }
+  uint32_t shift(uint32_t crc) const {
+    return t[0][crc & 0xff] ^ t[1][(crc >> 8) & 0xff] ^ t[2][(crc >> 16) & 0xff] ^ t[3][crc >> 24];
+  }
+};
+
+const ShiftTable& long_table() {
+  static const ShiftTable t(kLong);
+  return t;
+}
+const ShiftTable& short_table() {
+  static const ShiftTable t(kShort);
+  return t;
+}
+
+inline uint64_t ld64(const uint8_t* p) {
+  uint64_t v;
+  memcpy(&v, p, 8);
+  return v;
+}
+
+// three streams over consecutive blocks of `blk` bytes, combined with `tab`
+inline const uint8_t* crc3(const uint8_t* p, size_t& n, uint64_t& c0, size_t blk,
+                           const ShiftTable& tab) {
+  while (n >= 3 * blk) {
+    uint64_t c1 = 0, c2 = 0;
+    const uint8_t* end = p + blk;
+    do {
+      c0 = _mm_crc32_u64(c0, ld64(p));
+      c1 = _mm_crc32_u64(c1, ld64(p + blk));
+      c2 = _mm_crc32_u64(c2, ld64(p + 2 * blk));
+      p += 8;
+    } while (p < end);
+    c0 = tab.shift((uint32_t)c0) ^ (uint32_t)c1;
+    c0 = tab.shift((uint32_t)c0) ^ (uint32_t)c2;
+    p += 2 * blk;
+    n -= 3 * blk;
+  }
+  return p;
+}
+
+}  // namespace
+
 uint32_t crc32c(const uint8_t* p, size_t n, uint32_t crc) {
-  uint64_t c = ~crc;
-  // serial crc32q chain (~8 GB/s per core); batches are validated once per fetch/produce
+  uint64_t c = ~crc & 0xffffffffu;
   while (n && ((uintptr_t)p & 7)) {
     c = _mm_crc32_u8((uint32_t)c, *p++);
     --n;
   }
-  while (n >= 32) {
-    uint64_t a, b, d, e;
-    memcpy(&a, p, 8); memcpy(&b, p + 8, 8); memcpy(&d, p + 16, 8); memcpy(&e, p + 24, 8);
-    c = _mm_crc32_u64(c, a);
-    c = _mm_crc32_u64(c, b);
-    c = _mm_crc32_u64(c, d);
-    c = _mm_crc32_u64(c, e);
-    p += 32;
-    n -= 32;
-  }
+  p = crc3(p, n, c, kLong, long_table());
+  p = crc3(p, n, c, kShort, short_table());
   while (n >= 8) {
-    uint64_t a;
-    memcpy(&a, p, 8);
-    c = _mm_crc32_u64(c, a);
+    c = _mm_crc32_u64(c, ld64(p));
     p += 8;
     n -= 8;
   }
@@ -140,7 +227,8 @@ BatchInfo peek_batch(const uint8_t* p, size_t avail, bool check_crc) {
 }
 
 size_t decode_records(const uint8_t* base, size_t off, size_t len, int64_t min_offset,
-                      bool check_crc, std::vector<RecordRef>& out) {
+                      bool check_crc, std::vector<RecordRef>& out,
+                      std::vector<BatchSpan>* spans) {
   size_t added = 0;
   size_t pos = off;
   const size_t end = off + len;
@@ -152,6 +240,7 @@ size_t decode_records(const uint8_t* base, size_t off, size_t len, int64_t min_o
     const BatchInfo b = peek_batch(base + pos, end - pos, check_crc);
     if (b.attributes & 0x7) throw ProtocolError("compressed record batches are not supported");
     const bool control = (b.attributes & 0x20) != 0;
+    const size_t first = out.size();
     if (!control) {
       Reader r(base + pos + kBatchHeaderBytes, (size_t)b.length - kBatchHeaderBytes);
       const size_t rbase = pos + kBatchHeaderBytes;
@@ -182,6 +271,7 @@ size_t decode_records(const uint8_t* base, size_t off, size_t len, int64_t min_o
         }
       }
     }
+    if (spans && out.size() > first) spans->push_back({pos, (size_t)b.length, first, out.size() - first});
     pos += (size_t)b.length;
   }
   return added;

@@ -210,8 +210,15 @@ BatchInfo peek_batch(const uint8_t* p, size_t avail, bool check_crc);
 // Decode every record of a records blob [base+off, base+off+len) (a Fetch response's records
 // field). Records with offset < min_offset are skipped (a fetch may start mid-batch). A trailing
 // partial batch (allowed by the protocol) is ignored. Returns the number of records appended.
+// A record batch inside a decoded buffer and the records it contributed to `out`
+// (lets a caller defer CRC validation to other threads).
+struct BatchSpan {
+  size_t off = 0, len = 0;
+  size_t first_rec = 0, nrec = 0;
+};
 size_t decode_records(const uint8_t* base, size_t off, size_t len, int64_t min_offset,
-                      bool check_crc, std::vector<RecordRef>& out);
+                      bool check_crc, std::vector<RecordRef>& out,
+                      std::vector<BatchSpan>* spans = nullptr);
 
 std::vector<Header> decode_headers(const uint8_t* base, const RecordRef& r);
 

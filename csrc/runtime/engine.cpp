@@ -189,10 +189,18 @@ void Engine::start() {
   const int ns = std::min<int>(cfg_.source_parallelism, (int)parts.size());
   std::vector<std::vector<int>> split((size_t)ns);
   for (size_t i = 0; i < parts.size(); ++i) split[i % (size_t)ns].push_back(parts[i]);
+  bool any_gpu = false;
+  for (auto& rs : replicas_) any_gpu |= rs->rep->device() >= 0;
+  if (any_gpu && cfg_.pinned_fetch_bytes > 0 && !pinned_)
+    pinned_ = std::make_shared<PinnedPool>((size_t)cfg_.fetch_max_bytes + (1 << 20),
+                                           (size_t)cfg_.pinned_fetch_bytes);
   running_ = true;
   stopping_ = false;
   sources_done_ = false;
   sources_active_ = ns;
+  dec_closed_ = false;
+  for (int i = 0; i < cfg_.decode_threads; ++i)
+    decoders_.emplace_back([this, i] { decode_loop(i); });
   for (auto& rs : replicas_) workers_.emplace_back([this, rs] { worker_loop(rs.get()); });
   for (int i = 0; i < ns; ++i)
     sources_.emplace_back([this, i, p = split[(size_t)i]] { source_loop(i, p); });
@@ -203,10 +211,22 @@ void Engine::stop() {
   if (!running_) return;
   stopping_ = true;
   {
+    std::lock_guard<std::mutex> lk(dec_mu_);  // wake sources blocked on a full decode queue
+  }
+  dec_space_cv_.notify_all();
+  {
     // wait for the sources to stop fetching
     std::unique_lock<std::mutex> lk(done_mu_);
     done_cv_.wait_for(lk, std::chrono::seconds(30), [&] { return sources_active_ == 0; });
   }
+  {
+    std::lock_guard<std::mutex> lk(dec_mu_);
+    dec_closed_ = true;
+  }
+  dec_cv_.notify_all();
+  dec_space_cv_.notify_all();
+  for (auto& t : decoders_) t.join();
+  decoders_.clear();
   batcher_->close();
   for (size_t i = 0; i < workers_.size(); ++i) {
     if (replicas_[i]->alive) {
@@ -270,11 +290,20 @@ void Engine::source_loop(int idx, std::vector<int> parts) {
   cc.max_wait_ms = cfg_.fetch_max_wait_ms;
   cc.fetch_max_bytes = cfg_.fetch_max_bytes;
   cc.partition_max_bytes = cfg_.partition_max_bytes;
-  cc.check_crcs = cfg_.check_crcs;
+  // with decode workers the CRC32C check moves off this thread (decode_fetch)
+  cc.check_crcs = cfg_.check_crcs && cfg_.decode_threads <= 0;
   cc.auto_offset_reset = cfg_.start_offset == "earliest" ? "earliest" : "latest";
+  kafka::BufferAlloc alloc = kafka::heap_alloc;
+  if (pinned_) {
+    std::shared_ptr<PinnedPool> pool = pinned_;
+    alloc = [pool](size_t n) {
+      bool pinned = false;
+      return pool->alloc(n, &pinned);
+    };
+  }
   std::unique_ptr<kafka::Consumer> cons;
   try {
-    cons = std::make_unique<kafka::Consumer>(cc);
+    cons = std::make_unique<kafka::Consumer>(cc, alloc);
     cons->assign(cfg_.input_topic, parts);
     cons->seek_to(cfg_.start_offset);
     std::lock_guard<std::mutex> lk(pend_mu_);
@@ -285,65 +314,50 @@ void Engine::source_loop(int idx, std::vector<int> parts) {
   }
   int64_t last_commit = mono_ns();
   std::vector<InRecord> good;
-  kafka::Producer* prod = producer_for(idx);
   while (cons && !stopping_) {
     std::vector<kafka::Fetched> fs;
     try {
+      const int64_t t0 = mono_ns();
       fs = cons->poll();
+      ns_poll_ += mono_ns() - t0;
     } catch (const std::exception& e) {
       fprintf(stderr, "[gale source %d] fetch failed: %s\n", idx, e.what());
       std::this_thread::sleep_for(std::chrono::milliseconds(100));
       continue;
     }
     const int64_t now = mono_ns();
-    good.clear();
-    std::vector<InRecord> bad;
     {
+      // register before anything can complete, and before the commit position moves past them
       std::lock_guard<std::mutex> lk(pend_mu_);
       for (auto& f : fs)
         for (const kafka::RecordRef& rr : f.records) pending_[rr.partition][rr.offset] = 1;
       for (int p : parts) next_fetch_[p] = cons->position(p);
     }
-    for (auto& f : fs) {
-      for (const kafka::RecordRef& rr : f.records) {
-        InRecord r;
-        r.buf = f.buf;
-        r.value = rr.value_len >= 0 ? f.buf.get() + rr.value_off : nullptr;
-        r.len = rr.value_len;
-        r.partition = rr.partition;
-        r.offset = rr.offset;
-        r.timestamp_ms = rr.timestamp;
-        r.t_fetch_ns = now;
-        r.source = idx;
-        ++records_in_;
-        if (r.len < 0) {
-          r.status = codec::BAD_ENVELOPE;  // null value (Jackson would throw)
-        } else {
-          bytes_in_ += r.len;
-          const codec::Scan s = codec::scan_instances(r.value, (size_t)r.len, cfg_.H, cfg_.W, cfg_.C);
-          r.status = s.status;
-          r.arr_off = s.arr_off;
-          r.arr_len = s.arr_len;
-          r.images = s.images;
-          if (r.status == codec::OK && r.images > cfg_.max_batch) r.status = codec::TOO_LARGE;
-          if (r.status == codec::OK && fault_hit(parse_error_p_)) r.status = codec::BAD_ENVELOPE;
-        }
-        if (r.status == codec::OK) {
-          images_in_ += r.images;
-          good.push_back(std::move(r));
-        } else {
-          bad.push_back(std::move(r));
-        }
-      }
-    }
     if (!fs.empty()) {
       int64_t z = 0;
       t_first_ns_.compare_exchange_strong(z, now);
     }
-    for (InRecord& r : bad) emit_error(r, r.status, prod);
-    // when stopping with a full queue the rest stays pending (never committed, so a restart
-    // with start_offset=committed re-reads it)
-    if (!good.empty()) batcher_->push_many(good, stopping_);
+    for (auto& f : fs) {
+      FetchItem it;
+      it.pinned = pinned_ && pinned_->owns(f.buf.get());
+      it.f = std::move(f);
+      it.source = idx;
+      it.t_fetch_ns = now;
+      if (cfg_.decode_threads <= 0) {
+        good.clear();
+        decode_fetch(it, good);
+        // when stopping with a full queue the rest stays pending (never committed, so a
+        // restart with start_offset=committed re-reads it)
+        if (!good.empty()) batcher_->push_many(good, stopping_);
+      } else {
+        std::unique_lock<std::mutex> lk(dec_mu_);
+        dec_space_cv_.wait(lk, [&] { return dec_q_.size() < (size_t)(4 * cfg_.decode_threads) ||
+                                            stopping_; });
+        if (stopping_) break;
+        dec_q_.push_back(std::move(it));
+        dec_cv_.notify_one();
+      }
+    }
     if (mono_ns() - last_commit > (int64_t)cfg_.commit_interval_ms * 1000000) {
       commit(*cons, parts);
       last_commit = mono_ns();
@@ -359,6 +373,81 @@ void Engine::source_loop(int idx, std::vector<int> parts) {
     done_cv_.wait_for(lk, std::chrono::seconds(60), [&] { return sources_done_.load(); });
     lk.unlock();
     commit(*cons, parts);
+  }
+}
+
+void Engine::decode_loop(int idx) {
+  (void)idx;
+  std::vector<InRecord> good;
+  for (;;) {
+    FetchItem it;
+    {
+      std::unique_lock<std::mutex> lk(dec_mu_);
+      dec_cv_.wait(lk, [&] { return !dec_q_.empty() || dec_closed_; });
+      if (dec_q_.empty()) return;
+      it = std::move(dec_q_.front());
+      dec_q_.pop_front();
+      dec_space_cv_.notify_one();
+    }
+    good.clear();
+    const int64_t t0 = mono_ns();
+    decode_fetch(it, good);
+    ns_decode_ += mono_ns() - t0;
+    if (!good.empty()) batcher_->push_many(good, stopping_);
+  }
+}
+
+// CRC32C of every record batch (unless the consumer checked it), then the envelope scan of
+// every record; malformed records go straight to the error policy.
+void Engine::decode_fetch(FetchItem& it, std::vector<InRecord>& good) {
+  kafka::Fetched& f = it.f;
+  std::vector<char> corrupt;
+  if (cfg_.check_crcs && !f.crc_checked) {
+    corrupt.assign(f.records.size(), 0);
+    for (const kafka::BatchSpan& b : f.batches) {
+      const uint8_t* p = f.buf.get() + b.off;
+      uint32_t want;
+      kafka::Reader r(p + kafka::kBatchCrcOffset, 4);
+      want = r.u32();
+      const uint32_t got = kafka::crc32c(p + kafka::kBatchAttrOffset, b.len - kafka::kBatchAttrOffset);
+      if (got != want)
+        for (size_t i = 0; i < b.nrec; ++i) corrupt[b.first_rec + i] = 1;
+    }
+  }
+  kafka::Producer* prod = producer_for(it.source);
+  for (size_t i = 0; i < f.records.size(); ++i) {
+    const kafka::RecordRef& rr = f.records[i];
+    InRecord r;
+    r.buf = f.buf;
+    r.pinned = it.pinned;
+    r.value = rr.value_len >= 0 ? f.buf.get() + rr.value_off : nullptr;
+    r.len = rr.value_len;
+    r.partition = rr.partition;
+    r.offset = rr.offset;
+    r.timestamp_ms = rr.timestamp;
+    r.t_fetch_ns = it.t_fetch_ns;
+    r.source = it.source;
+    ++records_in_;
+    if (!corrupt.empty() && corrupt[i]) {
+      r.status = codec::BAD_ENVELOPE;  // corrupt Kafka batch (CRC32C mismatch)
+    } else if (r.len < 0) {
+      r.status = codec::BAD_ENVELOPE;  // null value (Jackson would throw)
+    } else {
+      bytes_in_ += r.len;
+      const codec::Scan s = codec::scan_instances(r.value, (size_t)r.len, cfg_.H, cfg_.W, cfg_.C);
+      r.status = s.status;
+      r.arr_off = s.arr_off;
+      r.arr_len = s.arr_len;
+      r.images = s.images;
+      if (r.status == codec::OK && r.images > cfg_.max_batch) r.status = codec::TOO_LARGE;
+      if (r.status == codec::OK && fault_hit(parse_error_p_)) r.status = codec::BAD_ENVELOPE;
+    }
+    if (r.status == codec::OK) {
+      images_in_ += r.images;
+      good.push_back(std::move(r));
+    } else {
+      emit_error(r, r.status, prod);
+    }
   }
 }
 
@@ -392,7 +481,10 @@ void Engine::worker_loop(ReplicaSlot* rs) {
     if (mine.size() < depth) {
       auto b = std::make_shared<Batch>();
       int images = 0;
-      if (!batcher_->take(cfg_.max_batch, max_wait_ns, !mine.empty(), b->recs, images)) {
+      const int64_t t_take0 = mono_ns();
+      const bool open = batcher_->take(cfg_.max_batch, max_wait_ns, !mine.empty(), b->recs, images);
+      ns_take_ += mono_ns() - t_take0;
+      if (!open) {
         if (mine.empty()) break;  // closed and drained
       } else if (!b->recs.empty()) {
         b->images = images;
@@ -409,6 +501,7 @@ void Engine::worker_loop(ReplicaSlot* rs) {
                                      std::to_string(crash_at_batch_) + ")");
           b->t_submit_ns = mono_ns();
           rep.submit(*b);
+          ns_submit_ += mono_ns() - b->t_submit_ns;
         } catch (const std::exception& e) {
           fail("submit", e.what());
           break;
@@ -419,6 +512,7 @@ void Engine::worker_loop(ReplicaSlot* rs) {
     }
     if (mine.empty()) continue;
     std::shared_ptr<Batch> f = mine.front();
+    const int64_t t_wait0 = mono_ns();
     try {
       rep.wait(*f);
     } catch (const std::exception& e) {
@@ -426,6 +520,7 @@ void Engine::worker_loop(ReplicaSlot* rs) {
       break;
     }
     f->t_done_ns = mono_ns();
+    ns_wait_ += f->t_done_ns - t_wait0;
     {
       std::lock_guard<std::mutex> lk(rs->mu);
       if (!rs->alive) break;  // the watchdog re-queued it already
@@ -433,6 +528,7 @@ void Engine::worker_loop(ReplicaSlot* rs) {
     }
     mine.pop_front();
     finish_batch(rs, *f);
+    ns_finish_ += mono_ns() - f->t_done_ns;
   }
 }
 
@@ -601,6 +697,12 @@ std::map<std::string, double> Engine::stats() const {
   int alive = 0;
   for (auto& r : replicas_) alive += r->alive ? 1 : 0;
   s["replicas_alive"] = alive;
+  s["thread_s_poll"] = ns_poll_ * 1e-9;
+  s["thread_s_decode"] = ns_decode_ * 1e-9;
+  s["thread_s_take"] = ns_take_ * 1e-9;
+  s["thread_s_submit"] = ns_submit_ * 1e-9;
+  s["thread_s_wait"] = ns_wait_ * 1e-9;
+  s["thread_s_finish"] = ns_finish_ * 1e-9;
   return s;
 }
 
@@ -627,6 +729,7 @@ void Engine::reset_stats() {
   h_batch_images_.reset();
   images_out_ = 0;
   records_out_ = 0;
+  ns_poll_ = ns_decode_ = ns_take_ = ns_submit_ = ns_wait_ = ns_finish_ = 0;
   t_first_ns_ = mono_ns();
   t_last_ns_ = t_first_ns_.load();
 }

@@ -37,6 +37,7 @@
 
 #include "../kafka/client.h"
 #include "metrics.h"
+#include "pinned_pool.h"
 #include "replica.h"
 
 namespace gale {
@@ -51,9 +52,11 @@ struct EngineConfig {
   int source_parallelism = 2;      // KAFKA_SPOUT_PARAL (MainTopology.java:26)
   std::string start_offset = "latest";  // latest | earliest | committed
   int fetch_max_wait_ms = 20;
-  int fetch_max_bytes = 64 << 20;
-  int partition_max_bytes = 16 << 20;
+  int fetch_max_bytes = 16 << 20;
+  int partition_max_bytes = 8 << 20;
   bool check_crcs = true;
+  int decode_threads = 2;          // CRC32C + envelope scan workers (0 = on the source thread)
+  int64_t pinned_fetch_bytes = 4ll << 30;  // pinned fetch-buffer budget (GPU replicas only)
   int commit_interval_ms = 2000;   // storm-kafka's ZK commit period
   // sink (R5, R9, E7-E9)
   int sink_parallelism = 2;        // KAFKA_BOLT_PARAL (MainTopology.java:28)
@@ -109,11 +112,18 @@ class Engine {
   const EngineConfig& config() const { return cfg_; }
 
  private:
-  struct Pending;    // per-partition outstanding offsets
   struct ReplicaSlot;
   class Batcher;
+  struct FetchItem {
+    kafka::Fetched f;
+    int source = 0;
+    int64_t t_fetch_ns = 0;
+    bool pinned = false;
+  };
 
   void source_loop(int idx, std::vector<int> parts);
+  void decode_loop(int idx);
+  void decode_fetch(FetchItem& it, std::vector<InRecord>& good);
   void worker_loop(ReplicaSlot* rs);
   void watchdog_loop();
   void finish_batch(ReplicaSlot* rs, Batch& b);
@@ -128,7 +138,12 @@ class Engine {
   std::vector<std::shared_ptr<ReplicaSlot>> replicas_;
   std::unique_ptr<Batcher> batcher_;
   std::vector<std::unique_ptr<kafka::Producer>> producers_;
-  std::vector<std::thread> sources_, workers_;
+  std::vector<std::thread> sources_, workers_, decoders_;
+  std::shared_ptr<PinnedPool> pinned_;
+  std::mutex dec_mu_;
+  std::condition_variable dec_cv_, dec_space_cv_;
+  std::deque<FetchItem> dec_q_;
+  bool dec_closed_ = false;
   std::thread watchdog_;
   std::atomic<bool> running_{false}, stopping_{false}, sources_done_{false};
   std::atomic<int> sources_active_{0};
@@ -154,6 +169,9 @@ class Engine {
   std::atomic<int64_t> requeued_{0}, replica_failures_{0}, commits_{0};
   std::atomic<int64_t> err_by_status_[8] = {};
   Histogram h_queue_us_, h_device_us_, h_engine_e2e_us_, h_record_e2e_ms_, h_batch_images_;
+  // thread time per pipeline stage (summed over threads): where the host spends its cycles
+  std::atomic<int64_t> ns_poll_{0}, ns_decode_{0}, ns_take_{0}, ns_submit_{0}, ns_wait_{0},
+      ns_finish_{0};
   std::atomic<int64_t> t_first_ns_{0}, t_last_ns_{0};
 };
 

@@ -1,0 +1,75 @@
+// Pinned fetch-buffer pool (see pinned_pool.h).
+#include "pinned_pool.h"
+
+#include <hip/hip_runtime.h>
+
+#include "../kafka/client.h"
+
+namespace gale {
+
+struct PinnedPool::State {
+  std::mutex mu;
+  std::vector<uint8_t*> free;
+  std::vector<uint8_t*> all;
+  size_t chunk = 0, max_bytes = 0;
+  bool closed = false;
+  ~State() {
+    for (uint8_t* p : all) hipHostFree(p);
+  }
+};
+
+PinnedPool::PinnedPool(size_t chunk_bytes, size_t max_bytes)
+    : st_(std::make_shared<State>()), chunk_(chunk_bytes) {
+  st_->chunk = chunk_bytes;
+  st_->max_bytes = max_bytes;
+}
+
+PinnedPool::~PinnedPool() {
+  std::lock_guard<std::mutex> lk(st_->mu);
+  st_->closed = true;  // outstanding buffers keep State alive and are freed with it
+}
+
+size_t PinnedPool::pinned_bytes() const {
+  std::lock_guard<std::mutex> lk(st_->mu);
+  return st_->all.size() * st_->chunk;
+}
+
+bool PinnedPool::owns(const uint8_t* p) const {
+  std::lock_guard<std::mutex> lk(st_->mu);
+  for (const uint8_t* q : st_->all)
+    if (q == p) return true;
+  return false;
+}
+
+std::shared_ptr<uint8_t> PinnedPool::alloc(size_t n, bool* pinned) {
+  if (n + 64 <= chunk_) {
+    uint8_t* p = nullptr;
+    {
+      std::lock_guard<std::mutex> lk(st_->mu);
+      if (!st_->free.empty()) {
+        p = st_->free.back();
+        st_->free.pop_back();
+      } else if ((st_->all.size() + 1) * st_->chunk <= st_->max_bytes) {
+        // portable: usable as a DMA source by every GPU of the process
+        if (hipHostMalloc(reinterpret_cast<void**>(&p), st_->chunk, hipHostMallocPortable) ==
+            hipSuccess) {
+          st_->all.push_back(p);
+        } else {
+          p = nullptr;
+        }
+      }
+    }
+    if (p) {
+      *pinned = true;
+      std::shared_ptr<State> st = st_;
+      return std::shared_ptr<uint8_t>(p, [st](uint8_t* q) {
+        std::lock_guard<std::mutex> lk(st->mu);
+        st->free.push_back(q);
+      });
+    }
+  }
+  *pinned = false;
+  return kafka::heap_alloc(n);
+}
+
+}  // namespace gale

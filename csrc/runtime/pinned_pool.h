@@ -1,0 +1,38 @@
+// Pool of pinned (page-locked) host buffers for Kafka fetch responses.
+//
+// The engine's consumers receive Fetch response bodies straight into these buffers, so the
+// GPU replica can DMA the JSON text of a micro-batch to the device with hipMemcpyAsync without
+// first copying it into a staging buffer (the reference copies every tuple's float arrays into a
+// fresh native Tensor instead, InferenceBolt.java:80). Buffers are recycled through the pool
+// when the last record referencing them is released; requests larger than a chunk or beyond the
+// pool's byte budget fall back to ordinary heap memory (the replica then stages them).
+#pragma once
+#include <stddef.h>
+#include <stdint.h>
+
+#include <memory>
+#include <mutex>
+#include <vector>
+
+namespace gale {
+
+class PinnedPool {
+ public:
+  PinnedPool(size_t chunk_bytes, size_t max_bytes);
+  ~PinnedPool();
+  PinnedPool(const PinnedPool&) = delete;
+  PinnedPool& operator=(const PinnedPool&) = delete;
+
+  // A buffer of at least n bytes (+64 slack). *pinned tells whether it is page-locked.
+  std::shared_ptr<uint8_t> alloc(size_t n, bool* pinned);
+  size_t chunk_bytes() const { return chunk_; }
+  bool owns(const uint8_t* p) const;  // p is the base of one of this pool's pinned chunks
+  size_t pinned_bytes() const;
+
+ private:
+  struct State;
+  std::shared_ptr<State> st_;
+  size_t chunk_;
+};
+
+}  // namespace gale

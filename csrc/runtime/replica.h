@@ -31,6 +31,7 @@ struct InRecord {
   int32_t images = 0;
   int32_t status = 0;            // codec::Status (scan, then device parse)
   int32_t source = 0;
+  bool pinned = false;           // buf is page-locked: the GPU replica DMAs straight from it
 };
 
 struct Batch {
@@ -58,7 +59,7 @@ class Replica {
 // followed by softmax. An optional per-batch delay emulates device time.
 class StubReplica : public Replica {
  public:
-  StubReplica(int H, int W, int C, int classes, int max_images, int delay_us);
+  StubReplica(int H, int W, int C, int classes, int max_images, int delay_us, bool compute = true);
   std::string name() const override { return "stub"; }
   int max_images() const override { return max_images_; }
   int depth() const override { return 1; }
@@ -67,6 +68,7 @@ class StubReplica : public Replica {
 
  private:
   int H_, W_, C_, classes_, max_images_, delay_us_;
+  bool compute_;  // false: a "null" replica (uniform softmax, no parsing) to measure host paths
   std::vector<float> x_, probs_;
 };
 
@@ -86,19 +88,22 @@ class GpuReplica : public Replica {
 
  private:
   struct Slot {
-    uint8_t* h_bytes = nullptr;  // pinned staging of the JSON text
-    uint8_t* d_bytes = nullptr;
-    size_t cap = 0;
+    uint8_t* h_bytes = nullptr;  // pinned staging for records that arrived in pageable memory
+    uint8_t* d_bytes = nullptr;  // device copy of the batch's JSON text
+    size_t h_cap = 0, d_cap = 0;
     JsonRecord* h_recs = nullptr;
     JsonRecord* d_recs = nullptr;
     float* h_out = nullptr;      // pinned softmax rows
     hipEvent_t done = nullptr;
+    hipEvent_t staged = nullptr;  // H2D of this slot's text finished (copy stream)
   };
-  void ensure_capacity(Slot& s, size_t bytes);
+  void ensure_host(Slot& s, size_t bytes);
+  void ensure_device(Slot& s, size_t bytes);
   std::shared_ptr<Executor> exec_;
   int H_, W_, C_, classes_;
   bool use_graph_;
-  hipStream_t stream_ = nullptr;
+  hipStream_t stream_ = nullptr;       // parse + forward + D2H
+  hipStream_t copy_stream_ = nullptr;  // H2D of batch k+1 overlaps compute of batch k
   std::vector<Slot> slots_;
   int next_slot_ = 0;
 };

@@ -41,6 +41,8 @@ class GaleConfig:
     partitions: str = ""               # comma-separated input partitions (empty = all)
     start_offset: str = "latest"       # reference: LatestTime + ignoreZkOffsets (:101-102)
     commit_interval_ms: int = 2000
+    decode_threads: int = 2            # CRC32C + envelope-scan workers behind each consumer
+    check_crcs: bool = True            # Kafka consumer check.crcs
     # parallelism (R3)
     workers: int = 8                   # NUM_WORKERS: placement only (one process per GPU here)
     source_parallelism: int = 2        # KAFKA_SPOUT_PARAL
@@ -66,6 +68,7 @@ class GaleConfig:
     queue_depth: int = 8192
     use_graph: bool = True
     stub: bool = False                 # CPU stub replicas (plumbing without a GPU)
+    stub_null: bool = False            # stub replicas skip parsing/compute (host-path benchmark)
     # robustness / observability
     watchdog_ms: int = 30000
     fault: str = ""                    # replica_crash@N,parse_error@P,producer_fail@P
@@ -103,6 +106,7 @@ class GaleConfig:
             partitions=[int(p) for p in self.partitions.split(",") if p.strip()],
             source_parallelism=self.source_parallelism, start_offset=self.start_offset,
             commit_interval_ms=self.commit_interval_ms, sink_parallelism=self.sink_parallelism,
+            decode_threads=self.decode_threads, check_crcs=self.check_crcs,
             acks=self.acks, sink_mode=self.sink_mode, linger_ms=self.linger_ms,
             value_format=self.value_format, type_id_header=self.type_id_header,
             on_error=self.on_error, H=H, W=W, C=C, classes=classes, max_batch=self.max_batch,

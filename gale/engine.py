@@ -43,7 +43,7 @@ class Engine:
         self.devices: List[int] = []
         if cfg.stub:
             for _ in range(max(1, cfg.replicas)):
-                self._native.add_stub_replica(cfg.max_batch, 0)
+                self._native.add_stub_replica(cfg.max_batch, 0, not cfg.stub_null)
             return
         if model_replicas is not None:
             reps = list(model_replicas)
@@ -82,7 +82,7 @@ class Engine:
                 else:  # same process: device-to-device copy over xGMI
                     packed[dev] = next(iter(packed.values())).to(torch.device("cuda", dev))
             reps.append(ModelReplica(self.net, packed[dev], max_batch=self.cfg.max_batch,
-                                     slots=2, wdtype=wdtype))
+                                     slots=3, wdtype=wdtype))
         for r in reps:
             r.capture()
         return reps
