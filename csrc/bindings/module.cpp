@@ -118,13 +118,16 @@ PYBIND11_MODULE(_C, m) {
               "cast_f32_bf16");
         });
   m.def("json_parse_instances",
-        [](int nrec, uintptr_t recs, uintptr_t bytes, int H, int W, int C, uintptr_t out,
-           uintptr_t stream) {
-          chk(gale::json_parse_instances(nrec, static_cast<const gale::JsonRecord*>(P(recs)),
+        [](int nrec, int ntiles, uintptr_t recs, uintptr_t bytes, int H, int W, int C,
+           uintptr_t tile_counts, uintptr_t out, uintptr_t stream) {
+          chk(gale::json_parse_instances(nrec, ntiles, static_cast<gale::JsonRecord*>(P(recs)),
                                          static_cast<const uint8_t*>(P(bytes)), H, W, C,
+                                         static_cast<int*>(P(tile_counts)),
                                          static_cast<float*>(P(out)), S(stream)),
               "json_parse_instances");
         });
+  m.def("json_tile_count", &gale::json_tile_count);
+  m.attr("JSON_TILE_BYTES") = gale::kJsonTileBytes;
   m.attr("JSON_RECORD_BYTES") = (int)sizeof(gale::JsonRecord);
   m.def("memcpy_async",
         [](uintptr_t dst, uintptr_t src, size_t n, uintptr_t stream) {

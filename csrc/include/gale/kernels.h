@@ -64,17 +64,24 @@ hipError_t quant_f32_e4m3(int64_t n, const float* x, const float* row_scale, int
 
 // GPU decoder for the InstObj JSON contract: parses every number of each record's instances
 // array into the fp32 NHWC batch tensor and validates the rectangular [N][H][W][C] structure.
-// recs: [nrec] {byte offset (16-aligned), length, first image slot, images}. The kernel writes
-// each record's status: 0 ok, 1 number-count mismatch, 2 malformed number / element, 3 bad
-// structure (ragged / wrong rank).
+// Work is split into kJsonTileBytes tiles of record text (one workgroup each); record i owns the
+// global tiles [tile0, tile0 + json_tile_count(off, len)), numbered consecutively over the batch.
+// The kernel raises each record's status (host zeroes it): 0 ok, 1 number-count mismatch,
+// 2 malformed number / element, 3 bad structure (ragged / wrong rank).
+constexpr int kJsonTileBytes = 4096;
 struct JsonRecord {
   int64_t off;      // byte offset of the instances array inside the staged byte buffer
   int32_t len;      // array length in bytes
   int32_t slot;     // first image slot of this record inside the batch
   int32_t images;   // images in this record (from the host '[' count)
-  int32_t status;   // written by the kernel
+  int32_t status;   // raised by the kernel
+  int32_t tile0;    // first global tile of this record
+  int32_t pad_;
 };
-hipError_t json_parse_instances(int nrec, const JsonRecord* recs, const uint8_t* bytes, int H,
-                                int W, int C, float* out, hipStream_t stream);
+int json_tile_count(int64_t off, int32_t len);
+// tile_counts: device scratch of >= ntiles ints.
+hipError_t json_parse_instances(int nrec, int ntiles, JsonRecord* recs, const uint8_t* bytes,
+                                int H, int W, int C, int* tile_counts, float* out,
+                                hipStream_t stream);
 
 }  // namespace gale

@@ -97,6 +97,7 @@ GpuReplica::GpuReplica(std::shared_ptr<Executor> exec, int H, int W, int C, int 
     check_hip(hipEventCreateWithFlags(&s.staged, hipEventDisableTiming), "hipEventCreate");
     // initial text capacity: ~12 bytes per number (Java Float.toString + ",") x a full batch
     ensure_device(s, (size_t)mb * H * W * C * 12 + 4096);
+    ensure_tiles(s, (int)(((size_t)mb * H * W * C * 12) / kJsonTileBytes) + 2 * mb);
   }
 }
 
@@ -108,6 +109,7 @@ GpuReplica::~GpuReplica() {
     if (s.d_bytes) hipFree(s.d_bytes);
     if (s.h_recs) hipHostFree(s.h_recs);
     if (s.d_recs) hipFree(s.d_recs);
+    if (s.d_tiles) hipFree(s.d_tiles);
     if (s.h_out) hipHostFree(s.h_out);
     if (s.done) hipEventDestroy(s.done);
     if (s.staged) hipEventDestroy(s.staged);
@@ -130,6 +132,18 @@ void GpuReplica::ensure_host(Slot& s, size_t bytes) {
   }
   check_hip(hipHostMalloc(reinterpret_cast<void**>(&s.h_bytes), cap), "hipHostMalloc(bytes)");
   s.h_cap = cap;
+}
+
+void GpuReplica::ensure_tiles(Slot& s, int ntiles) {
+  if (ntiles <= s.tiles_cap) return;
+  const int cap = std::max(ntiles, s.tiles_cap * 2);
+  if (s.d_tiles) {
+    check_hip(hipEventSynchronize(s.done), "hipEventSynchronize");
+    hipFree(s.d_tiles);
+  }
+  check_hip(hipMalloc(reinterpret_cast<void**>(&s.d_tiles), sizeof(int) * cap),
+            "hipMalloc(tiles)");
+  s.tiles_cap = cap;
 }
 
 void GpuReplica::ensure_device(Slot& s, size_t bytes) {
@@ -195,7 +209,7 @@ void GpuReplica::submit(Batch& b) {
   }
   const size_t staged_dev = doff;
   size_t hoff = 0;
-  int nrec = 0, img = 0;
+  int nrec = 0, img = 0, ntiles = 0;
   for (const InRecord& r : b.recs) {
     JsonRecord& jr = s.h_recs[nrec++];
     const uint8_t* base = r.buf.get();
@@ -214,6 +228,9 @@ void GpuReplica::submit(Batch& b) {
     jr.slot = img;
     jr.images = r.images;
     jr.status = 0;
+    jr.tile0 = ntiles;
+    jr.pad_ = 0;
+    ntiles += json_tile_count(jr.off, jr.len);
     img += r.images;
   }
   if (img > exec_->max_batch()) throw std::logic_error("GpuReplica: batch exceeds max_batch");
@@ -227,7 +244,8 @@ void GpuReplica::submit(Batch& b) {
             "H2D recs");
   check_hip(hipEventRecord(s.staged, copy_stream_), "hipEventRecord(staged)");
   check_hip(hipStreamWaitEvent(stream_, s.staged, 0), "hipStreamWaitEvent");
-  check_hip(json_parse_instances(nrec, s.d_recs, s.d_bytes, H_, W_, C_,
+  ensure_tiles(s, ntiles);
+  check_hip(json_parse_instances(nrec, ntiles, s.d_recs, s.d_bytes, H_, W_, C_, s.d_tiles,
                                  static_cast<float*>(exec_->input(slot)), stream_),
             "json_parse_instances");
   exec_->run(slot, img, stream_, use_graph_);

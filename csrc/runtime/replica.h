@@ -93,12 +93,15 @@ class GpuReplica : public Replica {
     size_t h_cap = 0, d_cap = 0;
     JsonRecord* h_recs = nullptr;
     JsonRecord* d_recs = nullptr;
+    int* d_tiles = nullptr;      // per-tile token counts (parser scratch)
+    int tiles_cap = 0;
     float* h_out = nullptr;      // pinned softmax rows
     hipEvent_t done = nullptr;
     hipEvent_t staged = nullptr;  // H2D of this slot's text finished (copy stream)
   };
   void ensure_host(Slot& s, size_t bytes);
   void ensure_device(Slot& s, size_t bytes);
+  void ensure_tiles(Slot& s, int ntiles);
   std::shared_ptr<Executor> exec_;
   int H_, W_, C_, classes_;
   bool use_graph_;

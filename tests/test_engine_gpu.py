@@ -18,29 +18,33 @@ pytestmark = pytest.mark.gpu
 C = native()
 K = C.kafka
 REC = np.dtype([("off", "<i8"), ("len", "<i4"), ("slot", "<i4"), ("images", "<i4"),
-                ("status", "<i4")])
+                ("status", "<i4"), ("tile0", "<i4"), ("pad", "<i4")])
+assert REC.itemsize == C.JSON_RECORD_BYTES
 
 
 def stage(arrays):
     """Pack JSON array texts 16-byte aligned (+16 slack) and their JsonRecord table."""
     buf = bytearray()
     recs = np.zeros(len(arrays), dtype=REC)
-    slot = 0
+    slot = tiles = 0
     for i, (txt, images) in enumerate(arrays):
-        recs[i] = (len(buf), len(txt), slot, images, 0)
+        recs[i] = (len(buf), len(txt), slot, images, 0, tiles, 0)
+        tiles += C.json_tile_count(len(buf), len(txt))
         buf += txt + b" " * ((-len(txt)) % 16)
         slot += images
     buf += b" " * 16
-    return np.frombuffer(bytes(buf), dtype=np.uint8), recs, slot
+    return np.frombuffer(bytes(buf), dtype=np.uint8), recs, slot, tiles
 
 
 def gpu_parse(arrays, H, Wd, Cc):
-    raw, recs, total = stage(arrays)
+    raw, recs, total, tiles = stage(arrays)
     d_raw = torch.from_numpy(raw.copy()).cuda()
     d_recs = torch.from_numpy(recs.view(np.uint8).copy()).cuda()
+    d_tiles = torch.zeros(max(tiles, 1), dtype=torch.int32, device="cuda")
     out = torch.full((max(total, 1), H, Wd, Cc), -7.0, device="cuda")
-    C.json_parse_instances(len(arrays), d_recs.data_ptr(), d_raw.data_ptr(), H, Wd, Cc,
-                           out.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    C.json_parse_instances(len(arrays), tiles, d_recs.data_ptr(), d_raw.data_ptr(), H, Wd, Cc,
+                           d_tiles.data_ptr(), out.data_ptr(),
+                           torch.cuda.current_stream().cuda_stream)
     torch.cuda.synchronize()
     st = d_recs.cpu().numpy().view(REC)["status"]
     return out.cpu().numpy(), st
@@ -70,6 +74,45 @@ def test_gpu_json_parse_matches_host():
     assert list(st) == [0, 0, 0, 0]
     ref = np.concatenate(xs)
     np.testing.assert_allclose(out, ref, rtol=1e-6, atol=0)
+
+
+def test_gpu_json_parse_multi_tile():
+    """CIFAR-sized records span many 4 KiB tiles: token indices carry across tiles, tokens
+    straddle tile edges, and a whitespace run longer than the LDS halo falls back to global."""
+    rng = np.random.default_rng(1)
+    H, Wd, Cc = 32, 32, 3
+    recs, xs = [], []
+    for n in (1, 2, 1):
+        x = (rng.standard_normal((n, H, Wd, Cc)) * 10.0 ** rng.integers(-6, 6, (n, H, Wd, Cc))
+             ).astype(np.float32)
+        xs.append(x)
+        recs.append(array_text(C.encode_instances(x), H, Wd, Cc))
+    x = rng.random((1, H, Wd, Cc)).astype(np.float32)
+    xs.append(x)
+    recs.append(array_text(json.dumps({"instances": x.astype(np.float64).tolist()},
+                                      indent=2).encode(), H, Wd, Cc))
+    x = rng.random((1, H, Wd, Cc)).astype(np.float32)
+    xs.append(x)
+    txt, n = array_text(C.encode_instances(x), H, Wd, Cc)
+    cut = txt.index(b",", 9000)
+    recs.append((txt[:cut] + b" " * 300 + txt[cut:cut + 1] + b"\n" * 200 + txt[cut + 1:], n))
+    out, st = gpu_parse(recs, H, Wd, Cc)
+    assert list(st) == [0] * len(recs)
+    np.testing.assert_allclose(out, np.concatenate(xs), rtol=1e-6, atol=0)
+
+
+def test_gpu_json_parse_multi_tile_errors():
+    rng = np.random.default_rng(2)
+    H, Wd, Cc = 32, 32, 3
+    good, n = array_text(C.encode_instances(rng.random((1, H, Wd, Cc)).astype(np.float32)),
+                         H, Wd, Cc)
+    d = next(i for i in range(20000, len(good)) if good[i:i + 1].isdigit())
+    bad_char = good[:d] + b"x" + good[d + 1:]
+    k = good.index(b"],[", 30000)
+    ragged = good[:k] + b"," + good[k + 3:]                  # two pixels fused: wrong structure
+    short = good[:good.rindex(b",")] + b"]]]]"               # last number dropped
+    _, st = gpu_parse([(good, n), (bad_char, n), (ragged, n), (short, n), (good, n)], H, Wd, Cc)
+    assert list(st) == [0, 2, 3, 1, 0]
 
 
 @pytest.mark.parametrize("txt,status", [

@@ -1,0 +1,37 @@
+#!/usr/bin/env python3
+"""Summarise a rocprofv3 run_results.db (kernel + memory-copy stats) as CSV-ish text.
+
+usage: python tools/prof_summary.py gpurun_out/prof/run_results.db [--top 25]
+"""
+import argparse
+import sqlite3
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("db")
+    ap.add_argument("--top", type=int, default=25)
+    a = ap.parse_args()
+    c = sqlite3.connect(a.db)
+    rows = c.execute(
+        "select name, count(*), sum(end-start), avg(end-start), min(end-start), max(end-start) "
+        "from kernels group by name order by sum(end-start) desc").fetchall()
+    total = sum(r[2] for r in rows) or 1
+    print("kernel,calls,total_us,avg_us,min_us,max_us,pct")
+    for name, n, tot, avg, mn, mx in rows[:a.top]:
+        short = name if len(name) < 110 else name[:107] + "..."
+        print(f'"{short}",{n},{tot/1e3:.1f},{avg/1e3:.2f},{mn/1e3:.2f},{mx/1e3:.2f},'
+              f"{100*tot/total:.1f}")
+    try:
+        mc = c.execute("select src_agent_type||'->'||dst_agent_type, count(*), sum(end-start), "
+                       "sum(size) from memory_copies group by 1").fetchall()
+    except sqlite3.Error:
+        mc = []
+    if mc:
+        print("\ncopy,calls,total_us,bytes,GB_per_s")
+        for k, n, tot, sz in mc:
+            print(f"{k},{n},{tot/1e3:.1f},{sz},{(sz or 0)/max(tot,1):.2f}")
+
+
+if __name__ == "__main__":
+    main()
