@@ -48,7 +48,9 @@ ConvDesc desc_from_dict(const py::dict& d) {
   c.in_f32 = get_or<int>(d, "in_f32", 0);
   c.out_f32 = get_or<int>(d, "out_f32", 0);
   c.fp8 = get_or<int>(d, "fp8", 0);
-  c.act_scale = get_or<float>(d, "act_scale", 1.0f);
+  c.in_scale = get_or<float>(d, "in_scale", 1.0f);
+  c.out_scale = get_or<float>(d, "out_scale", 1.0f);
+  c.res_scale = get_or<float>(d, "res_scale", 1.0f);
   return c;
 }
 
@@ -71,6 +73,8 @@ gale::PlanOp op_from_dict(const py::dict& d) {
   op.w = P(get_or<uintptr_t>(d, "w", 0));
   op.bias = static_cast<const float*>(P(get_or<uintptr_t>(d, "bias", 0)));
   op.wscale = static_cast<const float*>(P(get_or<uintptr_t>(d, "wscale", 0)));
+  op.fp8 = get_or<int>(d, "fp8", 0);
+  op.scale = get_or<float>(d, "scale", 1.0f);
   return op;
 }
 
@@ -91,21 +95,31 @@ PYBIND11_MODULE(_C, m) {
         py::arg("wscale"), py::arg("res"), py::arg("y"), py::arg("stream"));
   m.def("maxpool2d",
         [](int batch, int H, int W, int C, int k, int s, int p, int Ho, int Wo, uintptr_t x,
-           uintptr_t y, uintptr_t stream) {
-          chk(gale::maxpool2d(batch, H, W, C, k, s, p, Ho, Wo, P(x), P(y), S(stream)), "maxpool2d");
-        });
-  m.def("avgpool_global", [](int batch, int HW, int C, uintptr_t x, uintptr_t y, uintptr_t stream) {
-    chk(gale::avgpool_global(batch, HW, C, P(x), P(y), S(stream)), "avgpool_global");
-  });
+           uintptr_t y, uintptr_t stream, int fp8) {
+          chk(gale::maxpool2d(batch, H, W, C, k, s, p, Ho, Wo, P(x), P(y), fp8, S(stream)),
+              "maxpool2d");
+        },
+        py::arg("batch"), py::arg("H"), py::arg("W"), py::arg("C"), py::arg("k"), py::arg("s"),
+        py::arg("p"), py::arg("Ho"), py::arg("Wo"), py::arg("x"), py::arg("y"), py::arg("stream"),
+        py::arg("fp8") = 0);
+  m.def("avgpool_global",
+        [](int batch, int HW, int C, uintptr_t x, uintptr_t y, uintptr_t stream, int fp8) {
+          chk(gale::avgpool_global(batch, HW, C, P(x), P(y), fp8, S(stream)), "avgpool_global");
+        },
+        py::arg("batch"), py::arg("HW"), py::arg("C"), py::arg("x"), py::arg("y"),
+        py::arg("stream"), py::arg("fp8") = 0);
   m.def("head_pool_dense_softmax",
         [](int batch, int HW, int C, int N, uintptr_t x, uintptr_t w, uintptr_t b, uintptr_t out,
-           uintptr_t stream) {
-          chk(gale::head_pool_dense_softmax(batch, HW, C, N, P(x),
+           uintptr_t stream, int fp8, float in_scale) {
+          chk(gale::head_pool_dense_softmax(batch, HW, C, N, P(x), fp8, in_scale,
                                             static_cast<const float*>(P(w)),
                                             static_cast<const float*>(P(b)),
                                             static_cast<float*>(P(out)), S(stream)),
               "head_pool_dense_softmax");
-        });
+        },
+        py::arg("batch"), py::arg("HW"), py::arg("C"), py::arg("N"), py::arg("x"), py::arg("w"),
+        py::arg("b"), py::arg("out"), py::arg("stream"), py::arg("fp8") = 0,
+        py::arg("in_scale") = 1.0f);
   m.def("softmax_rows", [](int batch, int N, int ld, uintptr_t x, uintptr_t out, uintptr_t stream) {
     chk(gale::softmax_rows(batch, N, ld, static_cast<const float*>(P(x)),
                            static_cast<float*>(P(out)), S(stream)),

@@ -36,6 +36,8 @@ struct PlanOp {
   const void* w = nullptr;
   const float* bias = nullptr;
   const float* wscale = nullptr;
+  int fp8 = 0;        // pool / head ops: e4m3 activations
+  float scale = 1.f;  // head: input activation scale (fp8)
 };
 
 struct PlanSpec {

@@ -28,28 +28,36 @@ struct ConvDesc {
   int has_res, res_H, res_W, res_C, res_stride;
   int in_f32;           // input tensor is fp32 (network input; converted to bf16 while staging)
   int out_f32;          // output tensor is fp32 (classifier logits)
-  int fp8;              // weights are OCP e4m3 (fp8 MFMA path); activations quantised per tensor
-  float act_scale;      // fp8 path: activation quantisation scale (x_q = x * act_scale)
+  int fp8;              // OCP e4m3 operands (fp8 MFMA path): weights per-channel (wscale),
+                        // activations per tensor (value = code * scale)
+  float in_scale;       // fp8: input scale (in_f32: the input is quantised with this step)
+  float out_scale;      // fp8: output scale (ignored for out_f32)
+  float res_scale;      // fp8: residual scale
 };
 
 // y[B,Ho,Wo,Cout] = act(conv(x, w) + bias (+ residual)).
 // w: [Npad][Kpad] (bf16 or e4m3), k = (kh*KW + kw)*Cin + ci, zero padded.
 // bias: [Npad] fp32 (BatchNorm already folded in). wscale: [Npad] fp32 per-output-channel weight
-// dequant scale (fp8 path only; nullptr otherwise).
+// dequant scale (fp8 path only; nullptr otherwise). In the fp8 path x / res / y are e4m3 tensors
+// (x fp32 when in_f32, y fp32 when out_f32).
 hipError_t conv2d(const ConvDesc& d, int batch, const void* x, const void* w, const float* bias,
                   const float* wscale, const void* res, void* y, hipStream_t stream);
 
-// Max pooling, NHWC bf16, window k, stride s, symmetric zero... (-inf) padding p.
+// Max pooling, NHWC bf16 (or e4m3 when fp8; the scale passes through), window k, stride s,
+// -inf padding p.
 hipError_t maxpool2d(int batch, int H, int W, int C, int k, int s, int p, int Ho, int Wo,
-                     const void* x, void* y, hipStream_t stream);
+                     const void* x, void* y, int fp8, hipStream_t stream);
 
-// Global average pooling, NHWC bf16 [B,H,W,C] -> bf16 [B,C].
-hipError_t avgpool_global(int batch, int HW, int C, const void* x, void* y, hipStream_t stream);
+// Global average pooling, NHWC bf16 / e4m3 [B,H,W,C] -> same type [B,C] (same scale).
+hipError_t avgpool_global(int batch, int HW, int C, const void* x, void* y, int fp8,
+                          hipStream_t stream);
 
 // Fused classifier head: optional global average pool over HW, dense layer with fp32 weights
-// w[N][C] + bias[N], then row softmax. x: bf16 [B,HW,C]; out: fp32 [B,N]. One workgroup per image.
-hipError_t head_pool_dense_softmax(int batch, int HW, int C, int N, const void* x, const float* w,
-                                   const float* bias, float* out, hipStream_t stream);
+// w[N][C] + bias[N], then row softmax. x: bf16 (or e4m3 with scale in_scale) [B,HW,C]; out: fp32
+// [B,N]. One workgroup per image.
+hipError_t head_pool_dense_softmax(int batch, int HW, int C, int N, const void* x, int fp8,
+                                   float in_scale, const float* w, const float* bias, float* out,
+                                   hipStream_t stream);
 
 // Row softmax, fp32 [B, ld] -> fp32 [B, N] (first N columns of each row).
 hipError_t softmax_rows(int batch, int N, int ld, const float* x, float* out, hipStream_t stream);
@@ -58,9 +66,6 @@ hipError_t softmax_rows(int batch, int N, int ld, const float* x, float* out, hi
 hipError_t cast_f32_bf16(int64_t n, float scale, float shift, const float* x, void* y,
                          hipStream_t stream);
 
-// Quantise fp32 -> OCP e4m3 with a per-tensor scale (used to pack fp8 weights on device).
-hipError_t quant_f32_e4m3(int64_t n, const float* x, const float* row_scale, int row_len, void* y,
-                          hipStream_t stream);
 
 // GPU decoder for the InstObj JSON contract: parses every number of each record's instances
 // array into the fp32 NHWC batch tensor and validates the rectangular [N][H][W][C] structure.

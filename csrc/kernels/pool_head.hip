@@ -9,9 +9,48 @@
 namespace gale {
 namespace {
 
+// 8 channels of one pixel as floats (bf16 or e4m3 codes; e4m3 values are in units of the
+// tensor's scale, which pooling preserves)
+template <bool F8>
+__device__ __forceinline__ void load8f(const void* x, size_t off, float* v) {
+  if constexpr (F8) {
+    const uint2 r = *reinterpret_cast<const uint2*>(reinterpret_cast<const uint8_t*>(x) + off);
+    v[0] = __builtin_amdgcn_cvt_f32_fp8((int)r.x, 0);
+    v[1] = __builtin_amdgcn_cvt_f32_fp8((int)r.x, 1);
+    v[2] = __builtin_amdgcn_cvt_f32_fp8((int)r.x, 2);
+    v[3] = __builtin_amdgcn_cvt_f32_fp8((int)r.x, 3);
+    v[4] = __builtin_amdgcn_cvt_f32_fp8((int)r.y, 0);
+    v[5] = __builtin_amdgcn_cvt_f32_fp8((int)r.y, 1);
+    v[6] = __builtin_amdgcn_cvt_f32_fp8((int)r.y, 2);
+    v[7] = __builtin_amdgcn_cvt_f32_fp8((int)r.y, 3);
+  } else {
+    const bf16x8 b = ld_bf16x8(reinterpret_cast<const bf16*>(x) + off);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = (float)b[j];
+  }
+}
+
+template <bool F8>
+__device__ __forceinline__ void store8f(void* y, size_t off, const float* v) {
+  if constexpr (F8) {
+    int lo = __builtin_amdgcn_cvt_pk_fp8_f32(v[0], v[1], 0, false);
+    lo = __builtin_amdgcn_cvt_pk_fp8_f32(v[2], v[3], lo, true);
+    int hi = __builtin_amdgcn_cvt_pk_fp8_f32(v[4], v[5], 0, false);
+    hi = __builtin_amdgcn_cvt_pk_fp8_f32(v[6], v[7], hi, true);
+    *reinterpret_cast<uint2*>(reinterpret_cast<uint8_t*>(y) + off) =
+        make_uint2((uint32_t)lo, (uint32_t)hi);
+  } else {
+    bf16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = (bf16)v[j];
+    *reinterpret_cast<uint4*>(reinterpret_cast<bf16*>(y) + off) = __builtin_bit_cast(uint4, o);
+  }
+}
+
+template <bool F8>
 __global__ __launch_bounds__(256) void maxpool_kernel(int total, int H, int W, int C8, int k, int s,
-                                                      int p, int Ho, int Wo, const bf16* x,
-                                                      bf16* y) {
+                                                      int p, int Ho, int Wo, const void* x,
+                                                      void* y) {
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i >= total) return;
   const int cg = i % C8;
@@ -30,42 +69,43 @@ __global__ __launch_bounds__(256) void maxpool_kernel(int total, int H, int W, i
     for (int kw = 0; kw < k; ++kw) {
       const int wi = wo * s - p + kw;
       if ((unsigned)wi >= (unsigned)W) continue;
-      const bf16x8 v = ld_bf16x8(x + ((size_t)(n * H + hi) * W + wi) * C + cg * 8);
+      float v[8];
+      load8f<F8>(x, ((size_t)(n * H + hi) * W + wi) * C + cg * 8, v);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) m[j] = fmaxf(m[j], (float)v[j]);
+      for (int j = 0; j < 8; ++j) m[j] = fmaxf(m[j], v[j]);
     }
   }
-  bf16x8 o;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) o[j] = (bf16)m[j];
-  *reinterpret_cast<uint4*>(y + (size_t)pix * C + cg * 8) = __builtin_bit_cast(uint4, o);
+  store8f<F8>(y, (size_t)pix * C + cg * 8, m);  // max of e4m3 values re-encodes exactly
 }
 
-__global__ __launch_bounds__(256) void avgpool_kernel(int total, int HW, int C8, const bf16* x,
-                                                      bf16* y) {
+template <bool F8>
+__global__ __launch_bounds__(256) void avgpool_kernel(int total, int HW, int C8, const void* x,
+                                                      void* y) {
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i >= total) return;
   const int cg = i % C8;
   const int n = i / C8;
   const int C = C8 * 8;
   float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  const bf16* base = x + (size_t)n * HW * C + cg * 8;
+  const size_t base = (size_t)n * HW * C + cg * 8;
   for (int q = 0; q < HW; ++q) {
-    const bf16x8 v = ld_bf16x8(base + (size_t)q * C);
+    float v[8];
+    load8f<F8>(x, base + (size_t)q * C, v);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) s[j] += (float)v[j];
+    for (int j = 0; j < 8; ++j) s[j] += v[j];
   }
   const float inv = 1.f / (float)HW;
-  bf16x8 o;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) o[j] = (bf16)(s[j] * inv);
-  *reinterpret_cast<uint4*>(y + (size_t)n * C + cg * 8) = __builtin_bit_cast(uint4, o);
+  for (int j = 0; j < 8; ++j) s[j] *= inv;
+  store8f<F8>(y, (size_t)n * C + cg * 8, s);  // the mean keeps the input's scale
 }
 
-// One workgroup per image: pooled[C] -> logits[N] -> softmax, all fp32 in LDS.
-__global__ __launch_bounds__(256) void head_kernel(int HW, int C, int N, const bf16* x,
-                                                   const float* w, const float* bias,
-                                                   float* out) {
+// One workgroup per image: pooled[C] -> logits[N] -> softmax, all fp32 in LDS. fp8 inputs are
+// pooled in units of their scale, which is applied once to the pooled vector.
+template <bool F8>
+__global__ __launch_bounds__(256) void head_kernel(int HW, int C, int N, const void* x,
+                                                   float in_scale, const float* w,
+                                                   const float* bias, float* out) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int C8 = C >> 3;
   const int nps = 256 / C8 > 0 ? 256 / C8 : 1;  // pixel slices summed in parallel
@@ -73,20 +113,21 @@ __global__ __launch_bounds__(256) void head_kernel(int HW, int C, int N, const b
   float* pooled = part + (size_t)nps * C;                  // [C]
   float* logits = pooled + C;                              // [N]
   const int n = blockIdx.x;
-  const bf16* img = x + (size_t)n * HW * C;
+  const size_t img = (size_t)n * HW * C;
   for (int t = threadIdx.x; t < nps * C8; t += 256) {
     const int cg = t % C8, ps = t / C8;
     float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     for (int q = ps; q < HW; q += nps) {
-      const bf16x8 v = ld_bf16x8(img + (size_t)q * C + cg * 8);
+      float v[8];
+      load8f<F8>(x, img + (size_t)q * C + cg * 8, v);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) s[j] += (float)v[j];
+      for (int j = 0; j < 8; ++j) s[j] += v[j];
     }
 #pragma unroll
     for (int j = 0; j < 8; ++j) part[ps * C + cg * 8 + j] = s[j];
   }
   __syncthreads();
-  const float inv = 1.f / (float)HW;
+  const float inv = in_scale / (float)HW;
   for (int c = threadIdx.x; c < C; c += 256) {
     float s = 0.f;
     for (int ps = 0; ps < nps; ++ps) s += part[ps * C + c];
@@ -151,35 +192,37 @@ __global__ __launch_bounds__(256) void cast_kernel(int64_t n4, float scale, floa
 }  // namespace
 
 hipError_t maxpool2d(int batch, int H, int W, int C, int k, int s, int p, int Ho, int Wo,
-                     const void* x, void* y, hipStream_t stream) {
+                     const void* x, void* y, int fp8, hipStream_t stream) {
   if (batch <= 0) return hipSuccess;
   if (C % 8) return hipErrorInvalidValue;
   const int total = batch * Ho * Wo * (C / 8);
-  hipLaunchKernelGGL(maxpool_kernel, dim3((total + 255) / 256), dim3(256), 0, stream, total, H, W,
-                     C / 8, k, s, p, Ho, Wo, reinterpret_cast<const bf16*>(x),
-                     reinterpret_cast<bf16*>(y));
+  hipLaunchKernelGGL(fp8 ? maxpool_kernel<true> : maxpool_kernel<false>,
+                     dim3((total + 255) / 256), dim3(256), 0, stream, total, H, W, C / 8, k, s, p,
+                     Ho, Wo, x, y);
   return hipGetLastError();
 }
 
-hipError_t avgpool_global(int batch, int HW, int C, const void* x, void* y, hipStream_t stream) {
+hipError_t avgpool_global(int batch, int HW, int C, const void* x, void* y, int fp8,
+                          hipStream_t stream) {
   if (batch <= 0) return hipSuccess;
   if (C % 8) return hipErrorInvalidValue;
   const int total = batch * (C / 8);
-  hipLaunchKernelGGL(avgpool_kernel, dim3((total + 255) / 256), dim3(256), 0, stream, total, HW,
-                     C / 8, reinterpret_cast<const bf16*>(x), reinterpret_cast<bf16*>(y));
+  hipLaunchKernelGGL(fp8 ? avgpool_kernel<true> : avgpool_kernel<false>,
+                     dim3((total + 255) / 256), dim3(256), 0, stream, total, HW, C / 8, x, y);
   return hipGetLastError();
 }
 
-hipError_t head_pool_dense_softmax(int batch, int HW, int C, int N, const void* x, const float* w,
-                                   const float* bias, float* out, hipStream_t stream) {
+hipError_t head_pool_dense_softmax(int batch, int HW, int C, int N, const void* x, int fp8,
+                                   float in_scale, const float* w, const float* bias, float* out,
+                                   hipStream_t stream) {
   if (batch <= 0) return hipSuccess;
   if (C % 8 || C > 4096 || N > 4096) return hipErrorInvalidValue;
   const int C8 = C / 8;
   const int nps = 256 / C8 > 0 ? 256 / C8 : 1;
   const size_t lds = ((size_t)nps * C + C + N) * sizeof(float);
   if (lds > 160 * 1024) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(head_kernel, dim3(batch), dim3(256), lds, stream, HW, C, N,
-                     reinterpret_cast<const bf16*>(x), w, bias, out);
+  hipLaunchKernelGGL(fp8 ? head_kernel<true> : head_kernel<false>, dim3(batch), dim3(256), lds,
+                     stream, HW, C, N, x, fp8 ? in_scale : 1.f, w, bias, out);
   return hipGetLastError();
 }
 

@@ -79,13 +79,13 @@ void Executor::launch_all(int batch, void* const* bufs, hipStream_t stream) {
         break;
       case OP_MAXPOOL:
         e = maxpool2d(batch, op.p[0], op.p[1], op.p[2], op.p[3], op.p[4], op.p[5], op.p[6], op.p[7],
-                      in, out, stream);
+                      in, out, op.fp8, stream);
         break;
       case OP_AVGPOOL:
-        e = avgpool_global(batch, op.p[0], op.p[1], in, out, stream);
+        e = avgpool_global(batch, op.p[0], op.p[1], in, out, op.fp8, stream);
         break;
       case OP_HEAD:
-        e = head_pool_dense_softmax(batch, op.p[0], op.p[1], op.p[2], in,
+        e = head_pool_dense_softmax(batch, op.p[0], op.p[1], op.p[2], in, op.fp8, op.scale,
                                     static_cast<const float*>(op.w), op.bias,
                                     static_cast<float*>(out), stream);
         break;

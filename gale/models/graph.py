@@ -258,6 +258,12 @@ def param_layout(net: Network, wdtype: str = "bf16") -> Tuple[Dict[str, PackedEn
             cs = stored_channels(c)
             add(f"{L.name}.w", L.classes * cs * 4, torch.float32, (L.classes, cs))
             add(f"{L.name}.b", L.classes * 4, torch.float32, (L.classes,))
+    if wdtype == "fp8":
+        # per-tensor activation scales travel with the weights (one RCCL broadcast)
+        from gale.models.quant import activation_tensors
+
+        n = len(activation_tensors(net))
+        add("act_scales", n * 4, torch.float32, (n,))
     return layout, round_up(off, ALIGN)
 
 
@@ -304,7 +310,24 @@ def pack_params(net: Network, folded: Dict[str, torch.Tensor], wdtype: str = "bf
             w[:, :c] = folded[f"{L.name}.weight"]
             put(f"{L.name}.w", w)
             put(f"{L.name}.b", folded[f"{L.name}.bias"])
+    if wdtype == "fp8":
+        from gale.models.quant import activation_tensors, calibrate_act_scales
+
+        sc = calibrate_act_scales(net, folded)
+        put("act_scales", torch.tensor([sc[n] for n in activation_tensors(net)],
+                                       dtype=torch.float32))
     return buf
+
+
+def act_scales_from_packed(net: Network, packed: torch.Tensor) -> Dict[str, float]:
+    """Read the fp8 activation scales back out of a packed buffer (any device)."""
+    from gale.models.quant import activation_tensors
+
+    layout, _ = param_layout(net, "fp8")
+    e = layout["act_scales"]
+    raw = packed[e.offset: e.offset + e.nbytes].cpu().contiguous()
+    vals = raw.view(torch.float32).tolist()
+    return dict(zip(activation_tensors(net), vals))
 
 
 # --------------------------------------------------------------------------------------------
@@ -314,19 +337,24 @@ def pack_params(net: Network, folded: Dict[str, torch.Tensor], wdtype: str = "bf
 OP_CONV, OP_MAXPOOL, OP_AVGPOOL, OP_HEAD, OP_SOFTMAX = 0, 1, 2, 3, 4
 
 
-def _tensor_bytes(net: Network, name: str) -> int:
+def _tensor_bytes(net: Network, name: str, wdtype: str = "bf16") -> int:
     h, w, c = net.shapes[name]
     if name == "input":
         return h * w * c * 4
-    return h * w * stored_channels(c) * 2
+    return h * w * stored_channels(c) * (1 if wdtype == "fp8" else 2)
 
 
-def build_plan(net: Network, base_ptr: int, wdtype: str = "bf16") -> Tuple[List[dict], List[int]]:
+def build_plan(net: Network, base_ptr: int, wdtype: str = "bf16",
+               act_scales: Optional[Dict[str, float]] = None) -> Tuple[List[dict], List[int]]:
     """Executor plan for a packed parameter buffer living at device address ``base_ptr``.
 
     Returns (ops, buf_bytes_per_image). Buffer 0 = fp32 input, 1 = fp32 softmax output, >= 2 =
-    bf16 activations assigned by liveness so concurrently-live tensors never share a buffer.
+    bf16 (fp8: e4m3) activations assigned by liveness so concurrently-live tensors never share a
+    buffer. ``act_scales`` (fp8 only): per-tensor scales, see ``act_scales_from_packed``.
     """
+    fp8 = wdtype == "fp8"
+    if fp8 and act_scales is None:
+        raise ValueError("build_plan: the fp8 plan needs the activation scales")
     layout, _ = param_layout(net, wdtype)
     # liveness: last layer index reading each tensor
     last_use: Dict[str, int] = {}
@@ -344,7 +372,7 @@ def build_plan(net: Network, base_ptr: int, wdtype: str = "bf16") -> Tuple[List[
         if isinstance(L, (Head, Softmax)):
             buf_of["output"] = 1
         else:
-            need = _tensor_bytes(net, out_name)
+            need = _tensor_bytes(net, out_name, wdtype)
             if isinstance(L, Conv) and L.out_f32:
                 h, w, c = net.shapes[out_name]
                 need = h * w * stored_channels(c) * 4
@@ -364,12 +392,17 @@ def build_plan(net: Network, base_ptr: int, wdtype: str = "bf16") -> Tuple[List[
             d["relu"] = int(L.relu)
             d["in_f32"] = int(L.inp == "input")
             d["out_f32"] = int(L.out_f32)
-            d["fp8"] = int(wdtype == "fp8")
+            d["fp8"] = int(fp8)
+            if fp8:
+                d["in_scale"] = act_scales[L.inp]
+                d["out_scale"] = 1.0 if L.out_f32 else act_scales[L.out]
             res = -1
             if L.residual is not None:
                 rh, rw, rc = net.shapes[L.residual]
                 d.update(has_res=1, res_H=rh, res_W=rw, res_C=stored_channels(rc),
                          res_stride=2 if L.res_mode == "pad" else 1)
+                if fp8:
+                    d["res_scale"] = act_scales[L.residual]
                 res = buf_of[L.residual]
             op = dict(kind=OP_CONV, conv=d, **{"in": buf_of[L.inp]}, out=buf_of[out_name], res=res,
                       w=base_ptr + layout[f"{L.name}.w"].offset,
@@ -381,17 +414,18 @@ def build_plan(net: Network, base_ptr: int, wdtype: str = "bf16") -> Tuple[List[
             h, w, c = net.shapes[L.inp]
             ho, wo, _ = net.shapes[L.out]
             ops.append(dict(kind=OP_MAXPOOL, p=[h, w, stored_channels(c), L.k, L.s, L.p, ho, wo],
-                            **{"in": buf_of[L.inp]}, out=buf_of[L.out]))
+                            **{"in": buf_of[L.inp]}, out=buf_of[L.out], fp8=int(fp8)))
         elif isinstance(L, AvgPool):
             h, w, c = net.shapes[L.inp]
             ops.append(dict(kind=OP_AVGPOOL, p=[h * w, stored_channels(c)],
-                            **{"in": buf_of[L.inp]}, out=buf_of[L.out]))
+                            **{"in": buf_of[L.inp]}, out=buf_of[L.out], fp8=int(fp8)))
         elif isinstance(L, Head):
             h, w, c = net.shapes[L.inp]
             ops.append(dict(kind=OP_HEAD, p=[h * w, stored_channels(c), L.classes],
                             **{"in": buf_of[L.inp]}, out=1,
                             w=base_ptr + layout[f"{L.name}.w"].offset,
-                            bias=base_ptr + layout[f"{L.name}.b"].offset))
+                            bias=base_ptr + layout[f"{L.name}.b"].offset,
+                            fp8=int(fp8), scale=act_scales[L.inp] if fp8 else 1.0))
         elif isinstance(L, Softmax):
             h, w, c = net.shapes[L.inp]
             ops.append(dict(kind=OP_SOFTMAX, p=[L.classes, stored_channels(c)],

@@ -125,3 +125,93 @@ def cast_bf16(x: torch.Tensor, scale: float = 1.0, shift: float = 0.0) -> torch.
     y = torch.empty(x.shape, device=x.device, dtype=torch.bfloat16)
     native().cast_f32_bf16(x.numel(), scale, shift, x.data_ptr(), y.data_ptr(), _stream())
     return y
+
+
+# ---- fp8 (OCP e4m3fn) path: tensors of e4m3 codes are uint8 --------------------------------
+
+
+def pack_conv_fp8(w_oihw: torch.Tensor, bias: torch.Tensor, cin_stored: Optional[int] = None,
+                  device=None):
+    """Pack an fp32 conv weight as e4m3 codes with per-output-channel scales.
+
+    Returns (w codes uint8 [Npad, Kpad], bias fp32 [Npad], wscale fp32 [Npad], geometry dict).
+    """
+    from gale.models.quant import quantize_rows_e4m3
+
+    cout, cin, kh, kw = w_oihw.shape
+    cin_s = cin if cin_stored is None else cin_stored
+    cout_s = round_up(cout, 4)
+    K = kh * kw * cin_s
+    Kpad = round_up(K, 32)
+    Npad = round_up(cout_s, conv_n_tiles(cout_s) * 16)
+    q, s = quantize_rows_e4m3(pack_conv_weight(w_oihw.float().cpu(), cin_s, Npad, Kpad))
+    bp = torch.zeros(Npad)
+    bp[:cout] = bias.float().cpu()
+    dev = device if device is not None else torch.device("cuda")
+    return q.to(dev), bp.to(dev), s.to(dev), dict(Cin=cin_s, Cout=cout_s, KH=kh, KW=kw, K=K,
+                                                   Kpad=Kpad, Npad=Npad)
+
+
+def conv2d_fp8(x: torch.Tensor, w_codes: torch.Tensor, bias: torch.Tensor, wscale: torch.Tensor,
+               geom: dict, in_scale: float, out_scale: float = 1.0, stride: int = 1, pad: int = 0,
+               relu: bool = False, residual: Optional[torch.Tensor] = None,
+               res_scale: float = 1.0, res_mode: str = "identity",
+               out_f32: bool = False) -> torch.Tensor:
+    """NHWC conv on fp8 MFMA. x: e4m3 codes (uint8, value = code * in_scale) or fp32 (quantised
+    with step in_scale while loaded). Returns e4m3 codes at out_scale, or fp32 (out_f32)."""
+    B, H, W, C = x.shape
+    if C != geom["Cin"]:
+        raise ValueError(f"x has {C} channels, packed weight expects {geom['Cin']}")
+    _check(w_codes, torch.uint8, "w_codes")
+    _check(bias, torch.float32, "bias")
+    _check(wscale, torch.float32, "wscale")
+    if x.dtype not in (torch.uint8, torch.float32):
+        raise TypeError("x must be e4m3 codes (uint8) or fp32")
+    _check(x, x.dtype, "x")
+    kh, kw = geom["KH"], geom["KW"]
+    Ho = (H + 2 * pad - kh) // stride + 1
+    Wo = (W + 2 * pad - kw) // stride + 1
+    y = torch.empty(B, Ho, Wo, geom["Cout"], device=x.device,
+                    dtype=torch.float32 if out_f32 else torch.uint8)
+    d = dict(geom, H=H, W=W, Ho=Ho, Wo=Wo, stride=stride, pad=pad, relu=int(relu),
+             in_f32=int(x.dtype == torch.float32), out_f32=int(out_f32), fp8=1,
+             in_scale=float(in_scale), out_scale=float(out_scale), res_scale=float(res_scale))
+    res_ptr = 0
+    if residual is not None:
+        _check(residual, torch.uint8, "residual")
+        _, rh, rw, rc = residual.shape
+        d.update(has_res=1, res_H=rh, res_W=rw, res_C=rc, res_stride=2 if res_mode == "pad" else 1)
+        res_ptr = residual.data_ptr()
+    native().conv2d(d, B, x.data_ptr(), w_codes.data_ptr(), bias.data_ptr(), wscale.data_ptr(),
+                    res_ptr, y.data_ptr(), _stream())
+    return y
+
+
+def maxpool2d_fp8(x: torch.Tensor, k: int, s: int, p: int = 0) -> torch.Tensor:
+    _check(x, torch.uint8, "x")
+    B, H, W, C = x.shape
+    Ho = (H + 2 * p - k) // s + 1
+    Wo = (W + 2 * p - k) // s + 1
+    y = torch.empty(B, Ho, Wo, C, device=x.device, dtype=torch.uint8)
+    native().maxpool2d(B, H, W, C, k, s, p, Ho, Wo, x.data_ptr(), y.data_ptr(), _stream(), 1)
+    return y
+
+
+def avgpool_global_fp8(x: torch.Tensor) -> torch.Tensor:
+    _check(x, torch.uint8, "x")
+    B, H, W, C = x.shape
+    y = torch.empty(B, C, device=x.device, dtype=torch.uint8)
+    native().avgpool_global(B, H * W, C, x.data_ptr(), y.data_ptr(), _stream(), 1)
+    return y
+
+
+def head_fp8(x: torch.Tensor, in_scale: float, w: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    _check(x, torch.uint8, "x")
+    _check(w, torch.float32, "w")
+    _check(b, torch.float32, "b")
+    B, H, W, C = x.shape
+    N = w.shape[0]
+    out = torch.empty(B, N, device=x.device, dtype=torch.float32)
+    native().head_pool_dense_softmax(B, H * W, C, N, x.data_ptr(), w.data_ptr(), b.data_ptr(),
+                                     out.data_ptr(), _stream(), 1, float(in_scale))
+    return out

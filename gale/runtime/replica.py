@@ -12,7 +12,7 @@ from typing import Optional, Sequence
 import torch
 
 from gale._native import native
-from gale.models.graph import Network, build_plan
+from gale.models.graph import Network, act_scales_from_packed, build_plan
 
 
 class ModelReplica:
@@ -24,7 +24,8 @@ class ModelReplica:
         self.packed = packed  # keeps the weights alive
         self.device = packed.device
         self.wdtype = wdtype
-        ops, buf_bytes = build_plan(net, packed.data_ptr(), wdtype)
+        self.act_scales = act_scales_from_packed(net, packed) if wdtype == "fp8" else None
+        ops, buf_bytes = build_plan(net, packed.data_ptr(), wdtype, self.act_scales)
         self.ops = ops
         self.buf_bytes = buf_bytes
         self.executor = native().Executor(packed.device.index or 0, ops, buf_bytes, max_batch,

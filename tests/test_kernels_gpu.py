@@ -147,3 +147,104 @@ def test_no_cpu_fallback():
     w, b, geom = ops.pack_conv(torch.randn(16, 16, 3, 3), torch.zeros(16))
     with pytest.raises(RuntimeError):
         ops.conv2d(torch.randn(1, 8, 8, 16).to(torch.bfloat16), w, b, geom)
+
+
+# ---- fp8 (OCP e4m3fn) kernels -------------------------------------------------------------
+
+def _e4m3(t):
+    from gale.models.quant import e4m3_codes
+    return e4m3_codes(t)
+
+
+def _from_e4m3(codes):
+    return codes.view(torch.float8_e4m3fn).float()
+
+
+def test_conv2d_fp8_exact_small_integers():
+    """Exact check of the fp8 MFMA operand layout: small integers are exact in e4m3 and every
+    partial sum is exact in fp32, so the result must match bit for bit (asymmetric operands)."""
+    g = torch.Generator().manual_seed(21)
+    B, H, Cin, Cout = 2, 8, 32, 48
+    xv = torch.randint(-3, 4, (B, H, H, Cin), generator=g).float()
+    w = torch.randint(-3, 4, (Cout, Cin, 3, 3), generator=g).float() * 0.25
+    w[:, 0, 0, 0] = 0.875  # every row max is 448/512: power-of-two scale 1/512, codes exact
+    from gale import ops
+    wq, bq, ws, geom = ops.pack_conv_fp8(w, torch.zeros(Cout))
+    y = ops.conv2d_fp8(_e4m3(xv).to(DEV), wq, bq, ws, geom, in_scale=1.0, stride=1, pad=1,
+                       out_scale=4.0)
+    ref = _ref_conv(xv, w, torch.zeros(Cout), 1, 1, False)
+    # outputs are multiples of 1/4 (exact fp32 sums and scale products): both round v/4 to e4m3
+    got = _from_e4m3(y.cpu())
+    from gale.models.quant import e4m3_round
+    assert torch.equal(got[..., :Cout], e4m3_round(ref / 4.0))
+
+
+@pytest.mark.parametrize("case", [c for c in CONV_CASES if c[3] <= 256])
+def test_conv2d_fp8_matches_emulation(case):
+    B, H, W, Cin, Cout, k, s, p, in_f32 = case
+    g = torch.Generator().manual_seed(99 + Cin + Cout)
+    x = torch.randn(B, H, W, Cin, generator=g)
+    w = torch.randn(Cout, Cin, k, k, generator=g) / (Cin * k * k) ** 0.5
+    b = torch.randn(Cout, generator=g) * 0.1
+    from gale import ops
+    from gale.models.quant import e4m3_round, fake_quant_weight
+    in_scale = float(x.abs().max()) / 448
+    xq = e4m3_round(x / in_scale) * in_scale  # the values the kernel consumes
+    ref = _ref_conv(xq, fake_quant_weight(w), b, s, p, True)
+    out_scale = float(ref.abs().max()) / 448
+    wq, bq, ws, geom = ops.pack_conv_fp8(w, b)
+    xin = x.to(DEV) if in_f32 else _e4m3(x / in_scale).to(DEV)
+    y = ops.conv2d_fp8(xin, wq, bq, ws, geom, in_scale=in_scale, out_scale=out_scale, stride=s,
+                       pad=p, relu=True)
+    got = _from_e4m3(y.cpu())[..., :Cout] * out_scale
+    # same quantised operands; remaining differences: fp32 summation order + one e4m3 rounding
+    err = (got - e4m3_round(ref / out_scale) * out_scale).abs()
+    assert err.max().item() <= 0.0625 * float(ref.abs().max()) + 1e-6
+    assert err.mean().item() <= 1e-3 * float(ref.abs().max()) + 1e-6
+
+
+def test_conv2d_fp8_residual_and_out_f32():
+    g = torch.Generator().manual_seed(8)
+    from gale import ops
+    from gale.models.quant import e4m3_round, fake_quant_weight
+    B, Hin, Cin, Cout = 2, 16, 16, 32
+    x = torch.rand(B, Hin, Hin, Cin, generator=g)
+    res = torch.rand(B, Hin, Hin, Cin, generator=g) * 2
+    w = torch.randn(Cout, Cin, 3, 3, generator=g) / (Cin * 9) ** 0.5
+    b = torch.randn(Cout, generator=g) * 0.1
+    sx, sr = 1 / 448, 2 / 448
+    wq, bq, ws, geom = ops.pack_conv_fp8(w, b)
+    y = ops.conv2d_fp8(_e4m3(x / sx).to(DEV), wq, bq, ws, geom, in_scale=sx, out_scale=4 / 448,
+                       stride=2, pad=1, relu=True, residual=_e4m3(res / sr).to(DEV),
+                       res_scale=sr, res_mode="pad")
+    ref = _ref_conv(e4m3_round(x / sx) * sx, fake_quant_weight(w), b, 2, 1, True,
+                    res=e4m3_round(res / sr) * sr, res_mode="pad")
+    got = _from_e4m3(y.cpu()) * (4 / 448)
+    assert (got - ref).abs().max().item() < 0.07 * float(ref.abs().max())
+    # fc layer with fp32 logits out
+    K, N = 512, 100
+    xf = torch.rand(5, 1, 1, K, generator=g)
+    wf = torch.randn(N, K, 1, 1, generator=g) / K ** 0.5
+    wq, bq, ws, geom = ops.pack_conv_fp8(wf, torch.zeros(N))
+    yl = ops.conv2d_fp8(_e4m3(xf * 448).to(DEV), wq, bq, ws, geom, in_scale=1 / 448, out_f32=True)
+    refl = (e4m3_round(xf * 448) / 448).reshape(5, K) @ fake_quant_weight(wf).reshape(N, K).t()
+    assert (yl.cpu().reshape(5, -1)[:, :N] - refl).abs().max().item() < 1e-4
+
+
+def test_pool_and_head_fp8():
+    g = torch.Generator().manual_seed(4)
+    from gale import ops
+    x = torch.randn(3, 12, 12, 16, generator=g) * 50
+    codes = _e4m3(x)
+    xv = _from_e4m3(codes)
+    y = ops.maxpool2d_fp8(codes.to(DEV), 3, 2, 1).cpu()
+    ref = F.max_pool2d(xv.permute(0, 3, 1, 2), 3, 2, 1).permute(0, 2, 3, 1)
+    assert torch.equal(_from_e4m3(y), ref)
+    pooled = _from_e4m3(ops.avgpool_global_fp8(codes.to(DEV)).cpu())
+    from gale.models.quant import e4m3_round
+    assert torch.allclose(pooled, e4m3_round(xv.mean(dim=(1, 2))), rtol=0.07, atol=0.02)
+    w = torch.randn(10, 16, generator=g) * 0.01
+    b = torch.randn(10, generator=g) * 0.1
+    probs = ops.head_fp8(codes.to(DEV), 0.5, w.to(DEV), b.to(DEV)).cpu()
+    refp = torch.softmax((xv * 0.5).mean(dim=(1, 2)) @ w.t() + b, dim=1)
+    assert (probs - refp).abs().max().item() < 1e-4

@@ -32,3 +32,29 @@ def test_model_matches_reference(name, batch):
     # graph replay (bucket >= batch, padded tail) must equal eager bit for bit
     assert torch.equal(graph, eager)
     assert rep.executor.graphs_captured >= 1
+
+
+@pytest.mark.parametrize("name,batch", [("lenet5", 13), ("resnet20", 37), ("resnet50", 2)])
+def test_fp8_model_matches_emulation_and_fp32(name, batch):
+    """fp8 plan (e4m3 MFMA, calibrated per-tensor activation scales) against the fp8 emulation
+    oracle (tight: same quantised operands) and against the fp32 oracle (accuracy budget)."""
+    from gale.models.graph import act_scales_from_packed
+
+    net = get_model(name)
+    params = init_params(net, seed=11, calib_batch=4 if name == "resnet50" else 16)
+    packed = materialize_weights(net, torch.device("cuda", 0), params=params, wdtype="fp8")
+    rep = ModelReplica(net, packed, max_batch=64, slots=1, wdtype="fp8")
+    x = torch.rand((batch,) + net.input_shape, generator=torch.Generator().manual_seed(99))
+    folded = fold_params(net, params)
+    emu = forward(net, folded, x, fp8_scales=act_scales_from_packed(net, packed))
+    ref = forward(net, folded, x)
+    got = rep.infer(x, use_graph=True).cpu()
+    torch.cuda.synchronize()
+    e_emu = (got - emu).abs()
+    assert e_emu.mean().item() < 5e-3, f"{name}: mean |p - p_emu| = {e_emu.mean().item()}"
+    e_ref = (got - ref).abs()
+    assert e_ref.max().item() < 0.2 and e_ref.mean().item() < 0.02
+    top2 = ref.topk(2, dim=1).values
+    clear = (top2[:, 0] - top2[:, 1]) > 0.1
+    if clear.any():  # (1000-class random-init resnet50 has no clear winner)
+        assert (got.argmax(1)[clear] == ref.argmax(1)[clear]).float().mean().item() >= 0.9

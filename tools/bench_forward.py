@@ -24,12 +24,13 @@ def main():
     ap.add_argument("--batches", default="1,64,256,1024,4096")
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--eager", action="store_true")
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp8"])
     a = ap.parse_args()
     net = get_model(a.model)
     dev = torch.device("cuda", 0)
-    packed = materialize_weights(net, dev)
+    packed = materialize_weights(net, dev, wdtype=a.dtype)
     bs = [int(b) for b in a.batches.split(",")]
-    rep = ModelReplica(net, packed, max_batch=max(bs), slots=1, buckets=bs)
+    rep = ModelReplica(net, packed, max_batch=max(bs), slots=1, buckets=bs, wdtype=a.dtype)
     s = torch.cuda.current_stream().cuda_stream
     res = []
     for b in bs:
@@ -42,7 +43,7 @@ def main():
         torch.cuda.synchronize()
         dt = (time.perf_counter() - t) / a.iters
         flops = 2 * net.macs_per_image() * b
-        r = dict(model=a.model, batch=b, ms=dt * 1e3, img_s=b / dt, tflops=flops / dt / 1e12,
+        r = dict(model=a.model, dtype=a.dtype, batch=b, ms=dt * 1e3, img_s=b / dt, tflops=flops / dt / 1e12,
                  graph=not a.eager)
         res.append(r)
         print(json.dumps(r), flush=True)
