@@ -59,6 +59,18 @@ hipError_t head_pool_dense_softmax(int batch, int HW, int C, int N, const void* 
                                    float in_scale, const float* w, const float* bias, float* out,
                                    hipStream_t stream);
 
+// Whole-network CIFAR-10 ResNet-20 (csrc/kernels/resnet20_fused.hip): x fp32 [B,32,32,3] ->
+// softmax fp32 [B,10], one workgroup per image with every activation in LDS. w/b: the 19 convs
+// in network order (packed bf16 [Npad][Kpad] + folded-BN fp32 bias), fc_w fp32 [10][64].
+struct ResNet20Params {
+  const void* w[19];  // bf16
+  const float* b[19];
+  const float* fc_w;
+  const float* fc_b;
+};
+hipError_t resnet20_fused_forward(const ResNet20Params& p, int batch, const float* x, float* out,
+                                  hipStream_t stream);
+
 // Row softmax, fp32 [B, ld] -> fp32 [B, N] (first N columns of each row).
 hipError_t softmax_rows(int batch, int N, int ld, const float* x, float* out, hipStream_t stream);
 

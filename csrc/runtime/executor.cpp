@@ -93,6 +93,19 @@ void Executor::launch_all(int batch, void* const* bufs, hipStream_t stream) {
         e = softmax_rows(batch, op.p[0], op.p[1], static_cast<const float*>(in),
                          static_cast<float*>(out), stream);
         break;
+      case OP_RESNET20: {
+        if (op.ptrs.size() != 40) throw std::invalid_argument("resnet20 op needs 40 pointers");
+        ResNet20Params rp;
+        for (int i = 0; i < 19; ++i) {
+          rp.w[i] = op.ptrs[i];
+          rp.b[i] = static_cast<const float*>(op.ptrs[19 + i]);
+        }
+        rp.fc_w = static_cast<const float*>(op.ptrs[38]);
+        rp.fc_b = static_cast<const float*>(op.ptrs[39]);
+        e = resnet20_fused_forward(rp, batch, static_cast<const float*>(in),
+                                   static_cast<float*>(out), stream);
+        break;
+      }
       default:
         throw std::invalid_argument("unknown plan op kind");
     }

@@ -334,7 +334,26 @@ def act_scales_from_packed(net: Network, packed: torch.Tensor) -> Dict[str, floa
 # executor plan
 # --------------------------------------------------------------------------------------------
 
-OP_CONV, OP_MAXPOOL, OP_AVGPOOL, OP_HEAD, OP_SOFTMAX = 0, 1, 2, 3, 4
+OP_CONV, OP_MAXPOOL, OP_AVGPOOL, OP_HEAD, OP_SOFTMAX, OP_RESNET20 = 0, 1, 2, 3, 4, 5
+
+
+def is_cifar_resnet20(net: Network) -> bool:
+    """True for the exact architecture the fused whole-network kernel implements."""
+    from gale.models.zoo import resnet20
+
+    ref = resnet20()
+    return (net.input_shape == ref.input_shape and net.classes == ref.classes
+            and [repr(L) for L in net.layers] == [repr(L) for L in ref.layers])
+
+
+def _fused_resnet20_plan(net: Network, base_ptr: int) -> Tuple[List[dict], List[int]]:
+    layout, _ = param_layout(net, "bf16")
+    convs = [L for L in net.layers if isinstance(L, Conv)]
+    ptrs = [base_ptr + layout[f"{L.name}.w"].offset for L in convs]
+    ptrs += [base_ptr + layout[f"{L.name}.b"].offset for L in convs]
+    ptrs += [base_ptr + layout["fc.w"].offset, base_ptr + layout["fc.b"].offset]
+    op = dict(kind=OP_RESNET20, **{"in": 0}, out=1, ptrs=ptrs)
+    return [op], [_tensor_bytes(net, "input"), net.classes * 4]
 
 
 def _tensor_bytes(net: Network, name: str, wdtype: str = "bf16") -> int:
@@ -345,14 +364,18 @@ def _tensor_bytes(net: Network, name: str, wdtype: str = "bf16") -> int:
 
 
 def build_plan(net: Network, base_ptr: int, wdtype: str = "bf16",
-               act_scales: Optional[Dict[str, float]] = None) -> Tuple[List[dict], List[int]]:
+               act_scales: Optional[Dict[str, float]] = None,
+               fused: bool = True) -> Tuple[List[dict], List[int]]:
     """Executor plan for a packed parameter buffer living at device address ``base_ptr``.
 
     Returns (ops, buf_bytes_per_image). Buffer 0 = fp32 input, 1 = fp32 softmax output, >= 2 =
     bf16 (fp8: e4m3) activations assigned by liveness so concurrently-live tensors never share a
     buffer. ``act_scales`` (fp8 only): per-tensor scales, see ``act_scales_from_packed``.
+    ``fused``: the bf16 CIFAR ResNet-20 becomes ONE whole-network kernel (activations in LDS).
     """
     fp8 = wdtype == "fp8"
+    if fused and not fp8 and is_cifar_resnet20(net):
+        return _fused_resnet20_plan(net, base_ptr)
     if fp8 and act_scales is None:
         raise ValueError("build_plan: the fp8 plan needs the activation scales")
     layout, _ = param_layout(net, wdtype)

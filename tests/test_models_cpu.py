@@ -74,3 +74,17 @@ def test_plan_liveness_never_aliases(name):
 
 def test_stored_channels():
     assert stored_channels(6) == 8 and stored_channels(84) == 88 and stored_channels(64) == 64
+
+
+def test_resnet20_plan_is_one_fused_kernel():
+    from gale.models.graph import OP_RESNET20, is_cifar_resnet20
+
+    net = get_model("resnet20")
+    assert is_cifar_resnet20(net) and not is_cifar_resnet20(get_model("lenet5"))
+    ops, buf_bytes = build_plan(net, 1 << 20)
+    assert len(ops) == 1 and ops[0]["kind"] == OP_RESNET20 and len(ops[0]["ptrs"]) == 40
+    assert buf_bytes == [32 * 32 * 3 * 4, 40]
+    layered, _ = build_plan(net, 1 << 20, fused=False)
+    convs = [op for op in layered if op["kind"] == 0]
+    assert [op["w"] for op in convs] == ops[0]["ptrs"][:19]
+    assert [op["bias"] for op in convs] == ops[0]["ptrs"][19:38]
