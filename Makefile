@@ -34,7 +34,7 @@ $(OBJ)/%.o: csrc/%.cpp $(HDRS)
 	$(CXX) $(CXX_FLAGS) -c $< -o $@
 
 gale/_C.so: $(HIP_OBJ) $(CXX_OBJ)
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -L$(ROCM)/lib -lamdhip64 -pthread \
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -L$(ROCM)/lib -lamdhip64 -lrocprofiler-sdk-roctx -pthread \
 	    -Wl,-rpath,$(ROCM)/lib
 
 clean:

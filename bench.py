@@ -13,7 +13,8 @@ What one rank (= one GPU, launched by torch.distributed.run for N > 1) does:
   staging -> H2D -> GPU JSON parse -> hipGraph ResNet-20 forward -> D2H softmax ->
   {"predictions": ...} encode -> Kafka Produce (acks=1) -> ack.
 
-A "step" is ``--batch`` images completing that whole path (acknowledged by the broker). W warmup
+A "step" is one micro-batch per replica, i.e. ``--batch x --replicas-per-gpu`` images per GPU
+completing that whole path (acknowledged by the broker). W warmup
 steps run first (graphs are captured before that), then exactly K timed steps, bracketed by a
 barrier + ``torch.cuda.synchronize()``. ``value`` is the whole-job aggregate images/s (sum over
 ranks of timed images / the slowest rank's time). p50 latency = median time from a record's
@@ -25,6 +26,7 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import resource
 import sys
 import time
 
@@ -40,7 +42,7 @@ def parse_args():
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--model", default="resnet20", choices=["lenet5", "resnet20", "resnet50"])
-    ap.add_argument("--batch", type=int, default=256, help="images per step per GPU")
+    ap.add_argument("--batch", type=int, default=256, help="images per micro-batch (max_batch)")
     ap.add_argument("--images-per-record", type=int, default=1)
     ap.add_argument("--distinct", type=int, default=1024, help="distinct synthetic images")
     ap.add_argument("--partitions", type=int, default=0,
@@ -49,7 +51,8 @@ def parse_args():
                     help="consumer threads (default: one per partition)")
     ap.add_argument("--sink-parallelism", type=int, default=2)
     ap.add_argument("--decode-threads", type=int, default=2)
-    ap.add_argument("--replicas-per-gpu", type=int, default=1)
+    ap.add_argument("--replicas-per-gpu", type=int, default=4,
+                    help="model replicas (streams) per GPU; each gets its own input partition")
     ap.add_argument("--max-wait-us", type=int, default=2000)
     ap.add_argument("--queue-batches", type=int, default=4,
                     help="records buffered in the engine, in units of --batch")
@@ -87,14 +90,18 @@ def main() -> int:
     net = get_model(a.model)
     K = native().kafka
     ipr = a.images_per_record
+    parts = a.partitions or a.replicas_per_gpu
     rpb = 64  # records per preloaded RecordBatch
     broker = K.Broker(max_message_bytes=256 << 20, retention_bytes=1 << 62)
     broker.start()
-    parts = a.partitions or a.replicas_per_gpu
     broker.create_topic("gale-in", parts)
     broker.create_topic("gale-out", 1)
     # slack: the warm-up engine drains everything it fetched (queue + in-flight fetches)
-    per_rank_images = (a.warmup + a.steps + 4) * a.batch + 8192 * ipr + 4 * a.queue_batches * a.batch
+    # (records are appended by reference, so generous slack costs no memory: each partition can
+    # have a fetch or two (8 MiB each) in flight when the warm-up engine stops)
+    step_images = a.batch * a.replicas_per_gpu  # one micro-batch per replica
+    per_rank_images = ((a.warmup + a.steps + 4) * step_images + 8192 * ipr
+                       + 4 * a.queue_batches * a.batch + parts * 1024 * ipr)
     n_records = -(-per_rank_images // ipr)
     distinct = max(rpb, (a.distinct // (ipr * rpb)) * rpb) * ipr
     imgs = synthetic_images(distinct, net.input_shape, seed=1234 + rank)
@@ -113,14 +120,14 @@ def main() -> int:
                      decode_threads=a.decode_threads,
                      stub=a.stub, stub_null=a.stub_null, commit_interval_ms=500)
     devices = [local_rank] if use_gpu else None
-    warm_records = -(-a.warmup * a.batch // ipr)
+    warm_records = -(-a.warmup * step_images // ipr)
     eng = Engine(cfg, devices=devices, max_records=max(1, warm_records))  # weights: RCCL bcast
     eng.start()
     eng.wait(a.timeout)
     eng.stop()
     warm_done = eng.completed
 
-    timed_records = -(-a.steps * a.batch // ipr)
+    timed_records = -(-a.steps * step_images // ipr)
     cfg.start_offset = "committed"
     eng2 = Engine(cfg, devices=devices, max_records=timed_records,
                   model_replicas=eng.model_replicas if use_gpu else None)
@@ -129,11 +136,14 @@ def main() -> int:
     if use_gpu:
         torch.cuda.synchronize()
     t0 = time.perf_counter()
+    ru0 = resource.getrusage(resource.RUSAGE_SELF)
     eng2.start()
     reached = eng2.wait(a.timeout)
     if use_gpu:
         torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    ru1 = resource.getrusage(resource.RUSAGE_SELF)
+    cpu_s = (ru1.ru_utime - ru0.ru_utime) + (ru1.ru_stime - ru0.ru_stime)
     if world > 1:
         dist.barrier()
     st = eng2.stats()
@@ -163,7 +173,7 @@ def main() -> int:
             "data": "synthetic (uniform [0,1) CIFAR-shaped InstObj JSON records, Java float "
                     "format, preloaded into an embedded Kafka-protocol broker); random-init "
                     "weights (seed 0) RCCL-broadcast from rank 0",
-            "config": {"model": a.model, "global_batch": a.batch * world, "seq_len": None,
+            "config": {"model": a.model, "global_batch": step_images * world, "seq_len": None,
                        "parallelism": f"dp{world}", "images_per_record": ipr,
                        "max_wait_us": a.max_wait_us, "replicas_per_gpu": a.replicas_per_gpu,
                        "path": "kafka-fetch->gpu-json-parse->hipgraph-forward->kafka-produce"},
@@ -172,6 +182,7 @@ def main() -> int:
             "device_ms_p50": round(st["device_us_p50"] / 1e3, 3),
             "batch_images_mean": round(st["batch_images_mean"], 1),
             "json_mb_per_s_rank0": round(st["bytes_in"] / elapsed / 1e6, 1),
+            "cpu_cores_busy_rank0": round(cpu_s / elapsed, 2),
             "warmup_records": warm_done,
             "rank0_thread_s": {k[9:]: round(v, 3) for k, v in st.items()
                                if k.startswith("thread_s_")},

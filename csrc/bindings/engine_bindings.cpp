@@ -50,6 +50,7 @@ EngineConfig config_from_dict(const py::dict& d) {
   opt(d, "queue_depth", c.queue_depth);
   opt(d, "watchdog_ms", c.watchdog_ms);
   opt(d, "fault", c.fault);
+  opt(d, "trace", c.trace);
   opt(d, "max_records", c.max_records);
   opt(d, "seed", c.seed);
   return c;

@@ -8,6 +8,7 @@
 #include <sstream>
 
 #include "../codec/json_codec.h"
+#include "trace.h"
 
 namespace gale {
 
@@ -110,6 +111,7 @@ struct Engine::ReplicaSlot {
 // ---------------------------------------------------------------------------------------------
 
 Engine::Engine(EngineConfig cfg) : cfg_(std::move(cfg)), rng_(cfg_.seed) {
+  if (cfg_.trace) trace::set_enabled(true);
   if (cfg_.input_topic.empty() || cfg_.output_topic.empty())
     throw std::invalid_argument("engine: input and output topics are required");
   if (cfg_.sink_mode != "async" && cfg_.sink_mode != "sync" && cfg_.sink_mode != "fire-and-forget")
@@ -318,6 +320,7 @@ void Engine::source_loop(int idx, std::vector<int> parts) {
     std::vector<kafka::Fetched> fs;
     try {
       const int64_t t0 = mono_ns();
+      trace::Range tr("gale:fetch");
       fs = cons->poll();
       ns_poll_ += mono_ns() - t0;
     } catch (const std::exception& e) {
@@ -391,7 +394,10 @@ void Engine::decode_loop(int idx) {
     }
     good.clear();
     const int64_t t0 = mono_ns();
-    decode_fetch(it, good);
+    {
+      trace::Range tr("gale:decode");
+      decode_fetch(it, good);
+    }
     ns_decode_ += mono_ns() - t0;
     if (!good.empty()) batcher_->push_many(good, stopping_);
   }
@@ -482,7 +488,11 @@ void Engine::worker_loop(ReplicaSlot* rs) {
       auto b = std::make_shared<Batch>();
       int images = 0;
       const int64_t t_take0 = mono_ns();
-      const bool open = batcher_->take(cfg_.max_batch, max_wait_ns, !mine.empty(), b->recs, images);
+      bool open;
+      {
+        trace::Range tr("gale:batch");
+        open = batcher_->take(cfg_.max_batch, max_wait_ns, !mine.empty(), b->recs, images);
+      }
       ns_take_ += mono_ns() - t_take0;
       if (!open) {
         if (mine.empty()) break;  // closed and drained
@@ -500,7 +510,10 @@ void Engine::worker_loop(ReplicaSlot* rs) {
             throw std::runtime_error("injected replica crash (fault replica_crash@" +
                                      std::to_string(crash_at_batch_) + ")");
           b->t_submit_ns = mono_ns();
-          rep.submit(*b);
+          {
+            trace::Range tr("gale:h2d+launch");
+            rep.submit(*b);
+          }
           ns_submit_ += mono_ns() - b->t_submit_ns;
         } catch (const std::exception& e) {
           fail("submit", e.what());
@@ -514,6 +527,7 @@ void Engine::worker_loop(ReplicaSlot* rs) {
     std::shared_ptr<Batch> f = mine.front();
     const int64_t t_wait0 = mono_ns();
     try {
+      trace::Range tr("gale:device-wait");
       rep.wait(*f);
     } catch (const std::exception& e) {
       fail("wait", e.what());
@@ -527,7 +541,10 @@ void Engine::worker_loop(ReplicaSlot* rs) {
       rs->inflight.pop_front();
     }
     mine.pop_front();
-    finish_batch(rs, *f);
+    {
+      trace::Range tr("gale:encode+produce");
+      finish_batch(rs, *f);
+    }
     ns_finish_ += mono_ns() - f->t_done_ns;
   }
 }

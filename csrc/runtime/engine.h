@@ -76,6 +76,7 @@ struct EngineConfig {
   // robustness
   int watchdog_ms = 30000;         // a batch longer than this on a replica marks it dead
   std::string fault;               // "replica_crash@N,parse_error@P,producer_fail@P"
+  bool trace = false;              // roctx ranges around pipeline stages (also GALE_ROCTX=1)
   int64_t max_records = -1;        // stop once this many records are completed (bench/tests)
   uint64_t seed = 0;
 };

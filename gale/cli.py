@@ -12,6 +12,10 @@
     python -m gale produce <TOPIC> [--images N] [--model M] [--rate R]   synthetic InstObj load
     python -m gale consume <TOPIC> [--max N] [--from-beginning]          print output records
 
+``--profile DIR`` re-runs the topology under ``rocprofv3 --kernel-trace --marker-trace --stats``
+(roctx ranges on every host pipeline stage, ``--trace``); ``GALE_ROCTX=1`` turns the ranges on
+for an externally launched profiler.
+
 Multi-GPU, one process per GPU: ``python -m torch.distributed.run --nproc-per-node 8
 --master-addr 127.0.0.1 -m gale NAME IN OUT ...`` — rank r consumes the input partitions
 p % WORLD_SIZE == r and weights are RCCL-broadcast from rank 0.
@@ -63,10 +67,37 @@ def parse_topology_args(argv: List[str]) -> GaleConfig:
     return from_sources(cli=ns, toml_path=toml_path)
 
 
+def profile_command(cfg: GaleConfig, argv: List[str]) -> List[str]:
+    """The rocprofv3 command that re-runs this topology (minus --profile) with roctx ranges on.
+
+    Kernel dispatches + roctx markers + per-kernel stats land in ``cfg.profile`` (a directory).
+    The program runs as a CHILD of this (GPU-untouched) process, right after ``--``: rocprofv3
+    initialises the GPU in the profiled process, so no launcher may sit in between.
+    """
+    rest: List[str] = []
+    skip_next = False
+    for i, tok in enumerate(argv):
+        if skip_next:
+            skip_next = False
+            continue
+        if tok == "--profile":
+            skip_next = True
+            continue
+        if tok.startswith("--profile="):
+            continue
+        rest.append(tok)
+    return ["rocprofv3", "--kernel-trace", "--marker-trace", "--stats", "-d", cfg.profile,
+            "-o", cfg.topology_name, "--", sys.executable, "-m", "gale", *rest, "--trace"]
+
+
 def cmd_run(argv: List[str]) -> int:
     from gale.topology import AlreadyAliveError, InvalidTopologyError, run_topology
 
     cfg = parse_topology_args(argv)
+    if cfg.profile:
+        import subprocess
+
+        return subprocess.call(profile_command(cfg, argv))
     logging.basicConfig(level=getattr(logging, cfg.log_level.upper(), logging.INFO),
                         format="%(asctime)s %(name)s %(levelname)s %(message)s")
     try:

@@ -72,6 +72,8 @@ class GaleConfig:
     # robustness / observability
     watchdog_ms: int = 30000
     fault: str = ""                    # replica_crash@N,parse_error@P,producer_fail@P
+    trace: bool = False                # roctx ranges around pipeline stages (rocprofv3)
+    profile: str = ""                  # run under rocprofv3 --kernel-trace --marker-trace --stats
     metrics_interval: float = 10.0
     metrics_file: str = ""             # JSON lines; empty = stderr
     log_level: str = "INFO"
@@ -111,7 +113,7 @@ class GaleConfig:
             value_format=self.value_format, type_id_header=self.type_id_header,
             on_error=self.on_error, H=H, W=W, C=C, classes=classes, max_batch=self.max_batch,
             max_wait_us=self.max_wait_us, queue_depth=self.queue_depth,
-            watchdog_ms=self.watchdog_ms, fault=self.fault, seed=self.seed)
+            watchdog_ms=self.watchdog_ms, fault=self.fault, seed=self.seed, trace=self.trace)
 
 
 def _coerce(f: dataclasses.Field, raw: Any) -> Any:

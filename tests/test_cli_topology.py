@@ -134,3 +134,18 @@ def test_weights_roundtrip(tmp_path):
     save_params(bad, str(tmp_path / "bad.npz"))
     with pytest.raises(ValueError):
         load_params(str(tmp_path / "bad.npz"), net)
+
+
+def test_profile_flag_wraps_run_in_rocprofv3():
+    from gale.cli import parse_topology_args, profile_command
+
+    argv = ["t1", "in", "out", "--profile", "/tmp/p", "--model", "lenet5"]
+    cfg = parse_topology_args(argv)
+    cmd = profile_command(cfg, argv)
+    assert cmd[0] == "rocprofv3" and "--marker-trace" in cmd and "--kernel-trace" in cmd
+    dd = cmd.index("--")
+    assert cmd[dd + 1].endswith("python3") or "python" in cmd[dd + 1]
+    assert cmd[dd + 2:dd + 4] == ["-m", "gale"]
+    assert "--profile" not in cmd[dd:] and cmd[-1] == "--trace"
+    assert cmd[cmd.index("-d") + 1] == "/tmp/p"
+    assert parse_topology_args(cmd[dd + 4:]).trace is True

@@ -78,7 +78,7 @@ def test_fp8_packing_and_plan(name):
     assert all("wscale" in op for op in convs)
     assert convs[0]["conv"]["in_scale"] == pytest.approx(sc["input"])
     # e4m3 activations: half the bytes of the bf16 plan's activation buffers
-    _, bf16_bytes = build_plan(net, 0, "bf16")
+    _, bf16_bytes = build_plan(net, 0, "bf16", fused=False)
     assert sum(buf_bytes[2:]) * 2 == sum(bf16_bytes[2:])
     with pytest.raises(ValueError):
         build_plan(net, 0, "fp8")

@@ -12,9 +12,9 @@ timeout -k 10 300 python bench.py ${BENCH_ARGS:-} > gpurun_out/bench.log 2>&1
 rc=$?; echo "bench rc=$rc"; tail -1 gpurun_out/bench.log
 [ $rc -eq 0 ] || exit $rc
 rm -rf gpurun_out/prof
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run -- \
+GALE_ROCTX=1 timeout -k 10 300 rocprofv3 --kernel-trace --marker-trace --stats -d gpurun_out/prof -o run -- \
   python3 bench.py --steps 50 --warmup 5 ${BENCH_ARGS:-} > gpurun_out/prof_bench.log 2>&1
 rc=$?; echo "prof rc=$rc"; tail -1 gpurun_out/prof_bench.log
-f=$(find gpurun_out/prof -name '*kernel_stats.csv' | head -1)
-[ -n "$f" ] && cut -d, -f1-5 "$f" | head -20
+python3 tools/prof_summary.py $(find gpurun_out/prof -name '*.db' | head -1) > gpurun_out/prof_bench.txt
+cat gpurun_out/prof_bench.txt
 exit $rc

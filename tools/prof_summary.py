@@ -23,6 +23,17 @@ def main():
         print(f'"{short}",{n},{tot/1e3:.1f},{avg/1e3:.2f},{mn/1e3:.2f},{mx/1e3:.2f},'
               f"{100*tot/total:.1f}")
     try:
+        rg = c.execute(
+            "select json_extract(extdata, '$.message'), count(*), sum(end-start), avg(end-start), "
+            "count(distinct tid) from regions where extdata like '%message%' group by 1 "
+            "order by 3 desc").fetchall()
+    except sqlite3.Error:
+        rg = []
+    if rg:
+        print("\nroctx_range,calls,total_us,avg_us,threads")
+        for name, n, tot, avg, nt in rg:
+            print(f"{name},{n},{tot/1e3:.1f},{avg/1e3:.2f},{nt}")
+    try:
         mc = c.execute("select src_agent_type||'->'||dst_agent_type, count(*), sum(end-start), "
                        "sum(size) from memory_copies group by 1").fetchall()
     except sqlite3.Error:
