@@ -41,3 +41,32 @@ clean:
 	rm -rf build gale/_C.so
 
 .PHONY: all clean
+
+# ---- host-pipeline sanitizer builds: engine + Kafka client/broker + codec with
+# CPU stub replicas under ThreadSanitizer / AddressSanitizer. Host code only (no GPU code is
+# linked; GPU sanitizers are not available on this pool).
+SAN_SRC   := csrc/tests/engine_stress.cpp csrc/runtime/engine.cpp csrc/runtime/replica.cpp \
+             csrc/runtime/pinned_pool.cpp csrc/runtime/trace.cpp csrc/codec/json_codec.cpp \
+             $(wildcard csrc/kafka/*.cpp)
+SAN_FLAGS := -O1 -g -fno-omit-frame-pointer -std=c++17 -D__HIP_PLATFORM_AMD__ -I$(ROCM)/include \
+             -Icsrc/include -mavx2 -mfma -msse4.2 -mpclmul -mbmi2 -pthread
+SAN_LIBS  := -L$(ROCM)/lib -lamdhip64 -lrocprofiler-sdk-roctx -Wl,-rpath,$(ROCM)/lib
+# LLVM's sanitizer runtimes (ROCm's clang): gcc-11's libtsan does not intercept
+# pthread_cond_clockwait, which libstdc++'s condition_variable uses, and reports false races
+SAN_CXX   ?= $(ROCM)/lib/llvm/bin/clang++
+
+build/tsan/engine_stress: $(SAN_SRC) $(HDRS)
+	@mkdir -p $(dir $@)
+	$(SAN_CXX) $(SAN_FLAGS) -fsanitize=thread $(SAN_SRC) -o $@ $(SAN_LIBS)
+
+build/asan/engine_stress: $(SAN_SRC) $(HDRS)
+	@mkdir -p $(dir $@)
+	$(SAN_CXX) $(SAN_FLAGS) -fsanitize=address,undefined -fno-sanitize-recover=undefined $(SAN_SRC) -o $@ $(SAN_LIBS)
+
+tsan: build/tsan/engine_stress
+	TSAN_OPTIONS="halt_on_error=1 second_deadlock_stack=1" ./build/tsan/engine_stress 1500
+
+asan: build/asan/engine_stress
+	ASAN_OPTIONS="detect_leaks=1" ./build/asan/engine_stress 2000
+
+.PHONY: tsan asan

@@ -198,6 +198,7 @@ void Engine::start() {
                                            (size_t)cfg_.pinned_fetch_bytes);
   running_ = true;
   stopping_ = false;
+  workers_done_ = false;
   sources_done_ = false;
   sources_active_ = ns;
   dec_closed_ = false;
@@ -237,6 +238,7 @@ void Engine::stop() {
       workers_[i].detach();  // may be stuck on a dead device; its batches were re-queued
     }
   }
+  workers_done_ = true;  // (the watchdog polls this flag, never the vector being cleared)
   workers_.clear();
   for (auto& p : producers_) p->flush();
   sources_done_ = true;  // sources may now commit their final offsets
@@ -501,6 +503,7 @@ void Engine::worker_loop(ReplicaSlot* rs) {
         b->t_take_ns = mono_ns();
         for (const InRecord& r : b->recs) h_queue_us_.add((b->t_take_ns - r.t_fetch_ns) / 1000);
         const int64_t nb = ++batches_total_;
+        b->t_submit_ns = mono_ns();  // before publishing: the watchdog reads it under rs->mu
         {
           std::lock_guard<std::mutex> lk(rs->mu);
           rs->inflight.push_back(b);
@@ -509,7 +512,6 @@ void Engine::worker_loop(ReplicaSlot* rs) {
           if (crash_at_batch_ > 0 && nb == crash_at_batch_)
             throw std::runtime_error("injected replica crash (fault replica_crash@" +
                                      std::to_string(crash_at_batch_) + ")");
-          b->t_submit_ns = mono_ns();
           {
             trace::Range tr("gale:h2d+launch");
             rep.submit(*b);
@@ -550,7 +552,7 @@ void Engine::worker_loop(ReplicaSlot* rs) {
 }
 
 void Engine::watchdog_loop() {
-  while (running_ && !(stopping_ && workers_.empty())) {
+  while (running_ && !workers_done_) {
     std::this_thread::sleep_for(std::chrono::milliseconds(50));
     const int64_t now = mono_ns();
     for (auto& rs : replicas_) {

@@ -146,7 +146,8 @@ class Engine {
   std::deque<FetchItem> dec_q_;
   bool dec_closed_ = false;
   std::thread watchdog_;
-  std::atomic<bool> running_{false}, stopping_{false}, sources_done_{false};
+  std::atomic<bool> running_{false}, stopping_{false}, sources_done_{false},
+      workers_done_{false};
   std::atomic<int> sources_active_{0};
 
   std::mutex pend_mu_;

@@ -1,0 +1,214 @@
+// GpuReplica (see replica.h): staged JSON bytes -> GPU JSON parser -> hipGraph forward ->
+// softmax rows on the replica's own streams. Kept apart from the host-only replicas so the
+// sanitizer build of the host pipeline (make tsan / make asan) links no GPU code.
+#include <string.h>
+
+#include <algorithm>
+#include <stdexcept>
+
+#include "../codec/json_codec.h"
+#include "replica.h"
+
+namespace gale {
+
+// ---------------------------------------------------------------------------------------------
+// GpuReplica
+// ---------------------------------------------------------------------------------------------
+
+GpuReplica::GpuReplica(std::shared_ptr<Executor> exec, int H, int W, int C, int classes,
+                       bool use_graph)
+    : exec_(std::move(exec)), H_(H), W_(W), C_(C), classes_(classes), use_graph_(use_graph) {
+  if (exec_->input_bytes_per_image() != (long long)H * W * C * 4)
+    throw std::invalid_argument("GpuReplica: executor input is not fp32 [H, W, C]");
+  if (exec_->output_bytes_per_image() != (long long)classes * 4)
+    throw std::invalid_argument("GpuReplica: executor output is not fp32 [classes]");
+  check_hip(hipSetDevice(exec_->device()), "hipSetDevice");
+  check_hip(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "hipStreamCreate");
+  check_hip(hipStreamCreateWithFlags(&copy_stream_, hipStreamNonBlocking), "hipStreamCreate");
+  const int mb = exec_->max_batch();
+  slots_.resize((size_t)exec_->slots());
+  for (Slot& s : slots_) {
+    check_hip(hipHostMalloc(reinterpret_cast<void**>(&s.h_recs), sizeof(JsonRecord) * mb),
+              "hipHostMalloc(recs)");
+    check_hip(hipMalloc(reinterpret_cast<void**>(&s.d_recs), sizeof(JsonRecord) * mb),
+              "hipMalloc(recs)");
+    check_hip(hipHostMalloc(reinterpret_cast<void**>(&s.h_out), sizeof(float) * mb * classes),
+              "hipHostMalloc(out)");
+    check_hip(hipEventCreateWithFlags(&s.done, hipEventDisableTiming), "hipEventCreate");
+    check_hip(hipEventCreateWithFlags(&s.staged, hipEventDisableTiming), "hipEventCreate");
+    // initial text capacity: ~12 bytes per number (Java Float.toString + ",") x a full batch
+    ensure_device(s, (size_t)mb * H * W * C * 12 + 4096);
+    ensure_tiles(s, (int)(((size_t)mb * H * W * C * 12) / kJsonTileBytes) + 2 * mb);
+  }
+}
+
+GpuReplica::~GpuReplica() {
+  hipSetDevice(exec_->device());
+  if (stream_) hipStreamSynchronize(stream_);
+  for (Slot& s : slots_) {
+    if (s.h_bytes) hipHostFree(s.h_bytes);
+    if (s.d_bytes) hipFree(s.d_bytes);
+    if (s.h_recs) hipHostFree(s.h_recs);
+    if (s.d_recs) hipFree(s.d_recs);
+    if (s.d_tiles) hipFree(s.d_tiles);
+    if (s.h_out) hipHostFree(s.h_out);
+    if (s.done) hipEventDestroy(s.done);
+    if (s.staged) hipEventDestroy(s.staged);
+  }
+  if (copy_stream_) {
+    hipStreamSynchronize(copy_stream_);
+    hipStreamDestroy(copy_stream_);
+  }
+  if (stream_) hipStreamDestroy(stream_);
+}
+
+std::string GpuReplica::name() const { return "gpu" + std::to_string(exec_->device()); }
+
+void GpuReplica::ensure_host(Slot& s, size_t bytes) {
+  if (bytes <= s.h_cap) return;
+  const size_t cap = (std::max(bytes, s.h_cap * 2) + 4095) & ~(size_t)4095;
+  if (s.h_bytes) {
+    check_hip(hipEventSynchronize(s.done), "hipEventSynchronize");
+    hipHostFree(s.h_bytes);
+  }
+  check_hip(hipHostMalloc(reinterpret_cast<void**>(&s.h_bytes), cap), "hipHostMalloc(bytes)");
+  s.h_cap = cap;
+}
+
+void GpuReplica::ensure_tiles(Slot& s, int ntiles) {
+  if (ntiles <= s.tiles_cap) return;
+  const int cap = std::max(ntiles, s.tiles_cap * 2);
+  if (s.d_tiles) {
+    check_hip(hipEventSynchronize(s.done), "hipEventSynchronize");
+    hipFree(s.d_tiles);
+  }
+  check_hip(hipMalloc(reinterpret_cast<void**>(&s.d_tiles), sizeof(int) * cap),
+            "hipMalloc(tiles)");
+  s.tiles_cap = cap;
+}
+
+void GpuReplica::ensure_device(Slot& s, size_t bytes) {
+  if (bytes <= s.d_cap) return;
+  const size_t cap = (std::max(bytes, s.d_cap * 2) + 4095) & ~(size_t)4095;
+  if (s.d_bytes) {
+    check_hip(hipEventSynchronize(s.done), "hipEventSynchronize");
+    hipFree(s.d_bytes);
+  }
+  check_hip(hipMalloc(reinterpret_cast<void**>(&s.d_bytes), cap), "hipMalloc(bytes)");
+  s.d_cap = cap;
+}
+
+// Stage the batch's JSON text on the device. Records that arrived in pinned fetch buffers are
+// DMA'd straight from them: one hipMemcpyAsync per fetch buffer covering the records' span
+// (the few Kafka record-header bytes between values ride along); records in pageable memory are
+// first gathered into the slot's pinned staging buffer. Offsets keep their position modulo 16,
+// so the parser's aligned 16-byte loads see the same layout as on the host.
+void GpuReplica::submit(Batch& b) {
+  const int slot = next_slot_;
+  next_slot_ = (next_slot_ + 1) % (int)slots_.size();
+  b.slot = slot;
+  Slot& s = slots_[(size_t)slot];
+  struct Span {
+    const uint8_t* base;
+    size_t lo, hi;
+  };
+  std::vector<Span> spans;
+  size_t staged = 0;
+  for (const InRecord& r : b.recs) {
+    const uint8_t* base = r.buf.get();
+    const size_t lo = (size_t)(r.value + r.arr_off - base), hi = lo + (size_t)r.arr_len;
+    if (!r.pinned) {
+      staged += ((size_t)r.arr_len + 31) & ~(size_t)15;
+      continue;
+    }
+    Span* sp = nullptr;
+    for (Span& x : spans)
+      if (x.base == base) sp = &x;
+    if (!sp) {
+      spans.push_back({base, lo, hi});
+    } else {
+      sp->lo = std::min(sp->lo, lo);
+      sp->hi = std::max(sp->hi, hi);
+    }
+  }
+  size_t dev_total = 16 + staged;
+  for (Span& x : spans) {
+    x.lo &= ~(size_t)15;
+    dev_total += ((x.hi - x.lo) + 15) & ~(size_t)15;
+  }
+  ensure_device(s, dev_total + 16);
+  if (staged) ensure_host(s, staged + 16);
+  // device layout: [span 0][span 1]...[staged records]
+  std::vector<size_t> span_dev(spans.size());
+  size_t doff = 0;
+  for (size_t i = 0; i < spans.size(); ++i) {
+    span_dev[i] = doff;
+    check_hip(hipMemcpyAsync(s.d_bytes + doff, spans[i].base + spans[i].lo,
+                             spans[i].hi - spans[i].lo, hipMemcpyHostToDevice, copy_stream_),
+              "H2D span");
+    doff += ((spans[i].hi - spans[i].lo) + 15) & ~(size_t)15;
+  }
+  const size_t staged_dev = doff;
+  size_t hoff = 0;
+  int nrec = 0, img = 0, ntiles = 0;
+  for (const InRecord& r : b.recs) {
+    JsonRecord& jr = s.h_recs[nrec++];
+    const uint8_t* base = r.buf.get();
+    const size_t lo = (size_t)(r.value + r.arr_off - base);
+    if (r.pinned) {
+      size_t k = 0;
+      while (spans[k].base != base) ++k;
+      jr.off = (int64_t)(span_dev[k] + (lo - spans[k].lo));
+    } else {
+      hoff += (lo - hoff) & 15;  // keep the record's alignment modulo 16
+      memcpy(s.h_bytes + hoff, r.value + r.arr_off, (size_t)r.arr_len);
+      jr.off = (int64_t)(staged_dev + hoff);
+      hoff = (hoff + (size_t)r.arr_len + 15) & ~(size_t)15;
+    }
+    jr.len = (int32_t)r.arr_len;
+    jr.slot = img;
+    jr.images = r.images;
+    jr.status = 0;
+    jr.tile0 = ntiles;
+    jr.pad_ = 0;
+    ntiles += json_tile_count(jr.off, jr.len);
+    img += r.images;
+  }
+  if (img > exec_->max_batch()) throw std::logic_error("GpuReplica: batch exceeds max_batch");
+  b.images = img;
+  if (hoff)
+    check_hip(hipMemcpyAsync(s.d_bytes + staged_dev, s.h_bytes, hoff, hipMemcpyHostToDevice,
+                             copy_stream_),
+              "H2D staged");
+  check_hip(hipMemcpyAsync(s.d_recs, s.h_recs, sizeof(JsonRecord) * nrec, hipMemcpyHostToDevice,
+                           copy_stream_),
+            "H2D recs");
+  check_hip(hipEventRecord(s.staged, copy_stream_), "hipEventRecord(staged)");
+  check_hip(hipStreamWaitEvent(stream_, s.staged, 0), "hipStreamWaitEvent");
+  ensure_tiles(s, ntiles);
+  check_hip(json_parse_instances(nrec, ntiles, s.d_recs, s.d_bytes, H_, W_, C_, s.d_tiles,
+                                 static_cast<float*>(exec_->input(slot)), stream_),
+            "json_parse_instances");
+  exec_->run(slot, img, stream_, use_graph_);
+  check_hip(hipMemcpyAsync(s.h_out, exec_->output(slot), sizeof(float) * img * classes_,
+                           hipMemcpyDeviceToHost, stream_),
+            "D2H probs");
+  check_hip(hipMemcpyAsync(s.h_recs, s.d_recs, sizeof(JsonRecord) * nrec, hipMemcpyDeviceToHost,
+                           stream_),
+            "D2H status");
+  check_hip(hipEventRecord(s.done, stream_), "hipEventRecord");
+}
+
+void GpuReplica::wait(Batch& b) {
+  Slot& s = slots_[(size_t)b.slot];
+  check_hip(hipEventSynchronize(s.done), "hipEventSynchronize(batch)");
+  b.dev_status.assign(b.recs.size(), codec::OK);
+  for (size_t i = 0; i < b.recs.size(); ++i) {
+    const int st = s.h_recs[i].status;
+    if (st == 1 || st == 3) b.dev_status[i] = codec::BAD_SHAPE;
+    else if (st == 2) b.dev_status[i] = codec::BAD_NUMBER;
+  }
+  b.probs = s.h_out;
+}
+
+}  // namespace gale
