@@ -63,4 +63,5 @@ def test_bench_stub_torchrun_world2():
     assert len(lines) == 1  # rank 0 only
     r = lines[0]
     assert r["n_gpus"] == 2 and r["steps"] == 4 and r["value"] > 0
-    assert r["config"]["parallelism"] == "dp2" and r["config"]["global_batch"] == 64
+    # a step = one 32-image micro-batch per replica (4 per GPU by default), on both ranks
+    assert r["config"]["parallelism"] == "dp2" and r["config"]["global_batch"] == 32 * 4 * 2
