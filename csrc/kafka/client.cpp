@@ -602,6 +602,8 @@ Consumer::Consumer(ConsumerConfig cfg, BufferAlloc alloc)
     : cfg_(std::move(cfg)), alloc_(std::move(alloc)), cluster_(cfg_) {}
 
 void Consumer::assign(const std::string& topic, const std::vector<int>& partitions) {
+  drain();
+  ready_.clear();
   topic_ = topic;
   const int n = cluster_.partitions(topic);
   if (n < 0) throw KafkaError(UNKNOWN_TOPIC_OR_PARTITION, "unknown topic " + topic);
@@ -636,7 +638,11 @@ int64_t Consumer::list_offset(int partition, int64_t ts) {
   throw KafkaError(-1, "ListOffsets: partition missing from response");
 }
 
-void Consumer::seek(int partition, int64_t offset) { pos_[partition] = offset; }
+void Consumer::seek(int partition, int64_t offset) {
+  drain();
+  ready_.clear();  // nothing fetched before a seek may be returned after it
+  pos_[partition] = offset;
+}
 
 int64_t Consumer::position(int partition) const {
   auto it = pos_.find(partition);
@@ -644,6 +650,8 @@ int64_t Consumer::position(int partition) const {
 }
 
 void Consumer::seek_to(const std::string& where) {
+  drain();
+  ready_.clear();
   for (int p : parts_) {
     if (where == "latest") {
       pos_[p] = list_offset(p, kLatest);
@@ -658,10 +666,7 @@ void Consumer::seek_to(const std::string& where) {
   }
 }
 
-std::vector<Fetched> Consumer::poll() {
-  std::vector<Fetched> out;
-  for (int p : parts_)
-    if (!pos_.count(p)) pos_[p] = list_offset(p, cfg_.auto_offset_reset == "earliest" ? kEarliest : kLatest);
+void Consumer::send_fetches() {
   std::map<int32_t, std::vector<int>> by_leader;
   for (int p : parts_) {
     try {
@@ -671,7 +676,6 @@ std::vector<Fetched> Consumer::poll() {
     }
   }
   // issue every leader's fetch first (long polls run concurrently), then collect
-  std::vector<std::pair<int32_t, int32_t>> sent;  // node, corr
   for (auto& kv : by_leader) {
     FetchRequest req;
     req.max_wait_ms = cfg_.max_wait_ms;
@@ -679,21 +683,42 @@ std::vector<Fetched> Consumer::poll() {
     req.max_bytes = cfg_.fetch_max_bytes;
     FetchTopic ft;
     ft.name = topic_;
-    for (int p : kv.second) ft.partitions.push_back({p, pos_[p], cfg_.partition_max_bytes});
+    InFlight inf;
+    inf.node = kv.first;
+    for (int p : kv.second) {
+      ft.partitions.push_back({p, pos_[p], cfg_.partition_max_bytes});
+      inf.from[p] = pos_[p];
+    }
     req.topics.push_back(std::move(ft));
     Writer w;
     encode_fetch_request(w, req);
-    sent.push_back({kv.first, cluster_.node(kv.first).send(FETCH, w)});
+    inf.corr = cluster_.node(kv.first).send(FETCH, w);
+    inflight_.push_back(std::move(inf));
   }
+}
+
+void Consumer::collect(std::vector<Fetched>& out) {
+  std::vector<InFlight> infs;
+  infs.swap(inflight_);
   bool stale = false;
-  for (auto& s : sent) {
+  for (size_t i = 0; i < infs.size(); ++i) {
+    const InFlight& inf = infs[i];
     Fetched f;
     f.crc_checked = cfg_.check_crcs;
-    f.buf = cluster_.node(s.first).recv(s.second, &f.size, alloc_);
+    try {
+      f.buf = cluster_.node(inf.node).recv(inf.corr, &f.size, alloc_);
+    } catch (...) {
+      // these connections are mid-response: reconnect them, forget their in-flight fetches
+      for (size_t j = i; j < infs.size(); ++j) cluster_.drop(infs[j].node);
+      cluster_.invalidate();
+      throw;
+    }
     Reader r(f.buf.get(), f.size);
     const FetchResponse m = decode_fetch_response(r);
     for (auto& t : m.topics)
       for (auto& p : t.partitions) {
+        auto it = inf.from.find(p.index);
+        if (it == inf.from.end() || pos_[p.index] != it->second) continue;  // seeked meanwhile
         if (p.error == OFFSET_OUT_OF_RANGE) {
           pos_[p.index] = list_offset(p.index, cfg_.auto_offset_reset == "earliest" ? kEarliest : kLatest);
           continue;
@@ -707,18 +732,37 @@ std::vector<Fetched> Consumer::poll() {
         const size_t before = f.records.size();
         decode_records(f.buf.get(), p.records_off, (size_t)p.records_len, pos_[p.index],
                        cfg_.check_crcs, f.records, &f.batches);
-        for (size_t i = before; i < f.records.size(); ++i) f.records[i].partition = p.index;
+        for (size_t k = before; k < f.records.size(); ++k) f.records[k].partition = p.index;
         if (f.records.size() > before) pos_[p.index] = f.records.back().offset + 1;
       }
     if (!f.records.empty()) out.push_back(std::move(f));
   }
   if (stale) cluster_.invalidate();
+}
+
+void Consumer::drain() {
+  if (!inflight_.empty()) collect(ready_);
+}
+
+std::vector<Fetched> Consumer::poll() {
+  std::vector<Fetched> out;
+  out.swap(ready_);
+  if (!out.empty()) {  // responses drained by an earlier commit
+    if (cfg_.prefetch && inflight_.empty()) send_fetches();
+    return out;
+  }
+  for (int p : parts_)
+    if (!pos_.count(p)) pos_[p] = list_offset(p, cfg_.auto_offset_reset == "earliest" ? kEarliest : kLatest);
+  if (inflight_.empty()) send_fetches();
+  collect(out);
+  if (cfg_.prefetch) send_fetches();
   return out;
 }
 
 void Consumer::commit(const std::map<int, int64_t>& offsets) {
   if (cfg_.group_id.empty()) throw std::invalid_argument("commit needs a group_id");
   if (offsets.empty()) return;
+  drain();  // the coordinator may share a connection with an in-flight fetch
   OffsetCommitRequest req;
   req.group_id = cfg_.group_id;
   CommitTopic t;
@@ -740,6 +784,7 @@ void Consumer::commit(const std::map<int, int64_t>& offsets) {
 }
 
 int64_t Consumer::committed(int partition) {
+  drain();
   OffsetFetchRequest req;
   req.group_id = cfg_.group_id;
   CommitTopic t;

@@ -87,6 +87,9 @@ class Cluster {
   Connection& coordinator(const std::string& group);
   std::vector<BrokerNode> brokers() const;
   void invalidate() { topics_.clear(); }
+  // Close a node's connection (after a failed/timed-out exchange left it mid-response); the
+  // next node() call reconnects.
+  void drop(int32_t node_id) { conns_.erase(node_id); }
 
  private:
   void check_versions(Connection& c);
@@ -183,6 +186,9 @@ struct ConsumerConfig : ClientConfig {
   int partition_max_bytes = 16 << 20;
   bool check_crcs = true;
   std::string auto_offset_reset = "latest";  // on OFFSET_OUT_OF_RANGE / no committed offset
+  // keep the next fetch of every leader in flight while the application processes the previous
+  // response (the Java consumer's fetcher does the same): the broker's send overlaps our work
+  bool prefetch = true;
 };
 
 // One fetch round: records point into `buf` (the response body).
@@ -205,7 +211,7 @@ class Consumer {
   void seek(int partition, int64_t offset);
   int64_t position(int partition) const;
   // One fetch round over all assigned partitions (grouped by leader). Empty when nothing arrived
-  // within max_wait_ms.
+  // within max_wait_ms. With prefetch the next round is already requested when this returns.
   std::vector<Fetched> poll();
   void commit(const std::map<int, int64_t>& offsets);  // next offset to read, per partition
   int64_t committed(int partition);
@@ -214,12 +220,22 @@ class Consumer {
 
  private:
   int64_t list_offset(int partition, int64_t ts);
+  struct InFlight {
+    int32_t node, corr;
+    std::map<int, int64_t> from;  // partition -> offset the fetch was issued at
+  };
+  void send_fetches();
+  // receive every in-flight response; records at a position that moved meanwhile are dropped
+  void collect(std::vector<Fetched>& out);
+  void drain();  // collect into ready_ (before any other request on a fetch connection)
   ConsumerConfig cfg_;
   BufferAlloc alloc_;
   Cluster cluster_;
   std::string topic_;
   std::vector<int> parts_;
   std::map<int, int64_t> pos_, hw_;
+  std::vector<InFlight> inflight_;
+  std::vector<Fetched> ready_;  // drained responses not yet returned by poll()
 };
 
 }  // namespace kafka
