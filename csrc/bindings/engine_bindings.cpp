@@ -91,6 +91,12 @@ void bind_engine(py::module_& m) {
              return e.wait(timeout_ms);
            },
            py::arg("timeout_ms") = -1)
+      .def("wait_completed",
+           [](Engine& e, int64_t n, int64_t timeout_ms) {
+             py::gil_scoped_release nogil;
+             return e.wait_completed(n, timeout_ms);
+           },
+           py::arg("n"), py::arg("timeout_ms") = -1)
       .def_property_readonly("running", &Engine::running)
       .def_property_readonly("completed", &Engine::completed)
       .def("stats", &Engine::stats)

@@ -622,10 +622,21 @@ void Engine::complete_record(const InRecord& r, bool ok) {
   }
   t_last_ns_ = now;
   const int64_t c = ++completed_;
-  if (cfg_.max_records > 0 && c >= cfg_.max_records) {
+  const int64_t target = wait_target_.load(std::memory_order_relaxed);
+  if ((cfg_.max_records > 0 && c >= cfg_.max_records) || (target > 0 && c >= target)) {
     std::lock_guard<std::mutex> lk(done_mu_);
     done_cv_.notify_all();
   }
+}
+
+bool Engine::wait_completed(int64_t n, int64_t timeout_ms) {
+  wait_target_ = n;
+  std::unique_lock<std::mutex> lk(done_mu_);
+  auto pred = [&] { return !running_ || stopping_ || completed_.load() >= n; };
+  if (timeout_ms < 0) done_cv_.wait(lk, pred);
+  else done_cv_.wait_for(lk, std::chrono::milliseconds(timeout_ms), pred);
+  wait_target_ = 0;
+  return completed_.load() >= n;
 }
 
 void Engine::emit(InRecord& r, std::string value, bool null_value, kafka::Producer* prod) {

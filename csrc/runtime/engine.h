@@ -103,6 +103,9 @@ class Engine {
   // Block until max_records completed, stop() was called, or timeout (ms; <0 = forever).
   // Returns true when the record target was reached.
   bool wait(int64_t timeout_ms);
+  // Block (without stopping anything) until at least n records completed; false on timeout or
+  // when the engine stopped first.
+  bool wait_completed(int64_t n, int64_t timeout_ms);
   bool running() const { return running_; }
   int64_t completed() const { return completed_.load(); }
 
@@ -157,6 +160,7 @@ class Engine {
   std::mutex done_mu_;
   std::condition_variable done_cv_;
   std::atomic<int64_t> completed_{0};
+  std::atomic<int64_t> wait_target_{0};
 
   // fault injection
   int64_t crash_at_batch_ = -1;

@@ -97,6 +97,10 @@ class Engine:
     def wait(self, timeout_s: Optional[float] = None) -> bool:
         return self._native.wait(-1 if timeout_s is None else int(timeout_s * 1000))
 
+    def wait_completed(self, n: int, timeout_s: Optional[float] = None) -> bool:
+        """Block until >= n records completed (the engine keeps running)."""
+        return self._native.wait_completed(n, -1 if timeout_s is None else int(timeout_s * 1000))
+
     @property
     def running(self) -> bool:
         return self._native.running
