@@ -75,6 +75,7 @@ gale::PlanOp op_from_dict(const py::dict& d) {
   op.wscale = static_cast<const float*>(P(get_or<uintptr_t>(d, "wscale", 0)));
   if (d.contains("ptrs"))
     for (auto v : d["ptrs"].cast<std::vector<uintptr_t>>()) op.ptrs.push_back(P(v));
+  if (d.contains("scales")) op.scales = d["scales"].cast<std::vector<float>>();
   op.fp8 = get_or<int>(d, "fp8", 0);
   op.scale = get_or<float>(d, "scale", 1.0f);
   return op;

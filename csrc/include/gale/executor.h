@@ -25,6 +25,7 @@ enum OpKind : int {
   OP_HEAD = 3,      // p[0] = HW, p[1] = C, p[2] = N   (pool + dense(fp32 w) + softmax)
   OP_SOFTMAX = 4,   // p[0] = N, p[1] = ld
   OP_RESNET20 = 5,  // whole-network fused CIFAR ResNet-20; ptrs = 19 w, 19 b, fc_w, fc_b
+                    // (+ 19 wscale for fp8), scales = 19 s_in, 19 s_out, 19 s_res (fp8)
 };
 
 // Buffer ids: 0 = network input (fp32 NHWC), 1 = network output (fp32 [B, classes]),
@@ -38,6 +39,7 @@ struct PlanOp {
   const float* bias = nullptr;
   const float* wscale = nullptr;
   std::vector<const void*> ptrs;  // OP_RESNET20 parameter pointers
+  std::vector<float> scales;      // OP_RESNET20 fp8 activation scales
   int fp8 = 0;        // pool / head ops: e4m3 activations
   float scale = 1.f;  // head: input activation scale (fp8)
 };

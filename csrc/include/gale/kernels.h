@@ -61,12 +61,17 @@ hipError_t head_pool_dense_softmax(int batch, int HW, int C, int N, const void* 
 
 // Whole-network CIFAR-10 ResNet-20 (csrc/kernels/resnet20_fused.hip): x fp32 [B,32,32,3] ->
 // softmax fp32 [B,10], one workgroup per image with every activation in LDS. w/b: the 19 convs
-// in network order (packed bf16 [Npad][Kpad] + folded-BN fp32 bias), fc_w fp32 [10][64].
+// in network order (packed [Npad][Kpad] + folded-BN fp32 bias), fc_w fp32 [10][64].
+// fp8: w are e4m3 codes with per-channel scales ws; s_in / s_out / s_res are the per-tensor
+// activation scales of each conv's input / output / residual (s_in[0] quantises the input).
 struct ResNet20Params {
-  const void* w[19];  // bf16
+  const void* w[19];  // bf16 or e4m3
   const float* b[19];
   const float* fc_w;
   const float* fc_b;
+  int fp8;
+  const float* ws[19];
+  float s_in[19], s_out[19], s_res[19];
 };
 hipError_t resnet20_fused_forward(const ResNet20Params& p, int batch, const float* x, float* out,
                                   hipStream_t stream);

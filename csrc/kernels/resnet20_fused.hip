@@ -1,49 +1,131 @@
 // Whole-network CIFAR-10 ResNet-20 forward in ONE kernel: a workgroup carries an image through
 // all 19 convolutions, the residual adds, the global pool, the dense layer and the softmax with
-// every activation resident in LDS (BASELINE config 2/3 flagship; SURVEY.md §7.5 hard part 3:
+// every activation resident in LDS (BASELINE configs 2/3/5; SURVEY.md §7.5 hard part 3:
 // "consider whole-block or whole-network fusion (persistent kernel)").
 //
 // Why: per-layer kernels at serving batch sizes (64-256 images) are latency bound — ~20 launches,
 // each re-reading its input through L2 with a 9x implicit-im2col amplification and exposing a
 // global-memory latency per K step. Here the only HBM traffic per image is its 12 KB fp32 input
-// and 40 B of softmax output; weights (540 KB bf16) stream from L2 as MFMA A fragments.
+// and 40 B of softmax output; weights (540 KB bf16 / 270 KB e4m3) stream from L2 as MFMA A
+// fragments.
 //
-// LDS plan (78,464 B per workgroup -> 2 workgroups per CU), bf16 NHWC with a zero border so the
-// 3x3 windows need no bounds checks (padded layouts Hp x Wp x C):
-//   R0 [0, 36992)        X1 34x34x16 (stage-1 block input/output)  | stage 3: T3, X3 10x10x64
-//   R1 [36992, 78464)    IN 34x34x3 (stem input) -> T1 34x34x16     | stage 2: T2, X2 18x18x32
+// Two instantiations:
+//   bf16: v_mfma_f32_16x16x32_bf16, activations bf16 in LDS (78,464 B -> 2 workgroups per CU)
+//   fp8 : v_mfma_f32_16x16x32_fp8_fp8, OCP e4m3 weights (per-channel scale) and activations
+//         (per-tensor scales calibrated offline, gale/models/quant.py) -> 39,232 B of LDS
+//         (half the bytes per B fragment). Epilogue: acc*wscale[c]*s_in + bias + res*s_res, ReLU,
+//         requantise with 1/s_out (saturating at +-448).
+// LDS plan (element offsets scale with the element size EB), NHWC with a zero border so the 3x3
+// windows need no bounds checks (padded layouts Hp x Wp x C):
+//   R0 [0, 18496 EB)          X1 34x34x16 (stage-1 block input/output)  | stage 3: T3, X3 10x10x64
+//   R1 [18496, 39232 EB)      IN 34x34x3 (stem input) -> T1 34x34x16    | stage 2: T2, X2 18x18x32
 // Block conv2 writes its output in place over its residual (each lane reads the residual of the
 // pixel/channels it then writes, and no other lane reads that buffer in the same conv).
 //
-// MFMA mapping (v_mfma_f32_16x16x32_bf16, same orientation as conv_mfma.hip): D[channel][pixel];
-// A = weights [Cout][Kpad] from global (k = (kh*3 + kw)*Cin + ci), hoisted into registers once
-// per conv (each wave owns one 16-channel tile); B = 8 consecutive input channels of one tap of
-// one pixel = one ds_read_b128 from the padded LDS image. Each wave walks its pixel tiles four
-// at a time (four independent accumulators).
+// MFMA mapping (same orientation as conv_mfma.hip): D[channel][pixel]; A = weights [Cout][Kpad]
+// from global (k = (kh*3 + kw)*Cin + ci), hoisted into registers once per conv (each wave owns
+// one 16-channel tile); B = 8 consecutive input channels of one tap of one pixel = one
+// ds_read_b128 (bf16) / ds_read_b64 (fp8) from the padded LDS image. Each wave walks its pixel
+// tiles four at a time (four independent accumulators).
 //
 // Reference parity: the model the reference serves is an opaque SavedModel fetched as
 // "output/Softmax:0" (InferenceBolt.java:81-86); numerics equal the layer-by-layer gale plan
-// (same bf16 rounding points) and are checked against the fp32 oracle in tests.
+// (same rounding points) and are checked against the fp32 / fp8-emulation oracles in tests.
 #include "common.cuh"
 #include "gale/kernels.h"
 
 namespace gale {
 namespace {
 
+// element offsets (multiply by EB for bytes)
 constexpr int kR0 = 0;
-constexpr int kR1 = 36992;
-constexpr int kLds = 78464;
-constexpr int kT2 = kR1, kX2 = kR1 + 20736;
-constexpr int kT3 = kR0, kX3 = kR0 + 12800;
+constexpr int kR1 = 18496;           // 34*34*16
+constexpr int kElems = 39232;        // kR1 + 2*18*18*32
+constexpr int kT2 = kR1, kX2 = kR1 + 10368;
+constexpr int kT3 = kR0, kX3 = kR0 + 6400;
 
-__device__ __forceinline__ bf16* lds_at(char* smem, int byte_off) {
-  return reinterpret_cast<bf16*>(smem + byte_off);
+template <bool F8>
+struct Ty;
+template <>
+struct Ty<false> {
+  typedef bf16 elem;
+  typedef bf16x8 frag;
+  static constexpr int EB = 2;
+  static __device__ __forceinline__ frag ld(const elem* p) { return ld_bf16x8(p); }
+  static __device__ __forceinline__ f32x4 mma(frag a, frag b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+  }
+  static __device__ __forceinline__ void load4(const elem* p, float s, float* v) {
+    const bf16x4 r = __builtin_bit_cast(bf16x4, *reinterpret_cast<const uint2*>(p));
+    v[0] = (float)r[0]; v[1] = (float)r[1]; v[2] = (float)r[2]; v[3] = (float)r[3];
+    (void)s;
+  }
+  static __device__ __forceinline__ void store4(elem* p, float q, float a, float b, float c,
+                                                float d) {
+    (void)q;
+    bf16x4 o;
+    o[0] = (bf16)a; o[1] = (bf16)b; o[2] = (bf16)c; o[3] = (bf16)d;
+    *reinterpret_cast<uint2*>(p) = __builtin_bit_cast(uint2, o);
+  }
+  static __device__ __forceinline__ elem from_f32(float v, float q) {
+    (void)q;
+    return (bf16)v;
+  }
+  static __device__ __forceinline__ float to_f32(elem e) { return (float)e; }
+  static __device__ __forceinline__ elem zero() { return (bf16)0.f; }
+};
+template <>
+struct Ty<true> {
+  typedef uint8_t elem;
+  typedef long frag;
+  static constexpr int EB = 1;
+  static __device__ __forceinline__ frag ld(const elem* p) {
+    return *reinterpret_cast<const long*>(p);
+  }
+  static __device__ __forceinline__ f32x4 mma(frag a, frag b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(a, b, c, 0, 0, 0);
+  }
+  static __device__ __forceinline__ void load4(const elem* p, float s, float* v) {
+    const int r = *reinterpret_cast<const int*>(p);
+    v[0] = __builtin_amdgcn_cvt_f32_fp8(r, 0) * s;
+    v[1] = __builtin_amdgcn_cvt_f32_fp8(r, 1) * s;
+    v[2] = __builtin_amdgcn_cvt_f32_fp8(r, 2) * s;
+    v[3] = __builtin_amdgcn_cvt_f32_fp8(r, 3) * s;
+  }
+  static __device__ __forceinline__ float sat(float v) { return fminf(fmaxf(v, -448.f), 448.f); }
+  static __device__ __forceinline__ void store4(elem* p, float q, float a, float b, float c,
+                                                float d) {
+    int w = __builtin_amdgcn_cvt_pk_fp8_f32(sat(a * q), sat(b * q), 0, false);
+    w = __builtin_amdgcn_cvt_pk_fp8_f32(sat(c * q), sat(d * q), w, true);
+    *reinterpret_cast<int*>(p) = w;
+  }
+  static __device__ __forceinline__ elem from_f32(float v, float q) {
+    return (elem)(__builtin_amdgcn_cvt_pk_fp8_f32(sat(v * q), 0.f, 0, false) & 0xff);
+  }
+  static __device__ __forceinline__ float to_f32(elem e) {
+    return __builtin_amdgcn_cvt_f32_fp8((int)e, 0);
+  }
+  static __device__ __forceinline__ elem zero() { return 0; }
+};
+
+// per-conv quantisation constants (fp8; identity for bf16)
+struct Q {
+  float deq;    // s_in (acc * wscale[c] * deq)
+  float qout;   // 1 / s_out
+  float res;    // s_res
+};
+
+template <bool F8>
+__device__ __forceinline__ Q conv_q(const ResNet20Params& p, int i) {
+  if constexpr (F8) return Q{p.s_in[i], 1.f / p.s_out[i], p.s_res[i]};
+  (void)p; (void)i;
+  return Q{1.f, 1.f, 1.f};
 }
 
-// zero the one-pixel border of a padded Hp x Wp x C bf16 image (C % 8 == 0)
-template <int HP, int WP, int C>
-__device__ __forceinline__ void zero_border(bf16* buf) {
-  constexpr int V = C / 8;  // 16-byte vectors per cell
+// zero the one-pixel border of a padded Hp x Wp x C image (C * EB % 16 == 0)
+template <bool F8, int HP, int WP, int C>
+__device__ __forceinline__ void zero_border(typename Ty<F8>::elem* buf) {
+  constexpr int V = C * Ty<F8>::EB / 16;  // 16-byte vectors per cell
   constexpr int CELLS = 2 * WP + 2 * (HP - 2);
   for (int i = threadIdx.x; i < CELLS * V; i += 256) {
     const int cell = i / V, v = i - cell * V;
@@ -51,16 +133,23 @@ __device__ __forceinline__ void zero_border(bf16* buf) {
     if (cell < WP) { h = 0; w = cell; }
     else if (cell < 2 * WP) { h = HP - 1; w = cell - WP; }
     else { const int r = cell - 2 * WP; h = 1 + (r >> 1); w = (r & 1) ? WP - 1 : 0; }
-    *reinterpret_cast<uint4*>(buf + (h * WP + w) * C + v * 8) = make_uint4(0, 0, 0, 0);
+    *reinterpret_cast<uint4*>(reinterpret_cast<char*>(buf + (h * WP + w) * C) + v * 16) =
+        make_uint4(0, 0, 0, 0);
   }
 }
 
 // 3x3 pad-1 convolution LDS -> LDS with the folded-BN bias, optional residual and ReLU.
 // RES: 0 none, 1 identity (same layout as out), 2 option-A shortcut from the previous stage's
 // buffer (stride-2 subsample, channels >= RC are zero).
-template <int CIN, int COUT, int S, int HO, int RES, int RC>
-__device__ __forceinline__ void conv3x3(const bf16* __restrict__ wg, const float* __restrict__ bias,
-                                        const bf16* in, bf16* out, const bf16* res) {
+template <bool F8, int CIN, int COUT, int S, int HO, int RES, int RC>
+__device__ __forceinline__ void conv3x3(const void* wgv, const float* __restrict__ wscale,
+                                        const float* __restrict__ bias, Q q,
+                                        const typename Ty<F8>::elem* in,
+                                        typename Ty<F8>::elem* out,
+                                        const typename Ty<F8>::elem* res) {
+  typedef Ty<F8> T;
+  typedef typename T::elem elem;
+  const elem* wg = static_cast<const elem*>(wgv);
   constexpr int WPI = HO * S + 2;  // padded input width
   constexpr int WPO = HO + 2;      // padded output width
   constexpr int RWP = 2 * HO + 2;  // padded width of an option-A residual source
@@ -77,12 +166,12 @@ __device__ __forceinline__ void conv3x3(const bf16* __restrict__ wg, const float
   const int ct = wave / WPC;
   const int pt0 = (wave % WPC) * PTW;
 
-  bf16x8 afr[KS];
+  typename T::frag afr[KS];
   int koff[KS];
 #pragma unroll
   for (int ks = 0; ks < KS; ++ks) {
     const int k = ks * 32 + g * 8;
-    afr[ks] = ld_bf16x8(wg + (ct * 16 + col) * KPAD + k);
+    afr[ks] = T::ld(wg + (ct * 16 + col) * KPAD + k);
     int tap = k / CIN;
     const int ci = k - tap * CIN;
     if (tap >= 9) tap = 0;  // K padding: zero weights, any finite input
@@ -90,6 +179,11 @@ __device__ __forceinline__ void conv3x3(const bf16* __restrict__ wg, const float
   }
   const int c0 = ct * 16 + g * 4;  // this lane's 4 output channels
   const float4 bv = *reinterpret_cast<const float4*>(bias + c0);
+  float4 sc = make_float4(1.f, 1.f, 1.f, 1.f);
+  if constexpr (F8) {
+    sc = *reinterpret_cast<const float4*>(wscale + c0);
+    sc.x *= q.deq; sc.y *= q.deq; sc.z *= q.deq; sc.w *= q.deq;
+  }
 
 #pragma unroll 1
   for (int pg = 0; pg < PTW; pg += 4) {
@@ -106,43 +200,43 @@ __device__ __forceinline__ void conv3x3(const bf16* __restrict__ wg, const float
     for (int p = 0; p < 4; ++p) acc[p] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
-      bf16x8 b[4];
+      typename T::frag b[4];
 #pragma unroll
-      for (int p = 0; p < 4; ++p) b[p] = ld_bf16x8(in + pbase[p] + koff[ks]);
+      for (int p = 0; p < 4; ++p) b[p] = T::ld(in + pbase[p] + koff[ks]);
 #pragma unroll
-      for (int p = 0; p < 4; ++p)
-        acc[p] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[ks], b[p], acc[p], 0, 0, 0);
+      for (int p = 0; p < 4; ++p) acc[p] = T::mma(afr[ks], b[p], acc[p]);
+      // bound how far the scheduler hoists LDS reads (register pressure -> occupancy)
+      if (ks % 3 == 2) __builtin_amdgcn_sched_barrier(0);
     }
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
-      float v0 = acc[p][0] + bv.x, v1 = acc[p][1] + bv.y;
-      float v2 = acc[p][2] + bv.z, v3 = acc[p][3] + bv.w;
+      float v0 = acc[p][0] * sc.x + bv.x, v1 = acc[p][1] * sc.y + bv.y;
+      float v2 = acc[p][2] * sc.z + bv.z, v3 = acc[p][3] * sc.w + bv.w;
       const int o = ((ho[p] + 1) * WPO + wo[p] + 1) * COUT + c0;
-      if (RES == 1) {
-        const bf16x4 r = __builtin_bit_cast(bf16x4, *reinterpret_cast<const uint2*>(res + o));
-        v0 += (float)r[0]; v1 += (float)r[1]; v2 += (float)r[2]; v3 += (float)r[3];
-      } else if (RES == 2) {
-        if (c0 < RC) {
-          const int ro = ((2 * ho[p] + 1) * RWP + 2 * wo[p] + 1) * RC + c0;
-          const bf16x4 r = __builtin_bit_cast(bf16x4, *reinterpret_cast<const uint2*>(res + ro));
-          v0 += (float)r[0]; v1 += (float)r[1]; v2 += (float)r[2]; v3 += (float)r[3];
-        }
+      if (RES == 1 || (RES == 2 && c0 < RC)) {
+        const int ro = RES == 1 ? o : ((2 * ho[p] + 1) * RWP + 2 * wo[p] + 1) * RC + c0;
+        float r[4];
+        T::load4(res + ro, q.res, r);
+        v0 += r[0]; v1 += r[1]; v2 += r[2]; v3 += r[3];
       }
-      bf16x4 ov;
-      ov[0] = (bf16)fmaxf(v0, 0.f); ov[1] = (bf16)fmaxf(v1, 0.f);
-      ov[2] = (bf16)fmaxf(v2, 0.f); ov[3] = (bf16)fmaxf(v3, 0.f);
-      *reinterpret_cast<uint2*>(out + o) = __builtin_bit_cast(uint2, ov);
+      T::store4(out + o, q.qout, fmaxf(v0, 0.f), fmaxf(v1, 0.f), fmaxf(v2, 0.f), fmaxf(v3, 0.f));
     }
   }
 }
 
 // stem: 3x3x3 -> 16 over the 34x34x3 padded input (K = 27 padded to 32: one k step, the 8
 // k-values of a lane are 8 scalar LDS reads)
-__device__ __forceinline__ void stem(const bf16* __restrict__ wg, const float* __restrict__ bias,
-                                     const bf16* in, bf16* out) {
+template <bool F8>
+__device__ __forceinline__ void stem(const void* wgv, const float* __restrict__ wscale,
+                                     const float* __restrict__ bias, Q q,
+                                     const typename Ty<F8>::elem* in,
+                                     typename Ty<F8>::elem* out) {
+  typedef Ty<F8> T;
+  typedef typename T::elem elem;
+  const elem* wg = static_cast<const elem*>(wgv);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int g = lane >> 4, col = lane & 15;
-  const bf16x8 a = ld_bf16x8(wg + col * 32 + g * 8);
+  const typename T::frag a = T::ld(wg + col * 32 + g * 8);
   int off[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
@@ -151,6 +245,11 @@ __device__ __forceinline__ void stem(const bf16* __restrict__ wg, const float* _
     off[j] = ((tap / 3) * 34 + tap % 3) * 3 + ci;
   }
   const float4 bv = *reinterpret_cast<const float4*>(bias + g * 4);
+  float4 sc = make_float4(1.f, 1.f, 1.f, 1.f);
+  if constexpr (F8) {
+    sc = *reinterpret_cast<const float4*>(wscale + g * 4);
+    sc.x *= q.deq; sc.y *= q.deq; sc.z *= q.deq; sc.w *= q.deq;
+  }
 #pragma unroll 1
   for (int pg = 0; pg < 16; pg += 4) {
     f32x4 acc[4];
@@ -160,44 +259,54 @@ __device__ __forceinline__ void stem(const bf16* __restrict__ wg, const float* _
       const int m = (wave * 16 + pg + p) * 16 + col;
       ho[p] = m >> 5;
       wo[p] = m & 31;
-      const bf16* px = in + (ho[p] * 34 + wo[p]) * 3;
-      bf16x8 b;
+      const elem* px = in + (ho[p] * 34 + wo[p]) * 3;
+      typename T::frag b;
+      if constexpr (F8) {
+        uint64_t v = 0;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) b[j] = px[off[j]];
-      acc[p] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+        for (int j = 0; j < 8; ++j) v |= (uint64_t)px[off[j]] << (8 * j);
+        b = (long)v;
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) b[j] = px[off[j]];
+      }
+      acc[p] = T::mma(a, b, f32x4{0.f, 0.f, 0.f, 0.f});
     }
 #pragma unroll
-    for (int p = 0; p < 4; ++p) {
-      bf16x4 ov;
-      ov[0] = (bf16)fmaxf(acc[p][0] + bv.x, 0.f); ov[1] = (bf16)fmaxf(acc[p][1] + bv.y, 0.f);
-      ov[2] = (bf16)fmaxf(acc[p][2] + bv.z, 0.f); ov[3] = (bf16)fmaxf(acc[p][3] + bv.w, 0.f);
-      *reinterpret_cast<uint2*>(out + ((ho[p] + 1) * 34 + wo[p] + 1) * 16 + g * 4) =
-          __builtin_bit_cast(uint2, ov);
-    }
+    for (int p = 0; p < 4; ++p)
+      T::store4(out + ((ho[p] + 1) * 34 + wo[p] + 1) * 16 + g * 4, q.qout,
+                fmaxf(acc[p][0] * sc.x + bv.x, 0.f), fmaxf(acc[p][1] * sc.y + bv.y, 0.f),
+                fmaxf(acc[p][2] * sc.z + bv.z, 0.f), fmaxf(acc[p][3] * sc.w + bv.w, 0.f));
   }
 }
 
-__global__ __launch_bounds__(256, 2) void resnet20_fused_kernel(ResNet20Params p, const float* x,
-                                                                float* out, int batch) {
+template <bool F8>
+__global__ __launch_bounds__(256, 2) void resnet20_fused_kernel(ResNet20Params p,
+                                                                         const float* x,
+                                                                         float* out, int batch) {
+  typedef Ty<F8> T;
+  typedef typename T::elem elem;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  bf16* X1 = lds_at(smem, kR0);
-  bf16* T1 = lds_at(smem, kR1);
-  bf16* IN = lds_at(smem, kR1);
-  bf16* T2 = lds_at(smem, kT2);
-  bf16* X2 = lds_at(smem, kX2);
-  bf16* T3 = lds_at(smem, kT3);
-  bf16* X3 = lds_at(smem, kX3);
-  float* scratch = reinterpret_cast<float*>(smem + kR1);
+  elem* base = reinterpret_cast<elem*>(smem);
+  elem* X1 = base + kR0;
+  elem* T1 = base + kR1;
+  elem* IN = base + kR1;
+  elem* T2 = base + kT2;
+  elem* X2 = base + kX2;
+  elem* T3 = base + kT3;
+  elem* X3 = base + kX3;
+  float* scratch = reinterpret_cast<float*>(base + kR1);
+  const float in_q = F8 ? 1.f / p.s_in[0] : 1.f;  // quantisation of the fp32 network input
 
   for (int img = blockIdx.x; img < batch; img += gridDim.x) {
     __syncthreads();  // the previous image's head is done with R0/R1
-    // ---- stage the fp32 input image as bf16 into the zero-bordered 34x34x3 IN ----
+    // ---- stage the fp32 input image into the zero-bordered 34x34x3 IN ----
     for (int i = threadIdx.x; i < 34 * 34 * 3; i += 256) {
       const int cell = i / 3;
       const int h = cell / 34, w = cell - h * 34;
-      if (h == 0 || h == 33 || w == 0 || w == 33) IN[i] = (bf16)0.f;
+      if (h == 0 || h == 33 || w == 0 || w == 33) IN[i] = T::zero();
     }
-    zero_border<34, 34, 16>(X1);
+    zero_border<F8, 34, 34, 16>(X1);
     const float4* xi = reinterpret_cast<const float4*>(x + (size_t)img * 3072);
     for (int i = threadIdx.x; i < 768; i += 256) {
       const float4 v = xi[i];
@@ -207,66 +316,77 @@ __global__ __launch_bounds__(256, 2) void resnet20_fused_kernel(ResNet20Params p
         const int idx = i * 4 + j;  // (h*32 + w)*3 + c
         const int pix = idx / 3, c = idx - pix * 3;
         const int h = pix >> 5, w = pix & 31;
-        IN[((h + 1) * 34 + w + 1) * 3 + c] = (bf16)e[j];
+        IN[((h + 1) * 34 + w + 1) * 3 + c] = T::from_f32(e[j], in_q);
       }
     }
     __syncthreads();
-    stem(static_cast<const bf16*>(p.w[0]), p.b[0], IN, X1);
+    stem<F8>(p.w[0], p.ws[0], p.b[0], conv_q<F8>(p, 0), IN, X1);
     __syncthreads();
-    zero_border<34, 34, 16>(T1);  // IN is dead; T1's border overlaps its bytes
+    zero_border<F8, 34, 34, 16>(T1);  // IN is dead; T1's border overlaps its bytes
     // ---- stage 1: 32x32x16 ----
 #pragma unroll 1
     for (int blk = 0; blk < 3; ++blk) {
-      conv3x3<16, 16, 1, 32, 0, 16>(static_cast<const bf16*>(p.w[1 + 2 * blk]), p.b[1 + 2 * blk], X1, T1, nullptr);
+      const int c1 = 1 + 2 * blk, c2 = c1 + 1;
+      conv3x3<F8, 16, 16, 1, 32, 0, 16>(p.w[c1], p.ws[c1], p.b[c1], conv_q<F8>(p, c1), X1, T1,
+                                        nullptr);
       __syncthreads();
-      conv3x3<16, 16, 1, 32, 1, 16>(static_cast<const bf16*>(p.w[2 + 2 * blk]), p.b[2 + 2 * blk], T1, X1, X1);
+      conv3x3<F8, 16, 16, 1, 32, 1, 16>(p.w[c2], p.ws[c2], p.b[c2], conv_q<F8>(p, c2), T1, X1,
+                                        X1);
       __syncthreads();
     }
     // ---- stage 2: 16x16x32 ----
-    zero_border<18, 18, 32>(T2);
-    zero_border<18, 18, 32>(X2);
-    conv3x3<16, 32, 2, 16, 0, 16>(static_cast<const bf16*>(p.w[7]), p.b[7], X1, T2, nullptr);
+    zero_border<F8, 18, 18, 32>(T2);
+    zero_border<F8, 18, 18, 32>(X2);
+    conv3x3<F8, 16, 32, 2, 16, 0, 16>(p.w[7], p.ws[7], p.b[7], conv_q<F8>(p, 7), X1, T2, nullptr);
     __syncthreads();
-    conv3x3<32, 32, 1, 16, 2, 16>(static_cast<const bf16*>(p.w[8]), p.b[8], T2, X2, X1);
+    conv3x3<F8, 32, 32, 1, 16, 2, 16>(p.w[8], p.ws[8], p.b[8], conv_q<F8>(p, 8), T2, X2, X1);
     __syncthreads();
 #pragma unroll 1
     for (int blk = 1; blk < 3; ++blk) {
-      conv3x3<32, 32, 1, 16, 0, 32>(static_cast<const bf16*>(p.w[7 + 2 * blk]), p.b[7 + 2 * blk], X2, T2, nullptr);
+      const int c1 = 7 + 2 * blk, c2 = c1 + 1;
+      conv3x3<F8, 32, 32, 1, 16, 0, 32>(p.w[c1], p.ws[c1], p.b[c1], conv_q<F8>(p, c1), X2, T2,
+                                        nullptr);
       __syncthreads();
-      conv3x3<32, 32, 1, 16, 1, 32>(static_cast<const bf16*>(p.w[8 + 2 * blk]), p.b[8 + 2 * blk], T2, X2, X2);
+      conv3x3<F8, 32, 32, 1, 16, 1, 32>(p.w[c2], p.ws[c2], p.b[c2], conv_q<F8>(p, c2), T2, X2,
+                                        X2);
       __syncthreads();
     }
     // ---- stage 3: 8x8x64 ----
-    zero_border<10, 10, 64>(T3);
-    zero_border<10, 10, 64>(X3);
-    conv3x3<32, 64, 2, 8, 0, 32>(static_cast<const bf16*>(p.w[13]), p.b[13], X2, T3, nullptr);
+    zero_border<F8, 10, 10, 64>(T3);
+    zero_border<F8, 10, 10, 64>(X3);
+    conv3x3<F8, 32, 64, 2, 8, 0, 32>(p.w[13], p.ws[13], p.b[13], conv_q<F8>(p, 13), X2, T3,
+                                     nullptr);
     __syncthreads();
-    conv3x3<64, 64, 1, 8, 2, 32>(static_cast<const bf16*>(p.w[14]), p.b[14], T3, X3, X2);
+    conv3x3<F8, 64, 64, 1, 8, 2, 32>(p.w[14], p.ws[14], p.b[14], conv_q<F8>(p, 14), T3, X3, X2);
     __syncthreads();
 #pragma unroll 1
     for (int blk = 1; blk < 3; ++blk) {
-      conv3x3<64, 64, 1, 8, 0, 64>(static_cast<const bf16*>(p.w[13 + 2 * blk]), p.b[13 + 2 * blk], X3, T3, nullptr);
+      const int c1 = 13 + 2 * blk, c2 = c1 + 1;
+      conv3x3<F8, 64, 64, 1, 8, 0, 64>(p.w[c1], p.ws[c1], p.b[c1], conv_q<F8>(p, c1), X3, T3,
+                                       nullptr);
       __syncthreads();
-      conv3x3<64, 64, 1, 8, 1, 64>(static_cast<const bf16*>(p.w[14 + 2 * blk]), p.b[14 + 2 * blk], T3, X3, X3);
+      conv3x3<F8, 64, 64, 1, 8, 1, 64>(p.w[c2], p.ws[c2], p.b[c2], conv_q<F8>(p, c2), T3, X3,
+                                       X3);
       __syncthreads();
     }
     // ---- head: global average pool (8x8) -> dense 64 -> 10 -> softmax ----
     {
-      const int c = threadIdx.x & 63, q = threadIdx.x >> 6;  // 4 quarters of 16 pixels
+      const int c = threadIdx.x & 63, qq = threadIdx.x >> 6;  // 4 quarters of 16 pixels
       float s = 0.f;
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        const int pix = q * 16 + i;
+        const int pix = qq * 16 + i;
         const int h = pix >> 3, w = pix & 7;
-        s += (float)X3[((h + 1) * 10 + w + 1) * 64 + c];
+        s += T::to_f32(X3[((h + 1) * 10 + w + 1) * 64 + c]);
       }
-      scratch[q * 64 + c] = s;  // R1 is free in stage 3's last block (X2 is dead)
+      scratch[qq * 64 + c] = s;  // R1 is free in stage 3's last block (X2 is dead)
       __syncthreads();
       if (threadIdx.x < 64) {
         const int lane = threadIdx.x;
+        const float pool_scale = (F8 ? p.s_out[18] : 1.f) * (1.f / 64.f);
         const float pooled =
             (scratch[lane] + scratch[64 + lane] + scratch[128 + lane] + scratch[192 + lane]) *
-            (1.f / 64.f);
+            pool_scale;
         float logit = -3.0e38f;
         for (int o = 0; o < 10; ++o) {
           const float t = wave_sum(p.fc_w[o * 64 + lane] * pooled);
@@ -286,15 +406,30 @@ __global__ __launch_bounds__(256, 2) void resnet20_fused_kernel(ResNet20Params p
 hipError_t resnet20_fused_forward(const ResNet20Params& p, int batch, const float* x, float* out,
                                   hipStream_t stream) {
   if (batch <= 0) return hipSuccess;
-  static int grid_cap = 0;
-  if (grid_cap == 0) {
-    int dev = 0, cus = 256;
-    if (hipGetDevice(&dev) == hipSuccess)
-      (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    grid_cap = 2 * (cus > 0 ? cus : 256);  // 2 resident workgroups per CU (LDS bound)
+  const bool f8 = p.fp8 != 0;
+  if (f8) {
+    for (int i = 0; i < 19; ++i)
+      if (p.ws[i] == nullptr || !(p.s_in[i] > 0.f) || !(p.s_out[i] > 0.f))
+        return hipErrorInvalidValue;
   }
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0, n = 256;
+    if (hipGetDevice(&dev) == hipSuccess)
+      (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+    cus = n > 0 ? n : 256;
+  }
+  // resident workgroups per CU: 2 (bf16: LDS bound; fp8: register bound — its 39 KB of LDS
+  // would allow 4, but the hoisted A fragments need more than 128 VGPRs per lane)
+  const int grid_cap = 2 * cus;
   const int grid = batch < grid_cap ? batch : grid_cap;
-  hipLaunchKernelGGL(resnet20_fused_kernel, dim3(grid), dim3(256), kLds, stream, p, x, out, batch);
+  const size_t lds = (size_t)kElems * (f8 ? 1 : 2);
+  if (f8)
+    hipLaunchKernelGGL(resnet20_fused_kernel<true>, dim3(grid), dim3(256), lds, stream, p, x, out,
+                       batch);
+  else
+    hipLaunchKernelGGL(resnet20_fused_kernel<false>, dim3(grid), dim3(256), lds, stream, p, x,
+                       out, batch);
   return hipGetLastError();
 }
 

@@ -94,14 +94,24 @@ void Executor::launch_all(int batch, void* const* bufs, hipStream_t stream) {
                          static_cast<float*>(out), stream);
         break;
       case OP_RESNET20: {
-        if (op.ptrs.size() != 40) throw std::invalid_argument("resnet20 op needs 40 pointers");
-        ResNet20Params rp;
+        const bool f8 = op.fp8 != 0;
+        if (op.ptrs.size() != (f8 ? 59u : 40u) || (f8 && op.scales.size() != 57))
+          throw std::invalid_argument("resnet20 op: bad pointer / scale count");
+        ResNet20Params rp{};
         for (int i = 0; i < 19; ++i) {
           rp.w[i] = op.ptrs[i];
           rp.b[i] = static_cast<const float*>(op.ptrs[19 + i]);
         }
         rp.fc_w = static_cast<const float*>(op.ptrs[38]);
         rp.fc_b = static_cast<const float*>(op.ptrs[39]);
+        rp.fp8 = f8 ? 1 : 0;
+        if (f8)
+          for (int i = 0; i < 19; ++i) {
+            rp.ws[i] = static_cast<const float*>(op.ptrs[40 + i]);
+            rp.s_in[i] = op.scales[i];
+            rp.s_out[i] = op.scales[19 + i];
+            rp.s_res[i] = op.scales[38 + i];
+          }
         e = resnet20_fused_forward(rp, batch, static_cast<const float*>(in),
                                    static_cast<float*>(out), stream);
         break;

@@ -346,13 +346,20 @@ def is_cifar_resnet20(net: Network) -> bool:
             and [repr(L) for L in net.layers] == [repr(L) for L in ref.layers])
 
 
-def _fused_resnet20_plan(net: Network, base_ptr: int) -> Tuple[List[dict], List[int]]:
-    layout, _ = param_layout(net, "bf16")
+def _fused_resnet20_plan(net: Network, base_ptr: int, wdtype: str = "bf16",
+                         act_scales: Optional[Dict[str, float]] = None
+                         ) -> Tuple[List[dict], List[int]]:
+    layout, _ = param_layout(net, wdtype)
     convs = [L for L in net.layers if isinstance(L, Conv)]
     ptrs = [base_ptr + layout[f"{L.name}.w"].offset for L in convs]
     ptrs += [base_ptr + layout[f"{L.name}.b"].offset for L in convs]
     ptrs += [base_ptr + layout["fc.w"].offset, base_ptr + layout["fc.b"].offset]
     op = dict(kind=OP_RESNET20, **{"in": 0}, out=1, ptrs=ptrs)
+    if wdtype == "fp8":
+        op["fp8"] = 1
+        op["ptrs"] = ptrs + [base_ptr + layout[f"{L.name}.s"].offset for L in convs]
+        op["scales"] = ([act_scales[L.inp] for L in convs] + [act_scales[L.out] for L in convs]
+                        + [act_scales[L.residual] if L.residual else 1.0 for L in convs])
     return [op], [_tensor_bytes(net, "input"), net.classes * 4]
 
 
@@ -371,13 +378,14 @@ def build_plan(net: Network, base_ptr: int, wdtype: str = "bf16",
     Returns (ops, buf_bytes_per_image). Buffer 0 = fp32 input, 1 = fp32 softmax output, >= 2 =
     bf16 (fp8: e4m3) activations assigned by liveness so concurrently-live tensors never share a
     buffer. ``act_scales`` (fp8 only): per-tensor scales, see ``act_scales_from_packed``.
-    ``fused``: the bf16 CIFAR ResNet-20 becomes ONE whole-network kernel (activations in LDS).
+    ``fused``: the CIFAR ResNet-20 (bf16 or fp8) becomes ONE whole-network kernel (activations
+    resident in LDS).
     """
     fp8 = wdtype == "fp8"
-    if fused and not fp8 and is_cifar_resnet20(net):
-        return _fused_resnet20_plan(net, base_ptr)
     if fp8 and act_scales is None:
         raise ValueError("build_plan: the fp8 plan needs the activation scales")
+    if fused and is_cifar_resnet20(net):
+        return _fused_resnet20_plan(net, base_ptr, wdtype, act_scales)
     layout, _ = param_layout(net, wdtype)
     # liveness: last layer index reading each tensor
     last_use: Dict[str, int] = {}

@@ -81,3 +81,26 @@ def test_resnet20_fused_matches_layerwise_and_fp32(batch):
     assert torch.allclose(a.sum(1), torch.ones(batch), atol=1e-5)
     # eager launch equals graph replay
     assert torch.equal(fused.infer_eager(x).cpu(), a)
+
+
+def test_resnet20_fp8_fused_matches_layerwise():
+    """fp8 whole-network kernel (e4m3 activations in LDS) against the per-layer fp8 plan and the
+    fp8 emulation oracle on the same packed weights / calibrated scales."""
+    from gale.models.graph import act_scales_from_packed
+
+    net = get_model("resnet20")
+    params = init_params(net, seed=5)
+    packed = materialize_weights(net, torch.device("cuda", 0), params=params, wdtype="fp8")
+    fused = ModelReplica(net, packed, max_batch=700, slots=1, wdtype="fp8", fused=True)
+    layered = ModelReplica(net, packed, max_batch=700, slots=1, wdtype="fp8", fused=False)
+    assert len(fused.ops) == 1 and len(layered.ops) > 1
+    x = torch.rand((700, 32, 32, 3), generator=torch.Generator().manual_seed(3))
+    a = fused.infer(x, use_graph=True).cpu()
+    b = layered.infer(x, use_graph=True).cpu()
+    emu = forward(net, fold_params(net, params), x, fp8_scales=act_scales_from_packed(net, packed))
+    torch.cuda.synchronize()
+    # same quantised operands and rounding points; only fp32 summation order differs, which can
+    # flip an occasional e4m3 rounding
+    assert (a - b).abs().mean().item() < 2e-3
+    assert (a - emu).abs().mean().item() < 5e-3
+    assert (a.argmax(1) == b.argmax(1)).float().mean().item() > 0.97

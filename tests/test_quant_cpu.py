@@ -72,7 +72,7 @@ def test_fp8_packing_and_plan(name):
     assert buf.numel() == total
     sc = act_scales_from_packed(net, buf)
     assert sc == pytest.approx(calibrate_act_scales(net, f))
-    ops, buf_bytes = build_plan(net, 0, "fp8", sc)
+    ops, buf_bytes = build_plan(net, 0, "fp8", sc, fused=False)
     convs = [op for op in ops if op["kind"] == 0]
     assert all(op["conv"]["fp8"] == 1 and op["conv"]["in_scale"] > 0 for op in convs)
     assert all("wscale" in op for op in convs)
@@ -82,3 +82,21 @@ def test_fp8_packing_and_plan(name):
     assert sum(buf_bytes[2:]) * 2 == sum(bf16_bytes[2:])
     with pytest.raises(ValueError):
         build_plan(net, 0, "fp8")
+
+
+def test_fp8_fused_resnet20_plan_carries_scales():
+    from gale.models.graph import OP_RESNET20, Conv
+
+    net = get_model("resnet20")
+    f = fold_params(net, init_params(net, seed=1))
+    sc = act_scales_from_packed(net, pack_params(net, f, "fp8"))
+    ops, _ = build_plan(net, 4096, "fp8", sc)
+    assert len(ops) == 1 and ops[0]["kind"] == OP_RESNET20 and ops[0]["fp8"] == 1
+    assert len(ops[0]["ptrs"]) == 59 and len(ops[0]["scales"]) == 57
+    convs = [L for L in net.layers if isinstance(L, Conv)]
+    s_in, s_out, s_res = (ops[0]["scales"][i * 19:(i + 1) * 19] for i in range(3))
+    assert s_in[0] == pytest.approx(sc["input"])
+    for i, L in enumerate(convs):
+        assert s_in[i] == pytest.approx(sc[L.inp]) and s_out[i] == pytest.approx(sc[L.out])
+        if L.residual:
+            assert s_res[i] == pytest.approx(sc[L.residual])
