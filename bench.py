@@ -51,8 +51,9 @@ def parse_args():
                     help="consumer threads (default: one per partition)")
     ap.add_argument("--sink-parallelism", type=int, default=2)
     ap.add_argument("--decode-threads", type=int, default=2)
-    ap.add_argument("--replicas-per-gpu", type=int, default=4,
-                    help="model replicas (streams) per GPU; each gets its own input partition")
+    ap.add_argument("--replicas-per-gpu", type=int, default=0,
+                    help="model replicas (streams) per GPU, each with its own input partition "
+                         "(0 = from the host CPU share: 4 with >= 16 cores per GPU)")
     ap.add_argument("--max-wait-us", type=int, default=2000)
     ap.add_argument("--queue-batches", type=int, default=4,
                     help="records buffered in the engine, in units of --batch")
@@ -64,8 +65,25 @@ def parse_args():
     return ap.parse_args()
 
 
+def host_cpus_per_rank() -> float:
+    """CPUs this rank may use: min(affinity, cgroup CPU quota) / ranks on this node."""
+    n = float(len(os.sched_getaffinity(0)))
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        if quota != "max":
+            n = min(n, int(quota) / int(period))
+    except (OSError, ValueError):
+        pass
+    return n / max(1, int(os.environ.get("LOCAL_WORLD_SIZE", "1")))
+
+
 def main() -> int:
     a = parse_args()
+    if a.replicas_per_gpu <= 0:
+        # the host pipeline (Kafka fetch + CRC + scan + encode + produce, and the embedded
+        # broker of this rank) needs ~3 cores per replica at full rate
+        a.replicas_per_gpu = max(1, min(4, int(host_cpus_per_rank() // 4)))
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))

@@ -135,9 +135,10 @@ PYBIND11_MODULE(_C, m) {
               "cast_f32_bf16");
         });
   m.def("json_parse_instances",
-        [](int nrec, int ntiles, uintptr_t recs, uintptr_t bytes, int H, int W, int C,
-           uintptr_t tile_counts, uintptr_t out, uintptr_t stream) {
+        [](int nrec, int ntiles, uintptr_t recs, uintptr_t tile_rec, uintptr_t bytes, int H,
+           int W, int C, uintptr_t tile_counts, uintptr_t out, uintptr_t stream) {
           chk(gale::json_parse_instances(nrec, ntiles, static_cast<gale::JsonRecord*>(P(recs)),
+                                         static_cast<const int*>(P(tile_rec)),
                                          static_cast<const uint8_t*>(P(bytes)), H, W, C,
                                          static_cast<int*>(P(tile_counts)),
                                          static_cast<float*>(P(out)), S(stream)),

@@ -101,9 +101,10 @@ struct JsonRecord {
   int32_t pad_;
 };
 int json_tile_count(int64_t off, int32_t len);
-// tile_counts: device scratch of >= ntiles ints.
-hipError_t json_parse_instances(int nrec, int ntiles, JsonRecord* recs, const uint8_t* bytes,
-                                int H, int W, int C, int* tile_counts, float* out,
-                                hipStream_t stream);
+// tile_rec[t]: index of the record owning global tile t. tile_counts: device scratch of
+// >= ntiles ints.
+hipError_t json_parse_instances(int nrec, int ntiles, JsonRecord* recs, const int* tile_rec,
+                                const uint8_t* bytes, int H, int W, int C, int* tile_counts,
+                                float* out, hipStream_t stream);
 
 }  // namespace gale

@@ -160,14 +160,18 @@ __device__ float parse_number(const Text& t, int64_t i0, int64_t end, bool* ok, 
 
 // Delimiters in front of token `idx` (scanning back from pos-1). Between tokens the text must be
 // ws* (']' ws*)^k ',' ws* ('[' ws*)^k with k = number of trailing dimensions that wrap.
-__device__ bool gap_ok(const Text& t, int64_t beg, int64_t pos, int64_t idx, int C, int W,
-                       int H) {
+__device__ bool gap_ok(const Text& t, int64_t beg, int64_t pos, uint32_t idx, uint32_t C,
+                       uint32_t W, uint32_t H) {
   int k = 0;
-  if (idx > 0) {
-    if (idx % C) k = 0;
-    else if ((idx / C) % W) k = 1;
-    else if ((idx / ((int64_t)C * W)) % H) k = 2;
-    else k = 3;
+  if (idx > 0) {  // (32-bit: a record holds < 2^32 numbers; 64-bit division is ~10x dearer)
+    const uint32_t px = idx / C;
+    if (idx - px * C) k = 0;
+    else {
+      const uint32_t row = px / W;
+      if (px - row * W) k = 1;
+      else if (row % H) k = 2;
+      else k = 3;
+    }
   }
   int opens = 0, closes = 0, commas = 0;
   int64_t q = pos - 1;
@@ -203,17 +207,6 @@ __device__ bool tail_ok(const Text& t, int64_t pos, int64_t end) {
   return closes == 4;
 }
 
-// Record owning global tile `t` (records' tile0 are non-decreasing).
-__device__ __forceinline__ int tile_record(const JsonRecord* recs, int nrec, int t) {
-  int lo = 0, hi = nrec - 1;
-  while (lo < hi) {
-    const int mid = (lo + hi + 1) >> 1;
-    if (recs[mid].tile0 <= t) lo = mid;
-    else hi = mid - 1;
-  }
-  return lo;
-}
-
 __device__ __forceinline__ int block_sum(int v, int* red) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
@@ -225,11 +218,11 @@ __device__ __forceinline__ int block_sum(int v, int* red) {
   return s;
 }
 
-__global__ __launch_bounds__(256) void json_count_kernel(JsonRecord* recs, int nrec,
+__global__ __launch_bounds__(256) void json_count_kernel(JsonRecord* recs, const int* tile_rec,
                                                          const uint8_t* bytes, int* counts) {
   __shared__ int red[4];
   const int t = blockIdx.x;
-  const int ri = tile_record(recs, nrec, t);
+  const int ri = tile_rec[t];
   const JsonRecord r = recs[ri];
   const int64_t beg = r.off, end = r.off + r.len;
   const int64_t t0 = (beg & ~(int64_t)15) + (int64_t)(t - r.tile0) * kTile;
@@ -246,7 +239,7 @@ __global__ __launch_bounds__(256) void json_count_kernel(JsonRecord* recs, int n
   if (threadIdx.x == 0) counts[t] = cnt;
 }
 
-__global__ __launch_bounds__(256) void json_parse_kernel(JsonRecord* recs, int nrec,
+__global__ __launch_bounds__(256) void json_parse_kernel(JsonRecord* recs, const int* tile_rec,
                                                          const uint8_t* bytes, int H, int W,
                                                          int C, const int* counts, float* out) {
   __shared__ __attribute__((aligned(16))) uint8_t text[kTile + 2 * kHalo];
@@ -254,7 +247,7 @@ __global__ __launch_bounds__(256) void json_parse_kernel(JsonRecord* recs, int n
   __shared__ int wave_tot[4];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int t = blockIdx.x;
-  const int ri = tile_record(recs, nrec, t);
+  const int ri = tile_rec[t];
   const JsonRecord r = recs[ri];
   const int per_image = H * W * C;
   const int64_t beg = r.off, end = r.off + r.len;
@@ -314,7 +307,7 @@ __global__ __launch_bounds__(256) void json_parse_kernel(JsonRecord* recs, int n
     int len = 0;
     const float v = parse_number(tx, pos, end, &ok, &len);
     if (!ok) bad = max(bad, 2);
-    else if (!gap_ok(tx, beg, pos, idx, C, W, H)) bad = 3;
+    else if (!gap_ok(tx, beg, pos, (uint32_t)idx, (uint32_t)C, (uint32_t)W, (uint32_t)H)) bad = 3;
     else if (idx == expected - 1 && !tail_ok(tx, pos + len, end)) bad = 3;
     if (idx < expected) dst[idx] = v;
     ++idx;
@@ -331,14 +324,14 @@ int json_tile_count(int64_t off, int32_t len) {
   return (int)((off + len - abeg + kJsonTileBytes - 1) / kJsonTileBytes);
 }
 
-hipError_t json_parse_instances(int nrec, int ntiles, JsonRecord* recs, const uint8_t* bytes,
-                                int H, int W, int C, int* tile_counts, float* out,
-                                hipStream_t stream) {
+hipError_t json_parse_instances(int nrec, int ntiles, JsonRecord* recs, const int* tile_rec,
+                                const uint8_t* bytes, int H, int W, int C, int* tile_counts,
+                                float* out, hipStream_t stream) {
   if (nrec <= 0 || ntiles <= 0) return hipSuccess;
   if (H <= 0 || W <= 0 || C <= 0) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(json_count_kernel, dim3(ntiles), dim3(256), 0, stream, recs, nrec, bytes,
+  hipLaunchKernelGGL(json_count_kernel, dim3(ntiles), dim3(256), 0, stream, recs, tile_rec, bytes,
                      tile_counts);
-  hipLaunchKernelGGL(json_parse_kernel, dim3(ntiles), dim3(256), 0, stream, recs, nrec, bytes,
+  hipLaunchKernelGGL(json_parse_kernel, dim3(ntiles), dim3(256), 0, stream, recs, tile_rec, bytes,
                      H, W, C, tile_counts, out);
   return hipGetLastError();
 }

@@ -28,17 +28,13 @@ GpuReplica::GpuReplica(std::shared_ptr<Executor> exec, int H, int W, int C, int 
   const int mb = exec_->max_batch();
   slots_.resize((size_t)exec_->slots());
   for (Slot& s : slots_) {
-    check_hip(hipHostMalloc(reinterpret_cast<void**>(&s.h_recs), sizeof(JsonRecord) * mb),
-              "hipHostMalloc(recs)");
-    check_hip(hipMalloc(reinterpret_cast<void**>(&s.d_recs), sizeof(JsonRecord) * mb),
-              "hipMalloc(recs)");
     check_hip(hipHostMalloc(reinterpret_cast<void**>(&s.h_out), sizeof(float) * mb * classes),
               "hipHostMalloc(out)");
     check_hip(hipEventCreateWithFlags(&s.done, hipEventDisableTiming), "hipEventCreate");
     check_hip(hipEventCreateWithFlags(&s.staged, hipEventDisableTiming), "hipEventCreate");
     // initial text capacity: ~12 bytes per number (Java Float.toString + ",") x a full batch
     ensure_device(s, (size_t)mb * H * W * C * 12 + 4096);
-    ensure_tiles(s, (int)(((size_t)mb * H * W * C * 12) / kJsonTileBytes) + 2 * mb);
+    ensure_tiles(s, (int)(((size_t)mb * H * W * C * 12) / kJsonTileBytes) + 2 * mb, 0);
   }
 }
 
@@ -75,15 +71,29 @@ void GpuReplica::ensure_host(Slot& s, size_t bytes) {
   s.h_cap = cap;
 }
 
-void GpuReplica::ensure_tiles(Slot& s, int ntiles) {
+// Per-slot parser metadata: [JsonRecord x max_batch][tile -> record index x tiles_cap], pinned
+// on the host and mirrored on the device (one H2D per batch), plus the per-tile token counts.
+// Growing keeps the first `keep` records already written into the host copy.
+void GpuReplica::ensure_tiles(Slot& s, int ntiles, int keep) {
   if (ntiles <= s.tiles_cap) return;
   const int cap = std::max(ntiles, s.tiles_cap * 2);
-  if (s.d_tiles) {
-    check_hip(hipEventSynchronize(s.done), "hipEventSynchronize");
+  const size_t rec_bytes = sizeof(JsonRecord) * (size_t)exec_->max_batch();
+  const size_t bytes = rec_bytes + sizeof(int) * (size_t)cap;
+  if (s.h_recs) check_hip(hipEventSynchronize(s.done), "hipEventSynchronize");
+  JsonRecord* h = nullptr;
+  check_hip(hipHostMalloc(reinterpret_cast<void**>(&h), bytes), "hipHostMalloc(meta)");
+  if (s.h_recs) {
+    memcpy(h, s.h_recs, sizeof(JsonRecord) * (size_t)keep);
+    hipHostFree(s.h_recs);
+    hipFree(s.d_recs);
     hipFree(s.d_tiles);
   }
+  s.h_recs = h;
+  check_hip(hipMalloc(reinterpret_cast<void**>(&s.d_recs), bytes), "hipMalloc(meta)");
   check_hip(hipMalloc(reinterpret_cast<void**>(&s.d_tiles), sizeof(int) * cap),
             "hipMalloc(tiles)");
+  s.h_tile_rec = reinterpret_cast<int*>(reinterpret_cast<char*>(s.h_recs) + rec_bytes);
+  s.d_tile_rec = reinterpret_cast<int*>(reinterpret_cast<char*>(s.d_recs) + rec_bytes);
   s.tiles_cap = cap;
 }
 
@@ -176,17 +186,24 @@ void GpuReplica::submit(Batch& b) {
   }
   if (img > exec_->max_batch()) throw std::logic_error("GpuReplica: batch exceeds max_batch");
   b.images = img;
+  ensure_tiles(s, ntiles, nrec);
+  for (int i = 0; i < nrec; ++i) {
+    const JsonRecord& jr = s.h_recs[i];
+    const int nt = json_tile_count(jr.off, jr.len);
+    for (int t = 0; t < nt; ++t) s.h_tile_rec[jr.tile0 + t] = i;
+  }
   if (hoff)
     check_hip(hipMemcpyAsync(s.d_bytes + staged_dev, s.h_bytes, hoff, hipMemcpyHostToDevice,
                              copy_stream_),
               "H2D staged");
-  check_hip(hipMemcpyAsync(s.d_recs, s.h_recs, sizeof(JsonRecord) * nrec, hipMemcpyHostToDevice,
-                           copy_stream_),
+  const size_t meta = reinterpret_cast<char*>(s.h_tile_rec + ntiles) -
+                      reinterpret_cast<char*>(s.h_recs);
+  check_hip(hipMemcpyAsync(s.d_recs, s.h_recs, meta, hipMemcpyHostToDevice, copy_stream_),
             "H2D recs");
   check_hip(hipEventRecord(s.staged, copy_stream_), "hipEventRecord(staged)");
   check_hip(hipStreamWaitEvent(stream_, s.staged, 0), "hipStreamWaitEvent");
-  ensure_tiles(s, ntiles);
-  check_hip(json_parse_instances(nrec, ntiles, s.d_recs, s.d_bytes, H_, W_, C_, s.d_tiles,
+  check_hip(json_parse_instances(nrec, ntiles, s.d_recs, s.d_tile_rec, s.d_bytes, H_, W_, C_,
+                                 s.d_tiles,
                                  static_cast<float*>(exec_->input(slot)), stream_),
             "json_parse_instances");
   exec_->run(slot, img, stream_, use_graph_);

@@ -91,8 +91,10 @@ class GpuReplica : public Replica {
     uint8_t* h_bytes = nullptr;  // pinned staging for records that arrived in pageable memory
     uint8_t* d_bytes = nullptr;  // device copy of the batch's JSON text
     size_t h_cap = 0, d_cap = 0;
-    JsonRecord* h_recs = nullptr;
-    JsonRecord* d_recs = nullptr;
+    JsonRecord* h_recs = nullptr;  // [max_batch records][tile -> record map] (pinned)
+    JsonRecord* d_recs = nullptr;  // device mirror
+    int* h_tile_rec = nullptr;
+    int* d_tile_rec = nullptr;
     int* d_tiles = nullptr;      // per-tile token counts (parser scratch)
     int tiles_cap = 0;
     float* h_out = nullptr;      // pinned softmax rows
@@ -101,7 +103,7 @@ class GpuReplica : public Replica {
   };
   void ensure_host(Slot& s, size_t bytes);
   void ensure_device(Slot& s, size_t bytes);
-  void ensure_tiles(Slot& s, int ntiles);
+  void ensure_tiles(Slot& s, int ntiles, int keep);
   std::shared_ptr<Executor> exec_;
   int H_, W_, C_, classes_;
   bool use_graph_;

@@ -55,6 +55,7 @@ def test_bench_stub_torchrun_world2():
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "2",
            "--stub", "--steps", "4", "--warmup", "1", "--batch", "32", "--distinct", "64",
+           "--replicas-per-gpu", "4",
            "--timeout", "120"]
     out = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=300,
                          env=dict(os.environ, OMP_NUM_THREADS="1"))

@@ -38,12 +38,17 @@ def stage(arrays):
 
 def gpu_parse(arrays, H, Wd, Cc):
     raw, recs, total, tiles = stage(arrays)
+    tile_rec = np.zeros(max(tiles, 1), dtype=np.int32)
+    for i, r in enumerate(recs):
+        n = C.json_tile_count(int(r["off"]), int(r["len"]))
+        tile_rec[r["tile0"]:r["tile0"] + n] = i
     d_raw = torch.from_numpy(raw.copy()).cuda()
     d_recs = torch.from_numpy(recs.view(np.uint8).copy()).cuda()
+    d_tile_rec = torch.from_numpy(tile_rec).cuda()
     d_tiles = torch.zeros(max(tiles, 1), dtype=torch.int32, device="cuda")
     out = torch.full((max(total, 1), H, Wd, Cc), -7.0, device="cuda")
-    C.json_parse_instances(len(arrays), tiles, d_recs.data_ptr(), d_raw.data_ptr(), H, Wd, Cc,
-                           d_tiles.data_ptr(), out.data_ptr(),
+    C.json_parse_instances(len(arrays), tiles, d_recs.data_ptr(), d_tile_rec.data_ptr(),
+                           d_raw.data_ptr(), H, Wd, Cc, d_tiles.data_ptr(), out.data_ptr(),
                            torch.cuda.current_stream().cuda_stream)
     torch.cuda.synchronize()
     st = d_recs.cpu().numpy().view(REC)["status"]
