@@ -70,3 +70,9 @@ asan: build/asan/engine_stress
 	ASAN_OPTIONS="detect_leaks=1" ./build/asan/engine_stress 2000
 
 .PHONY: tsan asan
+
+# host codec micro-benchmark (CRC32C + envelope scan GB/s per core)
+build/host_bench: csrc/tests/host_bench.cpp csrc/codec/json_codec.cpp csrc/kafka/wire.cpp $(HDRS)
+	@mkdir -p build
+	$(CXX) -O3 -std=c++17 -mavx2 -mfma -msse4.2 -mpclmul -mbmi2 -Icsrc/include \
+	    csrc/tests/host_bench.cpp csrc/codec/json_codec.cpp csrc/kafka/wire.cpp -o $@

@@ -61,6 +61,8 @@ def parse_args():
     ap.add_argument("--stub", action="store_true", help="CPU stub replicas (no GPU)")
     ap.add_argument("--stub-null", action="store_true",
                     help="stub replicas skip parsing (measures the host Kafka/codec path only)")
+    ap.add_argument("--check-crcs", action=argparse.BooleanOptionalAction, default=True,
+                    help="consumer CRC32C verification (Kafka check.crcs; diagnosis only)")
     ap.add_argument("--timeout", type=float, default=600.0)
     return ap.parse_args()
 
@@ -135,7 +137,8 @@ def main() -> int:
                      source_parallelism=a.source_parallelism or parts,
                      sink_parallelism=a.sink_parallelism, replicas=a.replicas_per_gpu,
                      decode_threads=a.decode_threads,
-                     stub=a.stub, stub_null=a.stub_null, commit_interval_ms=500)
+                     stub=a.stub, stub_null=a.stub_null, commit_interval_ms=500,
+                     check_crcs=a.check_crcs)
     devices = [local_rank] if use_gpu else None
     warm_records = -(-max(1, a.warmup) * step_images // ipr)
     timed_records = -(-a.steps * step_images // ipr)

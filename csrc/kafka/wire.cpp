@@ -1,6 +1,7 @@
 // Kafka wire primitives: CRC32C and the RecordBatch v2 codec (see wire.h).
 #include "wire.h"
 
+#include <immintrin.h>
 #include <nmmintrin.h>
 
 namespace gale {
@@ -102,10 +103,81 @@ inline const uint8_t* crc3(const uint8_t* p, size_t& n, uint64_t& c0, size_t blk
   return p;
 }
 
+// CRC32C by carry-less-multiply folding on 512-bit registers (VPCLMULQDQ + AVX-512, e.g. Zen 4/5
+// hosts of MI355X nodes): four zmm accumulators fold 256 bytes per iteration, ~4x the crc32q
+// rate. Reflected-domain folding of a 128-bit lane R = [lo, hi] over L bits is
+//   R' = clmul(lo, reflect32(x^(64+L-1) mod P) << 32) ^ clmul(hi, reflect32(x^(L-1) mod P) << 32)
+// (P = CRC-32C); the folded last 16 bytes are finished with two crc32q from state 0 (the initial
+// state is XORed into the first 4 bytes, which is exactly what crc32q does with its state).
+// Constants derived and checked bit-exactly against the bytewise definition offline.
+constexpr uint64_t kF2048a = 0xe9a5d8be00000000ull, kF2048b = 0x1426a81500000000ull;
+constexpr uint64_t kF512a = 0x1c19243b00000000ull, kF512b = 0x75bba45b00000000ull;
+constexpr uint64_t kF128a = 0x3743f7bd00000000ull, kF128b = 0x3171d43000000000ull;
+
+__attribute__((target("avx512f,avx512vl,vpclmulqdq,pclmul,sse4.2"))) inline __m512i
+fold512(__m512i x, __m512i k, __m512i next) {
+  return _mm512_ternarylogic_epi64(_mm512_clmulepi64_epi128(x, k, 0x00),
+                                   _mm512_clmulepi64_epi128(x, k, 0x11), next, 0x96);
+}
+
+__attribute__((target("avx512f,avx512vl,vpclmulqdq,pclmul,sse4.2"))) inline __m128i
+fold128(__m128i a, __m128i k, __m128i next) {
+  return _mm_ternarylogic_epi64(_mm_clmulepi64_si128(a, k, 0x00), _mm_clmulepi64_si128(a, k, 0x11),
+                                next, 0x96);
+}
+
+// Consumes every whole 64-byte block of [p, p+n) (n >= 256); returns the raw crc32q state.
+__attribute__((target("avx512f,avx512vl,vpclmulqdq,pclmul,sse4.2"))) uint32_t
+crc32c_vpclmul(const uint8_t*& p, size_t& n, uint32_t state) {
+  const __m512i k2048 = _mm512_set_epi64(kF2048b, kF2048a, kF2048b, kF2048a, kF2048b, kF2048a,
+                                         kF2048b, kF2048a);
+  const __m512i k512 = _mm512_set_epi64(kF512b, kF512a, kF512b, kF512a, kF512b, kF512a, kF512b,
+                                        kF512a);
+  __m512i x0 = _mm512_loadu_si512(p);
+  __m512i x1 = _mm512_loadu_si512(p + 64);
+  __m512i x2 = _mm512_loadu_si512(p + 128);
+  __m512i x3 = _mm512_loadu_si512(p + 192);
+  x0 = _mm512_xor_si512(x0, _mm512_zextsi128_si512(_mm_cvtsi32_si128((int)state)));
+  p += 256;
+  n -= 256;
+  while (n >= 256) {
+    x0 = fold512(x0, k2048, _mm512_loadu_si512(p));
+    x1 = fold512(x1, k2048, _mm512_loadu_si512(p + 64));
+    x2 = fold512(x2, k2048, _mm512_loadu_si512(p + 128));
+    x3 = fold512(x3, k2048, _mm512_loadu_si512(p + 192));
+    p += 256;
+    n -= 256;
+  }
+  x1 = fold512(x0, k512, x1);
+  x2 = fold512(x1, k512, x2);
+  x3 = fold512(x2, k512, x3);
+  while (n >= 64) {
+    x3 = fold512(x3, k512, _mm512_loadu_si512(p));
+    p += 64;
+    n -= 64;
+  }
+  const __m128i k128 = _mm_set_epi64x((long long)kF128b, (long long)kF128a);
+  __m128i r = _mm512_extracti32x4_epi32(x3, 0);
+  r = fold128(r, k128, _mm512_extracti32x4_epi32(x3, 1));
+  r = fold128(r, k128, _mm512_extracti32x4_epi32(x3, 2));
+  r = fold128(r, k128, _mm512_extracti32x4_epi32(x3, 3));
+  uint64_t c = _mm_crc32_u64(0, (uint64_t)_mm_cvtsi128_si64(r));
+  c = _mm_crc32_u64(c, (uint64_t)_mm_extract_epi64(r, 1));
+  return (uint32_t)c;
+}
+
+bool has_vpclmul() {
+  static const bool ok = __builtin_cpu_supports("avx512f") &&
+                         __builtin_cpu_supports("avx512vl") &&
+                         __builtin_cpu_supports("vpclmulqdq");
+  return ok;
+}
+
 }  // namespace
 
 uint32_t crc32c(const uint8_t* p, size_t n, uint32_t crc) {
   uint64_t c = ~crc & 0xffffffffu;
+  if (n >= 256 && has_vpclmul()) c = crc32c_vpclmul(p, n, (uint32_t)c);
   while (n && ((uintptr_t)p & 7)) {
     c = _mm_crc32_u8((uint32_t)c, *p++);
     --n;

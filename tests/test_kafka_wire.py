@@ -27,12 +27,23 @@ def zigzag(v: int) -> bytes:
     return bytes(out)
 
 
+def _crc_table():
+    t = []
+    for n in range(256):
+        c = n
+        for _ in range(8):
+            c = (c >> 1) ^ (0x82F63B78 if c & 1 else 0)
+        t.append(c)
+    return t
+
+
+_CRC_T = _crc_table()
+
+
 def crc32c_ref(data: bytes) -> int:
     crc = 0xFFFFFFFF
     for b in data:
-        crc ^= b
-        for _ in range(8):
-            crc = (crc >> 1) ^ (0x82F63B78 if crc & 1 else 0)
+        crc = (crc >> 8) ^ _CRC_T[(crc ^ b) & 0xFF]
     return crc ^ 0xFFFFFFFF
 
 
@@ -42,6 +53,21 @@ def test_crc32c_vectors():
     data = bytes(range(256)) * 37 + b"tail"
     assert K.crc32c(data) == crc32c_ref(data)
     assert K.crc32c(data[3:]) == crc32c_ref(data[3:])  # unaligned start
+
+
+def test_crc32c_all_paths_lengths_and_offsets():
+    """Every length class of the dispatch (bytewise head, VPCLMULQDQ 256-B folding loop and its
+    64-B tail loop, 3-stream crc32q blocks, 8-B and 1-B tails) at several alignments."""
+    import random
+
+    rng = random.Random(7)
+    buf = bytes(rng.getrandbits(8) for _ in range(70000))
+    lengths = list(range(0, 70)) + [255, 256, 257, 319, 320, 321, 511, 512, 575, 1000, 4096,
+                                     8191, 24576 + 17, 65536 + 3]
+    for n in lengths:
+        for off in (0, 1, 5, 13):
+            d = buf[off:off + n]
+            assert K.crc32c(d) == crc32c_ref(d), (n, off)
 
 
 @pytest.mark.parametrize("key,expected", [
