@@ -90,7 +90,7 @@ hipError_t cast_f32_bf16(int64_t n, float scale, float shift, const float* x, vo
 // global tiles [tile0, tile0 + json_tile_count(off, len)), numbered consecutively over the batch.
 // The kernel raises each record's status (host zeroes it): 0 ok, 1 number-count mismatch,
 // 2 malformed number / element, 3 bad structure (ragged / wrong rank).
-constexpr int kJsonTileBytes = 4096;
+constexpr int kJsonTileBytes = 2048;
 struct JsonRecord {
   int64_t off;      // byte offset of the instances array inside the staged byte buffer
   int32_t len;      // array length in bytes

@@ -5,16 +5,24 @@
 // (InferenceBolt.java:76-77) and then copies the nested float arrays into a native tensor
 // (Tensor.create, :80). At ~35 KB of text per CIFAR image that float parsing is the dominant host
 // cost of the whole pipeline, so gale moves it to the GPU. The host only validates
-// the envelope and counts '[' to get N (codec::scan_instances, AVX2) and stages the raw bytes of
-// the instances array; the device then
-//   * splits every record's text into 4 KiB tiles (tile t of the batch = one workgroup, so a
-//     256-record CIFAR batch is ~2300 workgroups: the whole chip, not one workgroup per record),
+// the envelope and counts '[' to get N (codec::scan_instances) and stages the raw bytes of the
+// instances array; the device then
+//   * splits every record's text into 4 KiB tiles, ONE WAVE PER TILE (64 lanes x 64 contiguous
+//     bytes; 4 tiles per 256-thread workgroup, so a 256-record CIFAR batch is ~2300 waves and no
+//     kernel here has a workgroup barrier),
+//   * classifies 4 bytes per VALU op with a nibble lookup (two v_perm_b32 tables, as in SIMD JSON
+//     scanners) into delimiter / number-alphabet / digit bit masks,
 //   * pass 1 (json_count_kernel): counts the number tokens of each tile (a token starts at a
 //     non-delimiter byte that follows a delimiter) and rejects bytes outside the number alphabet,
-//   * pass 2 (json_parse_kernel): the tile's first token index = sum of the counts of the
-//     record's earlier tiles (block reduction), a block-wide prefix sum over 16-byte lane chunks
-//     gives every token its element index, and each token is parsed with the strict JSON number
-//     grammar straight into the fp32 NHWC batch tensor from an LDS copy of the tile (+ halos),
+//   * pass 2 (json_parse_kernel): stages the tile (+ halos) in LDS, a wave prefix sum over the
+//     lanes' token counts gives every token its element index (the record's earlier tiles are
+//     summed from pass 1), the token start offsets are compacted into an LDS list and then every
+//     lane parses tokens lane, lane+64, ... - balanced work, no per-lane divergence from uneven
+//     token density. A token is parsed from a 16-byte register window (v_alignbyte realignment
+//     of 5 LDS dwords) with bit-mask arithmetic for the strict JSON grammar
+//     -?(0|[1-9][0-9]*)(\.[0-9]+)?([eE][+-]?[0-9]+)? and two 32-bit digit accumulators; anything
+//     the window cannot decide (tokens >= 16 bytes, whitespace in the gap, the first/last token of
+//     a record) takes the sequential byte-by-byte path, which is the definitive check,
 //   * checks that the delimiters in front of token i are exactly what a rectangular
 //     [N][H][W][C] array requires ("," inside a pixel, "],[" between pixels, "]],[[" between
 //     rows, "]]],[[[" between images, "[[[[" before the first and "]]]]" after the last) and that
@@ -23,15 +31,21 @@
 // 2 malformed number / element, 3 bad structure; the host zeroes it before the launch.
 //
 // Each record's bytes start 16-byte aligned; the buffer must be readable 16 bytes past the last
-// record.
+// record. Positions below are record-relative: 0 = the record's 16-byte-aligned start.
 #include "common.cuh"
 #include "gale/kernels.h"
 
 namespace gale {
 namespace {
 
-constexpr int kTile = kJsonTileBytes;  // bytes per workgroup tile (256 lanes x 16 B)
-constexpr int kHalo = 64;              // LDS halo on each side (token tails, delimiter look-back)
+constexpr int kTile = kJsonTileBytes;           // bytes per tile = per wave
+constexpr int kLaneBytes = kTile / 64;          // contiguous bytes per lane
+constexpr int kChunks = kLaneBytes / 16;        // 16-byte chunks per lane
+static_assert(kChunks >= 1 && kChunks * 16 * 64 == kTile, "tile = 64 lanes x 16-byte chunks");
+constexpr int kHalo = 64;                       // LDS halo on each side of the tile
+constexpr int kWaves = 4;                       // tiles (waves) per workgroup
+constexpr int kText = kTile + 2 * kHalo + 16;   // LDS text bytes per wave (+16: window over-read)
+constexpr int kMaxTok = kTile / 2;              // a token start needs a delimiter before it
 
 __device__ __forceinline__ bool is_ws(unsigned c) {
   return c == ' ' || c == '\n' || c == '\r' || c == '\t';
@@ -39,52 +53,128 @@ __device__ __forceinline__ bool is_ws(unsigned c) {
 __device__ __forceinline__ bool is_delim(unsigned c) {
   return c == '[' || c == ']' || c == ',' || is_ws(c);
 }
-__device__ __forceinline__ bool is_numch(unsigned c) {
-  return (c >= '0' && c <= '9') || c == '-' || c == '+' || c == '.' || c == 'e' || c == 'E';
+
+// 10^k for 0 <= k <= 31 from its binary digits, in registers: a per-lane index into a __constant__
+// table is a vector memory load (hundreds of cycles per token), this is 5 selects + 4 multiplies.
+// Exact for k <= 22 (every partial product is a power of ten that a double represents exactly).
+__device__ __forceinline__ double pow10_exact(int k) {
+  const double a = (k & 1) ? 1e1 : 1.0, b = (k & 2) ? 1e2 : 1.0, c = (k & 4) ? 1e4 : 1.0,
+               d = (k & 8) ? 1e8 : 1.0, e = (k & 16) ? 1e16 : 1.0;
+  return ((a * b) * (c * d)) * e;
 }
 
-__constant__ double kPow10[23] = {1e0,  1e1,  1e2,  1e3,  1e4,  1e5,  1e6,  1e7,
-                                  1e8,  1e9,  1e10, 1e11, 1e12, 1e13, 1e14, 1e15,
-                                  1e16, 1e17, 1e18, 1e19, 1e20, 1e21, 1e22};
+// ---- 4-bytes-per-op classification ------------------------------------------------------------
+// Byte groups: g0 {\t \n \r} 0x01, g1 {' ' ','} 0x02, g2 {+ - .} 0x04, g3 digits 0x08,
+// g4 {E e} 0x10, g5 {[ ]} 0x20. class(c) = HI[c >> 4] & LO[c & 15] (0 for bytes >= 0x80):
+// delimiter = g0|g1|g5, number alphabet = g2|g3|g4, anything else is an invalid byte.
+constexpr uint32_t kHi03 = 0x08060001u, kHi47 = 0x00102010u;
+constexpr uint32_t kLo03 = 0x0808080Au, kLo47 = 0x08081808u, kLo8B = 0x24010908u,
+                   kLoCF = 0x00042502u;
+constexpr uint32_t kDelimG = 0x23232323u, kNumG = 0x1C1C1C1Cu, kDigitG = 0x08080808u;
 
-// The record text as seen by one workgroup: [lo, hi) is mirrored in LDS, anything else (a very
-// long token or a very long whitespace run) falls back to global memory.
+__device__ __forceinline__ uint32_t classify4(uint32_t x) {
+  const uint32_t hi = __builtin_amdgcn_perm(kHi47, kHi03, (x >> 4) & 0x07070707u);
+  const uint32_t l = x & 0x0F0F0F0Fu;
+  const uint32_t s = l & 0x07070707u;
+  const uint32_t p0 = __builtin_amdgcn_perm(kLo47, kLo03, s);
+  const uint32_t p1 = __builtin_amdgcn_perm(kLoCF, kLo8B, s);
+  const uint32_t m = ((l >> 3) & 0x01010101u) * 0xFFu;
+  const uint32_t lo = (m & p1) | (~m & p0);
+  const uint32_t ascii = ~(((x >> 7) & 0x01010101u) * 0xFFu);
+  return hi & lo & ascii;
+}
+
+// one bit per byte (bit j = byte j of x has a group bit in g): bytes of (cls & g) are < 0x80
+__device__ __forceinline__ uint32_t nz4(uint32_t cls, uint32_t g) {
+  const uint32_t t = ((cls & g) + 0x7F7F7F7Fu) & 0x80808080u;
+  return ((t >> 7) * 0x01020408u) >> 24;
+}
+
+struct Masks16 {
+  uint32_t delim, num, digit;  // 16-bit masks, bit j = byte j
+};
+
+__device__ __forceinline__ Masks16 classify16(uint32_t w0, uint32_t w1, uint32_t w2,
+                                              uint32_t w3) {
+  const uint32_t c0 = classify4(w0), c1 = classify4(w1), c2 = classify4(w2), c3 = classify4(w3);
+  Masks16 m;
+  m.delim = nz4(c0, kDelimG) | nz4(c1, kDelimG) << 4 | nz4(c2, kDelimG) << 8 |
+            nz4(c3, kDelimG) << 12;
+  m.num = nz4(c0, kNumG) | nz4(c1, kNumG) << 4 | nz4(c2, kNumG) << 8 | nz4(c3, kNumG) << 12;
+  m.digit = nz4(c0, kDigitG) | nz4(c1, kDigitG) << 4 | nz4(c2, kDigitG) << 8 |
+            nz4(c3, kDigitG) << 12;
+  return m;
+}
+
+// bits [a, b) of a 32-bit mask, 0 <= a, b <= 16
+__device__ __forceinline__ uint32_t bits_range(int a, int b) {
+  return b > a ? ((1u << b) - 1u) & ~((1u << a) - 1u) : 0u;
+}
+
+// valid-byte mask of the 16 bytes at p for the record extent [beg, end)
+__device__ __forceinline__ uint32_t valid16(int p, int beg, int end) {
+  return bits_range(min(max(beg - p, 0), 16), min(max(end - p, 0), 16));
+}
+
+// Packed masks of one 16-byte chunk at p: low half = delimiter bits (bytes outside the record
+// count as delimiters), high half = digit bits (inside the record).
+__device__ __forceinline__ uint32_t chunk_masks(const Masks16& m, int p, int beg, int end) {
+  const uint32_t vm = valid16(p, beg, end);
+  return ((m.delim | ~vm) & 0xFFFFu) | (m.digit & vm) << 16;
+}
+
+// Token starts of the lane's kChunks contiguous chunks at o and their packed chunk masks; *bad gets the
+// invalid bytes. prev_delim: the byte before o is a delimiter (or outside the record).
+__device__ __forceinline__ void token_starts(const uint4 (&v)[kChunks], int o, int beg, int end,
+                                             bool prev_delim, uint32_t (&st)[kChunks],
+                                             uint32_t (&cm)[kChunks], bool* bad) {
+  uint32_t carry = prev_delim ? 1u : 0u;
+  bool b = false;
+#pragma unroll
+  for (int i = 0; i < kChunks; ++i) {
+    const Masks16 m = classify16(v[i].x, v[i].y, v[i].z, v[i].w);
+    cm[i] = chunk_masks(m, o + 16 * i, beg, end);
+    const uint32_t dx = cm[i] & 0xFFFFu;
+    const uint32_t tokb = ~dx & 0xFFFFu;
+    b |= (tokb & ~m.num) != 0;
+    st[i] = tokb & ((dx << 1) | carry) & 0xFFFFu;
+    carry = dx >> 15;
+  }
+  *bad = b;
+}
+
+__device__ __forceinline__ int wave_sum_i(int v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+// ---- sequential (definitive) path ---------------------------------------------------------
+// The record text as seen by one wave: [lo, hi) is mirrored in LDS at text[q - lbase], anything
+// else (a very long token or whitespace run) falls back to global memory.
 struct Text {
   const uint8_t* g;
   const uint8_t* l;
-  int64_t lo, hi;
-  __device__ __forceinline__ unsigned at(int64_t q) const {
-    return (q >= lo && q < hi) ? (unsigned)l[q - lo] : (unsigned)g[q];
+  int lbase, lo, hi;
+  __device__ __forceinline__ unsigned at(int q) const {
+    return (q >= lo && q < hi) ? (unsigned)l[q - lbase] : (unsigned)g[q];
   }
 };
 
-// Token-start mask of the 16 bytes at p0 (bit j: byte p0+j starts a token); *badchar is set for a
-// byte inside [beg, end) that is neither a delimiter nor in the number alphabet.
-__device__ __forceinline__ unsigned token_mask(uint4 raw, unsigned prev, int64_t p0, int64_t beg,
-                                               int64_t end, bool* badchar) {
-  const uint32_t wd[4] = {raw.x, raw.y, raw.z, raw.w};
-  unsigned mask = 0;
-  bool bad = false;
-#pragma unroll
-  for (int j = 0; j < 16; ++j) {
-    const unsigned c = (wd[j >> 2] >> (8 * (j & 3))) & 0xff;
-    const int64_t pos = p0 + j;
-    if (pos >= beg && pos < end) {
-      if (!is_delim(c)) {
-        bad |= !is_numch(c);
-        if (is_delim(prev)) mask |= 1u << j;
-      }
-      prev = c;
-    }
-  }
-  *badchar = bad;
-  return mask;
+__device__ __forceinline__ float scale10(double mant, int exp10, bool neg) {
+  double v = mant;
+  if (mant == 0.0) v = 0.0;
+  else if (exp10 >= 0 && exp10 <= 22) v *= pow10_exact(exp10);
+  else if (exp10 < 0 && exp10 >= -22) v /= pow10_exact(-exp10);
+  else v *= pow(10.0, (double)exp10);
+  return (float)(neg ? -v : v);
 }
 
-// Strict JSON number -?(0|[1-9][0-9]*)(\.[0-9]+)?([eE][+-]?[0-9]+)? starting at i and ending at a
-// delimiter or `end`. *len receives the token length.
-__device__ float parse_number(const Text& t, int64_t i0, int64_t end, bool* ok, int* len) {
-  int64_t i = i0;
+// Strict JSON number starting at i0 and ending at a delimiter or `end`; *len = token length.
+__device__ float parse_number(const Text& t, int i0, int end, bool* ok, int* len) {
+  int i = i0;
   bool neg = false;
   unsigned c = i < end ? t.at(i) : 0u;
   if (c == '-') { neg = true; ++i; c = i < end ? t.at(i) : 0u; }
@@ -148,33 +238,37 @@ __device__ float parse_number(const Text& t, int64_t i0, int64_t end, bool* ok, 
     c = i < end ? t.at(i) : 0u;
   }
   *ok = good;
-  *len = (int)(i - i0);
-  if (!good) return 0.f;
-  double v = (double)mant;
-  if (mant == 0) v = 0.0;
-  else if (exp10 >= 0 && exp10 <= 22) v *= kPow10[exp10];
-  else if (exp10 < 0 && exp10 >= -22) v /= kPow10[-exp10];
-  else v *= pow(10.0, (double)exp10);
-  return (float)(neg ? -v : v);
+  *len = i - i0;
+  return good ? scale10((double)mant, exp10, neg) : 0.f;
+}
+
+// n / d for n < 2^32, d < 2^20 from a double reciprocal rd = 1/d: the product is below the true
+// quotient by < 1 (never above it by a whole unit), so one correction step is exact.
+__device__ __forceinline__ uint32_t udiv_rcp(uint32_t n, uint32_t d, double rd) {
+  uint32_t q = (uint32_t)((double)n * rd);
+  if (n - q * d >= d) ++q;
+  return q;
+}
+
+struct Dims {
+  uint32_t C, W, H;
+  double rC, rW, rH;
+};
+
+// number of array dimensions that close between element idx-1 and idx (idx > 0)
+__device__ __forceinline__ int wraps(uint32_t idx, const Dims& d) {
+  const uint32_t px = udiv_rcp(idx, d.C, d.rC);
+  if (idx - px * d.C) return 0;
+  const uint32_t row = udiv_rcp(px, d.W, d.rW);
+  if (px - row * d.W) return 1;
+  return (row - udiv_rcp(row, d.H, d.rH) * d.H) ? 2 : 3;
 }
 
 // Delimiters in front of token `idx` (scanning back from pos-1). Between tokens the text must be
-// ws* (']' ws*)^k ',' ws* ('[' ws*)^k with k = number of trailing dimensions that wrap.
-__device__ bool gap_ok(const Text& t, int64_t beg, int64_t pos, uint32_t idx, uint32_t C,
-                       uint32_t W, uint32_t H) {
-  int k = 0;
-  if (idx > 0) {  // (32-bit: a record holds < 2^32 numbers; 64-bit division is ~10x dearer)
-    const uint32_t px = idx / C;
-    if (idx - px * C) k = 0;
-    else {
-      const uint32_t row = px / W;
-      if (px - row * W) k = 1;
-      else if (row % H) k = 2;
-      else k = 3;
-    }
-  }
+// ws* (']' ws*)^k ',' ws* ('[' ws*)^k with k = wraps(idx).
+__device__ bool gap_ok(const Text& t, int beg, int pos, uint32_t idx, int k) {
   int opens = 0, closes = 0, commas = 0;
-  int64_t q = pos - 1;
+  int q = pos - 1;
   for (; q >= beg; --q) {
     const unsigned c = t.at(q);
     if (is_ws(c)) continue;
@@ -196,9 +290,9 @@ __device__ bool gap_ok(const Text& t, int64_t beg, int64_t pos, uint32_t idx, ui
 }
 
 // After the last token: ws* (']' ws*)^4 up to the end of the array text.
-__device__ bool tail_ok(const Text& t, int64_t pos, int64_t end) {
+__device__ bool tail_ok(const Text& t, int pos, int end) {
   int closes = 0;
-  for (int64_t q = pos; q < end; ++q) {
+  for (int q = pos; q < end; ++q) {
     const unsigned c = t.at(q);
     if (is_ws(c)) continue;
     if (c != ']') return false;
@@ -207,112 +301,239 @@ __device__ bool tail_ok(const Text& t, int64_t pos, int64_t end) {
   return closes == 4;
 }
 
-__device__ __forceinline__ int block_sum(int v, int* red) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+// ---- window (fast) path ---------------------------------------------------------------------
+__device__ __forceinline__ uint32_t byte_at(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3,
+                                            int k) {
+  const uint32_t lo = (k & 4) ? w1 : w0;
+  const uint32_t hi = (k & 4) ? w3 : w2;
+  return (((k & 8) ? hi : lo) >> ((k & 3) * 8)) & 0xFFu;
+}
+
+// Parses the token at LDS offset x from a 16-byte window; m0/m1 = packed masks of the chunk
+// holding the token start and the next one, off = the start's offset in its chunk. Returns false
+// when the window cannot decide (the caller then runs parse_number).
+__device__ __forceinline__ bool parse_window(const uint8_t* text, int x, uint32_t m0, uint32_t m1,
+                                             int off, float* out) {
+  const uint32_t* tw = reinterpret_cast<const uint32_t*>(text) + (x >> 2);
+  const uint32_t sh = (uint32_t)(x & 3);
+  const uint32_t d0 = tw[0], d1 = tw[1], d2 = tw[2], d3 = tw[3], d4 = tw[4];
+  const uint32_t w0 = __builtin_amdgcn_alignbyte(d1, d0, sh);
+  const uint32_t w1 = __builtin_amdgcn_alignbyte(d2, d1, sh);
+  const uint32_t w2 = __builtin_amdgcn_alignbyte(d3, d2, sh);
+  const uint32_t w3 = __builtin_amdgcn_alignbyte(d4, d3, sh);
+  const uint32_t delim = (((m1 << 16) | (m0 & 0xFFFFu)) >> off) & 0xFFFFu;
+  const uint32_t D = (((m1 & 0xFFFF0000u) | (m0 >> 16)) >> off) & 0xFFFFu;
+  const uint32_t tok = ~delim & 0xFFFFu;
+  const int L = __builtin_ctz(~tok);  // token length (a delimiter or the record end follows)
+  if (L >= 16) return false;
+  const int s = byte_at(w0, w1, w2, w3, 0) == '-' ? 1 : 0;
+  const int ie = s + __builtin_ctz(~(D >> s));
+  bool ok = ie > s && !(byte_at(w0, w1, w2, w3, s) == '0' && ie > s + 1);
+  int fb = ie, fe = ie;
+  if (byte_at(w0, w1, w2, w3, ie) == '.' && ie < L) {
+    fb = ie + 1;
+    fe = fb + __builtin_ctz(~(D >> fb));
+    ok &= fe > fb;
+  }
+  int eb = fe, ee = fe;
+  bool eneg = false;
+  const uint32_t ce = byte_at(w0, w1, w2, w3, fe);
+  if (fe < L && (ce == 'e' || ce == 'E')) {
+    int p = fe + 1;
+    const uint32_t c2 = byte_at(w0, w1, w2, w3, p);
+    if (p < L && (c2 == '+' || c2 == '-')) {
+      eneg = c2 == '-';
+      ++p;
+    }
+    eb = p;
+    ee = p + __builtin_ctz(~(D >> p));
+    ok &= ee > eb;
+  }
+  if (!ok || ee != L) return false;
+  const uint32_t mm = bits_range(s, ie) | bits_range(fb, fe);  // mantissa digits
+  // <= 15 mantissa digits (the window): exact in a 64-bit accumulator and in a double
+  uint64_t a = 0;
+  const uint32_t wd[4] = {w0, w1, w2, w3};
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  if (lane == 0) red[wave] = v;
-  __syncthreads();
-  const int s = red[0] + red[1] + red[2] + red[3];
-  __syncthreads();
-  return s;
+  for (int j = 0; j < 15; ++j) {
+    const uint32_t d = ((wd[j >> 2] >> ((j & 3) * 8)) & 0xFFu) - '0';
+    a = ((mm >> j) & 1u) ? a * 10u + d : a;
+  }
+  uint32_t e = 0;
+  for (int p = eb; p < ee; ++p)
+    if (e < 100000u) e = e * 10u + (byte_at(w0, w1, w2, w3, p) - '0');
+  const double mant = (double)a;
+  const int exp10 = (eneg ? -(int)e : (int)e) - (fe - fb);
+  *out = scale10(mant, exp10, s != 0);
+  return true;
+}
+
+// The k-wrap separator (",", "],[", "]],[[", "]]],[[[") directly in front of x with a digit
+// before it; false = undecided (whitespace, other bytes): the caller runs gap_ok.
+__device__ __forceinline__ bool gap_window(const uint8_t* text, int x, int k) {
+  const uint32_t* tw = reinterpret_cast<const uint32_t*>(text) + ((x - 8) >> 2);
+  const uint32_t sh = (uint32_t)(x & 3);
+  const uint32_t d0 = tw[0], d1 = tw[1], d2 = tw[2];
+  const uint64_t g = (uint64_t)__builtin_amdgcn_alignbyte(d2, d1, sh) << 32 |
+                     __builtin_amdgcn_alignbyte(d1, d0, sh);  // bytes x-8 .. x-1
+  const int plen = 2 * k + 1;
+  const uint64_t pat = k == 0 ? 0x2Cull : k == 1 ? 0x5B2C5Dull
+                     : k == 2 ? 0x5B5B2C5D5Dull : 0x5B5B5B2C5D5D5Dull;
+  if ((g >> (8 * (8 - plen))) != pat) return false;
+  const uint32_t prev = (uint32_t)(g >> (8 * (7 - plen))) & 0xFFu;
+  return prev - '0' < 10u;
 }
 
 __global__ __launch_bounds__(256) void json_count_kernel(JsonRecord* recs, const int* tile_rec,
-                                                         const uint8_t* bytes, int* counts) {
-  __shared__ int red[4];
-  const int t = blockIdx.x;
+                                                         int ntiles, const uint8_t* bytes,
+                                                         int* counts) {
+  const int lane = threadIdx.x & 63;
+  const int t = blockIdx.x * kWaves + (threadIdx.x >> 6);
+  if (t >= ntiles) return;  // (no workgroup barriers in this kernel)
   const int ri = tile_rec[t];
   const JsonRecord r = recs[ri];
-  const int64_t beg = r.off, end = r.off + r.len;
-  const int64_t t0 = (beg & ~(int64_t)15) + (int64_t)(t - r.tile0) * kTile;
-  const int64_t p0 = t0 + 16 * threadIdx.x;
-  int cnt = 0;
-  bool bad = false;
-  if (p0 < end) {
-    const uint4 raw = *reinterpret_cast<const uint4*>(bytes + p0);
-    const unsigned prev = (p0 > beg) ? bytes[p0 - 1] : '[';
-    cnt = __popc(token_mask(raw, prev, p0, beg, end, &bad));
-  }
+  const int64_t abeg = r.off & ~(int64_t)15;
+  const uint8_t* rb = bytes + abeg;
+  const int beg = (int)(r.off - abeg), end = beg + r.len;
+  const int o = (t - r.tile0) * kTile + kLaneBytes * lane;
+  uint4 v[kChunks];
+#pragma unroll
+  for (int i = 0; i < kChunks; ++i)
+    v[i] = (o + 16 * i < end) ? *reinterpret_cast<const uint4*>(rb + o + 16 * i)
+                              : make_uint4(0, 0, 0, 0);
+  unsigned prevb = __shfl_up(v[kChunks - 1].w >> 24, 1, 64);
+  if (lane == 0 && o - 1 >= beg) prevb = rb[o - 1];
+  const bool pd = (o - 1 < beg) || is_delim(prevb);
+  uint32_t st[kChunks], cm[kChunks];
+  bool bad;
+  token_starts(v, o, beg, end, pd, st, cm, &bad);
+  int lc = 0;
+#pragma unroll
+  for (int i = 0; i < kChunks; ++i) lc += __builtin_popcount(st[i]);
+  const int cnt = wave_sum_i(lc);
+  if (lane == 0) counts[t] = cnt;
   if (bad) atomicMax(&recs[ri].status, 2);
-  cnt = block_sum(cnt, red);
-  if (threadIdx.x == 0) counts[t] = cnt;
 }
 
 __global__ __launch_bounds__(256) void json_parse_kernel(JsonRecord* recs, const int* tile_rec,
-                                                         const uint8_t* bytes, int H, int W,
-                                                         int C, const int* counts, float* out) {
-  __shared__ __attribute__((aligned(16))) uint8_t text[kTile + 2 * kHalo];
-  __shared__ int red[4];
-  __shared__ int wave_tot[4];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int t = blockIdx.x;
+                                                         int ntiles, const uint8_t* bytes, int H,
+                                                         int W, int C, const int* counts,
+                                                         float* out) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds_text[kWaves][kText];
+  __shared__ uint16_t lds_tok[kWaves][kMaxTok];
+  __shared__ uint32_t lds_cm[kWaves][kTile / 16 + 1];  // packed masks of the tile's chunks + 1
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int t = blockIdx.x * kWaves + wave;
+  if (t >= ntiles) return;  // (waves only share LDS regions of their own: no barriers)
+  uint8_t* text = lds_text[wave];
+  uint16_t* tok = lds_tok[wave];
+  uint32_t* cmk = lds_cm[wave];
   const int ri = tile_rec[t];
   const JsonRecord r = recs[ri];
+  const int64_t abeg = r.off & ~(int64_t)15;
+  const uint8_t* rb = bytes + abeg;
+  const int beg = (int)(r.off - abeg), end = beg + r.len;
+  const int aend = (end + 15) & ~15;
   const int per_image = H * W * C;
-  const int64_t beg = r.off, end = r.off + r.len;
-  const int64_t abeg = beg & ~(int64_t)15;
-  const int64_t expected = (int64_t)r.images * per_image;
-  const int64_t t0 = abeg + (int64_t)(t - r.tile0) * kTile;
-  const int ntiles = (int)((end - abeg + kTile - 1) / kTile);
-  const bool last_tile = (t - r.tile0) == ntiles - 1;
+  const int expected = r.images * per_image;
+  const int tl = t - r.tile0;
+  const int t0 = tl * kTile;
+  const bool last_tile = t0 + kTile >= end;
 
   // stage [t0 - halo, t0 + tile + halo) clipped to the record's 16-byte-aligned extent
   Text tx;
-  tx.g = bytes;
+  tx.g = rb;
   tx.l = text;
-  tx.lo = t0 - kHalo < abeg ? abeg : t0 - kHalo;
-  const int64_t aend = (end + 15) & ~(int64_t)15;
-  tx.hi = t0 + kTile + kHalo > aend ? aend : t0 + kTile + kHalo;
-  for (int64_t q = tx.lo + 16 * tid; q < tx.hi; q += 16 * 256)
-    *reinterpret_cast<uint4*>(text + (q - tx.lo)) = *reinterpret_cast<const uint4*>(bytes + q);
+  tx.lbase = t0 - kHalo;
+  tx.lo = max(t0 - kHalo, 0);
+  tx.hi = min(t0 + kTile + kHalo, aend);
+  for (int q = tx.lo + 16 * lane; q < tx.hi; q += 16 * 64)
+    *reinterpret_cast<uint4*>(text + (q - tx.lbase)) = *reinterpret_cast<const uint4*>(rb + q);
 
-  // first token index of this tile: the counts of the record's earlier tiles
+  // first element index of this tile: the token counts of the record's earlier tiles
   int part = 0;
-  for (int k = r.tile0 + tid; k < t; k += 256) part += counts[k];
-  const int64_t base_idx = block_sum(part, red);  // (its barriers also publish the LDS text)
+  for (int k = r.tile0 + lane; k < t; k += 64) part += counts[k];
+  const int base = wave_sum_i(part);
+  wave_lds_sync();
 
-  const int64_t p0 = t0 + 16 * tid;
-  uint4 raw = make_uint4(0, 0, 0, 0);
-  unsigned mask = 0;
+  // token starts of this lane's 64 bytes, then a wave prefix sum -> local token indices
+  const int o = t0 + kLaneBytes * lane;
+  uint4 v[kChunks];
+#pragma unroll
+  for (int i = 0; i < kChunks; ++i)
+    v[i] = (o + 16 * i < end) ? *reinterpret_cast<const uint4*>(text + (o + 16 * i - tx.lbase))
+                              : make_uint4(0, 0, 0, 0);
+  const bool pd = (o - 1 < beg) || is_delim(text[o - 1 - tx.lbase]);
+  uint32_t st[kChunks], cm[kChunks];
   bool bad_ignored;
-  if (p0 < end) {
-    raw = *reinterpret_cast<const uint4*>(text + (p0 - tx.lo));
-    const unsigned prev = (p0 > beg) ? tx.at(p0 - 1) : '[';
-    mask = token_mask(raw, prev, p0, beg, end, &bad_ignored);
+  token_starts(v, o, beg, end, pd, st, cm, &bad_ignored);
+#pragma unroll
+  for (int i = 0; i < kChunks; ++i) cmk[kChunks * lane + i] = cm[i];
+  if (lane == 63) {  // the chunk after the tile (a window of the tile's last tokens reaches it)
+    const int p = t0 + kTile;
+    const uint4 h = p < end ? *reinterpret_cast<const uint4*>(text + (p - tx.lbase))
+                            : make_uint4(0, 0, 0, 0);
+    cmk[kTile / 16] = chunk_masks(classify16(h.x, h.y, h.z, h.w), p, beg, end);
   }
-  const int cnt = __popc(mask);
+  int cnt = 0;
+#pragma unroll
+  for (int i = 0; i < kChunks; ++i) cnt += __builtin_popcount(st[i]);
   int inc = cnt;
 #pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int v = __shfl_up(inc, o, 64);
-    if (lane >= o) inc += v;
+  for (int d = 1; d < 64; d <<= 1) {
+    const int u = __shfl_up(inc, d, 64);
+    if (lane >= d) inc += u;
   }
-  if (lane == 63) wave_tot[wave] = inc;
-  __syncthreads();
-  int wbase = 0, total = 0;
+  const int ntok = __shfl(inc, 63, 64);
+  int li = inc - cnt;
 #pragma unroll
-  for (int w = 0; w < 4; ++w) {
-    if (w < wave) wbase += wave_tot[w];
-    total += wave_tot[w];
+  for (int i = 0; i < kChunks; ++i) {
+    uint32_t s = st[i];
+    while (s) {
+      const int j = __builtin_ctz(s);
+      s &= s - 1;
+      tok[li++] = (uint16_t)(o + 16 * i + j - tx.lbase);
+    }
   }
-  int64_t idx = base_idx + wbase + inc - cnt;
+  wave_lds_sync();
+
+  // parse: lane handles tokens lane, lane + 64, ... (consecutive lanes -> consecutive elements)
+  Dims dims;
+  dims.C = (uint32_t)C; dims.W = (uint32_t)W; dims.H = (uint32_t)H;
+  dims.rC = 1.0 / C; dims.rW = 1.0 / W; dims.rH = 1.0 / H;
   float* dst = out + (int64_t)r.slot * per_image;
   int bad = 0;
-  while (mask) {
-    const int j = __ffs(mask) - 1;
-    mask &= mask - 1;
-    const int64_t pos = p0 + j;
-    bool ok = true;
+  for (int j = lane; j < ntok; j += 64) {
+    const int x = tok[j];
+    const int pos = x + tx.lbase;
+    const int idx = base + j;
+    float val;
     int len = 0;
-    const float v = parse_number(tx, pos, end, &ok, &len);
-    if (!ok) bad = max(bad, 2);
-    else if (!gap_ok(tx, beg, pos, (uint32_t)idx, (uint32_t)C, (uint32_t)W, (uint32_t)H)) bad = 3;
-    else if (idx == expected - 1 && !tail_ok(tx, pos + len, end)) bad = 3;
-    if (idx < expected) dst[idx] = v;
-    ++idx;
+    bool ok;
+    const int ci = (pos - t0) >> 4;
+    if (parse_window(text, x, cmk[ci], cmk[ci + 1], pos & 15, &val)) {
+      ok = true;
+      len = -1;  // only the last element needs its length (tail check)
+    } else {
+      ok = false;
+      val = parse_number(tx, pos, end, &ok, &len);
+    }
+    if (!ok) {
+      bad = max(bad, 2);
+    } else {
+      const int k = idx > 0 ? wraps((uint32_t)idx, dims) : 0;
+      const bool fast_gap = idx > 0 && pos - 8 >= tx.lo && pos - (2 * k + 2) >= beg &&
+                            gap_window(text, x, k);
+      if (!fast_gap && !gap_ok(tx, beg, pos, (uint32_t)idx, k)) {
+        bad = 3;
+      } else if (idx == expected - 1) {
+        if (len < 0) parse_number(tx, pos, end, &ok, &len);
+        if (!tail_ok(tx, pos + len, end)) bad = 3;
+      }
+    }
+    if (idx < expected) dst[idx] = val;
   }
-  if (last_tile && tid == 0 && base_idx + total != expected) bad = max(bad, 1);
+  if (last_tile && lane == 0 && base + ntok != expected) bad = max(bad, 1);
   if (bad) atomicMax(&recs[ri].status, bad);
 }
 
@@ -329,10 +550,11 @@ hipError_t json_parse_instances(int nrec, int ntiles, JsonRecord* recs, const in
                                 float* out, hipStream_t stream) {
   if (nrec <= 0 || ntiles <= 0) return hipSuccess;
   if (H <= 0 || W <= 0 || C <= 0) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(json_count_kernel, dim3(ntiles), dim3(256), 0, stream, recs, tile_rec, bytes,
-                     tile_counts);
-  hipLaunchKernelGGL(json_parse_kernel, dim3(ntiles), dim3(256), 0, stream, recs, tile_rec, bytes,
-                     H, W, C, tile_counts, out);
+  const int blocks = (ntiles + kWaves - 1) / kWaves;
+  hipLaunchKernelGGL(json_count_kernel, dim3(blocks), dim3(64 * kWaves), 0, stream, recs,
+                     tile_rec, ntiles, bytes, tile_counts);
+  hipLaunchKernelGGL(json_parse_kernel, dim3(blocks), dim3(64 * kWaves), 0, stream, recs,
+                     tile_rec, ntiles, bytes, H, W, C, tile_counts, out);
   return hipGetLastError();
 }
 
