@@ -51,6 +51,7 @@ ConvDesc desc_from_dict(const py::dict& d) {
   c.in_scale = get_or<float>(d, "in_scale", 1.0f);
   c.out_scale = get_or<float>(d, "out_scale", 1.0f);
   c.res_scale = get_or<float>(d, "res_scale", 1.0f);
+  c.stem = get_or<int>(d, "stem", 0);
   return c;
 }
 
@@ -96,6 +97,13 @@ PYBIND11_MODULE(_C, m) {
         },
         py::arg("desc"), py::arg("batch"), py::arg("x"), py::arg("w"), py::arg("bias"),
         py::arg("wscale"), py::arg("res"), py::arg("y"), py::arg("stream"));
+  m.def("stem_pack",
+        [](int batch, int H, int W, int C, int Wp, int lp, uintptr_t x, uintptr_t y,
+           uintptr_t stream) {
+          chk(gale::stem_pack(batch, H, W, C, Wp, lp, static_cast<const float*>(P(x)), P(y),
+                              S(stream)),
+              "stem_pack");
+        });
   m.def("maxpool2d",
         [](int batch, int H, int W, int C, int k, int s, int p, int Ho, int Wo, uintptr_t x,
            uintptr_t y, uintptr_t stream, int fp8) {
@@ -145,6 +153,8 @@ PYBIND11_MODULE(_C, m) {
               "json_parse_instances");
         });
   m.def("json_tile_count", &gale::json_tile_count);
+  m.def("set_conv_path", &gale::set_conv_path);
+  m.def("conv_path", &gale::conv_path);
   m.attr("JSON_TILE_BYTES") = gale::kJsonTileBytes;
   m.attr("JSON_RECORD_BYTES") = (int)sizeof(gale::JsonRecord);
   m.def("memcpy_async",

@@ -26,6 +26,7 @@ enum OpKind : int {
   OP_SOFTMAX = 4,   // p[0] = N, p[1] = ld
   OP_RESNET20 = 5,  // whole-network fused CIFAR ResNet-20; ptrs = 19 w, 19 b, fc_w, fc_b
                     // (+ 19 wscale for fp8), scales = 19 s_in, 19 s_out, 19 s_res (fp8)
+  OP_STEM_PACK = 6, // p[0..4] = H, W, C, Wp, lp  (fp32 input -> packed-stem bf16 image)
 };
 
 // Buffer ids: 0 = network input (fp32 NHWC), 1 = network output (fp32 [B, classes]),

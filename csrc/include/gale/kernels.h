@@ -33,6 +33,11 @@ struct ConvDesc {
   float in_scale;       // fp8: input scale (in_f32: the input is quantised with this step)
   float out_scale;      // fp8: output scale (ignored for out_f32)
   float res_scale;      // fp8: residual scale
+  // 1 = packed-stem layout (ResNet-50 7x7/2 stem, bf16): x is the stem_pack() image
+  // [B][H][W][4] bf16 with W = 2*Wo + 6 (3 zero columns left, the rest right), the packed weights
+  // are [Npad][256] with k = kh*32 + kw*4 + c over an 8x8x4 zero-padded kernel (KH = KW = 8,
+  // K = Kpad = 256), so each kernel row of one output pixel is ONE 64-byte run of x.
+  int stem;
 };
 
 // y[B,Ho,Wo,Cout] = act(conv(x, w) + bias (+ residual)).
@@ -42,6 +47,20 @@ struct ConvDesc {
 // (x fp32 when in_f32, y fp32 when out_f32).
 hipError_t conv2d(const ConvDesc& d, int batch, const void* x, const void* w, const float* bias,
                   const float* wscale, const void* res, void* y, hipStream_t stream);
+
+// The LDS-pipelined implicit-GEMM path (conv_gemm.hip) for wide bf16 layers; conv2d() routes
+// there by itself when conv_gemm_supported() holds.
+bool conv_gemm_supported(const ConvDesc& d, int batch, bool has_res);
+// conv path selection (tests / A-B benches): 0 auto, 1 never GEMM, 2 GEMM whenever the shape allows
+void set_conv_path(int mode);
+int conv_path();
+hipError_t conv2d_gemm(const ConvDesc& d, int batch, const void* x, const void* w,
+                       const float* bias, const void* res, void* y, hipStream_t stream);
+
+// fp32 NHWC [B][H][W][C<=4] -> bf16 [B][H][Wp][4] with `lp` zero columns on the left (and zeros
+// up to Wp on the right, channels >= C zero): the input of a packed-stem conv (ConvDesc::stem).
+hipError_t stem_pack(int batch, int H, int W, int C, int Wp, int lp, const float* x, void* y,
+                     hipStream_t stream);
 
 // Max pooling, NHWC bf16 (or e4m3 when fp8; the scale passes through), window k, stride s,
 // -inf padding p.

@@ -1,0 +1,301 @@
+// LDS-pipelined implicit-GEMM convolution for the wide layers (Cin % 64 == 0, bf16): the
+// ResNet-50 body (BASELINE config 4). conv_mfma.hip keeps the small-channel / odd-shaped layers.
+//
+// GEMM view (NHWC, swapped so every lane owns 4 consecutive output channels of one pixel):
+//   D[channel n][pixel m] = sum_k W[n][k] * X[m][k],  k = (kh*KW + kw)*Cin + ci
+// Both operands are K-contiguous rows, so one workgroup tile step stages
+//   * BM pixel rows x 64 k  (the im2col rows of one tap (kh, kw) and 64 input channels: one
+//     contiguous 128-B run of the NHWC input per pixel, or zeros for a padding tap), and
+//   * BN weight rows x 64 k,
+// with global_load_lds_dwordx4 (LDS-DMA, no VGPR round trip): 8 lanes per 128-B row, one
+// wave-instruction = 8 rows = 1 KiB of LDS. The LDS image is lane-linear, so the bank swizzle is
+// applied on the SOURCE side (cdna_hip_programming.md §5.4 rule 21): LDS slot s of row r holds the
+// global 16-B chunk s ^ ((r >> 1) & 7), and fragment reads apply the same involution; 16 lanes
+// reading 16 consecutive rows at one chunk then hit 16 distinct 4-bank groups (conflict-free).
+// Padding taps and rows past M point their source at a zero block.
+// Pipeline: two LDS stages, one barrier per 64-deep k-step; the DMA of step k+1 is issued right
+// after the barrier and lands while the MFMAs of step k run (v_mfma_f32_16x16x32_bf16, each wave
+// owning a (BN/2) x 64 sub-tile = TN x TM 16x16 accumulators).
+// Epilogue: folded-BN bias + identity residual + ReLU, bf16 NHWC, 8-byte stores.
+// Grid: one workgroup per (pixel tile, channel tile), remapped so the tiles of one XCD are
+// contiguous (T1): the channel tiles of a pixel tile, which re-read the same im2col rows, share an L2.
+#include "common.cuh"
+#include "gale/kernels.h"
+
+namespace gale {
+namespace {
+
+__device__ __attribute__((aligned(16))) uint8_t g_zero_rows[64];  // source of padding rows
+
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+typedef __attribute__((address_space(1))) void* gbl_ptr_t;
+
+struct GemmConvArgs {
+  const bf16* x;
+  const bf16* w;
+  const float* bias;
+  const bf16* res;
+  bf16* y;
+  int M, H, W, Cin, HWo, Wo, Cout, KW, stride, pad, Kpad;
+  int nkb;         // 64-deep k-steps = KH*KW*Cin / 64
+  int cin_blocks;  // Cin / 64
+  int relu, has_res;
+  int n_tiles, nwg;
+};
+
+__device__ __forceinline__ void glds16(const void* src, void* lds_base) {
+  __builtin_amdgcn_global_load_lds((gbl_ptr_t)(src), (lds_ptr_t)(lds_base), 16, 0, 0);
+}
+
+// STEM: the packed-stem layout (ConvDesc::stem): k-step kb covers kernel rows 2kb and 2kb+1, a
+// lane's 16-B chunk c reads row kh = 2kb + (c >> 2), bytes 16*(c & 3) of the 64-B run that
+// starts at column 2*wo of the padded image (columns never leave it, rows may: zero rows).
+template <int BM, int BN, bool STEM>
+__global__ __launch_bounds__(256, 2) void conv_gemm_kernel(GemmConvArgs a) {
+  constexpr int WM = 2, WN = 2;                 // 4 waves as 2 (pixels) x 2 (channels)
+  constexpr int TM = BM / WM / 16;              // 16-pixel tiles per wave
+  constexpr int TN = BN / WN / 16;              // 16-channel tiles per wave
+  constexpr int XI = BM / 32;                   // X wave-instructions (8 rows each) per wave
+  constexpr int WI = BN / 32;                   // W wave-instructions per wave
+  constexpr int STAGE = (BM + BN) * 128;        // bytes per LDS stage
+  __shared__ __attribute__((aligned(1024))) uint8_t lds[2 * STAGE];
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+
+  // XCD-contiguous tile order (bijective for any nwg)
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, q = a.nwg >> 3, r8 = a.nwg & 7;
+  const int rid = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + (bid >> 3);
+  const int mt = rid / a.n_tiles, nt = rid - mt * a.n_tiles;
+
+  // ---- per-lane staging sources ----
+  const int srow = lane >> 3;                   // row within a wave-instruction's 8 rows
+  const int slot = lane & 7;
+  int xoff[XI], xh[XI], xw[XI];
+#pragma unroll
+  for (int j = 0; j < XI; ++j) {
+    const int row = (wave * XI + j) * 8 + srow;
+    const int m = mt * BM + row;
+    const int chunk = slot ^ ((row >> 1) & 7);
+    if (m < a.M) {
+      const int n = m / a.HWo;
+      const int rem = m - n * a.HWo;
+      const int ho = rem / a.Wo;
+      const int wo = rem - ho * a.Wo;
+      if (STEM) {
+        xoff[j] = n * a.H * a.W * 4 + wo * 8 + (chunk & 3) * 8;
+        xh[j] = ho * 2 - a.pad + (chunk >> 2);
+        xw[j] = 0;
+      } else {
+        xoff[j] = n * a.H * a.W * a.Cin + chunk * 8;
+        xh[j] = ho * a.stride - a.pad;
+        xw[j] = wo * a.stride - a.pad;
+      }
+    } else {
+      xoff[j] = 0;
+      xh[j] = -(1 << 20);  // every tap out of bounds -> zero rows
+      xw[j] = 0;
+    }
+  }
+  const bf16* wsrc[WI];
+#pragma unroll
+  for (int j = 0; j < WI; ++j) {
+    const int row = (wave * WI + j) * 8 + srow;
+    const int chunk = slot ^ ((row >> 1) & 7);
+    wsrc[j] = a.w + (size_t)(nt * BN + row) * a.Kpad + chunk * 8;
+  }
+
+  auto stage = [&](int kb, uint8_t* buf) {
+    if (STEM) {
+#pragma unroll
+      for (int j = 0; j < XI; ++j) {
+        const int hi = xh[j] + 2 * kb;
+        const void* src = (unsigned)hi < (unsigned)a.H
+                              ? (const void*)(a.x + xoff[j] + hi * a.W * 4)
+                              : (const void*)(g_zero_rows + 16 * (lane & 3));
+        glds16(src, buf + (wave * XI + j) * 1024);
+      }
+#pragma unroll
+      for (int j = 0; j < WI; ++j)
+        glds16(wsrc[j] + kb * 64, buf + BM * 128 + (wave * WI + j) * 1024);
+      return;
+    }
+    const int tap = kb / a.cin_blocks;
+    const int cb = kb - tap * a.cin_blocks;
+    const int kh = tap / a.KW;
+    const int kw = tap - kh * a.KW;
+#pragma unroll
+    for (int j = 0; j < XI; ++j) {
+      const int hi = xh[j] + kh, wi = xw[j] + kw;
+      const bool ok = (unsigned)hi < (unsigned)a.H && (unsigned)wi < (unsigned)a.W;
+      const void* src = ok ? (const void*)(a.x + xoff[j] + (hi * a.W + wi) * a.Cin + cb * 64)
+                           : (const void*)(g_zero_rows + 16 * (lane & 3));
+      glds16(src, buf + (wave * XI + j) * 1024);
+    }
+#pragma unroll
+    for (int j = 0; j < WI; ++j)
+      glds16(wsrc[j] + kb * 64, buf + BM * 128 + (wave * WI + j) * 1024);
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int t = 0; t < TN; ++t) acc[i][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // fragment read offsets (row part; the chunk part depends on the k-step)
+  const int fr = lane & 15, fq = lane >> 4;
+  int xrow_off[TM], wrow_off[TN], xsw[TM], wsw[TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int row = wm * (BM / WM) + i * 16 + fr;
+    xrow_off[i] = row * 128;
+    xsw[i] = (row >> 1) & 7;
+  }
+#pragma unroll
+  for (int t = 0; t < TN; ++t) {
+    const int row = wn * (BN / WN) + t * 16 + fr;
+    wrow_off[t] = BM * 128 + row * 128;
+    wsw[t] = (row >> 1) & 7;
+  }
+
+  stage(0, lds);
+  for (int kb = 0; kb < a.nkb; ++kb) {
+    __syncthreads();  // step kb has landed (vmcnt(0)); every wave is done reading step kb-1
+    uint8_t* cur = lds + (kb & 1) * STAGE;
+    if (kb + 1 < a.nkb) stage(kb + 1, lds + ((kb + 1) & 1) * STAGE);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int chunk = kk * 4 + fq;
+      bf16x8 af[TN], bfr[TM];
+#pragma unroll
+      for (int t = 0; t < TN; ++t)
+        af[t] = *reinterpret_cast<const bf16x8*>(cur + wrow_off[t] + ((chunk ^ wsw[t]) << 4));
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+        bfr[i] = *reinterpret_cast<const bf16x8*>(cur + xrow_off[i] + ((chunk ^ xsw[i]) << 4));
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int t = 0; t < TN; ++t)
+          acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[t], bfr[i], acc[i][t], 0, 0, 0);
+    }
+  }
+
+  // ---- epilogue: lane owns channels c..c+3 of pixel m for every (i, t) ----
+#pragma unroll
+  for (int t = 0; t < TN; ++t) {
+    const int c = nt * BN + wn * (BN / WN) + t * 16 + fq * 4;
+    if (c >= a.Cout) continue;
+    const float4 b = *reinterpret_cast<const float4*>(a.bias + c);
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int m = mt * BM + wm * (BM / WM) + i * 16 + fr;
+      if (m >= a.M) continue;
+      const size_t o = (size_t)m * a.Cout + c;
+      float v0 = acc[i][t][0] + b.x, v1 = acc[i][t][1] + b.y;
+      float v2 = acc[i][t][2] + b.z, v3 = acc[i][t][3] + b.w;
+      if (a.has_res) {
+        const bf16x4 rr = __builtin_bit_cast(bf16x4, *reinterpret_cast<const uint2*>(a.res + o));
+        v0 += (float)rr[0]; v1 += (float)rr[1]; v2 += (float)rr[2]; v3 += (float)rr[3];
+      }
+      if (a.relu) {
+        v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f); v2 = fmaxf(v2, 0.f); v3 = fmaxf(v3, 0.f);
+      }
+      bf16x4 ov;
+      ov[0] = (bf16)v0; ov[1] = (bf16)v1; ov[2] = (bf16)v2; ov[3] = (bf16)v3;
+      *reinterpret_cast<uint2*>(a.y + o) = __builtin_bit_cast(uint2, ov);
+    }
+  }
+}
+
+}  // namespace
+
+static int g_conv_path = 0;  // 0 auto, 1 never the GEMM path, 2 GEMM path whenever the shape allows
+void set_conv_path(int mode) { g_conv_path = mode; }
+int conv_path() { return g_conv_path; }
+
+bool conv_gemm_supported(const ConvDesc& d, int batch, bool has_res) {
+  if (g_conv_path == 1) return false;
+  if (d.fp8 || d.in_f32 || d.out_f32) return false;
+  if (d.Cin % 64 != 0 || d.Cout % 64 != 0 || d.K != d.KH * d.KW * d.Cin || d.Kpad != d.K)
+    return false;
+  const int bn = (d.Cout % 128 == 0) ? 128 : 64;
+  if (d.Npad % bn != 0) return false;
+  if (has_res && (d.res_C != d.Cout || d.res_stride != 1 || d.res_H != d.Ho || d.res_W != d.Wo))
+    return false;
+  // enough workgroups to fill the chip (small late-stage layers at small batch keep conv_mfma)
+  const long long m = (long long)batch * d.Ho * d.Wo;
+  if (m >= (1ll << 31) || (long long)batch * d.H * d.W * d.Cin >= (1ll << 31)) return false;
+  const long long tiles = ((m + 127) / 128) * (d.Cout / bn);
+  return g_conv_path == 2 || tiles >= 1;
+}
+
+hipError_t conv2d_gemm(const ConvDesc& d, int batch, const void* x, const void* w,
+                       const float* bias, const void* res, void* y, hipStream_t stream) {
+  GemmConvArgs a;
+  a.x = static_cast<const bf16*>(x);
+  a.w = static_cast<const bf16*>(w);
+  a.bias = bias;
+  a.res = static_cast<const bf16*>(res);
+  a.y = static_cast<bf16*>(y);
+  a.M = batch * d.Ho * d.Wo;
+  a.H = d.H; a.W = d.W; a.Cin = d.Cin; a.HWo = d.Ho * d.Wo; a.Wo = d.Wo; a.Cout = d.Cout;
+  a.KW = d.KW; a.stride = d.stride; a.pad = d.pad; a.Kpad = d.Kpad;
+  a.nkb = d.K / 64;
+  a.cin_blocks = d.stem ? 1 : d.Cin / 64;
+  a.relu = d.relu;
+  a.has_res = d.has_res && res != nullptr;
+  const int bn = (d.Cout % 128 == 0) ? 128 : 64;
+  constexpr int BM = 128;
+  const int m_tiles = (a.M + BM - 1) / BM;
+  a.n_tiles = d.Cout / bn;
+  a.nwg = m_tiles * a.n_tiles;
+  if (d.stem) {
+    if (bn == 128)
+      hipLaunchKernelGGL((conv_gemm_kernel<BM, 128, true>), dim3(a.nwg), dim3(256), 0, stream, a);
+    else
+      hipLaunchKernelGGL((conv_gemm_kernel<BM, 64, true>), dim3(a.nwg), dim3(256), 0, stream, a);
+  } else if (bn == 128) {
+    hipLaunchKernelGGL((conv_gemm_kernel<BM, 128, false>), dim3(a.nwg), dim3(256), 0, stream, a);
+  } else {
+    hipLaunchKernelGGL((conv_gemm_kernel<BM, 64, false>), dim3(a.nwg), dim3(256), 0, stream, a);
+  }
+  return hipGetLastError();
+}
+
+namespace {
+// one thread per output pixel (8 bytes) of the packed-stem image
+__global__ __launch_bounds__(256) void stem_pack_kernel(int total, int W, int C, int Wp, int lp,
+                                                        const float* __restrict__ x,
+                                                        uint2* __restrict__ y) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= total) return;
+  const int row = i / Wp;  // n * H + h
+  const int w = i - row * Wp - lp;
+  float v[4] = {0.f, 0.f, 0.f, 0.f};
+  if (w >= 0 && w < W) {
+    const float* s = x + ((size_t)row * W + w) * C;
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+      if (c < C) v[c] = s[c];
+  }
+  bf16x4 o;
+  o[0] = (bf16)v[0]; o[1] = (bf16)v[1]; o[2] = (bf16)v[2]; o[3] = (bf16)v[3];
+  y[i] = __builtin_bit_cast(uint2, o);
+}
+}  // namespace
+
+hipError_t stem_pack(int batch, int H, int W, int C, int Wp, int lp, const float* x, void* y,
+                     hipStream_t stream) {
+  if (batch <= 0) return hipSuccess;
+  if (C < 1 || C > 4 || lp < 0 || Wp < W + lp) return hipErrorInvalidValue;
+  const long long total = (long long)batch * H * Wp;
+  if (total >= (1ll << 31)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(stem_pack_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
+                     stream, (int)total, W, C, Wp, lp, x, static_cast<uint2*>(y));
+  return hipGetLastError();
+}
+
+}  // namespace gale

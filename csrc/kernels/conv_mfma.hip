@@ -410,6 +410,15 @@ hipError_t conv2d(const ConvDesc& d, int batch, const void* x, const void* w, co
                   const float* wscale, const void* res, void* y, hipStream_t stream) {
   if (batch <= 0) return hipSuccess;
   const bool f8 = d.fp8 != 0;
+  if (d.stem) {
+    if (f8 || d.in_f32 || d.out_f32 || d.Cin != 4 || d.KH != 8 || d.KW != 8 || d.K != 256 ||
+        d.Kpad != 256 || d.stride != 2 || d.pad != 3 || d.W != 2 * d.Wo + 6 ||
+        d.Cout % 64 != 0 || d.Npad % 64 != 0 || (d.has_res && res != nullptr))
+      return hipErrorInvalidValue;
+    return conv2d_gemm(d, batch, x, w, bias, nullptr, y, stream);
+  }
+  if (!f8 && conv_gemm_supported(d, batch, d.has_res && res != nullptr))
+    return conv2d_gemm(d, batch, x, w, bias, d.has_res ? res : nullptr, y, stream);
   if (f8 && (wscale == nullptr || !(d.in_scale > 0.f) || !(d.out_scale > 0.f)))
     return hipErrorInvalidValue;
   ConvArgs a;

@@ -89,6 +89,10 @@ void Executor::launch_all(int batch, void* const* bufs, hipStream_t stream) {
                                     static_cast<const float*>(op.w), op.bias,
                                     static_cast<float*>(out), stream);
         break;
+      case OP_STEM_PACK:
+        e = stem_pack(batch, op.p[0], op.p[1], op.p[2], op.p[3], op.p[4],
+                      static_cast<const float*>(in), out, stream);
+        break;
       case OP_SOFTMAX:
         e = softmax_rows(batch, op.p[0], op.p[1], static_cast<const float*>(in),
                          static_cast<float*>(out), stream);

@@ -221,9 +221,23 @@ class PackedEntry:
     shape: Tuple[int, ...]
 
 
-def _conv_geometry(net: Network, L: Conv) -> Dict[str, int]:
+def stem_packed(net: Network, L: Conv, wdtype: str = "bf16") -> bool:
+    """A 7x7/2 (pad 3) conv on the <= 4-channel network input runs as a packed-stem GEMM
+    (ConvDesc::stem, csrc/kernels/conv_gemm.hip): the input is repacked to bf16 [H][2*Wo+6][4]
+    so every kernel row of an output pixel is one 64-byte run."""
+    return (wdtype == "bf16" and L.inp == "input" and L.k == 7 and L.stride == 2 and L.pad == 3
+            and L.cin <= 4 and stored_channels(L.cout) % 64 == 0 and not L.out_f32
+            and L.residual is None)
+
+
+def _conv_geometry(net: Network, L: Conv, wdtype: str = "bf16") -> Dict[str, int]:
     h, w, _ = net.shapes[L.inp]
     ho, wo, _ = net.shapes[L.out]
+    if stem_packed(net, L, wdtype):
+        cout_s = stored_channels(L.cout)
+        return dict(H=h, W=2 * wo + 6, Cin=4, Ho=ho, Wo=wo, Cout=cout_s, KH=8, KW=8, stride=2,
+                    pad=3, K=256, Kpad=256, Npad=round_up(cout_s, conv_n_tiles(cout_s) * 16),
+                    stem=1)
     cin_s = L.cin if L.inp == "input" else stored_channels(L.cin)
     cout_s = stored_channels(L.cout)
     K = L.k * L.k * cin_s
@@ -247,7 +261,7 @@ def param_layout(net: Network, wdtype: str = "bf16") -> Tuple[Dict[str, PackedEn
 
     for L in net.layers:
         if isinstance(L, Conv):
-            gm = _conv_geometry(net, L)
+            gm = _conv_geometry(net, L, wdtype)
             wdt = torch.bfloat16 if wdtype == "bf16" else torch.uint8
             add(f"{L.name}.w", gm["Npad"] * gm["Kpad"] * wbytes, wdt, (gm["Npad"], gm["Kpad"]))
             add(f"{L.name}.b", gm["Npad"] * 4, torch.float32, (gm["Npad"],))
@@ -290,8 +304,13 @@ def pack_params(net: Network, folded: Dict[str, torch.Tensor], wdtype: str = "bf
 
     for L in net.layers:
         if isinstance(L, Conv):
-            gm = _conv_geometry(net, L)
-            w = pack_conv_weight(folded[f"{L.name}.weight"], gm["Cin"], gm["Npad"], gm["Kpad"])
+            gm = _conv_geometry(net, L, wdtype)
+            wt = folded[f"{L.name}.weight"]
+            if gm.get("stem"):  # zero-pad the 7x7 kernel to 8x8: k = kh*32 + kw*4 + c
+                w8 = torch.zeros(wt.shape[0], wt.shape[1], 8, 8, dtype=wt.dtype)
+                w8[:, :, :L.k, :L.k] = wt
+                wt = w8
+            w = pack_conv_weight(wt, gm["Cin"], gm["Npad"], gm["Kpad"])
             b = torch.zeros(gm["Npad"])
             b[: L.cout] = folded[f"{L.name}.bias"]
             if wdtype == "bf16":
@@ -334,7 +353,7 @@ def act_scales_from_packed(net: Network, packed: torch.Tensor) -> Dict[str, floa
 # executor plan
 # --------------------------------------------------------------------------------------------
 
-OP_CONV, OP_MAXPOOL, OP_AVGPOOL, OP_HEAD, OP_SOFTMAX, OP_RESNET20 = 0, 1, 2, 3, 4, 5
+OP_CONV, OP_MAXPOOL, OP_AVGPOOL, OP_HEAD, OP_SOFTMAX, OP_RESNET20, OP_STEM_PACK = range(7)
 
 
 def is_cifar_resnet20(net: Network) -> bool:
@@ -418,10 +437,19 @@ def build_plan(net: Network, base_ptr: int, wdtype: str = "bf16",
             buf_bytes[bid] = max(buf_bytes[bid], need)
             buf_of[out_name] = bid
         if isinstance(L, Conv):
-            gm = _conv_geometry(net, L)
+            gm = _conv_geometry(net, L, wdtype)
             d = dict(gm)
             d["relu"] = int(L.relu)
             d["in_f32"] = int(L.inp == "input")
+            src = buf_of[L.inp]
+            if gm.get("stem"):
+                # fp32 input -> packed-stem bf16 image in a buffer of its own
+                h, w, c = net.shapes[L.inp]
+                src = len(buf_bytes)
+                buf_bytes.append(h * gm["W"] * 4 * 2)
+                ops.append(dict(kind=OP_STEM_PACK, p=[h, w, c, gm["W"], 3], **{"in": 0},
+                                out=src))
+                d["in_f32"] = 0
             d["out_f32"] = int(L.out_f32)
             d["fp8"] = int(fp8)
             if fp8:
@@ -435,7 +463,7 @@ def build_plan(net: Network, base_ptr: int, wdtype: str = "bf16",
                 if fp8:
                     d["res_scale"] = act_scales[L.residual]
                 res = buf_of[L.residual]
-            op = dict(kind=OP_CONV, conv=d, **{"in": buf_of[L.inp]}, out=buf_of[out_name], res=res,
+            op = dict(kind=OP_CONV, conv=d, **{"in": src}, out=buf_of[out_name], res=res,
                       w=base_ptr + layout[f"{L.name}.w"].offset,
                       bias=base_ptr + layout[f"{L.name}.b"].offset)
             if wdtype == "fp8":

@@ -34,6 +34,33 @@ def test_model_matches_reference(name, batch):
     assert rep.executor.graphs_captured >= 1
 
 
+def test_resnet50_gemm_convs_match_conv_mfma_and_fp32():
+    """ResNet-50 with every wide conv on the LDS-pipelined GEMM kernel and the packed stem
+    (conv_gemm.hip) against the same plan on conv_mfma only (the stem stays packed: its layout
+    is fixed by the plan) and against the fp32 oracle."""
+    from gale._native import native
+
+    net = get_model("resnet50")
+    params = init_params(net, seed=21, calib_batch=4)
+    packed = materialize_weights(net, torch.device("cuda", 0), params=params)
+    rep = ModelReplica(net, packed, max_batch=16, slots=1)
+    assert any(op["kind"] == 6 for op in rep.ops)  # OP_STEM_PACK
+    x = torch.rand((6,) + net.input_shape, generator=torch.Generator().manual_seed(5))
+    C = native()
+    try:
+        C.set_conv_path(2)
+        a = rep.infer_eager(x).cpu()
+        C.set_conv_path(1)
+        b = rep.infer_eager(x).cpu()
+    finally:
+        C.set_conv_path(0)
+    ref = forward(net, fold_params(net, params), x)
+    torch.cuda.synchronize()
+    assert (a - b).abs().max().item() < 1e-2
+    assert (a - ref).abs().max().item() < 3e-2
+    assert torch.allclose(a.sum(1), torch.ones(6), atol=1e-4)
+
+
 @pytest.mark.parametrize("name,batch", [("lenet5", 13), ("resnet20", 37), ("resnet50", 2)])
 def test_fp8_model_matches_emulation_and_fp32(name, batch):
     """fp8 plan (e4m3 MFMA, calibrated per-tensor activation scales) against the fp8 emulation

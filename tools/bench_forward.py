@@ -25,7 +25,11 @@ def main():
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--eager", action="store_true")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp8"])
+    ap.add_argument("--conv-path", type=int, default=0,
+                    help="0 auto, 1 conv_mfma only, 2 GEMM conv wherever the shape allows")
     a = ap.parse_args()
+    from gale._native import native
+    native().set_conv_path(a.conv_path)
     net = get_model(a.model)
     dev = torch.device("cuda", 0)
     packed = materialize_weights(net, dev, wdtype=a.dtype)
@@ -43,7 +47,7 @@ def main():
         torch.cuda.synchronize()
         dt = (time.perf_counter() - t) / a.iters
         flops = 2 * net.macs_per_image() * b
-        r = dict(model=a.model, dtype=a.dtype, batch=b, ms=dt * 1e3, img_s=b / dt, tflops=flops / dt / 1e12,
+        r = dict(model=a.model, dtype=a.dtype, conv_path=a.conv_path, batch=b, ms=dt * 1e3, img_s=b / dt, tflops=flops / dt / 1e12,
                  graph=not a.eager)
         res.append(r)
         print(json.dumps(r), flush=True)

@@ -38,3 +38,12 @@ if [ -n "${KB_PMC:-}" ]; then
     python3 tools/bench_json.py --batches 256 --iters 5 > gpurun_out/pmc_json.log 2>&1 || { tail -20 gpurun_out/pmc_json.log; exit 1; }
   python3 tools/pmc_summary.py $(find gpurun_out/pmc_json -name '*counter_collection.csv' | head -1)
 fi
+for step in ${KB_STEPS2:-}; do
+  case $step in
+    r50paths)
+      for cp in 1 0 2; do
+        timeout -k 10 240 python tools/bench_forward.py --model resnet50 --batches 64,256 --iters 10 --conv-path $cp > gpurun_out/kb_r50_p$cp.log 2>&1 || { tail -20 gpurun_out/kb_r50_p$cp.log; exit 1; }
+        grep '^{' gpurun_out/kb_r50_p$cp.log
+      done ;;
+  esac
+done

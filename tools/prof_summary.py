@@ -11,14 +11,20 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("db")
     ap.add_argument("--top", type=int, default=25)
+    ap.add_argument("--by-grid", action="store_true",
+                    help="one row per (kernel, grid size): per-layer view of a plan")
     a = ap.parse_args()
     c = sqlite3.connect(a.db)
+    key = "name || ' grid=' || grid_x || 'x' || grid_y" if a.by_grid else "name"
     rows = c.execute(
-        "select name, count(*), sum(end-start), avg(end-start), min(end-start), max(end-start) "
-        "from kernels group by name order by sum(end-start) desc").fetchall()
+        f"select {key}, count(*), sum(end-start), avg(end-start), min(end-start), max(end-start) "
+        "from kernels group by 1 order by sum(end-start) desc").fetchall()
     total = sum(r[2] for r in rows) or 1
     print("kernel,calls,total_us,avg_us,min_us,max_us,pct")
     for name, n, tot, avg, mn, mx in rows[:a.top]:
+        if a.by_grid and " grid=" in name:
+            base, grid = name.rsplit(" grid=", 1)
+            name = (base if len(base) < 70 else base[:67] + "...") + " grid=" + grid
         short = name if len(name) < 110 else name[:107] + "..."
         print(f'"{short}",{n},{tot/1e3:.1f},{avg/1e3:.2f},{mn/1e3:.2f},{mx/1e3:.2f},'
               f"{100*tot/total:.1f}")
