@@ -49,6 +49,8 @@ EngineConfig config_from_dict(const py::dict& d) {
   opt(d, "max_wait_us", c.max_wait_us);
   opt(d, "queue_depth", c.queue_depth);
   opt(d, "watchdog_ms", c.watchdog_ms);
+  opt(d, "max_restarts", c.max_restarts);
+  opt(d, "restart_backoff_ms", c.restart_backoff_ms);
   opt(d, "fault", c.fault);
   opt(d, "trace", c.trace);
   opt(d, "max_records", c.max_records);
@@ -111,6 +113,21 @@ void bind_engine(py::module_& m) {
           d["batches"] = s.batches;
           d["images"] = s.images;
           d["records"] = s.records;
+          d["restarts"] = s.restarts;
+          out.append(d);
+        }
+        return out;
+      })
+      .def("partition_offsets", [](Engine& e) {
+        py::list out;
+        for (const PartitionOffsets& o : e.partition_offsets()) {
+          py::dict d;
+          d["partition"] = o.partition;
+          d["high_watermark"] = o.high_watermark;
+          d["fetched"] = o.fetched;
+          d["committed"] = o.committed;
+          d["lag"] = o.lag;
+          d["fetch_lag"] = o.fetch_lag;
           out.append(d);
         }
         return out;

@@ -103,6 +103,9 @@ struct Engine::ReplicaSlot {
   std::shared_ptr<Replica> rep;
   int index = 0;
   std::atomic<bool> alive{true};
+  std::atomic<bool> watchdog_killed{false};
+  std::atomic<bool> restarting{false};  // failed, supervisor recovery pending
+  std::atomic<int> restarts{0};
   std::mutex mu;  // inflight
   std::deque<std::shared_ptr<Batch>> inflight;
   std::atomic<int64_t> batches{0}, images{0}, records{0};
@@ -232,7 +235,7 @@ void Engine::stop() {
   decoders_.clear();
   batcher_->close();
   for (size_t i = 0; i < workers_.size(); ++i) {
-    if (replicas_[i]->alive) {
+    if (replicas_[i]->alive || replicas_[i]->restarting) {
       workers_[i].join();
     } else {
       workers_[i].detach();  // may be stuck on a dead device; its batches were re-queued
@@ -337,6 +340,7 @@ void Engine::source_loop(int idx, std::vector<int> parts) {
       for (auto& f : fs)
         for (const kafka::RecordRef& rr : f.records) pending_[rr.partition][rr.offset] = 1;
       for (int p : parts) next_fetch_[p] = cons->position(p);
+      for (const auto& kv : cons->high_watermarks()) high_watermark_[kv.first] = kv.second;
     }
     if (!fs.empty()) {
       int64_t z = 0;
@@ -466,16 +470,50 @@ void Engine::decode_fetch(FetchItem& it, std::vector<InRecord>& good) {
 void Engine::worker_loop(ReplicaSlot* rs) {
   Replica& rep = *rs->rep;
   if (rep.device() >= 0) hipSetDevice(rep.device());
+  for (;;) {
+    serve(rs);
+    if (!rs->restarting) return;
+    // supervisor: back off (stop() interrupts), recover the replica, rejoin the pool
+    const int64_t until = mono_ns() + (int64_t)cfg_.restart_backoff_ms * 1000000;
+    while (!stopping_ && mono_ns() < until) std::this_thread::sleep_for(std::chrono::milliseconds(5));
+    bool ok = !stopping_;
+    if (ok) {
+      try {
+        rep.recover();
+      } catch (const std::exception& e) {
+        fprintf(stderr, "[gale supervisor] replica %d (%s) recovery failed: %s\n", rs->index,
+                rep.name().c_str(), e.what());
+        ok = false;
+      }
+    }
+    if (ok) {
+      ++rs->restarts;
+      ++replica_restarts_;
+      fprintf(stderr, "[gale supervisor] replica %d (%s) restarted (%d of %d)\n", rs->index,
+              rep.name().c_str(), rs->restarts.load(), cfg_.max_restarts);
+      rs->alive = true;
+    }
+    rs->restarting = false;  // (after alive: stop() joins while either is set)
+    if (!ok) return;
+  }
+}
+
+void Engine::serve(ReplicaSlot* rs) {
+  Replica& rep = *rs->rep;
   const int64_t max_wait_ns = (int64_t)cfg_.max_wait_us * 1000;
   const size_t depth = (size_t)std::max(1, rep.depth());
   std::deque<std::shared_ptr<Batch>> mine;
   auto fail = [&](const char* what, const std::string& msg) {
-    fprintf(stderr, "[gale replica %d %s] %s: %s -> replica marked dead, batches re-queued\n",
-            rs->index, rep.name().c_str(), what, msg.c_str());
+    const bool restart = cfg_.max_restarts > rs->restarts && !stopping_;
+    fprintf(stderr, "[gale replica %d %s] %s: %s -> replica marked dead, batches re-queued%s\n",
+            rs->index, rep.name().c_str(), what, msg.c_str(),
+            restart ? " (supervisor restart pending)" : "");
     std::vector<InRecord> back;
     {
       std::lock_guard<std::mutex> lk(rs->mu);
-      if (rs->alive.exchange(false)) {
+      if (rs->alive) {  // (else the watchdog killed it first: no restart on a hung device)
+        if (restart) rs->restarting = true;  // before alive drops: stop() never detaches us
+        rs->alive = false;
         for (auto& b : rs->inflight)
           for (const InRecord& r : b->recs) back.push_back(r);
         rs->inflight.clear();
@@ -563,6 +601,7 @@ void Engine::watchdog_loop() {
         const int64_t t0 = rs->inflight.front()->t_submit_ns;
         if (t0 == 0 || now - t0 < (int64_t)cfg_.watchdog_ms * 1000000) continue;
         rs->alive = false;
+        rs->watchdog_killed = true;
         for (auto& b : rs->inflight)
           for (const InRecord& r : b->recs) back.push_back(r);
         rs->inflight.clear();
@@ -704,7 +743,19 @@ std::map<std::string, double> Engine::stats() const {
   s["dropped"] = (double)dropped_;
   s["requeued"] = (double)requeued_;
   s["replica_failures"] = (double)replica_failures_;
+  s["replica_restarts"] = (double)replica_restarts_;
   s["commits"] = (double)commits_;
+  {
+    int64_t lag = 0, fetch_lag = 0, lag_max = 0;
+    for (const PartitionOffsets& o : partition_offsets()) {
+      lag += o.lag;
+      fetch_lag += o.fetch_lag;
+      lag_max = std::max(lag_max, o.lag);
+    }
+    s["lag_records"] = (double)lag;              // storm-kafka spoutLag, summed over partitions
+    s["lag_records_max"] = (double)lag_max;
+    s["fetch_lag_records"] = (double)fetch_lag;  // log end - next fetch
+  }
   s["batches"] = (double)batches_total_;
   s["queue_records"] = (double)const_cast<Batcher*>(batcher_.get())->size();
   for (int i = 1; i < 8; ++i)
@@ -746,7 +797,29 @@ std::vector<ReplicaStats> Engine::replica_stats() const {
     s.batches = r->batches;
     s.images = r->images;
     s.records = r->records;
+    s.restarts = r->restarts;
     v.push_back(s);
+  }
+  return v;
+}
+
+std::vector<PartitionOffsets> Engine::partition_offsets() const {
+  std::vector<PartitionOffsets> v;
+  std::lock_guard<std::mutex> lk(const_cast<std::mutex&>(pend_mu_));
+  for (const auto& kv : next_fetch_) {
+    PartitionOffsets o;
+    o.partition = kv.first;
+    o.fetched = kv.second;
+    auto pit = pending_.find(kv.first);
+    o.committed = (pit != pending_.end() && !pit->second.empty()) ? pit->second.begin()->first
+                                                                  : kv.second;
+    auto hit = high_watermark_.find(kv.first);
+    o.high_watermark = hit != high_watermark_.end() ? hit->second : -1;
+    if (o.high_watermark >= 0) {
+      o.lag = std::max<int64_t>(0, o.high_watermark - o.committed);
+      o.fetch_lag = std::max<int64_t>(0, o.high_watermark - o.fetched);
+    }
+    v.push_back(o);
   }
   return v;
 }

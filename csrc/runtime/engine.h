@@ -75,6 +75,11 @@ struct EngineConfig {
   int queue_depth = 8192;          // records buffered between source and replicas
   // robustness
   int watchdog_ms = 30000;         // a batch longer than this on a replica marks it dead
+  // supervisor (E4: Storm supervisors restart dead workers): a replica whose submit/wait threw is
+  // recovered (Replica::recover) after restart_backoff_ms and rejoins, at most max_restarts
+  // times; a replica the watchdog killed (hung device) is never restarted
+  int max_restarts = 0;
+  int restart_backoff_ms = 500;
   std::string fault;               // "replica_crash@N,parse_error@P,producer_fail@P"
   bool trace = false;              // roctx ranges around pipeline stages (also GALE_ROCTX=1)
   int64_t max_records = -1;        // stop once this many records are completed (bench/tests)
@@ -86,6 +91,17 @@ struct ReplicaStats {
   int device = -1;
   bool alive = true;
   int64_t batches = 0, images = 0, records = 0;
+  int restarts = 0;
+};
+
+// Per-partition offsets, the storm-kafka `kafkaOffset` spout metric: log end
+// (high watermark), next offset to fetch (emitted), first offset not yet acknowledged downstream
+// (completed / commit position) and the lag behind the log end.
+struct PartitionOffsets {
+  int partition = -1;
+  int64_t high_watermark = -1, fetched = -1, committed = -1;
+  int64_t lag = 0;        // high_watermark - committed
+  int64_t fetch_lag = 0;  // high_watermark - fetched
 };
 
 class Engine {
@@ -112,6 +128,7 @@ class Engine {
   // counters and latency quantiles for the metrics reporter
   std::map<std::string, double> stats() const;
   std::vector<ReplicaStats> replica_stats() const;
+  std::vector<PartitionOffsets> partition_offsets() const;
   void reset_stats();
   const EngineConfig& config() const { return cfg_; }
 
@@ -129,6 +146,7 @@ class Engine {
   void decode_loop(int idx);
   void decode_fetch(FetchItem& it, std::vector<InRecord>& good);
   void worker_loop(ReplicaSlot* rs);
+  void serve(ReplicaSlot* rs);  // one replica life: returns once it dies or the engine drains
   void watchdog_loop();
   void finish_batch(ReplicaSlot* rs, Batch& b);
   void emit(InRecord& r, std::string value, bool null_value, kafka::Producer* prod);
@@ -156,6 +174,7 @@ class Engine {
   std::mutex pend_mu_;
   std::map<int, std::map<int64_t, int>> pending_;  // partition -> offset -> 1
   std::map<int, int64_t> next_fetch_;              // partition -> next offset to fetch
+  std::map<int, int64_t> high_watermark_;          // partition -> log end (last fetch response)
 
   std::mutex done_mu_;
   std::condition_variable done_cv_;
@@ -172,7 +191,7 @@ class Engine {
   // metrics
   std::atomic<int64_t> records_in_{0}, images_in_{0}, records_out_{0}, images_out_{0};
   std::atomic<int64_t> bytes_in_{0}, errors_{0}, produce_failures_{0}, dropped_{0};
-  std::atomic<int64_t> requeued_{0}, replica_failures_{0}, commits_{0};
+  std::atomic<int64_t> requeued_{0}, replica_failures_{0}, replica_restarts_{0}, commits_{0};
   std::atomic<int64_t> err_by_status_[8] = {};
   Histogram h_queue_us_, h_device_us_, h_engine_e2e_us_, h_record_e2e_ms_, h_batch_images_;
   // thread time per pipeline stage (summed over threads): where the host spends its cycles

@@ -228,4 +228,14 @@ void GpuReplica::wait(Batch& b) {
   b.probs = s.h_out;
 }
 
+void GpuReplica::recover() {
+  // drain whatever the failed batches left queued on both streams, then clear the (non-sticky)
+  // error state; a sticky device fault makes these calls fail and the supervisor gives up
+  check_hip(hipSetDevice(exec_->device()), "recover: hipSetDevice");
+  check_hip(hipStreamSynchronize(copy_stream_), "recover: copy stream");
+  check_hip(hipStreamSynchronize(stream_), "recover: compute stream");
+  (void)hipGetLastError();
+  next_slot_ = 0;
+}
+
 }  // namespace gale

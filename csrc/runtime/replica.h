@@ -52,6 +52,9 @@ class Replica {
   virtual void submit(Batch& b) = 0;
   virtual void wait(Batch& b) = 0;
   virtual int device() const { return -1; }
+  // Supervisor restart after submit/wait threw (its in-flight batches were already re-queued):
+  // bring the replica back to an idle, usable state or throw if it cannot be.
+  virtual void recover() {}
 };
 
 // CPU stub (SURVEY.md §4 "stub replica for plumbing tests on GPU-less hosts"): parses on the
@@ -85,6 +88,7 @@ class GpuReplica : public Replica {
   int device() const override { return exec_->device(); }
   void submit(Batch& b) override;
   void wait(Batch& b) override;
+  void recover() override;
 
  private:
   struct Slot {

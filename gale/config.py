@@ -71,6 +71,10 @@ class GaleConfig:
     stub_null: bool = False            # stub replicas skip parsing/compute (host-path benchmark)
     # robustness / observability
     watchdog_ms: int = 30000
+    # supervisor (Storm supervisors restart dead workers): a replica that failed is
+    # recovered and rejoins after restart_backoff_ms, up to max_restarts times (0 = stays dead)
+    max_restarts: int = 3
+    restart_backoff_ms: int = 500
     fault: str = ""                    # replica_crash@N,parse_error@P,producer_fail@P
     trace: bool = False                # roctx ranges around pipeline stages (rocprofv3)
     profile: str = ""                  # run under rocprofv3 --kernel-trace --marker-trace --stats
@@ -113,7 +117,9 @@ class GaleConfig:
             value_format=self.value_format, type_id_header=self.type_id_header,
             on_error=self.on_error, H=H, W=W, C=C, classes=classes, max_batch=self.max_batch,
             max_wait_us=self.max_wait_us, queue_depth=self.queue_depth,
-            watchdog_ms=self.watchdog_ms, fault=self.fault, seed=self.seed, trace=self.trace)
+            watchdog_ms=self.watchdog_ms, max_restarts=self.max_restarts,
+            restart_backoff_ms=self.restart_backoff_ms, fault=self.fault, seed=self.seed,
+            trace=self.trace)
 
 
 def _coerce(f: dataclasses.Field, raw: Any) -> Any:

@@ -115,5 +115,10 @@ class Engine:
     def replica_stats(self) -> List[dict]:
         return list(self._native.replica_stats())
 
+    def partition_offsets(self) -> List[dict]:
+        """storm-kafka ``kafkaOffset`` analogue: per input partition the log end (high
+        watermark), next fetch offset, commit position and lag."""
+        return list(self._native.partition_offsets())
+
     def reset_stats(self) -> None:
         self._native.reset_stats()

@@ -16,7 +16,8 @@ import time
 from typing import Callable, Dict, Optional, TextIO
 
 KEYS = ("records_in", "records_out", "images_out", "errors", "produce_failures", "dropped",
-        "requeued", "replica_failures", "queue_records", "replicas_alive", "commits",
+        "requeued", "replica_failures", "replica_restarts", "queue_records", "replicas_alive",
+        "commits", "lag_records", "lag_records_max", "fetch_lag_records",
         "e2e_us_p50", "e2e_us_p99", "queue_us_p50", "device_us_p50", "device_us_p99",
         "record_e2e_ms_p50", "record_e2e_ms_p99", "batch_images_mean")
 

@@ -108,12 +108,41 @@ def test_json_string_value_and_type_header(broker):
 def test_replica_crash_requeues_without_loss(broker):
     counts = [1] * 120
     produce_images(broker, counts)
-    eng, out = run(broker, len(counts), replicas=2, fault="replica_crash@3")
+    eng, out = run(broker, len(counts), replicas=2, fault="replica_crash@3", max_restarts=0)
     st = eng.stats()
     assert st["replica_failures"] == 1 and st["replicas_alive"] == 1
+    assert st["replica_restarts"] == 0
     assert len([r for r in out if r["value"] is not None]) == 120
     rs = eng.replica_stats()
     assert sum(r["images"] for r in rs) == 120 and sum(not r["alive"] for r in rs) == 1
+
+
+def test_supervisor_restarts_crashed_replica(broker):
+    """Storm's supervisor restarts a dead worker; gale's recovers the replica,
+    which rejoins the pool and serves again, without losing or duplicating records."""
+    counts = [1] * 200
+    produce_images(broker, counts)
+    eng, out = run(broker, len(counts), replicas=1, fault="replica_crash@2", max_restarts=2,
+                   restart_backoff_ms=50)  # (1 replica: the records wait for its restart)
+    st = eng.stats()
+    assert st["replica_failures"] == 1 and st["replica_restarts"] == 1
+    assert st["replicas_alive"] == 1
+    vals = [r["value"] for r in out]
+    assert len(vals) == 200 and all(v is not None for v in vals)
+    (rs,) = eng.replica_stats()
+    assert rs["alive"] and rs["restarts"] == 1 and rs["images"] == 200
+
+
+def test_partition_offsets_report_lag(broker):
+    """kafkaOffset-style metrics: log end, fetched, committed and lag per input partition."""
+    produce_images(broker, [1] * 10)
+    eng, _ = run(broker, 10)
+    po = {o["partition"]: o for o in eng.partition_offsets()}
+    assert set(po) == {0, 1}
+    for p, o in po.items():
+        assert o["high_watermark"] == 5 and o["fetched"] == 5 and o["committed"] == 5
+        assert o["lag"] == 0 and o["fetch_lag"] == 0
+    assert eng.stats()["lag_records"] == 0
 
 
 @pytest.mark.parametrize("mode", ["sync", "fire-and-forget"])

@@ -2,6 +2,7 @@
 engine (Kafka -> GPU JSON parse -> hipGraph forward -> Kafka) against the fp32 torch oracle."""
 
 import json
+import time
 
 import numpy as np
 import pytest
@@ -197,9 +198,22 @@ def test_gpu_engine_two_replicas_on_one_gpu_and_crash(broker):
     rec = C.encode_instances(x)
     for _ in range(300):
         broker.append("in", 0, [rec])
-    eng, out = run_engine(broker, 300, replicas=2, fault="replica_crash@4")
+    cfg = GaleConfig(topology_name="g", input_topic="in", output_topic="out",
+                     bootstrap=f"127.0.0.1:{broker.port}", start_offset="earliest",
+                     max_batch=32, max_wait_us=500, replicas=2, fault="replica_crash@4",
+                     max_restarts=1, restart_backoff_ms=20)
+    eng = Engine(cfg, devices=[0], max_records=300)
+    eng.start()
+    assert eng.wait(120), eng.stats()
+    deadline = time.time() + 10  # the record target can be met before the backoff ends
+    while eng.stats()["replica_restarts"] < 1 and time.time() < deadline:
+        time.sleep(0.01)
+    eng.stop()
+    out = broker.read("out", 0)
     assert len(out) == 300 and all(r["value"] is not None for r in out)
     st = eng.stats()
-    assert st["replica_failures"] == 1 and st["replicas_alive"] == 1
+    # the crashed GPU replica was recovered by the supervisor (streams drained) and rejoined
+    assert st["replica_failures"] == 1 and st["replica_restarts"] == 1
+    assert st["replicas_alive"] == 2
     vals = {r["value"] for r in out}
     assert len(vals) == 1  # identical input -> identical output on both replicas
