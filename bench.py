@@ -193,9 +193,9 @@ def main() -> int:
             "ms_per_step": round(elapsed_max / (total_images / (step_images * world)) * 1e3, 4),
             "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": a.dtype,
-            "data": "synthetic (uniform [0,1) CIFAR-shaped InstObj JSON records, Java float "
-                    "format, preloaded into an embedded Kafka-protocol broker); random-init "
-                    "weights (seed 0) RCCL-broadcast from rank 0",
+            "data": f"synthetic (uniform [0,1) {'x'.join(map(str, net.input_shape))} InstObj "
+                    "JSON records, Java float format, preloaded into an embedded Kafka-protocol "
+                    "broker); random-init weights (seed 0) RCCL-broadcast from rank 0",
             "config": {"model": a.model, "global_batch": step_images * world, "seq_len": None,
                        "parallelism": f"dp{world}", "images_per_record": ipr,
                        "max_wait_us": a.max_wait_us, "replicas_per_gpu": a.replicas_per_gpu,

@@ -832,6 +832,7 @@ void Engine::reset_stats() {
   h_batch_images_.reset();
   images_out_ = 0;
   records_out_ = 0;
+  bytes_in_ = 0;  // (json MB/s of a window = bytes fetched inside it)
   ns_poll_ = ns_decode_ = ns_take_ = ns_submit_ = ns_wait_ = ns_finish_ = 0;
   t_first_ns_ = mono_ns();
   t_last_ns_ = t_first_ns_.load();
