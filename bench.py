@@ -63,6 +63,10 @@ def parse_args():
                     help="stub replicas skip parsing (measures the host Kafka/codec path only)")
     ap.add_argument("--check-crcs", action=argparse.BooleanOptionalAction, default=True,
                     help="consumer CRC32C verification (Kafka check.crcs; diagnosis only)")
+    ap.add_argument("--rate", type=float, default=0.0,
+                    help="offered load in images/s per GPU: records are appended to the broker "
+                         "at this rate while the engine runs (latency under load, BASELINE "
+                         "config 5); 0 = a preloaded backlog (maximum throughput)")
     ap.add_argument("--timeout", type=float, default=600.0)
     return ap.parse_args()
 
@@ -78,6 +82,40 @@ def host_cpus_per_rank() -> float:
     except (OSError, ValueError):
         pass
     return n / max(1, int(os.environ.get("LOCAL_WORLD_SIZE", "1")))
+
+
+class RateFeeder:
+    """Appends pre-encoded record batches (by reference) to the input partitions at a fixed
+    image rate from a background thread: an open-loop load generator, so latency is measured
+    at a known offered load instead of against a backlog."""
+
+    def __init__(self, broker, topic, parts, batches, images_per_batch, rate):
+        import threading
+
+        self.broker, self.topic, self.parts, self.batches = broker, topic, parts, batches
+        self.ipb, self.rate = images_per_batch, rate
+        self._stop = threading.Event()
+        self._t = threading.Thread(target=self._run, name="rate-feeder", daemon=True)
+
+    def _run(self):
+        t0 = time.perf_counter()
+        sent = 0
+        i = 0
+        while not self._stop.is_set():
+            due = (time.perf_counter() - t0) * self.rate
+            while sent + self.ipb <= due:
+                self.broker.append_batch_repeated(self.topic, i % self.parts,
+                                                  self.batches[i % len(self.batches)], 1)
+                sent += self.ipb
+                i += 1
+            time.sleep(0.0002)
+
+    def start(self):
+        self._t.start()
+
+    def stop(self):
+        self._stop.set()
+        self._t.join()
 
 
 def main() -> int:
@@ -111,7 +149,9 @@ def main() -> int:
     K = native().kafka
     ipr = a.images_per_record
     parts = a.partitions or a.replicas_per_gpu
-    rpb = 64  # records per preloaded RecordBatch
+    # records per preloaded RecordBatch (rate mode: small batches, arrivals are not bursty)
+    # (the feeder thread keeps to ~10k appends/s)
+    rpb = min(64, max(8, int(a.rate // 10000))) if a.rate > 0 else 64
     broker = K.Broker(max_message_bytes=256 << 20, retention_bytes=1 << 62)
     broker.start()
     broker.create_topic("gale-in", parts)
@@ -125,9 +165,13 @@ def main() -> int:
     distinct = max(rpb, (a.distinct // (ipr * rpb)) * rpb) * ipr
     imgs = synthetic_images(distinct, net.input_shape, seed=1234 + rank)
     batches = encode_batches(encode_records(imgs, ipr), rpb)
-    for p in range(parts):
-        preload(broker, "gale-in", p, batches, -(-n_records // parts), rpb)
+    if a.rate <= 0:
+        for p in range(parts):
+            preload(broker, "gale-in", p, batches, -(-n_records // parts), rpb)
     del imgs
+    feeder = None
+    if a.rate > 0:
+        feeder = RateFeeder(broker, "gale-in", parts, batches, rpb * ipr, a.rate)
 
     cfg = GaleConfig(topology_name=f"bench-r{rank}", input_topic="gale-in",
                      output_topic="gale-out", bootstrap=f"127.0.0.1:{broker.port}",
@@ -147,6 +191,8 @@ def main() -> int:
     # once every rank has completed its warm-up records and ends when K more steps completed.
     eng = Engine(cfg, devices=devices)  # weights: seeded on rank 0, RCCL-broadcast
     eng.start()
+    if feeder:
+        feeder.start()
     if not eng.wait_completed(warm_records, a.timeout):
         raise SystemExit(f"rank {rank}: warm-up timed out ({eng.completed}/{warm_records})")
     warm_done = eng.completed
@@ -168,6 +214,8 @@ def main() -> int:
     st = eng.stats()
     if world > 1:
         dist.barrier()
+    if feeder:
+        feeder.stop()
     eng.stop()
     broker.stop()
     if not reached:
@@ -200,6 +248,8 @@ def main() -> int:
                        "parallelism": f"dp{world}", "images_per_record": ipr,
                        "max_wait_us": a.max_wait_us, "replicas_per_gpu": a.replicas_per_gpu,
                        "path": "kafka-fetch->gpu-json-parse->hipgraph-forward->kafka-produce"},
+            "load": (f"offered {a.rate:.0f} images/s per GPU" if a.rate > 0
+                     else "preloaded backlog (max throughput; latency includes queueing)"),
             "p50_latency_ms": round(st["e2e_us_p50"] / 1e3, 3),
             "p99_latency_ms": round(st["e2e_us_p99"] / 1e3, 3),
             "device_ms_p50": round(st["device_us_p50"] / 1e3, 3),
