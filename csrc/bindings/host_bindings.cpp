@@ -498,6 +498,18 @@ void bind_host(py::module_& m) {
           for (auto item : records_to_py(f.buf.get(), f.records)) out.append(item);
         return out;
       })
+      .def("poll_count", [](Consumer& c) {
+        // (records, value bytes) of one poll without materialising Python objects: consumer
+        // throughput diagnostics
+        py::gil_scoped_release nogil;
+        int64_t n = 0, bytes = 0;
+        for (auto& f : c.poll())
+          for (const RecordRef& r : f.records) {
+            ++n;
+            bytes += r.value_len > 0 ? r.value_len : 0;
+          }
+        return std::make_pair(n, bytes);
+      })
       .def("commit", [](Consumer& c, std::map<int, int64_t> offs) {
         py::gil_scoped_release nogil;
         c.commit(offs);
