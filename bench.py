@@ -30,6 +30,8 @@ import resource
 import sys
 import time
 
+import numpy as np
+
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
@@ -152,6 +154,11 @@ def main() -> int:
     # records per preloaded RecordBatch (rate mode: small batches, arrivals are not bursty)
     # (the feeder thread keeps to ~10k appends/s)
     rpb = min(64, max(8, int(a.rate // 10000))) if a.rate > 0 else 64
+    # ... and at most ~4 MB per RecordBatch, as a producer's batch.size would keep it: a fetch
+    # always returns at least one whole batch (KIP-74), so 64 ResNet-50 records (1.7 MB each)
+    # in one batch would turn every fetch into a 109 MB response
+    rec_bytes = 12 * int(np.prod(net.input_shape)) * ipr  # ~Java float text per record
+    rpb = max(1, min(rpb, (4 << 20) // rec_bytes))
     broker = K.Broker(max_message_bytes=256 << 20, retention_bytes=1 << 62)
     broker.start()
     broker.create_topic("gale-in", parts)

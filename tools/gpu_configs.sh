@@ -19,7 +19,7 @@ run() {  # name, args...
   return $rc
 }
 run c2_resnet20_bf16 --steps 100 --warmup 10 || exit $?
-run c4_resnet50_bf16 --model resnet50 --batch 64 --replicas-per-gpu 2 --steps 20 --warmup 3 --distinct 64 || exit $?
+run c4_resnet50_bf16 --model resnet50 --batch 64 --replicas-per-gpu 2 --partitions 4 --source-parallelism 4 --decode-threads 4 --steps 30 --warmup 5 --distinct 64 || exit $?
 run c5_resnet20_fp8_slo --dtype fp8 --batch 32 --max-wait-us 200 --steps 200 --warmup 20 || exit $?
 # latency at a fixed offered load (open-loop feeder), fp8 and bf16
 for r in ${RATES:-100000 300000}; do
