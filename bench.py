@@ -73,19 +73,6 @@ def parse_args():
     return ap.parse_args()
 
 
-def host_cpus_per_rank() -> float:
-    """CPUs this rank may use: min(affinity, cgroup CPU quota) / ranks on this node."""
-    n = float(len(os.sched_getaffinity(0)))
-    try:
-        with open("/sys/fs/cgroup/cpu.max") as f:
-            quota, period = f.read().split()[:2]
-        if quota != "max":
-            n = min(n, int(quota) / int(period))
-    except (OSError, ValueError):
-        pass
-    return n / max(1, int(os.environ.get("LOCAL_WORLD_SIZE", "1")))
-
-
 class RateFeeder:
     """Appends pre-encoded record batches (by reference) to the input partitions at a fixed
     image rate from a background thread: an open-loop load generator, so latency is measured
@@ -125,6 +112,8 @@ def main() -> int:
     if a.replicas_per_gpu <= 0:
         # the host pipeline (Kafka fetch + CRC + scan + encode + produce, and the embedded
         # broker of this rank) needs ~3 cores per replica at full rate
+        from gale.utils import host_cpus_per_rank
+
         a.replicas_per_gpu = max(1, min(4, int(host_cpus_per_rank() // 4)))
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))

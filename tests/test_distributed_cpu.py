@@ -15,7 +15,7 @@ import torch.multiprocessing as mp
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _free_port():
+def _free_port():  # (kept local: the spawned workers import nothing from gale first)
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     p = s.getsockname()[1]
@@ -66,3 +66,18 @@ def test_bench_stub_torchrun_world2():
     assert r["n_gpus"] == 2 and r["steps"] == 4 and r["value"] > 0
     # a step = one 32-image micro-batch per replica (4 per GPU by default), on both ranks
     assert r["config"]["parallelism"] == "dp2" and r["config"]["global_batch"] == 32 * 4 * 2
+
+
+def test_bench_stub_rate_mode():
+    """bench.py --rate: the open-loop feeder offers a fixed image rate; the engine keeps up, so
+    the achieved rate matches the offer and the load is reported in the JSON line."""
+    cmd = [sys.executable, "bench.py", "--stub", "--stub-null", "--steps", "20", "--warmup", "2",
+           "--batch", "16", "--replicas-per-gpu", "2", "--rate", "3000", "--max-wait-us", "500",
+           "--timeout", "120"]
+    out = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=300,
+                         env=dict(os.environ, OMP_NUM_THREADS="1"))
+    assert out.returncode == 0, out.stderr[-3000:]
+    (r,) = [json.loads(x) for x in out.stdout.splitlines() if x.startswith("{")]
+    assert r["load"].startswith("offered 3000")
+    assert 0.7 * 3000 < r["value"] < 1.3 * 3000
+    assert r["p50_latency_ms"] < 50

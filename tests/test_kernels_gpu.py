@@ -309,3 +309,20 @@ def test_conv2d_gemm_identity_asymmetric():
     finally:
         native().set_conv_path(0)
     assert torch.equal(y.cpu(), x)
+
+
+def test_stem_pack_layout():
+    """stem_pack: fp32 NHWC (C=3) -> bf16 [H][Wp][4] with lp zero columns on the left, zero
+    right padding and a zero 4th channel (the packed-stem input, conv_gemm.hip)."""
+    from gale._native import native
+
+    B, H, W, C, lp = 2, 5, 7, 3, 3
+    Wp = W + 2 * lp + 1
+    x = torch.randn(B, H, W, C, generator=torch.Generator().manual_seed(4))
+    y = torch.full((B, H, Wp, 4), 7.0, dtype=torch.bfloat16, device=DEV)
+    xd = x.to(DEV)
+    native().stem_pack(B, H, W, C, Wp, lp, xd.data_ptr(), y.data_ptr(),
+                       torch.cuda.current_stream().cuda_stream)
+    ref = torch.zeros(B, H, Wp, 4)
+    ref[:, :, lp:lp + W, :C] = x
+    assert torch.equal(y.cpu(), ref.to(torch.bfloat16))
