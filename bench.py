@@ -69,6 +69,9 @@ def parse_args():
                     help="offered load in images/s per GPU: records are appended to the broker "
                          "at this rate while the engine runs (latency under load, BASELINE "
                          "config 5); 0 = a preloaded backlog (maximum throughput)")
+    ap.add_argument("--broker-zero-copy", action=argparse.BooleanOptionalAction, default=False,
+                    help="embedded broker sends fetched batches with vmsplice/splice (Kafka's "
+                         "sendfile analogue) instead of writev copies")
     ap.add_argument("--timeout", type=float, default=600.0)
     return ap.parse_args()
 
@@ -148,7 +151,8 @@ def main() -> int:
     # in one batch would turn every fetch into a 109 MB response
     rec_bytes = 12 * int(np.prod(net.input_shape)) * ipr  # ~Java float text per record
     rpb = max(1, min(rpb, (4 << 20) // rec_bytes))
-    broker = K.Broker(max_message_bytes=256 << 20, retention_bytes=1 << 62)
+    broker = K.Broker(max_message_bytes=256 << 20, retention_bytes=1 << 62,
+                      zero_copy=a.broker_zero_copy)
     broker.start()
     broker.create_topic("gale-in", parts)
     broker.create_topic("gale-out", 1)

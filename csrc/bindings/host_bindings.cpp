@@ -296,8 +296,9 @@ void bind_host(py::module_& m) {
   py::class_<Broker, std::shared_ptr<Broker>>(k, "Broker")
       .def(py::init([](const std::string& host, int port, int node_id, int default_partitions,
                        bool auto_create, int64_t max_message_bytes, int64_t retention_bytes,
-                       bool check_crcs) {
+                       bool check_crcs, bool zero_copy) {
              BrokerConfig c;
+             c.zero_copy = zero_copy;
              c.host = host;
              c.port = port;
              c.node_id = node_id;
@@ -311,7 +312,7 @@ void bind_host(py::module_& m) {
            py::arg("host") = "127.0.0.1", py::arg("port") = 0, py::arg("node_id") = 0,
            py::arg("default_partitions") = 1, py::arg("auto_create_topics") = true,
            py::arg("max_message_bytes") = 64ll << 20, py::arg("retention_bytes") = 4ll << 30,
-           py::arg("check_crcs") = true)
+           py::arg("check_crcs") = true, py::arg("zero_copy") = false)
       .def("start", &Broker::start)
       .def("stop", [](Broker& b) {
         py::gil_scoped_release nogil;
@@ -385,6 +386,7 @@ void bind_host(py::module_& m) {
         d["fetch_requests"] = s.fetch_requests;
         d["bytes_in"] = s.bytes_in;
         d["bytes_out"] = s.bytes_out;
+        d["bytes_spliced"] = s.bytes_spliced;
         d["records_in"] = s.records_in;
         d["connections"] = s.connections;
         return d;

@@ -69,6 +69,19 @@ struct Broker::Chunk {
 struct Broker::Conn {
   int fd = -1;
   std::deque<Chunk> out;
+  // zero-copy sends: the pipe, and references to recently spliced batches. The socket (and the
+  // peer's receive queue) may still reference their pages after splice() returns, so the last
+  // kSpliceKeepBytes sent stay alive here (more than both socket buffers can hold).
+  int pipe_rd = -1, pipe_wr = -1;
+  size_t pipe_cap = 0;
+  bool splice_ok = true;
+  std::deque<std::shared_ptr<const std::string>> spliced;
+  std::deque<size_t> spliced_len;
+  size_t spliced_bytes = 0;
+  ~Conn() {
+    if (pipe_rd >= 0) close(pipe_rd);
+    if (pipe_wr >= 0) close(pipe_wr);
+  }
   bool parked = false;
   FetchRequest fetch;
   int32_t fetch_corr = 0;
@@ -414,15 +427,89 @@ void Broker::serve(int fd) {
     if (!flush(c)) break;
   }
   close(fd);
+  if (!c.spliced.empty()) {
+    // data queued toward a peer that has not read it may still reference these pages: keep
+    // them for a grace period after the connection is gone
+    const int64_t now = now_ms();
+    std::lock_guard<std::mutex> lk(conn_mu_);
+    while (!spliced_grave_.empty() && now - spliced_grave_.front().first > 30000)
+      spliced_grave_.pop_front();
+    for (auto& p : c.spliced) spliced_grave_.emplace_back(now, std::move(p));
+  }
   std::lock_guard<std::mutex> lk(conn_mu_);
   conn_fds_.erase(std::remove(conn_fds_.begin(), conn_fds_.end(), fd), conn_fds_.end());
 }
 
+namespace {
+constexpr size_t kSpliceMinBytes = 64 << 10;    // smaller stored slices are just written
+constexpr size_t kSpliceKeepBytes = 96ull << 20;
+}  // namespace
+
+int Broker::splice_chunk(Conn& c, const Chunk& f) {
+  if (c.pipe_wr < 0) {
+    int fds[2];
+    if (pipe2(fds, O_CLOEXEC) != 0) return 0;
+    c.pipe_rd = fds[0];
+    c.pipe_wr = fds[1];
+    const int want = 1 << 20;  // (the unprivileged default pipe-max-size)
+    const int got = fcntl(c.pipe_wr, F_SETPIPE_SZ, want);
+    c.pipe_cap = got > 0 ? (size_t)got : (size_t)(64 << 10);
+  }
+  const char* p = f.data();
+  size_t left = f.len;
+  bool first = true;
+  while (left) {
+    iovec iv{const_cast<char*>(p), std::min(left, c.pipe_cap)};
+    const ssize_t n = vmsplice(c.pipe_wr, &iv, 1, 0);
+    if (n < 0) {
+      if (errno == EINTR) continue;
+      return first ? 0 : -1;  // unusable before any byte moved: fall back to write
+    }
+    first = false;
+    size_t m = (size_t)n;
+    while (m) {
+      const ssize_t w = splice(c.pipe_rd, nullptr, c.fd, nullptr, m, SPLICE_F_MOVE | SPLICE_F_MORE);
+      if (w < 0) {
+        if (errno == EINTR) continue;
+        return -1;
+      }
+      if (w == 0) return -1;
+      m -= (size_t)w;
+    }
+    p += n;
+    left -= (size_t)n;
+  }
+  c.spliced.push_back(f.shared);
+  c.spliced_len.push_back(f.len);
+  c.spliced_bytes += f.len;
+  while (c.spliced.size() > 1 && c.spliced_bytes - c.spliced_len.front() >= kSpliceKeepBytes) {
+    c.spliced_bytes -= c.spliced_len.front();
+    c.spliced.pop_front();
+    c.spliced_len.pop_front();
+  }
+  return 1;
+}
+
 bool Broker::flush(Conn& c) {
   while (!c.out.empty()) {
+    Chunk& head = c.out.front();
+    if (cfg_.zero_copy && c.splice_ok && head.shared && head.len >= kSpliceMinBytes) {
+      const int r = splice_chunk(c, head);
+      if (r < 0) return false;
+      if (r > 0) {
+        std::lock_guard<std::mutex> lk(mu_);
+        stats_.bytes_out += (int64_t)head.len;
+        stats_.bytes_spliced += (int64_t)head.len;
+        c.out.pop_front();
+        continue;
+      }
+      c.splice_ok = false;  // not supported here: plain writes from now on
+    }
     iovec iov[64];
     int n = 0;
     for (auto it = c.out.begin(); it != c.out.end() && n < 64; ++it, ++n) {
+      if (n > 0 && cfg_.zero_copy && c.splice_ok && it->shared && it->len >= kSpliceMinBytes)
+        break;  // (the next piece goes zero-copy)
       iov[n].iov_base = const_cast<char*>(it->data());
       iov[n].iov_len = it->len;
     }
