@@ -16,7 +16,8 @@
 // Pipeline: two LDS stages, one barrier per 64-deep k-step; the DMA of step k+1 is issued right
 // after the barrier and lands while the MFMAs of step k run (v_mfma_f32_16x16x32_bf16, each wave
 // owning a (BN/2) x 64 sub-tile = TN x TM 16x16 accumulators).
-// Epilogue: folded-BN bias + identity residual + ReLU, bf16 NHWC, 8-byte stores.
+// Epilogue: folded-BN bias + identity residual + ReLU, bf16 NHWC, staged through LDS so the
+// residual loads and output stores are 16-byte, whole-row accesses.
 // Grid: one workgroup per (pixel tile, channel tile), remapped so the tiles of one XCD are
 // contiguous (T1): the channel tiles of a pixel tile, which re-read the same im2col rows, share an L2.
 #include "common.cuh"
@@ -183,30 +184,61 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(GemmConvArgs a) {
     }
   }
 
-  // ---- epilogue: lane owns channels c..c+3 of pixel m for every (i, t) ----
+  // ---- epilogue through LDS: full-line global traffic ----
+  // A lane's accumulators hold 4 channels of one pixel (8-byte pieces of 16 pixel rows per
+  // store); instead each wave writes (acc + bias) as fp32 into its own LDS region, pixel-major,
+  // and reads back 8 consecutive channels per lane, so every residual load and output store is
+  // a 16-byte access and a wave instruction covers whole 128-byte rows. fp32 in LDS keeps the
+  // rounding identical to the register epilogue (one bf16 rounding after the residual/ReLU).
+  // Two halves of TM/2 pixel tiles each fit the 2-stage LDS allocation.
+  constexpr int CW = BN / WN;      // channels per wave
+  constexpr int EPS = CW + 4;      // fp32 row stride (+16 B: conflict-free 16-row writes)
+  constexpr int LPR = CW / 8;      // lanes per pixel row on read-back
+  constexpr int RPI = 64 / LPR;    // pixel rows per read-back instruction
+  constexpr int HALF = TM / 2 * 16;  // pixel rows per half
+  static_assert(4 * HALF * EPS * 4 <= 2 * STAGE, "epilogue staging exceeds the LDS allocation");
+  __syncthreads();  // every wave is done with the last k-stage
+  float* ep = reinterpret_cast<float*>(lds) + wave * HALF * EPS;
+  const int c0 = nt * BN + wn * CW;
+  const int mbase = mt * BM + wm * (BM / WM);
 #pragma unroll
-  for (int t = 0; t < TN; ++t) {
-    const int c = nt * BN + wn * (BN / WN) + t * 16 + fq * 4;
-    if (c >= a.Cout) continue;
-    const float4 b = *reinterpret_cast<const float4*>(a.bias + c);
+  for (int h = 0; h < 2; ++h) {
 #pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      const int m = mt * BM + wm * (BM / WM) + i * 16 + fr;
-      if (m >= a.M) continue;
-      const size_t o = (size_t)m * a.Cout + c;
-      float v0 = acc[i][t][0] + b.x, v1 = acc[i][t][1] + b.y;
-      float v2 = acc[i][t][2] + b.z, v3 = acc[i][t][3] + b.w;
-      if (a.has_res) {
-        const bf16x4 rr = __builtin_bit_cast(bf16x4, *reinterpret_cast<const uint2*>(a.res + o));
-        v0 += (float)rr[0]; v1 += (float)rr[1]; v2 += (float)rr[2]; v3 += (float)rr[3];
+    for (int t = 0; t < TN; ++t) {
+      const int cl = t * 16 + fq * 4;
+      const float4 b = *reinterpret_cast<const float4*>(a.bias + c0 + cl);
+#pragma unroll
+      for (int ii = 0; ii < TM / 2; ++ii) {
+        const int i = h * (TM / 2) + ii;
+        *reinterpret_cast<float4*>(ep + (ii * 16 + fr) * EPS + cl) =
+            make_float4(acc[i][t][0] + b.x, acc[i][t][1] + b.y, acc[i][t][2] + b.z,
+                        acc[i][t][3] + b.w);
       }
-      if (a.relu) {
-        v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f); v2 = fmaxf(v2, 0.f); v3 = fmaxf(v3, 0.f);
-      }
-      bf16x4 ov;
-      ov[0] = (bf16)v0; ov[1] = (bf16)v1; ov[2] = (bf16)v2; ov[3] = (bf16)v3;
-      *reinterpret_cast<uint2*>(a.y + o) = __builtin_bit_cast(uint2, ov);
     }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // (wave-private region)
+    const int cc = (lane % LPR) * 8;
+#pragma unroll
+    for (int r0 = 0; r0 < HALF; r0 += RPI) {
+      const int p = r0 + lane / LPR;
+      const int m = mbase + h * HALF + p;
+      if (m < a.M) {
+        const float* src = ep + p * EPS + cc;
+        const float4 lo = *reinterpret_cast<const float4*>(src);
+        const float4 hi = *reinterpret_cast<const float4*>(src + 4);
+        float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+        const size_t o = (size_t)m * a.Cout + c0 + cc;
+        if (a.has_res) {
+          const bf16x8 rr = ld_bf16x8(a.res + o);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] += (float)rr[e];
+        }
+        bf16x8 ov;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) ov[e] = (bf16)(a.relu ? fmaxf(v[e], 0.f) : v[e]);
+        *reinterpret_cast<uint4*>(a.y + o) = __builtin_bit_cast(uint4, ov);
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads done before the next half
   }
 }
 
