@@ -72,6 +72,8 @@ def parse_args():
     ap.add_argument("--broker-zero-copy", action=argparse.BooleanOptionalAction, default=False,
                     help="embedded broker sends fetched batches with vmsplice/splice (Kafka's "
                          "sendfile analogue) instead of writev copies")
+    ap.add_argument("--numa-pin", action=argparse.BooleanOptionalAction, default=False,
+                    help="pin the host pipeline's threads to the GPU's NUMA node")
     ap.add_argument("--timeout", type=float, default=600.0)
     return ap.parse_args()
 
@@ -129,6 +131,10 @@ def main() -> int:
         raise SystemExit("bench.py: no GPU visible (use --stub for the CPU plumbing run)")
     if use_gpu:
         torch.cuda.set_device(local_rank)
+        if a.numa_pin:
+            from gale.utils import pin_to_gpu_numa
+
+            pin_to_gpu_numa(local_rank)
     if world > 1:
         dist.init_process_group(backend="nccl" if use_gpu else "gloo",
                                 device_id=torch.device("cuda", local_rank) if use_gpu else None)

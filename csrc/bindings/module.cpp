@@ -154,6 +154,11 @@ PYBIND11_MODULE(_C, m) {
         });
   m.def("json_tile_count", &gale::json_tile_count);
   m.def("set_conv_path", &gale::set_conv_path);
+  m.def("device_pci_bus_id", [](int device) {
+    char buf[64] = {0};
+    chk(hipDeviceGetPCIBusId(buf, (int)sizeof(buf), device), "hipDeviceGetPCIBusId");
+    return std::string(buf);
+  });
   m.def("conv_path", &gale::conv_path);
   m.attr("JSON_TILE_BYTES") = gale::kJsonTileBytes;
   m.attr("JSON_RECORD_BYTES") = (int)sizeof(gale::JsonRecord);

@@ -24,6 +24,47 @@ def host_cpus_per_rank() -> float:
     return n / max(1, int(os.environ.get("LOCAL_WORLD_SIZE", "1")))
 
 
+def _parse_cpulist(text: str) -> set:
+    cpus = set()
+    for part in text.strip().split(","):
+        if not part:
+            continue
+        lo, _, hi = part.partition("-")
+        cpus.update(range(int(lo), int(hi or lo) + 1))
+    return cpus
+
+
+def gpu_numa_node(device: int) -> int:
+    """NUMA node of a GPU (its PCI function's sysfs ``numa_node``), -1 when unknown."""
+    from gale._native import native
+
+    try:
+        bdf = native().device_pci_bus_id(device).lower()
+        with open(f"/sys/bus/pci/devices/{bdf}/numa_node") as f:
+            return int(f.read().strip())
+    except (OSError, ValueError, RuntimeError):
+        return -1
+
+
+def pin_to_gpu_numa(device: int) -> set:
+    """Restrict this process's future threads to the CPUs of the GPU's NUMA node (within the
+    current affinity). The host pipeline moves ~35 KB of JSON per image through fetch buffers
+    that are DMA sources for this GPU: keeping its threads and their first-touch memory on the
+    GPU's socket avoids cross-socket copies. Returns the CPU set used (empty: left unpinned).
+    Call before the engine starts its threads (they inherit the creator's affinity)."""
+    node = gpu_numa_node(device)
+    if node < 0:
+        return set()
+    try:
+        with open(f"/sys/devices/system/node/node{node}/cpulist") as f:
+            cpus = _parse_cpulist(f.read()) & os.sched_getaffinity(0)
+    except OSError:
+        return set()
+    if cpus:
+        os.sched_setaffinity(0, cpus)
+    return cpus
+
+
 def free_port(host: str = "127.0.0.1") -> int:
     """An ephemeral TCP port that was free a moment ago (embedded brokers, rendezvous)."""
     s = socket.socket()
