@@ -72,8 +72,10 @@ def parse_args():
     ap.add_argument("--broker-zero-copy", action=argparse.BooleanOptionalAction, default=False,
                     help="embedded broker sends fetched batches with vmsplice/splice (Kafka's "
                          "sendfile analogue) instead of writev copies")
-    ap.add_argument("--numa-pin", action=argparse.BooleanOptionalAction, default=False,
+    ap.add_argument("--numa-pin", action=argparse.BooleanOptionalAction, default=True,
                     help="pin the host pipeline's threads to the GPU's NUMA node")
+    ap.add_argument("--cpus-per-rank", type=int, default=0,
+                    help="with --numa-pin: only this rank's slice of the node's CPUs (0 = all)")
     ap.add_argument("--timeout", type=float, default=600.0)
     return ap.parse_args()
 
@@ -134,7 +136,7 @@ def main() -> int:
         if a.numa_pin:
             from gale.utils import pin_to_gpu_numa
 
-            pin_to_gpu_numa(local_rank)
+            pin_to_gpu_numa(local_rank, a.cpus_per_rank)
     if world > 1:
         dist.init_process_group(backend="nccl" if use_gpu else "gloo",
                                 device_id=torch.device("cuda", local_rank) if use_gpu else None)

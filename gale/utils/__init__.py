@@ -46,12 +46,15 @@ def gpu_numa_node(device: int) -> int:
         return -1
 
 
-def pin_to_gpu_numa(device: int) -> set:
+def pin_to_gpu_numa(device: int, cpus_per_rank: int = 0) -> set:
     """Restrict this process's future threads to the CPUs of the GPU's NUMA node (within the
     current affinity). The host pipeline moves ~35 KB of JSON per image through fetch buffers
     that are DMA sources for this GPU: keeping its threads and their first-touch memory on the
-    GPU's socket avoids cross-socket copies. Returns the CPU set used (empty: left unpinned).
-    Call before the engine starts its threads (they inherit the creator's affinity)."""
+    GPU's socket avoids cross-socket copies. ``cpus_per_rank`` > 0 narrows it to this GPU's
+    own slice of the node (lowest CPU ids first: physical cores before their SMT siblings;
+    GPUs of one node take disjoint slices in device order), so the threads stop migrating over
+    the whole socket. Returns the CPU set used (empty: left unpinned). Call before the engine
+    starts its threads (they inherit the creator's affinity)."""
     node = gpu_numa_node(device)
     if node < 0:
         return set()
@@ -60,6 +63,12 @@ def pin_to_gpu_numa(device: int) -> set:
             cpus = _parse_cpulist(f.read()) & os.sched_getaffinity(0)
     except OSError:
         return set()
+    if cpus and cpus_per_rank > 0:
+        slot = sum(1 for d in range(device) if gpu_numa_node(d) == node)
+        ordered = sorted(cpus)
+        part = ordered[slot * cpus_per_rank:(slot + 1) * cpus_per_rank]
+        if len(part) == cpus_per_rank:
+            cpus = set(part)
     if cpus:
         os.sched_setaffinity(0, cpus)
     return cpus
