@@ -49,6 +49,8 @@ class GaleConfig:
     replicas: int = 0                  # INFERENCE_BOLT_PARAL; 0 = one per visible GPU
     sink_parallelism: int = 2          # KAFKA_BOLT_PARAL
     gpus: int = 0                      # GPUs to use (0 = all visible)
+    numa_pin: bool = True              # a process serving ONE GPU pins its threads to that
+                                       # GPU's NUMA node (gale.utils.pin_to_gpu_numa)
     # sink (R9, E7-E9)
     acks: int = 1                      # MainTopology.java:113
     sink_mode: str = "async"           # KafkaBolt async / sync / fire-and-forget

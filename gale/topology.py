@@ -132,6 +132,23 @@ def _dist_env():
             int(os.environ.get("LOCAL_RANK", "0")))
 
 
+def _pin_single_gpu(cfg: GaleConfig, devices) -> None:
+    """One GPU per process (a rank, or a single-GPU box): keep the host pipeline on its NUMA
+    node. A process spreading replicas over several GPUs is left unpinned."""
+    import torch
+
+    if devices is None:
+        n = torch.cuda.device_count() if torch.cuda.is_available() else 0
+        devices = [0] if (n == 1 or cfg.gpus == 1) else []
+    if len(devices) == 1:
+        from gale.utils import pin_to_gpu_numa
+
+        cpus = pin_to_gpu_numa(devices[0])
+        if cpus:
+            log.info("host pipeline pinned to the %d CPUs of GPU %d's NUMA node", len(cpus),
+                     devices[0])
+
+
 def run_topology(cfg: GaleConfig, stop_event: Optional[threading.Event] = None,
                  install_signals: bool = True) -> dict:
     """Serve ``cfg`` until its duration elapses, a signal arrives or ``stop_event`` is set.
@@ -162,6 +179,8 @@ def run_topology(cfg: GaleConfig, stop_event: Optional[threading.Event] = None,
             devices = [local_rank]
         if world > 1 and not cfg.partitions:
             cfg.partitions = rank_partitions(cfg, rank, world)
+        if cfg.numa_pin and not cfg.stub:
+            _pin_single_gpu(cfg, devices)
         engine = Engine(cfg, devices=devices)
         if install_signals and threading.current_thread() is threading.main_thread():
             for sig in (signal.SIGTERM, signal.SIGINT):
