@@ -196,3 +196,20 @@ def test_bad_config_is_rejected(broker):
         GaleConfig(sink_mode="bogus").validate()
     with pytest.raises(Exception):
         C.Engine(dict(input_topic="in", output_topic="out", on_error="explode"))
+
+
+def test_corrupt_batch_crc_marks_its_records(broker):
+    """The consumer-side CRC32C (fused with the envelope scan) rejects every record of a record
+    batch whose bytes were corrupted in flight; the other batches are served."""
+    rng = np.random.default_rng(5)
+    recs = [C.encode_instances(rng.random((1, H, W, CH), dtype=np.float32)) for _ in range(6)]
+    good = K.encode_batch([(None, r, -1, None) for r in recs[:3]], 0, 0)
+    bad = bytearray(K.encode_batch([(None, r, -1, None) for r in recs[3:]], 0, 0))
+    bad[len(bad) // 2] ^= 0x01  # a bit flip inside the second record's value
+    broker.append_batch_repeated("in", 0, good, 1)
+    broker.append_batch_repeated("in", 0, bytes(bad), 1)
+    eng, out = run(broker, 6, on_error="error-json")
+    vals = [r["value"] for r in out]
+    assert sum(b"predictions" in v for v in vals) == 3
+    errs = [json.loads(v)["error"] for v in vals if b"predictions" not in v]
+    assert errs == ["bad_envelope"] * 3
