@@ -20,6 +20,8 @@
 // residual loads and output stores are 16-byte, whole-row accesses.
 // Grid: one workgroup per (pixel tile, channel tile), remapped so the tiles of one XCD are
 // contiguous (T1): the channel tiles of a pixel tile, which re-read the same im2col rows, share an L2.
+#include <atomic>
+
 #include "common.cuh"
 #include "gale/kernels.h"
 
@@ -244,7 +246,8 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(GemmConvArgs a) {
 
 }  // namespace
 
-static int g_conv_path = 0;  // 0 auto, 1 never the GEMM path, 2 GEMM path whenever the shape allows
+// 0 auto, 1 never the GEMM path, 2 GEMM path whenever the shape allows (tests / A-B benches)
+static std::atomic<int> g_conv_path{0};
 void set_conv_path(int mode) { g_conv_path = mode; }
 int conv_path() { return g_conv_path; }
 
@@ -257,11 +260,10 @@ bool conv_gemm_supported(const ConvDesc& d, int batch, bool has_res) {
   if (d.Npad % bn != 0) return false;
   if (has_res && (d.res_C != d.Cout || d.res_stride != 1 || d.res_H != d.Ho || d.res_W != d.Wo))
     return false;
-  // enough workgroups to fill the chip (small late-stage layers at small batch keep conv_mfma)
+  // 32-bit element offsets inside the kernel. (No minimum size: measured faster than conv_mfma
+  // from ResNet-50 batch 64 up, including the 98-tile stage-4 layers, profiles/r1_resnet50_*.)
   const long long m = (long long)batch * d.Ho * d.Wo;
-  if (m >= (1ll << 31) || (long long)batch * d.H * d.W * d.Cin >= (1ll << 31)) return false;
-  const long long tiles = ((m + 127) / 128) * (d.Cout / bn);
-  return g_conv_path == 2 || tiles >= 1;
+  return m < (1ll << 31) && (long long)batch * d.H * d.W * d.Cin < (1ll << 31);
 }
 
 hipError_t conv2d_gemm(const ConvDesc& d, int batch, const void* x, const void* w,
