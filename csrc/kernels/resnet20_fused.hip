@@ -31,6 +31,8 @@
 // Reference parity: the model the reference serves is an opaque SavedModel fetched as
 // "output/Softmax:0" (InferenceBolt.java:81-86); numerics equal the layer-by-layer gale plan
 // (same rounding points) and are checked against the fp32 / fp8-emulation oracles in tests.
+#include <stdlib.h>
+
 #include "common.cuh"
 #include "gale/kernels.h"
 
@@ -122,12 +124,47 @@ __device__ __forceinline__ Q conv_q(const ResNet20Params& p, int i) {
   return Q{1.f, 1.f, 1.f};
 }
 
+// ---- weight prefetch into LDS (8-wave form, one workgroup per CU: 82 KB of LDS spare) ----
+// Every conv starts by hoisting its weights (A fragments) into registers; from global memory that
+// is an L2/HBM round trip that all waves wait for together, ~19 times per image. In the 8-wave
+// form the weights of conv i+1 are copied by LDS-DMA (global_load_lds_dwordx4) while conv i
+// computes, so the hoist reads LDS. One 1 KiB wave-instruction per chunk (lanes past the end of
+// the tensor are masked off; every packed size is a multiple of 16 bytes).
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+typedef __attribute__((address_space(1))) void* gbl_ptr_t;
+
+constexpr int kWeightLdsBytes = 64 * 576 * 2;  // largest packed conv weight (bf16)
+
+// packed weight bytes of conv i (Cout x Kpad x EB)
+__device__ __forceinline__ int conv_w_bytes(int i, int eb) {
+  const int n = i <= 6 ? 16 * 160 : i == 7 ? 32 * 160 : i <= 12 ? 32 * 288 : i == 13 ? 64 * 288
+                                                                                      : 64 * 576;
+  return n * eb;
+}
+
+template <int NW>
+__device__ __forceinline__ void prefetch_weights(const void* src, int bytes, void* dst) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int chunks = (bytes + 1023) >> 10;
+  for (int c = wave; c < chunks; c += NW)
+    if (c * 1024 + lane * 16 < bytes)
+      __builtin_amdgcn_global_load_lds(
+          (gbl_ptr_t)(static_cast<const char*>(src) + c * 1024 + lane * 16),
+          (lds_ptr_t)(static_cast<char*>(dst) + c * 1024), 16, 0, 0);
+}
+
+struct WPf {
+  void* wl;          // LDS weight buffer (nullptr: hoist from global, no prefetch)
+  const void* next;  // weights of the next conv (nullptr: none)
+  int next_bytes;
+};
+
 // zero the one-pixel border of a padded Hp x Wp x C image (C * EB % 16 == 0)
-template <bool F8, int HP, int WP, int C>
+template <bool F8, int NW, int HP, int WP, int C>
 __device__ __forceinline__ void zero_border(typename Ty<F8>::elem* buf) {
   constexpr int V = C * Ty<F8>::EB / 16;  // 16-byte vectors per cell
   constexpr int CELLS = 2 * WP + 2 * (HP - 2);
-  for (int i = threadIdx.x; i < CELLS * V; i += 256) {
+  for (int i = threadIdx.x; i < CELLS * V; i += 64 * NW) {
     const int cell = i / V, v = i - cell * V;
     int h, w;
     if (cell < WP) { h = 0; w = cell; }
@@ -141,15 +178,15 @@ __device__ __forceinline__ void zero_border(typename Ty<F8>::elem* buf) {
 // 3x3 pad-1 convolution LDS -> LDS with the folded-BN bias, optional residual and ReLU.
 // RES: 0 none, 1 identity (same layout as out), 2 option-A shortcut from the previous stage's
 // buffer (stride-2 subsample, channels >= RC are zero).
-template <bool F8, int CIN, int COUT, int S, int HO, int RES, int RC>
+template <bool F8, int NW, int CIN, int COUT, int S, int HO, int RES, int RC>
 __device__ __forceinline__ void conv3x3(const void* wgv, const float* __restrict__ wscale,
                                         const float* __restrict__ bias, Q q,
                                         const typename Ty<F8>::elem* in,
                                         typename Ty<F8>::elem* out,
-                                        const typename Ty<F8>::elem* res) {
+                                        const typename Ty<F8>::elem* res, WPf pf) {
   typedef Ty<F8> T;
   typedef typename T::elem elem;
-  const elem* wg = static_cast<const elem*>(wgv);
+  const elem* wg = static_cast<const elem*>(NW == 8 ? pf.wl : wgv);
   constexpr int WPI = HO * S + 2;  // padded input width
   constexpr int WPO = HO + 2;      // padded output width
   constexpr int RWP = 2 * HO + 2;  // padded width of an option-A residual source
@@ -158,9 +195,10 @@ __device__ __forceinline__ void conv3x3(const void* wgv, const float* __restrict
   constexpr int KS = KPAD / 32;
   constexpr int CT = COUT / 16;        // channel tiles
   constexpr int PT = HO * HO / 16;     // 16-pixel tiles
-  constexpr int WPC = 4 / CT;          // waves per channel tile
+  constexpr int WPC = NW / CT;         // waves per channel tile
   constexpr int PTW = PT / WPC;        // pixel tiles per wave
-  static_assert(PTW % 4 == 0, "pixel tiles per wave must be a multiple of 4");
+  constexpr int G = PTW < 4 ? PTW : 4;  // independent accumulators per pass
+  static_assert(WPC >= 1 && PTW >= 1 && PTW % G == 0, "wave partition of the conv");
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int g = lane >> 4, col = lane & 15;
   const int ct = wave / WPC;
@@ -184,32 +222,39 @@ __device__ __forceinline__ void conv3x3(const void* wgv, const float* __restrict
     sc = *reinterpret_cast<const float4*>(wscale + c0);
     sc.x *= q.deq; sc.y *= q.deq; sc.z *= q.deq; sc.w *= q.deq;
   }
+  if (pf.wl) {
+    // A fragments and epilogue constants in registers (no plain load may be pending once the
+    // DMA is in flight), every wave done reading the buffer, then refill it for the next conv
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (pf.next) prefetch_weights<NW>(pf.next, pf.next_bytes, pf.wl);
+  }
 
 #pragma unroll 1
-  for (int pg = 0; pg < PTW; pg += 4) {
-    int pbase[4], ho[4], wo[4];
+  for (int pg = 0; pg < PTW; pg += G) {
+    int pbase[G], ho[G], wo[G];
 #pragma unroll
-    for (int p = 0; p < 4; ++p) {
+    for (int p = 0; p < G; ++p) {
       const int m = (pt0 + pg + p) * 16 + col;
       ho[p] = m / HO;
       wo[p] = m - ho[p] * HO;
       pbase[p] = (ho[p] * S * WPI + wo[p] * S) * CIN;
     }
-    f32x4 acc[4];
+    f32x4 acc[G];
 #pragma unroll
-    for (int p = 0; p < 4; ++p) acc[p] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int p = 0; p < G; ++p) acc[p] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
-      typename T::frag b[4];
+      typename T::frag b[G];
 #pragma unroll
-      for (int p = 0; p < 4; ++p) b[p] = T::ld(in + pbase[p] + koff[ks]);
+      for (int p = 0; p < G; ++p) b[p] = T::ld(in + pbase[p] + koff[ks]);
 #pragma unroll
-      for (int p = 0; p < 4; ++p) acc[p] = T::mma(afr[ks], b[p], acc[p]);
+      for (int p = 0; p < G; ++p) acc[p] = T::mma(afr[ks], b[p], acc[p]);
       // bound how far the scheduler hoists LDS reads (register pressure -> occupancy)
       if (ks % 3 == 2) __builtin_amdgcn_sched_barrier(0);
     }
 #pragma unroll
-    for (int p = 0; p < 4; ++p) {
+    for (int p = 0; p < G; ++p) {
       float v0 = acc[p][0] * sc.x + bv.x, v1 = acc[p][1] * sc.y + bv.y;
       float v2 = acc[p][2] * sc.z + bv.z, v3 = acc[p][3] * sc.w + bv.w;
       const int o = ((ho[p] + 1) * WPO + wo[p] + 1) * COUT + c0;
@@ -222,11 +267,13 @@ __device__ __forceinline__ void conv3x3(const void* wgv, const float* __restrict
       T::store4(out + o, q.qout, fmaxf(v0, 0.f), fmaxf(v1, 0.f), fmaxf(v2, 0.f), fmaxf(v3, 0.f));
     }
   }
+  // the next conv's weights have landed before the caller's barrier
+  if (pf.wl && pf.next) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 // stem: 3x3x3 -> 16 over the 34x34x3 padded input (K = 27 padded to 32: one k step, the 8
 // k-values of a lane are 8 scalar LDS reads)
-template <bool F8>
+template <bool F8, int NW>
 __device__ __forceinline__ void stem(const void* wgv, const float* __restrict__ wscale,
                                      const float* __restrict__ bias, Q q,
                                      const typename Ty<F8>::elem* in,
@@ -250,13 +297,14 @@ __device__ __forceinline__ void stem(const void* wgv, const float* __restrict__ 
     sc = *reinterpret_cast<const float4*>(wscale + g * 4);
     sc.x *= q.deq; sc.y *= q.deq; sc.z *= q.deq; sc.w *= q.deq;
   }
+  constexpr int TPW = 64 / NW;  // 16-pixel tiles per wave (64 tiles of 32x32)
 #pragma unroll 1
-  for (int pg = 0; pg < 16; pg += 4) {
+  for (int pg = 0; pg < TPW; pg += 4) {
     f32x4 acc[4];
     int ho[4], wo[4];
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
-      const int m = (wave * 16 + pg + p) * 16 + col;
+      const int m = (wave * TPW + pg + p) * 16 + col;
       ho[p] = m >> 5;
       wo[p] = m & 31;
       const elem* px = in + (ho[p] * 34 + wo[p]) * 3;
@@ -280,8 +328,11 @@ __device__ __forceinline__ void stem(const void* wgv, const float* __restrict__ 
   }
 }
 
-template <bool F8>
-__global__ __launch_bounds__(256, 2) void resnet20_fused_kernel(ResNet20Params p,
+// NW waves per workgroup (one image per workgroup): 4 waves with 2 workgroups per CU, or 8 waves
+// with one workgroup per CU (every SIMD still runs 2 waves, but each image has twice the waves:
+// half the per-image latency when images are fewer than workgroup slots)
+template <bool F8, int NW>
+__global__ __launch_bounds__(64 * NW, 8 / NW) void resnet20_fused_kernel(ResNet20Params p,
                                                                          const float* x,
                                                                          float* out, int batch) {
   typedef Ty<F8> T;
@@ -296,19 +347,28 @@ __global__ __launch_bounds__(256, 2) void resnet20_fused_kernel(ResNet20Params p
   elem* T3 = base + kT3;
   elem* X3 = base + kX3;
   float* scratch = reinterpret_cast<float*>(base + kR1);
+  // 8-wave form: weights of the next conv prefetched into LDS behind the activations
+  void* wl = NW == 8 ? static_cast<void*>(smem + kElems * T::EB) : nullptr;
+  auto pfw = [&](int i) {
+    WPf f;
+    f.wl = wl;
+    f.next = i < 18 ? p.w[i + 1] : nullptr;
+    f.next_bytes = i < 18 ? conv_w_bytes(i + 1, T::EB) : 0;
+    return f;
+  };
   const float in_q = F8 ? 1.f / p.s_in[0] : 1.f;  // quantisation of the fp32 network input
 
   for (int img = blockIdx.x; img < batch; img += gridDim.x) {
     __syncthreads();  // the previous image's head is done with R0/R1
     // ---- stage the fp32 input image into the zero-bordered 34x34x3 IN ----
-    for (int i = threadIdx.x; i < 34 * 34 * 3; i += 256) {
+    for (int i = threadIdx.x; i < 34 * 34 * 3; i += 64 * NW) {
       const int cell = i / 3;
       const int h = cell / 34, w = cell - h * 34;
       if (h == 0 || h == 33 || w == 0 || w == 33) IN[i] = T::zero();
     }
-    zero_border<F8, 34, 34, 16>(X1);
+    zero_border<F8, NW, 34, 34, 16>(X1);
     const float4* xi = reinterpret_cast<const float4*>(x + (size_t)img * 3072);
-    for (int i = threadIdx.x; i < 768; i += 256) {
+    for (int i = threadIdx.x; i < 768; i += 64 * NW) {
       const float4 v = xi[i];
       const float e[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
@@ -320,62 +380,67 @@ __global__ __launch_bounds__(256, 2) void resnet20_fused_kernel(ResNet20Params p
       }
     }
     __syncthreads();
-    stem<F8>(p.w[0], p.ws[0], p.b[0], conv_q<F8>(p, 0), IN, X1);
+    stem<F8, NW>(p.w[0], p.ws[0], p.b[0], conv_q<F8>(p, 0), IN, X1);
+    if (wl) {  // conv 1's weights land during the barrier below and the border zeroing
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      prefetch_weights<NW>(p.w[1], conv_w_bytes(1, T::EB), wl);
+    }
     __syncthreads();
-    zero_border<F8, 34, 34, 16>(T1);  // IN is dead; T1's border overlaps its bytes
+    zero_border<F8, NW, 34, 34, 16>(T1);  // IN is dead; T1's border overlaps its bytes
     // ---- stage 1: 32x32x16 ----
 #pragma unroll 1
     for (int blk = 0; blk < 3; ++blk) {
       const int c1 = 1 + 2 * blk, c2 = c1 + 1;
-      conv3x3<F8, 16, 16, 1, 32, 0, 16>(p.w[c1], p.ws[c1], p.b[c1], conv_q<F8>(p, c1), X1, T1,
-                                        nullptr);
+      conv3x3<F8, NW, 16, 16, 1, 32, 0, 16>(p.w[c1], p.ws[c1], p.b[c1], conv_q<F8>(p, c1), X1, T1,
+                                        nullptr, pfw(c1));
       __syncthreads();
-      conv3x3<F8, 16, 16, 1, 32, 1, 16>(p.w[c2], p.ws[c2], p.b[c2], conv_q<F8>(p, c2), T1, X1,
-                                        X1);
+      conv3x3<F8, NW, 16, 16, 1, 32, 1, 16>(p.w[c2], p.ws[c2], p.b[c2], conv_q<F8>(p, c2), T1, X1,
+                                        X1, pfw(c2));
       __syncthreads();
     }
     // ---- stage 2: 16x16x32 ----
-    zero_border<F8, 18, 18, 32>(T2);
-    zero_border<F8, 18, 18, 32>(X2);
-    conv3x3<F8, 16, 32, 2, 16, 0, 16>(p.w[7], p.ws[7], p.b[7], conv_q<F8>(p, 7), X1, T2, nullptr);
+    zero_border<F8, NW, 18, 18, 32>(T2);
+    zero_border<F8, NW, 18, 18, 32>(X2);
+    conv3x3<F8, NW, 16, 32, 2, 16, 0, 16>(p.w[7], p.ws[7], p.b[7], conv_q<F8>(p, 7), X1, T2, nullptr, pfw(7));
     __syncthreads();
-    conv3x3<F8, 32, 32, 1, 16, 2, 16>(p.w[8], p.ws[8], p.b[8], conv_q<F8>(p, 8), T2, X2, X1);
+    conv3x3<F8, NW, 32, 32, 1, 16, 2, 16>(p.w[8], p.ws[8], p.b[8], conv_q<F8>(p, 8), T2, X2, X1, pfw(8));
     __syncthreads();
 #pragma unroll 1
     for (int blk = 1; blk < 3; ++blk) {
       const int c1 = 7 + 2 * blk, c2 = c1 + 1;
-      conv3x3<F8, 32, 32, 1, 16, 0, 32>(p.w[c1], p.ws[c1], p.b[c1], conv_q<F8>(p, c1), X2, T2,
-                                        nullptr);
+      conv3x3<F8, NW, 32, 32, 1, 16, 0, 32>(p.w[c1], p.ws[c1], p.b[c1], conv_q<F8>(p, c1), X2, T2,
+                                        nullptr, pfw(c1));
       __syncthreads();
-      conv3x3<F8, 32, 32, 1, 16, 1, 32>(p.w[c2], p.ws[c2], p.b[c2], conv_q<F8>(p, c2), T2, X2,
-                                        X2);
+      conv3x3<F8, NW, 32, 32, 1, 16, 1, 32>(p.w[c2], p.ws[c2], p.b[c2], conv_q<F8>(p, c2), T2, X2,
+                                        X2, pfw(c2));
       __syncthreads();
     }
     // ---- stage 3: 8x8x64 ----
-    zero_border<F8, 10, 10, 64>(T3);
-    zero_border<F8, 10, 10, 64>(X3);
-    conv3x3<F8, 32, 64, 2, 8, 0, 32>(p.w[13], p.ws[13], p.b[13], conv_q<F8>(p, 13), X2, T3,
-                                     nullptr);
+    zero_border<F8, NW, 10, 10, 64>(T3);
+    zero_border<F8, NW, 10, 10, 64>(X3);
+    conv3x3<F8, NW, 32, 64, 2, 8, 0, 32>(p.w[13], p.ws[13], p.b[13], conv_q<F8>(p, 13), X2, T3,
+                                     nullptr, pfw(13));
     __syncthreads();
-    conv3x3<F8, 64, 64, 1, 8, 2, 32>(p.w[14], p.ws[14], p.b[14], conv_q<F8>(p, 14), T3, X3, X2);
+    conv3x3<F8, NW, 64, 64, 1, 8, 2, 32>(p.w[14], p.ws[14], p.b[14], conv_q<F8>(p, 14), T3, X3, X2, pfw(14));
     __syncthreads();
 #pragma unroll 1
     for (int blk = 1; blk < 3; ++blk) {
       const int c1 = 13 + 2 * blk, c2 = c1 + 1;
-      conv3x3<F8, 64, 64, 1, 8, 0, 64>(p.w[c1], p.ws[c1], p.b[c1], conv_q<F8>(p, c1), X3, T3,
-                                       nullptr);
+      conv3x3<F8, NW, 64, 64, 1, 8, 0, 64>(p.w[c1], p.ws[c1], p.b[c1], conv_q<F8>(p, c1), X3, T3,
+                                       nullptr, pfw(c1));
       __syncthreads();
-      conv3x3<F8, 64, 64, 1, 8, 1, 64>(p.w[c2], p.ws[c2], p.b[c2], conv_q<F8>(p, c2), T3, X3,
-                                       X3);
+      conv3x3<F8, NW, 64, 64, 1, 8, 1, 64>(p.w[c2], p.ws[c2], p.b[c2], conv_q<F8>(p, c2), T3, X3,
+                                       X3, pfw(c2));
       __syncthreads();
     }
     // ---- head: global average pool (8x8) -> dense 64 -> 10 -> softmax ----
     {
-      const int c = threadIdx.x & 63, qq = threadIdx.x >> 6;  // 4 quarters of 16 pixels
+      constexpr int PPW = 64 / NW;  // pooled pixels per wave
+      const int c = threadIdx.x & 63, qq = threadIdx.x >> 6;
       float s = 0.f;
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int pix = qq * 16 + i;
+      for (int i = 0; i < PPW; ++i) {
+        const int pix = qq * PPW + i;
         const int h = pix >> 3, w = pix & 7;
         s += T::to_f32(X3[((h + 1) * 10 + w + 1) * 64 + c]);
       }
@@ -384,9 +449,10 @@ __global__ __launch_bounds__(256, 2) void resnet20_fused_kernel(ResNet20Params p
       if (threadIdx.x < 64) {
         const int lane = threadIdx.x;
         const float pool_scale = (F8 ? p.s_out[18] : 1.f) * (1.f / 64.f);
-        const float pooled =
-            (scratch[lane] + scratch[64 + lane] + scratch[128 + lane] + scratch[192 + lane]) *
-            pool_scale;
+        float acc = 0.f;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) acc += scratch[w * 64 + lane];
+        const float pooled = acc * pool_scale;
         float logit = -3.0e38f;
         for (int o = 0; o < 10; ++o) {
           const float t = wave_sum(p.fc_w[o * 64 + lane] * pooled);
@@ -419,17 +485,36 @@ hipError_t resnet20_fused_forward(const ResNet20Params& p, int batch, const floa
       (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
     cus = n > 0 ? n : 256;
   }
-  // resident workgroups per CU: 2 (bf16: LDS bound; fp8: register bound — its 39 KB of LDS
-  // would allow 4, but the hoisted A fragments need more than 128 VGPRs per lane)
-  const int grid_cap = 2 * cus;
+  // resident workgroups per CU: 2 of 4 waves (bf16: LDS bound; fp8: register bound — its 39 KB
+  // of LDS would allow 4, but the hoisted A fragments need more than 128 VGPRs per lane), or 1 of
+  // 8 waves. bf16 with no more images than CUs: the 8-wave form (each image gets twice the
+  // waves, weights prefetched into LDS; measured 62.3 -> 58.0 us at batch 1,
+  // profiles/r1_resnet20_waves_ab.txt). fp8 stays on 4 waves (its 8-wave form measured slower).
+  // GALE_R20_WAVES=4|8 pins the choice (A/B benches).
+  static int forced = -1;
+  if (forced < 0) {
+    const char* e = getenv("GALE_R20_WAVES");
+    forced = e ? atoi(e) : 0;
+  }
+  const int nw = forced == 4 || forced == 8 ? forced : (!f8 && batch <= cus ? 8 : 4);
+  const int grid_cap = nw == 8 ? cus : 2 * cus;
   const int grid = batch < grid_cap ? batch : grid_cap;
-  const size_t lds = (size_t)kElems * (f8 ? 1 : 2);
-  if (f8)
-    hipLaunchKernelGGL(resnet20_fused_kernel<true>, dim3(grid), dim3(256), lds, stream, p, x, out,
-                       batch);
-  else
-    hipLaunchKernelGGL(resnet20_fused_kernel<false>, dim3(grid), dim3(256), lds, stream, p, x,
+  const size_t lds = (size_t)kElems * (f8 ? 1 : 2) + (nw == 8 ? (size_t)kWeightLdsBytes : 0);
+  const dim3 block(64 * nw);
+  if (f8) {
+    if (nw == 8)
+      hipLaunchKernelGGL((resnet20_fused_kernel<true, 8>), dim3(grid), block, lds, stream, p, x,
+                         out, batch);
+    else
+      hipLaunchKernelGGL((resnet20_fused_kernel<true, 4>), dim3(grid), block, lds, stream, p, x,
+                         out, batch);
+  } else if (nw == 8) {
+    hipLaunchKernelGGL((resnet20_fused_kernel<false, 8>), dim3(grid), block, lds, stream, p, x,
                        out, batch);
+  } else {
+    hipLaunchKernelGGL((resnet20_fused_kernel<false, 4>), dim3(grid), block, lds, stream, p, x,
+                       out, batch);
+  }
   return hipGetLastError();
 }
 
