@@ -142,6 +142,15 @@ PYBIND11_MODULE(_C, m) {
                                   S(stream)),
               "cast_f32_bf16");
         });
+  m.def("bn_act",
+        [](int batch, int HW, int Wo, int C, uintptr_t x, uintptr_t scale, uintptr_t shift,
+           uintptr_t res, int res_H, int res_W, int res_C, int rs, int relu, uintptr_t y,
+           uintptr_t stream) {
+          chk(gale::bn_act(batch, HW, Wo, C, P(x), static_cast<const float*>(P(scale)),
+                           static_cast<const float*>(P(shift)), P(res), res_H, res_W, res_C, rs,
+                           relu, P(y), S(stream)),
+              "bn_act");
+        });
   m.def("json_parse_instances",
         [](int nrec, int ntiles, uintptr_t recs, uintptr_t tile_rec, uintptr_t bytes, int H,
            int W, int C, uintptr_t tile_counts, uintptr_t out, uintptr_t stream) {

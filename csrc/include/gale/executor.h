@@ -27,6 +27,8 @@ enum OpKind : int {
   OP_RESNET20 = 5,  // whole-network fused CIFAR ResNet-20; ptrs = 19 w, 19 b, fc_w, fc_b
                     // (+ 19 wscale for fp8), scales = 19 s_in, 19 s_out, 19 s_res (fp8)
   OP_STEM_PACK = 6, // p[0..4] = H, W, C, Wp, lp  (fp32 input -> packed-stem bf16 image)
+  OP_BN_ACT = 7,    // p[0..7] = HW, Wo, C, relu, res_H, res_W, res_C, res_stride; w = BN scale,
+                    // bias = BN shift (unfolded-BN plan: standalone BatchNorm + add + ReLU)
 };
 
 // Buffer ids: 0 = network input (fp32 NHWC), 1 = network output (fp32 [B, classes]),

@@ -99,6 +99,13 @@ hipError_t resnet20_fused_forward(const ResNet20Params& p, int batch, const floa
 hipError_t softmax_rows(int batch, int N, int ld, const float* x, float* out, hipStream_t stream);
 
 // fp32 -> bf16 cast with optional affine normalisation y = x*scale + shift (n elements).
+// Inference BatchNorm (per-channel scale/shift; nullptr = identity) + optional residual + ReLU
+// over NHWC bf16, [batch, HW = Ho*Wo, C stored]. The residual is [batch, res_H, res_W, res_C],
+// read at (ho*rs, wo*rs), zero for channels >= res_C. In-place (x == y) is allowed.
+hipError_t bn_act(int batch, int HW, int Wo, int C, const void* x, const float* scale,
+                  const float* shift, const void* res, int res_H, int res_W, int res_C, int rs,
+                  int relu, void* y, hipStream_t stream);
+
 hipError_t cast_f32_bf16(int64_t n, float scale, float shift, const float* x, void* y,
                          hipStream_t stream);
 

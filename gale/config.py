@@ -22,7 +22,9 @@ CHOICES = {
     "start_offset": ("latest", "earliest", "committed"),
     "value_format": ("json", "json-string"),
     "on_error": ("null", "error-json", "drop"),
-    "dtype": ("fp32", "bf16", "fp8"),
+    # compute dtype of the GPU kernels (MFMA bf16 / OCP e4m3 fp8); inputs and the softmax
+    # output stay fp32 as in the reference's TF graph (InferenceBolt.java:80-86)
+    "dtype": ("bf16", "fp8"),
     "model": ("lenet5", "resnet20", "resnet50"),
 }
 
@@ -69,6 +71,7 @@ class GaleConfig:
     max_wait_us: int = 2000
     queue_depth: int = 8192
     use_graph: bool = True
+    fold_bn: bool = True               # False: standalone BatchNorm kernels (debug/parity plan)
     stub: bool = False                 # CPU stub replicas (plumbing without a GPU)
     stub_null: bool = False            # stub replicas skip parsing/compute (host-path benchmark)
     # robustness / observability
@@ -100,6 +103,8 @@ class GaleConfig:
             raise ValueError("replicas/gpus must be >= 0")
         if not self.topology_name:
             raise ValueError("topology name is required")
+        if not self.fold_bn and self.dtype != "bf16":
+            raise ValueError("--no-fold-bn (standalone BatchNorm plan) is bf16 only")
         return self
 
     @property

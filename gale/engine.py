@@ -78,11 +78,11 @@ class Engine:
                 if not packed:
                     packed[dev] = materialize_weights(self.net, torch.device("cuda", dev),
                                                       seed=self.cfg.seed, wdtype=wdtype,
-                                                      params=params)
+                                                      params=params, fold_bn=self.cfg.fold_bn)
                 else:  # same process: device-to-device copy over xGMI
                     packed[dev] = next(iter(packed.values())).to(torch.device("cuda", dev))
             reps.append(ModelReplica(self.net, packed[dev], max_batch=self.cfg.max_batch,
-                                     slots=3, wdtype=wdtype))
+                                     slots=3, wdtype=wdtype, fold_bn=self.cfg.fold_bn))
         for r in reps:
             r.capture()
         return reps

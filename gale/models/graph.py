@@ -208,6 +208,26 @@ def fold_params(net: Network, p: Dict[str, torch.Tensor]) -> Dict[str, torch.Ten
     return f
 
 
+def unfolded_params(net: Network, p: Dict[str, torch.Tensor]) -> Dict[str, torch.Tensor]:
+    """Parameters for the unfolded-BN plan (``fold_bn=False``): raw conv weight/bias and each
+    BatchNorm as a per-channel affine (scale = gamma/sqrt(var+eps), shift = beta - mean*scale)
+    applied by the standalone ``bn_act`` kernel after the conv (TF's Conv2D -> FusedBatchNorm)."""
+    f: Dict[str, torch.Tensor] = {}
+    for L in net.layers:
+        if isinstance(L, Conv):
+            f[f"{L.name}.weight"] = p[f"{L.name}.weight"].float().contiguous()
+            f[f"{L.name}.bias"] = p.get(f"{L.name}.bias", torch.zeros(L.cout)).float().contiguous()
+            if L.bn:
+                s = p[f"{L.name}.bn.gamma"] / torch.sqrt(p[f"{L.name}.bn.var"] + BN_EPS)
+                f[f"{L.name}.bn_scale"] = s.float().contiguous()
+                f[f"{L.name}.bn_shift"] = (p[f"{L.name}.bn.beta"]
+                                           - p[f"{L.name}.bn.mean"] * s).float().contiguous()
+        elif isinstance(L, Head):
+            f[f"{L.name}.weight"] = p[f"{L.name}.weight"].float().contiguous()
+            f[f"{L.name}.bias"] = p[f"{L.name}.bias"].float().contiguous()
+    return f
+
+
 # --------------------------------------------------------------------------------------------
 # packing: one flat byte buffer, architecture-determined layout
 # --------------------------------------------------------------------------------------------
@@ -248,8 +268,12 @@ def _conv_geometry(net: Network, L: Conv, wdtype: str = "bf16") -> Dict[str, int
                 pad=L.pad, K=K, Kpad=Kpad, Npad=Npad)
 
 
-def param_layout(net: Network, wdtype: str = "bf16") -> Tuple[Dict[str, PackedEntry], int]:
-    """Byte layout of the packed parameter buffer (depends only on the architecture)."""
+def param_layout(net: Network, wdtype: str = "bf16",
+                 fold_bn: bool = True) -> Tuple[Dict[str, PackedEntry], int]:
+    """Byte layout of the packed parameter buffer (depends only on the architecture).
+    ``fold_bn=False`` (bf16 only) adds a BN scale and shift vector per BatchNorm conv."""
+    if not fold_bn and wdtype != "bf16":
+        raise ValueError("the unfolded-BN plan is bf16 only")
     wbytes = {"bf16": 2, "fp8": 1}[wdtype]
     layout: Dict[str, PackedEntry] = {}
     off = 0
@@ -267,6 +291,9 @@ def param_layout(net: Network, wdtype: str = "bf16") -> Tuple[Dict[str, PackedEn
             add(f"{L.name}.b", gm["Npad"] * 4, torch.float32, (gm["Npad"],))
             if wdtype == "fp8":
                 add(f"{L.name}.s", gm["Npad"] * 4, torch.float32, (gm["Npad"],))
+            if not fold_bn and L.bn:
+                add(f"{L.name}.bn_s", gm["Npad"] * 4, torch.float32, (gm["Npad"],))
+                add(f"{L.name}.bn_t", gm["Npad"] * 4, torch.float32, (gm["Npad"],))
         elif isinstance(L, Head):
             _, _, c = net.shapes[L.inp]
             cs = stored_channels(c)
@@ -291,9 +318,11 @@ def pack_conv_weight(w: torch.Tensor, cin_s: int, Npad: int, Kpad: int) -> torch
     return flat
 
 
-def pack_params(net: Network, folded: Dict[str, torch.Tensor], wdtype: str = "bf16") -> torch.Tensor:
-    """Fill the flat packed buffer (uint8 CPU tensor) from folded fp32 parameters."""
-    layout, total = param_layout(net, wdtype)
+def pack_params(net: Network, folded: Dict[str, torch.Tensor], wdtype: str = "bf16",
+                fold_bn: bool = True) -> torch.Tensor:
+    """Fill the flat packed buffer (uint8 CPU tensor) from folded fp32 parameters
+    (``fold_params``), or with ``fold_bn=False`` from ``unfolded_params``."""
+    layout, total = param_layout(net, wdtype, fold_bn)
     buf = torch.zeros(total, dtype=torch.uint8)
 
     def put(name: str, t: torch.Tensor):
@@ -322,6 +351,11 @@ def pack_params(net: Network, folded: Dict[str, torch.Tensor], wdtype: str = "bf
                 put(f"{L.name}.w", q)
                 put(f"{L.name}.s", s)
             put(f"{L.name}.b", b)
+            if not fold_bn and L.bn:
+                for key, src in (("bn_s", "bn_scale"), ("bn_t", "bn_shift")):
+                    v = torch.zeros(gm["Npad"])
+                    v[: L.cout] = folded[f"{L.name}.{src}"]
+                    put(f"{L.name}.{key}", v)
         elif isinstance(L, Head):
             _, _, c = net.shapes[L.inp]
             cs = stored_channels(c)
@@ -353,7 +387,7 @@ def act_scales_from_packed(net: Network, packed: torch.Tensor) -> Dict[str, floa
 # executor plan
 # --------------------------------------------------------------------------------------------
 
-OP_CONV, OP_MAXPOOL, OP_AVGPOOL, OP_HEAD, OP_SOFTMAX, OP_RESNET20, OP_STEM_PACK = range(7)
+OP_CONV, OP_MAXPOOL, OP_AVGPOOL, OP_HEAD, OP_SOFTMAX, OP_RESNET20, OP_STEM_PACK, OP_BN_ACT = range(8)
 
 
 def is_cifar_resnet20(net: Network) -> bool:
@@ -391,21 +425,23 @@ def _tensor_bytes(net: Network, name: str, wdtype: str = "bf16") -> int:
 
 def build_plan(net: Network, base_ptr: int, wdtype: str = "bf16",
                act_scales: Optional[Dict[str, float]] = None,
-               fused: bool = True) -> Tuple[List[dict], List[int]]:
+               fused: bool = True, fold_bn: bool = True) -> Tuple[List[dict], List[int]]:
     """Executor plan for a packed parameter buffer living at device address ``base_ptr``.
 
     Returns (ops, buf_bytes_per_image). Buffer 0 = fp32 input, 1 = fp32 softmax output, >= 2 =
     bf16 (fp8: e4m3) activations assigned by liveness so concurrently-live tensors never share a
     buffer. ``act_scales`` (fp8 only): per-tensor scales, see ``act_scales_from_packed``.
     ``fused``: the CIFAR ResNet-20 (bf16 or fp8) becomes ONE whole-network kernel (activations
-    resident in LDS).
+    resident in LDS). ``fold_bn=False`` (bf16, layer-wise; the buffer from ``pack_params(...,
+    fold_bn=False)``): every BatchNorm conv is followed by a standalone ``bn_act`` kernel that
+    applies the BN affine, the residual and the ReLU in place (the debugging / parity plan).
     """
     fp8 = wdtype == "fp8"
     if fp8 and act_scales is None:
         raise ValueError("build_plan: the fp8 plan needs the activation scales")
-    if fused and is_cifar_resnet20(net):
+    if fused and fold_bn and is_cifar_resnet20(net):
         return _fused_resnet20_plan(net, base_ptr, wdtype, act_scales)
-    layout, _ = param_layout(net, wdtype)
+    layout, _ = param_layout(net, wdtype, fold_bn)
     # liveness: last layer index reading each tensor
     last_use: Dict[str, int] = {}
     for i, L in enumerate(net.layers):
@@ -456,7 +492,10 @@ def build_plan(net: Network, base_ptr: int, wdtype: str = "bf16",
                 d["in_scale"] = act_scales[L.inp]
                 d["out_scale"] = 1.0 if L.out_f32 else act_scales[L.out]
             res = -1
-            if L.residual is not None:
+            unfold = not fold_bn and L.bn
+            if unfold:
+                d["relu"] = 0  # BN, residual and ReLU move to the bn_act op below
+            if L.residual is not None and not unfold:
                 rh, rw, rc = net.shapes[L.residual]
                 d.update(has_res=1, res_H=rh, res_W=rw, res_C=stored_channels(rc),
                          res_stride=2 if L.res_mode == "pad" else 1)
@@ -469,6 +508,18 @@ def build_plan(net: Network, base_ptr: int, wdtype: str = "bf16",
             if wdtype == "fp8":
                 op["wscale"] = base_ptr + layout[f"{L.name}.s"].offset
             ops.append(op)
+            if unfold:
+                ho, wo, c = net.shapes[L.out]
+                bn = dict(kind=OP_BN_ACT, **{"in": buf_of[out_name]}, out=buf_of[out_name], res=-1,
+                          w=base_ptr + layout[f"{L.name}.bn_s"].offset,
+                          bias=base_ptr + layout[f"{L.name}.bn_t"].offset)
+                p = [ho * wo, wo, stored_channels(c), int(L.relu), 0, 0, 0, 1]
+                if L.residual is not None:
+                    rh, rw, rc = net.shapes[L.residual]
+                    p[4:] = [rh, rw, stored_channels(rc), 2 if L.res_mode == "pad" else 1]
+                    bn["res"] = buf_of[L.residual]
+                bn["p"] = p
+                ops.append(bn)
         elif isinstance(L, MaxPool):
             h, w, c = net.shapes[L.inp]
             ho, wo, _ = net.shapes[L.out]

@@ -120,6 +120,39 @@ def softmax(x: torch.Tensor, n: Optional[int] = None) -> torch.Tensor:
     return out
 
 
+def batchnorm(x: torch.Tensor, scale: Optional[torch.Tensor], shift: Optional[torch.Tensor],
+              relu: bool = False, residual: Optional[torch.Tensor] = None,
+              res_mode: str = "identity", out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Inference BatchNorm as a per-channel affine (scale = gamma/sqrt(var+eps),
+    shift = beta - mean*scale; None = identity), + optional residual + ReLU. x: [B,H,W,C] bf16
+    (C % 8 == 0); scale/shift: fp32 [>= C]. ``res_mode="pad"``: ResNet option-A shortcut
+    (residual read at (2h, 2w), zero above its channel count). ``out`` may alias ``x``."""
+    _check(x, torch.bfloat16, "x")
+    B, H, W, C = x.shape
+    sp = hp = 0
+    if scale is not None:
+        _check(scale, torch.float32, "scale")
+        _check(shift, torch.float32, "shift")
+        if scale.numel() < C or shift.numel() < C:
+            raise ValueError("batchnorm: scale/shift shorter than the channel count")
+        sp, hp = scale.data_ptr(), shift.data_ptr()
+    rp, rh, rw, rc, rs = 0, 0, 0, 0, 1
+    if residual is not None:
+        _check(residual, torch.bfloat16, "residual")
+        _, rh, rw, rc = residual.shape
+        rs = 2 if res_mode == "pad" else 1
+        rp = residual.data_ptr()
+    y = torch.empty_like(x) if out is None else out
+    native().bn_act(B, H * W, W, C, x.data_ptr(), sp, hp, rp, rh, rw, rc, rs, int(relu),
+                    y.data_ptr(), _stream())
+    return y
+
+
+def relu(x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Standalone ReLU over a bf16 NHWC tensor (the conv epilogue fuses it on the fast path)."""
+    return batchnorm(x, None, None, relu=True, out=out)
+
+
 def cast_bf16(x: torch.Tensor, scale: float = 1.0, shift: float = 0.0) -> torch.Tensor:
     _check(x, torch.float32, "x")
     y = torch.empty(x.shape, device=x.device, dtype=torch.bfloat16)

@@ -14,24 +14,28 @@ from typing import Optional
 import torch
 import torch.distributed as dist
 
-from gale.models.graph import Network, fold_params, init_params, pack_params, param_layout
+from gale.models.graph import (Network, fold_params, init_params, pack_params, param_layout,
+                               unfolded_params)
 
 
 def host_packed_params(net: Network, seed: int = 0, wdtype: str = "bf16",
-                       params: Optional[dict] = None) -> torch.Tensor:
+                       params: Optional[dict] = None, fold_bn: bool = True) -> torch.Tensor:
     if params is None:
         params = init_params(net, seed=seed)
+    if not fold_bn:
+        return pack_params(net, unfolded_params(net, params), wdtype, fold_bn=False)
     return pack_params(net, fold_params(net, params), wdtype)
 
 
 def materialize_weights(net: Network, device: torch.device, seed: int = 0, wdtype: str = "bf16",
-                        src: int = 0, group=None, params: Optional[dict] = None) -> torch.Tensor:
+                        src: int = 0, group=None, params: Optional[dict] = None,
+                        fold_bn: bool = True) -> torch.Tensor:
     """Return the packed parameter buffer on ``device``, identical on every rank of ``group``."""
-    _, total = param_layout(net, wdtype)
+    _, total = param_layout(net, wdtype, fold_bn)
     distributed = dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1
     rank = dist.get_rank() if distributed else src
     if rank == src:
-        buf = host_packed_params(net, seed, wdtype, params).to(device)
+        buf = host_packed_params(net, seed, wdtype, params, fold_bn).to(device)
     else:
         buf = torch.empty(total, dtype=torch.uint8, device=device)
     if distributed:

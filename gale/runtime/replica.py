@@ -18,7 +18,7 @@ from gale.models.graph import Network, act_scales_from_packed, build_plan
 class ModelReplica:
     def __init__(self, net: Network, packed: torch.Tensor, max_batch: int = 256, slots: int = 2,
                  buckets: Optional[Sequence[int]] = None, wdtype: str = "bf16",
-                 fused: bool = True):
+                 fused: bool = True, fold_bn: bool = True):
         if not packed.is_cuda:
             raise RuntimeError("ModelReplica needs the packed weights on a GPU")
         self.net = net
@@ -26,7 +26,8 @@ class ModelReplica:
         self.device = packed.device
         self.wdtype = wdtype
         self.act_scales = act_scales_from_packed(net, packed) if wdtype == "fp8" else None
-        ops, buf_bytes = build_plan(net, packed.data_ptr(), wdtype, self.act_scales, fused=fused)
+        ops, buf_bytes = build_plan(net, packed.data_ptr(), wdtype, self.act_scales, fused=fused,
+                                    fold_bn=fold_bn)
         self.ops = ops
         self.buf_bytes = buf_bytes
         self.executor = native().Executor(packed.device.index or 0, ops, buf_bytes, max_batch,

@@ -194,6 +194,11 @@ def test_backpressure_small_queue(broker):
 def test_bad_config_is_rejected(broker):
     with pytest.raises(ValueError):
         GaleConfig(sink_mode="bogus").validate()
+    with pytest.raises(ValueError):
+        GaleConfig(dtype="fp32").validate()  # no silent bf16 stand-in for an fp32 request
+    with pytest.raises(ValueError):
+        GaleConfig(dtype="fp8", fold_bn=False).validate()
+    GaleConfig(fold_bn=False).validate()
     with pytest.raises(Exception):
         C.Engine(dict(input_topic="in", output_topic="out", on_error="explode"))
 

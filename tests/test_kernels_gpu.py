@@ -326,3 +326,33 @@ def test_stem_pack_layout():
     ref = torch.zeros(B, H, Wp, 4)
     ref[:, :, lp:lp + W, :C] = x
     assert torch.equal(y.cpu(), ref.to(torch.bfloat16))
+
+
+@pytest.mark.parametrize("mode", ["none", "identity", "pad"])
+def test_batchnorm_residual_relu(mode):
+    """Standalone inference BatchNorm (+ residual + ReLU) vs fp32, incl. the option-A shortcut."""
+    g = torch.Generator().manual_seed(8)
+    B, H, W, C = 3, 8, 10, 32
+    x = (torch.randn(B, H, W, C, generator=g) * 2).bfloat16()
+    scale = torch.rand(C, generator=g) + 0.5
+    shift = torch.randn(C, generator=g)
+    ref = x.float() * scale + shift
+    res = None
+    if mode == "identity":
+        res = torch.randn(B, H, W, C, generator=g).bfloat16()
+        ref = ref + res.float()
+    elif mode == "pad":
+        res = torch.randn(B, 2 * H, 2 * W, 16, generator=g).bfloat16()
+        ref[..., :16] += res.float()[:, ::2, ::2, :]
+    ref = ref.clamp(min=0)
+    y = ops.batchnorm(x.to(DEV), scale.to(DEV), shift.to(DEV), relu=True,
+                      residual=None if res is None else res.to(DEV),
+                      res_mode="pad" if mode == "pad" else "identity").float().cpu()
+    assert torch.all((y - ref).abs() <= ref.abs() * 8e-3 + 1e-3)
+
+
+def test_relu_standalone_in_place():
+    x = torch.randn(2, 5, 7, 24, generator=torch.Generator().manual_seed(2)).bfloat16().to(DEV)
+    want = x.clamp(min=0).cpu()
+    y = ops.relu(x, out=x)
+    assert y.data_ptr() == x.data_ptr() and torch.equal(x.cpu(), want)

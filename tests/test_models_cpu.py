@@ -88,3 +88,38 @@ def test_resnet20_plan_is_one_fused_kernel():
     convs = [op for op in layered if op["kind"] == 0]
     assert [op["w"] for op in convs] == ops[0]["ptrs"][:19]
     assert [op["bias"] for op in convs] == ops[0]["ptrs"][19:38]
+
+
+@pytest.mark.parametrize("name", ["resnet20", "resnet50"])
+def test_unfolded_bn_plan_structure(name):
+    """fold_bn=False: every BatchNorm conv is followed by one in-place bn_act op that carries
+    the BN affine, the residual and the ReLU; the conv itself is linear."""
+    from gale.models import unfolded_params
+    from gale.models.graph import OP_BN_ACT, OP_CONV
+
+    net = get_model(name)
+    params = init_params(net, seed=3, calib_batch=2)
+    ops, _ = build_plan(net, 0, fold_bn=False)
+    bn_convs = [L for L in net.layers if isinstance(L, Conv) and L.bn]
+    bn_ops = [i for i, o in enumerate(ops) if o["kind"] == OP_BN_ACT]
+    assert len(bn_ops) == len(bn_convs) > 0
+    for i, L in zip(bn_ops, bn_convs):
+        conv, bn = ops[i - 1], ops[i]
+        assert conv["kind"] == OP_CONV and conv["conv"]["relu"] == 0 and conv["res"] == -1
+        assert "has_res" not in conv["conv"]
+        assert bn["in"] == bn["out"] == conv["out"] and bn["p"][3] == int(L.relu)
+        assert (bn["res"] >= 0) == (L.residual is not None) and bn["res"] != bn["out"]
+    layout, total = param_layout(net, "bf16", fold_bn=False)
+    u = unfolded_params(net, params)
+    buf = pack_params(net, u, "bf16", fold_bn=False)
+    assert buf.numel() == total
+    L = bn_convs[-1]
+    e = layout[f"{L.name}.bn_s"]
+    got = buf[e.offset: e.offset + e.nbytes].view(torch.float32)[: L.cout]
+    assert torch.equal(got, u[f"{L.name}.bn_scale"])
+    # the affine after the raw conv is the folded conv, exactly in fp32 algebra
+    f = fold_params(net, params)
+    s, t = u[f"{L.name}.bn_scale"], u[f"{L.name}.bn_shift"]
+    assert torch.allclose(u[f"{L.name}.bias"] * s + t, f[f"{L.name}.bias"], atol=1e-5)
+    with pytest.raises(ValueError):
+        param_layout(net, "fp8", fold_bn=False)

@@ -131,3 +131,27 @@ def test_resnet20_fp8_fused_matches_layerwise():
     assert (a - b).abs().mean().item() < 2e-3
     assert (a - emu).abs().mean().item() < 5e-3
     assert (a.argmax(1) == b.argmax(1)).float().mean().item() > 0.97
+
+
+@pytest.mark.parametrize("name,batch", [("resnet20", 21), ("resnet50", 2)])
+def test_unfolded_bn_plan_matches_reference(name, batch):
+    """The debugging / parity plan: raw convs + standalone BatchNorm(+residual+ReLU) kernels
+    against the fp32 oracle, eager and graph replay."""
+    from gale.models.graph import OP_BN_ACT
+
+    net = get_model(name)
+    params = init_params(net, seed=17, calib_batch=4 if name == "resnet50" else 16)
+    packed = materialize_weights(net, torch.device("cuda", 0), params=params, fold_bn=False)
+    rep = ModelReplica(net, packed, max_batch=32, slots=1, fold_bn=False)
+    assert sum(op["kind"] == OP_BN_ACT for op in rep.ops) > 0
+    x = torch.rand((batch,) + net.input_shape, generator=torch.Generator().manual_seed(4))
+    ref = forward(net, fold_params(net, params), x)
+    eager = rep.infer_eager(x).cpu()
+    graph = rep.infer(x, use_graph=True).cpu()
+    torch.cuda.synchronize()
+    err = (eager - ref).abs().max().item()
+    assert err < 4e-2, f"{name}: max |p - p_ref| = {err}"
+    top2 = ref.topk(2, dim=1).values
+    clear = (top2[:, 0] - top2[:, 1]) > 0.05
+    assert torch.equal(eager.argmax(1)[clear], ref.argmax(1)[clear])
+    assert torch.equal(graph, eager)
