@@ -81,3 +81,18 @@ def test_bench_stub_rate_mode():
     assert r["load"].startswith("offered 3000")
     assert 0.7 * 3000 < r["value"] < 1.3 * 3000
     assert r["p50_latency_ms"] < 50
+
+
+def test_scaling_driver_stub_1_2():
+    """tools/scaling.py: bench.py at N = 1 (plain process) and N = 2 (torch.distributed.run,
+    gloo stub ranks), one JSON line per N and a summary with the weak-scaling efficiency."""
+    cmd = [sys.executable, "tools/scaling.py", "--gpus", "1,2", "--stub", "--steps", "4",
+           "--warmup", "1", "--timeout", "240", "--", "--batch", "32", "--distinct", "64",
+           "--replicas-per-gpu", "2", "--stub-null", "--timeout", "120"]
+    out = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=600,
+                         env=dict(os.environ, OMP_NUM_THREADS="1"))
+    assert out.returncode == 0, out.stdout[-3000:] + out.stderr[-3000:]
+    lines = [json.loads(x) for x in out.stdout.splitlines() if x.startswith("{")]
+    assert [r["n_gpus"] for r in lines[:2]] == [1, 2]
+    sc = lines[-1]["scaling"]
+    assert set(sc) == {"1", "2"} and sc["1"]["efficiency"] == 1.0 and sc["2"]["efficiency"] > 0

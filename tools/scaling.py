@@ -1,0 +1,104 @@
+#!/usr/bin/env python3
+"""Scaling curve of the headline benchmark (BASELINE.json: whole-node images/s + p50 latency,
+CIFAR-10 ResNet-20 at 1/2/4/8 GPUs).
+
+Runs ``bench.py`` once per GPU count N on ONE node -- N = 1 as a plain process, N > 1 under
+``torch.distributed.run`` (one rank per GPU, RCCL over xGMI, rendezvous on 127.0.0.1) -- and
+prints one JSON line per N plus a summary with the per-N images/s, p50/p99 latency and the
+weak-scaling efficiency value(N) / (N * value(1)). Every run is a child process (never an exec),
+bounded by ``--timeout``; the sweep stops at the first failing N.
+
+The reference has no benchmark of its own (E12 storm-perf is declared in
+pom.xml:44-54 but unused); this is the new framework's storm-perf-style scaling driver.
+
+    python tools/scaling.py --gpus 1,2,4,8 --steps 100 --warmup 10 [-- extra bench.py args]
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import socket
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def bench_cmd(n: int, steps: int, warmup: int, extra: list, stub: bool = False) -> list:
+    args = [os.path.join(ROOT, "bench.py"), "--gpus", str(n), "--steps", str(steps),
+            "--warmup", str(warmup)] + (["--stub"] if stub else []) + list(extra)
+    if n == 1:
+        return [sys.executable] + args
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+            f"--nproc-per-node={n}", "--master-addr", "127.0.0.1",
+            "--master-port", str(free_port())] + args
+
+
+def last_json(text: str):
+    for line in reversed(text.splitlines()):
+        line = line.strip()
+        if line.startswith("{") and '"metric"' in line:
+            return json.loads(line)
+    return None
+
+
+def efficiency(results: dict) -> dict:
+    """Weak-scaling efficiency value(N) / (N * value(1)) for every measured N."""
+    if 1 not in results:
+        return {}
+    base = results[1]["value"]
+    return {n: round(r["value"] / (n * base), 4) for n, r in sorted(results.items())}
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser(description=__doc__.split("\n\n")[0])
+    ap.add_argument("--gpus", default="1,2,4,8", help="comma-separated GPU counts")
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--stub", action="store_true", help="CPU stub replicas (gloo; plumbing)")
+    ap.add_argument("--timeout", type=float, default=900.0, help="seconds per bench run")
+    ap.add_argument("--out", default="", help="also append the JSON lines to this file")
+    ap.add_argument("extra", nargs=argparse.REMAINDER, help="-- extra bench.py arguments")
+    a = ap.parse_args(argv)
+    extra = a.extra[1:] if a.extra[:1] == ["--"] else a.extra
+    counts = [int(x) for x in a.gpus.split(",") if x.strip()]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", MASTER_ADDR="127.0.0.1")
+    results = {}
+    for n in counts:
+        cmd = bench_cmd(n, a.steps, a.warmup, extra, a.stub)
+        try:
+            p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True,
+                               timeout=a.timeout)
+        except subprocess.TimeoutExpired:
+            print(json.dumps({"n_gpus": n, "error": f"timed out after {a.timeout:.0f}s"}))
+            break
+        r = last_json(p.stdout)
+        if p.returncode != 0 or r is None:
+            tail = (p.stderr or p.stdout)[-2000:]
+            print(json.dumps({"n_gpus": n, "error": f"rc={p.returncode}", "tail": tail}))
+            break
+        results[n] = r
+        print(json.dumps(r), flush=True)
+        if a.out:
+            with open(a.out, "a") as f:
+                f.write(json.dumps(r) + "\n")
+    eff = efficiency(results)
+    summary = {"scaling": {str(n): {"images_per_s": r["value"],
+                                    "p50_ms": r.get("p50_latency_ms"),
+                                    "p99_ms": r.get("p99_latency_ms"),
+                                    "efficiency": eff.get(n)}
+                           for n, r in sorted(results.items())}}
+    print(json.dumps(summary), flush=True)
+    return 0 if len(results) == len(counts) else 1
+
+
+if __name__ == "__main__":
+    sys.exit(main())
