@@ -1,24 +1,32 @@
 #!/usr/bin/env python3
 """Headline benchmark (BASELINE.json): whole-node images/s + p50 latency of the streaming
-inference topology, CIFAR-10 ResNet-20 bf16, one data-parallel replica per GPU.
+inference topology, CIFAR-10 ResNet-20 bf16, one data-parallel replica group per GPU.
 
 What one rank (= one GPU, launched by torch.distributed.run for N > 1) does:
 
-* starts an embedded Kafka-protocol broker on 127.0.0.1 (one Kafka partition per replica,
-  BASELINE config 3) and preloads its input topic with synthetic InstObj records
-  ``{"instances": [[[[...32x32x3 Java-formatted floats...]]]]}`` (~35 KB of JSON per image);
+* starts an embedded Kafka-protocol broker on 127.0.0.1. With N ranks the N brokers form ONE
+  Kafka cluster: the input topic has N x P partitions, partition p led by rank p % N's broker,
+  and every rank consumes exactly the partitions it leads (one partition per replica, BASELINE
+  config 3) - so all ranks share one input topic, as the reference's spouts share INPUT_TOPIC;
+* feeds the input partitions with synthetic InstObj records ``{"instances": [[[[...]]]]}``
+  (32x32x3 Java-formatted floats, ~35 KB of JSON per image) drawn from ``--distinct`` distinct
+  images (default 65536, ~2.3 GB of JSON, so the host stages stream from DRAM, not from cache).
+  The pre-encoded batches are appended by reference and kept topped up ahead of the consumers;
+  the broker stamps them with LogAppendTime, so record end-to-end latency (append -> produce
+  ack) is measured exactly;
 * initialises ResNet-20 weights on rank 0 (seeded random init) and RCCL-broadcasts the packed
   buffer over xGMI to every other rank;
-* runs the full gale engine: Kafka Fetch over TCP -> envelope scan -> micro-batcher -> pinned
-  staging -> H2D -> GPU JSON parse -> hipGraph ResNet-20 forward -> D2H softmax ->
+* runs the full gale engine: Kafka Fetch over TCP -> envelope scan + CRC32C -> micro-batcher ->
+  pinned H2D -> GPU JSON parse -> hipGraph ResNet-20 forward -> D2H softmax ->
   {"predictions": ...} encode -> Kafka Produce (acks=1) -> ack.
 
-A "step" is one micro-batch per replica, i.e. ``--batch x --replicas-per-gpu`` images per GPU
-completing that whole path (acknowledged by the broker). W warmup
-steps run first (graphs are captured before that), then exactly K timed steps, bracketed by a
-barrier + ``torch.cuda.synchronize()``. ``value`` is the whole-job aggregate images/s (sum over
-ranks of timed images / the slowest rank's time). p50 latency = median time from a record's
-fetch to its output record's produce-ack, over all timed records of rank 0 (queue included).
+Steady state: warm-up is W steps AND at least ``--min-warmup-s`` seconds AND until two
+consecutive 250 ms windows agree within 5 % (capped at ``--max-warmup-s``). A step is
+``--step-images`` images per GPU (default 65536: 256 micro-batches of 256) completing the whole
+path (acknowledged by the broker), so the default K = 20 steps is a >= 1 s window on one
+MI355X. The K timed steps are bracketed by a barrier + ``torch.cuda.synchronize()``; ``value``
+is the whole-job images/s (sum over ranks of the images completed in the window / the slowest
+rank's window). The per-step rates give the within-run spread.
 """
 
 from __future__ import annotations
@@ -26,8 +34,9 @@ from __future__ import annotations
 import argparse
 import json
 import os
-import resource
+import statistics
 import sys
+import threading
 import time
 
 import numpy as np
@@ -38,15 +47,19 @@ sys.path.insert(0, ROOT)
 METRIC = "images/sec (whole node) + p50 latency, CIFAR-10 ResNet-20 at 1/2/4/8 GPUs"
 
 
-def parse_args():
+def parse_args(argv=None):
     ap = argparse.ArgumentParser(description=__doc__.split("\n\n")[0])
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=100)
-    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--step-images", type=int, default=65536,
+                    help="images per GPU per step (the unit of --steps / --warmup)")
+    ap.add_argument("--min-warmup-s", type=float, default=2.0)
+    ap.add_argument("--max-warmup-s", type=float, default=20.0)
     ap.add_argument("--model", default="resnet20", choices=["lenet5", "resnet20", "resnet50"])
     ap.add_argument("--batch", type=int, default=256, help="images per micro-batch (max_batch)")
     ap.add_argument("--images-per-record", type=int, default=1)
-    ap.add_argument("--distinct", type=int, default=1024, help="distinct synthetic images")
+    ap.add_argument("--distinct", type=int, default=65536, help="distinct synthetic images")
     ap.add_argument("--partitions", type=int, default=0,
                     help="input partitions per GPU (default: one per replica, BASELINE config 3)")
     ap.add_argument("--source-parallelism", type=int, default=0,
@@ -60,6 +73,8 @@ def parse_args():
     ap.add_argument("--queue-batches", type=int, default=4,
                     help="records buffered in the engine, in units of --batch")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp8"])
+    ap.add_argument("--slo-p99-ms", type=float, default=0.0,
+                    help="latency-SLO mode: adapt the batch/wait bound to keep p99 under this")
     ap.add_argument("--stub", action="store_true", help="CPU stub replicas (no GPU)")
     ap.add_argument("--stub-null", action="store_true",
                     help="stub replicas skip parsing (measures the host Kafka/codec path only)")
@@ -68,7 +83,7 @@ def parse_args():
     ap.add_argument("--rate", type=float, default=0.0,
                     help="offered load in images/s per GPU: records are appended to the broker "
                          "at this rate while the engine runs (latency under load, BASELINE "
-                         "config 5); 0 = a preloaded backlog (maximum throughput)")
+                         "config 5); 0 = a backlog kept ahead of the consumers (max throughput)")
     ap.add_argument("--broker-zero-copy", action=argparse.BooleanOptionalAction, default=False,
                     help="embedded broker sends fetched batches with vmsplice/splice (Kafka's "
                          "sendfile analogue) instead of writev copies")
@@ -76,37 +91,61 @@ def parse_args():
                     help="pin the host pipeline's threads to the GPU's NUMA node")
     ap.add_argument("--cpus-per-rank", type=int, default=0,
                     help="with --numa-pin: only this rank's slice of the node's CPUs (0 = all)")
+    ap.add_argument("--encode-threads", type=int, default=0,
+                    help="threads for encoding the synthetic records (0 = host CPU share)")
     ap.add_argument("--timeout", type=float, default=600.0)
-    return ap.parse_args()
+    return ap.parse_args(argv)
 
 
-class RateFeeder:
-    """Appends pre-encoded record batches (by reference) to the input partitions at a fixed
-    image rate from a background thread: an open-loop load generator, so latency is measured
-    at a known offered load instead of against a backlog."""
+class Feeder:
+    """Keeps the rank's input partitions supplied from a native BatchSet (batches appended by
+    reference). Backlog mode (rate = 0): tops every partition up to ``ahead`` records past the
+    engine's fetch position, so the consumers never starve and the log never holds more than
+    a bounded backlog. Rate mode: an open-loop generator appending at a fixed image rate."""
 
-    def __init__(self, broker, topic, parts, batches, images_per_batch, rate):
-        import threading
-
-        self.broker, self.topic, self.parts, self.batches = broker, topic, parts, batches
-        self.ipb, self.rate = images_per_batch, rate
+    def __init__(self, broker, topic, parts, bset, rate=0.0, ahead_records=0):
+        self.broker, self.topic, self.parts, self.bset = broker, topic, list(parts), bset
+        self.rate, self.ahead = rate, ahead_records
+        self.rpb = max(1, bset.records // len(bset))
+        self.ipb = self.rpb * bset.images_per_record
+        self.engine = None
+        self._next = 0
         self._stop = threading.Event()
-        self._t = threading.Thread(target=self._run, name="rate-feeder", daemon=True)
+        self._t = threading.Thread(target=self._run, name="feeder", daemon=True)
+
+    def fill(self, records_per_partition):
+        for p in self.parts:
+            n = -(-records_per_partition // self.rpb)
+            self.broker.append_cycled(self.topic, p, self.bset, n, self._next)
+            self._next += n
 
     def _run(self):
-        t0 = time.perf_counter()
-        sent = 0
-        i = 0
-        while not self._stop.is_set():
-            due = (time.perf_counter() - t0) * self.rate
-            while sent + self.ipb <= due:
-                self.broker.append_batch_repeated(self.topic, i % self.parts,
-                                                  self.batches[i % len(self.batches)], 1)
-                sent += self.ipb
-                i += 1
-            time.sleep(0.0002)
+        if self.rate > 0:
+            t0, sent, i = time.perf_counter(), 0, 0
+            while not self._stop.is_set():
+                due = (time.perf_counter() - t0) * self.rate
+                while sent + self.ipb <= due:
+                    self.broker.append_cycled(self.topic, self.parts[i % len(self.parts)],
+                                              self.bset, 1, self._next)
+                    self._next += 1
+                    sent += self.ipb
+                    i += 1
+                time.sleep(0.0002)
+            return
+        while not self._stop.wait(0.005):
+            eng = self.engine
+            if eng is None:
+                continue
+            pos = {o["partition"]: o["fetched"] for o in eng.partition_offsets()}
+            for p in self.parts:
+                short = pos.get(p, 0) + self.ahead - self.broker.log_end(self.topic, p)
+                if short > 0:
+                    n = -(-short // self.rpb)
+                    self.broker.append_cycled(self.topic, p, self.bset, n, self._next)
+                    self._next += n
 
-    def start(self):
+    def start(self, engine):
+        self.engine = engine
         self._t.start()
 
     def stop(self):
@@ -114,13 +153,30 @@ class RateFeeder:
         self._t.join()
 
 
-def main() -> int:
-    a = parse_args()
+def warm_up(eng, records, a, rate_window=0.25):
+    """W steps, then until >= min_warmup_s elapsed and two consecutive windows agree within 5 %
+    (or max_warmup_s). Returns (seconds, last window rates)."""
+    t_start = time.perf_counter()
+    if not eng.wait_completed(records, a.timeout):
+        raise SystemExit(f"warm-up timed out ({eng.completed}/{records})")
+    rates = []
+    while True:
+        c0, t0 = eng.completed, time.perf_counter()
+        time.sleep(rate_window)
+        rates.append((eng.completed - c0) / (time.perf_counter() - t0))
+        el = time.perf_counter() - t_start
+        stable = len(rates) >= 2 and abs(rates[-1] - rates[-2]) <= 0.05 * max(rates[-2:])
+        if (el >= a.min_warmup_s and stable) or el >= a.max_warmup_s:
+            return el, rates[-2:]
+
+
+def main(argv=None) -> int:
+    a = parse_args(argv)
+    from gale.utils import host_cpus_per_rank, thread_cpu_seconds
+
     if a.replicas_per_gpu <= 0:
         # the host pipeline (Kafka fetch + CRC + scan + encode + produce, and the embedded
-        # broker of this rank) needs ~3 cores per replica at full rate
-        from gale.utils import host_cpus_per_rank
-
+        # broker of this rank) needs ~3-4 cores per replica at full rate
         a.replicas_per_gpu = max(1, min(4, int(host_cpus_per_rank() // 4)))
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -143,92 +199,101 @@ def main() -> int:
 
     from gale._native import native
     from gale.config import GaleConfig
-    from gale.data import encode_batches, encode_records, preload, synthetic_images
+    from gale.data import synthetic_images
     from gale.engine import Engine
     from gale.models import get_model
 
     net = get_model(a.model)
     K = native().kafka
     ipr = a.images_per_record
-    parts = a.partitions or a.replicas_per_gpu
-    # records per preloaded RecordBatch (rate mode: small batches, arrivals are not bursty)
-    # (the feeder thread keeps to ~10k appends/s)
+    parts_per_rank = a.partitions or a.replicas_per_gpu
+    # records per RecordBatch: a producer's batch (rate mode: small batches, arrivals are not
+    # bursty; the feeder keeps to ~10k appends/s) ...
     rpb = min(64, max(8, int(a.rate // 10000))) if a.rate > 0 else 64
     # ... and at most ~4 MB per RecordBatch, as a producer's batch.size would keep it: a fetch
     # always returns at least one whole batch (KIP-74), so 64 ResNet-50 records (1.7 MB each)
     # in one batch would turn every fetch into a 109 MB response
     rec_bytes = 12 * int(np.prod(net.input_shape)) * ipr  # ~Java float text per record
     rpb = max(1, min(rpb, (4 << 20) // rec_bytes))
-    broker = K.Broker(max_message_bytes=256 << 20, retention_bytes=1 << 62,
-                      zero_copy=a.broker_zero_copy)
-    broker.start()
-    broker.create_topic("gale-in", parts)
-    broker.create_topic("gale-out", 1)
-    # slack: the pipeline keeps fetching past the timed window until stop() (records are
-    # appended by reference, so generous slack costs no memory)
-    step_images = a.batch * a.replicas_per_gpu  # one micro-batch per replica
-    per_rank_images = ((a.warmup + a.steps + 4) * step_images + 8192 * ipr
-                       + 4 * a.queue_batches * a.batch + parts * 1024 * ipr)
-    n_records = -(-per_rank_images // ipr)
-    distinct = max(rpb, (a.distinct // (ipr * rpb)) * rpb) * ipr
+    distinct = max(rpb * ipr, (a.distinct // (rpb * ipr)) * rpb * ipr)
+    t_enc = time.perf_counter()
     imgs = synthetic_images(distinct, net.input_shape, seed=1234 + rank)
-    batches = encode_batches(encode_records(imgs, ipr), rpb)
-    if a.rate <= 0:
-        for p in range(parts):
-            preload(broker, "gale-in", p, batches, -(-n_records // parts), rpb)
+    enc_threads = a.encode_threads or max(1, int(host_cpus_per_rank()))
+    bset = K.synthetic_batches(imgs, ipr, rpb, enc_threads)
     del imgs
-    feeder = None
-    if a.rate > 0:
-        feeder = RateFeeder(broker, "gale-in", parts, batches, rpb * ipr, a.rate)
+    t_enc = time.perf_counter() - t_enc
+
+    broker = K.Broker(node_id=rank, max_message_bytes=256 << 20, retention_bytes=1 << 62,
+                      zero_copy=a.broker_zero_copy, log_append_time=True)
+    broker.start()
+    n_parts = world * parts_per_rank
+    if world > 1:
+        ports = [None] * world
+        dist.all_gather_object(ports, broker.port)
+        broker.set_cluster([(r, "127.0.0.1", int(ports[r])) for r in range(world)])
+    broker.create_topic("gale-in", n_parts)
+    broker.create_topic("gale-out", world)
+    my_parts = [p for p in range(n_parts) if p % world == rank]  # the partitions this rank leads
+    step_images = a.step_images
+    step_records = -(-step_images // ipr)
+    feeder = Feeder(broker, "gale-in", my_parts, bset, rate=a.rate,
+                    ahead_records=-(-max(step_records, 65536 // ipr) // len(my_parts)))
+    if a.rate <= 0:
+        feeder.fill(feeder.ahead)
+    if world > 1:
+        dist.barrier()  # every broker of the cluster is up and has its topics
 
     cfg = GaleConfig(topology_name=f"bench-r{rank}", input_topic="gale-in",
                      output_topic="gale-out", bootstrap=f"127.0.0.1:{broker.port}",
+                     partitions=",".join(map(str, my_parts)),
                      group_id="bench", start_offset="earliest", model=a.model, dtype=a.dtype,
                      max_batch=a.batch, max_wait_us=a.max_wait_us,
                      queue_depth=max(1, a.queue_batches * a.batch // ipr),
-                     source_parallelism=a.source_parallelism or parts,
+                     source_parallelism=a.source_parallelism or len(my_parts),
                      sink_parallelism=a.sink_parallelism, replicas=a.replicas_per_gpu,
-                     decode_threads=a.decode_threads,
+                     decode_threads=a.decode_threads, slo_p99_ms=a.slo_p99_ms,
                      stub=a.stub, stub_null=a.stub_null, commit_interval_ms=500,
                      check_crcs=a.check_crcs)
     devices = [local_rank] if use_gpu else None
-    warm_records = -(-max(1, a.warmup) * step_images // ipr)
-    timed_records = -(-a.steps * step_images // ipr)
     # ONE engine: warm-up and timed window are the same steady-state pipeline (connections,
     # pinned fetch buffers, captured graphs all warm); the timed window starts at a barrier
-    # once every rank has completed its warm-up records and ends when K more steps completed.
+    # once every rank has warmed up and ends when K more steps completed on this rank.
     eng = Engine(cfg, devices=devices)  # weights: seeded on rank 0, RCCL-broadcast
     eng.start()
-    if feeder:
-        feeder.start()
-    if not eng.wait_completed(warm_records, a.timeout):
-        raise SystemExit(f"rank {rank}: warm-up timed out ({eng.completed}/{warm_records})")
+    feeder.start(eng)
+    warm_s, warm_rates = warm_up(eng, max(1, a.warmup) * step_records, a)
     warm_done = eng.completed
     if world > 1:
         dist.barrier()
     if use_gpu:
         torch.cuda.synchronize()
     eng.reset_stats()
+    cpu0 = thread_cpu_seconds()
     c0 = eng.completed
     t0 = time.perf_counter()
-    ru0 = resource.getrusage(resource.RUSAGE_SELF)
-    reached = eng.wait_completed(c0 + timed_records, a.timeout)
+    marks = []
+    reached = True
+    for k in range(1, a.steps + 1):
+        if not eng.wait_completed(c0 + k * step_records, a.timeout):
+            reached = False
+            break
+        marks.append(time.perf_counter())
     if use_gpu:
         torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    ru1 = resource.getrusage(resource.RUSAGE_SELF)
+    cpu1 = thread_cpu_seconds()
     done_records = eng.completed - c0
-    cpu_s = (ru1.ru_utime - ru0.ru_utime) + (ru1.ru_stime - ru0.ru_stime)
     st = eng.stats()
     if world > 1:
         dist.barrier()
-    if feeder:
-        feeder.stop()
+    feeder.stop()
     eng.stop()
+    if world > 1:
+        dist.barrier()  # (sinks produce to every rank's broker: stop brokers after all engines)
     broker.stop()
     if not reached:
         raise SystemExit(f"rank {rank}: timed out after {elapsed:.1f}s "
-                         f"({done_records}/{timed_records} records)")
+                         f"({done_records}/{a.steps * step_records} records)")
     images = done_records * ipr  # >= K steps (completions arrive a micro-batch at a time)
     t = torch.tensor([elapsed, float(images)], dtype=torch.float64)
     if world > 1:
@@ -242,31 +307,47 @@ def main() -> int:
         elapsed_max, total_images = elapsed, float(images)
     if rank == 0:
         value = total_images / elapsed_max
+        step_rates = [step_records * ipr / (b - a_) for a_, b in zip([t0] + marks[:-1], marks)]
+        med = statistics.median(step_rates)
+        cores = {k: round((cpu1[k] - cpu0[k]) / elapsed, 2) for k in cpu1}
         out = {
             "metric": METRIC, "value": round(value, 1), "unit": "images/s", "n_gpus": world,
             "steps": a.steps, "warmup": a.warmup,
-            # time per step-equivalent of completed work (>= K steps completed in the window)
-            "ms_per_step": round(elapsed_max / (total_images / (step_images * world)) * 1e3, 4),
+            "ms_per_step": round(elapsed_max / a.steps * 1e3, 4),
             "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": a.dtype,
-            "data": f"synthetic (uniform [0,1) {'x'.join(map(str, net.input_shape))} InstObj "
-                    "JSON records, Java float format, preloaded into an embedded Kafka-protocol "
-                    "broker); random-init weights (seed 0) RCCL-broadcast from rank 0",
-            "config": {"model": a.model, "global_batch": step_images * world, "seq_len": None,
-                       "parallelism": f"dp{world}", "images_per_record": ipr,
+            "data": f"synthetic ({distinct} distinct uniform [0,1) "
+                    f"{'x'.join(map(str, net.input_shape))} images as InstObj JSON records, "
+                    "Java float format, fed through an embedded Kafka-protocol broker cluster, "
+                    "one broker per rank); random-init weights (seed 0) RCCL-broadcast from "
+                    "rank 0",
+            "step": f"{step_images} images per GPU through fetch->parse->forward->produce-ack",
+            "config": {"model": a.model, "global_batch": a.batch * a.replicas_per_gpu * world,
+                       "seq_len": None, "parallelism": f"dp{world}",
+                       "images_per_record": ipr, "max_batch": a.batch,
                        "max_wait_us": a.max_wait_us, "replicas_per_gpu": a.replicas_per_gpu,
+                       "partitions": n_parts, "step_images_per_gpu": step_images,
                        "path": "kafka-fetch->gpu-json-parse->hipgraph-forward->kafka-produce"},
             "load": (f"offered {a.rate:.0f} images/s per GPU" if a.rate > 0
-                     else "preloaded backlog (max throughput; latency includes queueing)"),
+                     else "backlog kept ahead of the consumers (max throughput; latency "
+                          "includes queueing)"),
+            "timed_s": round(elapsed_max, 3),
             "p50_latency_ms": round(st["e2e_us_p50"] / 1e3, 3),
             "p99_latency_ms": round(st["e2e_us_p99"] / 1e3, 3),
+            "record_e2e_ms_p50": round(st["record_e2e_ms_p50"], 2),
+            "record_e2e_ms_p99": round(st["record_e2e_ms_p99"], 2),
             "device_ms_p50": round(st["device_us_p50"] / 1e3, 3),
             "batch_images_mean": round(st["batch_images_mean"], 1),
+            "step_rate_spread": {"min": round(min(step_rates)), "median": round(med),
+                                 "max": round(max(step_rates)),
+                                 "range_pct": round(100 * (max(step_rates) - min(step_rates))
+                                                    / med, 1)},
+            "warmup_s": round(warm_s, 2), "warmup_rates": [round(r) for r in warm_rates],
             "json_mb_per_s_rank0": round(st["bytes_in"] / elapsed / 1e6, 1),
-            "cpu_cores_busy_rank0": round(cpu_s / elapsed, 2),
+            "cpu_cores_busy_rank0": round(sum(cores.values()), 2),
+            "cpu_cores_by_stage_rank0": cores,
+            "encode_s": round(t_enc, 1),
             "warmup_records": warm_done,
-            "rank0_thread_s": {k[9:]: round(v, 3) for k, v in st.items()
-                               if k.startswith("thread_s_")},
         }
         print(json.dumps(out), flush=True)
     if world > 1:

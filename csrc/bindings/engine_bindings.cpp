@@ -47,6 +47,7 @@ EngineConfig config_from_dict(const py::dict& d) {
   opt(d, "classes", c.classes);
   opt(d, "max_batch", c.max_batch);
   opt(d, "max_wait_us", c.max_wait_us);
+  opt(d, "slo_p99_ms", c.slo_p99_ms);
   opt(d, "queue_depth", c.queue_depth);
   opt(d, "watchdog_ms", c.watchdog_ms);
   opt(d, "max_restarts", c.max_restarts);

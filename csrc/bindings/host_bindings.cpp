@@ -4,6 +4,9 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <atomic>
+#include <thread>
+
 #include "../codec/json_codec.h"
 #include "../kafka/broker.h"
 #include "../kafka/client.h"
@@ -92,6 +95,63 @@ py::bytes py_encode_batch(py::list records, int64_t base_offset, int64_t base_ts
   Writer w;
   encode_batch(w, ins.data(), ins.size(), base_offset, base_ts);
   return py::bytes(w.buf);
+}
+
+// Pre-encoded RecordBatch v2 blobs held natively and appended to the embedded broker by
+// reference (bench preloading / open-loop feeding): the distinct payload is materialised once.
+struct BatchSet {
+  std::vector<std::shared_ptr<const std::string>> batches;
+  std::vector<int32_t> records;  // records per batch
+  int64_t images_per_record = 1;
+  size_t bytes = 0;
+};
+
+// Encode images [N, H, W, C] as InstObj JSON records (images_per_record each, Java float text)
+// grouped records_per_batch per Kafka batch, on `threads` threads. key_prefix non-empty: record
+// j (0-based over the whole set) gets key "<key_prefix><j>".
+std::shared_ptr<BatchSet> synthetic_batches(const float* x, int64_t n, int H, int W, int C,
+                                            int ipr, int rpb, int threads,
+                                            const std::string& key_prefix) {
+  if (ipr <= 0 || rpb <= 0 || n <= 0) throw std::invalid_argument("synthetic_batches: bad sizes");
+  auto bs = std::make_shared<BatchSet>();
+  bs->images_per_record = ipr;
+  const int64_t nrec = (n + ipr - 1) / ipr;
+  const int64_t nb = (nrec + rpb - 1) / rpb;
+  bs->batches.resize((size_t)nb);
+  bs->records.resize((size_t)nb);
+  const size_t img = (size_t)H * W * C;
+  std::atomic<int64_t> next{0};
+  auto work = [&] {
+    std::vector<std::string> vals, keys;
+    std::vector<RecordIn> ins;
+    for (int64_t b; (b = next++) < nb;) {
+      const int64_t r0 = b * rpb, r1 = std::min<int64_t>(nrec, r0 + rpb);
+      vals.assign((size_t)(r1 - r0), std::string());
+      keys.assign((size_t)(r1 - r0), std::string());
+      ins.assign((size_t)(r1 - r0), RecordIn());
+      for (int64_t r = r0; r < r1; ++r) {
+        const int64_t i0 = r * ipr, cnt = std::min<int64_t>(ipr, n - i0);
+        codec::encode_instances(x + (size_t)i0 * img, (int)cnt, H, W, C, vals[(size_t)(r - r0)]);
+        RecordIn& ri = ins[(size_t)(r - r0)];
+        ri.value = vals[(size_t)(r - r0)];
+        if (!key_prefix.empty()) {
+          keys[(size_t)(r - r0)] = key_prefix + std::to_string(r);
+          ri.key = keys[(size_t)(r - r0)];
+          ri.key_null = false;
+        }
+      }
+      Writer w;
+      encode_batch(w, ins.data(), ins.size(), 0, 0);
+      bs->records[(size_t)b] = (int32_t)(r1 - r0);
+      bs->batches[(size_t)b] = std::make_shared<const std::string>(std::move(w.buf));
+    }
+  };
+  std::vector<std::thread> ts;
+  for (int t = 1; t < std::max(1, threads); ++t) ts.emplace_back(work);
+  work();
+  for (auto& t : ts) t.join();
+  for (auto& b : bs->batches) bs->bytes += b->size();
+  return bs;
 }
 
 std::vector<std::string> strs(const py::handle& o) { return o.cast<std::vector<std::string>>(); }
@@ -275,10 +335,45 @@ void bind_host(py::module_& m) {
     const std::string_view s = view(b);
     return crc32c(reinterpret_cast<const uint8_t*>(s.data()), s.size());
   });
+  k.def("crc32c_combine", &crc32c_combine, py::arg("crc_a"), py::arg("crc_b"), py::arg("len_b"));
   k.def("murmur2", [](py::bytes b) {
     const std::string_view s = view(b);
     return murmur2(reinterpret_cast<const uint8_t*>(s.data()), s.size());
   });
+  py::class_<BatchSet, std::shared_ptr<BatchSet>>(k, "BatchSet")
+      .def_static("from_bytes", [](py::list blobs) {
+        auto bs = std::make_shared<BatchSet>();
+        for (auto o : blobs) {
+          const std::string_view v = view(o.cast<py::bytes>());
+          const BatchInfo bi = peek_batch(reinterpret_cast<const uint8_t*>(v.data()), v.size(),
+                                          false);
+          bs->batches.push_back(std::make_shared<const std::string>(v));
+          bs->records.push_back(bi.records);
+          bs->bytes += v.size();
+        }
+        return bs;
+      })
+      .def("__len__", [](const BatchSet& b) { return b.batches.size(); })
+      .def_property_readonly("bytes", [](const BatchSet& b) { return b.bytes; })
+      .def_property_readonly("records", [](const BatchSet& b) {
+        int64_t n = 0;
+        for (int32_t r : b.records) n += r;
+        return n;
+      })
+      .def_property_readonly("images_per_record",
+                             [](const BatchSet& b) { return b.images_per_record; })
+      .def("records_in", [](const BatchSet& b, size_t i) { return b.records.at(i); })
+      .def("batch", [](const BatchSet& b, size_t i) { return py::bytes(*b.batches.at(i)); });
+  k.def("synthetic_batches", [](py::array_t<float, py::array::c_style | py::array::forcecast> x,
+                                int ipr, int rpb, int threads, const std::string& key_prefix) {
+    if (x.ndim() != 4) throw std::invalid_argument("images must be [N, H, W, C]");
+    const float* p = x.data();
+    const int64_t n = x.shape(0);
+    const int H = (int)x.shape(1), W = (int)x.shape(2), C = (int)x.shape(3);
+    py::gil_scoped_release nogil;
+    return synthetic_batches(p, n, H, W, C, ipr, rpb, threads, key_prefix);
+  }, py::arg("images"), py::arg("images_per_record") = 1, py::arg("records_per_batch") = 64,
+     py::arg("threads") = 8, py::arg("key_prefix") = "");
   k.def("encode_batch", &py_encode_batch, py::arg("records"), py::arg("base_offset") = 0,
         py::arg("base_timestamp") = 0);
   k.def("decode_records", [](py::bytes b, int64_t min_offset, bool check_crc) {
@@ -296,9 +391,10 @@ void bind_host(py::module_& m) {
   py::class_<Broker, std::shared_ptr<Broker>>(k, "Broker")
       .def(py::init([](const std::string& host, int port, int node_id, int default_partitions,
                        bool auto_create, int64_t max_message_bytes, int64_t retention_bytes,
-                       bool check_crcs, bool zero_copy) {
+                       bool check_crcs, bool zero_copy, bool log_append_time) {
              BrokerConfig c;
              c.zero_copy = zero_copy;
+             c.log_append_time = log_append_time;
              c.host = host;
              c.port = port;
              c.node_id = node_id;
@@ -312,7 +408,8 @@ void bind_host(py::module_& m) {
            py::arg("host") = "127.0.0.1", py::arg("port") = 0, py::arg("node_id") = 0,
            py::arg("default_partitions") = 1, py::arg("auto_create_topics") = true,
            py::arg("max_message_bytes") = 64ll << 20, py::arg("retention_bytes") = 4ll << 30,
-           py::arg("check_crcs") = true, py::arg("zero_copy") = false)
+           py::arg("check_crcs") = true, py::arg("zero_copy") = false,
+           py::arg("log_append_time") = false)
       .def("start", &Broker::start)
       .def("stop", [](Broker& b) {
         py::gil_scoped_release nogil;
@@ -365,6 +462,25 @@ void bind_host(py::module_& m) {
         }
         return first;
       })
+      .def("append_cycled", [](Broker& b, const std::string& topic, int partition,
+                               const BatchSet& set, int64_t n_batches, int64_t start) {
+        // append n_batches of `set` by reference, cycling from index `start`; returns
+        // (first offset, records appended)
+        if (set.batches.empty()) throw std::invalid_argument("empty BatchSet");
+        int64_t first = -1, recs = 0;
+        {
+          py::gil_scoped_release nogil;
+          const int64_t m = (int64_t)set.batches.size();
+          for (int64_t i = 0; i < n_batches; ++i) {
+            const size_t k = (size_t)(((start + i) % m + m) % m);
+            const int64_t o = b.append_shared(topic, partition, set.batches[k]);
+            if (i == 0) first = o;
+            recs += set.records[k];
+          }
+        }
+        return py::make_tuple(first, recs);
+      }, py::arg("topic"), py::arg("partition"), py::arg("batches"), py::arg("n_batches"),
+         py::arg("start") = 0)
       .def("log_start", &Broker::log_start)
       .def("log_end", &Broker::log_end)
       .def("committed", &Broker::committed)

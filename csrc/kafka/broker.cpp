@@ -1,5 +1,6 @@
 // Embedded Kafka-protocol broker (see broker.h).
 #include "broker.h"
+#include "gale/thread_name.h"
 
 #include <arpa/inet.h>
 #include <errno.h>
@@ -174,7 +175,10 @@ void Broker::start() {
   getsockname(listen_fd_, reinterpret_cast<sockaddr*>(&a), &len);
   port_ = ntohs(a.sin_port);
   running_ = true;
-  thread_ = std::thread([this] { accept_loop(); });
+  thread_ = std::thread([this] {
+    name_thread("gl-brk-acc");
+    accept_loop();
+  });
 }
 
 void Broker::stop() {
@@ -245,6 +249,23 @@ int64_t Broker::append_locked(PartitionLog& log, std::shared_ptr<const std::stri
   s.next = log.end + bi.last_offset_delta + 1;
   s.max_ts = bi.max_timestamp;
   s.bytes = std::move(batch);
+  if (cfg_.log_append_time) {
+    // the stored bytes may be shared (preloaded by reference): the stamp lives in the segment
+    const uint8_t* b = reinterpret_cast<const uint8_t*>(s.bytes->data());
+    const size_t n = kBatchMaxTsOffset + 8 - kBatchAttrOffset;
+    static_assert(kBatchMaxTsOffset + 8 - kBatchAttrOffset == sizeof(s.hdr), "header window");
+    memcpy(s.hdr, b + kBatchAttrOffset, n);
+    const int16_t attrs = (int16_t)(bi.attributes | kAttrLogAppendTime);
+    const int64_t now = wall_ms();
+    Writer::put_be(reinterpret_cast<char*>(s.hdr), &attrs, 2);
+    Writer::put_be(reinterpret_cast<char*>(s.hdr) + (kBatchMaxTsOffset - kBatchAttrOffset), &now,
+                   8);
+    Reader cr(b + kBatchCrcOffset, 4);
+    s.crc = patch_batch_crc(cr.u32(), b + kBatchAttrOffset, s.hdr, n,
+                            s.bytes->size() - (size_t)(kBatchMaxTsOffset + 8));
+    s.max_ts = now;
+    s.stamped = true;
+  }
   log.bytes += (int64_t)s.bytes->size();
   log.end = s.next;
   log.segs.push_back(std::move(s));
@@ -332,6 +353,10 @@ std::string Broker::read_raw(const std::string& topic, int partition, int64_t of
     const size_t at = out.size();
     out += *s.bytes;
     Writer::put_be(&out[at], &s.base, 8);
+    if (s.stamped) {
+      Writer::put_be(&out[at + kBatchCrcOffset], &s.crc, 4);
+      memcpy(&out[at + kBatchAttrOffset], s.hdr, sizeof(s.hdr));
+    }
   }
   return out;
 }
@@ -360,7 +385,10 @@ void Broker::accept_loop() {
       return;
     }
     conn_fds_.push_back(fd);
-    conn_threads_.emplace_back([this, fd] { serve(fd); });
+    conn_threads_.emplace_back([this, fd] {
+      name_thread("gl-brk-conn");
+      serve(fd);
+    });
     std::lock_guard<std::mutex> lk2(mu_);
     ++stats_.connections;
   }
@@ -839,7 +867,14 @@ bool Broker::try_fetch(Conn& c, bool final_attempt) {
         rb.w.i32((int32_t)pbytes);
         for (const Segment* s : sel) {
           rb.w.i64(s->base);
-          rb.shared(s->bytes, 8, s->bytes->size() - 8);
+          if (s->stamped) {  // batchLength, leaderEpoch, magic | crc | attrs .. maxTimestamp
+            rb.w.raw(s->bytes->data() + kBatchLengthOffset, kBatchCrcOffset - kBatchLengthOffset);
+            rb.w.u32(s->crc);
+            rb.w.raw(s->hdr, sizeof(s->hdr));
+            rb.shared(s->bytes, kBatchMaxTsOffset + 8, s->bytes->size() - (kBatchMaxTsOffset + 8));
+          } else {
+            rb.shared(s->bytes, 8, s->bytes->size() - 8);
+          }
         }
         data_bytes += pbytes;
       }

@@ -47,6 +47,11 @@ struct BrokerConfig {
   // Measured on loopback (bench.py --broker-zero-copy): no gain, the splice page pinning costs
   // about what the copy did; off by default.
   bool zero_copy = false;
+  // log.message.timestamp.type=LogAppendTime: every appended batch is stamped with the broker's
+  // wall clock (attributes timestamp-type bit + maxTimestamp, CRC patched in O(log n) without
+  // re-reading the batch); consumers then see the append time as each record's timestamp, which
+  // makes record-timestamp end-to-end latency exact even for pre-encoded (bench) batches.
+  bool log_append_time = false;
   std::string cluster_id = "gale-embedded";
 };
 
@@ -100,6 +105,10 @@ class Broker {
     int64_t next;  // base + lastOffsetDelta + 1
     int64_t max_ts;
     std::shared_ptr<const std::string> bytes;
+    // LogAppendTime: bytes [kBatchAttrOffset, kBatchMaxTsOffset + 8) and the CRC as sent
+    bool stamped = false;
+    uint32_t crc = 0;
+    uint8_t hdr[22] = {};
   };
   struct PartitionLog {
     std::vector<Segment> segs;

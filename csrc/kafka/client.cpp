@@ -1,5 +1,6 @@
 // Kafka-protocol client: connections, metadata, producer, consumer (see client.h).
 #include "client.h"
+#include "gale/thread_name.h"
 
 #include <arpa/inet.h>
 #include <errno.h>
@@ -327,7 +328,10 @@ Producer::Producer(ProducerConfig cfg)
     : cfg_(std::move(cfg)), cluster_(cfg_), meta_(cfg_) {
   if (cfg_.acks != 0 && cfg_.acks != 1 && cfg_.acks != -1)
     throw std::invalid_argument("acks must be 0, 1 or -1");
-  thread_ = std::thread([this] { run(); });
+  thread_ = std::thread([this] {
+    name_thread("gl-sink");
+    run();
+  });
 }
 
 Producer::~Producer() {

@@ -10,58 +10,57 @@ namespace kafka {
 namespace {
 
 // CRC32C with three independent crc32q streams (the instruction has 3-cycle latency and 1-cycle
-// throughput, so one serial chain runs at a third of the unit's rate). The partial CRCs are
-// combined with precomputed "append N zero bytes" operators in GF(2) (Mark Adler's crc32c
-// method): crc(A|B) = shift(crc(A), |B|) ^ crc(B).
-constexpr uint32_t kPoly = 0x82f63b78u;
+// throughput, so one serial chain runs at a third of the unit's rate). Partial CRCs are joined
+// with crc(A|B) = crc(A) * x^(8|B|) mod P  ^  crc(B) (raw, un-inverted states): the CRC register
+// is a polynomial over GF(2) and appending k zero bits multiplies it by x^k modulo P.
+constexpr uint32_t kPoly = 0x82f63b78u;  // CRC-32C polynomial, reflected
 constexpr size_t kLong = 8192, kShort = 256;
 
-uint32_t gf2_times(const uint32_t* mat, uint32_t vec) {
-  uint32_t sum = 0;
-  while (vec) {
-    if (vec & 1) sum ^= *mat;
-    vec >>= 1;
-    ++mat;
+// a * b mod P in the reflected domain (bit 31 = coefficient of x^0): sum of b * x^i over the set
+// bits i of a, b advancing by one x per step (one zero bit through the CRC register)
+uint32_t poly_mulmod(uint32_t a, uint32_t b) {
+  uint32_t r = 0;
+  for (int i = 0; i < 32 && a; ++i) {
+    const uint32_t bit = 0x80000000u >> i;
+    if (a & bit) {
+      r ^= b;
+      a &= ~bit;
+    }
+    b = (b >> 1) ^ (kPoly & (0u - (b & 1u)));
   }
-  return sum;
+  return r;
 }
 
-void gf2_square(uint32_t* square, const uint32_t* mat) {
-  for (int n = 0; n < 32; ++n) square[n] = gf2_times(mat, mat[n]);
-}
-
-// operator for appending len (a power of two) zero bytes
-void zeros_op(uint32_t* even, size_t len) {
-  uint32_t odd[32];
-  odd[0] = kPoly;
-  uint32_t row = 1;
-  for (int n = 1; n < 32; ++n) {
-    odd[n] = row;
-    row <<= 1;
+// x^(8 * 2^k) mod P for k = 0..63 (k = 0: one byte), by repeated squaring
+struct BytePowers {
+  uint32_t p[64];
+  BytePowers() {
+    p[0] = 0x80000000u >> 8;  // x^8
+    for (int k = 1; k < 64; ++k) p[k] = poly_mulmod(p[k - 1], p[k - 1]);
   }
-  gf2_square(even, odd);  // 2 zero bits
-  gf2_square(odd, even);  // 4 zero bits
-  do {
-    gf2_square(even, odd);
-    len >>= 1;
-    if (len == 0) return;
-    gf2_square(odd, even);
-    len >>= 1;
-  } while (len);
-  for (int n = 0; n < 32; ++n) even[n] = odd[n];
+};
+const BytePowers& byte_powers() {
+  static const BytePowers t;
+  return t;
 }
 
+// x^(8 n) mod P
+uint32_t x8n(uint64_t n) {
+  const BytePowers& bp = byte_powers();
+  uint32_t r = 0x80000000u;  // x^0
+  for (int k = 0; n; ++k, n >>= 1)
+    if (n & 1) r = poly_mulmod(r, bp.p[k]);
+  return r;
+}
+
+// Fixed-length shift by table lookup: t[j][v] = (v << 8j) * x^(8 len) mod P (linear in the
+// state, so four byte lookups cover a 32-bit register)
 struct ShiftTable {
   uint32_t t[4][256];
   explicit ShiftTable(size_t len) {
-    uint32_t op[32];
-    zeros_op(op, len);
-    for (uint32_t n = 0; n < 256; ++n) {
-      t[0][n] = gf2_times(op, n);
-      t[1][n] = gf2_times(op, n << 8);
-      t[2][n] = gf2_times(op, n << 16);
-      t[3][n] = gf2_times(op, n << 24);
-    }
+    const uint32_t op = x8n(len);
+    for (uint32_t v = 0; v < 256; ++v)
+      for (int j = 0; j < 4; ++j) t[j][v] = poly_mulmod(v << (8 * j), op);
   }
   uint32_t shift(uint32_t crc) const {
     return t[0][crc & 0xff] ^ t[1][(crc >> 8) & 0xff] ^ t[2][(crc >> 16) & 0xff] ^ t[3][crc >> 24];
@@ -191,6 +190,27 @@ uint32_t crc32c(const uint8_t* p, size_t n, uint32_t crc) {
   }
   while (n--) c = _mm_crc32_u8((uint32_t)c, *p++);
   return ~(uint32_t)c;
+}
+
+uint32_t crc32c_shift(uint32_t raw, uint64_t nbytes) { return poly_mulmod(raw, x8n(nbytes)); }
+
+uint32_t crc32c_combine(uint32_t crc_a, uint32_t crc_b, uint64_t len_b) {
+  // standard (inverted) CRCs: the inversions of A's final state and B's initial state cancel
+  return crc32c_shift(crc_a, len_b) ^ crc_b;
+}
+
+uint32_t crc32c_raw(const uint8_t* p, size_t n, uint32_t raw) {
+  return ~crc32c(p, n, ~raw);
+}
+
+uint32_t patch_batch_crc(uint32_t crc, const uint8_t* old_bytes, const uint8_t* new_bytes,
+                         size_t n, uint64_t bytes_after) {
+  // equal-length messages: crc(A) ^ crc(A') = raw(A ^ A'), and the difference is zero outside
+  // the patched window, so only that window and a shift over the tail are computed
+  uint8_t d[64];
+  if (n > sizeof(d)) throw ProtocolError("patch window too large");
+  for (size_t i = 0; i < n; ++i) d[i] = old_bytes[i] ^ new_bytes[i];
+  return crc ^ crc32c_shift(crc32c_raw(d, n, 0), bytes_after);
 }
 
 namespace {
@@ -324,7 +344,9 @@ size_t decode_records(const uint8_t* base, size_t off, size_t len, int64_t min_o
         const int32_t od = r.varint();
         RecordRef rr;
         rr.offset = b.base_offset + od;
-        rr.timestamp = b.base_timestamp + tsd;
+        // LogAppendTime batches (attribute bit 3): every record carries the broker's append time
+        rr.timestamp = (b.attributes & kAttrLogAppendTime) ? b.max_timestamp
+                                                          : b.base_timestamp + tsd;
         rr.key_len = r.varint();
         rr.key_off = (int64_t)(rbase + r.pos());
         if (rr.key_len > 0) r.skip((size_t)rr.key_len);

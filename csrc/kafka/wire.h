@@ -24,8 +24,18 @@ struct ProtocolError : std::runtime_error {
   using std::runtime_error::runtime_error;
 };
 
-// CRC32C (Castagnoli) with the SSE4.2 crc32 instruction.
+// CRC32C (Castagnoli) with the SSE4.2 crc32 instruction (VPCLMULQDQ folding when available).
 uint32_t crc32c(const uint8_t* p, size_t n, uint32_t crc = 0);
+// Raw (un-inverted) CRC register arithmetic: crc32c_raw continues a raw state over p[0..n);
+// crc32c_shift appends nbytes zero bytes to a raw state (multiplication by x^(8 nbytes) mod P).
+uint32_t crc32c_raw(const uint8_t* p, size_t n, uint32_t raw);
+uint32_t crc32c_shift(uint32_t raw, uint64_t nbytes);
+// crc32c(A ++ B) from crc32c(A), crc32c(B) and |B|.
+uint32_t crc32c_combine(uint32_t crc_a, uint32_t crc_b, uint64_t len_b);
+// CRC of a message after bytes [k, k+n) changed from old_bytes to new_bytes, with bytes_after
+// bytes following the window (n <= 64): O(log length), the message itself is not re-read.
+uint32_t patch_batch_crc(uint32_t crc, const uint8_t* old_bytes, const uint8_t* new_bytes,
+                         size_t n, uint64_t bytes_after);
 
 class Writer {
  public:
@@ -158,6 +168,8 @@ constexpr int kBatchHeaderBytes = 61;      // baseOffset .. recordCount
 constexpr int kBatchCrcOffset = 17;        // crc field
 constexpr int kBatchAttrOffset = 21;       // CRC covers attributes .. end
 constexpr int kBatchLengthOffset = 8;
+constexpr int kBatchMaxTsOffset = 35;      // maxTimestamp
+constexpr int16_t kAttrLogAppendTime = 0x08;  // timestamp type bit of the batch attributes
 
 struct Header {
   std::string key;

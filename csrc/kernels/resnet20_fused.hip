@@ -478,24 +478,23 @@ hipError_t resnet20_fused_forward(const ResNet20Params& p, int batch, const floa
       if (p.ws[i] == nullptr || !(p.s_in[i] > 0.f) || !(p.s_out[i] > 0.f))
         return hipErrorInvalidValue;
   }
-  static int cus = 0;
-  if (cus == 0) {
+  // (C++11 magic statics: initialised once, thread-safe, as replica workers launch concurrently)
+  static const int cus = [] {
     int dev = 0, n = 256;
     if (hipGetDevice(&dev) == hipSuccess)
       (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
-    cus = n > 0 ? n : 256;
-  }
+    return n > 0 ? n : 256;
+  }();
   // resident workgroups per CU: 2 of 4 waves (bf16: LDS bound; fp8: register bound — its 39 KB
   // of LDS would allow 4, but the hoisted A fragments need more than 128 VGPRs per lane), or 1 of
   // 8 waves. bf16 with no more images than CUs: the 8-wave form (each image gets twice the
   // waves, weights prefetched into LDS; measured 62.3 -> 58.0 us at batch 1,
   // profiles/r1_resnet20_waves_ab.txt). fp8 stays on 4 waves (its 8-wave form measured slower).
   // GALE_R20_WAVES=4|8 pins the choice (A/B benches).
-  static int forced = -1;
-  if (forced < 0) {
+  static const int forced = [] {
     const char* e = getenv("GALE_R20_WAVES");
-    forced = e ? atoi(e) : 0;
-  }
+    return e ? atoi(e) : 0;
+  }();
   const int nw = forced == 4 || forced == 8 ? forced : (!f8 && batch <= cus ? 8 : 4);
   const int grid_cap = nw == 8 ? cus : 2 * cus;
   const int grid = batch < grid_cap ? batch : grid_cap;

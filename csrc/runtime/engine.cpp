@@ -1,5 +1,6 @@
 // The gale serving engine (see engine.h).
 #include "engine.h"
+#include "gale/thread_name.h"
 
 #include <hip/hip_runtime.h>
 #include <stdio.h>
@@ -139,6 +140,10 @@ Engine::Engine(EngineConfig cfg) : cfg_(std::move(cfg)), rng_(cfg_.seed) {
     else throw std::invalid_argument("engine: unknown fault kind " + kind);
   }
   batcher_ = std::make_unique<Batcher>((size_t)std::max(1, cfg_.queue_depth));
+  eff_batch_ = cfg_.max_batch;
+  eff_wait_ns_ = (int64_t)cfg_.max_wait_us * 1000;
+  if (cfg_.slo_p99_ms > 0)  // start with a quarter of the budget for batch formation
+    eff_wait_ns_ = std::min<int64_t>(eff_wait_ns_, (int64_t)(cfg_.slo_p99_ms * 0.25e6));
 }
 
 Engine::~Engine() {
@@ -206,11 +211,24 @@ void Engine::start() {
   sources_active_ = ns;
   dec_closed_ = false;
   for (int i = 0; i < cfg_.decode_threads; ++i)
-    decoders_.emplace_back([this, i] { decode_loop(i); });
-  for (auto& rs : replicas_) workers_.emplace_back([this, rs] { worker_loop(rs.get()); });
+    decoders_.emplace_back([this, i] {
+      name_thread("gl-dec", i);
+      decode_loop(i);
+    });
+  for (auto& rs : replicas_)
+    workers_.emplace_back([this, rs] {
+      name_thread("gl-rep", rs->index);
+      worker_loop(rs.get());
+    });
   for (int i = 0; i < ns; ++i)
-    sources_.emplace_back([this, i, p = split[(size_t)i]] { source_loop(i, p); });
-  watchdog_ = std::thread([this] { watchdog_loop(); });
+    sources_.emplace_back([this, i, p = split[(size_t)i]] {
+      name_thread("gl-src", i);
+      source_loop(i, p);
+    });
+  watchdog_ = std::thread([this] {
+    name_thread("gl-watchdog");
+    watchdog_loop();
+  });
 }
 
 void Engine::stop() {
@@ -526,7 +544,6 @@ void Engine::worker_loop(ReplicaSlot* rs) {
 
 void Engine::serve(ReplicaSlot* rs) {
   Replica& rep = *rs->rep;
-  const int64_t max_wait_ns = (int64_t)cfg_.max_wait_us * 1000;
   const size_t depth = (size_t)std::max(1, rep.depth());
   std::deque<std::shared_ptr<Batch>> mine;
   auto fail = [&](const char* what, const std::string& msg) {
@@ -557,7 +574,9 @@ void Engine::serve(ReplicaSlot* rs) {
       bool open;
       {
         trace::Range tr("gale:batch");
-        open = batcher_->take(cfg_.max_batch, max_wait_ns, !mine.empty(), b->recs, images);
+        open = batcher_->take(eff_batch_.load(std::memory_order_relaxed),
+                              eff_wait_ns_.load(std::memory_order_relaxed), !mine.empty(),
+                              b->recs, images);
       }
       ns_take_ += mono_ns() - t_take0;
       if (!open) {
@@ -615,9 +634,40 @@ void Engine::serve(ReplicaSlot* rs) {
   }
 }
 
+// One step of the latency-SLO controller (every 100 ms while slo_p99_ms > 0).
+void Engine::slo_step() {
+  const int64_t n = h_slo_win_us_.count();
+  if (n < 16) return;  // too few completions in the window to estimate a p99
+  const double p99_ms = h_slo_win_us_.quantile(0.99) * 1e-3;
+  h_slo_win_us_.reset();
+  const int maxb = cfg_.max_batch, minb = std::max(1, cfg_.max_batch / 32);
+  const int64_t max_wait = (int64_t)cfg_.max_wait_us * 1000, min_wait = 20000;
+  int b = eff_batch_.load();
+  int64_t w = eff_wait_ns_.load();
+  const bool backlog = (int64_t)batcher_->size() > (int64_t)b * (int64_t)replicas_.size();
+  if (p99_ms > cfg_.slo_p99_ms) {
+    if (backlog) {
+      b = std::min(maxb, b + std::max(1, maxb / 8));  // overload: capacity first
+    } else {
+      b = std::max(minb, b * 3 / 4);
+      w = std::max(min_wait, w * 7 / 10);
+    }
+  } else if (p99_ms < 0.8 * cfg_.slo_p99_ms) {
+    b = std::min(maxb, b + std::max(1, maxb / 16));
+    w = std::min(max_wait, w * 5 / 4 + 20000);
+  } else {
+    return;
+  }
+  eff_batch_ = b;
+  eff_wait_ns_ = w;
+  ++slo_adjustments_;
+}
+
 void Engine::watchdog_loop() {
+  int tick = 0;
   while (running_ && !workers_done_) {
     std::this_thread::sleep_for(std::chrono::milliseconds(50));
+    if (cfg_.slo_p99_ms > 0 && (++tick & 1) == 0) slo_step();
     const int64_t now = mono_ns();
     for (auto& rs : replicas_) {
       std::vector<InRecord> back;
@@ -681,6 +731,7 @@ void Engine::complete_record(const InRecord& r, bool ok) {
     ++records_out_;
     images_out_ += r.images;
     h_engine_e2e_us_.add((now - r.t_fetch_ns) / 1000);
+    if (cfg_.slo_p99_ms > 0) h_slo_win_us_.add((now - r.t_fetch_ns) / 1000);
     if (r.timestamp_ms > 0) h_record_e2e_ms_.add(wall_ms_now() - r.timestamp_ms);
   } else {
     ++produce_failures_;
@@ -804,6 +855,9 @@ std::map<std::string, double> Engine::stats() const {
   int alive = 0;
   for (auto& r : replicas_) alive += r->alive ? 1 : 0;
   s["replicas_alive"] = alive;
+  s["eff_max_batch"] = (double)eff_batch_;
+  s["eff_max_wait_us"] = (double)eff_wait_ns_ / 1000.0;
+  s["slo_adjustments"] = (double)slo_adjustments_;
   s["thread_s_poll"] = ns_poll_ * 1e-9;
   s["thread_s_decode"] = ns_decode_ * 1e-9;
   s["thread_s_take"] = ns_take_ * 1e-9;

@@ -72,6 +72,12 @@ struct EngineConfig {
   // batching (P7)
   int max_batch = 256;             // images per micro-batch (<= every replica's max)
   int max_wait_us = 2000;          // latency bound on batch formation
+  // latency-SLO mode (BASELINE config 5): > 0 = a controller adapts the effective batch size and
+  // wait bound every 100 ms from the window's end-to-end p99 (AIMD, Clipper-style adaptive
+  // batching): back off while p99 exceeds the target, grow while well under it; when p99 is
+  // over the target because records queue up (offered load above capacity) it grows the batch
+  // instead, since only larger batches add capacity
+  double slo_p99_ms = 0;
   int queue_depth = 8192;          // records buffered between source and replicas
   // robustness
   int watchdog_ms = 30000;         // a batch longer than this on a replica marks it dead
@@ -148,6 +154,7 @@ class Engine {
   void worker_loop(ReplicaSlot* rs);
   void serve(ReplicaSlot* rs);  // one replica life: returns once it dies or the engine drains
   void watchdog_loop();
+  void slo_step();
   void finish_batch(ReplicaSlot* rs, Batch& b);
   void emit(InRecord& r, std::string value, bool null_value, kafka::Producer* prod);
   void emit_error(InRecord& r, int status, kafka::Producer* prod);
@@ -194,6 +201,10 @@ class Engine {
   std::atomic<int64_t> requeued_{0}, replica_failures_{0}, replica_restarts_{0}, commits_{0};
   std::atomic<int64_t> err_by_status_[8] = {};
   Histogram h_queue_us_, h_device_us_, h_engine_e2e_us_, h_record_e2e_ms_, h_batch_images_;
+  Histogram h_slo_win_us_;  // e2e latency of the SLO controller's current window
+  std::atomic<int> eff_batch_{0};
+  std::atomic<int64_t> eff_wait_ns_{0};
+  std::atomic<int64_t> slo_adjustments_{0};
   // thread time per pipeline stage (summed over threads): where the host spends its cycles
   std::atomic<int64_t> ns_poll_{0}, ns_decode_{0}, ns_take_{0}, ns_submit_{0}, ns_wait_{0},
       ns_finish_{0};

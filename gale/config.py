@@ -69,6 +69,7 @@ class GaleConfig:
     seed: int = 0
     max_batch: int = 256
     max_wait_us: int = 2000
+    slo_p99_ms: float = 0.0            # latency-SLO mode (config 5): adapt batch/wait to a p99
     queue_depth: int = 8192
     use_graph: bool = True
     fold_bn: bool = True               # False: standalone BatchNorm kernels (debug/parity plan)
@@ -99,6 +100,8 @@ class GaleConfig:
         for k in ("source_parallelism", "sink_parallelism", "max_batch", "queue_depth"):
             if getattr(self, k) <= 0:
                 raise ValueError(f"{k} must be positive")
+        if self.slo_p99_ms < 0:
+            raise ValueError("slo_p99_ms must be >= 0")
         if self.replicas < 0 or self.gpus < 0:
             raise ValueError("replicas/gpus must be >= 0")
         if not self.topology_name:
@@ -123,7 +126,8 @@ class GaleConfig:
             acks=self.acks, sink_mode=self.sink_mode, linger_ms=self.linger_ms,
             value_format=self.value_format, type_id_header=self.type_id_header,
             on_error=self.on_error, H=H, W=W, C=C, classes=classes, max_batch=self.max_batch,
-            max_wait_us=self.max_wait_us, queue_depth=self.queue_depth,
+            max_wait_us=self.max_wait_us, slo_p99_ms=self.slo_p99_ms,
+            queue_depth=self.queue_depth,
             watchdog_ms=self.watchdog_ms, max_restarts=self.max_restarts,
             restart_backoff_ms=self.restart_backoff_ms, fault=self.fault, seed=self.seed,
             trace=self.trace)

@@ -129,20 +129,43 @@ def batchnorm(x: torch.Tensor, scale: Optional[torch.Tensor], shift: Optional[to
     (residual read at (2h, 2w), zero above its channel count). ``out`` may alias ``x``."""
     _check(x, torch.bfloat16, "x")
     B, H, W, C = x.shape
+    if C % 8:
+        raise ValueError("batchnorm: channel count must be a multiple of 8")
     sp = hp = 0
     if scale is not None:
         _check(scale, torch.float32, "scale")
         _check(shift, torch.float32, "shift")
+        if scale.device != x.device or shift.device != x.device:
+            raise ValueError("batchnorm: scale/shift must be on x's device")
         if scale.numel() < C or shift.numel() < C:
             raise ValueError("batchnorm: scale/shift shorter than the channel count")
         sp, hp = scale.data_ptr(), shift.data_ptr()
     rp, rh, rw, rc, rs = 0, 0, 0, 0, 1
     if residual is not None:
         _check(residual, torch.bfloat16, "residual")
-        _, rh, rw, rc = residual.shape
+        if residual.device != x.device:
+            raise ValueError("batchnorm: residual must be on x's device")
+        rb, rh, rw, rc = residual.shape
+        if res_mode not in ("identity", "pad"):
+            raise ValueError(f"batchnorm: unknown res_mode {res_mode!r}")
         rs = 2 if res_mode == "pad" else 1
+        if rb != B:
+            raise ValueError(f"batchnorm: residual batch {rb} != {B}")
+        if res_mode == "identity" and (rh, rw, rc) != (H, W, C):
+            raise ValueError(f"batchnorm: identity residual {tuple(residual.shape)} != "
+                             f"{tuple(x.shape)}")
+        if res_mode == "pad" and (rh < 2 * (H - 1) + 1 or rw < 2 * (W - 1) + 1 or rc > C):
+            raise ValueError(f"batchnorm: pad residual {tuple(residual.shape)} does not cover "
+                             f"{tuple(x.shape)} at stride 2")
         rp = residual.data_ptr()
-    y = torch.empty_like(x) if out is None else out
+    if out is None:
+        y = torch.empty_like(x)
+    else:
+        _check(out, torch.bfloat16, "out")
+        if out.shape != x.shape or out.device != x.device:
+            raise ValueError(f"batchnorm: out {tuple(out.shape)} on {out.device} must match x "
+                             f"{tuple(x.shape)} on {x.device}")
+        y = out
     native().bn_act(B, H * W, W, C, x.data_ptr(), sp, hp, rp, rh, rw, rc, rs, int(relu),
                     y.data_ptr(), _stream())
     return y

@@ -74,6 +74,36 @@ def pin_to_gpu_numa(device: int, cpus_per_rank: int = 0) -> set:
     return cpus
 
 
+THREAD_GROUPS = (("gl-brk", "broker"), ("gl-src", "source"), ("gl-dec", "decode"),
+                 ("gl-rep", "replica"), ("gl-sink", "sink"), ("gl-watchdog", "watchdog"))
+
+
+def thread_cpu_seconds() -> dict:
+    """CPU seconds (user + system) of this process's live threads, summed per pipeline stage.
+
+    The native threads name themselves (csrc/include/gale/thread_name.h: gl-src<i>, gl-dec<i>,
+    gl-rep<i>, gl-sink, gl-brk-*); anything else (Python, HIP runtime, RCCL) is "other". Threads
+    that exited between two snapshots drop out, so take deltas over a window in which the
+    pipeline's threads stay alive."""
+    tick = os.sysconf("SC_CLK_TCK")
+    out = {g: 0.0 for _, g in THREAD_GROUPS}
+    out["other"] = 0.0
+    base = "/proc/self/task"
+    for tid in os.listdir(base):
+        try:
+            with open(f"{base}/{tid}/stat") as f:
+                st = f.read()
+        except OSError:
+            continue
+        lp, rp = st.index("("), st.rindex(")")
+        name = st[lp + 1:rp]
+        rest = st[rp + 2:].split()
+        sec = (int(rest[11]) + int(rest[12])) / tick  # fields 14, 15: utime, stime
+        group = next((g for pre, g in THREAD_GROUPS if name.startswith(pre)), "other")
+        out[group] += sec
+    return out
+
+
 def free_port(host: str = "127.0.0.1") -> int:
     """An ephemeral TCP port that was free a moment ago (embedded brokers, rendezvous)."""
     s = socket.socket()

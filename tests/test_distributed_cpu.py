@@ -55,7 +55,7 @@ def test_bench_stub_torchrun_world2():
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "2",
            "--stub", "--steps", "4", "--warmup", "1", "--batch", "32", "--distinct", "64",
-           "--replicas-per-gpu", "4",
+           "--replicas-per-gpu", "4", "--step-images", "512", "--min-warmup-s", "0.2",
            "--timeout", "120"]
     out = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=300,
                          env=dict(os.environ, OMP_NUM_THREADS="1"))
@@ -66,12 +66,16 @@ def test_bench_stub_torchrun_world2():
     assert r["n_gpus"] == 2 and r["steps"] == 4 and r["value"] > 0
     # a step = one 32-image micro-batch per replica (4 per GPU by default), on both ranks
     assert r["config"]["parallelism"] == "dp2" and r["config"]["global_batch"] == 32 * 4 * 2
+    # one input topic shared by the two ranks' broker cluster, one partition per replica
+    assert r["config"]["partitions"] == 8
+    assert r["step_rate_spread"]["min"] > 0 and r["timed_s"] > 0
 
 
 def test_bench_stub_rate_mode():
     """bench.py --rate: the open-loop feeder offers a fixed image rate; the engine keeps up, so
     the achieved rate matches the offer and the load is reported in the JSON line."""
     cmd = [sys.executable, "bench.py", "--stub", "--stub-null", "--steps", "20", "--warmup", "2",
+           "--step-images", "128", "--min-warmup-s", "0.2", "--distinct", "256",
            "--batch", "16", "--replicas-per-gpu", "2", "--rate", "3000", "--max-wait-us", "500",
            "--timeout", "120"]
     out = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=300,
@@ -88,6 +92,7 @@ def test_scaling_driver_stub_1_2():
     gloo stub ranks), one JSON line per N and a summary with the weak-scaling efficiency."""
     cmd = [sys.executable, "tools/scaling.py", "--gpus", "1,2", "--stub", "--steps", "4",
            "--warmup", "1", "--timeout", "240", "--", "--batch", "32", "--distinct", "64",
+           "--step-images", "512", "--min-warmup-s", "0.2",
            "--replicas-per-gpu", "2", "--stub-null", "--timeout", "120"]
     out = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=600,
                          env=dict(os.environ, OMP_NUM_THREADS="1"))

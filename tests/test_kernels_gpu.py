@@ -356,3 +356,21 @@ def test_relu_standalone_in_place():
     want = x.clamp(min=0).cpu()
     y = ops.relu(x, out=x)
     assert y.data_ptr() == x.data_ptr() and torch.equal(x.cpu(), want)
+
+
+def test_batchnorm_rejects_mismatched_operands():
+    """Shape/device/dtype errors are Python errors, never out-of-bounds device accesses."""
+    x = torch.randn(2, 4, 4, 16).bfloat16().to(DEV)
+    sc, sh = torch.ones(16, device=DEV), torch.zeros(16, device=DEV)
+    with pytest.raises(ValueError):  # short out
+        ops.batchnorm(x, sc, sh, out=torch.empty(1, 4, 4, 16, dtype=torch.bfloat16, device=DEV))
+    with pytest.raises(ValueError):  # residual batch
+        ops.batchnorm(x, sc, sh, residual=torch.zeros(1, 4, 4, 16, dtype=torch.bfloat16,
+                                                      device=DEV))
+    with pytest.raises(ValueError):  # identity residual of another shape
+        ops.batchnorm(x, sc, sh, residual=torch.zeros(2, 4, 4, 8, dtype=torch.bfloat16,
+                                                      device=DEV))
+    with pytest.raises(RuntimeError):  # scale on the host (no CPU fallback)
+        ops.batchnorm(x, torch.ones(16), torch.zeros(16))
+    with pytest.raises(TypeError):  # out dtype
+        ops.batchnorm(x, sc, sh, out=torch.empty(2, 4, 4, 16, device=DEV))

@@ -72,8 +72,12 @@ def main(argv=None) -> int:
     counts = [int(x) for x in a.gpus.split(",") if x.strip()]
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", MASTER_ADDR="127.0.0.1")
     results = {}
+    pinned: list = []
     for n in counts:
-        cmd = bench_cmd(n, a.steps, a.warmup, extra, a.stub)
+        # weak scaling compares equal per-GPU work: every N > first runs with the per-GPU
+        # configuration the first run chose for itself (bench.py sizes replicas per GPU from the
+        # rank's CPU share, which shrinks as more ranks share the node's CPUs)
+        cmd = bench_cmd(n, a.steps, a.warmup, extra + pinned, a.stub)
         try:
             p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True,
                                timeout=a.timeout)
@@ -86,6 +90,13 @@ def main(argv=None) -> int:
             print(json.dumps({"n_gpus": n, "error": f"rc={p.returncode}", "tail": tail}))
             break
         results[n] = r
+        if not pinned:
+            cfg = r.get("config", {})
+            for flag, key in (("--replicas-per-gpu", "replicas_per_gpu"),
+                              ("--batch", "max_batch"),
+                              ("--step-images", "step_images_per_gpu")):
+                if key in cfg and flag not in extra:
+                    pinned += [flag, str(cfg[key])]
         print(json.dumps(r), flush=True)
         if a.out:
             with open(a.out, "a") as f:
@@ -94,7 +105,10 @@ def main(argv=None) -> int:
     summary = {"scaling": {str(n): {"images_per_s": r["value"],
                                     "p50_ms": r.get("p50_latency_ms"),
                                     "p99_ms": r.get("p99_latency_ms"),
-                                    "efficiency": eff.get(n)}
+                                    "efficiency": eff.get(n),
+                                    "replicas_per_gpu": r["config"].get("replicas_per_gpu"),
+                                    "global_batch": r["config"].get("global_batch"),
+                                    "cpu_cores_busy_rank0": r.get("cpu_cores_busy_rank0")}
                            for n, r in sorted(results.items())}}
     print(json.dumps(summary), flush=True)
     return 0 if len(results) == len(counts) else 1
