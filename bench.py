@@ -78,6 +78,9 @@ def parse_args(argv=None):
     ap.add_argument("--stub", action="store_true", help="CPU stub replicas (no GPU)")
     ap.add_argument("--stub-null", action="store_true",
                     help="stub replicas skip parsing (measures the host Kafka/codec path only)")
+    ap.add_argument("--gpu-ingest", action=argparse.BooleanOptionalAction, default=True,
+                    help="CRC32C + image counting of fetch buffers on the GPU (host reads only "
+                         "Kafka framing)")
     ap.add_argument("--check-crcs", action=argparse.BooleanOptionalAction, default=True,
                     help="consumer CRC32C verification (Kafka check.crcs; diagnosis only)")
     ap.add_argument("--rate", type=float, default=0.0,
@@ -91,6 +94,8 @@ def parse_args(argv=None):
                     help="pin the host pipeline's threads to the GPU's NUMA node")
     ap.add_argument("--cpus-per-rank", type=int, default=0,
                     help="with --numa-pin: only this rank's slice of the node's CPUs (0 = all)")
+    ap.add_argument("--gpu-wait-poll-us", type=int, default=20,
+                    help="replica workers sleep-poll batch completion every N us (0 = spin)")
     ap.add_argument("--encode-threads", type=int, default=0,
                     help="threads for encoding the synthetic records (0 = host CPU share)")
     ap.add_argument("--timeout", type=float, default=600.0)
@@ -252,6 +257,7 @@ def main(argv=None) -> int:
                      source_parallelism=a.source_parallelism or len(my_parts),
                      sink_parallelism=a.sink_parallelism, replicas=a.replicas_per_gpu,
                      decode_threads=a.decode_threads, slo_p99_ms=a.slo_p99_ms,
+                     gpu_wait_poll_us=a.gpu_wait_poll_us, gpu_ingest=a.gpu_ingest,
                      stub=a.stub, stub_null=a.stub_null, commit_interval_ms=500,
                      check_crcs=a.check_crcs)
     devices = [local_rank] if use_gpu else None

@@ -3,6 +3,7 @@
 #include <pybind11/stl.h>
 
 #include "../runtime/engine.h"
+#include "../runtime/gpu_ingest.h"
 #include "gale/executor.h"
 
 namespace py = pybind11;
@@ -41,6 +42,7 @@ EngineConfig config_from_dict(const py::dict& d) {
   opt(d, "value_format", c.value_format);
   opt(d, "type_id_header", c.type_id_header);
   opt(d, "on_error", c.on_error);
+  opt(d, "output_key", c.output_key);
   opt(d, "H", c.H);
   opt(d, "W", c.W);
   opt(d, "C", c.C);
@@ -72,12 +74,17 @@ void bind_engine(py::module_& m) {
            },
            py::arg("max_images") = 256, py::arg("delay_us") = 0, py::arg("compute") = true)
       .def("add_gpu_replica",
-           [](Engine& e, std::shared_ptr<Executor> exec, bool use_graph) {
+           [](Engine& e, std::shared_ptr<Executor> exec, bool use_graph, int wait_poll_us) {
              const EngineConfig& c = e.config();
              e.add_replica(std::make_shared<GpuReplica>(std::move(exec), c.H, c.W, c.C,
-                                                        c.classes, use_graph));
+                                                        c.classes, use_graph, wait_poll_us));
            },
-           py::arg("executor"), py::arg("use_graph") = true)
+           py::arg("executor"), py::arg("use_graph") = true, py::arg("wait_poll_us") = 0)
+      .def("enable_gpu_ingest",
+           [](Engine& e, int device, int lanes, int poll_us) {
+             e.set_ingest(std::make_shared<GpuIngest>(device, lanes, poll_us));
+           },
+           py::arg("device"), py::arg("lanes") = 2, py::arg("poll_us") = 20)
       .def("start",
            [](Engine& e) {
              py::gil_scoped_release nogil;

@@ -335,6 +335,12 @@ void bind_host(py::module_& m) {
     const std::string_view s = view(b);
     return crc32c(reinterpret_cast<const uint8_t*>(s.data()), s.size());
   });
+  k.def("crc32c_device_tables", [] {
+    std::vector<uint32_t> t(kCrcDeviceTableWords);
+    crc32c_device_tables(t.data());
+    return t;
+  });
+  k.def("crc32c_shift", &crc32c_shift, py::arg("raw"), py::arg("nbytes"));
   k.def("crc32c_combine", &crc32c_combine, py::arg("crc_a"), py::arg("crc_b"), py::arg("len_b"));
   k.def("murmur2", [](py::bytes b) {
     const std::string_view s = view(b);

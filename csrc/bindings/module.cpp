@@ -162,6 +162,28 @@ PYBIND11_MODULE(_C, m) {
               "json_parse_instances");
         });
   m.def("json_tile_count", &gale::json_tile_count);
+  m.def("crc32c_chunks",
+        [](uintptr_t bytes, uintptr_t chunks, int n, uintptr_t tables, uintptr_t out,
+           uintptr_t stream) {
+          gale::check_hip(gale::crc32c_chunks(reinterpret_cast<const uint8_t*>(bytes),
+                                              reinterpret_cast<const gale::CrcChunk*>(chunks), n,
+                                              reinterpret_cast<const uint32_t*>(tables),
+                                              reinterpret_cast<uint32_t*>(out),
+                                              reinterpret_cast<hipStream_t>(stream)),
+                          "crc32c_chunks");
+        });
+  m.def("json_count_records",
+        [](int nrec, int ntiles, uintptr_t recs, uintptr_t tile_rec, uintptr_t bytes,
+           uintptr_t counts, uintptr_t rec_tokens, uintptr_t stream) {
+          gale::check_hip(
+              gale::json_count_records(nrec, ntiles, reinterpret_cast<gale::JsonRecord*>(recs),
+                                       reinterpret_cast<const int*>(tile_rec),
+                                       reinterpret_cast<const uint8_t*>(bytes),
+                                       reinterpret_cast<int*>(counts),
+                                       reinterpret_cast<int*>(rec_tokens),
+                                       reinterpret_cast<hipStream_t>(stream)),
+              "json_count_records");
+        });
   m.def("set_conv_path", &gale::set_conv_path);
   m.def("device_pci_bus_id", [](int device) {
     char buf[64] = {0};

@@ -163,9 +163,8 @@ void sci_digits(float a, int precision, char* dig, int* nd, int* e) {
 
 }  // namespace
 
-Scan scan_instances(const uint8_t* p, size_t n, int H, int W, int C) {
+Scan scan_envelope(const uint8_t* p, size_t n) {
   Scan s;
-  (void)C;
   size_t i = skip_ws(p, 0, n);
   if (i >= n || p[i] != '{') { s.status = BAD_ENVELOPE; return s; }
   i = skip_ws(p, i + 1, n);
@@ -204,7 +203,18 @@ Scan scan_instances(const uint8_t* p, size_t n, int H, int W, int C) {
     s.status = (j > beg) ? UNKNOWN_KEY : BAD_ENVELOPE;  // e.g. {"instances":[..],"k":1}
     return s;
   }
-  const size_t end = j;  // one past the closing ']'
+  s.arr_off = (int64_t)beg;
+  s.arr_len = (int64_t)(j - beg);  // up to and including the closing ']'
+  return s;
+}
+
+Scan scan_instances(const uint8_t* p, size_t n, int H, int W, int C) {
+  (void)C;
+  Scan s = scan_envelope(p, n);
+  if (s.status != OK) return s;
+  const size_t beg = (size_t)s.arr_off;
+  const size_t end = beg + (size_t)s.arr_len;  // one past the closing ']'
+  s.arr_off = s.arr_len = 0;
   const Counts c = count_brackets(p + beg, end - beg);
   if (c.quote > 0) {
     // a string inside the region: another key ("k": ...) or a non-number element

@@ -42,6 +42,11 @@ struct Scan {
   int images = 0;       // N
 };
 
+// Bounded envelope check: the {"instances": ... } prefix and the "] }" suffix only (reads a
+// few bytes at each end; the array's interior, its image count and any key hidden inside it are
+// left to the device ingest / parser). images stays 0.
+Scan scan_envelope(const uint8_t* p, size_t n);
+
 // Envelope validation + image count (the per-number work is left to the GPU parser).
 Scan scan_instances(const uint8_t* p, size_t n, int H, int W, int C);
 

@@ -133,4 +133,27 @@ hipError_t json_parse_instances(int nrec, int ntiles, JsonRecord* recs, const in
                                 const uint8_t* bytes, int H, int W, int C, int* tile_counts,
                                 float* out, hipStream_t stream);
 
+// Ingest pass over a Kafka fetch buffer already on the device: json_count_records counts the
+// number tokens of every record's instances array (rec_tokens[i] += tokens of record i, host
+// zeroes it; invalid bytes raise recs[i].status to 2) so the host learns each record's image
+// count without reading its text.
+hipError_t json_count_records(int nrec, int ntiles, JsonRecord* recs, const int* tile_rec,
+                              const uint8_t* bytes, int* tile_counts, int* rec_tokens,
+                              hipStream_t stream);
+
+// Raw (zero initial state, no final inversion) CRC32C of byte windows [end - len, end) of a
+// device buffer, one wave per window (len <= kCrcChunkBytes): each lane folds 64 bytes with
+// slicing-by-4 tables in LDS, shifts its register over the bytes after its piece (x^(8k) mod P
+// tables) and the wave XOR-reduces. The host joins the windows of a Kafka record batch with
+// crc = shift(crc, 4096) ^ window_crc and converts to the standard CRC (kafka::CrcShift).
+// tables: kafka::crc32c_device_tables() (7168 words) in device memory.
+constexpr int kCrcChunkBytes = 4096;
+struct CrcChunk {
+  int64_t end;  // one past the window's last byte (offset into `bytes`)
+  int32_t len;  // window length, 1..kCrcChunkBytes
+  int32_t pad_;
+};
+hipError_t crc32c_chunks(const uint8_t* bytes, const CrcChunk* chunks, int n,
+                         const uint32_t* tables, uint32_t* out, hipStream_t stream);
+
 }  // namespace gale

@@ -194,6 +194,35 @@ uint32_t crc32c(const uint8_t* p, size_t n, uint32_t crc) {
 
 uint32_t crc32c_shift(uint32_t raw, uint64_t nbytes) { return poly_mulmod(raw, x8n(nbytes)); }
 
+struct CrcShift::Impl {
+  ShiftTable t;
+  explicit Impl(uint64_t n) : t((size_t)n) {}
+};
+CrcShift::CrcShift(uint64_t nbytes) : impl_(std::make_shared<Impl>(nbytes)) {}
+uint32_t CrcShift::operator()(uint32_t raw) const { return impl_->t.shift(raw); }
+
+void crc32c_device_tables(uint32_t* out) {
+  // slicing-by-4 byte tables: S0[v] = raw CRC register after byte v from state 0,
+  // Sk[v] = Sk-1[v] advanced by one zero byte
+  uint32_t* s0 = out;
+  for (uint32_t v = 0; v < 256; ++v) {
+    uint32_t c = v;
+    for (int k = 0; k < 8; ++k) c = (c >> 1) ^ (kPoly & (0u - (c & 1u)));
+    s0[v] = c;
+  }
+  for (int k = 1; k < 4; ++k)
+    for (uint32_t v = 0; v < 256; ++v) {
+      const uint32_t prev = out[(k - 1) * 256 + v];
+      out[k * 256 + v] = (prev >> 8) ^ s0[prev & 0xff];
+    }
+  // shift tables: advance a raw register by 64 * 2^j zero bytes, j = 0..5
+  for (int j = 0; j < 6; ++j) {
+    const ShiftTable t((size_t)64 << j);
+    for (int b = 0; b < 4; ++b)
+      for (int v = 0; v < 256; ++v) out[1024 + j * 1024 + b * 256 + v] = t.t[b][v];
+  }
+}
+
 uint32_t crc32c_combine(uint32_t crc_a, uint32_t crc_b, uint64_t len_b) {
   // standard (inverted) CRCs: the inversions of A's final state and B's initial state cancel
   return crc32c_shift(crc_a, len_b) ^ crc_b;

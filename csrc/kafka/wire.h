@@ -11,6 +11,7 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <memory>
 #include <stdexcept>
 #include <string>
 #include <string_view>
@@ -30,6 +31,20 @@ uint32_t crc32c(const uint8_t* p, size_t n, uint32_t crc = 0);
 // crc32c_shift appends nbytes zero bytes to a raw state (multiplication by x^(8 nbytes) mod P).
 uint32_t crc32c_raw(const uint8_t* p, size_t n, uint32_t raw);
 uint32_t crc32c_shift(uint32_t raw, uint64_t nbytes);
+// Fixed-length shift of a raw CRC register by table lookup (4 loads).
+class CrcShift {
+ public:
+  explicit CrcShift(uint64_t nbytes);
+  uint32_t operator()(uint32_t raw) const;
+
+ private:
+  struct Impl;
+  std::shared_ptr<Impl> impl_;
+};
+// Tables of the GPU CRC32C kernel (csrc/kernels/ingest.hip), kCrcDeviceTableWords words:
+// [0, 1024) slicing-by-4 byte tables, [1024 + 1024 j, ...) shift-by-(64 * 2^j)-bytes tables.
+constexpr int kCrcDeviceTableWords = 1024 * 7;
+void crc32c_device_tables(uint32_t* out);
 // crc32c(A ++ B) from crc32c(A), crc32c(B) and |B|.
 uint32_t crc32c_combine(uint32_t crc_a, uint32_t crc_b, uint64_t len_b);
 // CRC of a message after bytes [k, k+n) changed from old_bytes to new_bytes, with bytes_after

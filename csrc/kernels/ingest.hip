@@ -1,0 +1,79 @@
+// GPU CRC32C of Kafka record batches (the consumer's check.crcs) for the
+// device-side ingest pass (csrc/runtime/gpu_ingest.cpp).
+//
+// The reference's KafkaSpout validates every fetched batch on a JVM thread (storm-kafka /
+// kafka-clients, MainTopology.java:53,95-106). gale's host did it with VPCLMULQDQ folding at
+// ~1.4 cores per MI355X of JSON; here the fetch buffer is DMA'd to the GPU once (the JSON parser
+// then reads it from there) and the GPU folds it: one wave per 4 KiB window, 64 contiguous bytes
+// per lane through slicing-by-4 tables in LDS, then each lane's register is advanced over the
+// bytes that follow its piece by table lookups of x^(8*64*2^j) mod P and the wave XOR-reduces
+// (CRCs are linear: crc(A ++ B) = crc(A) * x^(8|B|) ^ crc(B) for raw registers). Leading zero
+// bytes do not change a raw CRC, so a window shorter than 4 KiB simply leaves its first lanes
+// empty. Misaligned ends are folded byte by byte; everything else uses aligned dword loads.
+#include "common.cuh"
+#include "gale/kernels.h"
+
+namespace gale {
+namespace {
+
+constexpr int kCrcWaves = 4;
+constexpr int kTableWords = 7 * 1024;
+
+__device__ __forceinline__ uint32_t crc_byte(const uint32_t* T, uint32_t c, uint32_t b) {
+  return (c >> 8) ^ T[(c ^ b) & 0xffu];
+}
+
+__device__ __forceinline__ uint32_t crc_word(const uint32_t* T, uint32_t c, uint32_t w) {
+  const uint32_t x = c ^ w;  // byte 0 (first in the stream) is advanced the most
+  return T[768 + (x & 0xffu)] ^ T[512 + ((x >> 8) & 0xffu)] ^ T[256 + ((x >> 16) & 0xffu)] ^
+         T[x >> 24];
+}
+
+__device__ __forceinline__ uint32_t crc_shift(const uint32_t* S, uint32_t c) {
+  return S[c & 0xffu] ^ S[256 + ((c >> 8) & 0xffu)] ^ S[512 + ((c >> 16) & 0xffu)] ^
+         S[768 + (c >> 24)];
+}
+
+__global__ __launch_bounds__(256) void crc32c_chunks_kernel(const uint8_t* bytes,
+                                                            const CrcChunk* chunks, int n,
+                                                            const uint32_t* tables,
+                                                            uint32_t* out) {
+  __shared__ uint32_t T[kTableWords];
+  for (int i = threadIdx.x; i < kTableWords; i += blockDim.x) T[i] = tables[i];
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int c = blockIdx.x * kCrcWaves + wave; c < n; c += gridDim.x * kCrcWaves) {
+    const CrcChunk ch = chunks[c];
+    const int64_t cs = ch.end - ch.len;
+    const int64_t wa = ch.end - (int64_t)64 * (64 - lane);  // this lane's piece [wa, wa + 64)
+    const int64_t hi = wa + 64;
+    int64_t q = wa > cs ? wa : cs;
+    uint32_t crc = 0;
+    if (q < hi) {
+      while (q < hi && (q & 3)) crc = crc_byte(T, crc, bytes[q++]);
+      for (; q + 4 <= hi; q += 4) crc = crc_word(T, crc, *reinterpret_cast<const uint32_t*>(bytes + q));
+      while (q < hi) crc = crc_byte(T, crc, bytes[q++]);
+    }
+    const int s = 63 - lane;  // pieces after this one
+#pragma unroll
+    for (int j = 0; j < 6; ++j)
+      if ((s >> j) & 1) crc = crc_shift(T + 1024 * (j + 1), crc);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) crc ^= __shfl_xor(crc, o, 64);
+    if (lane == 0) out[c] = crc;
+  }
+}
+
+}  // namespace
+
+hipError_t crc32c_chunks(const uint8_t* bytes, const CrcChunk* chunks, int n,
+                         const uint32_t* tables, uint32_t* out, hipStream_t stream) {
+  if (n <= 0) return hipSuccess;
+  int blocks = (n + kCrcWaves - 1) / kCrcWaves;
+  if (blocks > 1024) blocks = 1024;  // waves loop: the 28 KB table load is amortised
+  hipLaunchKernelGGL(crc32c_chunks_kernel, dim3(blocks), dim3(64 * kCrcWaves), 0, stream, bytes,
+                     chunks, n, tables, out);
+  return hipGetLastError();
+}
+
+}  // namespace gale

@@ -7,9 +7,9 @@
 // cost of the whole pipeline, so gale moves it to the GPU. The host only validates
 // the envelope and counts '[' to get N (codec::scan_instances) and stages the raw bytes of the
 // instances array; the device then
-//   * splits every record's text into 4 KiB tiles, ONE WAVE PER TILE (64 lanes x 64 contiguous
-//     bytes; 4 tiles per 256-thread workgroup, so a 256-record CIFAR batch is ~2300 waves and no
-//     kernel here has a workgroup barrier),
+//   * splits every record's text into kJsonTileBytes = 2 KiB tiles, ONE WAVE PER TILE (64 lanes
+//     x 32 contiguous bytes; 4 tiles per 256-thread workgroup, so a 256-record CIFAR batch is
+//     ~4600 waves and no kernel here has a workgroup barrier),
 //   * classifies 4 bytes per VALU op with a nibble lookup (two v_perm_b32 tables, as in SIMD JSON
 //     scanners) into delimiter / number-alphabet / digit bit masks,
 //   * pass 1 (json_count_kernel): counts the number tokens of each tile (a token starts at a
@@ -386,7 +386,7 @@ __device__ __forceinline__ bool gap_window(const uint8_t* text, int x, int k) {
 
 __global__ __launch_bounds__(256) void json_count_kernel(JsonRecord* recs, const int* tile_rec,
                                                          int ntiles, const uint8_t* bytes,
-                                                         int* counts) {
+                                                         int* counts, int* rec_tokens) {
   const int lane = threadIdx.x & 63;
   const int t = blockIdx.x * kWaves + (threadIdx.x >> 6);
   if (t >= ntiles) return;  // (no workgroup barriers in this kernel)
@@ -411,7 +411,10 @@ __global__ __launch_bounds__(256) void json_count_kernel(JsonRecord* recs, const
 #pragma unroll
   for (int i = 0; i < kChunks; ++i) lc += __builtin_popcount(st[i]);
   const int cnt = wave_sum_i(lc);
-  if (lane == 0) counts[t] = cnt;
+  if (lane == 0) {
+    counts[t] = cnt;
+    if (rec_tokens) atomicAdd(&rec_tokens[ri], cnt);  // ingest: the record's element count
+  }
   if (bad) atomicMax(&recs[ri].status, 2);
 }
 
@@ -539,6 +542,16 @@ __global__ __launch_bounds__(256) void json_parse_kernel(JsonRecord* recs, const
 
 }  // namespace
 
+hipError_t json_count_records(int nrec, int ntiles, JsonRecord* recs, const int* tile_rec,
+                              const uint8_t* bytes, int* tile_counts, int* rec_tokens,
+                              hipStream_t stream) {
+  if (nrec <= 0 || ntiles <= 0) return hipSuccess;
+  const int blocks = (ntiles + kWaves - 1) / kWaves;
+  hipLaunchKernelGGL(json_count_kernel, dim3(blocks), dim3(64 * kWaves), 0, stream, recs,
+                     tile_rec, ntiles, bytes, tile_counts, rec_tokens);
+  return hipGetLastError();
+}
+
 int json_tile_count(int64_t off, int32_t len) {
   if (len <= 0) return 0;
   const int64_t abeg = off & ~(int64_t)15;
@@ -552,7 +565,7 @@ hipError_t json_parse_instances(int nrec, int ntiles, JsonRecord* recs, const in
   if (H <= 0 || W <= 0 || C <= 0) return hipErrorInvalidValue;
   const int blocks = (ntiles + kWaves - 1) / kWaves;
   hipLaunchKernelGGL(json_count_kernel, dim3(blocks), dim3(64 * kWaves), 0, stream, recs,
-                     tile_rec, ntiles, bytes, tile_counts);
+                     tile_rec, ntiles, bytes, tile_counts, nullptr);
   hipLaunchKernelGGL(json_parse_kernel, dim3(blocks), dim3(64 * kWaves), 0, stream, recs,
                      tile_rec, ntiles, bytes, H, W, C, tile_counts, out);
   return hipGetLastError();

@@ -4,6 +4,7 @@
 
 #include <hip/hip_runtime.h>
 #include <stdio.h>
+#include <sys/prctl.h>
 
 #include <algorithm>
 #include <sstream>
@@ -124,6 +125,8 @@ Engine::Engine(EngineConfig cfg) : cfg_(std::move(cfg)), rng_(cfg_.seed) {
     throw std::invalid_argument("engine: on_error must be null|error-json|drop");
   if (cfg_.value_format != "json" && cfg_.value_format != "json-string")
     throw std::invalid_argument("engine: value_format must be json|json-string");
+  if (cfg_.output_key != "none" && cfg_.output_key != "input")
+    throw std::invalid_argument("engine: output_key must be none|input");
   if (cfg_.max_batch <= 0 || cfg_.source_parallelism <= 0 || cfg_.sink_parallelism <= 0)
     throw std::invalid_argument("engine: max_batch / parallelism must be positive");
   // fault injection spec: comma separated kind@value
@@ -165,6 +168,11 @@ void Engine::add_replica(std::shared_ptr<Replica> r) {
   replicas_.push_back(std::move(s));
 }
 
+void Engine::set_ingest(std::shared_ptr<Ingest> ing) {
+  if (running_) throw std::logic_error("engine: set_ingest after start");
+  ingest_ = std::move(ing);
+}
+
 kafka::Producer* Engine::producer_for(int i) {
   return producers_[(size_t)i % producers_.size()].get();
 }
@@ -201,9 +209,11 @@ void Engine::start() {
   for (size_t i = 0; i < parts.size(); ++i) split[i % (size_t)ns].push_back(parts[i]);
   bool any_gpu = false;
   for (auto& rs : replicas_) any_gpu |= rs->rep->device() >= 0;
-  if (any_gpu && cfg_.pinned_fetch_bytes > 0 && !pinned_)
+  if ((any_gpu || ingest_) && cfg_.pinned_fetch_bytes > 0 && !pinned_) {
     pinned_ = std::make_shared<PinnedPool>((size_t)cfg_.fetch_max_bytes + (1 << 20),
                                            (size_t)cfg_.pinned_fetch_bytes);
+    if (ingest_) pinned_->set_mirror_device(ingest_->device());
+  }
   running_ = true;
   stopping_ = false;
   workers_done_ = false;
@@ -218,6 +228,7 @@ void Engine::start() {
   for (auto& rs : replicas_)
     workers_.emplace_back([this, rs] {
       name_thread("gl-rep", rs->index);
+      prctl(PR_SET_TIMERSLACK, 1000UL, 0, 0, 0);  // 1 us: sleep-polling GPU waits stay tight
       worker_loop(rs.get());
     });
   for (int i = 0; i < ns; ++i)
@@ -372,7 +383,7 @@ void Engine::source_loop(int idx, std::vector<int> parts) {
       it.t_fetch_ns = now;
       if (cfg_.decode_threads <= 0) {
         good.clear();
-        decode_fetch(it, good);
+        decode_fetch(it, good, idx);
         // when stopping with a full queue the rest stays pending (never committed, so a
         // restart with start_offset=committed re-reads it)
         if (!good.empty()) batcher_->push_many(good, stopping_);
@@ -404,7 +415,6 @@ void Engine::source_loop(int idx, std::vector<int> parts) {
 }
 
 void Engine::decode_loop(int idx) {
-  (void)idx;
   std::vector<InRecord> good;
   for (;;) {
     FetchItem it;
@@ -420,16 +430,90 @@ void Engine::decode_loop(int idx) {
     const int64_t t0 = mono_ns();
     {
       trace::Range tr("gale:decode");
-      decode_fetch(it, good);
+      decode_fetch(it, good, idx);
     }
     ns_decode_ += mono_ns() - t0;
     if (!good.empty()) batcher_->push_many(good, stopping_);
   }
 }
 
+// GPU ingest of one pinned fetch buffer (ingest.h): bounded envelope checks on the host, batch
+// CRCs and image counts on the device. False = not applicable (the caller takes the host path).
+bool Engine::ingest_fetch(FetchItem& it, std::vector<InRecord>& good, int lane) {
+  if (!ingest_ || !it.pinned || ingest_failed_) return false;
+  kafka::Fetched& f = it.f;
+  uint8_t* dev = pinned_->mirror(f.buf.get());
+  if (!dev) return false;
+  const int64_t t0 = mono_ns();
+  const size_t n = f.records.size();
+  IngestIO io;
+  io.status.assign(n, codec::OK);
+  io.arr_off.assign(n, 0);
+  io.arr_len.assign(n, 0);
+  for (size_t i = 0; i < n; ++i) {
+    const kafka::RecordRef& rr = f.records[i];
+    if (rr.value_len < 0) {
+      io.status[i] = codec::BAD_ENVELOPE;  // null value (Jackson would throw)
+      continue;
+    }
+    const codec::Scan s = codec::scan_envelope(f.buf.get() + rr.value_off, (size_t)rr.value_len);
+    io.status[i] = s.status;
+    io.arr_off[i] = s.arr_off;
+    io.arr_len[i] = s.arr_len;
+  }
+  try {
+    ingest_->run(lane, f, dev, cfg_.check_crcs && !f.crc_checked, cfg_.H, cfg_.W, cfg_.C, io);
+  } catch (const std::exception& e) {
+    if (!ingest_failed_.exchange(true))
+      fprintf(stderr, "[gale decode] GPU ingest failed (%s): host decode from now on\n", e.what());
+    return false;
+  }
+  std::vector<char> corrupt(n, 0);
+  for (size_t b = 0; b < f.batches.size(); ++b)
+    if (!io.batch_ok[b])
+      for (size_t i = 0; i < f.batches[b].nrec; ++i) corrupt[f.batches[b].first_rec + i] = 1;
+  kafka::Producer* prod = producer_for(it.source);
+  const int dev_id = ingest_->device();
+  for (size_t i = 0; i < n; ++i) {
+    const kafka::RecordRef& rr = f.records[i];
+    InRecord r;
+    r.buf = f.buf;
+    r.pinned = true;
+    r.value = rr.value_len >= 0 ? f.buf.get() + rr.value_off : nullptr;
+    r.len = rr.value_len;
+    r.key = rr.key_len >= 0 ? f.buf.get() + rr.key_off : nullptr;
+    r.key_len = rr.key_len;
+    r.partition = rr.partition;
+    r.offset = rr.offset;
+    r.timestamp_ms = rr.timestamp;
+    r.t_fetch_ns = it.t_fetch_ns;
+    r.source = it.source;
+    r.dev_value = dev + rr.value_off;
+    r.dev_device = dev_id;
+    ++records_in_;
+    if (r.len >= 0) bytes_in_ += r.len;
+    r.status = corrupt[i] ? (int)codec::BAD_ENVELOPE : io.status[i];
+    r.arr_off = io.arr_off[i];
+    r.arr_len = io.arr_len[i];
+    r.images = io.images[i];
+    if (r.status == codec::OK && r.images > cfg_.max_batch) r.status = codec::TOO_LARGE;
+    if (r.status == codec::OK && fault_hit(parse_error_p_)) r.status = codec::BAD_ENVELOPE;
+    if (r.status == codec::OK) {
+      images_in_ += r.images;
+      good.push_back(std::move(r));
+    } else {
+      emit_error(r, r.status, prod);
+    }
+  }
+  ingested_records_ += (int64_t)n;
+  ingest_ns_ += mono_ns() - t0;
+  return true;
+}
+
 // CRC32C of every record batch (unless the consumer checked it), then the envelope scan of
 // every record; malformed records go straight to the error policy.
-void Engine::decode_fetch(FetchItem& it, std::vector<InRecord>& good) {
+void Engine::decode_fetch(FetchItem& it, std::vector<InRecord>& good, int lane) {
+  if (ingest_fetch(it, good, lane)) return;
   kafka::Fetched& f = it.f;
   std::vector<char> corrupt;
   // CRC32C and envelope scan fused in one pass: the batch CRC is chained record by record
@@ -475,6 +559,8 @@ void Engine::decode_fetch(FetchItem& it, std::vector<InRecord>& good) {
     r.pinned = it.pinned;
     r.value = rr.value_len >= 0 ? f.buf.get() + rr.value_off : nullptr;
     r.len = rr.value_len;
+    r.key = rr.key_len >= 0 ? f.buf.get() + rr.key_off : nullptr;
+    r.key_len = rr.key_len;
     r.partition = rr.partition;
     r.offset = rr.offset;
     r.timestamp_ms = rr.timestamp;
@@ -766,6 +852,9 @@ void Engine::emit(InRecord& r, std::string value, bool null_value, kafka::Produc
   meta.t_fetch_ns = r.t_fetch_ns;
   meta.images = r.status == codec::OK ? r.images : 0;
   const bool ff = cfg_.sink_mode == "fire-and-forget";
+  std::string key;
+  const bool keyed = cfg_.output_key == "input" && r.key_len >= 0 && r.key;
+  if (keyed) key.assign(reinterpret_cast<const char*>(r.key), (size_t)r.key_len);
   kafka::SendCallback cb;
   if (!ff) {
     cb = [this, meta](const kafka::SendResult& res) {
@@ -774,8 +863,8 @@ void Engine::emit(InRecord& r, std::string value, bool null_value, kafka::Produc
     };
   }
   try {
-    prod->send(cfg_.output_topic, -1, nullptr, std::move(value), null_value, std::move(hs), -1,
-               std::move(cb));
+    prod->send(cfg_.output_topic, -1, keyed ? &key : nullptr, std::move(value), null_value,
+               std::move(hs), -1, std::move(cb));
   } catch (const std::exception& e) {
     fprintf(stderr, "[gale sink] send failed: %s\n", e.what());
     complete_record(meta, false);
@@ -855,6 +944,8 @@ std::map<std::string, double> Engine::stats() const {
   int alive = 0;
   for (auto& r : replicas_) alive += r->alive ? 1 : 0;
   s["replicas_alive"] = alive;
+  s["ingested_records"] = (double)ingested_records_;
+  s["thread_s_ingest"] = ingest_ns_ * 1e-9;
   s["eff_max_batch"] = (double)eff_batch_;
   s["eff_max_wait_us"] = (double)eff_wait_ns_ / 1000.0;
   s["slo_adjustments"] = (double)slo_adjustments_;

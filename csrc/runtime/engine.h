@@ -36,6 +36,7 @@
 #include <vector>
 
 #include "../kafka/client.h"
+#include "ingest.h"
 #include "metrics.h"
 #include "pinned_pool.h"
 #include "replica.h"
@@ -67,6 +68,9 @@ struct EngineConfig {
   std::string value_format = "json";  // json | json-string (spring JsonSerializer, E8)
   bool type_id_header = false;     // __TypeId__: java.lang.String header (E8)
   std::string on_error = "null";   // null | error-json | drop
+  // output record key: "none" = unkeyed (the reference, E9: FieldNameBasedTupleToKafkaMapper
+  // finds no "key" field) | "input" = the input record's key (request/response correlation)
+  std::string output_key = "none";
   // model I/O contract (InstObj [N][H][W][C] -> PredObj [N][classes])
   int H = 32, W = 32, C = 3, classes = 10;
   // batching (P7)
@@ -118,6 +122,9 @@ class Engine {
   Engine& operator=(const Engine&) = delete;
 
   void add_replica(std::shared_ptr<Replica> r);
+  // Device-side ingest of pinned fetch buffers (CRC32C + image counts on the GPU, ingest.h);
+  // set before start(). Records whose buffer has no device mirror take the host path.
+  void set_ingest(std::shared_ptr<Ingest> ing);
   void start();
   // Graceful stop: sources stop fetching, queued records drain through the replicas, the sink
   // is flushed and offsets are committed.
@@ -150,7 +157,8 @@ class Engine {
 
   void source_loop(int idx, std::vector<int> parts);
   void decode_loop(int idx);
-  void decode_fetch(FetchItem& it, std::vector<InRecord>& good);
+  void decode_fetch(FetchItem& it, std::vector<InRecord>& good, int lane);
+  bool ingest_fetch(FetchItem& it, std::vector<InRecord>& good, int lane);
   void worker_loop(ReplicaSlot* rs);
   void serve(ReplicaSlot* rs);  // one replica life: returns once it dies or the engine drains
   void watchdog_loop();
@@ -169,6 +177,9 @@ class Engine {
   std::vector<std::unique_ptr<kafka::Producer>> producers_;
   std::vector<std::thread> sources_, workers_, decoders_;
   std::shared_ptr<PinnedPool> pinned_;
+  std::shared_ptr<Ingest> ingest_;
+  std::atomic<bool> ingest_failed_{false};
+  std::atomic<int64_t> ingested_records_{0}, ingest_ns_{0};
   std::mutex dec_mu_;
   std::condition_variable dec_cv_, dec_space_cv_;
   std::deque<FetchItem> dec_q_;

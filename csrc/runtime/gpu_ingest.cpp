@@ -1,0 +1,212 @@
+// GpuIngest (see gpu_ingest.h / ingest.h).
+#include "gpu_ingest.h"
+
+#include <string.h>
+
+#include <chrono>
+#include <stdexcept>
+#include <thread>
+
+#include "../codec/json_codec.h"
+#include "gale/executor.h"
+
+namespace gale {
+
+GpuIngest::GpuIngest(int device, int lanes, int poll_us)
+    : device_(device), poll_us_(poll_us), shift_chunk_(kCrcChunkBytes) {
+  check_hip(hipSetDevice(device_), "ingest: hipSetDevice");
+  std::vector<uint32_t> t(kafka::kCrcDeviceTableWords);
+  kafka::crc32c_device_tables(t.data());
+  check_hip(hipMalloc(reinterpret_cast<void**>(&d_tables_), t.size() * 4), "ingest: tables");
+  check_hip(hipMemcpy(d_tables_, t.data(), t.size() * 4, hipMemcpyHostToDevice),
+            "ingest: tables H2D");
+  for (int i = 0; i < std::max(1, lanes); ++i) {
+    auto L = std::make_unique<Lane>();
+    check_hip(hipStreamCreateWithFlags(&L->stream, hipStreamNonBlocking), "ingest: stream");
+    check_hip(hipEventCreateWithFlags(&L->done, hipEventDisableTiming), "ingest: event");
+    lanes_.push_back(std::move(L));
+  }
+}
+
+GpuIngest::~GpuIngest() {
+  hipSetDevice(device_);
+  for (auto& L : lanes_) {
+    if (L->stream) hipStreamSynchronize(L->stream);
+    if (L->h_in) hipHostFree(L->h_in);
+    if (L->d_in) hipFree(L->d_in);
+    if (L->h_out) hipHostFree(L->h_out);
+    if (L->d_out) hipFree(L->d_out);
+    if (L->d_counts) hipFree(L->d_counts);
+    if (L->done) hipEventDestroy(L->done);
+    if (L->stream) hipStreamDestroy(L->stream);
+  }
+  if (d_tables_) hipFree(d_tables_);
+}
+
+void GpuIngest::grow(Lane& L, size_t in_bytes, size_t out_bytes, size_t tiles) {
+  auto up = [](size_t want, size_t have) {
+    return (std::max(want, have * 2) + 4095) & ~(size_t)4095;
+  };
+  if (in_bytes > L.in_cap) {
+    if (L.h_in) hipHostFree(L.h_in);
+    if (L.d_in) hipFree(L.d_in);
+    L.in_cap = up(in_bytes, L.in_cap);
+    check_hip(hipHostMalloc(reinterpret_cast<void**>(&L.h_in), L.in_cap), "ingest: h_in");
+    check_hip(hipMalloc(reinterpret_cast<void**>(&L.d_in), L.in_cap), "ingest: d_in");
+  }
+  if (out_bytes > L.out_cap) {
+    if (L.h_out) hipHostFree(L.h_out);
+    if (L.d_out) hipFree(L.d_out);
+    L.out_cap = up(out_bytes, L.out_cap);
+    check_hip(hipHostMalloc(reinterpret_cast<void**>(&L.h_out), L.out_cap), "ingest: h_out");
+    check_hip(hipMalloc(reinterpret_cast<void**>(&L.d_out), L.out_cap), "ingest: d_out");
+  }
+  if (tiles * sizeof(int) > L.counts_cap) {
+    if (L.d_counts) hipFree(L.d_counts);
+    L.counts_cap = up(tiles * sizeof(int), L.counts_cap);
+    check_hip(hipMalloc(reinterpret_cast<void**>(&L.d_counts), L.counts_cap), "ingest: counts");
+  }
+}
+
+void GpuIngest::wait(Lane& L) {
+  if (poll_us_ <= 0) {
+    check_hip(hipEventSynchronize(L.done), "ingest: hipEventSynchronize");
+    return;
+  }
+  for (;;) {
+    const hipError_t e = hipEventQuery(L.done);
+    if (e == hipSuccess) return;
+    if (e != hipErrorNotReady) check_hip(e, "ingest: hipEventQuery");
+    std::this_thread::sleep_for(std::chrono::microseconds(poll_us_));
+  }
+}
+
+namespace {
+size_t align16(size_t n) { return (n + 15) & ~(size_t)15; }
+}  // namespace
+
+void GpuIngest::run(int lane, const kafka::Fetched& f, uint8_t* dev, bool check_crcs, int H,
+                    int W, int C, IngestIO& io) {
+  Lane& L = *lanes_[(size_t)lane % lanes_.size()];
+  std::lock_guard<std::mutex> lk(L.mu);
+  const size_t nrec_all = f.records.size();
+  io.images.assign(nrec_all, 0);
+  io.batch_ok.assign(f.batches.size(), 1);
+  // ---- plan: CRC windows (aligned to each batch's end) and the records to count
+  std::vector<CrcChunk> chunks;
+  std::vector<std::pair<size_t, size_t>> batch_chunks;  // (first chunk, count) per batch
+  size_t lo = f.size, hi = 0;
+  for (const kafka::BatchSpan& b : f.batches) {
+    lo = std::min(lo, b.off);
+    hi = std::max(hi, b.off + b.len);
+    if (!check_crcs) continue;
+    const int64_t rs = (int64_t)b.off + kafka::kBatchAttrOffset, re = (int64_t)(b.off + b.len);
+    const int64_t len = re - rs;
+    const int64_t n = (len + kCrcChunkBytes - 1) / kCrcChunkBytes;
+    batch_chunks.emplace_back(chunks.size(), (size_t)n);
+    for (int64_t k = 0; k < n; ++k) {
+      CrcChunk c;
+      c.end = re - (int64_t)kCrcChunkBytes * (n - 1 - k);
+      c.len = k == 0 ? (int32_t)(len - (int64_t)kCrcChunkBytes * (n - 1)) : kCrcChunkBytes;
+      c.pad_ = 0;
+      chunks.push_back(c);
+    }
+  }
+  std::vector<int> rec_of;  // JsonRecord j -> record index
+  int ntiles = 0;
+  for (size_t i = 0; i < nrec_all; ++i) {
+    if (io.status[i] != codec::OK) continue;
+    const kafka::RecordRef& rr = f.records[i];
+    rec_of.push_back((int)i);
+    ntiles += json_tile_count(rr.value_off + io.arr_off[i], (int32_t)io.arr_len[i]);
+    lo = std::min(lo, (size_t)rr.value_off);
+    hi = std::max(hi, (size_t)(rr.value_off + rr.value_len));
+  }
+  const size_t nc = chunks.size(), nr = rec_of.size();
+  if (nc == 0 && nr == 0) return;
+  const size_t in_chunks = align16(nc * sizeof(CrcChunk)), in_recs = align16(nr * sizeof(JsonRecord));
+  const size_t in_bytes = in_chunks + in_recs + (size_t)ntiles * sizeof(int);
+  const size_t out_crc = align16(nc * 4), out_tok = align16(nr * 4);
+  const size_t out_bytes = out_crc + out_tok + nr * sizeof(JsonRecord);
+  check_hip(hipSetDevice(device_), "ingest: hipSetDevice");
+  grow(L, in_bytes + 16, out_bytes + 16, (size_t)ntiles + 1);
+  CrcChunk* hc = reinterpret_cast<CrcChunk*>(L.h_in);
+  JsonRecord* hr = reinterpret_cast<JsonRecord*>(L.h_in + in_chunks);
+  int* ht = reinterpret_cast<int*>(L.h_in + in_chunks + in_recs);
+  if (nc) memcpy(hc, chunks.data(), nc * sizeof(CrcChunk));
+  int tile = 0;
+  for (size_t j = 0; j < nr; ++j) {
+    const size_t i = (size_t)rec_of[j];
+    JsonRecord& jr = hr[j];
+    jr.off = f.records[i].value_off + io.arr_off[i];
+    jr.len = (int32_t)io.arr_len[i];
+    jr.slot = 0;
+    jr.images = 0;
+    jr.status = 0;
+    jr.tile0 = tile;
+    jr.pad_ = 0;
+    const int nt = json_tile_count(jr.off, jr.len);
+    for (int t = 0; t < nt; ++t) ht[tile + t] = (int)j;
+    tile += nt;
+  }
+  // ---- device: text span -> mirror, tables, CRC windows, token counts, results back
+  lo &= ~(size_t)15;
+  hipStream_t st = L.stream;
+  check_hip(hipMemcpyAsync(dev + lo, f.buf.get() + lo, hi - lo, hipMemcpyHostToDevice, st),
+            "ingest: H2D text");
+  check_hip(hipMemcpyAsync(L.d_in, L.h_in, in_bytes, hipMemcpyHostToDevice, st),
+            "ingest: H2D plan");
+  uint32_t* d_crc = reinterpret_cast<uint32_t*>(L.d_out);
+  int* d_tok = reinterpret_cast<int*>(L.d_out + out_crc);
+  JsonRecord* d_rec = reinterpret_cast<JsonRecord*>(L.d_in + in_chunks);
+  if (nr) check_hip(hipMemsetAsync(d_tok, 0, nr * 4, st), "ingest: memset");
+  if (nc)
+    check_hip(crc32c_chunks(dev, reinterpret_cast<const CrcChunk*>(L.d_in), (int)nc, d_tables_,
+                            d_crc, st),
+              "ingest: crc32c_chunks");
+  if (nr)
+    check_hip(json_count_records((int)nr, ntiles, d_rec,
+                                 reinterpret_cast<const int*>(L.d_in + in_chunks + in_recs), dev,
+                                 L.d_counts, d_tok, st),
+              "ingest: json_count_records");
+  check_hip(hipMemcpyAsync(L.h_out, L.d_out, out_crc + out_tok, hipMemcpyDeviceToHost, st),
+            "ingest: D2H results");
+  if (nr)
+    check_hip(hipMemcpyAsync(L.h_out + out_crc + out_tok, d_rec, nr * sizeof(JsonRecord),
+                             hipMemcpyDeviceToHost, st),
+              "ingest: D2H status");
+  check_hip(hipEventRecord(L.done, st), "ingest: event");
+  wait(L);
+  // ---- host: join the windows of each batch and compare; images from the element counts
+  const uint32_t* crc = reinterpret_cast<const uint32_t*>(L.h_out);
+  for (size_t b = 0; b < batch_chunks.size(); ++b) {
+    const kafka::BatchSpan& bs = f.batches[b];
+    uint32_t raw = 0;
+    for (size_t k = 0; k < batch_chunks[b].second; ++k) {
+      const uint32_t c = crc[batch_chunks[b].first + k];
+      raw = k == 0 ? c : shift_chunk_(raw) ^ c;
+    }
+    // standard CRC32C = raw ^ (initial ~0 carried over the message) ^ final ~0
+    const uint64_t len = bs.len - (size_t)kafka::kBatchAttrOffset;
+    const uint32_t got = raw ^ kafka::crc32c_shift(0xffffffffu, len) ^ 0xffffffffu;
+    kafka::Reader cr(f.buf.get() + bs.off + kafka::kBatchCrcOffset, 4);
+    io.batch_ok[b] = got == cr.u32();
+  }
+  const int* tok = reinterpret_cast<const int*>(L.h_out + out_crc);
+  const JsonRecord* rst = reinterpret_cast<const JsonRecord*>(L.h_out + out_crc + out_tok);
+  const int64_t per = (int64_t)H * W * C;
+  for (size_t j = 0; j < nr; ++j) {
+    const size_t i = (size_t)rec_of[j];
+    if (rst[j].status != 0) {
+      io.status[i] = codec::BAD_NUMBER;
+    } else if (tok[j] == 0) {
+      io.status[i] = codec::EMPTY;
+    } else if (tok[j] % per != 0) {
+      io.status[i] = codec::BAD_SHAPE;
+    } else {
+      io.images[i] = (int32_t)(tok[j] / per);
+    }
+  }
+}
+
+}  // namespace gale

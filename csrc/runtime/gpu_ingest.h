@@ -1,0 +1,47 @@
+// GpuIngest: the HIP implementation of Ingest (see ingest.h). Kept out of engine.cpp so the
+// sanitizer build of the host pipeline links no GPU kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <memory>
+#include <mutex>
+#include <vector>
+
+#include "gale/kernels.h"
+#include "ingest.h"
+
+namespace gale {
+
+class GpuIngest : public Ingest {
+ public:
+  // lanes: decode threads that may call run() concurrently; poll_us: sleep between completion
+  // polls (0 = hipEventSynchronize)
+  GpuIngest(int device, int lanes, int poll_us);
+  ~GpuIngest() override;
+  int device() const override { return device_; }
+  void run(int lane, const kafka::Fetched& f, uint8_t* dev, bool check_crcs, int H, int W, int C,
+           IngestIO& io) override;
+
+ private:
+  struct Lane {
+    std::mutex mu;
+    hipStream_t stream = nullptr;
+    hipEvent_t done = nullptr;
+    uint8_t* h_in = nullptr;  // pinned: [CrcChunk x nc][JsonRecord x nr][tile_rec x nt]
+    uint8_t* d_in = nullptr;
+    size_t in_cap = 0;
+    uint8_t* h_out = nullptr;  // pinned: [crc u32 x nc][tokens i32 x nr][JsonRecord x nr]
+    uint8_t* d_out = nullptr;
+    size_t out_cap = 0;
+    int* d_counts = nullptr;  // per-tile token counts (scratch)
+    size_t counts_cap = 0;
+  };
+  void grow(Lane& L, size_t in_bytes, size_t out_bytes, size_t tiles);
+  void wait(Lane& L);
+  int device_, poll_us_;
+  uint32_t* d_tables_ = nullptr;
+  std::vector<std::unique_ptr<Lane>> lanes_;
+  kafka::CrcShift shift_chunk_;
+};
+
+}  // namespace gale

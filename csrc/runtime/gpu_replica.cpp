@@ -4,6 +4,8 @@
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
+#include <thread>
 #include <stdexcept>
 
 #include "../codec/json_codec.h"
@@ -16,8 +18,9 @@ namespace gale {
 // ---------------------------------------------------------------------------------------------
 
 GpuReplica::GpuReplica(std::shared_ptr<Executor> exec, int H, int W, int C, int classes,
-                       bool use_graph)
-    : exec_(std::move(exec)), H_(H), W_(W), C_(C), classes_(classes), use_graph_(use_graph) {
+                       bool use_graph, int wait_poll_us)
+    : exec_(std::move(exec)), H_(H), W_(W), C_(C), classes_(classes), use_graph_(use_graph),
+      wait_poll_us_(wait_poll_us) {
   if (exec_->input_bytes_per_image() != (long long)H * W * C * 4)
     throw std::invalid_argument("GpuReplica: executor input is not fp32 [H, W, C]");
   if (exec_->output_bytes_per_image() != (long long)classes * 4)
@@ -124,7 +127,12 @@ void GpuReplica::submit(Batch& b) {
   };
   std::vector<Span> spans;
   size_t staged = 0;
+  const int my_dev = exec_->device();
+  auto resident = [my_dev](const InRecord& r) {
+    return r.dev_value != nullptr && r.dev_device == my_dev;
+  };
   for (const InRecord& r : b.recs) {
+    if (resident(r)) continue;  // already in device memory (GPU ingest): nothing to copy
     const uint8_t* base = r.buf.get();
     const size_t lo = (size_t)(r.value + r.arr_off - base), hi = lo + (size_t)r.arr_len;
     if (!r.pinned) {
@@ -165,7 +173,12 @@ void GpuReplica::submit(Batch& b) {
     JsonRecord& jr = s.h_recs[nrec++];
     const uint8_t* base = r.buf.get();
     const size_t lo = (size_t)(r.value + r.arr_off - base);
-    if (r.pinned) {
+    if (resident(r)) {
+      // offsets are relative to the slot's buffer; a mirror elsewhere in device memory is a
+      // (signed) distance in the flat address space, 16-byte phase preserved (both bases are
+      // 256-byte aligned allocations)
+      jr.off = (int64_t)((r.dev_value + r.arr_off) - s.d_bytes);
+    } else if (r.pinned) {
       size_t k = 0;
       while (spans[k].base != base) ++k;
       jr.off = (int64_t)(span_dev[k] + (lo - spans[k].lo));
@@ -218,7 +231,18 @@ void GpuReplica::submit(Batch& b) {
 
 void GpuReplica::wait(Batch& b) {
   Slot& s = slots_[(size_t)b.slot];
-  check_hip(hipEventSynchronize(s.done), "hipEventSynchronize(batch)");
+  if (wait_poll_us_ > 0) {
+    // sleep-poll: the thread sleeps while the GPU works (the engine's timer slack is set to
+    // 1 us on replica threads, so a sleep is not stretched by the default 50 us slack)
+    for (;;) {
+      const hipError_t e = hipEventQuery(s.done);
+      if (e == hipSuccess) break;
+      if (e != hipErrorNotReady) check_hip(e, "hipEventQuery(batch)");
+      std::this_thread::sleep_for(std::chrono::microseconds(wait_poll_us_));
+    }
+  } else {
+    check_hip(hipEventSynchronize(s.done), "hipEventSynchronize(batch)");
+  }
   b.dev_status.assign(b.recs.size(), codec::OK);
   for (size_t i = 0; i < b.recs.size(); ++i) {
     const int st = s.h_recs[i].status;

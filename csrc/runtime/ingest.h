@@ -1,0 +1,40 @@
+// Device-side ingest of Kafka fetch buffers (SURVEY.md §7.5 hard part 1: host throughput).
+//
+// The host path verifies every record batch's CRC32C and scans every record's JSON envelope to
+// count its images before micro-batching: ~35 KB of host reads per CIFAR image on top of the
+// socket receive. With an Ingest attached, a pinned fetch buffer is instead DMA'd once to its
+// device mirror (PinnedPool::mirror) and the GPU computes the batch CRCs and the per-record
+// element counts (csrc/kernels/ingest.hip, json_count_records). The host reads only Kafka framing
+// and a bounded prefix/suffix of each record (codec::scan_envelope); the GPU replica later parses
+// the records straight from the device mirror, so the JSON text crosses PCIe once and is never
+// read by a host core.
+#pragma once
+#include <stdint.h>
+
+#include <vector>
+
+#include "../kafka/client.h"
+
+namespace gale {
+
+struct IngestIO {
+  // in: per record (index into Fetched::records) the envelope check result (codec::Status,
+  // array extent relative to the record value); out: image count, status raised by the GPU
+  std::vector<int32_t> status;
+  std::vector<int64_t> arr_off, arr_len;
+  std::vector<int32_t> images;
+  // out: per Fetched::batches entry, false when its CRC32C did not match (check_crcs)
+  std::vector<char> batch_ok;
+};
+
+class Ingest {
+ public:
+  virtual ~Ingest() = default;
+  virtual int device() const = 0;
+  // lane: the calling decode thread (each lane owns its stream and staging buffers).
+  // dev: device mirror of f.buf (same offsets). Throws on a device error.
+  virtual void run(int lane, const kafka::Fetched& f, uint8_t* dev, bool check_crcs, int H, int W,
+                   int C, IngestIO& io) = 0;
+};
+
+}  // namespace gale

@@ -3,6 +3,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include <unordered_map>
+
 #include "../kafka/client.h"
 
 namespace gale {
@@ -11,12 +13,27 @@ struct PinnedPool::State {
   std::mutex mu;
   std::vector<uint8_t*> free;
   std::vector<uint8_t*> all;
+  std::unordered_map<const uint8_t*, uint8_t*> mirrors;  // pinned chunk -> device mirror
+  int mirror_device = -1;
   size_t chunk = 0, max_bytes = 0;
   bool closed = false;
   ~State() {
     for (uint8_t* p : all) hipHostFree(p);
+    if (mirror_device >= 0 && hipSetDevice(mirror_device) == hipSuccess)
+      for (auto& kv : mirrors) hipFree(kv.second);
   }
 };
+
+void PinnedPool::set_mirror_device(int device) {
+  std::lock_guard<std::mutex> lk(st_->mu);
+  st_->mirror_device = device;
+}
+
+uint8_t* PinnedPool::mirror(const uint8_t* base) const {
+  std::lock_guard<std::mutex> lk(st_->mu);
+  auto it = st_->mirrors.find(base);
+  return it == st_->mirrors.end() ? nullptr : it->second;
+}
 
 PinnedPool::PinnedPool(size_t chunk_bytes, size_t max_bytes)
     : st_(std::make_shared<State>()), chunk_(chunk_bytes) {
@@ -54,6 +71,10 @@ std::shared_ptr<uint8_t> PinnedPool::alloc(size_t n, bool* pinned) {
         if (hipHostMalloc(reinterpret_cast<void**>(&p), st_->chunk, hipHostMallocPortable) ==
             hipSuccess) {
           st_->all.push_back(p);
+          uint8_t* d = nullptr;
+          if (st_->mirror_device >= 0 && hipSetDevice(st_->mirror_device) == hipSuccess &&
+              hipMalloc(reinterpret_cast<void**>(&d), st_->chunk) == hipSuccess)
+            st_->mirrors[p] = d;  // (no mirror: this chunk's records take the host path)
         } else {
           p = nullptr;
         }

@@ -28,6 +28,11 @@ class PinnedPool {
   size_t chunk_bytes() const { return chunk_; }
   bool owns(const uint8_t* p) const;  // p is the base of one of this pool's pinned chunks
   size_t pinned_bytes() const;
+  // Device mirrors (GPU ingest, ingest.h): every pinned chunk gets a same-size buffer on
+  // `device`, at the same offsets. Set before the first alloc. mirror(base) -> nullptr when base
+  // is not a pinned chunk of this pool (or mirrors are off).
+  void set_mirror_device(int device);
+  uint8_t* mirror(const uint8_t* base) const;
 
  private:
   struct State;

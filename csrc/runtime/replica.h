@@ -23,6 +23,8 @@ struct InRecord {
   std::shared_ptr<uint8_t> buf;  // keeps the fetch buffer alive
   const uint8_t* value = nullptr;
   int32_t len = -1;              // -1 = null value
+  const uint8_t* key = nullptr;  // record key (inside buf), key_len -1 = null
+  int32_t key_len = -1;
   int32_t partition = -1;
   int64_t offset = -1;
   int64_t timestamp_ms = -1;     // Kafka record CreateTime
@@ -32,6 +34,9 @@ struct InRecord {
   int32_t status = 0;            // codec::Status (scan, then device parse)
   int32_t source = 0;
   bool pinned = false;           // buf is page-locked: the GPU replica DMAs straight from it
+  // GPU ingest (ingest.h): the value's bytes are already in device memory on dev_device
+  const uint8_t* dev_value = nullptr;
+  int32_t dev_device = -1;
 };
 
 struct Batch {
@@ -80,7 +85,11 @@ class StubReplica : public Replica {
 // with device work (the executor's per-slot graphs, csrc/runtime/executor.cpp).
 class GpuReplica : public Replica {
  public:
-  GpuReplica(std::shared_ptr<Executor> exec, int H, int W, int C, int classes, bool use_graph);
+  // wait_poll_us > 0: wait() polls the batch's completion event and sleeps wait_poll_us between
+  // polls (the worker thread then costs ~no CPU while the GPU works); 0: hipEventSynchronize
+  // (the HIP runtime busy-waits, lowest wake-up latency, one core per waiting replica)
+  GpuReplica(std::shared_ptr<Executor> exec, int H, int W, int C, int classes, bool use_graph,
+             int wait_poll_us = 0);
   ~GpuReplica() override;
   std::string name() const override;
   int max_images() const override { return exec_->max_batch(); }
@@ -111,6 +120,7 @@ class GpuReplica : public Replica {
   std::shared_ptr<Executor> exec_;
   int H_, W_, C_, classes_;
   bool use_graph_;
+  int wait_poll_us_ = 0;
   hipStream_t stream_ = nullptr;       // parse + forward + D2H
   hipStream_t copy_stream_ = nullptr;  // H2D of batch k+1 overlaps compute of batch k
   std::vector<Slot> slots_;

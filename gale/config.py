@@ -22,6 +22,7 @@ CHOICES = {
     "start_offset": ("latest", "earliest", "committed"),
     "value_format": ("json", "json-string"),
     "on_error": ("null", "error-json", "drop"),
+    "output_key": ("none", "input"),
     # compute dtype of the GPU kernels (MFMA bf16 / OCP e4m3 fp8); inputs and the softmax
     # output stay fp32 as in the reference's TF graph (InferenceBolt.java:80-86)
     "dtype": ("bf16", "fp8"),
@@ -45,6 +46,8 @@ class GaleConfig:
     commit_interval_ms: int = 2000
     decode_threads: int = 2            # CRC32C + envelope-scan workers behind each consumer
     check_crcs: bool = True            # Kafka consumer check.crcs
+    gpu_ingest: bool = True            # CRC32C + image counts of pinned fetch buffers on the GPU
+                                       # (the host reads only Kafka framing; csrc/runtime/ingest.h)
     # parallelism (R3)
     workers: int = 8                   # NUM_WORKERS: placement only (one process per GPU here)
     source_parallelism: int = 2        # KAFKA_SPOUT_PARAL
@@ -60,6 +63,7 @@ class GaleConfig:
     type_id_header: bool = False       # add __TypeId__: java.lang.String (spring JsonSerializer)
     linger_ms: int = 0
     on_error: str = "null"             # reference: malformed input -> null record
+    output_key: str = "none"           # reference: unkeyed output (E9); "input" = input's key
     # lifetime (reference: sleep 1 h then kill, MainTopology.java:71-77)
     duration: float = 3600.0
     # model / compute
@@ -72,6 +76,7 @@ class GaleConfig:
     slo_p99_ms: float = 0.0            # latency-SLO mode (config 5): adapt batch/wait to a p99
     queue_depth: int = 8192
     use_graph: bool = True
+    gpu_wait_poll_us: int = 20         # > 0: replicas sleep-poll their batch events (0: spin)
     fold_bn: bool = True               # False: standalone BatchNorm kernels (debug/parity plan)
     stub: bool = False                 # CPU stub replicas (plumbing without a GPU)
     stub_null: bool = False            # stub replicas skip parsing/compute (host-path benchmark)
@@ -125,7 +130,8 @@ class GaleConfig:
             decode_threads=self.decode_threads, check_crcs=self.check_crcs,
             acks=self.acks, sink_mode=self.sink_mode, linger_ms=self.linger_ms,
             value_format=self.value_format, type_id_header=self.type_id_header,
-            on_error=self.on_error, H=H, W=W, C=C, classes=classes, max_batch=self.max_batch,
+            on_error=self.on_error, output_key=self.output_key, H=H, W=W, C=C, classes=classes,
+            max_batch=self.max_batch,
             max_wait_us=self.max_wait_us, slo_p99_ms=self.slo_p99_ms,
             queue_depth=self.queue_depth,
             watchdog_ms=self.watchdog_ms, max_restarts=self.max_restarts,

@@ -50,9 +50,13 @@ class Engine:
         else:
             reps = self._build_gpu_replicas(devices, params)
         for rep in reps:
-            self._native.add_gpu_replica(rep.executor, cfg.use_graph)
+            self._native.add_gpu_replica(rep.executor, cfg.use_graph, cfg.gpu_wait_poll_us)
             self.model_replicas.append(rep)
             self.devices.append(rep.device.index or 0)
+        if cfg.gpu_ingest and len(set(self.devices)) == 1:
+            # one device: fetch buffers are mirrored on it once and parsed in place
+            self._native.enable_gpu_ingest(self.devices[0], max(1, cfg.decode_threads) +
+                                           cfg.source_parallelism, 20)
 
     def _build_gpu_replicas(self, devices: Optional[Sequence[int]], params: Optional[dict]):
         import torch

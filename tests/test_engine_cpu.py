@@ -218,3 +218,21 @@ def test_corrupt_batch_crc_marks_its_records(broker):
     assert sum(b"predictions" in v for v in vals) == 3
     errs = [json.loads(v)["error"] for v in vals if b"predictions" not in v]
     assert errs == ["bad_envelope"] * 3
+
+
+def test_output_key_input_correlates_every_record(broker):
+    """output_key=input: each prediction carries its request's key, so every output is checked
+    against ITS input (the reference's output is unkeyed, which stays the default)."""
+    rng = np.random.default_rng(9)
+    xs = {}
+    for i in range(24):
+        x = rng.random((1 + i % 3, H, W, CH), dtype=np.float32)
+        xs[f"k{i}".encode()] = x
+        broker.append("in", i % 2, [C.encode_instances(x)], [f"k{i}".encode()])
+    eng, out = run(broker, 24, output_key="input")
+    assert len(out) == 24 and {r["key"] for r in out} == set(xs)
+    for r in out:
+        got = np.array(json.loads(r["value"])["predictions"])
+        np.testing.assert_allclose(got, stub_probs(xs[r["key"]]), rtol=1e-5, atol=1e-7)
+    _, out2 = run(broker, 24)  # default: unkeyed (a fresh group reads the topic again)
+    assert all(r["key"] is None for r in out2[-24:])
