@@ -34,6 +34,11 @@ EngineConfig config_from_dict(const py::dict& d) {
   opt(d, "decode_threads", c.decode_threads);
   opt(d, "pinned_fetch_bytes", c.pinned_fetch_bytes);
   opt(d, "commit_interval_ms", c.commit_interval_ms);
+  opt(d, "group_membership", c.group_membership);
+  opt(d, "session_timeout_ms", c.session_timeout_ms);
+  opt(d, "rebalance_timeout_ms", c.rebalance_timeout_ms);
+  opt(d, "heartbeat_interval_ms", c.heartbeat_interval_ms);
+  opt(d, "assignor", c.assignor);
   opt(d, "sink_parallelism", c.sink_parallelism);
   opt(d, "acks", c.acks);
   opt(d, "sink_mode", c.sink_mode);

@@ -335,6 +335,8 @@ void bind_host(py::module_& m) {
     const std::string_view s = view(b);
     return crc32c(reinterpret_cast<const uint8_t*>(s.data()), s.size());
   });
+  k.def("group_assign", &GroupMember::assign, py::arg("assignor"), py::arg("members"),
+        py::arg("partitions"));
   k.def("crc32c_device_tables", [] {
     std::vector<uint32_t> t(kCrcDeviceTableWords);
     crc32c_device_tables(t.data());
@@ -487,6 +489,16 @@ void bind_host(py::module_& m) {
         return py::make_tuple(first, recs);
       }, py::arg("topic"), py::arg("partition"), py::arg("batches"), py::arg("n_batches"),
          py::arg("start") = 0)
+      .def("describe_group", [](Broker& b, const std::string& g) {
+        const GroupInfo gi = b.describe_group(g);
+        py::dict d;
+        d["state"] = gi.state;
+        d["generation"] = gi.generation;
+        d["leader"] = gi.leader;
+        d["protocol"] = gi.protocol;
+        d["members"] = gi.members;
+        return d;
+      })
       .def("log_start", &Broker::log_start)
       .def("log_end", &Broker::log_end)
       .def("committed", &Broker::committed)
@@ -642,7 +654,9 @@ void bind_host(py::module_& m) {
         py::gil_scoped_release nogil;
         return c.committed(p);
       })
-      .def("high_watermarks", &Consumer::high_watermarks);
+      .def("high_watermarks", &Consumer::high_watermarks)
+      .def("set_generation", &Consumer::set_generation, py::arg("generation"),
+           py::arg("member_id"));
 
   py::register_exception<KafkaError>(k, "KafkaError");
   py::register_exception<ProtocolError>(k, "ProtocolError");

@@ -183,6 +183,7 @@ void Broker::start() {
 
 void Broker::stop() {
   if (!running_.exchange(false)) return;
+  coord_.shutdown();  // wakes connection threads blocked in JoinGroup / SyncGroup
   shutdown(listen_fd_, SHUT_RDWR);  // unblocks accept()
   if (thread_.joinable()) thread_.join();
   close(listen_fd_);
@@ -592,7 +593,8 @@ bool Broker::handle_request(Conn& c, const uint8_t* p, size_t n) {
     ApiVersionsResponse resp;
     resp.error = h.api_version == 0 ? NONE : UNSUPPORTED_VERSION;
     for (ApiKey k : {PRODUCE, FETCH, LIST_OFFSETS, METADATA, OFFSET_COMMIT, OFFSET_FETCH,
-                     FIND_COORDINATOR, API_VERSIONS, CREATE_TOPICS})
+                     FIND_COORDINATOR, JOIN_GROUP, HEARTBEAT, LEAVE_GROUP, SYNC_GROUP,
+                     API_VERSIONS, CREATE_TOPICS})
       resp.apis.push_back({(int16_t)k, kVersion(k), kVersion(k)});
     encode_api_versions_response(w, resp);
     frame_into(c.out, w);
@@ -767,13 +769,36 @@ bool Broker::handle_request(Conn& c, const uint8_t* p, size_t n) {
     }
     case OFFSET_COMMIT: {
       OffsetCommitRequest req = decode_offset_commit_request(r);
+      // a member fenced out of its generation (its partitions moved on) must not overwrite the
+      // new owner's progress
+      const int16_t fence = coord_.check_commit(req.group_id, req.generation_id, req.member_id);
       std::lock_guard<std::mutex> lk(mu_);
       for (CommitTopic& t : req.topics)
         for (CommitPartition& cp : t.partitions) {
-          offsets_[offset_key(req.group_id, t.name, cp.index)] = cp.offset;
-          cp.error = NONE;
+          if (fence == NONE) offsets_[offset_key(req.group_id, t.name, cp.index)] = cp.offset;
+          cp.error = fence;
         }
       encode_offset_commit_response(w, req.topics);
+      break;
+    }
+    case JOIN_GROUP: {
+      const JoinGroupRequest req = decode_join_group_request(r);
+      encode_join_group_response(w, coord_.join(req, h.client_id));
+      break;
+    }
+    case SYNC_GROUP: {
+      const SyncGroupRequest req = decode_sync_group_request(r);
+      encode_sync_group_response(w, coord_.sync(req));
+      break;
+    }
+    case HEARTBEAT: {
+      const HeartbeatRequest req = decode_heartbeat_request(r);
+      encode_group_error_response(w, coord_.heartbeat(req));
+      break;
+    }
+    case LEAVE_GROUP: {
+      const LeaveGroupRequest req = decode_leave_group_request(r);
+      encode_group_error_response(w, coord_.leave(req));
       break;
     }
     case OFFSET_FETCH: {

@@ -10,7 +10,8 @@
 //   parallel); in-memory partition logs of RecordBatch v2 segments with byte-based retention;
 //   zero-copy Fetch responses (writev straight from the stored batches).
 // * Long-poll Fetch (max_wait_ms / min_bytes), acks 0/1/-1 Produce, ListOffsets, consumer-group
-//   offset storage (FindCoordinator / OffsetCommit / OffsetFetch), CreateTopics, ApiVersions.
+//   offset storage (FindCoordinator / OffsetCommit / OffsetFetch), group membership (JoinGroup /
+//   SyncGroup / Heartbeat / LeaveGroup, group_coordinator.h), CreateTopics, ApiVersions.
 // * Multi-broker clusters: set_cluster() makes partition p of every topic led by node
 //   nodes[p % n]; Metadata advertises the whole cluster (one broker per GPU rank in bench.py).
 #pragma once
@@ -26,6 +27,7 @@
 #include <thread>
 #include <vector>
 
+#include "group_coordinator.h"
 #include "protocol.h"
 #include "wire.h"
 
@@ -95,6 +97,7 @@ class Broker {
                        int64_t max_bytes) const;
   int64_t committed(const std::string& group, const std::string& topic, int partition) const;
   BrokerStats stats() const;
+  GroupInfo describe_group(const std::string& group) { return coord_.describe(group); }
 
  public:
   struct Chunk;  // one piece of a response (owned bytes or a zero-copy slice of a stored batch)
@@ -149,6 +152,7 @@ class Broker {
   std::map<std::string, int64_t> offsets_;  // "group\0topic\0partition" -> offset
   std::vector<BrokerNode> cluster_;
   BrokerStats stats_;
+  GroupCoordinator coord_;
 };
 
 }  // namespace kafka

@@ -769,6 +769,8 @@ void Consumer::commit(const std::map<int, int64_t>& offsets) {
   drain();  // the coordinator may share a connection with an in-flight fetch
   OffsetCommitRequest req;
   req.group_id = cfg_.group_id;
+  req.generation_id = generation_;
+  req.member_id = member_id_;
   CommitTopic t;
   t.name = topic_;
   for (auto& kv : offsets) {
@@ -784,7 +786,171 @@ void Consumer::commit(const std::map<int, int64_t>& offsets) {
   Reader r(resp);
   for (auto& ct : decode_offset_commit_response(r))
     for (auto& cp : ct.partitions)
-      if (cp.error != NONE) throw KafkaError(cp.error, "OffsetCommit failed");
+      if (cp.error != NONE)
+        throw KafkaError(cp.error, std::string("OffsetCommit failed: ") + error_name(cp.error));
+}
+
+// ---------------------------------------------------------------------------------------------
+// GroupMember
+// ---------------------------------------------------------------------------------------------
+
+GroupMember::GroupMember(GroupConfig cfg) : cfg_(std::move(cfg)), cluster_(cfg_) {
+  if (cfg_.group_id.empty() || cfg_.topic.empty())
+    throw std::invalid_argument("GroupMember needs a group_id and a topic");
+  if (cfg_.assignor != "range" && cfg_.assignor != "roundrobin")
+    throw std::invalid_argument("assignor must be range|roundrobin");
+  // JoinGroup blocks for up to the rebalance timeout: the socket timeout must outlast it
+  ClientConfig cc = cfg_;
+  cc.request_timeout_ms = std::max(cfg_.request_timeout_ms, cfg_.rebalance_timeout_ms + 5000);
+  cluster_ = Cluster(cc);
+}
+
+GroupMember::~GroupMember() {
+  try {
+    leave();
+  } catch (...) {
+  }
+}
+
+std::map<std::string, std::vector<int>> GroupMember::assign(const std::string& assignor,
+                                                            std::vector<std::string> members,
+                                                            int n) {
+  std::sort(members.begin(), members.end());
+  std::map<std::string, std::vector<int>> out;
+  for (const auto& m : members) out[m];
+  if (members.empty()) return out;
+  const int k = (int)members.size();
+  if (assignor == "roundrobin") {
+    for (int p = 0; p < n; ++p) out[members[(size_t)(p % k)]].push_back(p);
+  } else {  // range: contiguous blocks, the first n % k members take one extra
+    int p = 0;
+    for (int i = 0; i < k; ++i) {
+      const int cnt = n / k + (i < n % k ? 1 : 0);
+      for (int j = 0; j < cnt; ++j) out[members[(size_t)i]].push_back(p++);
+    }
+  }
+  return out;
+}
+
+std::vector<int> GroupMember::join() {
+  for (int attempt = 0;; ++attempt) {
+    if (attempt > 50) throw KafkaError(REBALANCE_IN_PROGRESS, "group join did not converge");
+    JoinGroupRequest jr;
+    jr.group_id = cfg_.group_id;
+    jr.session_timeout_ms = cfg_.session_timeout_ms;
+    jr.rebalance_timeout_ms = cfg_.rebalance_timeout_ms;
+    jr.member_id = member_id_;
+    ConsumerSubscription sub;
+    sub.topics = {cfg_.topic};
+    jr.protocols.push_back({cfg_.assignor, encode_subscription(sub)});
+    Writer w;
+    encode_join_group_request(w, jr);
+    JoinGroupResponse resp;
+    try {
+      const std::string raw = cluster_.coordinator(cfg_.group_id).request(JOIN_GROUP, w);
+      Reader r(raw);
+      resp = decode_join_group_response(r);
+    } catch (const KafkaError& e) {
+      if (e.code != -1 && e.code != REQUEST_TIMED_OUT) throw;
+      cluster_ = Cluster(cluster_.config());  // reconnect (the exchange may be half done)
+      usleep(100000);
+      continue;
+    }
+    if (resp.error == UNKNOWN_MEMBER_ID) {
+      member_id_.clear();  // fenced: rejoin as a new member
+      continue;
+    }
+    if (resp.error == REBALANCE_IN_PROGRESS) continue;
+    if (resp.error != NONE)
+      throw KafkaError(resp.error, std::string("JoinGroup: ") + error_name(resp.error));
+    member_id_ = resp.member_id;
+    generation_ = resp.generation_id;
+    leader_ = resp.leader_id == resp.member_id;
+    SyncGroupRequest sr;
+    sr.group_id = cfg_.group_id;
+    sr.generation_id = generation_;
+    sr.member_id = member_id_;
+    if (leader_) {
+      std::vector<std::string> subscribed;
+      for (const GroupMemberMeta& m : resp.members) {
+        const ConsumerSubscription s = decode_subscription(m.metadata);
+        if (std::find(s.topics.begin(), s.topics.end(), cfg_.topic) != s.topics.end())
+          subscribed.push_back(m.member_id);
+      }
+      cluster_.invalidate();  // the partition count may have grown
+      const int n = std::max(0, cluster_.partitions(cfg_.topic));
+      for (auto& kv : assign(resp.protocol, subscribed, n)) {
+        ConsumerAssignment a;
+        a.partitions.push_back({cfg_.topic, std::vector<int32_t>(kv.second.begin(),
+                                                                 kv.second.end())});
+        sr.assignments.push_back({kv.first, encode_assignment(a)});
+      }
+      for (const GroupMemberMeta& m : resp.members)  // members not on this topic: nothing
+        if (std::find(subscribed.begin(), subscribed.end(), m.member_id) == subscribed.end())
+          sr.assignments.push_back({m.member_id, encode_assignment(ConsumerAssignment())});
+    }
+    Writer w2;
+    encode_sync_group_request(w2, sr);
+    SyncGroupResponse sresp;
+    try {
+      const std::string raw = cluster_.coordinator(cfg_.group_id).request(SYNC_GROUP, w2);
+      Reader r(raw);
+      sresp = decode_sync_group_response(r);
+    } catch (const KafkaError& e) {
+      if (e.code != -1 && e.code != REQUEST_TIMED_OUT) throw;
+      cluster_ = Cluster(cluster_.config());
+      continue;
+    }
+    if (sresp.error == UNKNOWN_MEMBER_ID) {
+      member_id_.clear();
+      continue;
+    }
+    if (sresp.error == REBALANCE_IN_PROGRESS || sresp.error == ILLEGAL_GENERATION) continue;
+    if (sresp.error != NONE)
+      throw KafkaError(sresp.error, std::string("SyncGroup: ") + error_name(sresp.error));
+    std::vector<int> mine;
+    for (const auto& tp : decode_assignment(sresp.assignment).partitions)
+      if (tp.first == cfg_.topic) mine.insert(mine.end(), tp.second.begin(), tp.second.end());
+    std::sort(mine.begin(), mine.end());
+    return mine;
+  }
+}
+
+bool GroupMember::heartbeat() {
+  if (member_id_.empty()) return false;
+  HeartbeatRequest hr;
+  hr.group_id = cfg_.group_id;
+  hr.generation_id = generation_;
+  hr.member_id = member_id_;
+  Writer w;
+  encode_heartbeat_request(w, hr);
+  int16_t err;
+  try {
+    const std::string raw = cluster_.coordinator(cfg_.group_id).request(HEARTBEAT, w);
+    Reader r(raw);
+    err = decode_group_error_response(r);
+  } catch (const KafkaError& e) {
+    if (e.code != -1 && e.code != REQUEST_TIMED_OUT) throw;
+    cluster_ = Cluster(cluster_.config());
+    return true;  // transient: the session outlives one missed heartbeat
+  }
+  if (err == UNKNOWN_MEMBER_ID) member_id_.clear();
+  if (err == NONE) return true;
+  if (err == REBALANCE_IN_PROGRESS || err == ILLEGAL_GENERATION || err == UNKNOWN_MEMBER_ID)
+    return false;
+  throw KafkaError(err, std::string("Heartbeat: ") + error_name(err));
+}
+
+void GroupMember::leave() {
+  if (member_id_.empty()) return;
+  LeaveGroupRequest lr;
+  lr.group_id = cfg_.group_id;
+  lr.member_id = member_id_;
+  member_id_.clear();
+  generation_ = -1;
+  Writer w;
+  encode_leave_group_request(w, lr);
+  cluster_.coordinator(cfg_.group_id).request(LEAVE_GROUP, w);
 }
 
 int64_t Consumer::committed(int partition) {

@@ -214,6 +214,11 @@ class Consumer {
   // within max_wait_ms. With prefetch the next round is already requested when this returns.
   std::vector<Fetched> poll();
   void commit(const std::map<int, int64_t>& offsets);  // next offset to read, per partition
+  // group-managed consumers commit under their generation (fenced by the coordinator)
+  void set_generation(int32_t generation, const std::string& member_id) {
+    generation_ = generation;
+    member_id_ = member_id;
+  }
   int64_t committed(int partition);
   std::map<int, int64_t> high_watermarks() const { return hw_; }
   Cluster& cluster() { return cluster_; }
@@ -236,6 +241,47 @@ class Consumer {
   std::map<int, int64_t> pos_, hw_;
   std::vector<InFlight> inflight_;
   std::vector<Fetched> ready_;  // drained responses not yet returned by poll()
+  int32_t generation_ = -1;
+  std::string member_id_;
+};
+
+// Consumer-group membership (Kafka's eager rebalance protocol): JoinGroup -> (leader computes
+// the assignment with the chosen assignor) -> SyncGroup -> periodic Heartbeat; LeaveGroup on
+// close. The elastic replacement of the reference's static spout/partition split (E1, E4): a
+// member that dies stops heartbeating, the coordinator rebalances and the survivors adopt its
+// partitions. One topic per group (the engine's input topic).
+struct GroupConfig : ClientConfig {
+  std::string group_id;
+  std::string topic;
+  int session_timeout_ms = 6000;
+  int rebalance_timeout_ms = 8000;
+  std::string assignor = "range";  // range | roundrobin
+};
+
+class GroupMember {
+ public:
+  explicit GroupMember(GroupConfig cfg);
+  ~GroupMember();
+  GroupMember(const GroupMember&) = delete;
+  GroupMember& operator=(const GroupMember&) = delete;
+  // (Re)join: blocks through the rebalance; returns this member's partitions of cfg.topic.
+  std::vector<int> join();
+  // false: the group is rebalancing or this member was fenced -> revoke, then join() again
+  bool heartbeat();
+  void leave();
+  int32_t generation() const { return generation_; }
+  const std::string& member_id() const { return member_id_; }
+  bool is_leader() const { return leader_; }
+  // The assignors, exposed for tests: member -> partitions of one topic with n partitions
+  static std::map<std::string, std::vector<int>> assign(const std::string& assignor,
+                                                        std::vector<std::string> members, int n);
+
+ private:
+  GroupConfig cfg_;
+  Cluster cluster_;
+  std::string member_id_;
+  int32_t generation_ = -1;
+  bool leader_ = false;
 };
 
 }  // namespace kafka

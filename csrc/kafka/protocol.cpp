@@ -20,6 +20,11 @@ const char* error_name(int code) {
     case INVALID_TOPIC_EXCEPTION: return "INVALID_TOPIC_EXCEPTION";
     case RECORD_LIST_TOO_LARGE: return "RECORD_LIST_TOO_LARGE";
     case INVALID_REQUIRED_ACKS: return "INVALID_REQUIRED_ACKS";
+    case ILLEGAL_GENERATION: return "ILLEGAL_GENERATION";
+    case INCONSISTENT_GROUP_PROTOCOL: return "INCONSISTENT_GROUP_PROTOCOL";
+    case UNKNOWN_MEMBER_ID: return "UNKNOWN_MEMBER_ID";
+    case INVALID_SESSION_TIMEOUT: return "INVALID_SESSION_TIMEOUT";
+    case REBALANCE_IN_PROGRESS: return "REBALANCE_IN_PROGRESS";
     case UNSUPPORTED_VERSION: return "UNSUPPORTED_VERSION";
     case TOPIC_ALREADY_EXISTS: return "TOPIC_ALREADY_EXISTS";
     case INVALID_PARTITIONS: return "INVALID_PARTITIONS";
@@ -372,6 +377,181 @@ FindCoordinatorResponse decode_find_coordinator_response(Reader& r) {
   m.node.node_id = r.i32();
   m.node.host = r.str();
   m.node.port = r.i32();
+  return m;
+}
+
+// ---- JoinGroup v2 ----
+void encode_join_group_request(Writer& w, const JoinGroupRequest& m) {
+  w.str(m.group_id);
+  w.i32(m.session_timeout_ms);
+  w.i32(m.rebalance_timeout_ms);
+  w.str(m.member_id);
+  w.str(m.protocol_type);
+  put_array(w, m.protocols, [&](const GroupProtocol& p) {
+    w.str(p.name);
+    w.bytes(p.metadata);
+  });
+}
+JoinGroupRequest decode_join_group_request(Reader& r) {
+  JoinGroupRequest m;
+  m.group_id = r.str();
+  m.session_timeout_ms = r.i32();
+  m.rebalance_timeout_ms = r.i32();
+  m.member_id = r.str();
+  m.protocol_type = r.str();
+  m.protocols = get_array<GroupProtocol>(r, [&] {
+    GroupProtocol p;
+    p.name = r.str();
+    const auto b = r.bytes_ref();
+    if (b.second > 0) p.metadata.assign(reinterpret_cast<const char*>(r.base() + b.first),
+                                        (size_t)b.second);
+    return p;
+  });
+  return m;
+}
+void encode_join_group_response(Writer& w, const JoinGroupResponse& m) {
+  w.i32(m.throttle_ms);
+  w.i16(m.error);
+  w.i32(m.generation_id);
+  w.str(m.protocol);
+  w.str(m.leader_id);
+  w.str(m.member_id);
+  put_array(w, m.members, [&](const GroupMemberMeta& x) {
+    w.str(x.member_id);
+    w.bytes(x.metadata);
+  });
+}
+namespace {
+GroupMemberMeta get_member_meta(Reader& r) {
+  GroupMemberMeta x;
+  x.member_id = r.str();
+  const auto b = r.bytes_ref();
+  if (b.second > 0) x.metadata.assign(reinterpret_cast<const char*>(r.base() + b.first),
+                                      (size_t)b.second);
+  return x;
+}
+}  // namespace
+JoinGroupResponse decode_join_group_response(Reader& r) {
+  JoinGroupResponse m;
+  m.throttle_ms = r.i32();
+  m.error = r.i16();
+  m.generation_id = r.i32();
+  m.protocol = r.str();
+  m.leader_id = r.str();
+  m.member_id = r.str();
+  m.members = get_array<GroupMemberMeta>(r, [&] { return get_member_meta(r); });
+  return m;
+}
+
+// ---- SyncGroup v1 ----
+void encode_sync_group_request(Writer& w, const SyncGroupRequest& m) {
+  w.str(m.group_id);
+  w.i32(m.generation_id);
+  w.str(m.member_id);
+  put_array(w, m.assignments, [&](const GroupMemberMeta& x) {
+    w.str(x.member_id);
+    w.bytes(x.metadata);
+  });
+}
+SyncGroupRequest decode_sync_group_request(Reader& r) {
+  SyncGroupRequest m;
+  m.group_id = r.str();
+  m.generation_id = r.i32();
+  m.member_id = r.str();
+  m.assignments = get_array<GroupMemberMeta>(r, [&] { return get_member_meta(r); });
+  return m;
+}
+void encode_sync_group_response(Writer& w, const SyncGroupResponse& m) {
+  w.i32(m.throttle_ms);
+  w.i16(m.error);
+  w.bytes(m.assignment);
+}
+SyncGroupResponse decode_sync_group_response(Reader& r) {
+  SyncGroupResponse m;
+  m.throttle_ms = r.i32();
+  m.error = r.i16();
+  const auto b = r.bytes_ref();
+  if (b.second > 0) m.assignment.assign(reinterpret_cast<const char*>(r.base() + b.first),
+                                        (size_t)b.second);
+  return m;
+}
+
+// ---- Heartbeat v1 / LeaveGroup v1 ----
+void encode_heartbeat_request(Writer& w, const HeartbeatRequest& m) {
+  w.str(m.group_id);
+  w.i32(m.generation_id);
+  w.str(m.member_id);
+}
+HeartbeatRequest decode_heartbeat_request(Reader& r) {
+  HeartbeatRequest m;
+  m.group_id = r.str();
+  m.generation_id = r.i32();
+  m.member_id = r.str();
+  return m;
+}
+void encode_leave_group_request(Writer& w, const LeaveGroupRequest& m) {
+  w.str(m.group_id);
+  w.str(m.member_id);
+}
+LeaveGroupRequest decode_leave_group_request(Reader& r) {
+  LeaveGroupRequest m;
+  m.group_id = r.str();
+  m.member_id = r.str();
+  return m;
+}
+void encode_group_error_response(Writer& w, int16_t error) {
+  w.i32(0);
+  w.i16(error);
+}
+int16_t decode_group_error_response(Reader& r) {
+  r.i32();
+  return r.i16();
+}
+
+// ---- ConsumerProtocol v0 (Subscription / Assignment) ----
+std::string encode_subscription(const ConsumerSubscription& m) {
+  Writer w;
+  w.i16(0);
+  put_array(w, m.topics, [&](const std::string& t) { w.str(t); });
+  w.bytes(m.user_data);
+  return w.buf;
+}
+ConsumerSubscription decode_subscription(const std::string& b) {
+  Reader r(b);
+  ConsumerSubscription m;
+  r.i16();  // version (later versions only append fields)
+  m.topics = get_array<std::string>(r, [&] { return r.str(); });
+  if (r.remaining() >= 4) {
+    const auto u = r.bytes_ref();
+    if (u.second > 0) m.user_data = b.substr(u.first, (size_t)u.second);
+  }
+  return m;
+}
+std::string encode_assignment(const ConsumerAssignment& m) {
+  Writer w;
+  w.i16(0);
+  put_array(w, m.partitions, [&](const std::pair<std::string, std::vector<int32_t>>& tp) {
+    w.str(tp.first);
+    put_array(w, tp.second, [&](int32_t p) { w.i32(p); });
+  });
+  w.bytes(m.user_data);
+  return w.buf;
+}
+ConsumerAssignment decode_assignment(const std::string& b) {
+  ConsumerAssignment m;
+  if (b.empty()) return m;  // no partitions for this member
+  Reader r(b);
+  r.i16();
+  m.partitions = get_array<std::pair<std::string, std::vector<int32_t>>>(r, [&] {
+    std::pair<std::string, std::vector<int32_t>> tp;
+    tp.first = r.str();
+    tp.second = get_array<int32_t>(r, [&] { return r.i32(); });
+    return tp;
+  });
+  if (r.remaining() >= 4) {
+    const auto u = r.bytes_ref();
+    if (u.second > 0) m.user_data = b.substr(u.first, (size_t)u.second);
+  }
   return m;
 }
 

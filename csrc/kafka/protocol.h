@@ -3,12 +3,16 @@
 // One (non-flexible) version per API, chosen to be accepted by Kafka 2.x through 4.x brokers
 // (KIP-896 removed only older versions):
 //   ApiVersions v0, Metadata v4, Produce v3, Fetch v4, ListOffsets v1, FindCoordinator v1,
-//   OffsetCommit v2, OffsetFetch v1, CreateTopics v2.
+//   OffsetCommit v2, OffsetFetch v1, CreateTopics v2, and the consumer-group membership APIs
+//   JoinGroup v2, SyncGroup v1, Heartbeat v1, LeaveGroup v1 (with the "consumer" embedded
+//   protocol's Subscription / Assignment v0 encodings).
 // The client checks them against the broker's ApiVersions answer before use.
 //
 // Reference mapping: Metadata/Fetch/ListOffsets = KafkaSpout partition
 // discovery and reads (E1, MainTopology.java:95-106); OffsetCommit/OffsetFetch = the spout's ZK
-// offset commits (X3); Produce = KafkaProducer.send (E7, KafkaBolt.java:144).
+// offset commits (X3); Produce = KafkaProducer.send (E7, KafkaBolt.java:144). The group APIs
+// replace Storm's supervisor/rebalance machinery for consumers (E4): members of
+// one group share the input partitions and a dead member's partitions move to the survivors.
 #pragma once
 #include <stdint.h>
 
@@ -28,6 +32,10 @@ enum ApiKey : int16_t {
   OFFSET_COMMIT = 8,
   OFFSET_FETCH = 9,
   FIND_COORDINATOR = 10,
+  JOIN_GROUP = 11,
+  HEARTBEAT = 12,
+  LEAVE_GROUP = 13,
+  SYNC_GROUP = 14,
   API_VERSIONS = 18,
   CREATE_TOPICS = 19,
 };
@@ -35,7 +43,8 @@ enum ApiKey : int16_t {
 constexpr int16_t kVersion(ApiKey k) {
   return k == PRODUCE ? 3 : k == FETCH ? 4 : k == LIST_OFFSETS ? 1 : k == METADATA ? 4
        : k == OFFSET_COMMIT ? 2 : k == OFFSET_FETCH ? 1 : k == FIND_COORDINATOR ? 1
-       : k == API_VERSIONS ? 0 : k == CREATE_TOPICS ? 2 : -1;
+       : k == API_VERSIONS ? 0 : k == CREATE_TOPICS ? 2 : k == JOIN_GROUP ? 2
+       : k == HEARTBEAT ? 1 : k == LEAVE_GROUP ? 1 : k == SYNC_GROUP ? 1 : -1;
 }
 
 enum ErrorCode : int16_t {
@@ -53,6 +62,11 @@ enum ErrorCode : int16_t {
   INVALID_TOPIC_EXCEPTION = 17,
   RECORD_LIST_TOO_LARGE = 18,
   INVALID_REQUIRED_ACKS = 21,
+  ILLEGAL_GENERATION = 22,
+  INCONSISTENT_GROUP_PROTOCOL = 23,
+  UNKNOWN_MEMBER_ID = 25,
+  INVALID_SESSION_TIMEOUT = 26,
+  REBALANCE_IN_PROGRESS = 27,
   UNSUPPORTED_VERSION = 35,
   TOPIC_ALREADY_EXISTS = 36,
   INVALID_PARTITIONS = 37,
@@ -272,6 +286,84 @@ void encode_offset_fetch_request(Writer& w, const OffsetFetchRequest& m);
 OffsetFetchRequest decode_offset_fetch_request(Reader& r);
 void encode_offset_fetch_response(Writer& w, const std::vector<CommitTopic>& topics);
 std::vector<CommitTopic> decode_offset_fetch_response(Reader& r);
+
+// ---- group membership: JoinGroup v2 / SyncGroup v1 / Heartbeat v1 / LeaveGroup v1 ----
+struct GroupProtocol {
+  std::string name;      // assignor ("range", "roundrobin")
+  std::string metadata;  // consumer Subscription
+};
+struct JoinGroupRequest {
+  std::string group_id;
+  int32_t session_timeout_ms = 10000;
+  int32_t rebalance_timeout_ms = 30000;
+  std::string member_id;  // empty on the first join
+  std::string protocol_type = "consumer";
+  std::vector<GroupProtocol> protocols;
+};
+struct GroupMemberMeta {
+  std::string member_id;
+  std::string metadata;
+};
+struct JoinGroupResponse {
+  int32_t throttle_ms = 0;
+  int16_t error = 0;
+  int32_t generation_id = -1;
+  std::string protocol;  // the chosen assignor
+  std::string leader_id;
+  std::string member_id;
+  std::vector<GroupMemberMeta> members;  // leader only
+};
+void encode_join_group_request(Writer& w, const JoinGroupRequest& m);
+JoinGroupRequest decode_join_group_request(Reader& r);
+void encode_join_group_response(Writer& w, const JoinGroupResponse& m);
+JoinGroupResponse decode_join_group_response(Reader& r);
+
+struct SyncGroupRequest {
+  std::string group_id;
+  int32_t generation_id = -1;
+  std::string member_id;
+  std::vector<GroupMemberMeta> assignments;  // leader only: member -> Assignment bytes
+};
+struct SyncGroupResponse {
+  int32_t throttle_ms = 0;
+  int16_t error = 0;
+  std::string assignment;
+};
+void encode_sync_group_request(Writer& w, const SyncGroupRequest& m);
+SyncGroupRequest decode_sync_group_request(Reader& r);
+void encode_sync_group_response(Writer& w, const SyncGroupResponse& m);
+SyncGroupResponse decode_sync_group_response(Reader& r);
+
+struct HeartbeatRequest {
+  std::string group_id;
+  int32_t generation_id = -1;
+  std::string member_id;
+};
+void encode_heartbeat_request(Writer& w, const HeartbeatRequest& m);
+HeartbeatRequest decode_heartbeat_request(Reader& r);
+struct LeaveGroupRequest {
+  std::string group_id;
+  std::string member_id;
+};
+void encode_leave_group_request(Writer& w, const LeaveGroupRequest& m);
+LeaveGroupRequest decode_leave_group_request(Reader& r);
+// Heartbeat v1 / LeaveGroup v1 responses: throttle_time_ms, error_code
+void encode_group_error_response(Writer& w, int16_t error);
+int16_t decode_group_error_response(Reader& r);
+
+// "consumer" embedded protocol (Kafka's ConsumerProtocol v0)
+struct ConsumerSubscription {
+  std::vector<std::string> topics;
+  std::string user_data;
+};
+struct ConsumerAssignment {
+  std::vector<std::pair<std::string, std::vector<int32_t>>> partitions;
+  std::string user_data;
+};
+std::string encode_subscription(const ConsumerSubscription& m);
+ConsumerSubscription decode_subscription(const std::string& b);
+std::string encode_assignment(const ConsumerAssignment& m);
+ConsumerAssignment decode_assignment(const std::string& b);
 
 // ---- CreateTopics v2 ----
 struct CreateTopic {

@@ -195,18 +195,28 @@ void Engine::start() {
     pc.batch_size = cfg_.batch_size;
     producers_.push_back(std::make_unique<kafka::Producer>(pc));
   }
-  // resolve the input partitions and split them over the source threads
+  // static mode: resolve the input partitions and split them over the source threads now;
+  // group mode: the sources start idle and the group thread hands them the assignment
   std::vector<int> parts = cfg_.partitions;
-  if (parts.empty()) {
-    kafka::Cluster cl(kafka::ClientConfig{cfg_.bootstrap, cfg_.client_id, 30000, 10000});
-    const int n = cl.partitions(cfg_.input_topic);
-    if (n <= 0) throw kafka::KafkaError(kafka::UNKNOWN_TOPIC_OR_PARTITION,
-                                        "input topic " + cfg_.input_topic + " not found");
-    for (int p = 0; p < n; ++p) parts.push_back(p);
+  int ns = cfg_.source_parallelism;
+  if (!cfg_.group_membership) {
+    if (parts.empty()) {
+      kafka::Cluster cl(kafka::ClientConfig{cfg_.bootstrap, cfg_.client_id, 30000, 10000});
+      const int n = cl.partitions(cfg_.input_topic);
+      if (n <= 0) throw kafka::KafkaError(kafka::UNKNOWN_TOPIC_OR_PARTITION,
+                                          "input topic " + cfg_.input_topic + " not found");
+      for (int p = 0; p < n; ++p) parts.push_back(p);
+    }
+    ns = std::min<int>(cfg_.source_parallelism, (int)parts.size());
+  } else if (cfg_.group_id.empty()) {
+    throw std::invalid_argument("engine: group_membership needs a group_id");
   }
-  const int ns = std::min<int>(cfg_.source_parallelism, (int)parts.size());
-  std::vector<std::vector<int>> split((size_t)ns);
-  for (size_t i = 0; i < parts.size(); ++i) split[i % (size_t)ns].push_back(parts[i]);
+  src_ctl_.clear();
+  for (int i = 0; i < ns; ++i) src_ctl_.push_back(std::make_unique<SourceCtl>());
+  if (!cfg_.group_membership) {
+    for (size_t i = 0; i < parts.size(); ++i) src_ctl_[i % (size_t)ns]->parts.push_back(parts[i]);
+    for (auto& c : src_ctl_) c->epoch = 1;
+  }
   bool any_gpu = false;
   for (auto& rs : replicas_) any_gpu |= rs->rep->device() >= 0;
   if ((any_gpu || ingest_) && cfg_.pinned_fetch_bytes > 0 && !pinned_) {
@@ -232,9 +242,15 @@ void Engine::start() {
       worker_loop(rs.get());
     });
   for (int i = 0; i < ns; ++i)
-    sources_.emplace_back([this, i, p = split[(size_t)i]] {
+    sources_.emplace_back([this, i] {
       name_thread("gl-src", i);
-      source_loop(i, p);
+      source_loop(i);
+    });
+  group_stop_ = false;
+  if (cfg_.group_membership)
+    group_thread_ = std::thread([this] {
+      name_thread("gl-group");
+      group_loop();
     });
   watchdog_ = std::thread([this] {
     name_thread("gl-watchdog");
@@ -277,6 +293,8 @@ void Engine::stop() {
   done_cv_.notify_all();
   for (auto& t : sources_) t.join();
   sources_.clear();
+  group_stop_ = true;  // (after the sources' final commits: then leave the group)
+  if (group_thread_.joinable()) group_thread_.join();
   running_ = false;
   done_cv_.notify_all();
   if (watchdog_.joinable()) watchdog_.join();
@@ -318,7 +336,92 @@ void Engine::commit(kafka::Consumer& c, const std::vector<int>& parts) {
   }
 }
 
-void Engine::source_loop(int idx, std::vector<int> parts) {
+// Hands the sources a new partition set (group thread) and waits until each has taken it
+// (committed and dropped its previous partitions). false = not every source confirmed in time.
+bool Engine::distribute(const std::vector<int>& parts, int32_t generation,
+                        const std::string& member, int timeout_ms) {
+  const size_t ns = src_ctl_.size();
+  std::vector<uint64_t> want(ns);
+  for (size_t i = 0; i < ns; ++i) {
+    SourceCtl& c = *src_ctl_[i];
+    std::lock_guard<std::mutex> lk(c.mu);
+    c.parts.clear();
+    for (size_t k = i; k < parts.size(); k += ns) c.parts.push_back(parts[k]);
+    c.generation = generation;
+    c.member = member;
+    want[i] = ++c.epoch;
+  }
+  const int64_t until = mono_ns() + (int64_t)timeout_ms * 1000000;
+  bool ok = true;
+  for (size_t i = 0; i < ns; ++i) {
+    SourceCtl& c = *src_ctl_[i];
+    std::unique_lock<std::mutex> lk(c.mu);
+    while (c.acked < want[i] && !stopping_ && mono_ns() < until)
+      c.cv.wait_for(lk, std::chrono::milliseconds(10));
+    ok &= c.acked >= want[i];
+  }
+  return ok;
+}
+
+// Consumer-group membership (group_membership): join, give the assignment to the sources,
+// heartbeat; on a rebalance revoke everything (the sources commit first), rejoin, repeat.
+void Engine::group_loop() {
+  kafka::GroupConfig gc;
+  gc.bootstrap = cfg_.bootstrap;
+  gc.client_id = cfg_.client_id + "-group";
+  gc.group_id = cfg_.group_id;
+  gc.topic = cfg_.input_topic;
+  gc.session_timeout_ms = cfg_.session_timeout_ms;
+  gc.rebalance_timeout_ms = cfg_.rebalance_timeout_ms;
+  gc.assignor = cfg_.assignor;
+  std::unique_ptr<kafka::GroupMember> gm;
+  while (!group_stop_) {
+    try {
+      if (!gm) gm = std::make_unique<kafka::GroupMember>(gc);
+      if (stopping_) {  // draining: keep the session alive until the final commits are done
+        gm->heartbeat();
+        std::this_thread::sleep_for(std::chrono::milliseconds(cfg_.heartbeat_interval_ms));
+        continue;
+      }
+      const std::vector<int> mine = gm->join();
+      distribute(mine, gm->generation(), gm->member_id(), cfg_.rebalance_timeout_ms);
+      generation_ = gm->generation();
+      assigned_partitions_ = (int)mine.size();
+      ++rebalances_;
+      fprintf(stderr, "[gale group] %s generation %d: %zu partition(s)%s\n",
+              gm->member_id().c_str(), gm->generation(), mine.size(),
+              gm->is_leader() ? " (leader)" : "");
+      for (;;) {
+        const int64_t next = mono_ns() + (int64_t)cfg_.heartbeat_interval_ms * 1000000;
+        while (!group_stop_ && !stopping_ && mono_ns() < next)
+          std::this_thread::sleep_for(std::chrono::milliseconds(5));
+        if (group_stop_) break;
+        if (!gm->heartbeat()) {
+          if (stopping_) continue;
+          // eager rebalance: every partition is revoked (and committed) before rejoining
+          distribute({}, gm->generation(), gm->member_id(), cfg_.rebalance_timeout_ms / 2);
+          assigned_partitions_ = 0;
+          break;
+        }
+        if (stopping_) continue;
+      }
+    } catch (const std::exception& e) {
+      fprintf(stderr, "[gale group] %s: retrying\n", e.what());
+      gm.reset();
+      for (int i = 0; i < 50 && !group_stop_; ++i)
+        std::this_thread::sleep_for(std::chrono::milliseconds(10));
+    }
+  }
+  if (gm) {
+    try {
+      gm->leave();
+    } catch (const std::exception&) {
+    }
+  }
+}
+
+void Engine::source_loop(int idx) {
+  SourceCtl& ctl = *src_ctl_[(size_t)idx];
   kafka::ConsumerConfig cc;
   cc.bootstrap = cfg_.bootstrap;
   cc.client_id = cfg_.client_id + "-source-" + std::to_string(idx);
@@ -340,17 +443,65 @@ void Engine::source_loop(int idx, std::vector<int> parts) {
   std::unique_ptr<kafka::Consumer> cons;
   try {
     cons = std::make_unique<kafka::Consumer>(cc, alloc);
-    cons->assign(cfg_.input_topic, parts);
-    cons->seek_to(cfg_.start_offset);
-    std::lock_guard<std::mutex> lk(pend_mu_);
-    for (int p : parts) next_fetch_[p] = cons->position(p);
   } catch (const std::exception& e) {
     fprintf(stderr, "[gale source %d] failed to start: %s\n", idx, e.what());
-    cons.reset();
   }
+  std::vector<int> parts;
+  uint64_t epoch = 0;
+  // (re)assignment: commit and forget the old partitions, seek the new ones. Group-managed
+  // partitions resume from the group's committed offsets (that is how a survivor takes over a
+  // dead member's partitions); static ones from start_offset.
+  auto reassign = [&]() {
+    std::vector<int> want;
+    int32_t gen;
+    std::string member;
+    uint64_t e;
+    {
+      std::lock_guard<std::mutex> lk(ctl.mu);
+      if (ctl.epoch == epoch) return;
+      want = ctl.parts;
+      gen = ctl.generation;
+      member = ctl.member;
+      e = ctl.epoch;
+    }
+    if (!parts.empty()) {
+      commit(*cons, parts);
+      std::lock_guard<std::mutex> lk(pend_mu_);
+      for (int p : parts) {
+        next_fetch_.erase(p);
+        high_watermark_.erase(p);
+      }
+    }
+    parts = want;
+    cons->set_generation(gen, member);
+    if (!parts.empty()) {
+      cons->assign(cfg_.input_topic, parts);
+      cons->seek_to(cfg_.group_membership ? "committed" : cfg_.start_offset);
+      std::lock_guard<std::mutex> lk(pend_mu_);
+      for (int p : parts) next_fetch_[p] = cons->position(p);
+    }
+    epoch = e;
+    {
+      std::lock_guard<std::mutex> lk(ctl.mu);
+      ctl.acked = e;
+    }
+    ctl.cv.notify_all();
+  };
   int64_t last_commit = mono_ns();
   std::vector<InRecord> good;
   while (cons && !stopping_) {
+    try {
+      reassign();
+    } catch (const std::exception& e) {
+      fprintf(stderr, "[gale source %d] assignment failed: %s\n", idx, e.what());
+      std::this_thread::sleep_for(std::chrono::milliseconds(100));
+      continue;
+    }
+    if (parts.empty()) {  // idle until the group assigns this source something
+      std::unique_lock<std::mutex> lk(ctl.mu);
+      ctl.cv.wait_for(lk, std::chrono::milliseconds(20));
+      continue;
+    }
     std::vector<kafka::Fetched> fs;
     try {
       const int64_t t0 = mono_ns();
@@ -369,7 +520,9 @@ void Engine::source_loop(int idx, std::vector<int> parts) {
       for (auto& f : fs)
         for (const kafka::RecordRef& rr : f.records) pending_[rr.partition][rr.offset] = 1;
       for (int p : parts) next_fetch_[p] = cons->position(p);
-      for (const auto& kv : cons->high_watermarks()) high_watermark_[kv.first] = kv.second;
+      for (const auto& kv : cons->high_watermarks())
+        if (std::find(parts.begin(), parts.end(), kv.first) != parts.end())
+          high_watermark_[kv.first] = kv.second;
     }
     if (!fs.empty()) {
       int64_t z = 0;
@@ -410,7 +563,7 @@ void Engine::source_loop(int idx, std::vector<int> parts) {
     std::unique_lock<std::mutex> lk(done_mu_);
     done_cv_.wait_for(lk, std::chrono::seconds(60), [&] { return sources_done_.load(); });
     lk.unlock();
-    commit(*cons, parts);
+    if (!parts.empty()) commit(*cons, parts);
   }
 }
 
@@ -944,6 +1097,10 @@ std::map<std::string, double> Engine::stats() const {
   int alive = 0;
   for (auto& r : replicas_) alive += r->alive ? 1 : 0;
   s["replicas_alive"] = alive;
+  s["rebalances"] = (double)rebalances_;
+  s["generation"] = (double)generation_;
+  s["assigned_partitions"] = cfg_.group_membership ? (double)assigned_partitions_
+                                                   : (double)partition_offsets().size();
   s["ingested_records"] = (double)ingested_records_;
   s["thread_s_ingest"] = ingest_ns_ * 1e-9;
   s["eff_max_batch"] = (double)eff_batch_;

@@ -59,6 +59,14 @@ struct EngineConfig {
   int decode_threads = 2;          // CRC32C + envelope scan workers (0 = on the source thread)
   int64_t pinned_fetch_bytes = 4ll << 30;  // pinned fetch-buffer budget (GPU replicas only)
   int commit_interval_ms = 2000;   // storm-kafka's ZK commit period
+  // consumer-group membership (elastic DP, kafka::GroupMember): the input partitions are shared
+  // by every engine of group_id; a member that dies or leaves has its partitions moved to the
+  // survivors, which resume them from the committed offsets (at-least-once across the move)
+  bool group_membership = false;
+  int session_timeout_ms = 6000;
+  int rebalance_timeout_ms = 8000;
+  int heartbeat_interval_ms = 500;
+  std::string assignor = "range";  // range | roundrobin
   // sink (R5, R9, E7-E9)
   int sink_parallelism = 2;        // KAFKA_BOLT_PARAL (MainTopology.java:28)
   int acks = 1;                    // MainTopology.java:113
@@ -155,7 +163,18 @@ class Engine {
     bool pinned = false;
   };
 
-  void source_loop(int idx, std::vector<int> parts);
+  struct SourceCtl {  // a source thread's (group-managed) partition assignment
+    std::mutex mu;
+    std::condition_variable cv;
+    std::vector<int> parts;
+    uint64_t epoch = 0, acked = 0;
+    int32_t generation = -1;
+    std::string member;
+  };
+  void source_loop(int idx);
+  void group_loop();
+  bool distribute(const std::vector<int>& parts, int32_t generation, const std::string& member,
+                  int timeout_ms);
   void decode_loop(int idx);
   void decode_fetch(FetchItem& it, std::vector<InRecord>& good, int lane);
   bool ingest_fetch(FetchItem& it, std::vector<InRecord>& good, int lane);
@@ -176,6 +195,11 @@ class Engine {
   std::unique_ptr<Batcher> batcher_;
   std::vector<std::unique_ptr<kafka::Producer>> producers_;
   std::vector<std::thread> sources_, workers_, decoders_;
+  std::vector<std::unique_ptr<SourceCtl>> src_ctl_;
+  std::thread group_thread_;
+  std::atomic<bool> group_stop_{false};
+  std::atomic<int64_t> rebalances_{0};
+  std::atomic<int> assigned_partitions_{0}, generation_{-1};
   std::shared_ptr<PinnedPool> pinned_;
   std::shared_ptr<Ingest> ingest_;
   std::atomic<bool> ingest_failed_{false};

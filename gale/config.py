@@ -23,6 +23,7 @@ CHOICES = {
     "value_format": ("json", "json-string"),
     "on_error": ("null", "error-json", "drop"),
     "output_key": ("none", "input"),
+    "assignor": ("range", "roundrobin"),
     # compute dtype of the GPU kernels (MFMA bf16 / OCP e4m3 fp8); inputs and the softmax
     # output stay fp32 as in the reference's TF graph (InferenceBolt.java:80-86)
     "dtype": ("bf16", "fp8"),
@@ -44,6 +45,13 @@ class GaleConfig:
     partitions: str = ""               # comma-separated input partitions (empty = all)
     start_offset: str = "latest"       # reference: LatestTime + ignoreZkOffsets (:101-102)
     commit_interval_ms: int = 2000
+    # elastic data parallelism: every process of the group shares the input partitions through
+    # Kafka consumer-group membership; dead members' partitions move to the survivors
+    group_membership: bool = False
+    session_timeout_ms: int = 6000
+    rebalance_timeout_ms: int = 8000
+    heartbeat_interval_ms: int = 500
+    assignor: str = "range"
     decode_threads: int = 2            # CRC32C + envelope-scan workers behind each consumer
     check_crcs: bool = True            # Kafka consumer check.crcs
     gpu_ingest: bool = True            # CRC32C + image counts of pinned fetch buffers on the GPU
@@ -105,6 +113,10 @@ class GaleConfig:
         for k in ("source_parallelism", "sink_parallelism", "max_batch", "queue_depth"):
             if getattr(self, k) <= 0:
                 raise ValueError(f"{k} must be positive")
+        if self.group_membership and not (0 < self.heartbeat_interval_ms
+                                          < self.session_timeout_ms):
+            raise ValueError("group membership: need 0 < heartbeat_interval_ms < "
+                             "session_timeout_ms")
         if self.slo_p99_ms < 0:
             raise ValueError("slo_p99_ms must be >= 0")
         if self.replicas < 0 or self.gpus < 0:
@@ -127,6 +139,9 @@ class GaleConfig:
             partitions=[int(p) for p in self.partitions.split(",") if p.strip()],
             source_parallelism=self.source_parallelism, start_offset=self.start_offset,
             commit_interval_ms=self.commit_interval_ms, sink_parallelism=self.sink_parallelism,
+            group_membership=self.group_membership, session_timeout_ms=self.session_timeout_ms,
+            rebalance_timeout_ms=self.rebalance_timeout_ms,
+            heartbeat_interval_ms=self.heartbeat_interval_ms, assignor=self.assignor,
             decode_threads=self.decode_threads, check_crcs=self.check_crcs,
             acks=self.acks, sink_mode=self.sink_mode, linger_ms=self.linger_ms,
             value_format=self.value_format, type_id_header=self.type_id_header,

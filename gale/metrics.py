@@ -19,13 +19,16 @@ KEYS = ("records_in", "records_out", "images_out", "errors", "produce_failures",
         "requeued", "replica_failures", "replica_restarts", "queue_records", "replicas_alive",
         "commits", "lag_records", "lag_records_max", "fetch_lag_records",
         "e2e_us_p50", "e2e_us_p99", "queue_us_p50", "device_us_p50", "device_us_p99",
-        "record_e2e_ms_p50", "record_e2e_ms_p99", "batch_images_mean")
+        "record_e2e_ms_p50", "record_e2e_ms_p99", "batch_images_mean", "rebalances",
+        "generation", "assigned_partitions", "eff_max_batch", "eff_max_wait_us")
 
 
 class Reporter:
     def __init__(self, stats_fn: Callable[[], Dict[str, float]], interval: float = 10.0,
-                 out: Optional[TextIO] = None, path: str = "", labels: Optional[dict] = None):
+                 out: Optional[TextIO] = None, path: str = "", labels: Optional[dict] = None,
+                 extra_fn: Optional[Callable[[], dict]] = None):
         self.stats_fn = stats_fn
+        self.extra_fn = extra_fn  # merged into every line (e.g. the owned input partitions)
         self.interval = interval
         self.labels = dict(labels or {})
         self._own = open(path, "a", buffering=1) if path else None
@@ -47,6 +50,8 @@ class Reporter:
             if k in s:
                 v = s[k]
                 line[k] = int(v) if float(v).is_integer() else round(v, 3)
+        if self.extra_fn is not None:
+            line.update(self.extra_fn())
         self._last, self._last_t = s, now
         return line
 
@@ -70,7 +75,7 @@ class Reporter:
             self._thread.start()
         return self
 
-    def stop(self, final: bool = True) -> None:
+    def stop(self, final: bool = True, close: bool = True) -> None:
         self._stop.set()
         if self._thread:
             self._thread.join()
@@ -79,5 +84,9 @@ class Reporter:
                 self.report()
             except Exception:
                 pass
-        if self._own:
+        if close:
+            self.close()
+
+    def close(self) -> None:
+        if self._own and not self._own.closed:
             self._own.close()

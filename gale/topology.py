@@ -177,7 +177,7 @@ def run_topology(cfg: GaleConfig, stop_event: Optional[threading.Event] = None,
             if not dist.is_initialized():
                 dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
             devices = [local_rank]
-        if world > 1 and not cfg.partitions:
+        if world > 1 and not cfg.partitions and not cfg.group_membership:
             cfg.partitions = rank_partitions(cfg, rank, world)
         if cfg.numa_pin and not cfg.stub:
             _pin_single_gpu(cfg, devices)
@@ -190,11 +190,14 @@ def run_topology(cfg: GaleConfig, stop_event: Optional[threading.Event] = None,
                  cfg.input_topic, cfg.output_topic, cfg.bootstrap, cfg.model,
                  len(engine.replica_stats()))
         reporter = Reporter(engine.stats, cfg.metrics_interval, path=cfg.metrics_file,
-                            labels={"topology": name}).start()
+                            labels={"topology": name, "rank": rank},
+                            extra_fn=lambda: {"partitions": sorted(
+                                o["partition"] for o in engine.partition_offsets())}).start()
         stop_event.wait(cfg.duration if cfg.duration > 0 else None)
-        reporter.stop(final=False)
+        reporter.stop(final=False, close=False)
         engine.stop()
         final = reporter.report()
+        reporter.close()
         return dict(engine.stats(), final=final)
     finally:
         if engine is not None and engine.running:

@@ -1,0 +1,239 @@
+"""Elastic data parallelism through Kafka consumer-group membership (E3/E4), on
+CPU with stub replicas and the embedded broker's group coordinator.
+
+The reference spreads the input partitions statically over its spout tasks and relies on Storm
+supervisors to restart dead workers (MainTopology.java:25-28,61-66). gale's processes share the
+input topic through JoinGroup/SyncGroup/Heartbeat: a member that leaves or dies has its
+partitions moved to the survivors, which resume from the group's committed offsets
+(at-least-once across the move: no record is lost, a few may be served twice)."""
+
+import json
+import os
+import signal
+import subprocess
+import sys
+import time
+
+import numpy as np
+import pytest
+
+from gale._native import native
+from gale.config import GaleConfig
+from gale.engine import Engine
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+C = native()
+K = C.kafka
+
+
+def test_assignors():
+    r = K.group_assign("range", ["b", "a", "c"], 7)
+    assert r == {"a": [0, 1, 2], "b": [3, 4], "c": [5, 6]}
+    rr = K.group_assign("roundrobin", ["b", "a"], 5)
+    assert rr == {"a": [0, 2, 4], "b": [1, 3]}
+    assert K.group_assign("range", ["a", "b", "c"], 2) == {"a": [0], "b": [1], "c": []}
+
+
+@pytest.fixture()
+def broker():
+    b = K.Broker()
+    b.start()
+    b.create_topic("in", 4)
+    b.create_topic("out", 1)
+    yield b
+    b.stop()
+
+
+def group_cfg(broker, name, **kw):
+    base = dict(topology_name=name, group_id="G", input_topic="in", output_topic="out",
+                bootstrap=f"127.0.0.1:{broker.port}", start_offset="earliest", stub=True,
+                max_batch=16, max_wait_us=500, group_membership=True, session_timeout_ms=1500,
+                heartbeat_interval_ms=100, rebalance_timeout_ms=3000, output_key="input",
+                commit_interval_ms=100, source_parallelism=2)
+    base.update(kw)
+    return GaleConfig(**base).validate()
+
+
+def wait_for(pred, timeout=15.0):
+    t = time.time() + timeout
+    while time.time() < t:
+        if pred():
+            return True
+        time.sleep(0.05)
+    return False
+
+
+def test_two_engines_split_partitions_then_one_leaves(broker):
+    rng = np.random.default_rng(0)
+    keys = set()
+
+    def feed(n0, n):
+        for i in range(n0, n0 + n):
+            k = f"k{i}".encode()
+            keys.add(k)
+            broker.append("in", i % 4, [C.encode_instances(rng.random((1, 32, 32, 3),
+                                                                      dtype=np.float32))], [k])
+
+    feed(0, 40)
+    a = Engine(group_cfg(broker, "a"))
+    a.start()
+    assert wait_for(lambda: a.stats()["assigned_partitions"] == 4)
+    b = Engine(group_cfg(broker, "b"))
+    b.start()
+    assert wait_for(lambda: a.stats()["assigned_partitions"] == 2
+                    and b.stats()["assigned_partitions"] == 2)
+    g = broker.describe_group("G")
+    assert g["state"] == "Stable" and len(g["members"]) == 2 and g["protocol"] == "range"
+    pa = {o["partition"] for o in a.partition_offsets()}
+    pb = {o["partition"] for o in b.partition_offsets()}
+    assert pa | pb == {0, 1, 2, 3} and not pa & pb
+    feed(40, 40)
+    assert wait_for(lambda: {r["key"] for r in broker.read("out", 0)} >= keys)
+    b.stop()  # graceful: final commits, then LeaveGroup -> a takes every partition
+    assert wait_for(lambda: a.stats()["assigned_partitions"] == 4)
+    feed(80, 40)
+    assert wait_for(lambda: {r["key"] for r in broker.read("out", 0)} >= keys)
+    a.stop()
+    out = broker.read("out", 0)
+    got = [r["key"] for r in out]
+    assert set(got) == keys
+    # graceful moves commit before handing partitions over: exactly once here
+    assert len(got) == len(keys)
+
+
+def test_commit_from_a_stale_generation_is_fenced(broker):
+    """OffsetCommit carries the member's generation: after a rebalance, a zombie commit from
+    the previous generation is rejected, so it cannot overwrite the new owner's progress."""
+    a = Engine(group_cfg(broker, "a"))
+    a.start()
+    assert wait_for(lambda: a.stats()["assigned_partitions"] == 4)
+    g0 = broker.describe_group("G")
+    member = g0["members"][0]
+    c = K.Consumer(f"127.0.0.1:{broker.port}", "G")
+    c.assign("in", [0])
+    c.set_generation(g0["generation"], member)
+    c.commit({0: 0})  # current generation: accepted
+    b = Engine(group_cfg(broker, "b"))
+    b.start()
+    assert wait_for(lambda: broker.describe_group("G")["generation"] > g0["generation"]
+                    and broker.describe_group("G")["state"] == "Stable")
+    with pytest.raises(Exception, match="ILLEGAL_GENERATION"):
+        c.commit({0: 0})
+    c.set_generation(-1, "")
+    c.commit({0: 0})  # a group-less commit (generation -1) is not fenced
+    b.stop()
+    a.stop()
+
+
+def _cli(name, port, tmp, extra=(), env=None):
+    cmd = [sys.executable, "-m", "gale", name, "in", "out", "--bootstrap", f"127.0.0.1:{port}",
+           "--stub", "--start-offset", "earliest", "--output-key", "input",
+           "--registry-dir", str(tmp / "reg"), "--metrics-file", str(tmp / f"{name}.jsonl"),
+           "--metrics-interval", "0.5", "--max-batch", "16", "--max-wait-us", "500",
+           "--commit-interval-ms", "100", "--source-parallelism", "1", *extra]
+    return subprocess.Popen(cmd, cwd=ROOT, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                            text=True, env=dict(os.environ, OMP_NUM_THREADS="1", **(env or {})))
+
+
+def _final(tmp, name):
+    lines = [json.loads(x) for x in open(tmp / f"{name}.jsonl") if x.strip()]
+    return lines[-1]
+
+
+def test_torchrun_world3_shared_broker_static_partitions(tmp_path):
+    """BASELINE config 3 on CPU: torch.distributed.run world 3 against ONE broker and one input
+    topic with 6 partitions; rank r consumes exactly the partitions p % 3 == r, and every input
+    record yields exactly one output (matched by key)."""
+    b = K.Broker()
+    b.start()
+    try:
+        b.create_topic("in", 6)
+        b.create_topic("out", 1)
+        rng = np.random.default_rng(3)
+        keys = []
+        for i in range(180):
+            k = f"r{i}".encode()
+            keys.append(k)
+            b.append("in", i % 6, [C.encode_instances(rng.random((1, 32, 32, 3),
+                                                              dtype=np.float32))], [k])
+        from gale.utils import free_port
+
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=3",
+               "--master-addr", "127.0.0.1", "--master-port", str(free_port()), "-m", "gale",
+               "t", "in", "out", "--bootstrap", f"127.0.0.1:{b.port}", "--stub",
+               "--start-offset", "earliest", "--output-key", "input", "--duration", "6",
+               "--registry-dir", str(tmp_path / "reg"), "--metrics-interval", "0.5",
+               "--max-batch", "16", "--max-wait-us", "500", "--source-parallelism", "1"]
+        env = dict(os.environ, OMP_NUM_THREADS="1")
+        # one metrics file shared by the ranks (lines are labelled with the rank)
+        p = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=120,
+                           env=dict(env, GALE_METRICS_FILE=str(tmp_path / "m.jsonl")))
+        assert p.returncode == 0, p.stderr[-3000:]
+        out = b.read("out", 0)
+        got = [r["key"] for r in out]
+        assert sorted(got) == sorted(keys)  # exactly once, nothing lost
+        finals = {}
+        for line in open(tmp_path / "m.jsonl"):
+            r = json.loads(line)
+            finals[r["rank"]] = r  # last line per rank
+        assert set(finals) == {0, 1, 2}
+        for r, f in finals.items():
+            assert f["partitions"] == [p for p in range(6) if p % 3 == r]
+        assert sum(f["records_out"] for f in finals.values()) == 180
+    finally:
+        b.stop()
+
+
+def test_group_member_killed_survivors_adopt_its_partitions(tmp_path):
+    """Three independent serving processes in one consumer group; one is SIGKILLed mid-stream.
+    Its session expires, the survivors rebalance, adopt its partitions from the committed
+    offsets and serve everything: no input record is lost."""
+    b = K.Broker()
+    b.start()
+    procs = {}
+    try:
+        b.create_topic("in", 6)
+        b.create_topic("out", 1)
+        rng = np.random.default_rng(4)
+        payload = [C.encode_instances(rng.random((1, 32, 32, 3), dtype=np.float32))
+                   for _ in range(16)]
+        extra = ["--group-membership", "--group-id", "G", "--session-timeout-ms", "1500",
+                 "--heartbeat-interval-ms", "100", "--rebalance-timeout-ms", "3000",
+                 "--duration", "14"]
+        for name in ("A", "B", "C"):
+            procs[name] = _cli(name, b.port, tmp_path, extra)
+        assert wait_for(lambda: len(b.describe_group("G")["members"]) == 3, 60)
+        keys = []
+        t0 = time.time()
+        i = 0
+        killed = False
+        while time.time() - t0 < 6.0:
+            for _ in range(6):
+                k = f"x{i}".encode()
+                keys.append(k)
+                b.append("in", i % 6, [payload[i % 16]], [k])
+                i += 1
+            if not killed and time.time() - t0 > 2.0:
+                procs["C"].send_signal(signal.SIGKILL)
+                killed = True
+            time.sleep(0.02)
+        assert wait_for(lambda: set(keys) <= {r["key"] for r in b.read("out", 0)}, 30), \
+            "records of the killed member's partitions were not taken over"
+        for name in ("A", "B"):
+            out, err = procs[name].communicate(timeout=60)
+            assert procs[name].returncode == 0, err[-3000:]
+        procs["C"].wait(10)
+        g = b.describe_group("G")
+        assert len(g["members"]) == 0  # the survivors left cleanly at the end
+        fa, fb = _final(tmp_path, "A"), _final(tmp_path, "B")
+        assert set(fa["partitions"]) | set(fb["partitions"]) == set(range(6))
+        assert fa["rebalances"] >= 2 and fb["rebalances"] >= 2
+        got = [r["key"] for r in b.read("out", 0)]
+        dups = len(got) - len(set(got))
+        assert set(got) == set(keys)
+        assert dups <= len(keys) // 2  # at-least-once: re-served since C's last commit only
+    finally:
+        for p in procs.values():
+            if p.poll() is None:
+                p.kill()
+        b.stop()
