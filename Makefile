@@ -17,11 +17,12 @@ CXX_FLAGS := -O3 -fPIC -std=c++17 -D__HIP_PLATFORM_AMD__ -I$(ROCM)/include -Icsr
 
 HIP_SRC   := $(wildcard csrc/kernels/*.hip)
 CXX_SRC   := $(wildcard csrc/runtime/*.cpp) $(wildcard csrc/codec/*.cpp) \
-             $(wildcard csrc/kafka/*.cpp) $(wildcard csrc/bindings/*.cpp)
+             $(wildcard csrc/kafka/*.cpp) $(wildcard csrc/comm/*.cpp) $(wildcard csrc/bindings/*.cpp)
 HIP_OBJ   := $(patsubst csrc/%.hip,$(OBJ)/%.o,$(HIP_SRC))
 CXX_OBJ   := $(patsubst csrc/%.cpp,$(OBJ)/%.o,$(CXX_SRC))
 HDRS      := $(wildcard csrc/include/gale/*.h) $(wildcard csrc/kernels/*.cuh) \
-             $(wildcard csrc/runtime/*.h) $(wildcard csrc/codec/*.h) $(wildcard csrc/kafka/*.h)
+             $(wildcard csrc/runtime/*.h) $(wildcard csrc/codec/*.h) $(wildcard csrc/kafka/*.h) \
+             $(wildcard csrc/comm/*.h)
 
 all: gale/_C.so
 
@@ -34,7 +35,7 @@ $(OBJ)/%.o: csrc/%.cpp $(HDRS)
 	$(CXX) $(CXX_FLAGS) -c $< -o $@
 
 gale/_C.so: $(HIP_OBJ) $(CXX_OBJ)
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -L$(ROCM)/lib -lamdhip64 -lrocprofiler-sdk-roctx -pthread \
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -L$(ROCM)/lib -lamdhip64 -lrccl -lrocprofiler-sdk-roctx -pthread \
 	    -Wl,-rpath,$(ROCM)/lib
 
 clean:

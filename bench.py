@@ -98,6 +98,10 @@ def parse_args(argv=None):
                     help="replica workers sleep-poll batch completion every N us (0 = spin)")
     ap.add_argument("--encode-threads", type=int, default=0,
                     help="threads for encoding the synthetic records (0 = host CPU share)")
+    ap.add_argument("--single-process", action="store_true",
+                    help="one process drives all --gpus GPUs (one engine: per-GPU locality "
+                         "slots with work stealing, weights RCCL-broadcast in-process) instead "
+                         "of one torch.distributed rank per GPU")
     ap.add_argument("--timeout", type=float, default=600.0)
     return ap.parse_args(argv)
 
@@ -186,15 +190,22 @@ def main(argv=None) -> int:
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # GPUs driven by this process (> 1 only in --single-process mode)
+    local_gpus = a.gpus if a.single_process else 1
+    if a.single_process and world > 1:
+        raise SystemExit("bench.py: --single-process runs as ONE process (no torchrun)")
     import torch
     import torch.distributed as dist
 
     use_gpu = not a.stub
     if use_gpu and not torch.cuda.is_available():
         raise SystemExit("bench.py: no GPU visible (use --stub for the CPU plumbing run)")
+    if use_gpu and local_gpus > torch.cuda.device_count():
+        raise SystemExit(f"bench.py: {local_gpus} GPUs requested, "
+                         f"{torch.cuda.device_count()} visible")
     if use_gpu:
         torch.cuda.set_device(local_rank)
-        if a.numa_pin:
+        if a.numa_pin and local_gpus == 1:
             from gale.utils import pin_to_gpu_numa
 
             pin_to_gpu_numa(local_rank, a.cpus_per_rank)
@@ -211,7 +222,7 @@ def main(argv=None) -> int:
     net = get_model(a.model)
     K = native().kafka
     ipr = a.images_per_record
-    parts_per_rank = a.partitions or a.replicas_per_gpu
+    parts_per_rank = (a.partitions or a.replicas_per_gpu) * local_gpus
     # records per RecordBatch: a producer's batch (rate mode: small batches, arrivals are not
     # bursty; the feeder keeps to ~10k appends/s) ...
     rpb = min(64, max(8, int(a.rate // 10000))) if a.rate > 0 else 64
@@ -239,7 +250,7 @@ def main(argv=None) -> int:
     broker.create_topic("gale-in", n_parts)
     broker.create_topic("gale-out", world)
     my_parts = [p for p in range(n_parts) if p % world == rank]  # the partitions this rank leads
-    step_images = a.step_images
+    step_images = a.step_images * local_gpus  # (a step is per GPU)
     step_records = -(-step_images // ipr)
     feeder = Feeder(broker, "gale-in", my_parts, bset, rate=a.rate,
                     ahead_records=-(-max(step_records, 65536 // ipr) // len(my_parts)))
@@ -255,16 +266,19 @@ def main(argv=None) -> int:
                      max_batch=a.batch, max_wait_us=a.max_wait_us,
                      queue_depth=max(1, a.queue_batches * a.batch // ipr),
                      source_parallelism=a.source_parallelism or len(my_parts),
-                     sink_parallelism=a.sink_parallelism, replicas=a.replicas_per_gpu,
+                     sink_parallelism=a.sink_parallelism * local_gpus,
+                     replicas=a.replicas_per_gpu * local_gpus,
                      decode_threads=a.decode_threads, slo_p99_ms=a.slo_p99_ms,
                      gpu_wait_poll_us=a.gpu_wait_poll_us, gpu_ingest=a.gpu_ingest,
                      stub=a.stub, stub_null=a.stub_null, commit_interval_ms=500,
                      check_crcs=a.check_crcs)
-    devices = [local_rank] if use_gpu else None
+    devices = (list(range(local_gpus)) if local_gpus > 1 else [local_rank]) if use_gpu else None
     # ONE engine: warm-up and timed window are the same steady-state pipeline (connections,
     # pinned fetch buffers, captured graphs all warm); the timed window starts at a barrier
     # once every rank has warmed up and ends when K more steps completed on this rank.
-    eng = Engine(cfg, devices=devices)  # weights: seeded on rank 0, RCCL-broadcast
+    # weights: seeded on rank 0 (or the first GPU), RCCL-broadcast to every other GPU
+    eng = Engine(cfg, devices=devices,
+                 stub_localities=tuple(range(local_gpus)) if a.stub and local_gpus > 1 else ())
     eng.start()
     feeder.start(eng)
     warm_s, warm_rates = warm_up(eng, max(1, a.warmup) * step_records, a)
@@ -313,11 +327,12 @@ def main(argv=None) -> int:
         elapsed_max, total_images = elapsed, float(images)
     if rank == 0:
         value = total_images / elapsed_max
+        n_gpus = world * local_gpus
         step_rates = [step_records * ipr / (b - a_) for a_, b in zip([t0] + marks[:-1], marks)]
         med = statistics.median(step_rates)
         cores = {k: round((cpu1[k] - cpu0[k]) / elapsed, 2) for k in cpu1}
         out = {
-            "metric": METRIC, "value": round(value, 1), "unit": "images/s", "n_gpus": world,
+            "metric": METRIC, "value": round(value, 1), "unit": "images/s", "n_gpus": n_gpus,
             "steps": a.steps, "warmup": a.warmup,
             "ms_per_step": round(elapsed_max / a.steps * 1e3, 4),
             "higher_is_better": True,
@@ -327,12 +342,14 @@ def main(argv=None) -> int:
                     "Java float format, fed through an embedded Kafka-protocol broker cluster, "
                     "one broker per rank); random-init weights (seed 0) RCCL-broadcast from "
                     "rank 0",
-            "step": f"{step_images} images per GPU through fetch->parse->forward->produce-ack",
-            "config": {"model": a.model, "global_batch": a.batch * a.replicas_per_gpu * world,
-                       "seq_len": None, "parallelism": f"dp{world}",
+            "step": f"{a.step_images} images per GPU through fetch->parse->forward->produce-ack",
+            "config": {"model": a.model,
+                       "global_batch": a.batch * a.replicas_per_gpu * n_gpus,
+                       "seq_len": None, "parallelism": f"dp{n_gpus}",
+                       "processes": world,
                        "images_per_record": ipr, "max_batch": a.batch,
                        "max_wait_us": a.max_wait_us, "replicas_per_gpu": a.replicas_per_gpu,
-                       "partitions": n_parts, "step_images_per_gpu": step_images,
+                       "partitions": n_parts, "step_images_per_gpu": a.step_images,
                        "path": "kafka-fetch->gpu-json-parse->hipgraph-forward->kafka-produce"},
             "load": (f"offered {a.rate:.0f} images/s per GPU" if a.rate > 0
                      else "backlog kept ahead of the consumers (max throughput; latency "

@@ -39,6 +39,7 @@ EngineConfig config_from_dict(const py::dict& d) {
   opt(d, "rebalance_timeout_ms", c.rebalance_timeout_ms);
   opt(d, "heartbeat_interval_ms", c.heartbeat_interval_ms);
   opt(d, "assignor", c.assignor);
+  opt(d, "device_cpus", c.device_cpus);
   opt(d, "sink_parallelism", c.sink_parallelism);
   opt(d, "acks", c.acks);
   opt(d, "sink_mode", c.sink_mode);
@@ -72,12 +73,13 @@ void bind_engine(py::module_& m) {
   py::class_<Engine, std::shared_ptr<Engine>>(m, "Engine")
       .def(py::init([](py::dict cfg) { return std::make_shared<Engine>(config_from_dict(cfg)); }))
       .def("add_stub_replica",
-           [](Engine& e, int max_images, int delay_us, bool compute) {
+           [](Engine& e, int max_images, int delay_us, bool compute, int locality) {
              const EngineConfig& c = e.config();
              e.add_replica(std::make_shared<StubReplica>(c.H, c.W, c.C, c.classes, max_images,
-                                                         delay_us, compute));
+                                                         delay_us, compute, locality));
            },
-           py::arg("max_images") = 256, py::arg("delay_us") = 0, py::arg("compute") = true)
+           py::arg("max_images") = 256, py::arg("delay_us") = 0, py::arg("compute") = true,
+           py::arg("locality") = -1)
       .def("add_gpu_replica",
            [](Engine& e, std::shared_ptr<Executor> exec, bool use_graph, int wait_poll_us) {
              const EngineConfig& c = e.config();

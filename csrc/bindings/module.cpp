@@ -6,6 +6,7 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include "../comm/rccl.h"
 #include "gale/executor.h"
 #include "gale/kernels.h"
 
@@ -162,6 +163,32 @@ PYBIND11_MODULE(_C, m) {
               "json_parse_instances");
         });
   m.def("json_tile_count", &gale::json_tile_count);
+  py::module_ comm = m.def_submodule("comm", "in-process RCCL communicator (ncclCommInitAll)");
+  py::class_<gale::CommGroup, std::shared_ptr<gale::CommGroup>>(comm, "CommGroup")
+      .def(py::init([](std::vector<int> devices) {
+             py::gil_scoped_release nogil;
+             return std::make_shared<gale::CommGroup>(devices);
+           }),
+           py::arg("devices"))
+      .def_property_readonly("size", &gale::CommGroup::size)
+      .def_property_readonly("devices", &gale::CommGroup::devices)
+      .def("broadcast",
+           [](gale::CommGroup& g, uintptr_t send_root, std::vector<uintptr_t> recv, size_t bytes,
+              int root) {
+             std::vector<void*> r;
+             for (uintptr_t p : recv) r.push_back(reinterpret_cast<void*>(p));
+             py::gil_scoped_release nogil;
+             g.broadcast(reinterpret_cast<const void*>(send_root), r, bytes, root);
+           },
+           py::arg("send_root"), py::arg("recv"), py::arg("bytes"), py::arg("root") = 0)
+      .def("all_reduce_sum_f64",
+           [](gale::CommGroup& g, std::vector<uintptr_t> bufs, size_t count) {
+             std::vector<double*> b;
+             for (uintptr_t p : bufs) b.push_back(reinterpret_cast<double*>(p));
+             py::gil_scoped_release nogil;
+             g.all_reduce_sum_f64(b, count);
+           },
+           py::arg("bufs"), py::arg("count"));
   m.def("crc32c_chunks",
         [](uintptr_t bytes, uintptr_t chunks, int n, uintptr_t tables, uintptr_t out,
            uintptr_t stream) {

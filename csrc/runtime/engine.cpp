@@ -4,6 +4,7 @@
 
 #include <hip/hip_runtime.h>
 #include <stdio.h>
+#include <sched.h>
 #include <sys/prctl.h>
 
 #include <algorithm>
@@ -52,16 +53,21 @@ class Engine::Batcher {
   // oldest record has waited max_wait_ns, or immediately once the queue is closed (drain).
   // With a batch already in flight on the caller's replica, a partial batch is not taken early
   // (returns true with `out` empty) so the device work accumulates a fuller next batch.
+  // idle_ns > 0: also return (true, empty) when the queue stayed empty that long (the caller
+  // may then steal from another locality's queue).
   bool take(int max_images, int64_t max_wait_ns, bool have_inflight, std::vector<InRecord>& out,
-            int& images) {
+            int& images, int64_t idle_ns = 0) {
     out.clear();
     images = 0;
     std::unique_lock<std::mutex> lk(mu_);
+    const int64_t t_idle = idle_ns > 0 ? mono_ns() + idle_ns : 0;
     for (;;) {
       if (q_.empty()) {
         if (closed_) return false;
         if (have_inflight) return true;
-        cv_items_.wait_for(lk, std::chrono::milliseconds(20));
+        if (t_idle && mono_ns() >= t_idle) return true;
+        cv_items_.wait_for(lk, std::chrono::nanoseconds(t_idle ? std::max<int64_t>(
+                                   t_idle - mono_ns(), 1000) : 20000000));
         continue;
       }
       const int64_t deadline = q_.front().t_fetch_ns + max_wait_ns;
@@ -79,6 +85,26 @@ class Engine::Batcher {
       if (have_inflight) return true;
       cv_items_.wait_for(lk, std::chrono::nanoseconds(std::max<int64_t>(deadline - now, 1000)));
     }
+  }
+
+  // Non-blocking: whatever is queued now, up to max_images (work stealing by an idle replica
+  // of another locality).
+  bool try_take(int max_images, std::vector<InRecord>& out, int& images) {
+    out.clear();
+    images = 0;
+    std::lock_guard<std::mutex> lk(mu_);
+    while (!q_.empty() && (images == 0 || images + q_.front().images <= max_images)) {
+      images += q_.front().images;
+      images_ -= q_.front().images;
+      out.push_back(std::move(q_.front()));
+      q_.pop_front();
+    }
+    if (!out.empty()) cv_space_.notify_all();
+    return !out.empty();
+  }
+  int64_t queued_images() {
+    std::lock_guard<std::mutex> lk(mu_);
+    return images_;
   }
 
   void close() {
@@ -104,6 +130,7 @@ class Engine::Batcher {
 struct Engine::ReplicaSlot {
   std::shared_ptr<Replica> rep;
   int index = 0;
+  int slot = 0;  // locality slot (its device's batcher / fetch pool)
   std::atomic<bool> alive{true};
   std::atomic<bool> watchdog_killed{false};
   std::atomic<bool> restarting{false};  // failed, supervisor recovery pending
@@ -142,7 +169,6 @@ Engine::Engine(EngineConfig cfg) : cfg_(std::move(cfg)), rng_(cfg_.seed) {
     else if (kind == "producer_fail") producer_fail_p_ = std::stod(val);
     else throw std::invalid_argument("engine: unknown fault kind " + kind);
   }
-  batcher_ = std::make_unique<Batcher>((size_t)std::max(1, cfg_.queue_depth));
   eff_batch_ = cfg_.max_batch;
   eff_wait_ns_ = (int64_t)cfg_.max_wait_us * 1000;
   if (cfg_.slo_p99_ms > 0)  // start with a quarter of the budget for batch formation
@@ -170,7 +196,22 @@ void Engine::add_replica(std::shared_ptr<Replica> r) {
 
 void Engine::set_ingest(std::shared_ptr<Ingest> ing) {
   if (running_) throw std::logic_error("engine: set_ingest after start");
-  ingest_ = std::move(ing);
+  ingests_[ing->device()] = std::move(ing);
+}
+
+Ingest* Engine::ingest_for(int slot) {
+  auto it = ingests_.find(slot_dev_[(size_t)slot]);
+  return it == ingests_.end() ? nullptr : it->second.get();
+}
+
+void Engine::pin_thread(int device) {
+  auto it = cfg_.device_cpus.find(device);
+  if (it == cfg_.device_cpus.end() || it->second.empty()) return;
+  cpu_set_t set;
+  CPU_ZERO(&set);
+  for (int c : it->second)
+    if (c >= 0 && c < CPU_SETSIZE) CPU_SET(c, &set);
+  sched_setaffinity(0, sizeof(set), &set);  // (best effort: a failure leaves it unpinned)
 }
 
 kafka::Producer* Engine::producer_for(int i) {
@@ -217,12 +258,30 @@ void Engine::start() {
     for (size_t i = 0; i < parts.size(); ++i) src_ctl_[i % (size_t)ns]->parts.push_back(parts[i]);
     for (auto& c : src_ctl_) c->epoch = 1;
   }
-  bool any_gpu = false;
-  for (auto& rs : replicas_) any_gpu |= rs->rep->device() >= 0;
-  if ((any_gpu || ingest_) && cfg_.pinned_fetch_bytes > 0 && !pinned_) {
-    pinned_ = std::make_shared<PinnedPool>((size_t)cfg_.fetch_max_bytes + (1 << 20),
-                                           (size_t)cfg_.pinned_fetch_bytes);
-    if (ingest_) pinned_->set_mirror_device(ingest_->device());
+  // locality slots: one per distinct replica device (first-seen order). Each has its own
+  // batcher, pinned fetch pool (mirrored on its device for GPU ingest) and sources; replicas
+  // serve their own slot first and steal from the most loaded other slot when idle (the
+  // locality-preferring, load-aware dispatch of Storm's LoadAwareShuffleGrouping)
+  slot_dev_.clear();
+  for (auto& rs : replicas_) {
+    const int d = rs->rep->locality();
+    auto it = std::find(slot_dev_.begin(), slot_dev_.end(), d);
+    rs->slot = (int)(it - slot_dev_.begin());
+    if (it == slot_dev_.end()) slot_dev_.push_back(d);
+  }
+  const size_t nslots = slot_dev_.size();
+  batchers_.clear();
+  for (size_t i = 0; i < nslots; ++i)
+    batchers_.push_back(std::make_unique<Batcher>(
+        (size_t)std::max(1, cfg_.queue_depth / (int)nslots)));
+  pools_.assign(nslots, nullptr);
+  for (size_t i = 0; i < nslots; ++i) {
+    bool gpu = false;
+    for (auto& rs : replicas_) gpu |= rs->slot == (int)i && rs->rep->device() >= 0;
+    if (!gpu || cfg_.pinned_fetch_bytes <= 0) continue;
+    pools_[i] = std::make_shared<PinnedPool>((size_t)cfg_.fetch_max_bytes + (1 << 20),
+                                             (size_t)cfg_.pinned_fetch_bytes / nslots);
+    if (ingest_for((int)i)) pools_[i]->set_mirror_device(slot_dev_[i]);
   }
   running_ = true;
   stopping_ = false;
@@ -238,12 +297,14 @@ void Engine::start() {
   for (auto& rs : replicas_)
     workers_.emplace_back([this, rs] {
       name_thread("gl-rep", rs->index);
+      pin_thread(rs->rep->device());
       prctl(PR_SET_TIMERSLACK, 1000UL, 0, 0, 0);  // 1 us: sleep-polling GPU waits stay tight
       worker_loop(rs.get());
     });
   for (int i = 0; i < ns; ++i)
     sources_.emplace_back([this, i] {
       name_thread("gl-src", i);
+      pin_thread(slot_dev_[(size_t)i % slot_dev_.size()]);
       source_loop(i);
     });
   group_stop_ = false;
@@ -278,7 +339,7 @@ void Engine::stop() {
   dec_space_cv_.notify_all();
   for (auto& t : decoders_) t.join();
   decoders_.clear();
-  batcher_->close();
+  for (auto& b : batchers_) b->close();
   for (size_t i = 0; i < workers_.size(); ++i) {
     if (replicas_[i]->alive || replicas_[i]->restarting) {
       workers_[i].join();
@@ -432,9 +493,12 @@ void Engine::source_loop(int idx) {
   // with decode workers the CRC32C check moves off this thread (decode_fetch)
   cc.check_crcs = cfg_.check_crcs && cfg_.decode_threads <= 0;
   cc.auto_offset_reset = cfg_.start_offset == "earliest" ? "earliest" : "latest";
+  const int slot = idx % (int)slot_dev_.size();
+  const std::shared_ptr<PinnedPool> pinned = pools_[(size_t)slot];
+  Batcher& batcher = *batchers_[(size_t)slot];
   kafka::BufferAlloc alloc = kafka::heap_alloc;
-  if (pinned_) {
-    std::shared_ptr<PinnedPool> pool = pinned_;
+  if (pinned) {
+    std::shared_ptr<PinnedPool> pool = pinned;
     alloc = [pool](size_t n) {
       bool pinned = false;
       return pool->alloc(n, &pinned);
@@ -530,16 +594,17 @@ void Engine::source_loop(int idx) {
     }
     for (auto& f : fs) {
       FetchItem it;
-      it.pinned = pinned_ && pinned_->owns(f.buf.get());
+      it.pinned = pinned && pinned->owns(f.buf.get());
       it.f = std::move(f);
       it.source = idx;
+      it.slot = slot;
       it.t_fetch_ns = now;
       if (cfg_.decode_threads <= 0) {
         good.clear();
         decode_fetch(it, good, idx);
         // when stopping with a full queue the rest stays pending (never committed, so a
         // restart with start_offset=committed re-reads it)
-        if (!good.empty()) batcher_->push_many(good, stopping_);
+        if (!good.empty()) batcher.push_many(good, stopping_);
       } else {
         std::unique_lock<std::mutex> lk(dec_mu_);
         dec_space_cv_.wait(lk, [&] { return dec_q_.size() < (size_t)(4 * cfg_.decode_threads) ||
@@ -586,16 +651,17 @@ void Engine::decode_loop(int idx) {
       decode_fetch(it, good, idx);
     }
     ns_decode_ += mono_ns() - t0;
-    if (!good.empty()) batcher_->push_many(good, stopping_);
+    if (!good.empty()) batchers_[(size_t)it.slot]->push_many(good, stopping_);
   }
 }
 
 // GPU ingest of one pinned fetch buffer (ingest.h): bounded envelope checks on the host, batch
 // CRCs and image counts on the device. False = not applicable (the caller takes the host path).
 bool Engine::ingest_fetch(FetchItem& it, std::vector<InRecord>& good, int lane) {
-  if (!ingest_ || !it.pinned || ingest_failed_) return false;
+  Ingest* ingest = ingest_for(it.slot);
+  if (!ingest || !it.pinned || ingest_failed_) return false;
   kafka::Fetched& f = it.f;
-  uint8_t* dev = pinned_->mirror(f.buf.get());
+  uint8_t* dev = pools_[(size_t)it.slot]->mirror(f.buf.get());
   if (!dev) return false;
   const int64_t t0 = mono_ns();
   const size_t n = f.records.size();
@@ -615,7 +681,7 @@ bool Engine::ingest_fetch(FetchItem& it, std::vector<InRecord>& good, int lane) 
     io.arr_len[i] = s.arr_len;
   }
   try {
-    ingest_->run(lane, f, dev, cfg_.check_crcs && !f.crc_checked, cfg_.H, cfg_.W, cfg_.C, io);
+    ingest->run(lane, f, dev, cfg_.check_crcs && !f.crc_checked, cfg_.H, cfg_.W, cfg_.C, io);
   } catch (const std::exception& e) {
     if (!ingest_failed_.exchange(true))
       fprintf(stderr, "[gale decode] GPU ingest failed (%s): host decode from now on\n", e.what());
@@ -626,7 +692,7 @@ bool Engine::ingest_fetch(FetchItem& it, std::vector<InRecord>& good, int lane) 
     if (!io.batch_ok[b])
       for (size_t i = 0; i < f.batches[b].nrec; ++i) corrupt[f.batches[b].first_rec + i] = 1;
   kafka::Producer* prod = producer_for(it.source);
-  const int dev_id = ingest_->device();
+  const int dev_id = ingest->device();
   for (size_t i = 0; i < n; ++i) {
     const kafka::RecordRef& rr = f.records[i];
     InRecord r;
@@ -803,7 +869,7 @@ void Engine::serve(ReplicaSlot* rs) {
     }
     ++replica_failures_;
     requeued_ += (int64_t)back.size();
-    if (!back.empty()) batcher_->requeue(std::move(back));
+    if (!back.empty()) batchers_[(size_t)rs->slot]->requeue(std::move(back));
   };
   while (rs->alive) {
     if (mine.size() < depth) {
@@ -813,9 +879,27 @@ void Engine::serve(ReplicaSlot* rs) {
       bool open;
       {
         trace::Range tr("gale:batch");
-        open = batcher_->take(eff_batch_.load(std::memory_order_relaxed),
-                              eff_wait_ns_.load(std::memory_order_relaxed), !mine.empty(),
-                              b->recs, images);
+        const int maxb = eff_batch_.load(std::memory_order_relaxed);
+        const bool steal = batchers_.size() > 1;
+        open = batchers_[(size_t)rs->slot]->take(maxb,
+                                                 eff_wait_ns_.load(std::memory_order_relaxed),
+                                                 !mine.empty(), b->recs, images,
+                                                 steal ? 2000000 : 0);
+        if (open && steal && b->recs.empty() && mine.empty()) {
+          // idle: take from the most loaded other locality (its text then comes over PCIe
+          // from the pinned host copy instead of the device mirror)
+          Batcher* victim = nullptr;
+          int64_t most = maxb / 2;
+          for (size_t k = 0; k < batchers_.size(); ++k) {
+            if ((int)k == rs->slot) continue;
+            const int64_t q = batchers_[k]->queued_images();
+            if (q >= most) {
+              most = q;
+              victim = batchers_[k].get();
+            }
+          }
+          if (victim && victim->try_take(maxb, b->recs, images)) ++steals_;
+        }
       }
       ns_take_ += mono_ns() - t_take0;
       if (!open) {
@@ -883,7 +967,9 @@ void Engine::slo_step() {
   const int64_t max_wait = (int64_t)cfg_.max_wait_us * 1000, min_wait = 20000;
   int b = eff_batch_.load();
   int64_t w = eff_wait_ns_.load();
-  const bool backlog = (int64_t)batcher_->size() > (int64_t)b * (int64_t)replicas_.size();
+  size_t queued = 0;
+  for (auto& q : batchers_) queued += q->size();
+  const bool backlog = (int64_t)queued > (int64_t)b * (int64_t)replicas_.size();
   if (p99_ms > cfg_.slo_p99_ms) {
     if (backlog) {
       b = std::min(maxb, b + std::max(1, maxb / 8));  // overload: capacity first
@@ -925,7 +1011,7 @@ void Engine::watchdog_loop() {
               "re-queued\n", rs->index, rs->rep->name().c_str(), cfg_.watchdog_ms, back.size());
       ++replica_failures_;
       requeued_ += (int64_t)back.size();
-      batcher_->requeue(std::move(back));
+      batchers_[(size_t)rs->slot]->requeue(std::move(back));
     }
   }
 }
@@ -1076,7 +1162,11 @@ std::map<std::string, double> Engine::stats() const {
     s["fetch_lag_records"] = (double)fetch_lag;  // log end - next fetch
   }
   s["batches"] = (double)batches_total_;
-  s["queue_records"] = (double)const_cast<Batcher*>(batcher_.get())->size();
+  size_t queued = 0;
+  for (auto& q : batchers_) queued += q->size();
+  s["queue_records"] = (double)queued;
+  s["locality_slots"] = (double)batchers_.size();
+  s["steals"] = (double)steals_;
   for (int i = 1; i < 8; ++i)
     s[std::string("err_") + codec::status_name(i)] = (double)err_by_status_[i];
   const double el = (double)(t_last_ns_ - t_first_ns_) * 1e-9;

@@ -67,6 +67,9 @@ struct EngineConfig {
   int rebalance_timeout_ms = 8000;
   int heartbeat_interval_ms = 500;
   std::string assignor = "range";  // range | roundrobin
+  // NUMA placement: device -> CPUs for the threads serving it (replica workers, the sources of
+  // its locality slot); empty = no pinning
+  std::map<int, std::vector<int>> device_cpus;
   // sink (R5, R9, E7-E9)
   int sink_parallelism = 2;        // KAFKA_BOLT_PARAL (MainTopology.java:28)
   int acks = 1;                    // MainTopology.java:113
@@ -159,6 +162,7 @@ class Engine {
   struct FetchItem {
     kafka::Fetched f;
     int source = 0;
+    int slot = 0;  // locality slot of the source (its batcher, pool and ingest device)
     int64_t t_fetch_ns = 0;
     bool pinned = false;
   };
@@ -192,7 +196,8 @@ class Engine {
 
   EngineConfig cfg_;
   std::vector<std::shared_ptr<ReplicaSlot>> replicas_;
-  std::unique_ptr<Batcher> batcher_;
+  std::vector<std::unique_ptr<Batcher>> batchers_;  // one per locality slot
+  std::vector<int> slot_dev_;                         // slot -> replica device (-1: CPU)
   std::vector<std::unique_ptr<kafka::Producer>> producers_;
   std::vector<std::thread> sources_, workers_, decoders_;
   std::vector<std::unique_ptr<SourceCtl>> src_ctl_;
@@ -200,8 +205,11 @@ class Engine {
   std::atomic<bool> group_stop_{false};
   std::atomic<int64_t> rebalances_{0};
   std::atomic<int> assigned_partitions_{0}, generation_{-1};
-  std::shared_ptr<PinnedPool> pinned_;
-  std::shared_ptr<Ingest> ingest_;
+  std::vector<std::shared_ptr<PinnedPool>> pools_;    // per locality slot (null: heap)
+  std::map<int, std::shared_ptr<Ingest>> ingests_;    // device -> GPU ingest
+  Ingest* ingest_for(int slot);
+  void pin_thread(int device);
+  std::atomic<int64_t> steals_{0};
   std::atomic<bool> ingest_failed_{false};
   std::atomic<int64_t> ingested_records_{0}, ingest_ns_{0};
   std::mutex dec_mu_;

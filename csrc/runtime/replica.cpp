@@ -17,9 +17,9 @@ namespace gale {
 // ---------------------------------------------------------------------------------------------
 
 StubReplica::StubReplica(int H, int W, int C, int classes, int max_images, int delay_us,
-                         bool compute)
+                         bool compute, int locality)
     : H_(H), W_(W), C_(C), classes_(classes), max_images_(max_images), delay_us_(delay_us),
-      compute_(compute) {
+      compute_(compute), locality_(locality) {
   x_.resize((size_t)max_images * H * W * C);
   probs_.resize((size_t)max_images * classes);
 }

@@ -57,6 +57,9 @@ class Replica {
   virtual void submit(Batch& b) = 0;
   virtual void wait(Batch& b) = 0;
   virtual int device() const { return -1; }
+  // locality slot key: replicas with the same key share a batcher and fetch-buffer pool (the
+  // device for GPU replicas; stub replicas take a tag so the scheme is testable on CPU)
+  virtual int locality() const { return device(); }
   // Supervisor restart after submit/wait threw (its in-flight batches were already re-queued):
   // bring the replica back to an idle, usable state or throw if it cannot be.
   virtual void recover() {}
@@ -67,8 +70,10 @@ class Replica {
 // followed by softmax. An optional per-batch delay emulates device time.
 class StubReplica : public Replica {
  public:
-  StubReplica(int H, int W, int C, int classes, int max_images, int delay_us, bool compute = true);
+  StubReplica(int H, int W, int C, int classes, int max_images, int delay_us, bool compute = true,
+              int locality = -1);
   std::string name() const override { return "stub"; }
+  int locality() const override { return locality_; }
   int max_images() const override { return max_images_; }
   int depth() const override { return 1; }
   void submit(Batch& b) override;
@@ -76,7 +81,8 @@ class StubReplica : public Replica {
 
  private:
   int H_, W_, C_, classes_, max_images_, delay_us_;
-  bool compute_;  // false: a "null" replica (uniform softmax, no parsing) to measure host paths
+  bool compute_;
+  int locality_ = -1;  // false: a "null" replica (uniform softmax, no parsing) to measure host paths
   std::vector<float> x_, probs_;
 };
 

@@ -23,6 +23,22 @@ from gale.config import GaleConfig
 from gale.models import get_model
 
 
+def device_cpus(device: int) -> set:
+    """CPUs of the GPU's NUMA node within this process's affinity (empty when unknown)."""
+    import os
+
+    from gale.utils import _parse_cpulist, gpu_numa_node
+
+    node = gpu_numa_node(device)
+    if node < 0:
+        return set()
+    try:
+        with open(f"/sys/devices/system/node/node{node}/cpulist") as f:
+            return _parse_cpulist(f.read()) & os.sched_getaffinity(0)
+    except OSError:
+        return set()
+
+
 def replica_devices(n_replicas: int, devices: Sequence[int]) -> List[int]:
     if not devices:
         raise ValueError("no devices to place replicas on")
@@ -32,31 +48,41 @@ def replica_devices(n_replicas: int, devices: Sequence[int]) -> List[int]:
 class Engine:
     def __init__(self, cfg: GaleConfig, devices: Optional[Sequence[int]] = None,
                  max_records: int = -1, params: Optional[dict] = None,
-                 model_replicas: Optional[list] = None):
+                 model_replicas: Optional[list] = None, stub_localities: Sequence[int] = ()):
         self.cfg = cfg
         self.net = get_model(cfg.model)
         H, W, C = self.net.input_shape
         d = cfg.engine_dict(H, W, C, self.net.classes)
         d["max_records"] = max_records
-        self._native = native().Engine(d)
         self.model_replicas: list = []
         self.devices: List[int] = []
         if cfg.stub:
-            for _ in range(max(1, cfg.replicas)):
-                self._native.add_stub_replica(cfg.max_batch, 0, not cfg.stub_null)
+            self._native = native().Engine(d)
+            for i in range(max(1, cfg.replicas)):
+                loc = stub_localities[i % len(stub_localities)] if stub_localities else -1
+                self._native.add_stub_replica(cfg.max_batch, 0, not cfg.stub_null, loc)
             return
         if model_replicas is not None:
             reps = list(model_replicas)
         else:
             reps = self._build_gpu_replicas(devices, params)
+        devs = sorted({r.device.index or 0 for r in reps}, key=[r.device.index or 0
+                                                                for r in reps].index)
+        if len(devs) > 1 and cfg.numa_pin:
+            # single-process multi-GPU: each GPU's replica workers and sources run on the CPUs
+            # of that GPU's NUMA node (its pinned fetch buffers are first-touched there)
+            d["device_cpus"] = {dev: sorted(device_cpus(dev)) for dev in devs}
+        self._native = native().Engine(d)
         for rep in reps:
             self._native.add_gpu_replica(rep.executor, cfg.use_graph, cfg.gpu_wait_poll_us)
             self.model_replicas.append(rep)
             self.devices.append(rep.device.index or 0)
-        if cfg.gpu_ingest and len(set(self.devices)) == 1:
-            # one device: fetch buffers are mirrored on it once and parsed in place
-            self._native.enable_gpu_ingest(self.devices[0], max(1, cfg.decode_threads) +
-                                           cfg.source_parallelism, 20)
+        if cfg.gpu_ingest:
+            # fetch buffers of each device's sources are mirrored on that device once and
+            # parsed in place
+            for dev in devs:
+                self._native.enable_gpu_ingest(dev, max(1, cfg.decode_threads) +
+                                               cfg.source_parallelism, 20)
 
     def _build_gpu_replicas(self, devices: Optional[Sequence[int]], params: Optional[dict]):
         import torch
@@ -75,16 +101,18 @@ class Engine:
             from gale.models.weights_io import load_params
 
             params = load_params(self.cfg.weights, self.net)
-        packed: Dict[int, "torch.Tensor"] = {}
+        placement = replica_devices(n_rep, devices)
+        used = sorted(set(placement), key=placement.index)
+        src = materialize_weights(self.net, torch.device("cuda", used[0]), seed=self.cfg.seed,
+                                  wdtype=wdtype, params=params, fold_bn=self.cfg.fold_bn)
+        if len(used) > 1:  # one process, several GPUs: RCCL broadcast over xGMI
+            from gale.parallel.weights import replicate_weights
+
+            packed: Dict[int, "torch.Tensor"] = dict(zip(used, replicate_weights(src, used)))
+        else:
+            packed = {used[0]: src}
         reps = []
-        for dev in replica_devices(n_rep, devices):
-            if dev not in packed:
-                if not packed:
-                    packed[dev] = materialize_weights(self.net, torch.device("cuda", dev),
-                                                      seed=self.cfg.seed, wdtype=wdtype,
-                                                      params=params, fold_bn=self.cfg.fold_bn)
-                else:  # same process: device-to-device copy over xGMI
-                    packed[dev] = next(iter(packed.values())).to(torch.device("cuda", dev))
+        for dev in placement:
             reps.append(ModelReplica(self.net, packed[dev], max_batch=self.cfg.max_batch,
                                      slots=3, wdtype=wdtype, fold_bn=self.cfg.fold_bn))
         for r in reps:

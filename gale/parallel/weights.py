@@ -9,7 +9,7 @@ without knowing any values.
 
 from __future__ import annotations
 
-from typing import Optional
+from typing import List, Optional
 
 import torch
 import torch.distributed as dist
@@ -41,3 +41,17 @@ def materialize_weights(net: Network, device: torch.device, seed: int = 0, wdtyp
     if distributed:
         dist.broadcast(buf, src=src, group=group)  # RCCL over xGMI with the "nccl" backend
     return buf
+
+
+def replicate_weights(src: torch.Tensor, devices: List[int]) -> List[torch.Tensor]:
+    """One copy of the packed buffer per device of THIS process: an in-process RCCL
+    communicator (ncclCommInitAll) broadcasts it from ``src``'s device over xGMI
+    (csrc/comm/rccl.cpp). ``src``'s device must be one of ``devices`` (the root)."""
+    from gale._native import native
+
+    root = devices.index(src.device.index or 0)
+    out = [src if i == root else torch.empty_like(src, device=torch.device("cuda", d))
+           for i, d in enumerate(devices)]
+    comm = native().comm.CommGroup(list(devices))
+    comm.broadcast(src.data_ptr(), [t.data_ptr() for t in out], src.numel(), root)
+    return out

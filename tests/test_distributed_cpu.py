@@ -101,3 +101,19 @@ def test_scaling_driver_stub_1_2():
     assert [r["n_gpus"] for r in lines[:2]] == [1, 2]
     sc = lines[-1]["scaling"]
     assert set(sc) == {"1", "2"} and sc["1"]["efficiency"] == 1.0 and sc["2"]["efficiency"] > 0
+
+
+def test_scaling_driver_single_process_mode():
+    """tools/scaling.py --mode single-process: ONE bench.py process drives N "GPUs" (stub
+    replicas in N locality slots) - the single-process multi-GPU serving mode."""
+    cmd = [sys.executable, "tools/scaling.py", "--gpus", "1,2", "--stub", "--steps", "4",
+           "--warmup", "1", "--timeout", "240", "--mode", "single-process", "--",
+           "--batch", "32", "--distinct", "64", "--step-images", "512", "--min-warmup-s", "0.2",
+           "--replicas-per-gpu", "2", "--stub-null", "--timeout", "120"]
+    out = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=600,
+                         env=dict(os.environ, OMP_NUM_THREADS="1"))
+    assert out.returncode == 0, out.stdout[-3000:] + out.stderr[-3000:]
+    lines = [json.loads(x) for x in out.stdout.splitlines() if x.startswith("{")]
+    assert [r["n_gpus"] for r in lines[:2]] == [1, 2]
+    assert lines[1]["config"]["processes"] == 1 and lines[1]["config"]["partitions"] == 4
+    assert lines[-1]["mode"] == "single-process"

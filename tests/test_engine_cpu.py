@@ -236,3 +236,31 @@ def test_output_key_input_correlates_every_record(broker):
         np.testing.assert_allclose(got, stub_probs(xs[r["key"]]), rtol=1e-5, atol=1e-7)
     _, out2 = run(broker, 24)  # default: unkeyed (a fresh group reads the topic again)
     assert all(r["key"] is None for r in out2[-24:])
+
+
+def test_locality_slots_and_work_stealing(broker):
+    """Replicas of two localities (two GPUs of one process, emulated with stub tags): each
+    locality has its own sources/batcher; when one locality's replicas are starved the other's
+    backlog is stolen, and every record is served exactly once."""
+    rng = np.random.default_rng(11)
+    keys = set()
+    for i in range(200):
+        k = f"s{i}".encode()
+        keys.add(k)
+        # every record on partition 0 -> only source 0 (locality 0) has input
+        broker.append("in", 0, [C.encode_instances(rng.random((1, H, W, CH),
+                                                               dtype=np.float32))], [k])
+    cfg = make_cfg(broker, replicas=4, source_parallelism=2, output_key="input", max_batch=8,
+                   queue_depth=256)
+    eng = Engine(cfg, max_records=200, stub_localities=(0, 1))
+    eng.start()
+    assert eng.wait(30), eng.stats()
+    eng.stop()
+    st = eng.stats()
+    assert st["locality_slots"] == 2
+    out = broker.read("out", 0)
+    assert sorted(r["key"] for r in out) == sorted(keys)
+    served = [r["records"] for r in eng.replica_stats()]
+    # replicas 1 and 3 (locality 1) had no input of their own: whatever they served was stolen
+    assert sum(served) == 200
+    assert st["steals"] > 0 and served[1] + served[3] > 0

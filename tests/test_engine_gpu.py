@@ -79,7 +79,7 @@ def test_gpu_json_parse_matches_host():
     out, st = gpu_parse(recs, H, Wd, Cc)
     assert list(st) == [0, 0, 0, 0]
     ref = np.concatenate(xs)
-    np.testing.assert_allclose(out, ref, rtol=1e-6, atol=0)
+    np.testing.assert_array_equal(out, ref)  # correctly rounded: bit-exact round trip
 
 
 def test_gpu_json_parse_multi_tile():
@@ -104,7 +104,7 @@ def test_gpu_json_parse_multi_tile():
     recs.append((txt[:cut] + b" " * 300 + txt[cut:cut + 1] + b"\n" * 200 + txt[cut + 1:], n))
     out, st = gpu_parse(recs, H, Wd, Cc)
     assert list(st) == [0] * len(recs)
-    np.testing.assert_allclose(out, np.concatenate(xs), rtol=1e-6, atol=0)
+    np.testing.assert_array_equal(out, np.concatenate(xs))
 
 
 def test_gpu_json_parse_multi_tile_errors():

@@ -32,11 +32,12 @@ def free_port() -> int:
         return s.getsockname()[1]
 
 
-def bench_cmd(n: int, steps: int, warmup: int, extra: list, stub: bool = False) -> list:
+def bench_cmd(n: int, steps: int, warmup: int, extra: list, stub: bool = False,
+              single_process: bool = False) -> list:
     args = [os.path.join(ROOT, "bench.py"), "--gpus", str(n), "--steps", str(steps),
             "--warmup", str(warmup)] + (["--stub"] if stub else []) + list(extra)
-    if n == 1:
-        return [sys.executable] + args
+    if n == 1 or single_process:  # one process drives all n GPUs
+        return [sys.executable] + args + (["--single-process"] if single_process else [])
     return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
             f"--nproc-per-node={n}", "--master-addr", "127.0.0.1",
             "--master-port", str(free_port())] + args
@@ -66,18 +67,31 @@ def main(argv=None) -> int:
     ap.add_argument("--stub", action="store_true", help="CPU stub replicas (gloo; plumbing)")
     ap.add_argument("--timeout", type=float, default=900.0, help="seconds per bench run")
     ap.add_argument("--out", default="", help="also append the JSON lines to this file")
+    ap.add_argument("--mode", default="per-process",
+                    choices=["per-process", "single-process", "both"],
+                    help="per-process: one torch.distributed rank per GPU; single-process: one "
+                         "engine driving every GPU (bench.py --single-process)")
     ap.add_argument("extra", nargs=argparse.REMAINDER, help="-- extra bench.py arguments")
     a = ap.parse_args(argv)
     extra = a.extra[1:] if a.extra[:1] == ["--"] else a.extra
     counts = [int(x) for x in a.gpus.split(",") if x.strip()]
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", MASTER_ADDR="127.0.0.1")
+    modes = ["per-process", "single-process"] if a.mode == "both" else [a.mode]
+    rc = 0
+    for mode in modes:
+        rc |= sweep(a, counts, extra, env, mode)
+    return rc
+
+
+def sweep(a, counts, extra, env, mode) -> int:
     results = {}
     pinned: list = []
     for n in counts:
         # weak scaling compares equal per-GPU work: every N > first runs with the per-GPU
         # configuration the first run chose for itself (bench.py sizes replicas per GPU from the
         # rank's CPU share, which shrinks as more ranks share the node's CPUs)
-        cmd = bench_cmd(n, a.steps, a.warmup, extra + pinned, a.stub)
+        cmd = bench_cmd(n, a.steps, a.warmup, extra + pinned, a.stub,
+                        single_process=mode == "single-process")
         try:
             p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True,
                                timeout=a.timeout)
@@ -102,14 +116,13 @@ def main(argv=None) -> int:
             with open(a.out, "a") as f:
                 f.write(json.dumps(r) + "\n")
     eff = efficiency(results)
-    summary = {"scaling": {str(n): {"images_per_s": r["value"],
-                                    "p50_ms": r.get("p50_latency_ms"),
-                                    "p99_ms": r.get("p99_latency_ms"),
-                                    "efficiency": eff.get(n),
-                                    "replicas_per_gpu": r["config"].get("replicas_per_gpu"),
-                                    "global_batch": r["config"].get("global_batch"),
-                                    "cpu_cores_busy_rank0": r.get("cpu_cores_busy_rank0")}
-                           for n, r in sorted(results.items())}}
+    summary = {"mode": mode, "scaling": {
+        str(n): {"images_per_s": r["value"], "p50_ms": r.get("p50_latency_ms"),
+                 "p99_ms": r.get("p99_latency_ms"), "efficiency": eff.get(n),
+                 "replicas_per_gpu": r["config"].get("replicas_per_gpu"),
+                 "global_batch": r["config"].get("global_batch"),
+                 "cpu_cores_busy_rank0": r.get("cpu_cores_busy_rank0")}
+        for n, r in sorted(results.items())}}
     print(json.dumps(summary), flush=True)
     return 0 if len(results) == len(counts) else 1
 
