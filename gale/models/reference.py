@@ -28,13 +28,17 @@ def forward(net: Network, params: Dict[str, torch.Tensor], x_nhwc: torch.Tensor,
             folded: bool = True, bn_stats: Dict[str, torch.Tensor] | None = None,
             collect: Dict[str, torch.Tensor] | None = None,
             tensors: Dict[str, torch.Tensor] | None = None,
-            fp8_scales: Dict[str, float] | None = None) -> torch.Tensor:
+            fp8_scales: Dict[str, float] | None = None,
+            bf16: bool = False) -> torch.Tensor:
     """fp32 forward. ``folded``: params come from ``fold_params`` (conv bias already has BN).
 
     With ``folded=False`` BatchNorm is applied from its running statistics (or, when ``bn_stats``
     is a dict, from batch statistics that are written into it — calibration mode). ``tensors``
     receives every activation (NCHW). ``fp8_scales`` turns this into the emulation of the fp8
     kernel path: e4m3 per-channel weights and every activation rounded to e4m3 at its scale.
+    ``bf16`` emulates the bf16 kernel path: conv weights and the network input rounded to bf16,
+    every stored activation rounded to bf16 (fp32 accumulation, fp32 bias and head), so the
+    kernels can be held to accumulation-order differences against it.
     """
     if fp8_scales is not None:
         from gale.models.quant import e4m3_round, fake_quant_weight
@@ -42,14 +46,19 @@ def forward(net: Network, params: Dict[str, torch.Tensor], x_nhwc: torch.Tensor,
         def q(name, v):
             s = fp8_scales[name]
             return e4m3_round(v / s) * s
+    def rb(v):  # round to bf16 and back
+        return v.to(torch.bfloat16).float() if bf16 else v
+
     x0 = x_nhwc.float().permute(0, 3, 1, 2)
-    t: Dict[str, torch.Tensor] = {"input": q("input", x0) if fp8_scales is not None else x0}
+    t: Dict[str, torch.Tensor] = {"input": q("input", x0) if fp8_scales is not None
+                                  else rb(x0)}
     out = None
     for L in net.layers:
         if isinstance(L, Conv):
             w = params[f"{L.name}.weight"]
             if fp8_scales is not None:
                 w = fake_quant_weight(w)
+            w = rb(w)
             b = params.get(f"{L.name}.bias")
             y = F.conv2d(t[L.inp], w, b, stride=L.stride, padding=L.pad)
             if not folded and L.bn:
@@ -69,11 +78,13 @@ def forward(net: Network, params: Dict[str, torch.Tensor], x_nhwc: torch.Tensor,
                 y = F.relu(y)
             if fp8_scales is not None and not L.out_f32:
                 y = q(L.out, y)
+            if not L.out_f32:
+                y = rb(y)
             t[L.out] = y
         elif isinstance(L, MaxPool):
             t[L.out] = F.max_pool2d(t[L.inp], L.k, L.s, L.p)
         elif isinstance(L, AvgPool):
-            t[L.out] = t[L.inp].mean(dim=(2, 3), keepdim=True)
+            t[L.out] = rb(t[L.inp].mean(dim=(2, 3), keepdim=True))
             if fp8_scales is not None:
                 t[L.out] = q(L.out, t[L.out])
         elif isinstance(L, Head):

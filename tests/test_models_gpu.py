@@ -1,7 +1,27 @@
-"""End-to-end model numerics: the gfx950 plan (eager and hipGraph replay) vs the fp32 oracle."""
+"""End-to-end model numerics: the gfx950 plan (eager and hipGraph replay) vs the fp32 oracle.
+
+Comparisons are on LOGITS (the softmax inverted: centered log-probabilities, exact up to the
+per-row constant the softmax removes), relative to the row's logit scale, so an error that
+would hide inside probabilities near 1/classes still fails."""
 
 import pytest
 import torch
+
+
+def logits(p: torch.Tensor) -> torch.Tensor:
+    lp = p.double().clamp_min(1e-300).log()
+    return lp - lp.mean(dim=1, keepdim=True)
+
+
+def rel_logit_err(p: torch.Tensor, ref: torch.Tensor) -> torch.Tensor:
+    """Per-row max |dlogit| / max(|ref logit|, 1)."""
+    a, b = logits(p), logits(ref)
+    return (a - b).abs().amax(1) / b.abs().amax(1).clamp_min(1.0)
+
+
+def margin(ref: torch.Tensor) -> torch.Tensor:
+    top2 = ref.topk(2, dim=1).values
+    return top2[:, 0] - top2[:, 1]
 
 from gale.models import fold_params, get_model, init_params
 from gale.models.reference import forward
@@ -23,11 +43,19 @@ def test_model_matches_reference(name, batch):
     eager = rep.infer_eager(x).cpu()
     graph = rep.infer(x, use_graph=True, slot=1).cpu()
     torch.cuda.synchronize()
+    emu = forward(net, fold_params(net, params), x, bf16=True)
     assert eager.shape == ref.shape
-    err = (eager - ref).abs().max().item()
-    assert err < 3e-2, f"{name}: max |p - p_ref| = {err}"
-    top2 = ref.topk(2, dim=1).values
-    clear = (top2[:, 0] - top2[:, 1]) > 0.05  # argmax must agree wherever it is not a near-tie
+    err = rel_logit_err(eager, ref).max().item()
+    e_emu = rel_logit_err(eager, emu).max().item()
+    budget = rel_logit_err(emu, ref).max().item()  # what bf16 storage alone costs
+    print(f"\n{name} bf16 rel logit err vs fp32 {err:.2e} (bf16 emulation vs fp32 "
+          f"{budget:.2e}), vs bf16 emulation {e_emu:.2e}")
+    # the kernels match the bf16 emulation up to accumulation order, and are no further from
+    # fp32 than bf16 storage itself puts them
+    # (deep nets amplify accumulation-order rounding flips: allow a fraction of the budget)
+    assert e_emu < max(1e-2, 0.35 * budget), f"{name}: vs bf16 emulation {e_emu}"
+    assert err < 1.5 * budget + 5e-3, f"{name}: relative logit error {err} (budget {budget})"
+    clear = margin(ref) > 0.05  # argmax must agree wherever it is not a near-tie
     assert torch.equal(eager.argmax(1)[clear], ref.argmax(1)[clear])
     # graph replay (bucket >= batch, padded tail) must equal eager bit for bit
     assert torch.equal(graph, eager)
@@ -55,9 +83,14 @@ def test_resnet50_gemm_convs_match_conv_mfma_and_fp32():
     finally:
         C.set_conv_path(0)
     ref = forward(net, fold_params(net, params), x)
+    emu = forward(net, fold_params(net, params), x, bf16=True)
     torch.cuda.synchronize()
-    assert (a - b).abs().max().item() < 1e-2
-    assert (a - ref).abs().max().item() < 3e-2
+    e_ab, e_emu = rel_logit_err(a, b).max().item(), rel_logit_err(a, emu).max().item()
+    e_ref, budget = rel_logit_err(a, ref).max().item(), rel_logit_err(emu, ref).max().item()
+    print(f"\nresnet50 gemm vs mfma {e_ab:.2e}, vs bf16 emulation {e_emu:.2e}, vs fp32 "
+          f"{e_ref:.2e} (budget {budget:.2e})")
+    assert e_ab < max(1e-2, 0.35 * budget) and e_emu < max(1e-2, 0.35 * budget)
+    assert e_ref < 1.5 * budget + 5e-3
     assert torch.allclose(a.sum(1), torch.ones(6), atol=1e-4)
 
 
@@ -77,14 +110,23 @@ def test_fp8_model_matches_emulation_and_fp32(name, batch):
     ref = forward(net, folded, x)
     got = rep.infer(x, use_graph=True).cpu()
     torch.cuda.synchronize()
-    e_emu = (got - emu).abs()
-    assert e_emu.mean().item() < 5e-3, f"{name}: mean |p - p_emu| = {e_emu.mean().item()}"
-    e_ref = (got - ref).abs()
-    assert e_ref.max().item() < 0.2 and e_ref.mean().item() < 0.02
-    top2 = ref.topk(2, dim=1).values
-    clear = (top2[:, 0] - top2[:, 1]) > 0.1
+    e_emu = rel_logit_err(got, emu)
+    e_ref = rel_logit_err(got, ref)
+    budget = rel_logit_err(emu, ref)  # what e4m3 quantisation alone costs
+    print(f"\n{name} fp8 vs emulation mean {e_emu.mean().item():.2e} max "
+          f"{e_emu.max().item():.2e}; vs fp32 mean {e_ref.mean().item():.2e} max "
+          f"{e_ref.max().item():.2e} (quantisation budget mean {budget.mean().item():.2e})")
+    # e4m3 rounding flips (fp32 summation order) compound with depth: ResNet-50's 53 layers
+    # decorrelate kernel and emulation up to the quantisation budget itself
+    frac = 1.0 if name == "resnet50" else 0.5
+    assert e_emu.mean().item() < max(1e-2, frac * budget.mean().item()), \
+        f"{name}: fp8 vs emulation {e_emu.mean().item()}"
+    # the kernels are no further from fp32 than the quantisation itself puts them
+    assert e_ref.mean().item() < 1.25 * budget.mean().item() + 5e-3
+    clear = margin(ref) > 0.05
     if clear.any():  # (1000-class random-init resnet50 has no clear winner)
-        assert (got.argmax(1)[clear] == ref.argmax(1)[clear]).float().mean().item() >= 0.9
+        agree = (got.argmax(1)[clear] == ref.argmax(1)[clear]).float().mean().item()
+        assert agree >= 0.97, f"{name}: fp8 argmax agreement {agree}"
 
 
 @pytest.mark.parametrize("batch", [1, 37, 600])
@@ -102,9 +144,13 @@ def test_resnet20_fused_matches_layerwise_and_fp32(batch):
     a = fused.infer(x, use_graph=True).cpu()
     b = layered.infer(x, use_graph=True).cpu()
     ref = forward(net, fold_params(net, params), x)
+    emu = forward(net, fold_params(net, params), x, bf16=True)
     torch.cuda.synchronize()
-    assert (a - b).abs().max().item() < 2e-3
-    assert (a - ref).abs().max().item() < 3e-2
+    e_ab, e_emu = rel_logit_err(a, b).max().item(), rel_logit_err(a, emu).max().item()
+    e_ref, budget = rel_logit_err(a, ref).max().item(), rel_logit_err(emu, ref).max().item()
+    print(f"\nresnet20 fused vs layered {e_ab:.2e}, vs bf16 emulation {e_emu:.2e}, vs fp32 "
+          f"{e_ref:.2e} (budget {budget:.2e})")
+    assert e_ab < 5e-3 and e_emu < 5e-3 and e_ref < 1.5 * budget + 5e-3
     assert torch.allclose(a.sum(1), torch.ones(batch), atol=1e-5)
     # eager launch equals graph replay
     assert torch.equal(fused.infer_eager(x).cpu(), a)
@@ -128,8 +174,11 @@ def test_resnet20_fp8_fused_matches_layerwise():
     torch.cuda.synchronize()
     # same quantised operands and rounding points; only fp32 summation order differs, which can
     # flip an occasional e4m3 rounding
-    assert (a - b).abs().mean().item() < 2e-3
-    assert (a - emu).abs().mean().item() < 5e-3
+    budget = rel_logit_err(emu, forward(net, fold_params(net, params), x)).mean().item()
+    e_ab, e_emu = rel_logit_err(a, b).mean().item(), rel_logit_err(a, emu).mean().item()
+    print(f"\nresnet20 fp8 fused vs layered mean {e_ab:.2e}, vs emulation {e_emu:.2e} "
+          f"(quantisation budget {budget:.2e})")
+    assert e_ab < 1e-3 and e_emu < 0.5 * budget
     assert (a.argmax(1) == b.argmax(1)).float().mean().item() > 0.97
 
 
@@ -146,12 +195,14 @@ def test_unfolded_bn_plan_matches_reference(name, batch):
     assert sum(op["kind"] == OP_BN_ACT for op in rep.ops) > 0
     x = torch.rand((batch,) + net.input_shape, generator=torch.Generator().manual_seed(4))
     ref = forward(net, fold_params(net, params), x)
+    budget = rel_logit_err(forward(net, fold_params(net, params), x, bf16=True), ref).max().item()
     eager = rep.infer_eager(x).cpu()
     graph = rep.infer(x, use_graph=True).cpu()
     torch.cuda.synchronize()
-    err = (eager - ref).abs().max().item()
-    assert err < 4e-2, f"{name}: max |p - p_ref| = {err}"
-    top2 = ref.topk(2, dim=1).values
-    clear = (top2[:, 0] - top2[:, 1]) > 0.05
+    err = rel_logit_err(eager, ref).max().item()
+    print(f"\n{name} unfolded-BN rel logit err {err:.2e} (budget {budget:.2e})")
+    # one more bf16 rounding point than the folded plan (the raw conv output before BN)
+    assert err < 2 * budget + 1e-2, f"{name}: relative logit error {err}"
+    clear = margin(ref) > 0.05
     assert torch.equal(eager.argmax(1)[clear], ref.argmax(1)[clear])
     assert torch.equal(graph, eager)
