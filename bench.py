@@ -72,7 +72,7 @@ def parse_args(argv=None):
     ap.add_argument("--max-wait-us", type=int, default=2000)
     ap.add_argument("--queue-batches", type=int, default=4,
                     help="records buffered in the engine, in units of --batch")
-    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp8"])
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp8", "fp32"])
     ap.add_argument("--slo-p99-ms", type=float, default=0.0,
                     help="latency-SLO mode: adapt the batch/wait bound to keep p99 under this")
     ap.add_argument("--stub", action="store_true", help="CPU stub replicas (no GPU)")

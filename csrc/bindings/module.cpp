@@ -53,6 +53,7 @@ ConvDesc desc_from_dict(const py::dict& d) {
   c.out_scale = get_or<float>(d, "out_scale", 1.0f);
   c.res_scale = get_or<float>(d, "res_scale", 1.0f);
   c.stem = get_or<int>(d, "stem", 0);
+  c.f32 = get_or<int>(d, "f32", 0);
   return c;
 }
 
@@ -78,7 +79,7 @@ gale::PlanOp op_from_dict(const py::dict& d) {
   if (d.contains("ptrs"))
     for (auto v : d["ptrs"].cast<std::vector<uintptr_t>>()) op.ptrs.push_back(P(v));
   if (d.contains("scales")) op.scales = d["scales"].cast<std::vector<float>>();
-  op.fp8 = get_or<int>(d, "fp8", 0);
+  op.fp8 = get_or<int>(d, "et", get_or<int>(d, "fp8", 0));  // pool/head activation ElemType
   op.scale = get_or<float>(d, "scale", 1.0f);
   return op;
 }

@@ -43,7 +43,7 @@ struct PlanOp {
   const float* wscale = nullptr;
   std::vector<const void*> ptrs;  // OP_RESNET20 parameter pointers
   std::vector<float> scales;      // OP_RESNET20 fp8 activation scales
-  int fp8 = 0;        // pool / head ops: e4m3 activations
+  int fp8 = 0;        // pool / head ops: activation ElemType (0 bf16, 1 e4m3, 2 fp32)
   float scale = 1.f;  // head: input activation scale (fp8)
 };
 

@@ -38,6 +38,9 @@ struct ConvDesc {
   // are [Npad][256] with k = kh*32 + kw*4 + c over an 8x8x4 zero-padded kernel (KH = KW = 8,
   // K = Kpad = 256), so each kernel row of one output pixel is ONE 64-byte run of x.
   int stem;
+  // 1 = reference-precision plan (--dtype fp32): x, w, residual and y are all fp32 and the conv
+  // runs on the fp32 matrix core (conv_f32.hip, v_mfma_f32_16x16x4_f32); Kpad % 16 == 0
+  int f32;
 };
 
 // y[B,Ho,Wo,Cout] = act(conv(x, w) + bias (+ residual)).
@@ -47,6 +50,12 @@ struct ConvDesc {
 // (x fp32 when in_f32, y fp32 when out_f32).
 hipError_t conv2d(const ConvDesc& d, int batch, const void* x, const void* w, const float* bias,
                   const float* wscale, const void* res, void* y, hipStream_t stream);
+hipError_t conv2d_f32(const ConvDesc& d, int batch, const void* x, const void* w,
+                      const float* bias, const void* res, void* y, hipStream_t stream);
+
+// Activation element types of the pooling / head kernels (their `et` argument; 1 was the old
+// fp8 flag, so fp8 callers are unchanged)
+enum ElemType : int { ET_BF16 = 0, ET_FP8 = 1, ET_F32 = 2 };
 
 // The LDS-pipelined implicit-GEMM path (conv_gemm.hip) for wide bf16 layers; conv2d() routes
 // there by itself when conv_gemm_supported() holds.
@@ -62,19 +71,19 @@ hipError_t conv2d_gemm(const ConvDesc& d, int batch, const void* x, const void* 
 hipError_t stem_pack(int batch, int H, int W, int C, int Wp, int lp, const float* x, void* y,
                      hipStream_t stream);
 
-// Max pooling, NHWC bf16 (or e4m3 when fp8; the scale passes through), window k, stride s,
-// -inf padding p.
+// Max pooling, NHWC bf16 / e4m3 (the scale passes through) / fp32 by `et` (ElemType), window k,
+// stride s, -inf padding p.
 hipError_t maxpool2d(int batch, int H, int W, int C, int k, int s, int p, int Ho, int Wo,
-                     const void* x, void* y, int fp8, hipStream_t stream);
+                     const void* x, void* y, int et, hipStream_t stream);
 
-// Global average pooling, NHWC bf16 / e4m3 [B,H,W,C] -> same type [B,C] (same scale).
-hipError_t avgpool_global(int batch, int HW, int C, const void* x, void* y, int fp8,
+// Global average pooling, NHWC [B,H,W,C] -> same type [B,C] (same scale), `et` = ElemType.
+hipError_t avgpool_global(int batch, int HW, int C, const void* x, void* y, int et,
                           hipStream_t stream);
 
 // Fused classifier head: optional global average pool over HW, dense layer with fp32 weights
-// w[N][C] + bias[N], then row softmax. x: bf16 (or e4m3 with scale in_scale) [B,HW,C]; out: fp32
-// [B,N]. One workgroup per image.
-hipError_t head_pool_dense_softmax(int batch, int HW, int C, int N, const void* x, int fp8,
+// w[N][C] + bias[N], then row softmax. x: bf16, e4m3 (scale in_scale) or fp32 [B,HW,C] by `et`
+// (ElemType); out: fp32 [B,N]. One workgroup per image.
+hipError_t head_pool_dense_softmax(int batch, int HW, int C, int N, const void* x, int et,
                                    float in_scale, const float* w, const float* bias, float* out,
                                    hipStream_t stream);
 

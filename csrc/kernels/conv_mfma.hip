@@ -409,6 +409,7 @@ int conv_n_tiles(int Cout) {
 hipError_t conv2d(const ConvDesc& d, int batch, const void* x, const void* w, const float* bias,
                   const float* wscale, const void* res, void* y, hipStream_t stream) {
   if (batch <= 0) return hipSuccess;
+  if (d.f32) return conv2d_f32(d, batch, x, w, bias, d.has_res ? res : nullptr, y, stream);
   const bool f8 = d.fp8 != 0;
   if (d.stem) {
     if (f8 || d.in_f32 || d.out_f32 || d.Cin != 4 || d.KH != 8 || d.KW != 8 || d.K != 256 ||

@@ -9,11 +9,16 @@
 namespace gale {
 namespace {
 
-// 8 channels of one pixel as floats (bf16 or e4m3 codes; e4m3 values are in units of the
-// tensor's scale, which pooling preserves)
-template <bool F8>
+// 8 channels of one pixel as floats (ET: ElemType; e4m3 values are in units of the tensor's
+// scale, which pooling preserves)
+template <int ET>
 __device__ __forceinline__ void load8f(const void* x, size_t off, float* v) {
-  if constexpr (F8) {
+  if constexpr (ET == ET_F32) {
+    const float4* p = reinterpret_cast<const float4*>(reinterpret_cast<const float*>(x) + off);
+    const float4 a = p[0], b = p[1];
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+    v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+  } else if constexpr (ET == ET_FP8) {
     const uint2 r = *reinterpret_cast<const uint2*>(reinterpret_cast<const uint8_t*>(x) + off);
     v[0] = __builtin_amdgcn_cvt_f32_fp8((int)r.x, 0);
     v[1] = __builtin_amdgcn_cvt_f32_fp8((int)r.x, 1);
@@ -30,9 +35,13 @@ __device__ __forceinline__ void load8f(const void* x, size_t off, float* v) {
   }
 }
 
-template <bool F8>
+template <int ET>
 __device__ __forceinline__ void store8f(void* y, size_t off, const float* v) {
-  if constexpr (F8) {
+  if constexpr (ET == ET_F32) {
+    float4* p = reinterpret_cast<float4*>(reinterpret_cast<float*>(y) + off);
+    p[0] = make_float4(v[0], v[1], v[2], v[3]);
+    p[1] = make_float4(v[4], v[5], v[6], v[7]);
+  } else if constexpr (ET == ET_FP8) {
     int lo = __builtin_amdgcn_cvt_pk_fp8_f32(v[0], v[1], 0, false);
     lo = __builtin_amdgcn_cvt_pk_fp8_f32(v[2], v[3], lo, true);
     int hi = __builtin_amdgcn_cvt_pk_fp8_f32(v[4], v[5], 0, false);
@@ -47,7 +56,7 @@ __device__ __forceinline__ void store8f(void* y, size_t off, const float* v) {
   }
 }
 
-template <bool F8>
+template <int ET>
 __global__ __launch_bounds__(256) void maxpool_kernel(int total, int H, int W, int C8, int k, int s,
                                                       int p, int Ho, int Wo, const void* x,
                                                       void* y) {
@@ -70,15 +79,15 @@ __global__ __launch_bounds__(256) void maxpool_kernel(int total, int H, int W, i
       const int wi = wo * s - p + kw;
       if ((unsigned)wi >= (unsigned)W) continue;
       float v[8];
-      load8f<F8>(x, ((size_t)(n * H + hi) * W + wi) * C + cg * 8, v);
+      load8f<ET>(x, ((size_t)(n * H + hi) * W + wi) * C + cg * 8, v);
 #pragma unroll
       for (int j = 0; j < 8; ++j) m[j] = fmaxf(m[j], v[j]);
     }
   }
-  store8f<F8>(y, (size_t)pix * C + cg * 8, m);  // max of e4m3 values re-encodes exactly
+  store8f<ET>(y, (size_t)pix * C + cg * 8, m);  // max of e4m3 values re-encodes exactly
 }
 
-template <bool F8>
+template <int ET>
 __global__ __launch_bounds__(256) void avgpool_kernel(int total, int HW, int C8, const void* x,
                                                       void* y) {
   const int i = blockIdx.x * 256 + threadIdx.x;
@@ -90,19 +99,19 @@ __global__ __launch_bounds__(256) void avgpool_kernel(int total, int HW, int C8,
   const size_t base = (size_t)n * HW * C + cg * 8;
   for (int q = 0; q < HW; ++q) {
     float v[8];
-    load8f<F8>(x, base + (size_t)q * C, v);
+    load8f<ET>(x, base + (size_t)q * C, v);
 #pragma unroll
     for (int j = 0; j < 8; ++j) s[j] += v[j];
   }
   const float inv = 1.f / (float)HW;
 #pragma unroll
   for (int j = 0; j < 8; ++j) s[j] *= inv;
-  store8f<F8>(y, (size_t)n * C + cg * 8, s);  // the mean keeps the input's scale
+  store8f<ET>(y, (size_t)n * C + cg * 8, s);  // the mean keeps the input's scale
 }
 
 // One workgroup per image: pooled[C] -> logits[N] -> softmax, all fp32 in LDS. fp8 inputs are
 // pooled in units of their scale, which is applied once to the pooled vector.
-template <bool F8>
+template <int ET>
 __global__ __launch_bounds__(256) void head_kernel(int HW, int C, int N, const void* x,
                                                    float in_scale, const float* w,
                                                    const float* bias, float* out) {
@@ -119,7 +128,7 @@ __global__ __launch_bounds__(256) void head_kernel(int HW, int C, int N, const v
     float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     for (int q = ps; q < HW; q += nps) {
       float v[8];
-      load8f<F8>(x, img + (size_t)q * C + cg * 8, v);
+      load8f<ET>(x, img + (size_t)q * C + cg * 8, v);
 #pragma unroll
       for (int j = 0; j < 8; ++j) s[j] += v[j];
     }
@@ -206,7 +215,7 @@ __global__ __launch_bounds__(256) void bn_act_kernel(int total, int HW, int Wo, 
   const int pix = i / C8;
   const size_t off = (size_t)pix * (C8 * 8) + cg * 8;
   float v[8];
-  load8f<false>(x, off, v);
+  load8f<ET_BF16>(x, off, v);
   if (scale) {
     const float4* s4 = reinterpret_cast<const float4*>(scale) + cg * 2;
     const float4* t4 = reinterpret_cast<const float4*>(shift) + cg * 2;
@@ -222,7 +231,7 @@ __global__ __launch_bounds__(256) void bn_act_kernel(int total, int HW, int Wo, 
     const int ho = q / Wo;
     const int wo = q - ho * Wo;
     float r[8];
-    load8f<false>(res, ((size_t)(n * res_H + ho * rs) * res_W + wo * rs) * res_C + cg * 8, r);
+    load8f<ET_BF16>(res, ((size_t)(n * res_H + ho * rs) * res_W + wo * rs) * res_C + cg * 8, r);
 #pragma unroll
     for (int j = 0; j < 8; ++j) v[j] += r[j];
   }
@@ -230,43 +239,47 @@ __global__ __launch_bounds__(256) void bn_act_kernel(int total, int HW, int Wo, 
 #pragma unroll
     for (int j = 0; j < 8; ++j) v[j] = fmaxf(v[j], 0.f);
   }
-  store8f<false>(y, off, v);
+  store8f<ET_BF16>(y, off, v);
 }
 
 }  // namespace
 
 hipError_t maxpool2d(int batch, int H, int W, int C, int k, int s, int p, int Ho, int Wo,
-                     const void* x, void* y, int fp8, hipStream_t stream) {
+                     const void* x, void* y, int et, hipStream_t stream) {
   if (batch <= 0) return hipSuccess;
-  if (C % 8) return hipErrorInvalidValue;
+  if (C % 8 || et < 0 || et > 2) return hipErrorInvalidValue;
   const int total = batch * Ho * Wo * (C / 8);
-  hipLaunchKernelGGL(fp8 ? maxpool_kernel<true> : maxpool_kernel<false>,
+  hipLaunchKernelGGL(et == ET_F32 ? maxpool_kernel<ET_F32>
+                     : et == ET_FP8 ? maxpool_kernel<ET_FP8> : maxpool_kernel<ET_BF16>,
                      dim3((total + 255) / 256), dim3(256), 0, stream, total, H, W, C / 8, k, s, p,
                      Ho, Wo, x, y);
   return hipGetLastError();
 }
 
-hipError_t avgpool_global(int batch, int HW, int C, const void* x, void* y, int fp8,
+hipError_t avgpool_global(int batch, int HW, int C, const void* x, void* y, int et,
                           hipStream_t stream) {
   if (batch <= 0) return hipSuccess;
-  if (C % 8) return hipErrorInvalidValue;
+  if (C % 8 || et < 0 || et > 2) return hipErrorInvalidValue;
   const int total = batch * (C / 8);
-  hipLaunchKernelGGL(fp8 ? avgpool_kernel<true> : avgpool_kernel<false>,
+  hipLaunchKernelGGL(et == ET_F32 ? avgpool_kernel<ET_F32>
+                     : et == ET_FP8 ? avgpool_kernel<ET_FP8> : avgpool_kernel<ET_BF16>,
                      dim3((total + 255) / 256), dim3(256), 0, stream, total, HW, C / 8, x, y);
   return hipGetLastError();
 }
 
-hipError_t head_pool_dense_softmax(int batch, int HW, int C, int N, const void* x, int fp8,
+hipError_t head_pool_dense_softmax(int batch, int HW, int C, int N, const void* x, int et,
                                    float in_scale, const float* w, const float* bias, float* out,
                                    hipStream_t stream) {
   if (batch <= 0) return hipSuccess;
-  if (C % 8 || C > 4096 || N > 4096) return hipErrorInvalidValue;
+  if (C % 8 || C > 4096 || N > 4096 || et < 0 || et > 2) return hipErrorInvalidValue;
   const int C8 = C / 8;
   const int nps = 256 / C8 > 0 ? 256 / C8 : 1;
   const size_t lds = ((size_t)nps * C + C + N) * sizeof(float);
   if (lds > 160 * 1024) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(fp8 ? head_kernel<true> : head_kernel<false>, dim3(batch), dim3(256), lds,
-                     stream, HW, C, N, x, fp8 ? in_scale : 1.f, w, bias, out);
+  hipLaunchKernelGGL(et == ET_F32 ? head_kernel<ET_F32>
+                     : et == ET_FP8 ? head_kernel<ET_FP8> : head_kernel<ET_BF16>,
+                     dim3(batch), dim3(256), lds, stream, HW, C, N, x,
+                     et == ET_FP8 ? in_scale : 1.f, w, bias, out);
   return hipGetLastError();
 }
 

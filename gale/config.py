@@ -24,9 +24,10 @@ CHOICES = {
     "on_error": ("null", "error-json", "drop"),
     "output_key": ("none", "input"),
     "assignor": ("range", "roundrobin"),
-    # compute dtype of the GPU kernels (MFMA bf16 / OCP e4m3 fp8); inputs and the softmax
-    # output stay fp32 as in the reference's TF graph (InferenceBolt.java:80-86)
-    "dtype": ("bf16", "fp8"),
+    # compute dtype of the GPU kernels (MFMA bf16 / OCP e4m3 fp8 serving plans; fp32 = the
+    # reference-precision plan on the fp32 matrix core, every tensor binary32 like the
+    # reference's TF graph, InferenceBolt.java:80-86); inputs and the softmax output are fp32
+    "dtype": ("bf16", "fp8", "fp32"),
     "model": ("lenet5", "resnet20", "resnet50"),
 }
 

@@ -96,7 +96,7 @@ class Engine:
             n = torch.cuda.device_count()
             devices = list(range(n if self.cfg.gpus <= 0 else min(self.cfg.gpus, n)))
         n_rep = self.cfg.replicas if self.cfg.replicas > 0 else len(devices)
-        wdtype = "fp8" if self.cfg.dtype == "fp8" else "bf16"
+        wdtype = self.cfg.dtype  # bf16 | fp8 | fp32 (packed weight / activation type)
         if params is None and self.cfg.weights:
             from gale.models.weights_io import load_params
 

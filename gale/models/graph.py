@@ -264,6 +264,8 @@ def _conv_geometry(net: Network, L: Conv, wdtype: str = "bf16") -> Dict[str, int
     Kpad = round_up(K, 32)
     nt = conv_n_tiles(cout_s)
     Npad = round_up(cout_s, nt * 16)
+    if wdtype == "fp32":  # conv_f32.hip: K chunks of 16, 64-channel tiles (rows >= Npad read 0)
+        Kpad, Npad = round_up(K, 16), cout_s
     return dict(H=h, W=w, Cin=cin_s, Ho=ho, Wo=wo, Cout=cout_s, KH=L.k, KW=L.k, stride=L.stride,
                 pad=L.pad, K=K, Kpad=Kpad, Npad=Npad)
 
@@ -274,7 +276,7 @@ def param_layout(net: Network, wdtype: str = "bf16",
     ``fold_bn=False`` (bf16 only) adds a BN scale and shift vector per BatchNorm conv."""
     if not fold_bn and wdtype != "bf16":
         raise ValueError("the unfolded-BN plan is bf16 only")
-    wbytes = {"bf16": 2, "fp8": 1}[wdtype]
+    wbytes = {"bf16": 2, "fp8": 1, "fp32": 4}[wdtype]
     layout: Dict[str, PackedEntry] = {}
     off = 0
 
@@ -286,7 +288,7 @@ def param_layout(net: Network, wdtype: str = "bf16",
     for L in net.layers:
         if isinstance(L, Conv):
             gm = _conv_geometry(net, L, wdtype)
-            wdt = torch.bfloat16 if wdtype == "bf16" else torch.uint8
+            wdt = {"bf16": torch.bfloat16, "fp8": torch.uint8, "fp32": torch.float32}[wdtype]
             add(f"{L.name}.w", gm["Npad"] * gm["Kpad"] * wbytes, wdt, (gm["Npad"], gm["Kpad"]))
             add(f"{L.name}.b", gm["Npad"] * 4, torch.float32, (gm["Npad"],))
             if wdtype == "fp8":
@@ -344,6 +346,8 @@ def pack_params(net: Network, folded: Dict[str, torch.Tensor], wdtype: str = "bf
             b[: L.cout] = folded[f"{L.name}.bias"]
             if wdtype == "bf16":
                 put(f"{L.name}.w", w.to(torch.bfloat16))
+            elif wdtype == "fp32":
+                put(f"{L.name}.w", w)
             else:
                 from gale.models.quant import quantize_rows_e4m3
 
@@ -420,7 +424,7 @@ def _tensor_bytes(net: Network, name: str, wdtype: str = "bf16") -> int:
     h, w, c = net.shapes[name]
     if name == "input":
         return h * w * c * 4
-    return h * w * stored_channels(c) * (1 if wdtype == "fp8" else 2)
+    return h * w * stored_channels(c) * {"fp8": 1, "bf16": 2, "fp32": 4}[wdtype]
 
 
 def build_plan(net: Network, base_ptr: int, wdtype: str = "bf16",
@@ -437,9 +441,11 @@ def build_plan(net: Network, base_ptr: int, wdtype: str = "bf16",
     applies the BN affine, the residual and the ReLU in place (the debugging / parity plan).
     """
     fp8 = wdtype == "fp8"
+    f32 = wdtype == "fp32"  # reference-precision plan: fp32 everything, fp32 MFMA convs
+    et = 2 if f32 else int(fp8)  # pool / head activation element type (kernels.h ElemType)
     if fp8 and act_scales is None:
         raise ValueError("build_plan: the fp8 plan needs the activation scales")
-    if fused and fold_bn and is_cifar_resnet20(net):
+    if fused and fold_bn and is_cifar_resnet20(net) and not f32:
         return _fused_resnet20_plan(net, base_ptr, wdtype, act_scales)
     layout, _ = param_layout(net, wdtype, fold_bn)
     # liveness: last layer index reading each tensor
@@ -488,6 +494,7 @@ def build_plan(net: Network, base_ptr: int, wdtype: str = "bf16",
                 d["in_f32"] = 0
             d["out_f32"] = int(L.out_f32)
             d["fp8"] = int(fp8)
+            d["f32"] = int(f32)
             if fp8:
                 d["in_scale"] = act_scales[L.inp]
                 d["out_scale"] = 1.0 if L.out_f32 else act_scales[L.out]
@@ -524,18 +531,18 @@ def build_plan(net: Network, base_ptr: int, wdtype: str = "bf16",
             h, w, c = net.shapes[L.inp]
             ho, wo, _ = net.shapes[L.out]
             ops.append(dict(kind=OP_MAXPOOL, p=[h, w, stored_channels(c), L.k, L.s, L.p, ho, wo],
-                            **{"in": buf_of[L.inp]}, out=buf_of[L.out], fp8=int(fp8)))
+                            **{"in": buf_of[L.inp]}, out=buf_of[L.out], et=et))
         elif isinstance(L, AvgPool):
             h, w, c = net.shapes[L.inp]
             ops.append(dict(kind=OP_AVGPOOL, p=[h * w, stored_channels(c)],
-                            **{"in": buf_of[L.inp]}, out=buf_of[L.out], fp8=int(fp8)))
+                            **{"in": buf_of[L.inp]}, out=buf_of[L.out], et=et))
         elif isinstance(L, Head):
             h, w, c = net.shapes[L.inp]
             ops.append(dict(kind=OP_HEAD, p=[h * w, stored_channels(c), L.classes],
                             **{"in": buf_of[L.inp]}, out=1,
                             w=base_ptr + layout[f"{L.name}.w"].offset,
                             bias=base_ptr + layout[f"{L.name}.b"].offset,
-                            fp8=int(fp8), scale=act_scales[L.inp] if fp8 else 1.0))
+                            et=et, scale=act_scales[L.inp] if fp8 else 1.0))
         elif isinstance(L, Softmax):
             h, w, c = net.shapes[L.inp]
             ops.append(dict(kind=OP_SOFTMAX, p=[L.classes, stored_channels(c)],

@@ -195,7 +195,10 @@ def test_bad_config_is_rejected(broker):
     with pytest.raises(ValueError):
         GaleConfig(sink_mode="bogus").validate()
     with pytest.raises(ValueError):
-        GaleConfig(dtype="fp32").validate()  # no silent bf16 stand-in for an fp32 request
+        GaleConfig(dtype="fp16").validate()
+    GaleConfig(dtype="fp32").validate()  # the reference-precision plan (fp32 MFMA)
+    with pytest.raises(ValueError):
+        GaleConfig(dtype="fp32", fold_bn=False).validate()
     with pytest.raises(ValueError):
         GaleConfig(dtype="fp8", fold_bn=False).validate()
     GaleConfig(fold_bn=False).validate()

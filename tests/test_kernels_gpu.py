@@ -374,3 +374,45 @@ def test_batchnorm_rejects_mismatched_operands():
         ops.batchnorm(x, torch.ones(16), torch.zeros(16))
     with pytest.raises(TypeError):  # out dtype
         ops.batchnorm(x, sc, sh, out=torch.empty(2, 4, 4, 16, device=DEV))
+
+
+@pytest.mark.parametrize("B,H,W,Cin,Cout,k,stride,pad,res", [
+    (3, 32, 32, 3, 16, 3, 1, 1, None),       # network-input gather (Cin 3)
+    (4, 16, 16, 16, 32, 3, 2, 1, "pad"),     # stride 2 + option-A shortcut
+    (2, 8, 8, 64, 72, 3, 1, 1, "identity"),  # Cout not a multiple of the 64-channel tile
+    (5, 7, 7, 40, 24, 1, 1, 0, None),        # 1x1
+])
+def test_conv_f32_matches_fp32(B, H, W, Cin, Cout, k, stride, pad, res):
+    """The fp32-MFMA conv (conv_f32.hip) against an fp32 conv: summation-order-level error."""
+    from gale._native import native
+    from gale.models.graph import pack_conv_weight, round_up
+
+    g = torch.Generator().manual_seed(B * 100 + Cout)
+    x = torch.randn(B, H, W, Cin, generator=g)
+    w = torch.randn(Cout, Cin, k, k, generator=g) / (k * k * Cin) ** 0.5
+    b = torch.randn(Cout, generator=g)
+    Ho, Wo = (H + 2 * pad - k) // stride + 1, (W + 2 * pad - k) // stride + 1
+    r = None
+    if res == "identity":
+        r = torch.randn(B, Ho, Wo, Cout, generator=g)
+    elif res == "pad":
+        r = torch.randn(B, H, W, Cin, generator=g)
+    K = k * k * Cin
+    Kpad = round_up(K, 16)
+    wp = pack_conv_weight(w, Cin, Cout, Kpad).to(DEV)
+    y = torch.empty(B, Ho, Wo, Cout, device=DEV)
+    d = dict(H=H, W=W, Cin=Cin, Ho=Ho, Wo=Wo, Cout=Cout, KH=k, KW=k, stride=stride, pad=pad, K=K,
+             Kpad=Kpad, Npad=Cout, relu=1, f32=1)
+    rd = 0
+    if r is not None:
+        rd_t = r.to(DEV)
+        d.update(has_res=1, res_H=r.shape[1], res_W=r.shape[2], res_C=r.shape[3],
+                 res_stride=2 if res == "pad" else 1)
+        rd = rd_t.data_ptr()
+    xd, bd = x.to(DEV), b.to(DEV)
+    native().conv2d(d, B, xd.data_ptr(), wp.data_ptr(), bd.data_ptr(), 0, rd, y.data_ptr(),
+                    torch.cuda.current_stream().cuda_stream)
+    ref = _ref_conv(x, w, b, stride, pad, True, r, res or "identity")
+    got = y.cpu()
+    scale = ref.abs().max().item()
+    assert (got - ref).abs().max().item() < 2e-5 * max(scale, 1.0)

@@ -206,3 +206,25 @@ def test_unfolded_bn_plan_matches_reference(name, batch):
     clear = margin(ref) > 0.05
     assert torch.equal(eager.argmax(1)[clear], ref.argmax(1)[clear])
     assert torch.equal(graph, eager)
+
+
+@pytest.mark.parametrize("name,batch", [("lenet5", 13), ("resnet20", 37), ("resnet50", 3)])
+def test_fp32_plan_matches_fp32_reference(name, batch):
+    """--dtype fp32: the reference-precision plan (fp32 weights and activations, convs on the fp32
+    matrix core v_mfma_f32_16x16x4_f32) agrees with the fp32 oracle to summation order: relative
+    logit error < 1e-4, argmax identical, eager == graph replay."""
+    net = get_model(name)
+    params = init_params(net, seed=11, calib_batch=4 if name == "resnet50" else 16)
+    packed = materialize_weights(net, torch.device("cuda", 0), params=params, wdtype="fp32")
+    rep = ModelReplica(net, packed, max_batch=64, slots=1, wdtype="fp32")
+    assert all(op["conv"]["f32"] == 1 for op in rep.ops if op["kind"] == 0)
+    x = torch.rand((batch,) + net.input_shape, generator=torch.Generator().manual_seed(99))
+    ref = forward(net, fold_params(net, params), x)
+    eager = rep.infer_eager(x).cpu()
+    graph = rep.infer(x, use_graph=True).cpu()
+    torch.cuda.synchronize()
+    err = rel_logit_err(eager, ref).max().item()
+    print(f"\n{name} fp32 plan rel logit err {err:.2e}")
+    assert err < 1e-4, f"{name}: fp32 plan relative logit error {err}"
+    assert torch.equal(eager.argmax(1), ref.argmax(1))
+    assert torch.equal(graph, eager)
