@@ -20,6 +20,8 @@
 // residual loads and output stores are 16-byte, whole-row accesses.
 // Grid: one workgroup per (pixel tile, channel tile), remapped so the tiles of one XCD are
 // contiguous (T1): the channel tiles of a pixel tile, which re-read the same im2col rows, share an L2.
+#include <stdlib.h>
+
 #include <atomic>
 
 #include "common.cuh"
@@ -38,11 +40,12 @@ struct GemmConvArgs {
   const bf16* w;
   const float* bias;
   const bf16* res;
-  bf16* y;
+  void* y;         // bf16 NHWC, or fp32 when out_f32 (classifier logits)
   int M, H, W, Cin, HWo, Wo, Cout, KW, stride, pad, Kpad;
   int nkb;         // 64-deep k-steps = KH*KW*Cin / 64
   int cin_blocks;  // Cin / 64
-  int relu, has_res;
+  int relu, has_res, out_f32;
+  int res_prefetch;  // residual rows loaded during the last k-step (GALE_GEMM_RES_PREFETCH)
   int n_tiles, nwg;
 };
 
@@ -53,15 +56,21 @@ __device__ __forceinline__ void glds16(const void* src, void* lds_base) {
 // STEM: the packed-stem layout (ConvDesc::stem): k-step kb covers kernel rows 2kb and 2kb+1, a
 // lane's 16-B chunk c reads row kh = 2kb + (c >> 2), bytes 16*(c & 3) of the 64-B run that
 // starts at column 2*wo of the padded image (columns never leave it, rows may: zero rows).
-template <int BM, int BN, bool STEM>
-__global__ __launch_bounds__(256, 2) void conv_gemm_kernel(GemmConvArgs a) {
+// NST: LDS stages. 2 = double-buffered k-loop; 1 = the single-k-step (K = 64: the 1x1 convs
+// on 64 input channels) form, which needs no second stage and so fits 4 workgroups per CU
+// instead of 2 - these layers are bound by their epilogue traffic (a 128 x 128 bf16 output tile
+// plus the residual per 16 KB of input), which more resident workgroups overlap.
+template <int BM, int BN, bool STEM, int NST>
+__global__ __launch_bounds__(256, NST == 1 ? 4 : 2) void conv_gemm_kernel(GemmConvArgs a) {
   constexpr int WM = 2, WN = 2;                 // 4 waves as 2 (pixels) x 2 (channels)
   constexpr int TM = BM / WM / 16;              // 16-pixel tiles per wave
   constexpr int TN = BN / WN / 16;              // 16-channel tiles per wave
   constexpr int XI = BM / 32;                   // X wave-instructions (8 rows each) per wave
   constexpr int WI = BN / 32;                   // W wave-instructions per wave
   constexpr int STAGE = (BM + BN) * 128;        // bytes per LDS stage
-  __shared__ __attribute__((aligned(1024))) uint8_t lds[2 * STAGE];
+  constexpr int EPI = 4 * (TM / 2 * 16) * (BN / WN + 4) * 4;  // epilogue staging bytes
+  constexpr int LDS_BYTES = NST * STAGE > EPI ? NST * STAGE : EPI;
+  __shared__ __attribute__((aligned(1024))) uint8_t lds[LDS_BYTES];
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int wm = wave >> 1, wn = wave & 1;
@@ -163,11 +172,37 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(GemmConvArgs a) {
     wsw[t] = (row >> 1) & 7;
   }
 
+  // epilogue geometry (see below) and the residual prefetch: the residual rows this lane will
+  // add are loaded into registers while the last k-step's MFMAs run, so their DRAM latency is
+  // hidden instead of stalling the epilogue (the 1x1 expansion convs with a shortcut were
+  // latency-bound at ~3 TB/s, profiles/r2_resnet50_layers_pmc.txt)
+  constexpr int CW = BN / WN;      // channels per wave
+  constexpr int EPS = CW + 4;      // fp32 row stride (+16 B: conflict-free 16-row writes)
+  constexpr int LPR = CW / 8;      // lanes per pixel row on read-back
+  constexpr int RPI = 64 / LPR;    // pixel rows per read-back instruction
+  constexpr int HALF = TM / 2 * 16;  // pixel rows per half
+  constexpr int NRI = HALF / RPI;  // read-back instructions per half
+  const int c0 = nt * BN + wn * CW;
+  const int mbase = mt * BM + wm * (BM / WM);
+  const int cc = (lane % LPR) * 8;
+  bf16x8 rpre[2][NRI];
+  auto prefetch_res = [&]() {
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int j = 0; j < NRI; ++j) {
+        const int m = mbase + h * HALF + j * RPI + lane / LPR;
+        if (m < a.M && c0 + cc < a.Cout)
+          rpre[h][j] = ld_bf16x8(a.res + (size_t)m * a.Cout + c0 + cc);
+      }
+  };
+
   stage(0, lds);
   for (int kb = 0; kb < a.nkb; ++kb) {
     __syncthreads();  // step kb has landed (vmcnt(0)); every wave is done reading step kb-1
     uint8_t* cur = lds + (kb & 1) * STAGE;
     if (kb + 1 < a.nkb) stage(kb + 1, lds + ((kb + 1) & 1) * STAGE);
+    else if (NST == 2 && a.has_res && a.res_prefetch) prefetch_res();
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       const int chunk = kk * 4 + fq;
@@ -193,16 +228,9 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(GemmConvArgs a) {
   // a 16-byte access and a wave instruction covers whole 128-byte rows. fp32 in LDS keeps the
   // rounding identical to the register epilogue (one bf16 rounding after the residual/ReLU).
   // Two halves of TM/2 pixel tiles each fit the 2-stage LDS allocation.
-  constexpr int CW = BN / WN;      // channels per wave
-  constexpr int EPS = CW + 4;      // fp32 row stride (+16 B: conflict-free 16-row writes)
-  constexpr int LPR = CW / 8;      // lanes per pixel row on read-back
-  constexpr int RPI = 64 / LPR;    // pixel rows per read-back instruction
-  constexpr int HALF = TM / 2 * 16;  // pixel rows per half
-  static_assert(4 * HALF * EPS * 4 <= 2 * STAGE, "epilogue staging exceeds the LDS allocation");
+  static_assert(4 * HALF * EPS * 4 <= LDS_BYTES, "epilogue staging exceeds the LDS allocation");
   __syncthreads();  // every wave is done with the last k-stage
   float* ep = reinterpret_cast<float*>(lds) + wave * HALF * EPS;
-  const int c0 = nt * BN + wn * CW;
-  const int mbase = mt * BM + wm * (BM / WM);
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
 #pragma unroll
@@ -218,26 +246,36 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(GemmConvArgs a) {
       }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // (wave-private region)
-    const int cc = (lane % LPR) * 8;
 #pragma unroll
-    for (int r0 = 0; r0 < HALF; r0 += RPI) {
+    for (int j = 0; j < NRI; ++j) {
+      const int r0 = j * RPI;
       const int p = r0 + lane / LPR;
       const int m = mbase + h * HALF + p;
-      if (m < a.M) {
+      if (m < a.M && c0 + cc < a.Cout) {  // (Cout % 8 == 0; channels >= Cout are padding)
         const float* src = ep + p * EPS + cc;
         const float4 lo = *reinterpret_cast<const float4*>(src);
         const float4 hi = *reinterpret_cast<const float4*>(src + 4);
         float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
         const size_t o = (size_t)m * a.Cout + c0 + cc;
         if (a.has_res) {
-          const bf16x8 rr = ld_bf16x8(a.res + o);
+          const bf16x8 rr = (NST == 2 && a.res_prefetch) ? rpre[h][j] : ld_bf16x8(a.res + o);
 #pragma unroll
           for (int e = 0; e < 8; ++e) v[e] += (float)rr[e];
         }
-        bf16x8 ov;
+        if (a.relu) {
 #pragma unroll
-        for (int e = 0; e < 8; ++e) ov[e] = (bf16)(a.relu ? fmaxf(v[e], 0.f) : v[e]);
-        *reinterpret_cast<uint4*>(a.y + o) = __builtin_bit_cast(uint4, ov);
+          for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
+        }
+        if (a.out_f32) {  // classifier logits stay fp32 (the softmax op follows)
+          float4* yo = reinterpret_cast<float4*>(static_cast<float*>(a.y) + o);
+          yo[0] = make_float4(v[0], v[1], v[2], v[3]);
+          yo[1] = make_float4(v[4], v[5], v[6], v[7]);
+        } else {
+          bf16x8 ov;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) ov[e] = (bf16)v[e];
+          *reinterpret_cast<uint4*>(static_cast<bf16*>(a.y) + o) = __builtin_bit_cast(uint4, ov);
+        }
       }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads done before the next half
@@ -248,16 +286,26 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(GemmConvArgs a) {
 
 // 0 auto, 1 never the GEMM path, 2 GEMM path whenever the shape allows (tests / A-B benches)
 static std::atomic<int> g_conv_path{0};
+// single-stage form for K = 64 layers (A/B switch: GALE_GEMM_SINGLE_STAGE=0 turns it off)
+static std::atomic<bool> g_gemm_single_stage{[] {
+  const char* e = getenv("GALE_GEMM_SINGLE_STAGE");
+  return !(e && *e == '0');
+}()};
+static std::atomic<bool> g_gemm_res_prefetch{[] {
+  const char* e = getenv("GALE_GEMM_RES_PREFETCH");
+  return !(e && *e == '0');
+}()};
 void set_conv_path(int mode) { g_conv_path = mode; }
 int conv_path() { return g_conv_path; }
 
 bool conv_gemm_supported(const ConvDesc& d, int batch, bool has_res) {
   if (g_conv_path == 1) return false;
-  if (d.fp8 || d.in_f32 || d.out_f32) return false;
-  if (d.Cin % 64 != 0 || d.Cout % 64 != 0 || d.K != d.KH * d.KW * d.Cin || d.Kpad != d.K)
+  if (d.fp8 || d.in_f32 || d.f32) return false;
+  if (d.Cin % 64 != 0 || d.Cout % 8 != 0 || d.K != d.KH * d.KW * d.Cin || d.Kpad != d.K)
     return false;
-  const int bn = (d.Cout % 128 == 0) ? 128 : 64;
-  if (d.Npad % bn != 0) return false;
+  // channel tiles cover Npad (zero weight rows past Cout; the epilogue stores c < Cout only)
+  const int bn = (d.Npad % 128 == 0) ? 128 : 64;
+  if (d.Npad % bn != 0 || d.Npad < d.Cout) return false;
   if (has_res && (d.res_C != d.Cout || d.res_stride != 1 || d.res_H != d.Ho || d.res_W != d.Wo))
     return false;
   // 32-bit element offsets inside the kernel. (No minimum size: measured faster than conv_mfma
@@ -273,7 +321,9 @@ hipError_t conv2d_gemm(const ConvDesc& d, int batch, const void* x, const void* 
   a.w = static_cast<const bf16*>(w);
   a.bias = bias;
   a.res = static_cast<const bf16*>(res);
-  a.y = static_cast<bf16*>(y);
+  a.y = y;
+  a.out_f32 = d.out_f32;
+  a.res_prefetch = g_gemm_res_prefetch.load(std::memory_order_relaxed) ? 1 : 0;
   a.M = batch * d.Ho * d.Wo;
   a.H = d.H; a.W = d.W; a.Cin = d.Cin; a.HWo = d.Ho * d.Wo; a.Wo = d.Wo; a.Cout = d.Cout;
   a.KW = d.KW; a.stride = d.stride; a.pad = d.pad; a.Kpad = d.Kpad;
@@ -281,20 +331,33 @@ hipError_t conv2d_gemm(const ConvDesc& d, int batch, const void* x, const void* 
   a.cin_blocks = d.stem ? 1 : d.Cin / 64;
   a.relu = d.relu;
   a.has_res = d.has_res && res != nullptr;
-  const int bn = (d.Cout % 128 == 0) ? 128 : 64;
+  const int bn = (d.Npad % 128 == 0) ? 128 : 64;
   constexpr int BM = 128;
   const int m_tiles = (a.M + BM - 1) / BM;
-  a.n_tiles = d.Cout / bn;
+  a.n_tiles = d.Npad / bn;
   a.nwg = m_tiles * a.n_tiles;
+  const bool one = a.nkb == 1 && g_gemm_single_stage.load(std::memory_order_relaxed);
   if (d.stem) {
     if (bn == 128)
-      hipLaunchKernelGGL((conv_gemm_kernel<BM, 128, true>), dim3(a.nwg), dim3(256), 0, stream, a);
+      hipLaunchKernelGGL((conv_gemm_kernel<BM, 128, true, 2>), dim3(a.nwg), dim3(256), 0, stream,
+                         a);
     else
-      hipLaunchKernelGGL((conv_gemm_kernel<BM, 64, true>), dim3(a.nwg), dim3(256), 0, stream, a);
+      hipLaunchKernelGGL((conv_gemm_kernel<BM, 64, true, 2>), dim3(a.nwg), dim3(256), 0, stream,
+                         a);
   } else if (bn == 128) {
-    hipLaunchKernelGGL((conv_gemm_kernel<BM, 128, false>), dim3(a.nwg), dim3(256), 0, stream, a);
+    if (one)
+      hipLaunchKernelGGL((conv_gemm_kernel<BM, 128, false, 1>), dim3(a.nwg), dim3(256), 0,
+                         stream, a);
+    else
+      hipLaunchKernelGGL((conv_gemm_kernel<BM, 128, false, 2>), dim3(a.nwg), dim3(256), 0,
+                         stream, a);
   } else {
-    hipLaunchKernelGGL((conv_gemm_kernel<BM, 64, false>), dim3(a.nwg), dim3(256), 0, stream, a);
+    if (one)
+      hipLaunchKernelGGL((conv_gemm_kernel<BM, 64, false, 1>), dim3(a.nwg), dim3(256), 0, stream,
+                         a);
+    else
+      hipLaunchKernelGGL((conv_gemm_kernel<BM, 64, false, 2>), dim3(a.nwg), dim3(256), 0, stream,
+                         a);
   }
   return hipGetLastError();
 }

@@ -1,0 +1,8 @@
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 300 python -u -m pytest tests/test_models_gpu.py -x -q --timeout 120 --timeout-method thread > gpurun_out/r2_r50_tests.log 2>&1 || { tail -30 gpurun_out/r2_r50_tests.log; exit 1; }
+tail -1 gpurun_out/r2_r50_tests.log
+for v in "GALE_GEMM_RES_PREFETCH=0" "GALE_GEMM_RES_PREFETCH=1" "GALE_GEMM_RES_PREFETCH=0" "GALE_GEMM_RES_PREFETCH=1"; do
+  env $v timeout -k 10 240 python tools/bench_forward.py --model resnet50 --batches 256 --iters 30 > gpurun_out/r2_r50_fwd.log 2>&1 || { tail -20 gpurun_out/r2_r50_fwd.log; exit 1; }
+  echo "$v $(grep '^{' gpurun_out/r2_r50_fwd.log)"
+done
