@@ -65,10 +65,11 @@ def parse_args(argv=None):
     ap.add_argument("--source-parallelism", type=int, default=0,
                     help="consumer threads (default: one per partition)")
     ap.add_argument("--sink-parallelism", type=int, default=2)
-    ap.add_argument("--decode-threads", type=int, default=2)
+    ap.add_argument("--decode-threads", type=int, default=0,
+                    help="GPU-ingest / decode workers (0 = from the host CPU share)")
     ap.add_argument("--replicas-per-gpu", type=int, default=0,
-                    help="model replicas (streams) per GPU, each with its own input partition "
-                         "(0 = from the host CPU share: 4 with >= 16 cores per GPU)")
+                    help="model replicas (streams) per GPU (0 = from the host CPU share: 6 "
+                         "with >= 16 cores per GPU, else ~1 per 4 cores, at most 4)")
     ap.add_argument("--max-wait-us", type=int, default=2000)
     ap.add_argument("--queue-batches", type=int, default=4,
                     help="records buffered in the engine, in units of --batch")
@@ -183,10 +184,19 @@ def main(argv=None) -> int:
     a = parse_args(argv)
     from gale.utils import host_cpus_per_rank, thread_cpu_seconds
 
+    # Host pipeline sizing from the rank's CPU share. Throughput is bound by per-connection
+    # copy bandwidth and GPU-ingest round trips, not by the total core count: with >= 16 cores
+    # per GPU, 12 input partitions (TCP connections), 6 replica streams and 4 ingest workers
+    # saturate the share (1.47 M img/s vs 0.97 M with 4/4/2 on one MI355X box,
+    # profiles/r2_host_pipeline_shape_ab.txt); smaller shares keep ~4 cores per replica.
+    cpus = host_cpus_per_rank()
+    big = cpus >= 16
     if a.replicas_per_gpu <= 0:
-        # the host pipeline (Kafka fetch + CRC + scan + encode + produce, and the embedded
-        # broker of this rank) needs ~3-4 cores per replica at full rate
-        a.replicas_per_gpu = max(1, min(4, int(host_cpus_per_rank() // 4)))
+        a.replicas_per_gpu = 6 if big else max(1, min(4, int(cpus // 4)))
+    if a.partitions <= 0:
+        a.partitions = 2 * a.replicas_per_gpu if big else a.replicas_per_gpu
+    if a.decode_threads <= 0:
+        a.decode_threads = 4 if big else 2
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -222,7 +232,7 @@ def main(argv=None) -> int:
     net = get_model(a.model)
     K = native().kafka
     ipr = a.images_per_record
-    parts_per_rank = (a.partitions or a.replicas_per_gpu) * local_gpus
+    parts_per_rank = a.partitions * local_gpus
     # records per RecordBatch: a producer's batch (rate mode: small batches, arrivals are not
     # bursty; the feeder keeps to ~10k appends/s) ...
     rpb = min(64, max(8, int(a.rate // 10000))) if a.rate > 0 else 64
@@ -349,6 +359,7 @@ def main(argv=None) -> int:
                        "processes": world,
                        "images_per_record": ipr, "max_batch": a.batch,
                        "max_wait_us": a.max_wait_us, "replicas_per_gpu": a.replicas_per_gpu,
+                       "decode_threads": a.decode_threads,
                        "partitions": n_parts, "step_images_per_gpu": a.step_images,
                        "path": "kafka-fetch->gpu-json-parse->hipgraph-forward->kafka-produce"},
             "load": (f"offered {a.rate:.0f} images/s per GPU" if a.rate > 0

@@ -215,12 +215,9 @@ void crc32c_device_tables(uint32_t* out) {
       const uint32_t prev = out[(k - 1) * 256 + v];
       out[k * 256 + v] = (prev >> 8) ^ s0[prev & 0xff];
     }
-  // shift tables: advance a raw register by 64 * 2^j zero bytes, j = 0..5
-  for (int j = 0; j < 6; ++j) {
-    const ShiftTable t((size_t)64 << j);
-    for (int b = 0; b < 4; ++b)
-      for (int v = 0; v < 256; ++v) out[1024 + j * 1024 + b * 256 + v] = t.t[b][v];
-  }
+  // per-lane shift constants: x^(8 * 64 * (63 - lane)) mod P (the bytes after lane l's piece
+  // of a 4 KiB window), applied on the device by a GF(2) multiply
+  for (int l = 0; l < 64; ++l) out[1024 + l] = x8n((uint64_t)64 * (63 - l));
 }
 
 uint32_t crc32c_combine(uint32_t crc_a, uint32_t crc_b, uint64_t len_b) {

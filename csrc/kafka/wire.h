@@ -42,8 +42,9 @@ class CrcShift {
   std::shared_ptr<Impl> impl_;
 };
 // Tables of the GPU CRC32C kernel (csrc/kernels/ingest.hip), kCrcDeviceTableWords words:
-// [0, 1024) slicing-by-4 byte tables, [1024 + 1024 j, ...) shift-by-(64 * 2^j)-bytes tables.
-constexpr int kCrcDeviceTableWords = 1024 * 7;
+// [0, 1024) slicing-by-4 byte tables, [1024, 1088) per-lane shift constants
+// x^(8 * 64 * (63 - lane)) mod P (reflected).
+constexpr int kCrcDeviceTableWords = 1024 + 64;
 void crc32c_device_tables(uint32_t* out);
 // crc32c(A ++ B) from crc32c(A), crc32c(B) and |B|.
 uint32_t crc32c_combine(uint32_t crc_a, uint32_t crc_b, uint64_t len_b);

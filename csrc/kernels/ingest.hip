@@ -6,8 +6,10 @@
 // ~1.4 cores per MI355X of JSON; here the fetch buffer is DMA'd to the GPU once (the JSON parser
 // then reads it from there) and the GPU folds it: one wave per 4 KiB window, 64 contiguous bytes
 // per lane through slicing-by-4 tables in LDS, then each lane's register is advanced over the
-// bytes that follow its piece by table lookups of x^(8*64*2^j) mod P and the wave XOR-reduces
-// (CRCs are linear: crc(A ++ B) = crc(A) * x^(8|B|) ^ crc(B) for raw registers). Leading zero
+// bytes that follow its piece by ONE GF(2) multiply with its constant x^(8*64*(63-lane)) mod P
+// (a 32-step shift-and-xor: no per-level shift tables, so a workgroup stages 4.25 KB of tables
+// instead of 28 KB) and the wave XOR-reduces (CRCs are linear: crc(A ++ B) =
+// crc(A) * x^(8|B|) ^ crc(B) for raw registers). Leading zero
 // bytes do not change a raw CRC, so a window shorter than 4 KiB simply leaves its first lanes
 // empty. Misaligned ends are folded byte by byte; everything else uses aligned dword loads.
 #include "common.cuh"
@@ -17,7 +19,8 @@ namespace gale {
 namespace {
 
 constexpr int kCrcWaves = 4;
-constexpr int kTableWords = 7 * 1024;
+constexpr int kTableWords = 1024 + 64;
+constexpr uint32_t kPoly = 0x82f63b78u;  // CRC-32C, reflected
 
 __device__ __forceinline__ uint32_t crc_byte(const uint32_t* T, uint32_t c, uint32_t b) {
   return (c >> 8) ^ T[(c ^ b) & 0xffu];
@@ -29,9 +32,15 @@ __device__ __forceinline__ uint32_t crc_word(const uint32_t* T, uint32_t c, uint
          T[x >> 24];
 }
 
-__device__ __forceinline__ uint32_t crc_shift(const uint32_t* S, uint32_t c) {
-  return S[c & 0xffu] ^ S[256 + ((c >> 8) & 0xffu)] ^ S[512 + ((c >> 16) & 0xffu)] ^
-         S[768 + (c >> 24)];
+// a * b mod P, reflected domain (bit 31 = x^0): the host's poly_mulmod (csrc/kafka/wire.cpp)
+__device__ __forceinline__ uint32_t gf2_mulmod(uint32_t a, uint32_t b) {
+  uint32_t r = 0;
+#pragma unroll
+  for (int i = 0; i < 32; ++i) {
+    r ^= b & (0u - ((a >> (31 - i)) & 1u));
+    b = (b >> 1) ^ (kPoly & (0u - (b & 1u)));
+  }
+  return r;
 }
 
 __global__ __launch_bounds__(256) void crc32c_chunks_kernel(const uint8_t* bytes,
@@ -54,10 +63,7 @@ __global__ __launch_bounds__(256) void crc32c_chunks_kernel(const uint8_t* bytes
       for (; q + 4 <= hi; q += 4) crc = crc_word(T, crc, *reinterpret_cast<const uint32_t*>(bytes + q));
       while (q < hi) crc = crc_byte(T, crc, bytes[q++]);
     }
-    const int s = 63 - lane;  // pieces after this one
-#pragma unroll
-    for (int j = 0; j < 6; ++j)
-      if ((s >> j) & 1) crc = crc_shift(T + 1024 * (j + 1), crc);
+    crc = gf2_mulmod(crc, T[1024 + lane]);  // over the 64 * (63 - lane) bytes that follow
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) crc ^= __shfl_xor(crc, o, 64);
     if (lane == 0) out[c] = crc;

@@ -1,6 +1,6 @@
 """The GPU CRC32C kernel's algorithm (csrc/kernels/ingest.hip) emulated on the host with the
 exact tables it loads (kafka.crc32c_device_tables): slicing-by-4 folding of 64-byte lane pieces,
-per-lane shifts by x^(8*64*k) mod P from the six shift tables, XOR reduction, and the host-side
+per-lane shifts by a GF(2) multiply with x^(8*64*(63-lane)) mod P, XOR reduction, and the host-side
 join of 4 KiB windows into a record batch's standard CRC. Checked against the host CRC32C."""
 
 import os
@@ -24,10 +24,13 @@ def _word(c, w):
                ^ T[x >> 24])
 
 
-def _shift(j, c):
-    S = T[1024 * (j + 1):1024 * (j + 2)]
-    return int(S[c & 0xFF] ^ S[256 + ((c >> 8) & 0xFF)] ^ S[512 + ((c >> 16) & 0xFF)]
-               ^ S[768 + (c >> 24)])
+def _mulmod(a, b):  # the device's gf2_mulmod: a * b mod P, reflected
+    r = 0
+    for i in range(32):
+        if (a >> (31 - i)) & 1:
+            r ^= b
+        b = (b >> 1) ^ (0x82F63B78 if b & 1 else 0)
+    return r
 
 
 def window_crc(buf, end, length):
@@ -45,11 +48,7 @@ def window_crc(buf, end, length):
             c = _word(c, int.from_bytes(buf[q:q + 4], "little")); q += 4
         while q < hi:
             c = _byte(c, buf[q]); q += 1
-        s = 63 - lane
-        for j in range(6):
-            if (s >> j) & 1:
-                c = _shift(j, c)
-        acc ^= c
+        acc ^= _mulmod(c, int(T[1024 + lane]))
     return acc
 
 

@@ -106,7 +106,11 @@ def sweep(a, counts, extra, env, mode) -> int:
         results[n] = r
         if not pinned:
             cfg = r.get("config", {})
+            per_gpu_parts = cfg.get("partitions", 0) // max(1, r.get("n_gpus", 1))
+            if per_gpu_parts and "--partitions" not in extra:
+                pinned += ["--partitions", str(per_gpu_parts)]
             for flag, key in (("--replicas-per-gpu", "replicas_per_gpu"),
+                              ("--decode-threads", "decode_threads"),
                               ("--batch", "max_batch"),
                               ("--step-images", "step_images_per_gpu")):
                 if key in cfg and flag not in extra:
