@@ -79,6 +79,8 @@ def parse_args(argv=None):
     ap.add_argument("--stub", action="store_true", help="CPU stub replicas (no GPU)")
     ap.add_argument("--stub-null", action="store_true",
                     help="stub replicas skip parsing (measures the host Kafka/codec path only)")
+    ap.add_argument("--gpu-encode", action=argparse.BooleanOptionalAction, default=True,
+                    help="format the prediction text (Java Float.toString) on the GPU")
     ap.add_argument("--gpu-ingest", action=argparse.BooleanOptionalAction, default=True,
                     help="CRC32C + image counting of fetch buffers on the GPU (host reads only "
                          "Kafka framing)")
@@ -279,7 +281,7 @@ def main(argv=None) -> int:
                      sink_parallelism=a.sink_parallelism * local_gpus,
                      replicas=a.replicas_per_gpu * local_gpus,
                      decode_threads=a.decode_threads, slo_p99_ms=a.slo_p99_ms,
-                     gpu_wait_poll_us=a.gpu_wait_poll_us, gpu_ingest=a.gpu_ingest,
+                     gpu_wait_poll_us=a.gpu_wait_poll_us, gpu_ingest=a.gpu_ingest, gpu_encode=a.gpu_encode,
                      stub=a.stub, stub_null=a.stub_null, commit_interval_ms=500,
                      check_crcs=a.check_crcs)
     devices = (list(range(local_gpus)) if local_gpus > 1 else [local_rank]) if use_gpu else None

@@ -81,12 +81,15 @@ void bind_engine(py::module_& m) {
            py::arg("max_images") = 256, py::arg("delay_us") = 0, py::arg("compute") = true,
            py::arg("locality") = -1)
       .def("add_gpu_replica",
-           [](Engine& e, std::shared_ptr<Executor> exec, bool use_graph, int wait_poll_us) {
+           [](Engine& e, std::shared_ptr<Executor> exec, bool use_graph, int wait_poll_us,
+              bool gpu_encode) {
              const EngineConfig& c = e.config();
              e.add_replica(std::make_shared<GpuReplica>(std::move(exec), c.H, c.W, c.C,
-                                                        c.classes, use_graph, wait_poll_us));
+                                                        c.classes, use_graph, wait_poll_us,
+                                                        gpu_encode));
            },
-           py::arg("executor"), py::arg("use_graph") = true, py::arg("wait_poll_us") = 0)
+           py::arg("executor"), py::arg("use_graph") = true, py::arg("wait_poll_us") = 0,
+           py::arg("gpu_encode") = false)
       .def("enable_gpu_ingest",
            [](Engine& e, int device, int lanes, int poll_us) {
              e.set_ingest(std::make_shared<GpuIngest>(device, lanes, poll_us));

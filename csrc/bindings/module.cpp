@@ -212,6 +212,12 @@ PYBIND11_MODULE(_C, m) {
                                        reinterpret_cast<hipStream_t>(stream)),
               "json_count_records");
         });
+  m.def("format_floats_java", [](int n, uintptr_t x, uintptr_t out16, uintptr_t stream) {
+    gale::check_hip(gale::format_floats_java(n, reinterpret_cast<const float*>(x),
+                                             reinterpret_cast<void*>(out16),
+                                             reinterpret_cast<hipStream_t>(stream)),
+                    "format_floats_java");
+  });
   m.def("set_conv_path", &gale::set_conv_path);
   m.def("device_pci_bus_id", [](int device) {
     char buf[64] = {0};

@@ -356,6 +356,31 @@ void encode_predictions(const float* probs, int n, int classes, bool json_string
   if (json_string) out.push_back('"');
 }
 
+void encode_predictions_text(const uint8_t* text16, int n, int classes, bool json_string,
+                             std::string& out) {
+  out.clear();
+  out.reserve((size_t)n * classes * 12 + 32);
+  const char* q = json_string ? "\\\"" : "\"";
+  if (json_string) out.push_back('"');
+  out.push_back('{');
+  out.append(q);
+  out.append("predictions");
+  out.append(q);
+  out.append(":[");
+  for (int i = 0; i < n; ++i) {
+    if (i) out.push_back(',');
+    out.push_back('[');
+    for (int k = 0; k < classes; ++k) {
+      if (k) out.push_back(',');
+      const uint8_t* t = text16 + ((size_t)i * classes + k) * 16;
+      out.append(reinterpret_cast<const char*>(t), t[15]);
+    }
+    out.push_back(']');
+  }
+  out.append("]}");
+  if (json_string) out.push_back('"');
+}
+
 void encode_instances(const float* x, int n, int H, int W, int C, std::string& out) {
   out.clear();
   out.reserve((size_t)n * H * W * C * 12 + 32);

@@ -64,6 +64,10 @@ int format_float_java(float v, char* out);
 // already-serialized String value (MainTopology.java:115).
 void encode_predictions(const float* probs, int n, int classes, bool json_string,
                         std::string& out);
+// Same output from pre-formatted values: text16 holds n * classes 16-byte slots (characters,
+// length in byte 15; format_floats_java in csrc/kernels/format.hip).
+void encode_predictions_text(const uint8_t* text16, int n, int classes, bool json_string,
+                             std::string& out);
 
 // {"instances":[[[[x,...]]]]} with Java Float.toString numbers: the load generator's encoder
 // (the reference's producers are external; this is the shape README.md:22-27 documents).

@@ -152,10 +152,10 @@ hipError_t json_count_records(int nrec, int ntiles, JsonRecord* recs, const int*
 
 // Raw (zero initial state, no final inversion) CRC32C of byte windows [end - len, end) of a
 // device buffer, one wave per window (len <= kCrcChunkBytes): each lane folds 64 bytes with
-// slicing-by-4 tables in LDS, shifts its register over the bytes after its piece (x^(8k) mod P
-// tables) and the wave XOR-reduces. The host joins the windows of a Kafka record batch with
-// crc = shift(crc, 4096) ^ window_crc and converts to the standard CRC (kafka::CrcShift).
-// tables: kafka::crc32c_device_tables() (7168 words) in device memory.
+// slicing-by-4 tables in LDS, shifts its register over the bytes after its piece (one GF(2)
+// multiply by a per-lane constant) and the wave XOR-reduces. The host joins the windows of a
+// Kafka record batch with crc = shift(crc, 4096) ^ window_crc and converts to the standard CRC
+// (kafka::CrcShift). tables: kafka::crc32c_device_tables() (1088 words) in device memory.
 constexpr int kCrcChunkBytes = 4096;
 struct CrcChunk {
   int64_t end;  // one past the window's last byte (offset into `bytes`)
@@ -164,5 +164,12 @@ struct CrcChunk {
 };
 hipError_t crc32c_chunks(const uint8_t* bytes, const CrcChunk* chunks, int n,
                          const uint32_t* tables, uint32_t* out, hipStream_t stream);
+
+// ---- prediction text (format.hip) -----------------------------------------------------------
+// n binary32 values -> Java Float.toString text (JDK 19+ shortest-digit rules, the same text as
+// codec::format_float_java), one 16-byte slot per value: characters from byte 0, length in
+// byte 15 (at most 14 characters).
+constexpr int kFloatTextSlot = 16;
+hipError_t format_floats_java(int n, const float* x, void* out16, hipStream_t stream);
 
 }  // namespace gale

@@ -60,6 +60,10 @@ __device__ __forceinline__ void glds16(const void* src, void* lds_base) {
 // on 64 input channels) form, which needs no second stage and so fits 4 workgroups per CU
 // instead of 2 - these layers are bound by their epilogue traffic (a 128 x 128 bf16 output tile
 // plus the residual per 16 KB of input), which more resident workgroups overlap.
+// 3 = a ring of three stages with two k-steps of DMA in flight (128 x 64 tiles, 72 KB: still 2
+// workgroups per CU; an A/B variant, see g_gemm_ring). The ring waits with an explicit vmcnt
+// that leaves the younger stage in flight and a bare s_barrier (a __syncthreads would drain
+// every outstanding load).
 template <int BM, int BN, bool STEM, int NST>
 __global__ __launch_bounds__(256, NST == 1 ? 4 : 2) void conv_gemm_kernel(GemmConvArgs a) {
   constexpr int WM = 2, WN = 2;                 // 4 waves as 2 (pixels) x 2 (channels)
@@ -198,11 +202,25 @@ __global__ __launch_bounds__(256, NST == 1 ? 4 : 2) void conv_gemm_kernel(GemmCo
   };
 
   stage(0, lds);
+  if (NST == 3 && a.nkb > 1) stage(1, lds + STAGE);
   for (int kb = 0; kb < a.nkb; ++kb) {
-    __syncthreads();  // step kb has landed (vmcnt(0)); every wave is done reading step kb-1
-    uint8_t* cur = lds + (kb & 1) * STAGE;
-    if (kb + 1 < a.nkb) stage(kb + 1, lds + ((kb + 1) & 1) * STAGE);
-    else if (NST == 2 && a.has_res && a.res_prefetch) prefetch_res();
+    uint8_t* cur;
+    if (NST == 3) {
+      // step kb has landed when at most the XI + WI loads of step kb+1 are still outstanding;
+      // the barrier also means every wave is done reading step kb-1's buffer, refilled below
+      if (kb + 1 < a.nkb)
+        asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(XI + WI) : "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+      const int sb = kb % 3;
+      cur = lds + sb * STAGE;
+      if (kb + 2 < a.nkb) stage(kb + 2, lds + (sb == 0 ? 2 : sb - 1) * STAGE);
+    } else {
+      __syncthreads();  // step kb has landed (vmcnt(0)); every wave is done reading step kb-1
+      cur = lds + (kb & 1) * STAGE;
+      if (kb + 1 < a.nkb) stage(kb + 1, lds + ((kb + 1) & 1) * STAGE);
+    }
+    if (NST >= 2 && kb + 1 == a.nkb && a.has_res && a.res_prefetch) prefetch_res();
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       const int chunk = kk * 4 + fq;
@@ -258,7 +276,7 @@ __global__ __launch_bounds__(256, NST == 1 ? 4 : 2) void conv_gemm_kernel(GemmCo
         float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
         const size_t o = (size_t)m * a.Cout + c0 + cc;
         if (a.has_res) {
-          const bf16x8 rr = (NST == 2 && a.res_prefetch) ? rpre[h][j] : ld_bf16x8(a.res + o);
+          const bf16x8 rr = (NST >= 2 && a.res_prefetch) ? rpre[h][j] : ld_bf16x8(a.res + o);
 #pragma unroll
           for (int e = 0; e < 8; ++e) v[e] += (float)rr[e];
         }
@@ -294,6 +312,14 @@ static std::atomic<bool> g_gemm_single_stage{[] {
 static std::atomic<bool> g_gemm_res_prefetch{[] {
   const char* e = getenv("GALE_GEMM_RES_PREFETCH");
   return !(e && *e == '0');
+}()};
+// three-stage 128 x 64 ring for layers with >= 3 k-steps, OFF by default (GALE_GEMM_RING=1 on):
+// measured slower at batch 256 (4.86 -> 5.71 ms; batch 64: 1.78 -> 1.74 ms,
+// profiles/r2_resnet50_gemm_ab.txt) - the halved channel tile doubles the im2col traffic per
+// FLOP, which costs more than the extra step of look-ahead gains
+static std::atomic<bool> g_gemm_ring{[] {
+  const char* e = getenv("GALE_GEMM_RING");
+  return e && *e == '1';
 }()};
 void set_conv_path(int mode) { g_conv_path = mode; }
 int conv_path() { return g_conv_path; }
@@ -337,7 +363,12 @@ hipError_t conv2d_gemm(const ConvDesc& d, int batch, const void* x, const void* 
   a.n_tiles = d.Npad / bn;
   a.nwg = m_tiles * a.n_tiles;
   const bool one = a.nkb == 1 && g_gemm_single_stage.load(std::memory_order_relaxed);
-  if (d.stem) {
+  if (!d.stem && a.nkb >= 3 && g_gemm_ring.load(std::memory_order_relaxed)) {
+    a.n_tiles = d.Npad / 64;  // (Npad % 64 == 0 whenever a 128- or 64-wide tiling is allowed)
+    a.nwg = m_tiles * a.n_tiles;
+    hipLaunchKernelGGL((conv_gemm_kernel<BM, 64, false, 3>), dim3(a.nwg), dim3(256), 0, stream,
+                       a);
+  } else if (d.stem) {
     if (bn == 128)
       hipLaunchKernelGGL((conv_gemm_kernel<BM, 128, true, 2>), dim3(a.nwg), dim3(256), 0, stream,
                          a);

@@ -1032,8 +1032,12 @@ void Engine::finish_batch(ReplicaSlot* rs, Batch& b) {
     if (r.status != codec::OK) {
       emit_error(r, r.status, prod);
     } else {
-      codec::encode_predictions(b.probs + (size_t)img * cfg_.classes, r.images, cfg_.classes, js,
-                                out);
+      if (b.pred_text)
+        codec::encode_predictions_text(b.pred_text + (size_t)img * cfg_.classes * 16, r.images,
+                                       cfg_.classes, js, out);
+      else
+        codec::encode_predictions(b.probs + (size_t)img * cfg_.classes, r.images, cfg_.classes,
+                                  js, out);
       emit(r, out, false, prod);
     }
     img += r.images;

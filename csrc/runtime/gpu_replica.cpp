@@ -18,9 +18,9 @@ namespace gale {
 // ---------------------------------------------------------------------------------------------
 
 GpuReplica::GpuReplica(std::shared_ptr<Executor> exec, int H, int W, int C, int classes,
-                       bool use_graph, int wait_poll_us)
+                       bool use_graph, int wait_poll_us, bool gpu_encode)
     : exec_(std::move(exec)), H_(H), W_(W), C_(C), classes_(classes), use_graph_(use_graph),
-      wait_poll_us_(wait_poll_us) {
+      wait_poll_us_(wait_poll_us), gpu_encode_(gpu_encode) {
   if (exec_->input_bytes_per_image() != (long long)H * W * C * 4)
     throw std::invalid_argument("GpuReplica: executor input is not fp32 [H, W, C]");
   if (exec_->output_bytes_per_image() != (long long)classes * 4)
@@ -33,6 +33,11 @@ GpuReplica::GpuReplica(std::shared_ptr<Executor> exec, int H, int W, int C, int 
   for (Slot& s : slots_) {
     check_hip(hipHostMalloc(reinterpret_cast<void**>(&s.h_out), sizeof(float) * mb * classes),
               "hipHostMalloc(out)");
+    if (gpu_encode_) {
+      const size_t tb = (size_t)kFloatTextSlot * mb * classes;
+      check_hip(hipHostMalloc(reinterpret_cast<void**>(&s.h_text), tb), "hipHostMalloc(text)");
+      check_hip(hipMalloc(reinterpret_cast<void**>(&s.d_text), tb), "hipMalloc(text)");
+    }
     check_hip(hipEventCreateWithFlags(&s.done, hipEventDisableTiming), "hipEventCreate");
     check_hip(hipEventCreateWithFlags(&s.staged, hipEventDisableTiming), "hipEventCreate");
     // initial text capacity: ~12 bytes per number (Java Float.toString + ",") x a full batch
@@ -51,6 +56,8 @@ GpuReplica::~GpuReplica() {
     if (s.d_recs) hipFree(s.d_recs);
     if (s.d_tiles) hipFree(s.d_tiles);
     if (s.h_out) hipHostFree(s.h_out);
+    if (s.h_text) hipHostFree(s.h_text);
+    if (s.d_text) hipFree(s.d_text);
     if (s.done) hipEventDestroy(s.done);
     if (s.staged) hipEventDestroy(s.staged);
   }
@@ -223,6 +230,16 @@ void GpuReplica::submit(Batch& b) {
   check_hip(hipMemcpyAsync(s.h_out, exec_->output(slot), sizeof(float) * img * classes_,
                            hipMemcpyDeviceToHost, stream_),
             "D2H probs");
+  if (gpu_encode_) {
+    // the prediction text (Java Float.toString per value) is formatted on the stream, so the
+    // emitting thread only concatenates slots (format.hip)
+    check_hip(format_floats_java(img * classes_, static_cast<const float*>(exec_->output(slot)),
+                                 s.d_text, stream_),
+              "format_floats_java");
+    check_hip(hipMemcpyAsync(s.h_text, s.d_text, (size_t)kFloatTextSlot * img * classes_,
+                             hipMemcpyDeviceToHost, stream_),
+              "D2H text");
+  }
   check_hip(hipMemcpyAsync(s.h_recs, s.d_recs, sizeof(JsonRecord) * nrec, hipMemcpyDeviceToHost,
                            stream_),
             "D2H status");
@@ -250,6 +267,7 @@ void GpuReplica::wait(Batch& b) {
     else if (st == 2) b.dev_status[i] = codec::BAD_NUMBER;
   }
   b.probs = s.h_out;
+  b.pred_text = gpu_encode_ ? s.h_text : nullptr;
 }
 
 void GpuReplica::recover() {

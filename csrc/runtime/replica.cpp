@@ -34,6 +34,8 @@ void StubReplica::submit(Batch& b) {
     std::fill(probs_.begin(), probs_.begin() + (size_t)n * classes_, 1.0f / (float)classes_);
     if (delay_us_ > 0) usleep((useconds_t)delay_us_);
     b.probs = probs_.data();
+  b.pred_text = nullptr;
+    b.pred_text = nullptr;
     return;
   }
   for (size_t ri = 0; ri < b.recs.size(); ++ri) {

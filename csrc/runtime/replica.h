@@ -44,6 +44,9 @@ struct Batch {
   int images = 0;
   int slot = 0;
   const float* probs = nullptr;  // [images, classes] after wait()
+  // [images, classes] Java Float.toString slots (kFloatTextSlot bytes each) when the replica
+  // formats on the device (GpuReplica gpu_encode), else null: the engine formats `probs`
+  const uint8_t* pred_text = nullptr;
   std::vector<int32_t> dev_status;  // per-record codec::Status found by the replica's parser
   int64_t t_take_ns = 0, t_submit_ns = 0, t_done_ns = 0;
 };
@@ -94,8 +97,9 @@ class GpuReplica : public Replica {
   // wait_poll_us > 0: wait() polls the batch's completion event and sleeps wait_poll_us between
   // polls (the worker thread then costs ~no CPU while the GPU works); 0: hipEventSynchronize
   // (the HIP runtime busy-waits, lowest wake-up latency, one core per waiting replica)
+  // gpu_encode: the softmax rows are also formatted as prediction text on the device
   GpuReplica(std::shared_ptr<Executor> exec, int H, int W, int C, int classes, bool use_graph,
-             int wait_poll_us = 0);
+             int wait_poll_us = 0, bool gpu_encode = false);
   ~GpuReplica() override;
   std::string name() const override;
   int max_images() const override { return exec_->max_batch(); }
@@ -117,6 +121,8 @@ class GpuReplica : public Replica {
     int* d_tiles = nullptr;      // per-tile token counts (parser scratch)
     int tiles_cap = 0;
     float* h_out = nullptr;      // pinned softmax rows
+    uint8_t* h_text = nullptr;   // pinned prediction text slots (gpu_encode)
+    uint8_t* d_text = nullptr;
     hipEvent_t done = nullptr;
     hipEvent_t staged = nullptr;  // H2D of this slot's text finished (copy stream)
   };
@@ -127,6 +133,7 @@ class GpuReplica : public Replica {
   int H_, W_, C_, classes_;
   bool use_graph_;
   int wait_poll_us_ = 0;
+  bool gpu_encode_ = false;
   hipStream_t stream_ = nullptr;       // parse + forward + D2H
   hipStream_t copy_stream_ = nullptr;  // H2D of batch k+1 overlaps compute of batch k
   std::vector<Slot> slots_;

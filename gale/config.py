@@ -86,6 +86,7 @@ class GaleConfig:
     queue_depth: int = 8192
     use_graph: bool = True
     gpu_wait_poll_us: int = 20         # > 0: replicas sleep-poll their batch events (0: spin)
+    gpu_encode: bool = True            # prediction text (Float.toString) formatted on the GPU
     fold_bn: bool = True               # False: standalone BatchNorm kernels (debug/parity plan)
     stub: bool = False                 # CPU stub replicas (plumbing without a GPU)
     stub_null: bool = False            # stub replicas skip parsing/compute (host-path benchmark)

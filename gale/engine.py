@@ -74,7 +74,8 @@ class Engine:
             d["device_cpus"] = {dev: sorted(device_cpus(dev)) for dev in devs}
         self._native = native().Engine(d)
         for rep in reps:
-            self._native.add_gpu_replica(rep.executor, cfg.use_graph, cfg.gpu_wait_poll_us)
+            self._native.add_gpu_replica(rep.executor, cfg.use_graph, cfg.gpu_wait_poll_us,
+                                         cfg.gpu_encode)
             self.model_replicas.append(rep)
             self.devices.append(rep.device.index or 0)
         if cfg.gpu_ingest:
