@@ -34,7 +34,6 @@ void StubReplica::submit(Batch& b) {
     std::fill(probs_.begin(), probs_.begin() + (size_t)n * classes_, 1.0f / (float)classes_);
     if (delay_us_ > 0) usleep((useconds_t)delay_us_);
     b.probs = probs_.data();
-  b.pred_text = nullptr;
     b.pred_text = nullptr;
     return;
   }
@@ -68,6 +67,7 @@ void StubReplica::submit(Batch& b) {
   }
   if (delay_us_ > 0) usleep((useconds_t)delay_us_);
   b.probs = probs_.data();
+  b.pred_text = nullptr;
 }
 
 void StubReplica::wait(Batch& b) { (void)b; }

@@ -121,8 +121,7 @@ class GpuReplica : public Replica {
     int* d_tiles = nullptr;      // per-tile token counts (parser scratch)
     int tiles_cap = 0;
     float* h_out = nullptr;      // pinned softmax rows
-    uint8_t* h_text = nullptr;   // pinned prediction text slots (gpu_encode)
-    uint8_t* d_text = nullptr;
+    uint8_t* h_text = nullptr;   // pinned, device-mapped prediction text slots (gpu_encode)
     hipEvent_t done = nullptr;
     hipEvent_t staged = nullptr;  // H2D of this slot's text finished (copy stream)
   };
