@@ -101,6 +101,8 @@ class GaleConfig:
     profile: str = ""                  # run under rocprofv3 --kernel-trace --marker-trace --stats
     metrics_interval: float = 10.0
     metrics_file: str = ""             # JSON lines; empty = stderr
+    metrics_port: int = -1             # >= 0: HTTP /metrics (Prometheus) + /stats (JSON) on
+                                       # 127.0.0.1:port+local_rank (0 = any free port); -1 off
     log_level: str = "INFO"
     registry_dir: str = field(default_factory=lambda: os.path.join(
         os.path.expanduser("~"), ".gale", "topologies"))

@@ -1,19 +1,25 @@
-"""Periodic JSON-lines metrics reporter.
+"""Metrics: a periodic JSON-lines reporter and a live HTTP endpoint.
 
 Replaces what the reference gets from Storm UI (per-component latency / capacity /
-emitted / acked / failed, E4) and the KafkaSpout ``kafkaOffset`` metric (E1). Every interval it
-writes one line with the interval's throughput (images/s, records/s), cumulative counters,
-per-stage latency quantiles from the engine's native histograms, queue depth and replica
-health, to stderr or a file.
+emitted / acked / failed, E4) and the KafkaSpout ``kafkaOffset`` metric (E1).
+
+* ``Reporter``: every interval one line with the interval's throughput (images/s, records/s),
+  cumulative counters, per-stage latency quantiles from the engine's native histograms, queue
+  depth and replica health, to stderr or a file.
+* ``MetricsServer`` (``--metrics-port``): the same numbers on demand, like Storm UI's REST API -
+  ``GET /metrics`` in the Prometheus text format (engine counters/gauges, per replica and per
+  input partition series), ``GET /stats`` as one JSON document.
 """
 
 from __future__ import annotations
 
 import json
+import math
 import sys
 import threading
 import time
-from typing import Callable, Dict, Optional, TextIO
+from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
+from typing import Callable, Dict, List, Optional, TextIO
 
 KEYS = ("records_in", "records_out", "images_out", "errors", "produce_failures", "dropped",
         "requeued", "replica_failures", "replica_restarts", "queue_records", "replicas_alive",
@@ -90,3 +96,96 @@ class Reporter:
     def close(self) -> None:
         if self._own and not self._own.closed:
             self._own.close()
+
+
+def _label_str(labels: dict) -> str:
+    if not labels:
+        return ""
+    esc = (lambda v: str(v).replace("\\", "\\\\").replace('"', '\\"').replace("\n", "\\n"))
+    return "{" + ",".join(f'{k}="{esc(v)}"' for k, v in sorted(labels.items())) + "}"
+
+
+def prometheus_text(stats: dict, replicas: List[dict], partitions: List[dict],
+                    labels: Optional[dict] = None) -> str:
+    """Prometheus exposition (text format 0.0.4) of an engine snapshot: every numeric engine
+    stat as ``gale_<name>``, replica health/work as ``gale_replica_<name>{replica=..}``, the
+    kafkaOffset equivalent as ``gale_partition_<name>{partition=..}``."""
+    base = dict(labels or {})
+    fams: Dict[str, list] = {}  # metric family -> samples (grouped, as the format requires)
+
+    def emit(name: str, value, extra: Optional[dict] = None):
+        if isinstance(value, bool):
+            value = int(value)
+        if not isinstance(value, (int, float)) or (isinstance(value, float)
+                                                    and not math.isfinite(value)):
+            return
+        fams.setdefault(name, []).append(f"{name}{_label_str(dict(base, **(extra or {})))} "
+                                         f"{value}")
+
+    for k in sorted(stats):
+        emit(f"gale_{k}", stats[k])
+    for i, r in enumerate(replicas):
+        for k in sorted(r):
+            if k != "name":
+                emit(f"gale_replica_{k}", r[k], {"replica": i, "name": r.get("name", "")})
+    for o in partitions:
+        for k in sorted(o):
+            if k != "partition":
+                emit(f"gale_partition_{k}", o[k], {"partition": o["partition"]})
+    lines = []
+    for name, samples in fams.items():
+        lines.append(f"# TYPE {name} gauge")
+        lines.extend(samples)
+    return "\n".join(lines) + "\n"
+
+
+class MetricsServer:
+    """Live metrics over HTTP on ``host:port`` (port 0 picks a free one: see ``.port``)."""
+
+    def __init__(self, engine, port: int = 0, host: str = "127.0.0.1",
+                 labels: Optional[dict] = None):
+        self.engine = engine
+        self.labels = dict(labels or {})
+        srv = self
+
+        class Handler(BaseHTTPRequestHandler):
+            def log_message(self, *args):  # quiet
+                pass
+
+            def do_GET(self):
+                try:
+                    if self.path.startswith("/metrics"):
+                        body = prometheus_text(srv.engine.stats(), srv.engine.replica_stats(),
+                                               srv.engine.partition_offsets(), srv.labels)
+                        ctype = "text/plain; version=0.0.4"
+                    elif self.path.startswith("/stats"):
+                        body = json.dumps({**srv.labels, "stats": srv.engine.stats(),
+                                           "replicas": srv.engine.replica_stats(),
+                                           "partitions": srv.engine.partition_offsets()})
+                        ctype = "application/json"
+                    else:
+                        self.send_error(404)
+                        return
+                except Exception as e:  # never take the topology down
+                    self.send_error(500, str(e))
+                    return
+                data = body.encode()
+                self.send_response(200)
+                self.send_header("Content-Type", ctype)
+                self.send_header("Content-Length", str(len(data)))
+                self.end_headers()
+                self.wfile.write(data)
+
+        self._httpd = ThreadingHTTPServer((host, port), Handler)
+        self._httpd.daemon_threads = True
+        self.port = self._httpd.server_address[1]
+        self._thread = threading.Thread(target=self._httpd.serve_forever, name="gale-http",
+                                        daemon=True)
+
+    def start(self) -> "MetricsServer":
+        self._thread.start()
+        return self
+
+    def stop(self) -> None:
+        self._httpd.shutdown()
+        self._httpd.server_close()

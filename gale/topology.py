@@ -154,7 +154,7 @@ def run_topology(cfg: GaleConfig, stop_event: Optional[threading.Event] = None,
     """Serve ``cfg`` until its duration elapses, a signal arrives or ``stop_event`` is set.
     Returns the final engine stats."""
     from gale.engine import Engine
-    from gale.metrics import Reporter
+    from gale.metrics import MetricsServer, Reporter
 
     rank, world, local_rank = _dist_env()
     name = cfg.topology_name if world == 1 else f"{cfg.topology_name}.r{rank}"
@@ -193,7 +193,15 @@ def run_topology(cfg: GaleConfig, stop_event: Optional[threading.Event] = None,
                             labels={"topology": name, "rank": rank},
                             extra_fn=lambda: {"partitions": sorted(
                                 o["partition"] for o in engine.partition_offsets())}).start()
+        http = None
+        if cfg.metrics_port >= 0:
+            port = cfg.metrics_port + local_rank if cfg.metrics_port > 0 else 0
+            http = MetricsServer(engine, port, labels={"topology": name, "rank": rank}).start()
+            log.info("metrics: http://127.0.0.1:%d/metrics (Prometheus), /stats (JSON)",
+                     http.port)
         stop_event.wait(cfg.duration if cfg.duration > 0 else None)
+        if http is not None:
+            http.stop()
         reporter.stop(final=False, close=False)
         engine.stop()
         final = reporter.report()

@@ -149,3 +149,44 @@ def test_profile_flag_wraps_run_in_rocprofv3():
     assert "--profile" not in cmd[dd:] and cmd[-1] == "--trace"
     assert cmd[cmd.index("-d") + 1] == "/tmp/p"
     assert parse_topology_args(cmd[dd + 4:]).trace is True
+
+
+def test_metrics_http_endpoint_prometheus_and_json():
+    """--metrics-port: Storm UI's per-component numbers on demand (Prometheus text + JSON)."""
+    import json as _json
+    import re as _re
+    import urllib.request
+
+    from gale.config import GaleConfig
+    from gale.engine import Engine
+    from gale.metrics import MetricsServer
+    from gale._native import native
+
+    C = native()
+    b = C.kafka.Broker()
+    b.start()
+    try:
+        b.create_topic("in", 2)
+        b.create_topic("out", 1)
+        for i in range(6):
+            b.append("in", i % 2, [C.encode_instances(np.zeros((1, 32, 32, 3), np.float32))])
+        cfg = GaleConfig(topology_name="m", input_topic="in", output_topic="out", stub=True,
+                         bootstrap=f"127.0.0.1:{b.port}", start_offset="earliest", replicas=2)
+        eng = Engine(cfg, max_records=6)
+        eng.start()
+        assert eng.wait(30)
+        srv = MetricsServer(eng, 0, labels={"topology": "m", "rank": 0}).start()
+        try:
+            txt = urllib.request.urlopen(f"http://127.0.0.1:{srv.port}/metrics").read().decode()
+            js = _json.loads(urllib.request.urlopen(f"http://127.0.0.1:{srv.port}/stats").read())
+        finally:
+            srv.stop()
+            eng.stop()
+    finally:
+        b.stop()
+    assert 'gale_records_out{rank="0",topology="m"} 6' in txt
+    assert len(_re.findall(r'^gale_replica_alive\{', txt, _re.M)) == 2
+    assert len(_re.findall(r'^gale_partition_lag\{', txt, _re.M)) == 2
+    names = [ln.split()[2] for ln in txt.splitlines() if ln.startswith("# TYPE")]
+    assert len(names) == len(set(names))  # one family block per metric
+    assert js["stats"]["records_out"] == 6 and len(js["replicas"]) == 2
