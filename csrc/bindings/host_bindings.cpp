@@ -313,6 +313,17 @@ void bind_host(py::module_& m) {
     codec::encode_predictions(p.data(), (int)p.shape(0), (int)p.shape(1), json_string, out);
     return py::bytes(out);
   }, py::arg("probs"), py::arg("json_string") = false);
+  m.def("encode_predictions_text", [](py::bytes text16, int n, int classes, bool json_string) {
+    const std::string t = text16;
+    if (n < 0 || classes <= 0 || t.size() != (size_t)n * classes * 16)
+      throw std::invalid_argument("text16 must hold n * classes 16-byte slots");
+    for (size_t i = 15; i < t.size(); i += 16)
+      if ((unsigned char)t[i] > 15) throw std::invalid_argument("slot length > 15");
+    std::string out;
+    codec::encode_predictions_text(reinterpret_cast<const uint8_t*>(t.data()), n, classes,
+                                   json_string, out);
+    return py::bytes(out);
+  }, py::arg("text16"), py::arg("n"), py::arg("classes"), py::arg("json_string") = false);
   m.def("encode_instances", [](py::array_t<float, py::array::c_style | py::array::forcecast> x) {
     if (x.ndim() != 4) throw std::invalid_argument("instances must be [N, H, W, C]");
     std::string out;

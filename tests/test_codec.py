@@ -124,3 +124,18 @@ def test_instances_roundtrip(n, h, w, c, seed):
     st2, y = C.parse_instances_host(data, h, w, c)
     assert st2 == OK
     np.testing.assert_array_equal(y, x)
+
+
+@pytest.mark.parametrize("json_string", [False, True])
+def test_encode_predictions_text_slots_match_float_encoder(json_string):
+    """The engine's path for device-formatted predictions (16-byte slots, length in byte 15,
+    csrc/kernels/format.hip) produces exactly the bytes of the float encoder."""
+    rng = np.random.default_rng(7)
+    p = rng.random((3, 10)).astype(np.float32)
+    p[0, 0], p[1, 1], p[2, 2] = 0.0, 1.0, 1.4e-45
+    slots = bytearray()
+    for v in p.ravel():
+        s = C.format_float_java(float(v)).encode()
+        slots += s + bytes(15 - len(s)) + bytes([len(s)])
+    got = C.encode_predictions_text(bytes(slots), 3, 10, json_string)
+    assert got == C.encode_predictions(p, json_string)
