@@ -43,9 +43,9 @@ bool valid_topic(const std::string& t) {
 void set_sock_opts(int fd) {
   int one = 1;
   setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
-  int sz = 8 << 20;
-  setsockopt(fd, SOL_SOCKET, SO_SNDBUF, &sz, sizeof(sz));
-  setsockopt(fd, SOL_SOCKET, SO_RCVBUF, &sz, sizeof(sz));
+  const int sz = socket_buffer_bytes();
+  if (sz > 0) setsockopt(fd, SOL_SOCKET, SO_SNDBUF, &sz, sizeof(sz));
+  if (sz > 0) setsockopt(fd, SOL_SOCKET, SO_RCVBUF, &sz, sizeof(sz));
   fcntl(fd, F_SETFL, fcntl(fd, F_GETFL) | O_NONBLOCK);
 }
 
@@ -377,9 +377,9 @@ void Broker::accept_loop() {
     }
     int one = 1;
     setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
-    int sz = 8 << 20;
-    setsockopt(fd, SOL_SOCKET, SO_SNDBUF, &sz, sizeof(sz));
-    setsockopt(fd, SOL_SOCKET, SO_RCVBUF, &sz, sizeof(sz));
+    const int sz = socket_buffer_bytes();
+    if (sz > 0) setsockopt(fd, SOL_SOCKET, SO_SNDBUF, &sz, sizeof(sz));
+    if (sz > 0) setsockopt(fd, SOL_SOCKET, SO_RCVBUF, &sz, sizeof(sz));
     std::lock_guard<std::mutex> lk(conn_mu_);
     if (!running_) {
       close(fd);

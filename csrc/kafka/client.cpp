@@ -91,9 +91,9 @@ Connection::Connection(const std::string& host, int port, const ClientConfig& cf
   fcntl(fd_, F_SETFL, fcntl(fd_, F_GETFL) & ~O_NONBLOCK);
   int one = 1;
   setsockopt(fd_, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
-  int sz = 8 << 20;
-  setsockopt(fd_, SOL_SOCKET, SO_RCVBUF, &sz, sizeof(sz));
-  setsockopt(fd_, SOL_SOCKET, SO_SNDBUF, &sz, sizeof(sz));
+  const int sz = socket_buffer_bytes();
+  if (sz > 0) setsockopt(fd_, SOL_SOCKET, SO_RCVBUF, &sz, sizeof(sz));
+  if (sz > 0) setsockopt(fd_, SOL_SOCKET, SO_SNDBUF, &sz, sizeof(sz));
   timeval tv{cfg.request_timeout_ms / 1000, (cfg.request_timeout_ms % 1000) * 1000};
   setsockopt(fd_, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof(tv));
   setsockopt(fd_, SOL_SOCKET, SO_SNDTIMEO, &tv, sizeof(tv));

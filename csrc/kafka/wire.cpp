@@ -1,6 +1,8 @@
 // Kafka wire primitives: CRC32C and the RecordBatch v2 codec (see wire.h).
 #include "wire.h"
 
+#include <stdlib.h>
+
 #include <immintrin.h>
 #include <nmmintrin.h>
 
@@ -417,6 +419,14 @@ std::vector<Header> decode_headers(const uint8_t* base, const RecordRef& rr) {
     hs.push_back(std::move(h));
   }
   return hs;
+}
+
+int socket_buffer_bytes() {
+  static const int v = [] {
+    const char* e = getenv("GALE_SOCK_BUF");
+    return e && *e ? atoi(e) : (8 << 20);
+  }();
+  return v;
 }
 
 }  // namespace kafka

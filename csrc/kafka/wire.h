@@ -250,5 +250,10 @@ size_t decode_records(const uint8_t* base, size_t off, size_t len, int64_t min_o
 
 std::vector<Header> decode_headers(const uint8_t* base, const RecordRef& r);
 
+// SO_SNDBUF / SO_RCVBUF for broker and client sockets: GALE_SOCK_BUF bytes (read once; default
+// 8 MiB). 0 leaves the kernel's buffer autotuning on (an explicit size turns it off and is
+// clamped to net.core.{w,r}mem_max).
+int socket_buffer_bytes();
+
 }  // namespace kafka
 }  // namespace gale
