@@ -64,15 +64,23 @@ __device__ __forceinline__ void glds16(const void* src, void* lds_base) {
 // workgroups per CU; an A/B variant, see g_gemm_ring). The ring waits with an explicit vmcnt
 // that leaves the younger stage in flight and a bare s_barrier (a __syncthreads would drain
 // every outstanding load).
-template <int BM, int BN, bool STEM, int NST>
-__global__ __launch_bounds__(256, NST == 1 ? 4 : 2) void conv_gemm_kernel(GemmConvArgs a) {
-  constexpr int WM = 2, WN = 2;                 // 4 waves as 2 (pixels) x 2 (channels)
+// BM = 256: 8 waves (512 threads) as 4 x 2, one workgroup per CU (96 KB of stages): the same
+// waves per SIMD as two 128-pixel workgroups, but each 64-deep k-step stages 48 KB instead of
+// 2 x 32 KB for the same MFMA work (intensity 85 instead of 64 FLOP per staged byte).
+// WM = 2 with BM = 256: 4 waves of 128 x 64 (TM = 8: 128 accumulator registers, one wave per
+// SIMD), 25 % fewer LDS fragment bytes per MFMA than 64 x 64 wave tiles.
+template <int BM, int BN, bool STEM, int NST, int WM = BM / 64>
+__global__ __launch_bounds__(WM * 128, NST == 1 ? 4 : (BM == 256 ? 1 : 2))
+void conv_gemm_kernel(GemmConvArgs a) {
+  constexpr int WN = 2;                         // waves as WM (pixels) x 2 (channels)
+  constexpr int NW = WM * WN;                   // waves per workgroup
   constexpr int TM = BM / WM / 16;              // 16-pixel tiles per wave
   constexpr int TN = BN / WN / 16;              // 16-channel tiles per wave
-  constexpr int XI = BM / 32;                   // X wave-instructions (8 rows each) per wave
-  constexpr int WI = BN / 32;                   // W wave-instructions per wave
+  constexpr int XI = BM / (8 * NW);             // X wave-instructions (8 rows each) per wave
+  constexpr int WI = BN / (8 * NW);             // W wave-instructions per wave
+  static_assert(XI >= 1 && WI >= 1, "tile too small for the workgroup");
   constexpr int STAGE = (BM + BN) * 128;        // bytes per LDS stage
-  constexpr int EPI = 4 * (TM / 2 * 16) * (BN / WN + 4) * 4;  // epilogue staging bytes
+  constexpr int EPI = NW * (TM / 2 * 16) * (BN / WN + 4) * 4;  // epilogue staging bytes
   constexpr int LDS_BYTES = NST * STAGE > EPI ? NST * STAGE : EPI;
   __shared__ __attribute__((aligned(1024))) uint8_t lds[LDS_BYTES];
 
@@ -180,6 +188,8 @@ __global__ __launch_bounds__(256, NST == 1 ? 4 : 2) void conv_gemm_kernel(GemmCo
   // add are loaded into registers while the last k-step's MFMAs run, so their DRAM latency is
   // hidden instead of stalling the epilogue (the 1x1 expansion convs with a shortcut were
   // latency-bound at ~3 TB/s, profiles/r2_resnet50_layers_pmc.txt)
+  // (not for 256-pixel tiles: 512-thread workgroups get 128 VGPRs, no room for 32 more)
+  constexpr bool PREF = NST >= 2 && (BM == 128 || WM == 2);
   constexpr int CW = BN / WN;      // channels per wave
   constexpr int EPS = CW + 4;      // fp32 row stride (+16 B: conflict-free 16-row writes)
   constexpr int LPR = CW / 8;      // lanes per pixel row on read-back
@@ -220,7 +230,7 @@ __global__ __launch_bounds__(256, NST == 1 ? 4 : 2) void conv_gemm_kernel(GemmCo
       cur = lds + (kb & 1) * STAGE;
       if (kb + 1 < a.nkb) stage(kb + 1, lds + ((kb + 1) & 1) * STAGE);
     }
-    if (NST >= 2 && kb + 1 == a.nkb && a.has_res && a.res_prefetch) prefetch_res();
+    if (PREF && kb + 1 == a.nkb && a.has_res && a.res_prefetch) prefetch_res();
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       const int chunk = kk * 4 + fq;
@@ -246,7 +256,7 @@ __global__ __launch_bounds__(256, NST == 1 ? 4 : 2) void conv_gemm_kernel(GemmCo
   // a 16-byte access and a wave instruction covers whole 128-byte rows. fp32 in LDS keeps the
   // rounding identical to the register epilogue (one bf16 rounding after the residual/ReLU).
   // Two halves of TM/2 pixel tiles each fit the 2-stage LDS allocation.
-  static_assert(4 * HALF * EPS * 4 <= LDS_BYTES, "epilogue staging exceeds the LDS allocation");
+  static_assert(NW * HALF * EPS * 4 <= LDS_BYTES, "epilogue staging exceeds the LDS allocation");
   __syncthreads();  // every wave is done with the last k-stage
   float* ep = reinterpret_cast<float*>(lds) + wave * HALF * EPS;
 #pragma unroll
@@ -276,7 +286,7 @@ __global__ __launch_bounds__(256, NST == 1 ? 4 : 2) void conv_gemm_kernel(GemmCo
         float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
         const size_t o = (size_t)m * a.Cout + c0 + cc;
         if (a.has_res) {
-          const bf16x8 rr = (NST >= 2 && a.res_prefetch) ? rpre[h][j] : ld_bf16x8(a.res + o);
+          const bf16x8 rr = (PREF && a.res_prefetch) ? rpre[h][j] : ld_bf16x8(a.res + o);
 #pragma unroll
           for (int e = 0; e < 8; ++e) v[e] += (float)rr[e];
         }
@@ -317,6 +327,15 @@ static std::atomic<bool> g_gemm_res_prefetch{[] {
 // measured slower at batch 256 (4.86 -> 5.71 ms; batch 64: 1.78 -> 1.74 ms,
 // profiles/r2_resnet50_gemm_ab.txt) - the halved channel tile doubles the im2col traffic per
 // FLOP, which costs more than the extra step of look-ahead gains
+// 256 x 128 tiles for layers with >= 2 k-steps, OFF by default (A/B variants): GALE_GEMM_BM256=1
+// 8 waves of 64 x 64 whenever eligible, 2 the same when the tiles fill the chip twice, 3 four
+// waves of 128 x 64. Measured at ResNet-50 batch 256 (profiles/r2_resnet50_gemm_ab.txt):
+// 4.87 ms default vs 5.34 (2), 5.44 (1), 6.10 (3) - neither fewer staged bytes per FLOP nor
+// larger wave tiles at one wave per SIMD beat two 128 x 128 workgroups per CU
+static std::atomic<int> g_gemm_bm256{[] {
+  const char* e = getenv("GALE_GEMM_BM256");
+  return e && *e ? atoi(e) : 0;
+}()};
 static std::atomic<bool> g_gemm_ring{[] {
   const char* e = getenv("GALE_GEMM_RING");
   return e && *e == '1';
@@ -363,7 +382,18 @@ hipError_t conv2d_gemm(const ConvDesc& d, int batch, const void* x, const void* 
   a.n_tiles = d.Npad / bn;
   a.nwg = m_tiles * a.n_tiles;
   const bool one = a.nkb == 1 && g_gemm_single_stage.load(std::memory_order_relaxed);
-  if (!d.stem && a.nkb >= 3 && g_gemm_ring.load(std::memory_order_relaxed)) {
+  const int big = g_gemm_bm256.load(std::memory_order_relaxed);
+  const int m256 = (a.M + 255) / 256;
+  if (!d.stem && !one && bn == 128 && big &&
+      (big == 1 || big == 3 || (long long)m256 * a.n_tiles >= 2 * 256)) {
+    a.nwg = m256 * a.n_tiles;
+    if (big == 3)
+      hipLaunchKernelGGL((conv_gemm_kernel<256, 128, false, 2, 2>), dim3(a.nwg), dim3(256), 0,
+                         stream, a);
+    else
+      hipLaunchKernelGGL((conv_gemm_kernel<256, 128, false, 2>), dim3(a.nwg), dim3(512), 0,
+                         stream, a);
+  } else if (!d.stem && a.nkb >= 3 && g_gemm_ring.load(std::memory_order_relaxed)) {
     a.n_tiles = d.Npad / 64;  // (Npad % 64 == 0 whenever a 128- or 64-wide tiling is allowed)
     a.nwg = m_tiles * a.n_tiles;
     hipLaunchKernelGGL((conv_gemm_kernel<BM, 64, false, 3>), dim3(a.nwg), dim3(256), 0, stream,
