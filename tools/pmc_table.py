@@ -63,6 +63,8 @@ def main():
     ap.add_argument("--cus", type=int, default=256)
     ap.add_argument("--label-model", default="", help="label dispatches by the model's plan")
     ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--show", default="", help="extra counters (comma list) printed per layer "
+                    "as per-CU-cycle rates: value / (GRBM_GUI_ACTIVE / xcds * cus)")
     a = ap.parse_args()
     if a.label_model:
         return per_layer(a)
@@ -106,6 +108,7 @@ def per_layer(a):
     sequence); counters joined by dispatch position within the forward."""
     labels = layer_labels(a.label_model, a.batch)
     n = len(labels)
+    show = [k for k in a.show.split(",") if k]
 
     def ordered(path):
         rows = []
@@ -133,7 +136,8 @@ def per_layer(a):
             if d in pos:
                 ctr[pos[d]][r["Counter_Name"]].append(float(r["Counter_Value"]))
     print(f"{'layer':44s} {'us':>7s} {'TF/s':>6s} {'%pk':>5s} {'minGB':>6s} {'TB/s':>5s} "
-          f"{'hbmGB':>6s} {'mfma%':>6s} {'ldsCf':>6s} {'L2hit':>6s}")
+          f"{'hbmGB':>6s} {'mfma%':>6s} {'ldsCf':>6s} {'L2hit':>6s}"
+          + "".join(f" {k[3:17] if k.startswith('SQ_') else k[:14]:>14s}" for k in show))
     tot_us = tot_fl = 0.0
     for i in range(n):
         name, fl, by = labels[i]
@@ -151,7 +155,8 @@ def per_layer(a):
         hit, miss = c.get("TCC_HIT_sum", 0.0), c.get("TCC_MISS_sum", 0.0)
         l2 = 100.0 * hit / (hit + miss) if hit + miss else 0.0
         print(f"{name:44s} {us:7.1f} {tf:6.0f} {100 * tf / a.peak_tf:5.1f} {by / 1e9:6.3f} "
-              f"{tbs:5.2f} {hbm:6.3f} {mfma:6.1f} {cf:6.2f} {l2:6.1f}")
+              f"{tbs:5.2f} {hbm:6.3f} {mfma:6.1f} {cf:6.2f} {l2:6.1f}"
+              + "".join(f" {c.get(k, 0.0) / (cyc * a.cus) if cyc else 0.0:14.3f}" for k in show))
     print(f"{'TOTAL':44s} {tot_us:7.1f} {tot_fl / (tot_us * 1e-6) / 1e12:6.0f}")
 
 
