@@ -52,14 +52,16 @@ def parse_args(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--step-images", type=int, default=65536,
-                    help="images per GPU per step (the unit of --steps / --warmup)")
+    ap.add_argument("--step-images", type=int, default=0,
+                    help="images per GPU per step (the unit of --steps / --warmup); default "
+                         "65536 (4096 for resnet50)")
     ap.add_argument("--min-warmup-s", type=float, default=2.0)
     ap.add_argument("--max-warmup-s", type=float, default=20.0)
     ap.add_argument("--model", default="resnet20", choices=["lenet5", "resnet20", "resnet50"])
     ap.add_argument("--batch", type=int, default=256, help="images per micro-batch (max_batch)")
     ap.add_argument("--images-per-record", type=int, default=1)
-    ap.add_argument("--distinct", type=int, default=65536, help="distinct synthetic images")
+    ap.add_argument("--distinct", type=int, default=0,
+                    help="distinct synthetic images (default 65536; 256 = 435 MB for resnet50)")
     ap.add_argument("--partitions", type=int, default=0,
                     help="input partitions per GPU (default: one per replica, BASELINE config 3)")
     ap.add_argument("--source-parallelism", type=int, default=0,
@@ -70,7 +72,8 @@ def parse_args(argv=None):
     ap.add_argument("--replicas-per-gpu", type=int, default=0,
                     help="model replicas (streams) per GPU (0 = from the host CPU share: 6 "
                          "with >= 16 cores per GPU, else ~1 per 4 cores, at most 4)")
-    ap.add_argument("--max-wait-us", type=int, default=2000)
+    ap.add_argument("--max-wait-us", type=int, default=-1,
+                    help="micro-batch wait (default 2000; 20000 for resnet50)")
     ap.add_argument("--queue-batches", type=int, default=4,
                     help="records buffered in the engine, in units of --batch")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp8", "fp32"])
@@ -191,12 +194,29 @@ def main(argv=None) -> int:
     # per GPU, 12 input partitions (TCP connections), 6 replica streams and 4 ingest workers
     # saturate the share (1.47 M img/s vs 0.97 M with 4/4/2 on one MI355X box,
     # profiles/r2_host_pipeline_shape_ab.txt); smaller shares keep ~4 cores per replica.
+    # ResNet-50 records are 1.7 MB of JSON each: the GPU, not the host, sets the pace unless the
+    # batches are full, so fewer replicas wait longer for full 256-image batches while 12
+    # partitions keep the fetches parallel (29.0 k img/s vs 23.8 k with the CIFAR sizing,
+    # profiles/r2_configs_1_4_e2e.txt)
+    r50 = a.model == "resnet50"
+    if a.step_images <= 0:
+        a.step_images = 4096 if r50 else 65536
+    if a.distinct <= 0:
+        a.distinct = 256 if r50 else 65536
+    if a.max_wait_us < 0:
+        a.max_wait_us = 20000 if r50 else 2000
     cpus = host_cpus_per_rank()
     big = cpus >= 16
     if a.replicas_per_gpu <= 0:
-        a.replicas_per_gpu = 6 if big else max(1, min(4, int(cpus // 4)))
+        if r50:
+            a.replicas_per_gpu = 2
+        else:
+            a.replicas_per_gpu = 6 if big else max(1, min(4, int(cpus // 4)))
     if a.partitions <= 0:
-        a.partitions = 2 * a.replicas_per_gpu if big else a.replicas_per_gpu
+        if r50:
+            a.partitions = 12 if big else 4
+        else:
+            a.partitions = 2 * a.replicas_per_gpu if big else a.replicas_per_gpu
     if a.decode_threads <= 0:
         a.decode_threads = 4 if big else 2
     rank = int(os.environ.get("RANK", "0"))
