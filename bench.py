@@ -329,7 +329,7 @@ def main(argv=None) -> int:
         if not eng.wait_completed(c0 + k * step_records, a.timeout):
             reached = False
             break
-        marks.append(time.perf_counter())
+        marks.append((time.perf_counter(), eng.completed))
     if use_gpu:
         torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
@@ -360,7 +360,14 @@ def main(argv=None) -> int:
     if rank == 0:
         value = total_images / elapsed_max
         n_gpus = world * local_gpus
-        step_rates = [step_records * ipr / (b - a_) for a_, b in zip([t0] + marks[:-1], marks)]
+        # per-step rates from (time, completed) marks; a completion burst can cross several step
+        # boundaries at once, so intervals shorter than half a mean step are merged with the next
+        step_rates, ta, ca = [], t0, c0
+        for tb, cb in marks:
+            if tb - ta >= 0.5 * elapsed / max(1, len(marks)) and cb > ca:
+                step_rates.append((cb - ca) * ipr / (tb - ta))
+                ta, ca = tb, cb
+        step_rates = step_rates or [value]
         med = statistics.median(step_rates)
         cores = {k: round((cpu1[k] - cpu0[k]) / elapsed, 2) for k in cpu1}
         out = {
