@@ -109,11 +109,12 @@ hipError_t softmax_rows(int batch, int N, int ld, const float* x, float* out, hi
 
 // fp32 -> bf16 cast with optional affine normalisation y = x*scale + shift (n elements).
 // Inference BatchNorm (per-channel scale/shift; nullptr = identity) + optional residual + ReLU
-// over NHWC bf16, [batch, HW = Ho*Wo, C stored]. The residual is [batch, res_H, res_W, res_C],
-// read at (ho*rs, wo*rs), zero for channels >= res_C. In-place (x == y) is allowed.
+// over NHWC bf16 (et = ET_BF16) or fp32 (ET_F32: the fp32 unfolded-BN plan), [batch,
+// HW = Ho*Wo, C stored]. The residual is [batch, res_H, res_W, res_C], read at (ho*rs, wo*rs),
+// zero for channels >= res_C. In-place (x == y) is allowed.
 hipError_t bn_act(int batch, int HW, int Wo, int C, const void* x, const float* scale,
                   const float* shift, const void* res, int res_H, int res_W, int res_C, int rs,
-                  int relu, void* y, hipStream_t stream);
+                  int relu, void* y, hipStream_t stream, int et = 0);
 
 hipError_t cast_f32_bf16(int64_t n, float scale, float shift, const float* x, void* y,
                          hipStream_t stream);

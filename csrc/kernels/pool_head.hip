@@ -198,24 +198,25 @@ __global__ __launch_bounds__(256) void cast_kernel(int64_t n4, float scale, floa
   reinterpret_cast<uint2*>(y)[i] = __builtin_bit_cast(uint2, o);
 }
 
-// Standalone inference BatchNorm + residual + ReLU over NHWC bf16 (TF FusedBatchNorm + Add +
-// Relu): y = act(x * scale[c] + shift[c] + res). The fast path folds BN into the conv weights
+// Standalone inference BatchNorm + residual + ReLU over NHWC bf16 or fp32 (ET; TF
+// FusedBatchNorm + Add + Relu): y = act(x * scale[c] + shift[c] + res). The fast path folds BN into the conv weights
 // and fuses the rest into the conv epilogue; this kernel serves the unfolded (fold_bn=False)
 // plan and the standalone ops. scale == nullptr -> identity affine (plain ReLU / add). The
 // residual is read at (ho*rs, wo*rs) with res_C stored channels and zero above them (ResNet
 // option-A shortcut when rs == 2). One lane per 8 channels of one pixel (16-byte accesses).
+template <int ET>
 __global__ __launch_bounds__(256) void bn_act_kernel(int total, int HW, int Wo, int C8,
-                                                     const bf16* x, const float* scale,
-                                                     const float* shift, const bf16* res,
+                                                     const void* x, const float* scale,
+                                                     const float* shift, const void* res,
                                                      int res_H, int res_W, int res_C, int rs,
-                                                     int relu, bf16* y) {
+                                                     int relu, void* y) {
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i >= total) return;
   const int cg = i % C8;
   const int pix = i / C8;
   const size_t off = (size_t)pix * (C8 * 8) + cg * 8;
   float v[8];
-  load8f<ET_BF16>(x, off, v);
+  load8f<ET>(x, off, v);
   if (scale) {
     const float4* s4 = reinterpret_cast<const float4*>(scale) + cg * 2;
     const float4* t4 = reinterpret_cast<const float4*>(shift) + cg * 2;
@@ -231,7 +232,7 @@ __global__ __launch_bounds__(256) void bn_act_kernel(int total, int HW, int Wo, 
     const int ho = q / Wo;
     const int wo = q - ho * Wo;
     float r[8];
-    load8f<ET_BF16>(res, ((size_t)(n * res_H + ho * rs) * res_W + wo * rs) * res_C + cg * 8, r);
+    load8f<ET>(res, ((size_t)(n * res_H + ho * rs) * res_W + wo * rs) * res_C + cg * 8, r);
 #pragma unroll
     for (int j = 0; j < 8; ++j) v[j] += r[j];
   }
@@ -239,7 +240,7 @@ __global__ __launch_bounds__(256) void bn_act_kernel(int total, int HW, int Wo, 
 #pragma unroll
     for (int j = 0; j < 8; ++j) v[j] = fmaxf(v[j], 0.f);
   }
-  store8f<ET_BF16>(y, off, v);
+  store8f<ET>(y, off, v);
 }
 
 }  // namespace
@@ -302,17 +303,17 @@ hipError_t cast_f32_bf16(int64_t n, float scale, float shift, const float* x, vo
 
 hipError_t bn_act(int batch, int HW, int Wo, int C, const void* x, const float* scale,
                   const float* shift, const void* res, int res_H, int res_W, int res_C, int rs,
-                  int relu, void* y, hipStream_t stream) {
+                  int relu, void* y, hipStream_t stream, int et) {
   if (batch <= 0) return hipSuccess;
+  if (et != ET_BF16 && et != ET_F32) return hipErrorInvalidValue;
   if (C % 8 || res_C % 8 || HW <= 0 || Wo <= 0 || HW % Wo || (scale && !shift)) return hipErrorInvalidValue;
   if (res && (rs < 1 || res_C > C || (HW / Wo - 1) * rs >= res_H || (Wo - 1) * rs >= res_W))
     return hipErrorInvalidValue;
   const long long total = (long long)batch * HW * (C / 8);
   if (total > 0x7fffffffLL) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(bn_act_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream,
-                     (int)total, HW, Wo, C / 8, reinterpret_cast<const bf16*>(x), scale, shift,
-                     reinterpret_cast<const bf16*>(res), res_H, res_W, res_C, rs, relu,
-                     reinterpret_cast<bf16*>(y));
+  auto k = et == ET_F32 ? bn_act_kernel<ET_F32> : bn_act_kernel<ET_BF16>;
+  hipLaunchKernelGGL(k, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream, (int)total,
+                     HW, Wo, C / 8, x, scale, shift, res, res_H, res_W, res_C, rs, relu, y);
   return hipGetLastError();
 }
 

@@ -100,7 +100,7 @@ void Executor::launch_all(int batch, void* const* bufs, hipStream_t stream) {
       case OP_BN_ACT:
         e = bn_act(batch, op.p[0], op.p[1], op.p[2], in, static_cast<const float*>(op.w), op.bias,
                    op.res >= 0 ? bufs[op.res] : nullptr, op.p[4], op.p[5], op.p[6], op.p[7],
-                   op.p[3], out, stream);
+                   op.p[3], out, stream, (int)op.fp8);
         break;
       case OP_RESNET20: {
         const bool f8 = op.fp8 != 0;

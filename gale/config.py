@@ -87,7 +87,7 @@ class GaleConfig:
     use_graph: bool = True
     gpu_wait_poll_us: int = 20         # > 0: replicas sleep-poll their batch events (0: spin)
     gpu_encode: bool = True            # prediction text (Float.toString) formatted on the GPU
-    fold_bn: bool = True               # False: standalone BatchNorm kernels (debug/parity plan)
+    fold_bn: bool = True               # False: standalone BatchNorm kernels (bf16 / fp32)
     stub: bool = False                 # CPU stub replicas (plumbing without a GPU)
     stub_null: bool = False            # stub replicas skip parsing/compute (host-path benchmark)
     # robustness / observability
@@ -127,8 +127,8 @@ class GaleConfig:
             raise ValueError("replicas/gpus must be >= 0")
         if not self.topology_name:
             raise ValueError("topology name is required")
-        if not self.fold_bn and self.dtype != "bf16":
-            raise ValueError("--no-fold-bn (standalone BatchNorm plan) is bf16 only")
+        if not self.fold_bn and self.dtype == "fp8":
+            raise ValueError("--no-fold-bn (standalone BatchNorm plan) is bf16 / fp32 only")
         return self
 
     @property

@@ -273,9 +273,9 @@ def _conv_geometry(net: Network, L: Conv, wdtype: str = "bf16") -> Dict[str, int
 def param_layout(net: Network, wdtype: str = "bf16",
                  fold_bn: bool = True) -> Tuple[Dict[str, PackedEntry], int]:
     """Byte layout of the packed parameter buffer (depends only on the architecture).
-    ``fold_bn=False`` (bf16 only) adds a BN scale and shift vector per BatchNorm conv."""
-    if not fold_bn and wdtype != "bf16":
-        raise ValueError("the unfolded-BN plan is bf16 only")
+    ``fold_bn=False`` (bf16 / fp32) adds a BN scale and shift vector per BatchNorm conv."""
+    if not fold_bn and wdtype == "fp8":
+        raise ValueError("the unfolded-BN plan is bf16 / fp32 only")
     wbytes = {"bf16": 2, "fp8": 1, "fp32": 4}[wdtype]
     layout: Dict[str, PackedEntry] = {}
     off = 0
@@ -519,7 +519,8 @@ def build_plan(net: Network, base_ptr: int, wdtype: str = "bf16",
                 ho, wo, c = net.shapes[L.out]
                 bn = dict(kind=OP_BN_ACT, **{"in": buf_of[out_name]}, out=buf_of[out_name], res=-1,
                           w=base_ptr + layout[f"{L.name}.bn_s"].offset,
-                          bias=base_ptr + layout[f"{L.name}.bn_t"].offset)
+                          bias=base_ptr + layout[f"{L.name}.bn_t"].offset,
+                          et=2 if f32 else 0)
                 p = [ho * wo, wo, stored_channels(c), int(L.relu), 0, 0, 0, 1]
                 if L.residual is not None:
                     rh, rw, rc = net.shapes[L.residual]

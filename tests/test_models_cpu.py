@@ -123,3 +123,8 @@ def test_unfolded_bn_plan_structure(name):
     assert torch.allclose(u[f"{L.name}.bias"] * s + t, f[f"{L.name}.bias"], atol=1e-5)
     with pytest.raises(ValueError):
         param_layout(net, "fp8", fold_bn=False)
+    # fp32 unfolded plan: fp32 weights + the same BN vectors, bn_act ops on fp32 tensors (et 2)
+    lay32, _ = param_layout(net, "fp32", fold_bn=False)
+    assert f"{L.name}.bn_s" in lay32 and lay32[f"{L.name}.w"].dtype == torch.float32
+    ops32, _ = build_plan(net, 0, wdtype="fp32", fold_bn=False)
+    assert all(op.get("et") == 2 for op in ops32 if op["kind"] == OP_BN_ACT)

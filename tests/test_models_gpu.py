@@ -208,6 +208,29 @@ def test_unfolded_bn_plan_matches_reference(name, batch):
     assert torch.equal(graph, eager)
 
 
+@pytest.mark.parametrize("name,batch", [("resnet20", 19), ("resnet50", 2)])
+def test_fp32_unfolded_bn_plan_matches_reference(name, batch):
+    """--dtype fp32 --no-fold-bn: raw fp32 convs, then the standalone BatchNorm(+residual+ReLU)
+    kernel on fp32 NHWC (TF's Conv2D -> FusedBatchNorm with no extra rounding point): relative
+    logit error < 1e-4 against the fp32 oracle."""
+    from gale.models.graph import OP_BN_ACT
+
+    net = get_model(name)
+    params = init_params(net, seed=23, calib_batch=4 if name == "resnet50" else 16)
+    packed = materialize_weights(net, torch.device("cuda", 0), params=params, wdtype="fp32",
+                                 fold_bn=False)
+    rep = ModelReplica(net, packed, max_batch=32, slots=1, wdtype="fp32", fold_bn=False)
+    assert sum(op["kind"] == OP_BN_ACT for op in rep.ops) > 0
+    x = torch.rand((batch,) + net.input_shape, generator=torch.Generator().manual_seed(6))
+    ref = forward(net, fold_params(net, params), x)
+    got = rep.infer(x, use_graph=True).cpu()
+    torch.cuda.synchronize()
+    err = rel_logit_err(got, ref).max().item()
+    print(f"\n{name} fp32 unfolded-BN rel logit err {err:.2e}")
+    assert err < 1e-4, err
+    assert torch.equal(got.argmax(1), ref.argmax(1))
+
+
 @pytest.mark.parametrize("name,batch", [("lenet5", 13), ("resnet20", 37), ("resnet50", 3)])
 def test_fp32_plan_matches_fp32_reference(name, batch):
     """--dtype fp32: the reference-precision plan (fp32 weights and activations, convs on the fp32
