@@ -969,7 +969,15 @@ void Engine::slo_step() {
   int64_t w = eff_wait_ns_.load();
   size_t queued = 0;
   for (auto& q : batchers_) queued += q->size();
-  const bool backlog = (int64_t)queued > (int64_t)b * (int64_t)replicas_.size();
+  // Overload shows as records waiting anywhere - in the batchers, or still in the broker when
+  // fetch/decode is the tight stage (then the batchers look empty): a latency miss under
+  // overload needs capacity (bigger batches), not smaller ones. Unacknowledged records beyond
+  // what the replicas hold in flight at the current batch size count as backlog.
+  int64_t unacked = 0;
+  for (const PartitionOffsets& o : partition_offsets()) unacked += o.lag;
+  const int64_t in_flight = (int64_t)b * (int64_t)replicas_.size() * 3;
+  const bool backlog =
+      (int64_t)queued > (int64_t)b * (int64_t)replicas_.size() || unacked > 2 * in_flight;
   if (p99_ms > cfg_.slo_p99_ms) {
     if (backlog) {
       b = std::min(maxb, b + std::max(1, maxb / 8));  // overload: capacity first

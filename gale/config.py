@@ -90,6 +90,7 @@ class GaleConfig:
     fold_bn: bool = True               # False: standalone BatchNorm kernels (bf16 / fp32)
     stub: bool = False                 # CPU stub replicas (plumbing without a GPU)
     stub_null: bool = False            # stub replicas skip parsing/compute (host-path benchmark)
+    stub_delay_us: int = 0             # stub replicas: emulated device time per batch
     # robustness / observability
     watchdog_ms: int = 30000
     # supervisor (Storm supervisors restart dead workers): a replica that failed is

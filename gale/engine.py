@@ -60,7 +60,8 @@ class Engine:
             self._native = native().Engine(d)
             for i in range(max(1, cfg.replicas)):
                 loc = stub_localities[i % len(stub_localities)] if stub_localities else -1
-                self._native.add_stub_replica(cfg.max_batch, 0, not cfg.stub_null, loc)
+                self._native.add_stub_replica(cfg.max_batch, cfg.stub_delay_us, not cfg.stub_null,
+                                              loc)
             return
         if model_replicas is not None:
             reps = list(model_replicas)

@@ -266,3 +266,70 @@ def test_locality_slots_and_work_stealing(broker):
     # replicas 1 and 3 (locality 1) had no input of their own: whatever they served was stolen
     assert sum(served) == 200
     assert st["steals"] > 0 and served[1] + served[3] > 0
+
+
+def _trickle(broker, n, interval_s, seed=0):
+    import threading
+    import time as _t
+
+    rng = np.random.default_rng(seed)
+    recs = [C.encode_instances(rng.random((1, H, W, CH), dtype=np.float32)) for _ in range(8)]
+
+    def run():
+        for i in range(n):
+            broker.append("in", i % 2, [recs[i % 8]])
+            _t.sleep(interval_s)
+
+    t = threading.Thread(target=run, daemon=True)
+    t.start()
+    return t
+
+
+def test_slo_controller_shrinks_wait_when_batching_delay_misses():
+    """--slo-p99-ms: with a trickle of records and a long batching window the latency is the
+    window itself; the controller must shorten it (and the batch cap) to meet the target."""
+    b = K.Broker()
+    b.start()
+    b.create_topic("in", 2)
+    b.create_topic("out", 1)
+    try:
+        t = _trickle(b, 300, 0.005)
+        cfg = make_cfg(b, max_batch=64, max_wait_us=40000, slo_p99_ms=5.0, replicas=1)
+        eng = Engine(cfg, max_records=300)
+        eng.start()
+        assert eng.wait(60), eng.stats()
+        st = eng.stats()
+        eng.stop()
+        t.join()
+    finally:
+        b.stop()
+    assert st["slo_adjustments"] > 0
+    assert st["eff_max_wait_us"] < 40000 and st["eff_max_batch"] < 64
+
+
+def test_slo_controller_grows_batches_under_backlog():
+    """Overload (a backlog the replicas cannot drain at the target): a p99 miss calls for
+    capacity, so the controller keeps / grows the batch cap instead of shrinking it."""
+    b = K.Broker()
+    b.start()
+    b.create_topic("in", 2)
+    b.create_topic("out", 1)
+    try:
+        produce_images(b, [1] * 3000)
+        cfg = make_cfg(b, max_batch=64, max_wait_us=2000, slo_p99_ms=1.0, replicas=1,
+                       stub_delay_us=3000, queue_depth=64)  # backlog waits in the broker
+        eng = Engine(cfg, max_records=3000)
+        eng.start()
+        import time as _t
+
+        seen = []  # the batch cap while most of the backlog is still there
+        while not eng.wait(0.05):
+            s = eng.stats()
+            if s["records_out"] < 2000:
+                seen.append((s["eff_max_batch"], s["slo_adjustments"]))
+        st = eng.stats()
+        eng.stop()
+    finally:
+        b.stop()
+    assert st["slo_adjustments"] > 0 and any(adj > 0 for _, adj in seen)
+    assert min(cap for cap, _ in seen) == 64  # never shrunk while the backlog lasted
