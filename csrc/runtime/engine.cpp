@@ -973,8 +973,13 @@ void Engine::slo_step() {
   // fetch/decode is the tight stage (then the batchers look empty): a latency miss under
   // overload needs capacity (bigger batches), not smaller ones. Unacknowledged records beyond
   // what the replicas hold in flight at the current batch size count as backlog.
+  static const bool use_lag = [] {  // (A/B switch: GALE_SLO_LAG_BACKLOG=0 ignores the lag)
+    const char* e = getenv("GALE_SLO_LAG_BACKLOG");
+    return !(e && *e == '0');
+  }();
   int64_t unacked = 0;
-  for (const PartitionOffsets& o : partition_offsets()) unacked += o.lag;
+  if (use_lag)
+    for (const PartitionOffsets& o : partition_offsets()) unacked += o.lag;
   const int64_t in_flight = (int64_t)b * (int64_t)replicas_.size() * 3;
   const bool backlog =
       (int64_t)queued > (int64_t)b * (int64_t)replicas_.size() || unacked > 2 * in_flight;
