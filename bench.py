@@ -108,6 +108,11 @@ def parse_args(argv=None):
                     help="one process drives all --gpus GPUs (one engine: per-GPU locality "
                          "slots with work stealing, weights RCCL-broadcast in-process) instead "
                          "of one torch.distributed rank per GPU")
+    ap.add_argument("--shared-gpu-rehearsal", action="store_true",
+                    help="multi-rank rehearsal on a box with fewer GPUs than ranks: rank r uses "
+                         "GPU r %% device_count and the process group runs over gloo (RCCL refuses "
+                         "two ranks on one GPU); every other part of the per-rank path is the "
+                         "real one. Not a measurement")
     ap.add_argument("--timeout", type=float, default=600.0)
     return ap.parse_args(argv)
 
@@ -235,6 +240,8 @@ def main(argv=None) -> int:
     if use_gpu and local_gpus > torch.cuda.device_count():
         raise SystemExit(f"bench.py: {local_gpus} GPUs requested, "
                          f"{torch.cuda.device_count()} visible")
+    if use_gpu and a.shared_gpu_rehearsal:
+        local_rank %= torch.cuda.device_count()
     if use_gpu:
         torch.cuda.set_device(local_rank)
         if a.numa_pin and local_gpus == 1:
@@ -242,8 +249,9 @@ def main(argv=None) -> int:
 
             pin_to_gpu_numa(local_rank, a.cpus_per_rank)
     if world > 1:
-        dist.init_process_group(backend="nccl" if use_gpu else "gloo",
-                                device_id=torch.device("cuda", local_rank) if use_gpu else None)
+        nccl = use_gpu and not a.shared_gpu_rehearsal
+        dist.init_process_group(backend="nccl" if nccl else "gloo",
+                                device_id=torch.device("cuda", local_rank) if nccl else None)
 
     from gale._native import native
     from gale.config import GaleConfig
@@ -349,7 +357,7 @@ def main(argv=None) -> int:
     images = done_records * ipr  # >= K steps (completions arrive a micro-batch at a time)
     t = torch.tensor([elapsed, float(images)], dtype=torch.float64)
     if world > 1:
-        tt = t.cuda() if use_gpu else t
+        tt = t.cuda() if use_gpu and not a.shared_gpu_rehearsal else t
         mx = tt.clone()
         dist.all_reduce(mx, op=dist.ReduceOp.MAX)
         sm = tt.clone()

@@ -81,6 +81,10 @@ gale::PlanOp op_from_dict(const py::dict& d) {
   if (d.contains("scales")) op.scales = d["scales"].cast<std::vector<float>>();
   op.fp8 = get_or<int>(d, "et", get_or<int>(d, "fp8", 0));  // pool/head activation ElemType
   op.scale = get_or<float>(d, "scale", 1.0f);
+  if (d.contains("bpi")) {
+    auto v = d["bpi"].cast<std::vector<long long>>();
+    for (size_t i = 0; i < v.size() && i < 3; ++i) op.bpi[i] = v[i];
+  }
   return op;
 }
 
@@ -238,17 +242,20 @@ PYBIND11_MODULE(_C, m) {
 
   py::class_<gale::Executor, std::shared_ptr<gale::Executor>>(m, "Executor")
       .def(py::init([](int device, py::list ops, std::vector<long long> buf_bytes, int max_batch,
-                       int slots, std::vector<int> buckets) {
+                       int slots, std::vector<int> buckets, int chunk_ops, int chunk_images) {
              gale::PlanSpec spec;
              for (auto o : ops) spec.ops.push_back(op_from_dict(o.cast<py::dict>()));
              spec.buf_bytes_per_image = std::move(buf_bytes);
              spec.max_batch = max_batch;
              spec.slots = slots;
              spec.buckets = std::move(buckets);
+             spec.chunk_ops = chunk_ops;
+             spec.chunk_images = chunk_images;
              return std::make_shared<gale::Executor>(device, std::move(spec));
            }),
            py::arg("device"), py::arg("ops"), py::arg("buf_bytes"), py::arg("max_batch"),
-           py::arg("slots") = 2, py::arg("buckets") = std::vector<int>{})
+           py::arg("slots") = 2, py::arg("buckets") = std::vector<int>{}, py::arg("chunk_ops") = 0,
+           py::arg("chunk_images") = 0)
       .def("run",
            [](gale::Executor& e, int slot, int batch, uintptr_t stream, bool use_graph) {
              py::gil_scoped_release nogil;

@@ -45,6 +45,7 @@ struct PlanOp {
   std::vector<float> scales;      // OP_RESNET20 fp8 activation scales
   int fp8 = 0;        // pool / head ops: activation ElemType (0 bf16, 1 e4m3, 2 fp32)
   float scale = 1.f;  // head: input activation scale (fp8)
+  long long bpi[3] = {0, 0, 0};  // bytes per image of the in / out / res tensors (chunking)
 };
 
 struct PlanSpec {
@@ -53,6 +54,15 @@ struct PlanSpec {
   int max_batch = 256;
   int slots = 2;                               // independent I/O buffer sets (pipelining depth)
   std::vector<int> buckets;                    // graph batch buckets (ascending); empty = powers of 2
+  // Batch chunking of the leading ops: ops [0, chunk_ops) run once per chunk of chunk_images
+  // images (operands offset by the first image of the chunk times their PlanOp::bpi; activations
+  // are batch-major), the
+  // rest once over the whole batch. Keeps the wide early tensors (ResNet-50 56x56x256 at batch
+  // 256: 411 MB each) small enough to stay in the 256 MB Infinity Cache between producer and
+  // consumer. 0 = off. The plan must keep every tensor that outlives the prefix in a buffer no
+  // other prefix tensor uses (a later chunk would overwrite it): build_plan(chunk_layers=...).
+  int chunk_ops = 0;
+  int chunk_images = 0;
 };
 
 class Executor {
@@ -84,6 +94,9 @@ class Executor {
 
  private:
   void launch_all(int batch, void* const* bufs, hipStream_t stream);
+  // ops [begin, end) for images [c0, c0 + batch) of the buffers (c0 > 0: a chunk)
+  void launch_ops(size_t begin, size_t end, int batch, void* const* bufs, hipStream_t stream,
+                  int c0 = 0);
   int device_;
   PlanSpec spec_;
   std::vector<int> buckets_;

@@ -20,6 +20,13 @@ Executor::Executor(int device, PlanSpec spec) : device_(device), spec_(std::move
     for (int b = 1; b < spec_.max_batch; b *= 2) buckets_.push_back(b);
     buckets_.push_back(spec_.max_batch);
   }
+  if (spec_.chunk_ops < 0 || spec_.chunk_ops > (int)spec_.ops.size() || spec_.chunk_images < 0)
+    throw std::invalid_argument("bad chunk_ops / chunk_images");
+  for (int i = 0; spec_.chunk_images > 0 && i < spec_.chunk_ops; ++i) {
+    const PlanOp& op = spec_.ops[i];
+    if (op.bpi[0] <= 0 || op.bpi[1] <= 0 || (op.res >= 0 && op.bpi[2] <= 0))
+      throw std::invalid_argument("chunked plan op without per-image operand bytes");
+  }
   std::sort(buckets_.begin(), buckets_.end());
   buckets_.erase(std::unique(buckets_.begin(), buckets_.end()), buckets_.end());
   if (buckets_.back() < spec_.max_batch) buckets_.push_back(spec_.max_batch);
@@ -68,14 +75,30 @@ int Executor::bucket_for(int batch) const {
 }
 
 void Executor::launch_all(int batch, void* const* bufs, hipStream_t stream) {
-  for (const PlanOp& op : spec_.ops) {
-    const void* in = bufs[op.in];
-    void* out = bufs[op.out];
+  size_t begin = 0;
+  const int ch = spec_.chunk_images;
+  if (spec_.chunk_ops > 0 && ch > 0 && batch > ch) {
+    for (int c0 = 0; c0 < batch; c0 += ch)
+      launch_ops(0, spec_.chunk_ops, std::min(ch, batch - c0), bufs, stream, c0);
+    begin = spec_.chunk_ops;
+  }
+  launch_ops(begin, spec_.ops.size(), batch, bufs, stream);
+}
+
+void Executor::launch_ops(size_t begin, size_t end, int batch, void* const* bufs,
+                          hipStream_t stream, int c0) {
+  auto at = [&](int id, long long bpi) -> void* {
+    return static_cast<char*>(bufs[id]) + (size_t)c0 * (size_t)bpi;
+  };
+  for (size_t oi = begin; oi < end; ++oi) {
+    const PlanOp& op = spec_.ops[oi];
+    const void* in = at(op.in, op.bpi[0]);
+    void* out = at(op.out, op.bpi[1]);
+    void* res = op.res >= 0 ? at(op.res, op.bpi[2]) : nullptr;
     hipError_t e = hipSuccess;
     switch (op.kind) {
       case OP_CONV:
-        e = conv2d(op.conv, batch, in, op.w, op.bias, op.wscale, op.res >= 0 ? bufs[op.res] : nullptr,
-                   out, stream);
+        e = conv2d(op.conv, batch, in, op.w, op.bias, op.wscale, res, out, stream);
         break;
       case OP_MAXPOOL:
         e = maxpool2d(batch, op.p[0], op.p[1], op.p[2], op.p[3], op.p[4], op.p[5], op.p[6], op.p[7],
@@ -99,7 +122,7 @@ void Executor::launch_all(int batch, void* const* bufs, hipStream_t stream) {
         break;
       case OP_BN_ACT:
         e = bn_act(batch, op.p[0], op.p[1], op.p[2], in, static_cast<const float*>(op.w), op.bias,
-                   op.res >= 0 ? bufs[op.res] : nullptr, op.p[4], op.p[5], op.p[6], op.p[7],
+                   res, op.p[4], op.p[5], op.p[6], op.p[7],
                    op.p[3], out, stream, (int)op.fp8);
         break;
       case OP_RESNET20: {

@@ -429,7 +429,8 @@ def _tensor_bytes(net: Network, name: str, wdtype: str = "bf16") -> int:
 
 def build_plan(net: Network, base_ptr: int, wdtype: str = "bf16",
                act_scales: Optional[Dict[str, float]] = None,
-               fused: bool = True, fold_bn: bool = True) -> Tuple[List[dict], List[int]]:
+               fused: bool = True, fold_bn: bool = True,
+               chunk_layers: int = 0) -> Tuple[List[dict], List[int]]:
     """Executor plan for a packed parameter buffer living at device address ``base_ptr``.
 
     Returns (ops, buf_bytes_per_image). Buffer 0 = fp32 input, 1 = fp32 softmax output, >= 2 =
@@ -439,6 +440,10 @@ def build_plan(net: Network, base_ptr: int, wdtype: str = "bf16",
     resident in LDS). ``fold_bn=False`` (bf16, layer-wise; the buffer from ``pack_params(...,
     fold_bn=False)``): every BatchNorm conv is followed by a standalone ``bn_act`` kernel that
     applies the BN affine, the residual and the ReLU in place (the debugging / parity plan).
+    ``chunk_layers``: the first ``chunk_layers`` layers may run per batch chunk (the executor's
+    PlanSpec::chunk_ops; every op carries ``layer``, its layer index): each tensor they produce
+    that is still read after them gets a buffer of its own, so a later chunk cannot overwrite an
+    earlier chunk's live-out rows.
     """
     fp8 = wdtype == "fp8"
     f32 = wdtype == "fp32"  # reference-precision plan: fp32 everything, fp32 MFMA convs
@@ -456,6 +461,9 @@ def build_plan(net: Network, base_ptr: int, wdtype: str = "bf16",
             last_use[L.residual] = i
     buf_of: Dict[str, int] = {"input": 0}
     buf_bytes: List[int] = [_tensor_bytes(net, "input"), net.classes * 4]
+    # bytes per image of a tensor as stored (every op also carries bpi = [in, out, res] for the
+    # executor's batch chunking, PlanSpec::chunk_ops)
+    tbytes: Dict[str, int] = {"input": _tensor_bytes(net, "input"), "output": net.classes * 4}
     free: List[int] = []
     ops: List[dict] = []
     # fp32 logits tensors (Conv.out_f32) get their own dedicated buffers
@@ -469,7 +477,10 @@ def build_plan(net: Network, base_ptr: int, wdtype: str = "bf16",
                 h, w, c = net.shapes[out_name]
                 need = h * w * stored_channels(c) * 4
             bid = None
+            live_out = i < chunk_layers and last_use.get(out_name, len(net.layers)) >= chunk_layers
             for j, b in enumerate(free):
+                if live_out:
+                    break  # (a fresh buffer: no other prefix tensor ever used it)
                 bid = b
                 free.pop(j)
                 break
@@ -478,6 +489,7 @@ def build_plan(net: Network, base_ptr: int, wdtype: str = "bf16",
                 buf_bytes.append(0)
             buf_bytes[bid] = max(buf_bytes[bid], need)
             buf_of[out_name] = bid
+            tbytes[out_name] = need
         if isinstance(L, Conv):
             gm = _conv_geometry(net, L, wdtype)
             d = dict(gm)
@@ -490,7 +502,7 @@ def build_plan(net: Network, base_ptr: int, wdtype: str = "bf16",
                 src = len(buf_bytes)
                 buf_bytes.append(h * gm["W"] * 4 * 2)
                 ops.append(dict(kind=OP_STEM_PACK, p=[h, w, c, gm["W"], 3], **{"in": 0},
-                                out=src))
+                                out=src, bpi=[tbytes["input"], buf_bytes[src], 0]))
                 d["in_f32"] = 0
             d["out_f32"] = int(L.out_f32)
             d["fp8"] = int(fp8)
@@ -509,9 +521,11 @@ def build_plan(net: Network, base_ptr: int, wdtype: str = "bf16",
                 if fp8:
                     d["res_scale"] = act_scales[L.residual]
                 res = buf_of[L.residual]
+            in_bpi = buf_bytes[src] if gm.get("stem") else tbytes[L.inp]
             op = dict(kind=OP_CONV, conv=d, **{"in": src}, out=buf_of[out_name], res=res,
                       w=base_ptr + layout[f"{L.name}.w"].offset,
-                      bias=base_ptr + layout[f"{L.name}.b"].offset)
+                      bias=base_ptr + layout[f"{L.name}.b"].offset,
+                      bpi=[in_bpi, tbytes[out_name], tbytes[L.residual] if res >= 0 else 0])
             if wdtype == "fp8":
                 op["wscale"] = base_ptr + layout[f"{L.name}.s"].offset
             ops.append(op)
@@ -520,34 +534,41 @@ def build_plan(net: Network, base_ptr: int, wdtype: str = "bf16",
                 bn = dict(kind=OP_BN_ACT, **{"in": buf_of[out_name]}, out=buf_of[out_name], res=-1,
                           w=base_ptr + layout[f"{L.name}.bn_s"].offset,
                           bias=base_ptr + layout[f"{L.name}.bn_t"].offset,
-                          et=2 if f32 else 0)
+                          et=2 if f32 else 0, bpi=[tbytes[out_name], tbytes[out_name], 0])
                 p = [ho * wo, wo, stored_channels(c), int(L.relu), 0, 0, 0, 1]
                 if L.residual is not None:
                     rh, rw, rc = net.shapes[L.residual]
                     p[4:] = [rh, rw, stored_channels(rc), 2 if L.res_mode == "pad" else 1]
                     bn["res"] = buf_of[L.residual]
+                    bn["bpi"][2] = tbytes[L.residual]
                 bn["p"] = p
                 ops.append(bn)
         elif isinstance(L, MaxPool):
             h, w, c = net.shapes[L.inp]
             ho, wo, _ = net.shapes[L.out]
             ops.append(dict(kind=OP_MAXPOOL, p=[h, w, stored_channels(c), L.k, L.s, L.p, ho, wo],
-                            **{"in": buf_of[L.inp]}, out=buf_of[L.out], et=et))
+                            **{"in": buf_of[L.inp]}, out=buf_of[L.out], et=et,
+                            bpi=[tbytes[L.inp], tbytes[L.out], 0]))
         elif isinstance(L, AvgPool):
             h, w, c = net.shapes[L.inp]
             ops.append(dict(kind=OP_AVGPOOL, p=[h * w, stored_channels(c)],
-                            **{"in": buf_of[L.inp]}, out=buf_of[L.out], et=et))
+                            **{"in": buf_of[L.inp]}, out=buf_of[L.out], et=et,
+                            bpi=[tbytes[L.inp], tbytes[L.out], 0]))
         elif isinstance(L, Head):
             h, w, c = net.shapes[L.inp]
             ops.append(dict(kind=OP_HEAD, p=[h * w, stored_channels(c), L.classes],
                             **{"in": buf_of[L.inp]}, out=1,
                             w=base_ptr + layout[f"{L.name}.w"].offset,
                             bias=base_ptr + layout[f"{L.name}.b"].offset,
-                            et=et, scale=act_scales[L.inp] if fp8 else 1.0))
+                            et=et, scale=act_scales[L.inp] if fp8 else 1.0,
+                            bpi=[tbytes[L.inp], tbytes["output"], 0]))
         elif isinstance(L, Softmax):
             h, w, c = net.shapes[L.inp]
             ops.append(dict(kind=OP_SOFTMAX, p=[L.classes, stored_channels(c)],
-                            **{"in": buf_of[L.inp]}, out=1))
+                            **{"in": buf_of[L.inp]}, out=1,
+                            bpi=[tbytes[L.inp], tbytes["output"], 0]))
+        for op in ops:
+            op.setdefault("layer", i)
         # release buffers whose tensors die here
         for t, lu in list(last_use.items()):
             if lu == i and t in buf_of and buf_of[t] >= 2:

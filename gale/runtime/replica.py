@@ -7,7 +7,7 @@ forward on the replica's compute stream (graphs captured per batch bucket and I/
 
 from __future__ import annotations
 
-from typing import Optional, Sequence
+from typing import Optional, Sequence, Tuple
 
 import torch
 
@@ -18,7 +18,8 @@ from gale.models.graph import Network, act_scales_from_packed, build_plan
 class ModelReplica:
     def __init__(self, net: Network, packed: torch.Tensor, max_batch: int = 256, slots: int = 2,
                  buckets: Optional[Sequence[int]] = None, wdtype: str = "bf16",
-                 fused: bool = True, fold_bn: bool = True):
+                 fused: bool = True, fold_bn: bool = True,
+                 chunk: Optional[Tuple[int, int]] = None):
         if not packed.is_cuda:
             raise RuntimeError("ModelReplica needs the packed weights on a GPU")
         self.net = net
@@ -26,12 +27,16 @@ class ModelReplica:
         self.device = packed.device
         self.wdtype = wdtype
         self.act_scales = act_scales_from_packed(net, packed) if wdtype == "fp8" else None
+        # chunk = (leading layers, images per chunk): those layers' ops run per chunk of images
+        # (PlanSpec::chunk_ops, executor.h), the rest over the whole batch
+        cl, ci = chunk if chunk is not None else (0, 0)
         ops, buf_bytes = build_plan(net, packed.data_ptr(), wdtype, self.act_scales, fused=fused,
-                                    fold_bn=fold_bn)
+                                    fold_bn=fold_bn, chunk_layers=cl if ci > 0 else 0)
+        co = sum(1 for op in ops if op.get("layer", len(net.layers)) < cl) if ci > 0 else 0
         self.ops = ops
         self.buf_bytes = buf_bytes
         self.executor = native().Executor(packed.device.index or 0, ops, buf_bytes, max_batch,
-                                          slots, list(buckets or []))
+                                          slots, list(buckets or []), co, ci)
 
     @property
     def max_batch(self) -> int:

@@ -42,3 +42,4 @@ def test_replicate_weights_over_rccl():
     assert [b.device.index for b in bufs] == devs
     for b in bufs:
         assert torch.equal(b.cpu(), src.cpu())
+

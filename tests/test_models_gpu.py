@@ -94,6 +94,27 @@ def test_resnet50_gemm_convs_match_conv_mfma_and_fp32():
     assert torch.allclose(a.sum(1), torch.ones(6), atol=1e-4)
 
 
+@pytest.mark.parametrize("end", ["l2.0.down", "l2.0.conv3"])
+def test_resnet50_batch_chunked_prefix_is_bit_identical(end):
+    """PlanSpec chunking (the leading layers run per chunk of images, the rest over the whole
+    batch) changes only the launch grids: every output element keeps its kernel and k-order, so
+    logits are bit identical to the unchunked plan, eager and graph, with a ragged last chunk.
+    "l2.0.conv3": the prefix ends mid-block, its live-out shortcut (l2.0.down) is produced
+    before the last prefix op and must survive the later chunks."""
+    net = get_model("resnet50")
+    params = init_params(net, seed=23, calib_batch=4)
+    packed = materialize_weights(net, torch.device("cuda", 0), params=params)
+    x = torch.rand((7,) + net.input_shape, generator=torch.Generator().manual_seed(9))
+    n_pre = [L.name for L in net.layers].index(end)
+    base = ModelReplica(net, packed, max_batch=8, slots=1)
+    chunked = ModelReplica(net, packed, max_batch=8, slots=1, chunk=(n_pre, 3))
+    a = base.infer_eager(x).cpu()
+    b = chunked.infer_eager(x).cpu()
+    c = chunked.infer(x).cpu()
+    torch.cuda.synchronize()
+    assert torch.equal(a, b) and torch.equal(a, c)
+
+
 @pytest.mark.parametrize("name,batch", [("lenet5", 13), ("resnet20", 37), ("resnet50", 2)])
 def test_fp8_model_matches_emulation_and_fp32(name, batch):
     """fp8 plan (e4m3 MFMA, calibrated per-tensor activation scales) against the fp8 emulation

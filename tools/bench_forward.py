@@ -27,6 +27,9 @@ def main():
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp8"])
     ap.add_argument("--conv-path", type=int, default=0,
                     help="0 auto, 1 conv_mfma only, 2 GEMM conv wherever the shape allows")
+    ap.add_argument("--chunk", default="",
+                    help="LAYER:N - layers before LAYER run per chunk of N images "
+                         "(PlanSpec::chunk_ops)")
     a = ap.parse_args()
     from gale._native import native
     native().set_conv_path(a.conv_path)
@@ -34,7 +37,12 @@ def main():
     dev = torch.device("cuda", 0)
     packed = materialize_weights(net, dev, wdtype=a.dtype)
     bs = [int(b) for b in a.batches.split(",")]
-    rep = ModelReplica(net, packed, max_batch=max(bs), slots=1, buckets=bs, wdtype=a.dtype)
+    chunk = None
+    if a.chunk:
+        name, n = a.chunk.split(":")
+        chunk = ([L.name for L in net.layers].index(name), int(n))
+    rep = ModelReplica(net, packed, max_batch=max(bs), slots=1, buckets=bs, wdtype=a.dtype,
+                       chunk=chunk)
     s = torch.cuda.current_stream().cuda_stream
     res = []
     for b in bs:
@@ -47,8 +55,8 @@ def main():
         torch.cuda.synchronize()
         dt = (time.perf_counter() - t) / a.iters
         flops = 2 * net.macs_per_image() * b
-        r = dict(model=a.model, dtype=a.dtype, conv_path=a.conv_path, batch=b, ms=dt * 1e3, img_s=b / dt, tflops=flops / dt / 1e12,
-                 graph=not a.eager)
+        r = dict(model=a.model, dtype=a.dtype, conv_path=a.conv_path, batch=b, ms=dt * 1e3,
+                 img_s=b / dt, tflops=flops / dt / 1e12, graph=not a.eager, chunk=a.chunk)
         res.append(r)
         print(json.dumps(r), flush=True)
 
