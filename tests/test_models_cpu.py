@@ -128,3 +128,57 @@ def test_unfolded_bn_plan_structure(name):
     assert f"{L.name}.bn_s" in lay32 and lay32[f"{L.name}.w"].dtype == torch.float32
     ops32, _ = build_plan(net, 0, wdtype="fp32", fold_bn=False)
     assert all(op.get("et") == 2 for op in ops32 if op["kind"] == OP_BN_ACT)
+
+
+def _simulate_chunked(ops, chunk_ops, batch, chunk):
+    """Replay the executor's launch order (executor.cpp launch_all) on byte intervals of the
+    buffers: every operand read must find, for each of its images, the bytes the op that
+    produced it in the unchunked order wrote for that image - nothing overwritten in between."""
+    writes = {}  # buffer -> [(lo_byte, hi_byte, writer op, first image, bpi)]
+
+    def write(buf, op_i, i0, n, bpi):
+        writes.setdefault(buf, []).append((i0 * bpi, (i0 + n) * bpi, op_i, i0, bpi))
+
+    def check(buf, want, i0, n, bpi):
+        for img in range(i0, i0 + n):
+            lo, hi = img * bpi, (img + 1) * bpi
+            last = next((w for w in reversed(writes.get(buf, [])) if w[0] < hi and lo < w[1]),
+                        None)
+            assert last is not None and last[2] == want and last[4] == bpi, (buf, want, img)
+            assert lo >= last[0] and hi <= last[1]
+
+    # producer of each operand in plain (unchunked) order
+    producer, last_writer = [], {0: -1}
+    for i, op in enumerate(ops):
+        producer.append({k: last_writer.get(op[k]) for k in ("in", "res") if op.get(k, -1) >= 0})
+        last_writer[op["out"]] = i
+
+    def run(lo, hi, i0, n):
+        for i in range(lo, hi):
+            op = ops[i]
+            for k, slot in (("in", 0), ("res", 2)):
+                if op.get(k, -1) >= 0 and producer[i][k] >= 0:
+                    check(op[k], producer[i][k], i0, n, op["bpi"][slot])
+            write(op["out"], i, i0, n, op["bpi"][1])
+
+    for c0 in range(0, batch, chunk):
+        run(0, chunk_ops, c0, min(chunk, batch - c0))
+    run(chunk_ops, len(ops), 0, batch)
+
+
+@pytest.mark.parametrize("end", ["l1.0.down", "l2.0.down", "l2.0.conv2", "l2.0.conv3",
+                                 "l3.0.conv1"])
+def test_chunked_plan_keeps_live_out_tensors(end):
+    """build_plan(chunk_layers=k): replaying the chunked launch order on buffer byte ranges, no
+    chunk overwrites rows another op still reads (live-out tensors of the prefix sit in buffers
+    no other prefix tensor uses); the unchunked allocation would fail this."""
+    net = get_model("resnet50")
+    k = [L.name for L in net.layers].index(end)
+    ops, _ = build_plan(net, 0, chunk_layers=k)
+    n = sum(1 for op in ops if op["layer"] < k)
+    _simulate_chunked(ops, n, batch=7, chunk=3)
+    _simulate_chunked(ops, n, batch=6, chunk=3)
+    if end in ("l2.0.conv2", "l2.0.conv3"):
+        plain, _ = build_plan(net, 0)
+        with pytest.raises(AssertionError):
+            _simulate_chunked(plain, n, batch=7, chunk=3)
