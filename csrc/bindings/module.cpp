@@ -223,6 +223,10 @@ PYBIND11_MODULE(_C, m) {
                     "format_floats_java");
   });
   m.def("set_conv_path", &gale::set_conv_path);
+  m.def("set_conv_patch", &gale::set_conv_patch);
+  m.def("conv_patch_supported", [](py::dict desc, int batch, bool has_res) {
+    return gale::conv_patch_supported(desc_from_dict(desc), batch, has_res);
+  });
   m.def("device_pci_bus_id", [](int device) {
     char buf[64] = {0};
     chk(hipDeviceGetPCIBusId(buf, (int)sizeof(buf), device), "hipDeviceGetPCIBusId");

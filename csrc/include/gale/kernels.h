@@ -66,6 +66,15 @@ int conv_path();
 hipError_t conv2d_gemm(const ConvDesc& d, int batch, const void* x, const void* w,
                        const float* bias, const void* res, void* y, hipStream_t stream);
 
+// 3x3 stride-1 convs with an LDS-resident input patch per 64-channel block (conv_patch.hip):
+// bf16, Cin % 64 == 0, tiles of whole output rows (<= 128 pixels, >= 96). conv2d() routes there
+// first when conv_patch_supported() holds. set_conv_patch / GALE_CONV_PATCH: 0 off, 1 (default)
+// 128-channel tiles only, 2 also 64-channel tiles.
+bool conv_patch_supported(const ConvDesc& d, int batch, bool has_res);
+void set_conv_patch(int mode);
+hipError_t conv2d_patch(const ConvDesc& d, int batch, const void* x, const void* w,
+                        const float* bias, const void* res, void* y, hipStream_t stream);
+
 // fp32 NHWC [B][H][W][C<=4] -> bf16 [B][H][Wp][4] with `lp` zero columns on the left (and zeros
 // up to Wp on the right, channels >= C zero): the input of a packed-stem conv (ConvDesc::stem).
 hipError_t stem_pack(int batch, int H, int W, int C, int Wp, int lp, const float* x, void* y,

@@ -418,6 +418,8 @@ hipError_t conv2d(const ConvDesc& d, int batch, const void* x, const void* w, co
       return hipErrorInvalidValue;
     return conv2d_gemm(d, batch, x, w, bias, nullptr, y, stream);
   }
+  if (!f8 && conv_patch_supported(d, batch, d.has_res && res != nullptr))
+    return conv2d_patch(d, batch, x, w, bias, d.has_res ? res : nullptr, y, stream);
   if (!f8 && conv_gemm_supported(d, batch, d.has_res && res != nullptr))
     return conv2d_gemm(d, batch, x, w, bias, d.has_res ? res : nullptr, y, stream);
   if (f8 && (wscale == nullptr || !(d.in_scale > 0.f) || !(d.out_scale > 0.f)))

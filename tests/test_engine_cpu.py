@@ -287,7 +287,9 @@ def _trickle(broker, n, interval_s, seed=0):
 
 def test_slo_controller_shrinks_wait_when_batching_delay_misses():
     """--slo-p99-ms: with a trickle of records and a long batching window the latency is the
-    window itself; the controller must shorten it (and the batch cap) to meet the target."""
+    window itself; the controller must keep it far below the configured 40 ms. (The batch cap
+    oscillates: it grows back on every step under 0.8 x the target, so its final value depends
+    on where the run stops - not asserted.)"""
     b = K.Broker()
     b.start()
     b.create_topic("in", 2)
@@ -304,7 +306,7 @@ def test_slo_controller_shrinks_wait_when_batching_delay_misses():
     finally:
         b.stop()
     assert st["slo_adjustments"] > 0
-    assert st["eff_max_wait_us"] < 40000 and st["eff_max_batch"] < 64
+    assert st["eff_max_wait_us"] < 20000
 
 
 def test_slo_controller_grows_batches_under_backlog():

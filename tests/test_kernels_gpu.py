@@ -416,3 +416,75 @@ def test_conv_f32_matches_fp32(B, H, W, Cin, Cout, k, stride, pad, res):
     got = y.cpu()
     scale = ref.abs().max().item()
     assert (got - ref).abs().max().item() < 2e-5 * max(scale, 1.0)
+
+
+PATCH_CASES = [  # B, H, W, Cin, Cout, with_res: the ResNet-50 3x3 stride-1 shapes (+ residual)
+    (2, 56, 56, 64, 64, False),     # 2 rows x 56 per tile, BN = 64, 240-row patch
+    (3, 28, 28, 128, 128, True),    # 4 rows x 28, BN = 128
+    (2, 14, 14, 256, 256, False),   # 7 rows x 14 (98 of 128 MFMA rows), two channel tiles
+    (1, 14, 14, 128, 64, True),     # BN = 64 at 14 x 14
+]
+
+
+def _patch_desc(geom, B, H, W, has_res):
+    d = dict(geom, H=H, W=W, Ho=H, Wo=W, stride=1, pad=1, relu=1, in_f32=0, out_f32=0)
+    if has_res:
+        d.update(has_res=1, res_H=H, res_W=W, res_C=geom["Cout"], res_stride=1)
+    return d
+
+
+@pytest.mark.parametrize("case", PATCH_CASES)
+def test_conv2d_patch_path_matches_torch(case):
+    """conv_patch.hip (3x3 stride 1 from an LDS-resident halo patch) vs fp32 torch and vs the
+    im2col GEMM path on the same inputs."""
+    from gale._native import native
+
+    B, H, W, Cin, Cout, with_res = case
+    g = torch.Generator().manual_seed(7 + Cin + Cout + H)
+    x = torch.randn(B, H, W, Cin, generator=g).to(torch.bfloat16)
+    w = torch.randn(Cout, Cin, 3, 3, generator=g) / (Cin * 9) ** 0.5
+    b = torch.randn(Cout, generator=g) * 0.1
+    wp, bp, geom = ops.pack_conv(w, b)
+    res = torch.randn(B, H, W, Cout, generator=g).to(torch.bfloat16) if with_res else None
+    C = native()
+    try:
+        C.set_conv_patch(2)  # (2: the 64-channel tiles too)
+        assert C.conv_patch_supported(_patch_desc(geom, B, H, W, with_res), B, with_res)
+        y = ops.conv2d(x.to(DEV), wp, bp, geom, stride=1, pad=1, relu=True,
+                       residual=None if res is None else res.to(DEV))
+        C.set_conv_patch(0)
+        y_gemm = ops.conv2d(x.to(DEV), wp, bp, geom, stride=1, pad=1, relu=True,
+                            residual=None if res is None else res.to(DEV))
+    finally:
+        C.set_conv_patch(1)
+    ref = _ref_conv(x.float(), w.to(torch.bfloat16).float(), b, 1, 1, True, res=res)
+    got = y.float().cpu()
+    scale = ref.abs().max().item() + 1e-6
+    err = (got - ref).abs().max().item()
+    assert err <= 2e-2 * scale + 1e-2, f"max err {err} (scale {scale})"
+    assert (y.float() - y_gemm.float()).abs().max().item() <= 1e-2 * scale + 1e-2
+
+
+@pytest.mark.parametrize("H,C,tap", [(56, 64, 4), (28, 128, 0), (14, 256, 8), (28, 128, 5)])
+def test_conv2d_patch_single_tap_shift_is_exact(H, C, tap):
+    """One identity tap (kh, kw) and zeros elsewhere: y[n, i, j] = x[n, i + kh - 1, j + kw - 1]
+    (zero outside the image), bit exact - pins the patch-row mapping, the halo and the zero
+    padding of every tap position on an asymmetric input."""
+    from gale._native import native
+
+    B = 2
+    x = (torch.arange(B * H * H * C, dtype=torch.float32).reshape(B, H, H, C) % 251) / 16.0
+    x = x.to(torch.bfloat16)
+    kh, kw = divmod(tap, 3)
+    w = torch.zeros(C, C, 3, 3)
+    w[:, :, kh, kw] = torch.eye(C)
+    wp, bp, geom = ops.pack_conv(w, torch.zeros(C))
+    try:
+        native().set_conv_patch(2)
+        assert native().conv_patch_supported(_patch_desc(geom, B, H, H, False), B, False)
+        y = ops.conv2d(x.to(DEV), wp, bp, geom, stride=1, pad=1).cpu()
+    finally:
+        native().set_conv_patch(1)
+    xp = torch.nn.functional.pad(x.float(), (0, 0, 1, 1, 1, 1))
+    want = xp[:, kh:kh + H, kw:kw + H, :].to(torch.bfloat16)
+    assert torch.equal(y, want)
