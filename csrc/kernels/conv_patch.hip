@@ -52,13 +52,14 @@ struct PatchArgs {
   int n_tiles, nwg;
 };
 
-constexpr int kBM = 128;  // MFMA rows per tile (pixels P <= kBM, the rest read the zero row)
-
 // PRR: patch rows held in LDS (>= PR + 1 for the zero row, a multiple of 8 = one
-// wave-instruction); compile-time so the two stages are static LDS (2 workgroups per CU)
-template <int BN, int PRR>
-__global__ __launch_bounds__(256, 2) void conv_patch_kernel(PatchArgs a) {
-  constexpr int WM = 2, WN = 2, NW = 4;
+// wave-instruction); compile-time so the two stages are static LDS (2 workgroups per CU).
+// WM: waves along the pixels (2: 128 MFMA rows, 4 waves; 4: 256 rows, 8 waves, 1 workgroup per
+// CU - half the weight bytes per pixel, an A/B variant)
+template <int BN, int PRR, int WM = 2>
+__global__ __launch_bounds__(WM * 128, WM == 2 ? 2 : 1) void conv_patch_kernel(PatchArgs a) {
+  constexpr int kBM = WM * 64;       // MFMA rows per tile (pixels P <= kBM; the rest read zeros)
+  constexpr int WN = 2, NW = WM * WN;
   constexpr int TM = kBM / WM / 16;  // 16-pixel tiles per wave
   constexpr int TN = BN / WN / 16;   // 16-channel tiles per wave
   constexpr int WI = BN / (8 * NW);  // weight wave-instructions per wave per step
@@ -252,12 +253,13 @@ __global__ __launch_bounds__(256, 2) void conv_patch_kernel(PatchArgs a) {
   }
 }
 
-// the patch-row capacities compiled (2 workgroups per CU at BN = 128 up to 184 rows)
-constexpr int kPrr[3] = {152, 184, 240};
+// the patch-row capacities compiled (2 workgroups per CU at BN = 128 up to 184 rows; 272 for
+// the 256-row tiles)
+constexpr int kPrr[4] = {152, 184, 240, 272};
 
-int patch_tile_rows(const ConvDesc& d) {
-  // largest divisor of H whose rows hold <= 128 pixels
-  for (int tr = kBM / d.W; tr >= 1; --tr)
+int patch_tile_rows(const ConvDesc& d, int bm) {
+  // largest divisor of H whose rows hold <= bm pixels
+  for (int tr = bm / d.W; tr >= 1; --tr)
     if (d.H % tr == 0) return tr;
   return 0;
 }
@@ -267,6 +269,16 @@ int patch_prr(int PR) {
     if (PR + 1 <= c) return c;
   return 0;
 }
+
+// GALE_CONV_PATCH_BM: 256 = 8-wave 256-row tiles for the 128-channel layers (A/B, off: 28x28
+// 77 -> 90 us, 14x14 77 -> 79 us - halving the weight bytes per pixel does not pay for one
+// workgroup per CU; profiles/r2_conv_patch.txt)
+std::atomic<int> g_patch_bm{[] {
+  const char* e = getenv("GALE_CONV_PATCH_BM");
+  return e && *e ? atoi(e) : 128;
+}()};
+
+int patch_bm(int bn) { return bn == 128 && g_patch_bm.load(std::memory_order_relaxed) == 256 ? 256 : 128; }
 
 }  // namespace
 
@@ -286,17 +298,19 @@ bool conv_patch_supported(const ConvDesc& d, int batch, bool has_res) {
   if (d.stem || d.fp8 || d.f32 || d.in_f32 || d.out_f32) return false;
   if (d.KH != 3 || d.KW != 3 || d.stride != 1 || d.pad != 1) return false;
   if (d.Cin % 64 != 0 || d.K != 9 * d.Cin || d.Kpad != d.K) return false;
-  if (d.Ho != d.H || d.Wo != d.W || d.W > kBM || d.Cout % 8 != 0) return false;
+  if (d.Ho != d.H || d.Wo != d.W || d.W > 128 || d.Cout % 8 != 0) return false;
   const int bn = (d.Npad % 128 == 0) ? 128 : 64;
   if (d.Npad % bn != 0 || d.Npad < d.Cout) return false;
   if (bn == 64 && g_conv_patch.load(std::memory_order_relaxed) < 2) return false;
   if (has_res && (d.res_C != d.Cout || d.res_stride != 1 || d.res_H != d.H || d.res_W != d.W))
     return false;
-  const int tr = patch_tile_rows(d);
-  // (a tile below 96 pixels wastes over a quarter of the MFMA rows: 7x7 stays on conv_gemm)
-  if (tr < 1 || tr * d.W < 96) return false;
+  const int bm = patch_bm(bn);
+  const int tr = patch_tile_rows(d, bm);
+  // (a tile below 3/4 of its MFMA rows wastes too much: 7x7 stays on conv_gemm)
+  if (tr < 1 || tr * d.W * 4 < bm * 3 - 16) return false;
   const int prr = patch_prr((tr + 2) * (d.W + 2));
-  if (prr == 0 || (bn == 128 && prr > 184)) return false;
+  if (prr == 0 || (bm == 128 && bn == 128 && prr > 184) || (bm == 256 && prr != 272))
+    return false;
   return (long long)batch * d.H * d.W * d.Cin < (1ll << 31) &&
          (long long)batch * d.H * d.W * d.Cout < (1ll << 31);
 }
@@ -310,7 +324,9 @@ hipError_t conv2d_patch(const ConvDesc& d, int batch, const void* x, const void*
   a.res = static_cast<const bf16*>(res);
   a.y = static_cast<bf16*>(y);
   a.H = d.H; a.W = d.W; a.Cin = d.Cin; a.Cout = d.Cout; a.Kpad = d.Kpad;
-  a.TR = patch_tile_rows(d);
+  const int bn = (d.Npad % 128 == 0) ? 128 : 64;
+  const int bm = patch_bm(bn);
+  a.TR = patch_tile_rows(d, bm);
   if (a.TR < 1) return hipErrorInvalidValue;
   a.P = a.TR * d.W;
   a.PW = d.W + 2;
@@ -319,12 +335,15 @@ hipError_t conv2d_patch(const ConvDesc& d, int batch, const void* x, const void*
   a.nsteps = 9 * (d.Cin / 64);
   a.relu = d.relu;
   a.has_res = d.has_res && res != nullptr;
-  const int bn = (d.Npad % 128 == 0) ? 128 : 64;
   a.n_tiles = d.Npad / bn;
   a.nwg = batch * a.rblocks * a.n_tiles;
   const int prr = patch_prr(a.PR);
-  if (a.P > kBM || prr == 0 || (bn == 128 && prr > 184)) return hipErrorInvalidValue;
-  if (bn == 128) {
+  if (a.P > bm || prr == 0) return hipErrorInvalidValue;
+  if (bm == 256) {
+    if (prr != 272) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((conv_patch_kernel<128, 272, 4>), dim3(a.nwg), dim3(512), 0, stream, a);
+  } else if (bn == 128) {
+    if (prr > 184) return hipErrorInvalidValue;
     if (prr == 152)
       hipLaunchKernelGGL((conv_patch_kernel<128, 152>), dim3(a.nwg), dim3(256), 0, stream, a);
     else
