@@ -56,8 +56,11 @@ struct PatchArgs {
 // wave-instruction); compile-time so the two stages are static LDS (2 workgroups per CU).
 // WM: waves along the pixels (2: 128 MFMA rows, 4 waves; 4: 256 rows, 8 waves, 1 workgroup per
 // CU - half the weight bytes per pixel, an A/B variant)
-template <int BN, int PRR, int WM = 2>
-__global__ __launch_bounds__(WM * 128, WM == 2 ? 2 : 1) void conv_patch_kernel(PatchArgs a) {
+// PB: patch buffers (2: the next block's patch loads during the last tap; 1: loaded at the block
+// boundary, exposed, but with 64-channel tiles the workgroup fits 4 per CU - an A/B variant)
+template <int BN, int PRR, int WM = 2, int PB = 2>
+__global__ __launch_bounds__(WM * 128, WM == 2 ? (PB == 1 && BN == 64 ? 4 : 2) : 1)
+void conv_patch_kernel(PatchArgs a) {
   constexpr int kBM = WM * 64;       // MFMA rows per tile (pixels P <= kBM; the rest read zeros)
   constexpr int WN = 2, NW = WM * WN;
   constexpr int TM = kBM / WM / 16;  // 16-pixel tiles per wave
@@ -73,7 +76,7 @@ __global__ __launch_bounds__(WM * 128, WM == 2 ? 2 : 1) void conv_patch_kernel(P
   constexpr int RPI = 64 / LPR;
   constexpr int HALF = TM / 2 * 16;
   constexpr int NRI = HALF / RPI;
-  constexpr int LDS_BYTES = 2 * WST + 2 * PST;
+  constexpr int LDS_BYTES = 2 * WST + PB * PST;
   static_assert(NW * HALF * EPS * 4 <= LDS_BYTES, "epilogue staging exceeds the LDS allocation");
   static_assert(WI >= 1, "tile too small for the workgroup");
   __shared__ __attribute__((aligned(1024))) uint8_t lds[LDS_BYTES];
@@ -168,11 +171,15 @@ __global__ __launch_bounds__(WM * 128, WM == 2 ? 2 : 1) void conv_patch_kernel(P
     // on a block's last tap, the previous block's patch buffer) is refilled below
     __syncthreads();
     const int cb = s / 9, tap = s - cb * 9;
+    if (PB == 1 && tap == 0 && cb > 0) {  // every wave is done with block cb-1's patch
+      stage_patch(cb, pbuf);
+      __syncthreads();
+    }
     const uint8_t* wcur = wbuf + (s & 1) * WST;
-    const uint8_t* pcur = pbuf + (cb & 1) * PST;
+    const uint8_t* pcur = pbuf + (PB == 2 ? (cb & 1) * PST : 0);
     if (s + 1 < a.nsteps) {
       stage_w(s + 1, wbuf + ((s + 1) & 1) * WST);
-      if (tap == 8) stage_patch(cb + 1, pbuf + ((cb + 1) & 1) * PST);
+      if (PB == 2 && tap == 8) stage_patch(cb + 1, pbuf + ((cb + 1) & 1) * PST);
     }
     const int kh = tap / 3;
     const int toff = kh * a.PW + (tap - kh * 3);
@@ -280,6 +287,18 @@ std::atomic<int> g_patch_bm{[] {
 
 int patch_bm(int bn) { return bn == 128 && g_patch_bm.load(std::memory_order_relaxed) == 256 ? 256 : 128; }
 
+// GALE_CONV_PATCH_OCC=4: 64-channel tiles with one patch buffer (4 workgroups per CU) for every
+// eligible layer (A/B, off: 14x14 77 -> 80 us, 28x28 and 56x56 unchanged vs the default paths)
+std::atomic<int> g_patch_occ{[] {
+  const char* e = getenv("GALE_CONV_PATCH_OCC");
+  return e && *e ? atoi(e) : 2;
+}()};
+
+int patch_bn(const ConvDesc& d) {
+  if (g_patch_occ.load(std::memory_order_relaxed) == 4 && d.Npad % 64 == 0) return 64;
+  return (d.Npad % 128 == 0) ? 128 : 64;
+}
+
 }  // namespace
 
 // GALE_CONV_PATCH: 0 off, 1 (default) the 128-channel tiles (ResNet-50 28x28 and 14x14 conv2:
@@ -299,9 +318,10 @@ bool conv_patch_supported(const ConvDesc& d, int batch, bool has_res) {
   if (d.KH != 3 || d.KW != 3 || d.stride != 1 || d.pad != 1) return false;
   if (d.Cin % 64 != 0 || d.K != 9 * d.Cin || d.Kpad != d.K) return false;
   if (d.Ho != d.H || d.Wo != d.W || d.W > 128 || d.Cout % 8 != 0) return false;
-  const int bn = (d.Npad % 128 == 0) ? 128 : 64;
+  const int bn = patch_bn(d);
+  const bool occ4 = g_patch_occ.load(std::memory_order_relaxed) == 4;
   if (d.Npad % bn != 0 || d.Npad < d.Cout) return false;
-  if (bn == 64 && g_conv_patch.load(std::memory_order_relaxed) < 2) return false;
+  if (bn == 64 && !occ4 && g_conv_patch.load(std::memory_order_relaxed) < 2) return false;
   if (has_res && (d.res_C != d.Cout || d.res_stride != 1 || d.res_H != d.H || d.res_W != d.W))
     return false;
   const int bm = patch_bm(bn);
@@ -324,7 +344,7 @@ hipError_t conv2d_patch(const ConvDesc& d, int batch, const void* x, const void*
   a.res = static_cast<const bf16*>(res);
   a.y = static_cast<bf16*>(y);
   a.H = d.H; a.W = d.W; a.Cin = d.Cin; a.Cout = d.Cout; a.Kpad = d.Kpad;
-  const int bn = (d.Npad % 128 == 0) ? 128 : 64;
+  const int bn = patch_bn(d);
   const int bm = patch_bm(bn);
   a.TR = patch_tile_rows(d, bm);
   if (a.TR < 1) return hipErrorInvalidValue;
@@ -348,6 +368,13 @@ hipError_t conv2d_patch(const ConvDesc& d, int batch, const void* x, const void*
       hipLaunchKernelGGL((conv_patch_kernel<128, 152>), dim3(a.nwg), dim3(256), 0, stream, a);
     else
       hipLaunchKernelGGL((conv_patch_kernel<128, 184>), dim3(a.nwg), dim3(256), 0, stream, a);
+  } else if (g_patch_occ.load(std::memory_order_relaxed) == 4) {
+    if (prr == 152)
+      hipLaunchKernelGGL((conv_patch_kernel<64, 152, 2, 1>), dim3(a.nwg), dim3(256), 0, stream, a);
+    else if (prr == 184)
+      hipLaunchKernelGGL((conv_patch_kernel<64, 184, 2, 1>), dim3(a.nwg), dim3(256), 0, stream, a);
+    else
+      hipLaunchKernelGGL((conv_patch_kernel<64, 240, 2, 1>), dim3(a.nwg), dim3(256), 0, stream, a);
   } else {
     if (prr == 152)
       hipLaunchKernelGGL((conv_patch_kernel<64, 152>), dim3(a.nwg), dim3(256), 0, stream, a);
