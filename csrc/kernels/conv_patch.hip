@@ -59,7 +59,7 @@ struct PatchArgs {
 // PB: patch buffers (2: the next block's patch loads during the last tap; 1: loaded at the block
 // boundary, exposed, but with 64-channel tiles the workgroup fits 4 per CU - an A/B variant)
 template <int BN, int PRR, int WM = 2, int PB = 2>
-__global__ __launch_bounds__(WM * 128, WM == 2 ? (PB == 1 && BN == 64 ? 4 : 2) : 1)
+__global__ __launch_bounds__(WM * 128, WM == 2 ? (PB == 1 && BN == 64 ? (PRR > 200 ? 3 : 4) : 2) : 1)
 void conv_patch_kernel(PatchArgs a) {
   constexpr int kBM = WM * 64;       // MFMA rows per tile (pixels P <= kBM; the rest read zeros)
   constexpr int WN = 2, NW = WM * WN;
