@@ -114,6 +114,10 @@ def parse_args(argv=None):
                          "GPU r %% device_count and the process group runs over gloo (RCCL refuses "
                          "two ranks on one GPU); every other part of the per-rank path is the "
                          "real one. Not a measurement")
+    ap.add_argument("--local-output", action=argparse.BooleanOptionalAction, default=True,
+                    help="each rank produces its outputs to the output partition its own broker "
+                         "leads (--output-partition RANK) instead of round-robin over every "
+                         "rank's broker (the unkeyed default)")
     ap.add_argument("--timeout", type=float, default=600.0)
     return ap.parse_args(argv)
 
@@ -312,7 +316,8 @@ def main(argv=None) -> int:
                      decode_threads=a.decode_threads, slo_p99_ms=a.slo_p99_ms,
                      gpu_wait_poll_us=a.gpu_wait_poll_us, gpu_ingest=a.gpu_ingest, gpu_encode=a.gpu_encode,
                      stub=a.stub, stub_null=a.stub_null, commit_interval_ms=500,
-                     check_crcs=a.check_crcs)
+                     check_crcs=a.check_crcs,
+                     output_partition=rank if a.local_output and world > 1 else -1)
     devices = (list(range(local_gpus)) if local_gpus > 1 else [local_rank]) if use_gpu else None
     # ONE engine: warm-up and timed window are the same steady-state pipeline (connections,
     # pinned fetch buffers, captured graphs all warm); the timed window starts at a barrier

@@ -1119,8 +1119,8 @@ void Engine::emit(InRecord& r, std::string value, bool null_value, kafka::Produc
     };
   }
   try {
-    prod->send(cfg_.output_topic, -1, keyed ? &key : nullptr, std::move(value), null_value,
-               std::move(hs), -1, std::move(cb));
+    prod->send(cfg_.output_topic, cfg_.output_partition, keyed ? &key : nullptr,
+               std::move(value), null_value, std::move(hs), -1, std::move(cb));
   } catch (const std::exception& e) {
     fprintf(stderr, "[gale sink] send failed: %s\n", e.what());
     complete_record(meta, false);

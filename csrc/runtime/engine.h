@@ -47,6 +47,7 @@ struct EngineConfig {
   // source (R4, E1)
   std::string bootstrap = "127.0.0.1:9092";
   std::string input_topic, output_topic;
+  int output_partition = -1;       // -1: the producer's partitioner; >= 0: this partition
   std::string group_id;            // offsets committed under this group (empty: no commits)
   std::string client_id = "gale";
   std::vector<int> partitions;     // empty = every partition of input_topic

@@ -73,6 +73,9 @@ class GaleConfig:
     linger_ms: int = 0
     on_error: str = "null"             # reference: malformed input -> null record
     output_key: str = "none"           # reference: unkeyed output (E9); "input" = input's key
+    output_partition: int = -1         # -1: the producer's partitioner (reference: unkeyed
+                                       # round-robin); >= 0: every output record to this
+                                       # partition (e.g. the one this process's broker leads)
     # lifetime (reference: sleep 1 h then kill, MainTopology.java:71-77)
     duration: float = 3600.0
     # model / compute
@@ -109,6 +112,8 @@ class GaleConfig:
         os.path.expanduser("~"), ".gale", "topologies"))
 
     def validate(self) -> "GaleConfig":
+        if self.output_partition < -1:
+            raise ValueError("--output-partition must be -1 (partitioner) or a partition index")
         for k, allowed in CHOICES.items():
             v = getattr(self, k)
             if v not in allowed:
@@ -150,7 +155,8 @@ class GaleConfig:
             decode_threads=self.decode_threads, check_crcs=self.check_crcs,
             acks=self.acks, sink_mode=self.sink_mode, linger_ms=self.linger_ms,
             value_format=self.value_format, type_id_header=self.type_id_header,
-            on_error=self.on_error, output_key=self.output_key, H=H, W=W, C=C, classes=classes,
+            on_error=self.on_error, output_key=self.output_key,
+            output_partition=self.output_partition, H=H, W=W, C=C, classes=classes,
             max_batch=self.max_batch,
             max_wait_us=self.max_wait_us, slo_p99_ms=self.slo_p99_ms,
             queue_depth=self.queue_depth,

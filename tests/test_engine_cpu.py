@@ -335,3 +335,34 @@ def test_slo_controller_grows_batches_under_backlog():
         b.stop()
     assert st["slo_adjustments"] > 0 and any(adj > 0 for _, adj in seen)
     assert min(cap for cap, _ in seen) == 64  # never shrunk while the backlog lasted
+
+
+def test_output_partition_pins_every_output_record():
+    """--output-partition P: every output record goes to partition P (bench.py: the partition
+    the rank's own broker leads) instead of the producer's unkeyed round-robin."""
+    b = K.Broker()
+    b.start()
+    b.create_topic("in", 2)
+    b.create_topic("out", 3)
+    try:
+        counts = [1, 2, 1, 3] * 4
+        produce_images(b, counts)
+        eng = Engine(make_cfg(b, output_partition=2), max_records=len(counts))
+        eng.start()
+        assert eng.wait(30), eng.stats()
+        eng.stop()
+        assert len(b.read("out", 2)) == len(counts)
+        assert b.read("out", 0) == [] and b.read("out", 1) == []
+        # default: the 0.11-style round-robin partitioner spreads them
+        b.create_topic("out2", 3)
+        eng = Engine(make_cfg(b, output_topic="out2", group_id="g2"), max_records=len(counts))
+        eng.start()
+        assert eng.wait(30), eng.stats()
+        eng.stop()
+        per = [len(b.read("out2", p)) for p in range(3)]
+        assert sum(per) == len(counts) and min(per) > 0
+    finally:
+        b.stop()
+    with pytest.raises(ValueError):
+        GaleConfig(topology_name="t", input_topic="in", output_topic="out",
+                   output_partition=-2).validate()
