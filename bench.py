@@ -114,6 +114,8 @@ def parse_args(argv=None):
                          "GPU r %% device_count and the process group runs over gloo (RCCL refuses "
                          "two ranks on one GPU); every other part of the per-rank path is the "
                          "real one. Not a measurement")
+    ap.add_argument("--producer-buffer-mb", type=int, default=32,
+                    help="unsent output bytes per sink producer (Kafka buffer.memory)")
     ap.add_argument("--local-output", action=argparse.BooleanOptionalAction, default=True,
                     help="each rank produces its outputs to the output partition its own broker "
                          "leads (--output-partition RANK) instead of round-robin over every "
@@ -317,7 +319,8 @@ def main(argv=None) -> int:
                      gpu_wait_poll_us=a.gpu_wait_poll_us, gpu_ingest=a.gpu_ingest, gpu_encode=a.gpu_encode,
                      stub=a.stub, stub_null=a.stub_null, commit_interval_ms=500,
                      check_crcs=a.check_crcs,
-                     output_partition=rank if a.local_output and world > 1 else -1)
+                     output_partition=rank if a.local_output and world > 1 else -1,
+                     producer_buffer_mb=a.producer_buffer_mb)
     devices = (list(range(local_gpus)) if local_gpus > 1 else [local_rank]) if use_gpu else None
     # ONE engine: warm-up and timed window are the same steady-state pipeline (connections,
     # pinned fetch buffers, captured graphs all warm); the timed window starts at a barrier

@@ -48,6 +48,7 @@ struct EngineConfig {
   std::string bootstrap = "127.0.0.1:9092";
   std::string input_topic, output_topic;
   int output_partition = -1;       // -1: the producer's partitioner; >= 0: this partition
+  int64_t producer_buffer_bytes = 32ll << 20;  // per sink producer (Kafka buffer.memory)
   std::string group_id;            // offsets committed under this group (empty: no commits)
   std::string client_id = "gale";
   std::vector<int> partitions;     // empty = every partition of input_topic
