@@ -964,6 +964,8 @@ void Engine::slo_step() {
   if (n < 16) return;  // too few completions in the window to estimate a p99
   const double p99_ms = h_slo_win_us_.quantile(0.99) * 1e-3;
   h_slo_win_us_.reset();
+  const double mean_batch = h_slo_batch_.mean();
+  h_slo_batch_.reset();
   const int maxb = cfg_.max_batch, minb = std::max(1, cfg_.max_batch / 32);
   const int64_t max_wait = (int64_t)cfg_.max_wait_us * 1000, min_wait = 20000;
   int b = eff_batch_.load();
@@ -984,8 +986,17 @@ void Engine::slo_step() {
   const int64_t in_flight = (int64_t)b * (int64_t)replicas_.size() * 3;
   const bool backlog =
       (int64_t)queued > (int64_t)b * (int64_t)replicas_.size() || unacked > 2 * in_flight;
+  // Batches leaving (nearly) full: they form faster than the window, so the latency is set by
+  // the replicas' capacity, not by batching delay - shrinking them would only cut capacity (the
+  // fp8 ResNet-20 at 1.0 M img/s fell into that cycle: mean batch 256 -> 110, p99 2 -> 8-60 ms,
+  // profiles/r2_slo_controller_ab.txt). A/B switch: GALE_SLO_FULL_BATCH=0 ignores it.
+  static const bool use_fill = [] {
+    const char* e = getenv("GALE_SLO_FULL_BATCH");
+    return !(e && *e == '0');
+  }();
+  const bool full = use_fill && mean_batch >= 0.9 * b;
   if (p99_ms > cfg_.slo_p99_ms) {
-    if (backlog) {
+    if (backlog || full) {
       b = std::min(maxb, b + std::max(1, maxb / 8));  // overload: capacity first
     } else {
       b = std::max(minb, b * 3 / 4);
@@ -1033,6 +1044,7 @@ void Engine::watchdog_loop() {
 void Engine::finish_batch(ReplicaSlot* rs, Batch& b) {
   h_device_us_.add((b.t_done_ns - b.t_submit_ns) / 1000);
   h_batch_images_.add(b.images);
+  if (cfg_.slo_p99_ms > 0) h_slo_batch_.add(b.images);
   rs->batches++;
   rs->images += b.images;
   rs->records += (int64_t)b.recs.size();

@@ -247,6 +247,7 @@ class Engine {
   std::atomic<int64_t> err_by_status_[8] = {};
   Histogram h_queue_us_, h_device_us_, h_engine_e2e_us_, h_record_e2e_ms_, h_batch_images_;
   Histogram h_slo_win_us_;  // e2e latency of the SLO controller's current window
+  Histogram h_slo_batch_;   // batch sizes (images) of the SLO controller's current window
   std::atomic<int> eff_batch_{0};
   std::atomic<int64_t> eff_wait_ns_{0};
   std::atomic<int64_t> slo_adjustments_{0};
