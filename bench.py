@@ -116,10 +116,15 @@ def parse_args(argv=None):
                          "real one. Not a measurement")
     ap.add_argument("--producer-buffer-mb", type=int, default=32,
                     help="unsent output bytes per sink producer (Kafka buffer.memory)")
+    ap.add_argument("--producer-request-kb", type=int, default=1024,
+                    help="bytes per produce request (Kafka max.request.size)")
     ap.add_argument("--local-output", action=argparse.BooleanOptionalAction, default=True,
                     help="each rank produces its outputs to the output partition its own broker "
                          "leads (--output-partition RANK) instead of round-robin over every "
                          "rank's broker (the unkeyed default)")
+    ap.add_argument("--all-stats", action="store_true",
+                    help="add every engine statistic of rank 0 (queue / device / e2e quantiles, "
+                         "lag, thread seconds) to the JSON line")
     ap.add_argument("--timeout", type=float, default=600.0)
     return ap.parse_args(argv)
 
@@ -320,7 +325,8 @@ def main(argv=None) -> int:
                      stub=a.stub, stub_null=a.stub_null, commit_interval_ms=500,
                      check_crcs=a.check_crcs,
                      output_partition=rank if a.local_output and world > 1 else -1,
-                     producer_buffer_mb=a.producer_buffer_mb)
+                     producer_buffer_mb=a.producer_buffer_mb,
+                     producer_request_kb=a.producer_request_kb)
     devices = (list(range(local_gpus)) if local_gpus > 1 else [local_rank]) if use_gpu else None
     # ONE engine: warm-up and timed window are the same steady-state pipeline (connections,
     # pinned fetch buffers, captured graphs all warm); the timed window starts at a barrier
@@ -433,6 +439,8 @@ def main(argv=None) -> int:
             "encode_s": round(t_enc, 1),
             "warmup_records": warm_done,
         }
+        if a.all_stats:
+            out["engine_stats_rank0"] = {k: round(v, 3) for k, v in st.items()}
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -24,6 +24,7 @@ EngineConfig config_from_dict(const py::dict& d) {
   opt(d, "output_topic", c.output_topic);
   opt(d, "output_partition", c.output_partition);
   opt(d, "producer_buffer_bytes", c.producer_buffer_bytes);
+  opt(d, "producer_request_bytes", c.producer_request_bytes);
   opt(d, "group_id", c.group_id);
   opt(d, "client_id", c.client_id);
   opt(d, "partitions", c.partitions);

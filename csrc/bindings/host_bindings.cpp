@@ -539,8 +539,10 @@ void bind_host(py::module_& m) {
 
   py::class_<Producer, std::shared_ptr<Producer>>(k, "Producer")
       .def(py::init([](const std::string& bootstrap, int acks, int linger_ms, int batch_size,
-                       const std::string& client_id, int request_timeout_ms, int max_in_flight) {
+                       const std::string& client_id, int request_timeout_ms, int max_in_flight,
+                       int max_request_size) {
              ProducerConfig c;
+             c.max_request_size = max_request_size;
              c.bootstrap = bootstrap;
              c.acks = acks;
              c.linger_ms = linger_ms;
@@ -553,7 +555,8 @@ void bind_host(py::module_& m) {
            }),
            py::arg("bootstrap"), py::arg("acks") = 1, py::arg("linger_ms") = 0,
            py::arg("batch_size") = 16384, py::arg("client_id") = "gale-producer",
-           py::arg("request_timeout_ms") = 30000, py::arg("max_in_flight") = 5)
+           py::arg("request_timeout_ms") = 30000, py::arg("max_in_flight") = 5,
+           py::arg("max_request_size") = 64 << 20)
       .def("send", [](Producer& p, const std::string& topic, py::object value, py::object key,
                       int partition, py::object headers, int64_t timestamp, py::object callback) {
         std::string v;

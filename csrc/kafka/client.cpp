@@ -488,9 +488,31 @@ void Producer::run() {
           }
           if (flush_req_ || closing_ || b.bytes >= (size_t)cfg_.batch_size ||
               now - b.first_ms >= cfg_.linger_ms) {
-            for (auto& p : b.recs) unsent_bytes_ -= (int64_t)(p.value.size() + p.key.size() + 32);
-            ready.push_back({it->first, std::move(b.recs)});
-            it = acc_.erase(it);
+            // at most max_request_size of records per drained batch (at least one record): what
+            // accumulated behind a busy sender leaves in request-sized batches, so the bytes in
+            // flight stay bounded by max_in_flight x max_request_size instead of growing with
+            // the backlog (one 30 MB batch per request was 0.5-1 s of ack latency at
+            // saturation, profiles/r2_producer_request_ab.txt)
+            size_t take = 0, bytes = 0;
+            while (take < b.recs.size()) {
+              const Pending& p = b.recs[take];
+              const size_t sz = p.value.size() + p.key.size() + 32;
+              if (take > 0 && bytes + sz > (size_t)cfg_.max_request_size) break;
+              bytes += sz;
+              ++take;
+            }
+            unsent_bytes_ -= (int64_t)bytes;
+            if (take == b.recs.size()) {
+              ready.push_back({it->first, std::move(b.recs)});
+              it = acc_.erase(it);
+            } else {
+              std::vector<Pending> head(std::make_move_iterator(b.recs.begin()),
+                                        std::make_move_iterator(b.recs.begin() + (long)take));
+              b.recs.erase(b.recs.begin(), b.recs.begin() + (long)take);
+              b.bytes -= bytes;
+              ready.push_back({it->first, std::move(head)});
+              ++it;
+            }
           } else {
             next = std::min(next, b.first_ms + cfg_.linger_ms);
             ++it;

@@ -235,6 +235,7 @@ void Engine::start() {
     pc.linger_ms = cfg_.linger_ms;
     pc.batch_size = cfg_.batch_size;
     pc.buffer_memory = cfg_.producer_buffer_bytes;
+    pc.max_request_size = (int)cfg_.producer_request_bytes;
     producers_.push_back(std::make_unique<kafka::Producer>(pc));
   }
   // static mode: resolve the input partitions and split them over the source threads now;

@@ -49,6 +49,7 @@ struct EngineConfig {
   std::string input_topic, output_topic;
   int output_partition = -1;       // -1: the producer's partitioner; >= 0: this partition
   int64_t producer_buffer_bytes = 32ll << 20;  // per sink producer (Kafka buffer.memory)
+  int64_t producer_request_bytes = 1 << 20;    // per produce request (Kafka max.request.size)
   std::string group_id;            // offsets committed under this group (empty: no commits)
   std::string client_id = "gale";
   std::vector<int> partitions;     // empty = every partition of input_topic

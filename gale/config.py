@@ -75,6 +75,7 @@ class GaleConfig:
     output_key: str = "none"           # reference: unkeyed output (E9); "input" = input's key
     producer_buffer_mb: int = 32       # unsent output bytes per sink producer before the sink
                                        # blocks (Kafka buffer.memory, 32 MB default)
+    producer_request_kb: int = 1024    # bytes per produce request (Kafka max.request.size)
     output_partition: int = -1         # -1: the producer's partitioner (reference: unkeyed
                                        # round-robin); >= 0: every output record to this
                                        # partition (e.g. the one this process's broker leads)
@@ -114,6 +115,8 @@ class GaleConfig:
         os.path.expanduser("~"), ".gale", "topologies"))
 
     def validate(self) -> "GaleConfig":
+        if self.producer_request_kb < 1:
+            raise ValueError("--producer-request-kb must be >= 1")
         if self.producer_buffer_mb < 1:
             raise ValueError("--producer-buffer-mb must be >= 1")
         if self.output_partition < -1:
@@ -161,7 +164,8 @@ class GaleConfig:
             value_format=self.value_format, type_id_header=self.type_id_header,
             on_error=self.on_error, output_key=self.output_key,
             output_partition=self.output_partition,
-            producer_buffer_bytes=self.producer_buffer_mb << 20, H=H, W=W, C=C, classes=classes,
+            producer_buffer_bytes=self.producer_buffer_mb << 20,
+            producer_request_bytes=self.producer_request_kb << 10, H=H, W=W, C=C, classes=classes,
             max_batch=self.max_batch,
             max_wait_us=self.max_wait_us, slo_p99_ms=self.slo_p99_ms,
             queue_depth=self.queue_depth,

@@ -286,3 +286,29 @@ def test_crc32c_combine_and_shift():
     a, bb = _os.urandom(1000), _os.urandom(3333)
     ca, cb = K.crc32c(a), K.crc32c(bb)
     assert K.crc32c_combine(ca, cb, len(bb)) == K.crc32c(a + bb)
+
+
+def test_producer_backlog_leaves_in_request_sized_batches(broker):
+    """Records that pile up behind a busy sender are drained in batches of at most
+    max_request_size (at least one record each), not as one batch of the whole backlog; order
+    within the partition is kept and every record is acknowledged once."""
+    p = K.Producer(bs(broker), acks=1, max_request_size=4096, max_in_flight=2)
+    acks = []
+    n = 400
+    for i in range(n):
+        p.send("big", (b"%04d" % i) * 50, partition=0,
+               callback=lambda e, part, off: acks.append((e, off)))
+    p.flush()
+    assert len(acks) == n and all(e == 0 for e, _ in acks)
+    assert sorted(off for _, off in acks) == list(range(n))
+    st = p.stats()
+    assert st["requests"] >= n * 200 // 4096  # 200-byte values: ~20 per 4 KB request
+    c = K.Consumer(bs(broker), auto_offset_reset="earliest")
+    c.assign("big", [0])
+    c.seek_to("earliest")
+    got = []
+    for _ in range(50):
+        got += c.poll()
+        if len(got) >= n:
+            break
+    assert [r["value"][:4] for r in got] == [b"%04d" % i for i in range(n)]
