@@ -58,7 +58,9 @@ struct PatchArgs {
 // CU - half the weight bytes per pixel, an A/B variant)
 // PB: patch buffers (2: the next block's patch loads during the last tap; 1: loaded at the block
 // boundary, exposed, but with 64-channel tiles the workgroup fits 4 per CU - an A/B variant)
-template <int BN, int PRR, int WM = 2, int PB = 2>
+// TPS: taps per k-step (between two barriers; the weight stage holds TPS taps): 2 halves the
+// barriers per MFMA - the A/B that tests whether the barrier cadence bounds these layers
+template <int BN, int PRR, int WM = 2, int PB = 2, int TPS = 1>
 __global__ __launch_bounds__(WM * 128, WM == 2 ? (PB == 1 && BN == 64 ? (PRR > 200 ? 3 : 4) : 2) : 1)
 void conv_patch_kernel(PatchArgs a) {
   constexpr int kBM = WM * 64;       // MFMA rows per tile (pixels P <= kBM; the rest read zeros)
@@ -68,7 +70,8 @@ void conv_patch_kernel(PatchArgs a) {
   constexpr int WI = BN / (8 * NW);  // weight wave-instructions per wave per step
   constexpr int NPJ = PRR / 8;       // patch wave-instructions
   constexpr int PJ = (NPJ + NW - 1) / NW;  // ... per wave
-  constexpr int WST = BN * 128;      // bytes per weight stage
+  constexpr int SPB = (9 + TPS - 1) / TPS;  // k-steps per 64-channel input block
+  constexpr int WST = TPS * BN * 128;  // bytes per weight stage
   constexpr int PST = PRR * 128;     // bytes per patch stage
   constexpr int CW = BN / WN;        // epilogue geometry (as conv_gemm)
   constexpr int EPS = CW + 4;
@@ -129,12 +132,19 @@ void conv_patch_kernel(PatchArgs a) {
       }
     }
   };
-  // step s = cb * 9 + tap: weight columns k = tap * Cin + cb * 64 (k = (kh*3 + kw)*Cin + ci)
+  // step s = cb * SPB + taps [TPS*(s % SPB), +TPS): weight columns k = tap * Cin + cb * 64
+  // (k = (kh*3 + kw)*Cin + ci)
   auto stage_w = [&](int s, uint8_t* buf) __attribute__((always_inline)) {
-    const int cb = s / 9, tap = s - cb * 9;
-    const int k0 = tap * a.Cin + cb * 64;
+    const int cb = s / SPB, t0 = (s - cb * SPB) * TPS;
 #pragma unroll
-    for (int j = 0; j < WI; ++j) glds16(wsrc[j] + k0, buf + (wave * WI + j) * 1024);
+    for (int tt = 0; tt < TPS; ++tt) {
+      if (t0 + tt < 9) {
+        const int k0 = (t0 + tt) * a.Cin + cb * 64;
+#pragma unroll
+        for (int j = 0; j < WI; ++j)
+          glds16(wsrc[j] + k0, buf + tt * BN * 128 + (wave * WI + j) * 1024);
+      }
+    }
   };
 
   // ---- fragment geometry ----
@@ -170,8 +180,8 @@ void conv_patch_kernel(PatchArgs a) {
     // step s has landed (vmcnt(0)); every wave is done with step s-1, whose weight buffer (and,
     // on a block's last tap, the previous block's patch buffer) is refilled below
     __syncthreads();
-    const int cb = s / 9, tap = s - cb * 9;
-    if (PB == 1 && tap == 0 && cb > 0) {  // every wave is done with block cb-1's patch
+    const int cb = s / SPB, sl = s - cb * SPB;
+    if (PB == 1 && sl == 0 && cb > 0) {  // every wave is done with block cb-1's patch
       stage_patch(cb, pbuf);
       __syncthreads();
     }
@@ -179,32 +189,39 @@ void conv_patch_kernel(PatchArgs a) {
     const uint8_t* pcur = pbuf + (PB == 2 ? (cb & 1) * PST : 0);
     if (s + 1 < a.nsteps) {
       stage_w(s + 1, wbuf + ((s + 1) & 1) * WST);
-      if (PB == 2 && tap == 8) stage_patch(cb + 1, pbuf + ((cb + 1) & 1) * PST);
-    }
-    const int kh = tap / 3;
-    const int toff = kh * a.PW + (tap - kh * 3);
-    int xoff[TM], xsw[TM];
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      const int row = pbase[i] >= 0 ? pbase[i] + toff : a.PR;  // (row PR: zeros)
-      xoff[i] = row * 128;
-      xsw[i] = (row >> 1) & 7;
+      if (PB == 2 && sl == SPB - 1) stage_patch(cb + 1, pbuf + ((cb + 1) & 1) * PST);
     }
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      const int chunk = kk * 4 + fq;
-      bf16x8 af[TN], bfr[TM];
+    for (int tt = 0; tt < TPS; ++tt) {
+      const int tap = sl * TPS + tt;
+      if (tap >= 9) break;
+      const uint8_t* wtap = wcur + tt * BN * 128;
+      const int kh = tap / 3;
+      const int toff = kh * a.PW + (tap - kh * 3);
+      int xoff[TM], xsw[TM];
 #pragma unroll
-      for (int t = 0; t < TN; ++t)
-        af[t] = *reinterpret_cast<const bf16x8*>(wcur + wrow_off[t] + ((chunk ^ wsw[t]) << 4));
+      for (int i = 0; i < TM; ++i) {
+        const int row = pbase[i] >= 0 ? pbase[i] + toff : a.PR;  // (row PR: zeros)
+        xoff[i] = row * 128;
+        xsw[i] = (row >> 1) & 7;
+      }
 #pragma unroll
-      for (int i = 0; i < TM; ++i)
-        bfr[i] = *reinterpret_cast<const bf16x8*>(pcur + xoff[i] + ((chunk ^ xsw[i]) << 4));
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
+      for (int kk = 0; kk < 2; ++kk) {
+        const int chunk = kk * 4 + fq;
+        bf16x8 af[TN], bfr[TM];
 #pragma unroll
         for (int t = 0; t < TN; ++t)
-          acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[t], bfr[i], acc[i][t], 0, 0, 0);
+          af[t] = *reinterpret_cast<const bf16x8*>(wtap + wrow_off[t] + ((chunk ^ wsw[t]) << 4));
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+          bfr[i] = *reinterpret_cast<const bf16x8*>(pcur + xoff[i] + ((chunk ^ xsw[i]) << 4));
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int t = 0; t < TN; ++t)
+            acc[i][t] =
+                __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[t], bfr[i], acc[i][t], 0, 0, 0);
+      }
     }
   }
 
@@ -294,7 +311,17 @@ std::atomic<int> g_patch_occ{[] {
   return e && *e ? atoi(e) : 2;
 }()};
 
+// GALE_CONV_PATCH_TPS: 1 = 64-channel tiles everywhere eligible, one tap per k-step; 2 = the same
+// with two taps per k-step (half the barriers per MFMA). The A/B pair for the barrier-cadence
+// question (measured: 103-105 -> 98 us per layer, ~5 %; both below the default 128-channel tiles
+// at 79-81 us, profiles/r2_conv_patch.txt); 0 (default) = neither.
+std::atomic<int> g_patch_tps{[] {
+  const char* e = getenv("GALE_CONV_PATCH_TPS");
+  return e && *e ? atoi(e) : 0;
+}()};
+
 int patch_bn(const ConvDesc& d) {
+  if (g_patch_tps.load(std::memory_order_relaxed) > 0 && d.Npad % 64 == 0) return 64;
   if (g_patch_occ.load(std::memory_order_relaxed) == 4 && d.Npad % 64 == 0) return 64;
   return (d.Npad % 128 == 0) ? 128 : 64;
 }
@@ -319,7 +346,8 @@ bool conv_patch_supported(const ConvDesc& d, int batch, bool has_res) {
   if (d.Cin % 64 != 0 || d.K != 9 * d.Cin || d.Kpad != d.K) return false;
   if (d.Ho != d.H || d.Wo != d.W || d.W > 128 || d.Cout % 8 != 0) return false;
   const int bn = patch_bn(d);
-  const bool occ4 = g_patch_occ.load(std::memory_order_relaxed) == 4;
+  const bool occ4 = g_patch_occ.load(std::memory_order_relaxed) == 4 ||
+                    g_patch_tps.load(std::memory_order_relaxed) > 0;
   if (d.Npad % bn != 0 || d.Npad < d.Cout) return false;
   if (bn == 64 && !occ4 && g_conv_patch.load(std::memory_order_relaxed) < 2) return false;
   if (has_res && (d.res_C != d.Cout || d.res_stride != 1 || d.res_H != d.H || d.res_W != d.W))
@@ -331,6 +359,7 @@ bool conv_patch_supported(const ConvDesc& d, int batch, bool has_res) {
   const int prr = patch_prr((tr + 2) * (d.W + 2));
   if (prr == 0 || (bm == 128 && bn == 128 && prr > 184) || (bm == 256 && prr != 272))
     return false;
+  if (g_patch_tps.load(std::memory_order_relaxed) == 2 && prr > 184) return false;
   return (long long)batch * d.H * d.W * d.Cin < (1ll << 31) &&
          (long long)batch * d.H * d.W * d.Cout < (1ll << 31);
 }
@@ -352,7 +381,8 @@ hipError_t conv2d_patch(const ConvDesc& d, int batch, const void* x, const void*
   a.PW = d.W + 2;
   a.PR = (a.TR + 2) * a.PW;
   a.rblocks = d.H / a.TR;
-  a.nsteps = 9 * (d.Cin / 64);
+  const int tps = g_patch_tps.load(std::memory_order_relaxed) == 2 ? 2 : 1;
+  a.nsteps = (tps == 2 ? 5 : 9) * (d.Cin / 64);  // k-steps: ceil(9 / taps per step) per block
   a.relu = d.relu;
   a.has_res = d.has_res && res != nullptr;
   a.n_tiles = d.Npad / bn;
@@ -368,6 +398,15 @@ hipError_t conv2d_patch(const ConvDesc& d, int batch, const void* x, const void*
       hipLaunchKernelGGL((conv_patch_kernel<128, 152>), dim3(a.nwg), dim3(256), 0, stream, a);
     else
       hipLaunchKernelGGL((conv_patch_kernel<128, 184>), dim3(a.nwg), dim3(256), 0, stream, a);
+  } else if (tps == 2) {
+    if (prr == 152)
+      hipLaunchKernelGGL((conv_patch_kernel<64, 152, 2, 2, 2>), dim3(a.nwg), dim3(256), 0, stream,
+                         a);
+    else if (prr == 184)
+      hipLaunchKernelGGL((conv_patch_kernel<64, 184, 2, 2, 2>), dim3(a.nwg), dim3(256), 0, stream,
+                         a);
+    else
+      return hipErrorInvalidValue;
   } else if (g_patch_occ.load(std::memory_order_relaxed) == 4) {
     if (prr == 152)
       hipLaunchKernelGGL((conv_patch_kernel<64, 152, 2, 1>), dim3(a.nwg), dim3(256), 0, stream, a);
