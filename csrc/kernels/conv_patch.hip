@@ -194,7 +194,7 @@ void conv_patch_kernel(PatchArgs a) {
 #pragma unroll
     for (int tt = 0; tt < TPS; ++tt) {
       const int tap = sl * TPS + tt;
-      if (tap >= 9) break;
+      if (TPS > 1 && tap >= 9) break;  // (a partial last step; TPS = 1 never)
       const uint8_t* wtap = wcur + tt * BN * 128;
       const int kh = tap / 3;
       const int toff = kh * a.PW + (tap - kh * 3);
