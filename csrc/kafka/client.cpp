@@ -488,31 +488,28 @@ void Producer::run() {
           }
           if (flush_req_ || closing_ || b.bytes >= (size_t)cfg_.batch_size ||
               now - b.first_ms >= cfg_.linger_ms) {
-            // at most max_request_size of records per drained batch (at least one record): what
-            // accumulated behind a busy sender leaves in request-sized batches, so the bytes in
-            // flight stay bounded by max_in_flight x max_request_size instead of growing with
-            // the backlog (one 30 MB batch per request was 0.5-1 s of ack latency at
-            // saturation, profiles/r2_producer_request_ab.txt)
-            size_t take = 0, bytes = 0;
-            while (take < b.recs.size()) {
-              const Pending& p = b.recs[take];
+            // drained as batches of at most max_request_size (at least one record each): what
+            // accumulated behind a busy sender leaves in request-sized batches, so a request
+            // (and the bytes awaiting acks, max_in_flight of them) stays bounded instead of
+            // growing with the backlog (one 30 MB batch per request was 0.5-1 s of ack latency
+            // at saturation, profiles/r2_producer_request_ab.txt)
+            size_t total = 0;
+            std::vector<Pending> chunk;
+            size_t cbytes = 0;
+            for (auto& p : b.recs) {
               const size_t sz = p.value.size() + p.key.size() + 32;
-              if (take > 0 && bytes + sz > (size_t)cfg_.max_request_size) break;
-              bytes += sz;
-              ++take;
+              if (!chunk.empty() && cbytes + sz > (size_t)cfg_.max_request_size) {
+                ready.push_back({it->first, std::move(chunk)});
+                chunk.clear();
+                cbytes = 0;
+              }
+              chunk.push_back(std::move(p));
+              cbytes += sz;
+              total += sz;
             }
-            unsent_bytes_ -= (int64_t)bytes;
-            if (take == b.recs.size()) {
-              ready.push_back({it->first, std::move(b.recs)});
-              it = acc_.erase(it);
-            } else {
-              std::vector<Pending> head(std::make_move_iterator(b.recs.begin()),
-                                        std::make_move_iterator(b.recs.begin() + (long)take));
-              b.recs.erase(b.recs.begin(), b.recs.begin() + (long)take);
-              b.bytes -= bytes;
-              ready.push_back({it->first, std::move(head)});
-              ++it;
-            }
+            if (!chunk.empty()) ready.push_back({it->first, std::move(chunk)});
+            unsent_bytes_ -= (int64_t)total;
+            it = acc_.erase(it);
           } else {
             next = std::min(next, b.first_ms + cfg_.linger_ms);
             ++it;
@@ -553,6 +550,11 @@ void Producer::run() {
         size_t bytes = 0;
         for (; k < kv.second.size(); ++k) {
           auto& item = ready[kv.second[k]];
+          // one batch per partition per request (consecutive chunks of one partition's backlog
+          // go in separate requests, in order)
+          bool dup = false;
+          for (const auto& fb : f.batches) dup |= fb.first == item.first;
+          if (dup) break;
           std::vector<RecordIn> ins(item.second.size());
           for (size_t j = 0; j < item.second.size(); ++j) {
             const Pending& p = item.second[j];
