@@ -21,6 +21,7 @@
 // The epilogue (bias, residual, ReLU) is the same as conv_gemm's, staged through LDS.
 #include <stdlib.h>
 
+#include <algorithm>
 #include <atomic>
 
 #include "common.cuh"
@@ -47,6 +48,8 @@ struct PatchArgs {
   int H, W, Cin, Cout, Kpad;
   int TR, P, PW, PR;    // rows per tile, pixels per tile (TR * W), patch width W + 2, patch rows
   int rblocks;          // H / TR
+  int IMG, PR1, B;      // whole images per tile (> 1 only when TR == H: 7x7), patch rows per
+                        // image, batch (the last tile of a multi-image layer may be partial)
   int nsteps;           // 9 * Cin / 64
   int relu, has_res;
   int n_tiles, nwg;
@@ -95,8 +98,10 @@ void conv_patch_kernel(PatchArgs a) {
   const int xcd = bid & 7, q = a.nwg >> 3, r8 = a.nwg & 7;
   const int rid = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + (bid >> 3);
   const int mt = rid / a.n_tiles, nt = rid - mt * a.n_tiles;
-  const int img = mt / a.rblocks, rb = mt - img * a.rblocks;
+  const int img = (mt / a.rblocks) * a.IMG, rb = mt - (mt / a.rblocks) * a.rblocks;
   const int y0 = rb * a.TR;
+  // pixels of this tile that exist (a partial last multi-image tile has fewer images)
+  const int pvalid = a.IMG > 1 ? min(a.P, (a.B - img) * a.H * a.W) : a.P;
 
   // ---- staging sources ----
   const int srow = lane >> 3, slot = lane & 7;
@@ -108,10 +113,11 @@ void conv_patch_kernel(PatchArgs a) {
     const int chunk = slot ^ ((row >> 1) & 7);
     poff[j] = -1;
     if (wi < NPJ && row < a.PR) {
-      const int py = row / a.PW, px = row - py * a.PW;
+      const int ii = row / a.PR1, r1 = row - ii * a.PR1;  // image of the tile, row within its patch
+      const int py = r1 / a.PW, px = r1 - py * a.PW;
       const int yy = y0 - 1 + py, xx = px - 1;
-      if ((unsigned)yy < (unsigned)a.H && (unsigned)xx < (unsigned)a.W)
-        poff[j] = ((img * a.H + yy) * a.W + xx) * a.Cin + chunk * 8;
+      if ((unsigned)yy < (unsigned)a.H && (unsigned)xx < (unsigned)a.W && img + ii < a.B)
+        poff[j] = (((img + ii) * a.H + yy) * a.W + xx) * a.Cin + chunk * 8;
     }
   }
   const bf16* wsrc[WI];
@@ -153,9 +159,10 @@ void conv_patch_kernel(PatchArgs a) {
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
     const int p = wm * (kBM / WM) + i * 16 + fr;
-    if (p < a.P) {
-      const int py = p / a.W;
-      pbase[i] = py * a.PW + (p - py * a.W);
+    if (p < pvalid) {
+      const int ii = p / (a.TR * a.W), q1 = p - ii * (a.TR * a.W);
+      const int py = q1 / a.W;
+      pbase[i] = ii * a.PR1 + py * a.PW + (q1 - py * a.W);
     } else {
       pbase[i] = -1;
     }
@@ -252,7 +259,7 @@ void conv_patch_kernel(PatchArgs a) {
     for (int j = 0; j < NRI; ++j) {
       const int pr = j * RPI + lane / LPR;
       const int p = pw0 + h * HALF + pr;
-      if (p < a.P && c0 + cc < a.Cout) {
+      if (p < pvalid && c0 + cc < a.Cout) {
         const float* src = ep + pr * EPS + cc;
         const float4 lo = *reinterpret_cast<const float4*>(src);
         const float4 hi = *reinterpret_cast<const float4*>(src + 4);
@@ -286,6 +293,18 @@ int patch_tile_rows(const ConvDesc& d, int bm) {
   for (int tr = bm / d.W; tr >= 1; --tr)
     if (d.H % tr == 0) return tr;
   return 0;
+}
+
+// whole images per tile: several when one image's rows fill less than half the tile (7x7: 2 x 49
+// of 128 MFMA rows; GALE_CONV_PATCH_MULTI=0 keeps one image per tile)
+std::atomic<int> g_patch_multi{[] {
+  const char* e = getenv("GALE_CONV_PATCH_MULTI");
+  return !(e && *e == '0');
+}()};
+
+int patch_images(const ConvDesc& d, int bm, int tr) {
+  if (tr != d.H || !g_patch_multi.load(std::memory_order_relaxed)) return 1;
+  return std::max(1, bm / (d.H * d.W));
 }
 
 int patch_prr(int PR) {
@@ -354,9 +373,10 @@ bool conv_patch_supported(const ConvDesc& d, int batch, bool has_res) {
     return false;
   const int bm = patch_bm(bn);
   const int tr = patch_tile_rows(d, bm);
-  // (a tile below 3/4 of its MFMA rows wastes too much: 7x7 stays on conv_gemm)
-  if (tr < 1 || tr * d.W * 4 < bm * 3 - 16) return false;
-  const int prr = patch_prr((tr + 2) * (d.W + 2));
+  const int img = tr >= 1 ? patch_images(d, bm, tr) : 1;
+  // (a tile below 3/4 of its MFMA rows wastes too much)
+  if (tr < 1 || img * tr * d.W * 4 < bm * 3 - 16) return false;
+  const int prr = patch_prr(img * (tr + 2) * (d.W + 2));
   if (prr == 0 || (bm == 128 && bn == 128 && prr > 184) || (bm == 256 && prr != 272))
     return false;
   if (g_patch_tps.load(std::memory_order_relaxed) == 2 && prr > 184) return false;
@@ -377,16 +397,19 @@ hipError_t conv2d_patch(const ConvDesc& d, int batch, const void* x, const void*
   const int bm = patch_bm(bn);
   a.TR = patch_tile_rows(d, bm);
   if (a.TR < 1) return hipErrorInvalidValue;
-  a.P = a.TR * d.W;
+  a.IMG = patch_images(d, bm, a.TR);
+  a.B = batch;
+  a.P = a.IMG * a.TR * d.W;
   a.PW = d.W + 2;
-  a.PR = (a.TR + 2) * a.PW;
+  a.PR1 = (a.TR + 2) * a.PW;
+  a.PR = a.IMG * a.PR1;
   a.rblocks = d.H / a.TR;
   const int tps = g_patch_tps.load(std::memory_order_relaxed) == 2 ? 2 : 1;
   a.nsteps = (tps == 2 ? 5 : 9) * (d.Cin / 64);  // k-steps: ceil(9 / taps per step) per block
   a.relu = d.relu;
   a.has_res = d.has_res && res != nullptr;
   a.n_tiles = d.Npad / bn;
-  a.nwg = batch * a.rblocks * a.n_tiles;
+  a.nwg = (batch + a.IMG - 1) / a.IMG * a.rblocks * a.n_tiles;
   const int prr = patch_prr(a.PR);
   if (a.P > bm || prr == 0) return hipErrorInvalidValue;
   if (bm == 256) {

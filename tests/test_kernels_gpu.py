@@ -423,6 +423,7 @@ PATCH_CASES = [  # B, H, W, Cin, Cout, with_res: the ResNet-50 3x3 stride-1 shap
     (3, 28, 28, 128, 128, True),    # 4 rows x 28, BN = 128
     (2, 14, 14, 256, 256, False),   # 7 rows x 14 (98 of 128 MFMA rows), two channel tiles
     (1, 14, 14, 128, 64, True),     # BN = 64 at 14 x 14
+    (3, 7, 7, 512, 512, True),      # two whole 7 x 7 images per tile, a partial last tile
 ]
 
 
@@ -465,7 +466,8 @@ def test_conv2d_patch_path_matches_torch(case):
     assert (y.float() - y_gemm.float()).abs().max().item() <= 1e-2 * scale + 1e-2
 
 
-@pytest.mark.parametrize("H,C,tap", [(56, 64, 4), (28, 128, 0), (14, 256, 8), (28, 128, 5)])
+@pytest.mark.parametrize("H,C,tap", [(56, 64, 4), (28, 128, 0), (14, 256, 8), (28, 128, 5),
+                                     (7, 128, 0), (7, 128, 8)])
 def test_conv2d_patch_single_tap_shift_is_exact(H, C, tap):
     """One identity tap (kh, kw) and zeros elsewhere: y[n, i, j] = x[n, i + kh - 1, j + kw - 1]
     (zero outside the image), bit exact - pins the patch-row mapping, the halo and the zero
