@@ -20,8 +20,8 @@ What one rank (= one GPU, launched by torch.distributed.run for N > 1) does:
   pinned H2D -> GPU JSON parse -> hipGraph ResNet-20 forward -> D2H softmax ->
   {"predictions": ...} encode -> Kafka Produce (acks=1) -> ack.
 
-Steady state: warm-up is W steps AND at least ``--min-warmup-s`` seconds AND until two
-consecutive 250 ms windows agree within 5 % (capped at ``--max-warmup-s``). A step is
+Steady state: warm-up is W steps AND at least ``--min-warmup-s`` seconds AND until the last
+four 500 ms rate windows (2 s) all lie within 5 % of their mean (capped at ``--max-warmup-s``). A step is
 ``--step-images`` images per GPU (default 131072: 512 micro-batches of 256) completing the whole
 path (acknowledged by the broker), so the default K = 20 steps is a >= 1 s window on one
 MI355X (1.7 s at 1.5 M img/s; 65536-image steps fell to 0.86 s once the pipeline passed
@@ -99,8 +99,12 @@ def parse_args(argv=None):
                          "sendfile analogue) instead of writev copies")
     ap.add_argument("--numa-pin", action=argparse.BooleanOptionalAction, default=True,
                     help="pin the host pipeline's threads to the GPU's NUMA node")
-    ap.add_argument("--cpus-per-rank", type=int, default=0,
-                    help="with --numa-pin: only this rank's slice of the node's CPUs (0 = all)")
+    ap.add_argument("--cpus-per-rank", type=int, default=-1,
+                    help="with --numa-pin: only this rank's slice of the node's CPUs (0 = the "
+                         "whole NUMA node; -1 = the rank's cgroup CPU quota when one is set, "
+                         "so the pipeline is scheduled on as many CPUs as it may use instead of "
+                         "being frozen by CFS bandwidth throttling whenever its threads burst "
+                         "above the quota)")
     ap.add_argument("--gpu-wait-poll-us", type=int, default=20,
                     help="replica workers sleep-poll batch completion every N us (0 = spin)")
     ap.add_argument("--encode-threads", type=int, default=0,
@@ -125,8 +129,95 @@ def parse_args(argv=None):
     ap.add_argument("--all-stats", action="store_true",
                     help="add every engine statistic of rank 0 (queue / device / e2e quantiles, "
                          "lag, thread seconds) to the JSON line")
+    ap.add_argument("--timeline", default="",
+                    help="write a JSON line every --timeline-ms (completions, per-stage CPU, "
+                         "cgroup throttling, RSS, queue depth, lag) to this file (rank 0)")
+    ap.add_argument("--timeline-ms", type=int, default=100)
     ap.add_argument("--timeout", type=float, default=600.0)
     return ap.parse_args(argv)
+
+
+def _cgroup_cpu_stat() -> dict:
+    try:
+        with open("/sys/fs/cgroup/cpu.stat") as f:
+            return {k: int(v) for k, v in (ln.split() for ln in f if ln.strip())}
+    except (OSError, ValueError):
+        return {}
+
+
+def _rss_mb() -> float:
+    try:
+        with open("/proc/self/statm") as f:
+            return int(f.read().split()[1]) * os.sysconf("SC_PAGE_SIZE") / 2**20
+    except (OSError, ValueError):
+        return -1.0
+
+
+class Timeline:
+    """Diagnostic sampler (--timeline): one JSON line per interval with the completion rate,
+    CPU cores per pipeline stage, cgroup CPU throttling, RSS and the engine's queue / lag, so
+    a throughput dip can be lined up with what the host was doing at that moment."""
+
+    def __init__(self, path, interval_ms, broker):
+        from gale.utils import thread_cpu_by_thread, thread_cpu_seconds
+
+        self.per_thread = thread_cpu_by_thread
+        self.f = open(path, "w")
+        self.dt = interval_ms / 1e3
+        self.broker = broker
+        self.cpu = thread_cpu_seconds
+        self.engine = None
+        self.phase = "warmup"
+        self._stop = threading.Event()
+        self._t = threading.Thread(target=self._run, name="timeline", daemon=True)
+
+    def start(self, engine):
+        self.engine = engine
+        self._t.start()
+
+    def _run(self):
+        t0 = time.perf_counter()
+        prev_t, prev_c, prev_cpu, prev_cg = t0, self.engine.completed, self.cpu(), _cgroup_cpu_stat()
+        prev_b = self.broker.stats() if self.broker is not None else None
+        prev_th = self.per_thread()
+        groups = ("gl-brk", "gl-src", "gl-dec", "gl-rep", "gl-sink", "gl-watchdog")
+        while not self._stop.wait(self.dt):
+            now, c, cpu, cg = time.perf_counter(), self.engine.completed, self.cpu(), _cgroup_cpu_stat()
+            dt = now - prev_t
+            st = self.engine.stats()
+            row = {"t": round(now - t0, 3), "phase": self.phase,
+                   "rate": round((c - prev_c) / dt),
+                   "cores": {k: round((cpu[k] - prev_cpu.get(k, 0.0)) / dt, 2) for k in cpu},
+                   "rss_mb": round(_rss_mb()),
+                   "queue": int(st.get("queue_records", 0)),
+                   "lag": int(st.get("lag_records", 0)),
+                   "fetch_lag": int(st.get("fetch_lag_records", 0))}
+            if cg:
+                row["throttled_ms"] = round((cg.get("throttled_usec", 0)
+                                             - prev_cg.get("throttled_usec", 0)) / 1e3, 1)
+                row["cg_cores"] = round((cg.get("usage_usec", 0)
+                                         - prev_cg.get("usage_usec", 0)) / 1e6 / dt, 2)
+            th = self.per_thread()
+            other = {}
+            for k, v in th.items():
+                if not k[1].startswith(groups):
+                    other[k[1]] = other.get(k[1], 0.0) + v - prev_th.get(k, 0.0)
+            row["other_top"] = {k: round(v / dt, 2) for k, v in
+                                sorted(other.items(), key=lambda kv: -kv[1])[:4] if v > 0}
+            prev_th = th
+            if prev_b is not None:
+                b = self.broker.stats()
+                row["brk_out_gbs"] = round((b["bytes_out"] - prev_b["bytes_out"]) / dt / 1e9, 2)
+                row["brk_in_mbs"] = round((b["bytes_in"] - prev_b["bytes_in"]) / dt / 1e6, 1)
+                prev_b = b
+            self.f.write(json.dumps(row) + "\n")
+            self.f.flush()
+            prev_t, prev_c, prev_cpu, prev_cg = now, c, cpu, cg
+
+    def stop(self):
+        self._stop.set()
+        self._t.join()
+        self.f.close()
 
 
 class Feeder:
@@ -185,9 +276,11 @@ class Feeder:
         self._t.join()
 
 
-def warm_up(eng, records, a, rate_window=0.25):
-    """W steps, then until >= min_warmup_s elapsed and two consecutive windows agree within 5 %
-    (or max_warmup_s). Returns (seconds, last window rates)."""
+def warm_up(eng, records, a, rate_window=0.5, windows=4, tol=0.05):
+    """W steps, then until >= min_warmup_s elapsed and the last ``windows`` rate windows of
+    ``rate_window`` s (>= 2 s together) all lie within ``tol`` of their mean (or max_warmup_s).
+    A slow oscillation (e.g. CFS throttling phases of ~0.5-1 s) shows up as a spread across
+    the 2 s span, which two adjacent 250 ms windows could miss. Returns (seconds, rates)."""
     t_start = time.perf_counter()
     if not eng.wait_completed(records, a.timeout):
         raise SystemExit(f"warm-up timed out ({eng.completed}/{records})")
@@ -197,9 +290,12 @@ def warm_up(eng, records, a, rate_window=0.25):
         time.sleep(rate_window)
         rates.append((eng.completed - c0) / (time.perf_counter() - t0))
         el = time.perf_counter() - t_start
-        stable = len(rates) >= 2 and abs(rates[-1] - rates[-2]) <= 0.05 * max(rates[-2:])
+        last = rates[-windows:]
+        mean = sum(last) / len(last)
+        stable = len(last) == windows and mean > 0 and \
+            max(abs(r - mean) for r in last) <= tol * mean
         if (el >= a.min_warmup_s and stable) or el >= a.max_warmup_s:
-            return el, rates[-2:]
+            return el, last
 
 
 def main(argv=None) -> int:
@@ -254,12 +350,17 @@ def main(argv=None) -> int:
                          f"{torch.cuda.device_count()} visible")
     if use_gpu and a.shared_gpu_rehearsal:
         local_rank %= torch.cuda.device_count()
+    pinned_cpus = set()
     if use_gpu:
         torch.cuda.set_device(local_rank)
         if a.numa_pin and local_gpus == 1:
-            from gale.utils import pin_to_gpu_numa
+            from gale.utils import cgroup_cpu_quota, pin_to_gpu_numa
 
-            pin_to_gpu_numa(local_rank, a.cpus_per_rank)
+            if a.cpus_per_rank < 0:
+                q = cgroup_cpu_quota()
+                a.cpus_per_rank = int(q // max(1, int(os.environ.get("LOCAL_WORLD_SIZE", "1")))) \
+                    if q else 0
+            pinned_cpus = pin_to_gpu_numa(local_rank, a.cpus_per_rank)
     if world > 1:
         nccl = use_gpu and not a.shared_gpu_rehearsal
         dist.init_process_group(backend="nccl" if nccl else "gloo",
@@ -291,7 +392,11 @@ def main(argv=None) -> int:
     del imgs
     t_enc = time.perf_counter() - t_enc
 
-    broker = K.Broker(node_id=rank, max_message_bytes=256 << 20, retention_bytes=1 << 62,
+    # byte retention per partition: far above the backlog the feeder keeps ahead of the
+    # consumers (input batches are shared references, so input retention costs no copies), but
+    # bounded, so the output topic (~0.3 GB/s of predictions at 1.5 M img/s) does not grow the
+    # broker's memory for the whole run
+    broker = K.Broker(node_id=rank, max_message_bytes=256 << 20, retention_bytes=2 << 30,
                       zero_copy=a.broker_zero_copy, log_append_time=True)
     broker.start()
     n_parts = world * parts_per_rank
@@ -336,7 +441,12 @@ def main(argv=None) -> int:
                  stub_localities=tuple(range(local_gpus)) if a.stub and local_gpus > 1 else ())
     eng.start()
     feeder.start(eng)
+    timeline = Timeline(a.timeline, a.timeline_ms, broker) if a.timeline and rank == 0 else None
+    if timeline:
+        timeline.start(eng)
     warm_s, warm_rates = warm_up(eng, max(1, a.warmup) * step_records, a)
+    if timeline:
+        timeline.phase = "timed"
     warm_done = eng.completed
     if world > 1:
         dist.barrier()
@@ -359,6 +469,8 @@ def main(argv=None) -> int:
     cpu1 = thread_cpu_seconds()
     done_records = eng.completed - c0
     st = eng.stats()
+    if timeline:
+        timeline.stop()
     if world > 1:
         dist.barrier()
     feeder.stop()
@@ -437,6 +549,7 @@ def main(argv=None) -> int:
             "cpu_cores_busy_rank0": round(sum(cores.values()), 2),
             "cpu_cores_by_stage_rank0": cores,
             "encode_s": round(t_enc, 1),
+            "cpus_pinned_rank0": len(pinned_cpus),
             "warmup_records": warm_done,
         }
         if a.all_stats:

@@ -672,6 +672,41 @@ void bind_host(py::module_& m) {
       .def("set_generation", &Consumer::set_generation, py::arg("generation"),
            py::arg("member_id"));
 
+  py::class_<GroupMember, std::shared_ptr<GroupMember>>(k, "GroupMember")
+      .def(py::init([](const std::string& bootstrap, const std::string& group_id,
+                       const std::string& topic, int session_timeout_ms,
+                       int rebalance_timeout_ms, const std::string& assignor,
+                       const std::string& client_id) {
+             GroupConfig c;
+             c.bootstrap = bootstrap;
+             c.group_id = group_id;
+             c.topic = topic;
+             c.session_timeout_ms = session_timeout_ms;
+             c.rebalance_timeout_ms = rebalance_timeout_ms;
+             c.assignor = assignor;
+             c.client_id = client_id;
+             py::gil_scoped_release nogil;
+             return std::make_shared<GroupMember>(c);
+           }),
+           py::arg("bootstrap"), py::arg("group_id"), py::arg("topic"),
+           py::arg("session_timeout_ms") = 6000, py::arg("rebalance_timeout_ms") = 8000,
+           py::arg("assignor") = "range", py::arg("client_id") = "gale-group")
+      .def("join", [](GroupMember& g) {
+        py::gil_scoped_release nogil;
+        return g.join();
+      })
+      .def("heartbeat", [](GroupMember& g) {
+        py::gil_scoped_release nogil;
+        return g.heartbeat();
+      })
+      .def("leave", [](GroupMember& g) {
+        py::gil_scoped_release nogil;
+        g.leave();
+      })
+      .def_property_readonly("member_id", &GroupMember::member_id)
+      .def_property_readonly("generation", &GroupMember::generation)
+      .def_property_readonly("is_leader", &GroupMember::is_leader);
+
   py::register_exception<KafkaError>(k, "KafkaError");
   py::register_exception<ProtocolError>(k, "ProtocolError");
 

@@ -366,6 +366,21 @@ int Producer::choose_partition(const std::string& topic, const std::string* key)
   return (int)((rr_++ & 0x7fffffffu) % (uint32_t)n);
 }
 
+// Upper bound of one record's encoded size in a RecordBatch v2: the varint fields (length,
+// attributes, timestamp / offset deltas, key / value lengths, header count) take at most 36
+// bytes, each header at most 10 more besides its key and value. Chunks are cut on this bound so
+// an encoded batch never exceeds max_request_size (headers such as __TypeId__ included).
+static size_t record_bound(const std::string& key, const std::string& value,
+                           const std::vector<Header>& headers) {
+  size_t n = key.size() + value.size() + 36;
+  for (const Header& h : headers) n += h.key.size() + h.value.size() + 10;
+  return n;
+}
+
+// request bytes outside the records: request header, topic / partition framing and the
+// 61-byte RecordBatch header
+static constexpr size_t kRequestOverhead = 1024;
+
 void Producer::send(const std::string& topic, int partition, const std::string* key,
                     std::string value, bool value_null, std::vector<Header> headers,
                     int64_t timestamp, SendCallback cb) {
@@ -383,7 +398,7 @@ void Producer::send(const std::string& topic, int partition, const std::string* 
   p.headers = std::move(headers);
   p.ts = timestamp >= 0 ? timestamp : wall_ms();
   p.cb = std::move(cb);
-  const size_t sz = p.value.size() + p.key.size() + 32;
+  const size_t sz = record_bound(p.key, p.value, p.headers);
   PartBatch& b = acc_[{topic, partition}];
   if (b.recs.empty()) b.first_ms = mono_ms();
   b.bytes += sz;
@@ -496,9 +511,12 @@ void Producer::run() {
             size_t total = 0;
             std::vector<Pending> chunk;
             size_t cbytes = 0;
+            const size_t cap = (size_t)cfg_.max_request_size > 2 * kRequestOverhead
+                                   ? (size_t)cfg_.max_request_size - kRequestOverhead
+                                   : (size_t)cfg_.max_request_size / 2;
             for (auto& p : b.recs) {
-              const size_t sz = p.value.size() + p.key.size() + 32;
-              if (!chunk.empty() && cbytes + sz > (size_t)cfg_.max_request_size) {
+              const size_t sz = record_bound(p.key, p.value, p.headers);
+              if (!chunk.empty() && cbytes + sz > cap) {
                 ready.push_back({it->first, std::move(chunk)});
                 chunk.clear();
                 cbytes = 0;

@@ -24,11 +24,16 @@ GroupCoordinator::Group& GroupCoordinator::group(const std::string& id) {
   return *g;
 }
 
-// Members whose session lapsed leave the group; a stable group then rebalances.
+// Members whose session lapsed leave the group; a stable group then rebalances. As in Kafka, a
+// member blocked in JoinGroup / SyncGroup (or already rejoined while the group prepares a
+// rebalance) is not expired: it is waiting on the coordinator, not silent. Members that never
+// rejoin are dropped by complete_join at the rebalance deadline instead.
 void GroupCoordinator::expire(Group& g, int64_t now) {
   bool gone = false;
   for (auto it = g.members.begin(); it != g.members.end();) {
-    if (now - it->second.last_seen > it->second.session_ms) {
+    const Member& m = it->second;
+    const bool exempt = m.waiting > 0 || (g.state == "PreparingRebalance" && m.joined);
+    if (!exempt && now - m.last_seen > m.session_ms) {
       if (g.leader == it->first) g.leader.clear();
       it = g.members.erase(it);
       gone = true;
@@ -87,7 +92,13 @@ bool GroupCoordinator::complete_join(Group& g) {
   ++g.generation;
   g.state = "CompletingRebalance";
   g.synced = false;
-  for (auto& kv : g.members) kv.second.assignment.clear();
+  // every survivor's session restarts now (its JoinGroup answer is on its way; a member whose
+  // thread has not woken yet must not be expired by another request in the meantime)
+  const int64_t now = now_ms();
+  for (auto& kv : g.members) {
+    kv.second.assignment.clear();
+    kv.second.last_seen = now;
+  }
   g.cv.notify_all();
   return true;
 }
@@ -127,17 +138,19 @@ JoinGroupResponse GroupCoordinator::join(const JoinGroupRequest& req, const std:
   m.joined = true;
   g.cv.notify_all();
   const int32_t gen0 = g.generation;
+  ++m.waiting;
   while (g.generation == gen0 && !closed_) {
     bool all = true;
     for (auto& kv : g.members) all &= kv.second.joined;
     now = now_ms();
     if (all || now >= g.deadline) {
-      if (!complete_join(g)) break;
+      complete_join(g);
       break;
     }
     g.cv.wait_until(lk, at_ms(std::min(g.deadline, now + 100)));
   }
   auto it = g.members.find(id);
+  if (it != g.members.end()) --it->second.waiting;
   if (closed_ || it == g.members.end() || g.generation == gen0) {
     resp.error = closed_ ? COORDINATOR_NOT_AVAILABLE : UNKNOWN_MEMBER_ID;
     return resp;
@@ -183,6 +196,8 @@ SyncGroupResponse GroupCoordinator::sync(const SyncGroupRequest& req) {
   }
   it->second.last_seen = now_ms();
   if (req.member_id == g.leader && g.state == "CompletingRebalance") {
+    const int64_t now = now_ms();
+    for (auto& kv : g.members) kv.second.last_seen = now;  // (sessions restart with the answer)
     for (const GroupMemberMeta& a : req.assignments) {
       auto m = g.members.find(a.member_id);
       if (m != g.members.end()) m->second.assignment = a.metadata;
@@ -193,10 +208,12 @@ SyncGroupResponse GroupCoordinator::sync(const SyncGroupRequest& req) {
   }
   const int32_t gen = g.generation;
   const int64_t deadline = now_ms() + it->second.rebalance_ms;
+  ++it->second.waiting;
   while (!closed_ && g.generation == gen && !g.synced && g.state == "CompletingRebalance" &&
          now_ms() < deadline)
     g.cv.wait_until(lk, at_ms(std::min(deadline, now_ms() + 100)));
   it = g.members.find(req.member_id);
+  if (it != g.members.end()) --it->second.waiting;
   if (closed_ || it == g.members.end()) {
     resp.error = closed_ ? COORDINATOR_NOT_AVAILABLE : UNKNOWN_MEMBER_ID;
   } else if (g.generation != gen || !g.synced) {

@@ -53,6 +53,7 @@ class GroupCoordinator {
     int64_t last_seen = 0;
     int64_t order = 0;    // join order (the leader is the longest-standing member)
     bool joined = false;  // has (re)joined the rebalance in progress
+    int waiting = 0;      // requests of this member blocked in JoinGroup / SyncGroup right now
     std::string assignment;
   };
   struct Group {

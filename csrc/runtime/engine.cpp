@@ -399,6 +399,24 @@ void Engine::commit(kafka::Consumer& c, const std::vector<int>& parts) {
   }
 }
 
+// Waits until no fetched record of `parts` is still in the pipeline (or timeout_ms).
+bool Engine::drain_pending(const std::vector<int>& parts, int timeout_ms) {
+  const int64_t until = mono_ns() + (int64_t)timeout_ms * 1000000;
+  for (;;) {
+    bool empty = true;
+    {
+      std::lock_guard<std::mutex> lk(pend_mu_);
+      for (int p : parts) {
+        auto it = pending_.find(p);
+        empty &= it == pending_.end() || it->second.empty();
+      }
+    }
+    if (empty) return true;
+    if (mono_ns() >= until || stopping_) return false;
+    std::this_thread::sleep_for(std::chrono::milliseconds(2));
+  }
+}
+
 // Hands the sources a new partition set (group thread) and waits until each has taken it
 // (committed and dropped its previous partitions). false = not every source confirmed in time.
 bool Engine::distribute(const std::vector<int>& parts, int32_t generation,
@@ -461,8 +479,24 @@ void Engine::group_loop() {
         if (group_stop_) break;
         if (!gm->heartbeat()) {
           if (stopping_) continue;
-          // eager rebalance: every partition is revoked (and committed) before rejoining
-          distribute({}, gm->generation(), gm->member_id(), cfg_.rebalance_timeout_ms / 2);
+          // eager rebalance: every partition is revoked (drained and committed) before
+          // rejoining. Revocation is a barrier: until every source confirmed, keep the session
+          // alive and retry (a source that is still fetching a revoked partition would serve
+          // records the next owner serves again), within 3/4 of the rebalance timeout so this
+          // member still rejoins before the coordinator's deadline
+          const int64_t until =
+              mono_ns() + (int64_t)cfg_.rebalance_timeout_ms * 3 / 4 * 1000000;
+          bool revoked = false;
+          while (!revoked && !stopping_ && !group_stop_) {
+            const int64_t left_ms = (until - mono_ns()) / 1000000;
+            if (left_ms <= 0) break;
+            revoked = distribute({}, gm->generation(), gm->member_id(),
+                                 (int)std::min<int64_t>(left_ms, 500));
+            if (!revoked) gm->heartbeat();
+          }
+          if (!revoked && !stopping_)
+            fprintf(stderr, "[gale group] revocation not confirmed by every source within "
+                    "%d ms: rejoining anyway\n", cfg_.rebalance_timeout_ms * 3 / 4);
           assigned_partitions_ = 0;
           break;
         }
@@ -531,6 +565,9 @@ void Engine::source_loop(int idx) {
       e = ctl.epoch;
     }
     if (!parts.empty()) {
+      // revoked partitions: let their fetched records finish (bounded) so the commit covers
+      // them and the next owner does not serve them again
+      if (cfg_.group_membership) drain_pending(parts, cfg_.rebalance_timeout_ms / 4);
       commit(*cons, parts);
       std::lock_guard<std::mutex> lk(pend_mu_);
       for (int p : parts) {

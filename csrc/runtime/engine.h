@@ -182,6 +182,7 @@ class Engine {
   void group_loop();
   bool distribute(const std::vector<int>& parts, int32_t generation, const std::string& member,
                   int timeout_ms);
+  bool drain_pending(const std::vector<int>& parts, int timeout_ms);
   void decode_loop(int idx);
   void decode_fetch(FetchItem& it, std::vector<InRecord>& good, int lane);
   bool ingest_fetch(FetchItem& it, std::vector<InRecord>& good, int lane);

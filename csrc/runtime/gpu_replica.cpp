@@ -9,6 +9,7 @@
 #include <stdexcept>
 
 #include "../codec/json_codec.h"
+#include "metrics.h"
 #include "replica.h"
 
 namespace gale {
@@ -38,7 +39,9 @@ GpuReplica::GpuReplica(std::shared_ptr<Executor> exec, int H, int W, int C, int 
       check_hip(hipHostMalloc(reinterpret_cast<void**>(&s.h_text), tb, hipHostMallocMapped),
                 "hipHostMalloc(text)");
     }
-    check_hip(hipEventCreateWithFlags(&s.done, hipEventDisableTiming), "hipEventCreate");
+    check_hip(hipEventCreateWithFlags(&s.done, hipEventDisableTiming |
+                                                   (wait_poll_us_ < 0 ? hipEventBlockingSync : 0)),
+              "hipEventCreate");
     check_hip(hipEventCreateWithFlags(&s.staged, hipEventDisableTiming), "hipEventCreate");
     // initial text capacity: ~12 bytes per number (Java Float.toString + ",") x a full batch
     ensure_device(s, (size_t)mb * H * W * C * 12 + 4096);
@@ -243,19 +246,29 @@ void GpuReplica::submit(Batch& b) {
                            stream_),
             "D2H status");
   check_hip(hipEventRecord(s.done, stream_), "hipEventRecord");
+  s.t_submit_ns = mono_ns();
 }
 
 void GpuReplica::wait(Batch& b) {
   Slot& s = slots_[(size_t)b.slot];
   if (wait_poll_us_ > 0) {
     // sleep-poll: the thread sleeps while the GPU works (the engine's timer slack is set to
-    // 1 us on replica threads, so a sleep is not stretched by the default 50 us slack)
+    // 1 us on replica threads, so a sleep is not stretched by the default 50 us slack). It
+    // sleeps through most of the expected batch time at once and polls only near the end:
+    // polling every 20 us through a 0.5 ms batch cost ~0.25 core per replica (6 replicas:
+    // 1.5 of a 16-core host share, which then tipped it into CFS throttling)
+    const int64_t due = s.t_submit_ns + expect_ns_ * 85 / 100;
+    const int64_t now = mono_ns();
+    if (expect_ns_ > 0 && due - now > 2000ll * wait_poll_us_)
+      std::this_thread::sleep_for(std::chrono::nanoseconds(due - now));
     for (;;) {
       const hipError_t e = hipEventQuery(s.done);
       if (e == hipSuccess) break;
       if (e != hipErrorNotReady) check_hip(e, "hipEventQuery(batch)");
       std::this_thread::sleep_for(std::chrono::microseconds(wait_poll_us_));
     }
+    const int64_t took = mono_ns() - s.t_submit_ns;
+    expect_ns_ = expect_ns_ > 0 ? (expect_ns_ * 7 + took) / 8 : took;
   } else {
     check_hip(hipEventSynchronize(s.done), "hipEventSynchronize(batch)");
   }

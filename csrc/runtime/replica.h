@@ -94,9 +94,12 @@ class StubReplica : public Replica {
 // with device work (the executor's per-slot graphs, csrc/runtime/executor.cpp).
 class GpuReplica : public Replica {
  public:
-  // wait_poll_us > 0: wait() polls the batch's completion event and sleeps wait_poll_us between
-  // polls (the worker thread then costs ~no CPU while the GPU works); 0: hipEventSynchronize
-  // (the HIP runtime busy-waits, lowest wake-up latency, one core per waiting replica)
+  // wait_poll_us > 0: wait() first sleeps until ~85 % of the batch's expected submit -> done
+  // time (a running average of the replica's recent batches), then polls the completion event
+  // every wait_poll_us (the worker thread costs ~no CPU while the GPU works, and polls only
+  // around the expected completion); 0: hipEventSynchronize (the HIP runtime busy-waits, lowest
+  // wake-up latency, one core per waiting replica); < 0: blocking-sync completion events (the
+  // thread sleeps on the device interrupt)
   // gpu_encode: the softmax rows are also formatted as prediction text on the device
   GpuReplica(std::shared_ptr<Executor> exec, int H, int W, int C, int classes, bool use_graph,
              int wait_poll_us = 0, bool gpu_encode = false);
@@ -124,6 +127,7 @@ class GpuReplica : public Replica {
     uint8_t* h_text = nullptr;   // pinned, device-mapped prediction text slots (gpu_encode)
     hipEvent_t done = nullptr;
     hipEvent_t staged = nullptr;  // H2D of this slot's text finished (copy stream)
+    int64_t t_submit_ns = 0;
   };
   void ensure_host(Slot& s, size_t bytes);
   void ensure_device(Slot& s, size_t bytes);
@@ -137,6 +141,7 @@ class GpuReplica : public Replica {
   hipStream_t copy_stream_ = nullptr;  // H2D of batch k+1 overlaps compute of batch k
   std::vector<Slot> slots_;
   int next_slot_ = 0;
+  int64_t expect_ns_ = 0;  // running average of submit -> done (adaptive sleep-poll)
 };
 
 }  // namespace gale

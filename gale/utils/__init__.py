@@ -6,6 +6,16 @@ import os
 import socket
 
 
+def cgroup_cpu_quota() -> float:
+    """The cgroup v2 CPU bandwidth quota in CPUs (cpu.max), 0.0 when unlimited or unknown."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        return 0.0 if quota == "max" else int(quota) / int(period)
+    except (OSError, ValueError):
+        return 0.0
+
+
 def host_cpus_per_rank() -> float:
     """CPUs this rank may use: min(affinity, cgroup CPU quota) / ranks on this node.
 
@@ -76,6 +86,23 @@ def pin_to_gpu_numa(device: int, cpus_per_rank: int = 0) -> set:
 
 THREAD_GROUPS = (("gl-brk", "broker"), ("gl-src", "source"), ("gl-dec", "decode"),
                  ("gl-rep", "replica"), ("gl-sink", "sink"), ("gl-watchdog", "watchdog"))
+
+
+def thread_cpu_by_thread() -> dict:
+    """CPU seconds (user + system) per live thread of this process: {(tid, name): seconds}."""
+    tick = os.sysconf("SC_CLK_TCK")
+    out = {}
+    base = "/proc/self/task"
+    for tid in os.listdir(base):
+        try:
+            with open(f"{base}/{tid}/stat") as f:
+                st = f.read()
+        except OSError:
+            continue
+        lp, rp = st.index("("), st.rindex(")")
+        rest = st[rp + 2:].split()
+        out[(int(tid), st[lp + 1:rp])] = (int(rest[11]) + int(rest[12])) / tick
+    return out
 
 
 def thread_cpu_seconds() -> dict:

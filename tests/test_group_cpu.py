@@ -97,7 +97,9 @@ def test_two_engines_split_partitions_then_one_leaves(broker):
     out = broker.read("out", 0)
     got = [r["key"] for r in out]
     assert set(got) == keys
-    # graceful moves commit before handing partitions over: exactly once here
+    # graceful moves drain the revoked partitions' in-flight records and commit before handing
+    # them over, so each record is served once here (a member that dies, below, is only
+    # at-least-once: records it fetched after its last commit are served again)
     assert len(got) == len(keys)
 
 
@@ -237,3 +239,49 @@ def test_group_member_killed_survivors_adopt_its_partitions(tmp_path):
             if p.poll() is None:
                 p.kill()
         b.stop()
+
+
+def test_waiting_members_are_not_expired_during_a_long_join(broker):
+    """A rebalance can wait longer than a member's session timeout (a dead member with a long
+    session holds it open until the rebalance deadline). Members blocked in JoinGroup must not
+    be expired meanwhile by other requests (describe / heartbeat run the expiry): they keep
+    their member ids and join the next generation (Kafka does not expire awaiting members)."""
+    import threading
+
+    boot = f"127.0.0.1:{broker.port}"
+    mk = lambda s, cid: K.GroupMember(boot, "W", "in", session_timeout_ms=s,  # noqa: E731
+                                      rebalance_timeout_ms=3000, client_id=cid)
+    a = mk(800, "a")
+    assert a.join() == [0, 1, 2, 3]
+    d = mk(20000, "d")  # will go silent, but its session outlives the rebalance wait
+    res = {}
+    t = threading.Thread(target=lambda: res.__setitem__("d", d.join()))
+    t.start()
+    assert wait_for(lambda: broker.describe_group("W")["state"] == "PreparingRebalance", 5)
+    assert not a.heartbeat()  # rebalance in progress: rejoin
+    assert sorted(a.join() + (t.join() or res["d"])) == [0, 1, 2, 3]
+    gen = a.generation
+    id_a = a.member_id
+    # d is now silent; a newcomer n triggers a rebalance that only ends at the deadline (3 s),
+    # well past a's and n's 0.8 s sessions
+    n = mk(800, "n")
+    t_n = threading.Thread(target=lambda: res.__setitem__("n", n.join()))
+    t_n.start()
+    assert wait_for(lambda: broker.describe_group("W")["state"] == "PreparingRebalance", 5)
+    assert not a.heartbeat()
+    t_a = threading.Thread(target=lambda: res.__setitem__("a", a.join()))
+    t_a.start()
+    t0 = time.time()
+    while t_a.is_alive() and time.time() - t0 < 6:
+        broker.describe_group("W")  # runs the session expiry while a and n wait
+        time.sleep(0.1)
+    t_a.join(10)
+    t_n.join(10)
+    assert a.member_id == id_a, "a waiting member was expired and had to rejoin as a new one"
+    assert a.generation == gen + 1 and n.generation == gen + 1
+    g = broker.describe_group("W")
+    assert g["state"] == "Stable" and sorted(g["members"]) == sorted([a.member_id, n.member_id])
+    assert sorted(res["a"] + res["n"]) == [0, 1, 2, 3]
+    a.leave()
+    n.leave()
+    d.leave()

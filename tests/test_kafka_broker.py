@@ -312,3 +312,27 @@ def test_producer_backlog_leaves_in_request_sized_batches(broker):
         if len(got) >= n:
             break
     assert [r["value"][:4] for r in got] == [b"%04d" % i for i in range(n)]
+
+
+def test_producer_chunks_with_headers_fit_max_request_size():
+    """The producer cuts a backlog into batches by an upper bound of each record's encoded size
+    that includes its headers (the __TypeId__ header of --type-id-header adds ~28 bytes to a
+    ~120-byte prediction record): every batch stays within max_request_size, so a broker whose
+    message.max.bytes equals it accepts them all."""
+    cap = 16 << 10
+    b = K.Broker(max_message_bytes=cap)
+    b.start()
+    try:
+        b.create_topic("h", 1)
+        p = K.Producer(bs(b), linger_ms=300, batch_size=1 << 20, max_request_size=cap)
+        errs = []
+        n = 2000
+        for i in range(n):
+            p.send("h", b"x" * 120, partition=0, headers=[("__TypeId__", b"java.lang.String")],
+                   callback=lambda e, pa, o: errs.append(e))
+        p.flush()
+        assert len(errs) == n and set(errs) == {0}
+        assert p.stats()["requests"] >= n * 150 // cap
+        p.close()
+    finally:
+        b.stop()
