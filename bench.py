@@ -113,6 +113,10 @@ def parse_args(argv=None):
                     help="one process drives all --gpus GPUs (one engine: per-GPU locality "
                          "slots with work stealing, weights RCCL-broadcast in-process) instead "
                          "of one torch.distributed rank per GPU")
+    ap.add_argument("--locality-split", type=int, default=1,
+                    help="locality slots per GPU in this process (each with its own sources, "
+                         "batcher and pinned pool; idle slots steal and parse stolen text from "
+                         "host-pinned memory): the single-process multi-GPU dispatch on one GPU")
     ap.add_argument("--shared-gpu-rehearsal", action="store_true",
                     help="multi-rank rehearsal on a box with fewer GPUs than ranks: rank r uses "
                          "GPU r %% device_count and the process group runs over gloo (RCCL refuses "
@@ -129,6 +133,14 @@ def parse_args(argv=None):
     ap.add_argument("--all-stats", action="store_true",
                     help="add every engine statistic of rank 0 (queue / device / e2e quantiles, "
                          "lag, thread seconds) to the JSON line")
+    ap.add_argument("--latency-load", type=float, default=0.8,
+                    help="after the throughput window, offer this fraction of the measured "
+                         "throughput at a fixed rate (native open-loop producer) and report "
+                         "p50/p99 of record append -> produce ack at microsecond resolution "
+                         "(BASELINE's latency half); 0 = skip (p50 is then fetch -> ack under "
+                         "the backlog, i.e. mostly queueing)")
+    ap.add_argument("--latency-warmup-s", type=float, default=1.0)
+    ap.add_argument("--latency-s", type=float, default=2.0)
     ap.add_argument("--timeline", default="",
                     help="write a JSON line every --timeline-ms (completions, per-stage CPU, "
                          "cgroup throttling, RSS, queue depth, lag) to this file (rank 0)")
@@ -298,6 +310,35 @@ def warm_up(eng, records, a, rate_window=0.5, windows=4, tol=0.05):
             return el, last
 
 
+def latency_phase(eng, broker, feeder, bset, parts, rate_img_s, a, ipr):
+    """Record-level latency at a fixed offered load (this rank's share ``rate_img_s``): the
+    backlog top-up stops, the backlog drains, a native open-loop producer appends the same
+    synthetic batches at the offered rate and logs every append (CLOCK_MONOTONIC), the engine
+    logs every produce ack on the same clock; the join gives append -> produce-ack per record.
+    Returns (latencies_us, achieved images/s, unmatched acks)."""
+    from gale._native import native
+    from gale.metrics import append_to_ack_us
+
+    feeder.stop()
+    t_end = time.perf_counter() + 10.0
+    while time.perf_counter() < t_end:  # drain the backlog phase's records first
+        if sum(o["lag"] for o in eng.partition_offsets()) <= 2 * a.batch:
+            break
+        time.sleep(0.005)
+    rf = native().kafka.RateFeeder(broker, "gale-in", parts, bset)
+    rf.start(rate_img_s / ipr, feeder._next)
+    time.sleep(a.latency_warmup_s)
+    eng.set_ack_log(True)
+    c0, t0 = eng.completed, time.perf_counter()
+    time.sleep(a.latency_s)
+    eng.set_ack_log(False)
+    achieved = (eng.completed - c0) * ipr / (time.perf_counter() - t0)
+    rf.stop()
+    ack = eng.take_ack_log()
+    lat = append_to_ack_us(rf.take_log(), ack)
+    return lat, achieved, int(len(ack[0]) - len(lat))
+
+
 def main(argv=None) -> int:
     a = parse_args(argv)
     from gale.utils import host_cpus_per_rank, thread_cpu_seconds
@@ -431,6 +472,7 @@ def main(argv=None) -> int:
                      check_crcs=a.check_crcs,
                      output_partition=rank if a.local_output and world > 1 else -1,
                      producer_buffer_mb=a.producer_buffer_mb,
+                     locality_split=a.locality_split,
                      producer_request_kb=a.producer_request_kb)
     devices = (list(range(local_gpus)) if local_gpus > 1 else [local_rank]) if use_gpu else None
     # ONE engine: warm-up and timed window are the same steady-state pipeline (connections,
@@ -471,13 +513,6 @@ def main(argv=None) -> int:
     st = eng.stats()
     if timeline:
         timeline.stop()
-    if world > 1:
-        dist.barrier()
-    feeder.stop()
-    eng.stop()
-    if world > 1:
-        dist.barrier()  # (sinks produce to every rank's broker: stop brokers after all engines)
-    broker.stop()
     if not reached:
         raise SystemExit(f"rank {rank}: timed out after {elapsed:.1f}s "
                          f"({done_records}/{a.steps * step_records} records)")
@@ -492,12 +527,36 @@ def main(argv=None) -> int:
         elapsed_max, total_images = float(mx[0]), float(sm[1])
     else:
         elapsed_max, total_images = elapsed, float(images)
+    value = total_images / elapsed_max
+    n_gpus = world * local_gpus
+    lat_us, lat_achieved, lat_unmatched = None, 0.0, 0
+    offered = a.latency_load * value  # whole job, images/s
+    if a.latency_load > 0 and a.rate <= 0:
+        if world > 1:
+            dist.barrier()
+        lat_us, lat_achieved, lat_unmatched = latency_phase(
+            eng, broker, feeder, bset, my_parts, offered / world, a, ipr)
+        if world > 1:
+            # every rank's samples (subsampled to <= 200k) and achieved rate to rank 0
+            if len(lat_us) > 200_000:
+                lat_us = lat_us[np.random.default_rng(rank).choice(len(lat_us), 200_000,
+                                                                   replace=False)]
+            got = [None] * world
+            dist.all_gather_object(got, (lat_us, lat_achieved, lat_unmatched))
+            lat_us = np.concatenate([g[0] for g in got])
+            lat_achieved = sum(g[1] for g in got)
+            lat_unmatched = sum(g[2] for g in got)
+    if world > 1:
+        dist.barrier()
+    feeder.stop()
+    eng.stop()
+    if world > 1:
+        dist.barrier()  # (sinks produce to every rank's broker: stop brokers after all engines)
+    broker.stop()
     if rank == 0 and elapsed_max < 1.0:
         print(f"bench.py: timed window {elapsed_max:.3f} s < 1 s: raise --step-images",
               file=sys.stderr)
     if rank == 0:
-        value = total_images / elapsed_max
-        n_gpus = world * local_gpus
         # per-step rates from (time, completed) marks; a completion burst can cross several step
         # boundaries at once, so intervals shorter than half a mean step are merged with the next
         step_rates, ta, ca = [], t0, c0
@@ -527,16 +586,40 @@ def main(argv=None) -> int:
                        "images_per_record": ipr, "max_batch": a.batch,
                        "max_wait_us": a.max_wait_us, "replicas_per_gpu": a.replicas_per_gpu,
                        "decode_threads": a.decode_threads,
+                       "locality_split": a.locality_split,
                        "partitions": n_parts, "step_images_per_gpu": a.step_images,
                        "path": "kafka-fetch->gpu-json-parse->hipgraph-forward->kafka-produce"},
             "load": (f"offered {a.rate:.0f} images/s per GPU" if a.rate > 0
-                     else "backlog kept ahead of the consumers (max throughput; latency "
-                          "includes queueing)"),
+                     else "value: backlog kept ahead of the consumers (max throughput); "
+                          "latency: a second phase at a fixed offered load"),
             "timed_s": round(elapsed_max, 3),
-            "p50_latency_ms": round(st["e2e_us_p50"] / 1e3, 3),
-            "p99_latency_ms": round(st["e2e_us_p99"] / 1e3, 3),
-            "record_e2e_ms_p50": round(st["record_e2e_ms_p50"], 2),
-            "record_e2e_ms_p99": round(st["record_e2e_ms_p99"], 2),
+        }
+        if lat_us is not None and len(lat_us):
+            out.update({
+                "p50_latency_ms": round(float(np.percentile(lat_us, 50)) / 1e3, 3),
+                "p99_latency_ms": round(float(np.percentile(lat_us, 99)) / 1e3, 3),
+                "latency_definition": "Kafka record append -> prediction produce-ack, per "
+                                      "record, CLOCK_MONOTONIC (us resolution), at a fixed "
+                                      "offered load (open-loop native producer)",
+                "latency_offered_img_s": round(offered, 1),
+                "latency_achieved_img_s": round(lat_achieved, 1),
+                "latency_samples": int(len(lat_us)),
+                "latency_unmatched": lat_unmatched,
+                "p90_latency_ms": round(float(np.percentile(lat_us, 90)) / 1e3, 3),
+                "p999_latency_ms": round(float(np.percentile(lat_us, 99.9)) / 1e3, 3),
+            })
+        else:
+            out.update({
+                "p50_latency_ms": round(st["e2e_us_p50"] / 1e3, 3),
+                "p99_latency_ms": round(st["e2e_us_p99"] / 1e3, 3),
+                "latency_definition": "fetch -> produce-ack under the backlog (includes "
+                                      "queueing; no offered-load phase)",
+            })
+        out.update({
+            "backlog_fetch_to_ack_ms_p50": round(st["e2e_us_p50"] / 1e3, 3),
+            "backlog_fetch_to_ack_ms_p99": round(st["e2e_us_p99"] / 1e3, 3),
+            "backlog_record_e2e_ms_p50": round(st["record_e2e_ms_p50"], 2),
+            "backlog_record_e2e_ms_p99": round(st["record_e2e_ms_p99"], 2),
             "device_ms_p50": round(st["device_us_p50"] / 1e3, 3),
             "batch_images_mean": round(st["batch_images_mean"], 1),
             "step_rate_spread": {"min": round(min(step_rates)), "median": round(med),
@@ -550,8 +633,9 @@ def main(argv=None) -> int:
             "cpu_cores_by_stage_rank0": cores,
             "encode_s": round(t_enc, 1),
             "cpus_pinned_rank0": len(pinned_cpus),
+            "steals": int(st.get("steals", 0)),
             "warmup_records": warm_done,
-        }
+        })
         if a.all_stats:
             out["engine_stats_rank0"] = {k: round(v, 3) for k, v in st.items()}
         print(json.dumps(out), flush=True)

@@ -1,4 +1,5 @@
 // Python bindings of the serving engine (gale._C.Engine).
+#include <pybind11/numpy.h>
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
@@ -85,14 +86,14 @@ void bind_engine(py::module_& m) {
            py::arg("locality") = -1)
       .def("add_gpu_replica",
            [](Engine& e, std::shared_ptr<Executor> exec, bool use_graph, int wait_poll_us,
-              bool gpu_encode) {
+              bool gpu_encode, int locality) {
              const EngineConfig& c = e.config();
              e.add_replica(std::make_shared<GpuReplica>(std::move(exec), c.H, c.W, c.C,
                                                         c.classes, use_graph, wait_poll_us,
-                                                        gpu_encode));
+                                                        gpu_encode, locality));
            },
            py::arg("executor"), py::arg("use_graph") = true, py::arg("wait_poll_us") = 0,
-           py::arg("gpu_encode") = false)
+           py::arg("gpu_encode") = false, py::arg("locality") = -1)
       .def("enable_gpu_ingest",
            [](Engine& e, int device, int lanes, int poll_us) {
              e.set_ingest(std::make_shared<GpuIngest>(device, lanes, poll_us));
@@ -124,6 +125,22 @@ void bind_engine(py::module_& m) {
       .def_property_readonly("completed", &Engine::completed)
       .def("stats", &Engine::stats)
       .def("reset_stats", &Engine::reset_stats)
+      .def("set_ack_log", &Engine::set_ack_log, py::arg("on"),
+           py::arg("capacity") = (size_t)(8u << 20))
+      .def("take_ack_log", [](Engine& e) {
+        const std::vector<AckSample> v = e.take_ack_log();
+        py::array_t<int32_t> p(v.size());
+        py::array_t<int64_t> o(v.size()), t(v.size());
+        auto pp = p.mutable_unchecked<1>();
+        auto po = o.mutable_unchecked<1>();
+        auto pt = t.mutable_unchecked<1>();
+        for (size_t i = 0; i < v.size(); ++i) {
+          pp((py::ssize_t)i) = v[i].partition;
+          po((py::ssize_t)i) = v[i].offset;
+          pt((py::ssize_t)i) = v[i].t_ns;
+        }
+        return py::make_tuple(p, o, t);
+      })
       .def("replica_stats", [](Engine& e) {
         py::list out;
         for (const ReplicaStats& s : e.replica_stats()) {
@@ -135,6 +152,9 @@ void bind_engine(py::module_& m) {
           d["images"] = s.images;
           d["records"] = s.records;
           d["restarts"] = s.restarts;
+          d["slot"] = s.slot;
+          d["resident_records"] = s.resident_records;
+          d["host_records"] = s.host_records;
           out.append(d);
         }
         return out;

@@ -4,7 +4,11 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <time.h>
+
 #include <atomic>
+#include <chrono>
+#include <mutex>
 #include <thread>
 
 #include "../codec/json_codec.h"
@@ -104,6 +108,103 @@ struct BatchSet {
   std::vector<int32_t> records;  // records per batch
   int64_t images_per_record = 1;
   size_t bytes = 0;
+};
+
+// Open-loop producer of the benchmark's offered load: appends the batches of a BatchSet (by
+// reference) to an embedded broker's partitions at a fixed record rate, round-robin over the
+// partitions, and logs each append as (partition, base offset, records, CLOCK_MONOTONIC ns). The
+// log is the "record appended" end of the record-level latency (bench.py latency phase); the
+// engine's ack log (Engine::ack_log) is the other end - both on the same monotonic clock.
+class RateFeeder {
+ public:
+  RateFeeder(std::shared_ptr<Broker> b, std::string topic, std::vector<int> parts,
+             std::shared_ptr<BatchSet> set)
+      : b_(std::move(b)), topic_(std::move(topic)), parts_(std::move(parts)),
+        set_(std::move(set)) {
+    if (parts_.empty() || !set_ || set_->batches.empty())
+      throw std::invalid_argument("RateFeeder: no partitions or empty BatchSet");
+  }
+  ~RateFeeder() { stop(); }
+  void start(double records_per_s, int64_t start_batch) {
+    if (t_.joinable()) throw std::logic_error("RateFeeder: already running");
+    if (records_per_s <= 0) throw std::invalid_argument("RateFeeder: rate must be > 0");
+    stop_ = false;
+    next_ = start_batch;
+    t_ = std::thread([this, records_per_s] { run(records_per_s); });
+  }
+  void stop() {
+    stop_ = true;
+    if (t_.joinable()) t_.join();
+  }
+  int64_t next_batch() const { return next_; }
+  // (partition, base_offset, records, t_ns) arrays; clears the log
+  py::tuple take_log() {
+    std::vector<int32_t> p;
+    std::vector<int64_t> base, t;
+    std::vector<int32_t> n;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      p.swap(lp_);
+      base.swap(lbase_);
+      n.swap(ln_);
+      t.swap(lt_);
+    }
+    return py::make_tuple(py::array_t<int32_t>(p.size(), p.data()),
+                          py::array_t<int64_t>(base.size(), base.data()),
+                          py::array_t<int32_t>(n.size(), n.data()),
+                          py::array_t<int64_t>(t.size(), t.data()));
+  }
+  int64_t appended_records() const { return appended_; }
+
+ private:
+  static int64_t now_ns() {
+    timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (int64_t)ts.tv_sec * 1000000000ll + ts.tv_nsec;
+  }
+  void run(double rate) {
+    const int64_t t0 = now_ns();
+    const int64_t m = (int64_t)set_->batches.size();
+    size_t pi = 0;
+    int64_t sent = 0;
+    while (!stop_) {
+      const double due = (double)(now_ns() - t0) * 1e-9 * rate;
+      while (!stop_) {
+        const size_t k = (size_t)(((next_ % m) + m) % m);
+        const int32_t nrec = set_->records[k];
+        if ((double)(sent + nrec) > due) break;
+        const int part = parts_[pi++ % parts_.size()];
+        const int64_t base = b_->append_shared(topic_, part, set_->batches[k]);
+        const int64_t t = now_ns();
+        {
+          std::lock_guard<std::mutex> lk(mu_);
+          lp_.push_back(part);
+          lbase_.push_back(base);
+          ln_.push_back(nrec);
+          lt_.push_back(t);
+        }
+        sent += nrec;
+        appended_ += nrec;
+        ++next_;
+      }
+      // sleep until the next batch is due (at least 20 us: a loop that polls the clock would
+      // take a core from the pipeline under test)
+      const int32_t nrec = set_->records[(size_t)(((next_ % m) + m) % m)];
+      const double wait_s = ((double)(sent + nrec) - (double)(now_ns() - t0) * 1e-9 * rate) / rate;
+      std::this_thread::sleep_for(std::chrono::nanoseconds(
+          std::max<int64_t>(20000, (int64_t)(wait_s * 1e9))));
+    }
+  }
+  std::shared_ptr<Broker> b_;
+  std::string topic_;
+  std::vector<int> parts_;
+  std::shared_ptr<BatchSet> set_;
+  std::thread t_;
+  std::atomic<bool> stop_{true};
+  std::atomic<int64_t> next_{0}, appended_{0};
+  std::mutex mu_;
+  std::vector<int32_t> lp_, ln_;
+  std::vector<int64_t> lbase_, lt_;
 };
 
 // Encode images [N, H, W, C] as InstObj JSON records (images_per_record each, Java float text)
@@ -536,6 +637,19 @@ void bind_host(py::module_& m) {
         d["connections"] = s.connections;
         return d;
       });
+
+  py::class_<RateFeeder, std::shared_ptr<RateFeeder>>(k, "RateFeeder")
+      .def(py::init<std::shared_ptr<Broker>, std::string, std::vector<int>,
+                    std::shared_ptr<BatchSet>>(),
+           py::arg("broker"), py::arg("topic"), py::arg("partitions"), py::arg("batches"))
+      .def("start", &RateFeeder::start, py::arg("records_per_s"), py::arg("start_batch") = 0)
+      .def("stop", [](RateFeeder& f) {
+        py::gil_scoped_release nogil;
+        f.stop();
+      })
+      .def("take_log", &RateFeeder::take_log)
+      .def_property_readonly("next_batch", &RateFeeder::next_batch)
+      .def_property_readonly("appended_records", &RateFeeder::appended_records);
 
   py::class_<Producer, std::shared_ptr<Producer>>(k, "Producer")
       .def(py::init([](const std::string& bootstrap, int acks, int linger_ms, int batch_size,

@@ -90,8 +90,13 @@ gale::PlanOp op_from_dict(const py::dict& d) {
 
 }  // namespace
 
+namespace gale {
+void install_crash_handler();  // runtime/crash.cpp
+}
+
 PYBIND11_MODULE(_C, m) {
   m.doc() = "gale native library: gfx950 kernels, plan executor, host runtime";
+  gale::install_crash_handler();
 
   m.def("conv2d",
         [](py::dict desc, int batch, uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t wscale,

@@ -264,14 +264,18 @@ void Engine::start() {
   // batcher, pinned fetch pool (mirrored on its device for GPU ingest) and sources; replicas
   // serve their own slot first and steal from the most loaded other slot when idle (the
   // locality-preferring, load-aware dispatch of Storm's LoadAwareShuffleGrouping)
+  slot_key_.clear();
   slot_dev_.clear();
   for (auto& rs : replicas_) {
-    const int d = rs->rep->locality();
-    auto it = std::find(slot_dev_.begin(), slot_dev_.end(), d);
-    rs->slot = (int)(it - slot_dev_.begin());
-    if (it == slot_dev_.end()) slot_dev_.push_back(d);
+    const int key = rs->rep->locality();
+    auto it = std::find(slot_key_.begin(), slot_key_.end(), key);
+    rs->slot = (int)(it - slot_key_.begin());
+    if (it == slot_key_.end()) {
+      slot_key_.push_back(key);
+      slot_dev_.push_back(rs->rep->device() >= 0 ? rs->rep->device() : key);
+    }
   }
-  const size_t nslots = slot_dev_.size();
+  const size_t nslots = slot_key_.size();
   batchers_.clear();
   for (size_t i = 0; i < nslots; ++i)
     batchers_.push_back(std::make_unique<Batcher>(
@@ -731,7 +735,6 @@ bool Engine::ingest_fetch(FetchItem& it, std::vector<InRecord>& good, int lane) 
     if (!io.batch_ok[b])
       for (size_t i = 0; i < f.batches[b].nrec; ++i) corrupt[f.batches[b].first_rec + i] = 1;
   kafka::Producer* prod = producer_for(it.source);
-  const int dev_id = ingest->device();
   for (size_t i = 0; i < n; ++i) {
     const kafka::RecordRef& rr = f.records[i];
     InRecord r;
@@ -747,7 +750,7 @@ bool Engine::ingest_fetch(FetchItem& it, std::vector<InRecord>& good, int lane) 
     r.t_fetch_ns = it.t_fetch_ns;
     r.source = it.source;
     r.dev_value = dev + rr.value_off;
-    r.dev_device = dev_id;
+    r.dev_locality = slot_key_[(size_t)it.slot];
     ++records_in_;
     if (r.len >= 0) bytes_in_ += r.len;
     r.status = corrupt[i] ? (int)codec::BAD_ENVELOPE : io.status[i];
@@ -1130,12 +1133,33 @@ void Engine::complete_record(const InRecord& r, bool ok) {
     ++produce_failures_;
   }
   t_last_ns_ = now;
+  if (ack_log_on_.load(std::memory_order_relaxed) && ok) {
+    std::lock_guard<std::mutex> lk(ack_mu_);
+    if (ack_log_.size() < ack_cap_) ack_log_.push_back({r.partition, r.offset, now});
+  }
   const int64_t c = ++completed_;
   const int64_t target = wait_target_.load(std::memory_order_relaxed);
   if ((cfg_.max_records > 0 && c >= cfg_.max_records) || (target > 0 && c >= target)) {
     std::lock_guard<std::mutex> lk(done_mu_);
     done_cv_.notify_all();
   }
+}
+
+void Engine::set_ack_log(bool on, size_t capacity) {
+  std::lock_guard<std::mutex> lk(ack_mu_);
+  if (on) {
+    ack_log_.clear();
+    ack_cap_ = capacity;
+    ack_log_.reserve(std::min<size_t>(capacity, 4u << 20));
+  }
+  ack_log_on_ = on;
+}
+
+std::vector<AckSample> Engine::take_ack_log() {
+  std::lock_guard<std::mutex> lk(ack_mu_);
+  std::vector<AckSample> out;
+  out.swap(ack_log_);
+  return out;
 }
 
 bool Engine::wait_completed(int64_t n, int64_t timeout_ms) {
@@ -1284,6 +1308,9 @@ std::vector<ReplicaStats> Engine::replica_stats() const {
     s.images = r->images;
     s.records = r->records;
     s.restarts = r->restarts;
+    s.slot = r->slot;
+    s.resident_records = r->rep->resident_records();
+    s.host_records = r->rep->host_records();
     v.push_back(s);
   }
   return v;

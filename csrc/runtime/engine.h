@@ -110,12 +110,22 @@ struct EngineConfig {
   uint64_t seed = 0;
 };
 
+// One acknowledged output (ack log): input record (partition, offset) and the monotonic time its
+// prediction was acknowledged by the sink (CLOCK_MONOTONIC ns, the clock of mono_ns()).
+struct AckSample {
+  int32_t partition;
+  int64_t offset;
+  int64_t t_ns;
+};
+
 struct ReplicaStats {
   std::string name;
   int device = -1;
   bool alive = true;
   int64_t batches = 0, images = 0, records = 0;
   int restarts = 0;
+  int slot = 0;                                 // locality slot
+  int64_t resident_records = 0, host_records = 0;  // parsed from the slot's device mirror / host
 };
 
 // Per-partition offsets, the storm-kafka `kafkaOffset` spout metric: log end
@@ -157,6 +167,11 @@ class Engine {
   std::vector<ReplicaStats> replica_stats() const;
   std::vector<PartitionOffsets> partition_offsets() const;
   void reset_stats();
+  // Record-level latency probe: while on, every acknowledged record is logged (bounded at
+  // `capacity` samples); switching it on clears the log. The benchmark joins the log with its
+  // producer's append times for the append -> produce-ack latency at microsecond resolution.
+  void set_ack_log(bool on, size_t capacity = 8u << 20);
+  std::vector<AckSample> take_ack_log();
   const EngineConfig& config() const { return cfg_; }
 
  private:
@@ -201,6 +216,7 @@ class Engine {
   EngineConfig cfg_;
   std::vector<std::shared_ptr<ReplicaSlot>> replicas_;
   std::vector<std::unique_ptr<Batcher>> batchers_;  // one per locality slot
+  std::vector<int> slot_key_;                         // slot -> locality key of its replicas
   std::vector<int> slot_dev_;                         // slot -> replica device (-1: CPU)
   std::vector<std::unique_ptr<kafka::Producer>> producers_;
   std::vector<std::thread> sources_, workers_, decoders_;
@@ -257,6 +273,10 @@ class Engine {
   std::atomic<int64_t> ns_poll_{0}, ns_decode_{0}, ns_take_{0}, ns_submit_{0}, ns_wait_{0},
       ns_finish_{0};
   std::atomic<int64_t> t_first_ns_{0}, t_last_ns_{0};
+  std::atomic<bool> ack_log_on_{false};
+  std::mutex ack_mu_;
+  std::vector<AckSample> ack_log_;
+  size_t ack_cap_ = 0;
 };
 
 }  // namespace gale

@@ -19,9 +19,9 @@ namespace gale {
 // ---------------------------------------------------------------------------------------------
 
 GpuReplica::GpuReplica(std::shared_ptr<Executor> exec, int H, int W, int C, int classes,
-                       bool use_graph, int wait_poll_us, bool gpu_encode)
+                       bool use_graph, int wait_poll_us, bool gpu_encode, int locality)
     : exec_(std::move(exec)), H_(H), W_(W), C_(C), classes_(classes), use_graph_(use_graph),
-      wait_poll_us_(wait_poll_us), gpu_encode_(gpu_encode) {
+      wait_poll_us_(wait_poll_us), gpu_encode_(gpu_encode), locality_(locality) {
   if (exec_->input_bytes_per_image() != (long long)H * W * C * 4)
     throw std::invalid_argument("GpuReplica: executor input is not fp32 [H, W, C]");
   if (exec_->output_bytes_per_image() != (long long)classes * 4)
@@ -136,9 +136,9 @@ void GpuReplica::submit(Batch& b) {
   };
   std::vector<Span> spans;
   size_t staged = 0;
-  const int my_dev = exec_->device();
-  auto resident = [my_dev](const InRecord& r) {
-    return r.dev_value != nullptr && r.dev_device == my_dev;
+  const int my_loc = locality();
+  auto resident = [my_loc](const InRecord& r) {
+    return r.dev_value != nullptr && r.dev_locality == my_loc;
   };
   for (const InRecord& r : b.recs) {
     if (resident(r)) continue;  // already in device memory (GPU ingest): nothing to copy
@@ -207,6 +207,12 @@ void GpuReplica::submit(Batch& b) {
     img += r.images;
   }
   if (img > exec_->max_batch()) throw std::logic_error("GpuReplica: batch exceeds max_batch");
+  {
+    int64_t res = 0;
+    for (const InRecord& r : b.recs) res += resident(r) ? 1 : 0;
+    resident_ += res;
+    host_ += (int64_t)b.recs.size() - res;
+  }
   b.images = img;
   ensure_tiles(s, ntiles, nrec);
   for (int i = 0; i < nrec; ++i) {

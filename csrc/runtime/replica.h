@@ -10,6 +10,7 @@
 #pragma once
 #include <stdint.h>
 
+#include <atomic>
 #include <memory>
 #include <string>
 #include <vector>
@@ -34,9 +35,10 @@ struct InRecord {
   int32_t status = 0;            // codec::Status (scan, then device parse)
   int32_t source = 0;
   bool pinned = false;           // buf is page-locked: the GPU replica DMAs straight from it
-  // GPU ingest (ingest.h): the value's bytes are already in device memory on dev_device
+  // GPU ingest (ingest.h): the value's bytes are already in device memory, in the mirror of
+  // the fetch pool of locality slot dev_locality (its key: the device, or the split slot)
   const uint8_t* dev_value = nullptr;
-  int32_t dev_device = -1;
+  int32_t dev_locality = -1;
 };
 
 struct Batch {
@@ -66,6 +68,10 @@ class Replica {
   // Supervisor restart after submit/wait threw (its in-flight batches were already re-queued):
   // bring the replica back to an idle, usable state or throw if it cannot be.
   virtual void recover() {}
+  // records whose text this replica parsed from device memory already holding it (GPU ingest
+  // mirror of its own locality slot) vs. copied over the host link (pinned or staged)
+  virtual int64_t resident_records() const { return 0; }
+  virtual int64_t host_records() const { return 0; }
 };
 
 // CPU stub (SURVEY.md §4 "stub replica for plumbing tests on GPU-less hosts"): parses on the
@@ -101,16 +107,23 @@ class GpuReplica : public Replica {
   // wake-up latency, one core per waiting replica); < 0: blocking-sync completion events (the
   // thread sleeps on the device interrupt)
   // gpu_encode: the softmax rows are also formatted as prediction text on the device
+  // locality: the replica's locality slot key (-1 = its device). Records ingested by another
+  // slot - a steal - are not resident for this replica even on the same device: their text is
+  // DMA'd from the host-pinned fetch buffer, as it would be across GPUs (--locality-split
+  // exercises the multi-GPU dispatch on one device)
   GpuReplica(std::shared_ptr<Executor> exec, int H, int W, int C, int classes, bool use_graph,
-             int wait_poll_us = 0, bool gpu_encode = false);
+             int wait_poll_us = 0, bool gpu_encode = false, int locality = -1);
   ~GpuReplica() override;
   std::string name() const override;
   int max_images() const override { return exec_->max_batch(); }
   int depth() const override { return exec_->slots(); }
   int device() const override { return exec_->device(); }
+  int locality() const override { return locality_ >= 0 ? locality_ : exec_->device(); }
   void submit(Batch& b) override;
   void wait(Batch& b) override;
   void recover() override;
+  int64_t resident_records() const override { return resident_; }
+  int64_t host_records() const override { return host_; }
 
  private:
   struct Slot {
@@ -141,6 +154,8 @@ class GpuReplica : public Replica {
   hipStream_t copy_stream_ = nullptr;  // H2D of batch k+1 overlaps compute of batch k
   std::vector<Slot> slots_;
   int next_slot_ = 0;
+  int locality_ = -1;
+  std::atomic<int64_t> resident_{0}, host_{0};
   int64_t expect_ns_ = 0;  // running average of submit -> done (adaptive sleep-poll)
 };
 

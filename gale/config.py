@@ -65,6 +65,11 @@ class GaleConfig:
     gpus: int = 0                      # GPUs to use (0 = all visible)
     numa_pin: bool = True              # a process serving ONE GPU pins its threads to that
                                        # GPU's NUMA node (gale.utils.pin_to_gpu_numa)
+    locality_split: int = 1            # locality slots per GPU (single process): K slots on one
+                                       # device, each with its own sources, batcher, pinned
+                                       # pool + device mirror; a slot's idle replicas steal from
+                                       # the others and parse stolen text from host-pinned
+                                       # memory, as across GPUs (the multi-GPU dispatch on 1 GPU)
     # sink (R9, E7-E9)
     acks: int = 1                      # MainTopology.java:113
     sink_mode: str = "async"           # KafkaBolt async / sync / fire-and-forget
@@ -138,6 +143,8 @@ class GaleConfig:
             raise ValueError("slo_p99_ms must be >= 0")
         if self.replicas < 0 or self.gpus < 0:
             raise ValueError("replicas/gpus must be >= 0")
+        if self.locality_split < 1:
+            raise ValueError("locality_split must be >= 1")
         if not self.topology_name:
             raise ValueError("topology name is required")
         if not self.fold_bn and self.dtype == "fp8":

@@ -69,16 +69,23 @@ class Engine:
             reps = self._build_gpu_replicas(devices, params)
         devs = sorted({r.device.index or 0 for r in reps}, key=[r.device.index or 0
                                                                 for r in reps].index)
-        if len(devs) > 1 and cfg.numa_pin:
+        if (len(devs) > 1 or cfg.locality_split > 1) and cfg.numa_pin:
             # single-process multi-GPU: each GPU's replica workers and sources run on the CPUs
             # of that GPU's NUMA node (its pinned fetch buffers are first-touched there)
             d["device_cpus"] = {dev: sorted(device_cpus(dev)) for dev in devs}
         self._native = native().Engine(d)
+        per_dev: Dict[int, int] = {}
+        k = max(1, cfg.locality_split)
         for rep in reps:
+            dev = rep.device.index or 0
+            j = per_dev.get(dev, 0)
+            per_dev[dev] = j + 1
+            # --locality-split K: the device's replicas are dealt over K locality slots
+            loc = dev * k + (j % k) if k > 1 else -1
             self._native.add_gpu_replica(rep.executor, cfg.use_graph, cfg.gpu_wait_poll_us,
-                                         cfg.gpu_encode)
+                                         cfg.gpu_encode, loc)
             self.model_replicas.append(rep)
-            self.devices.append(rep.device.index or 0)
+            self.devices.append(dev)
         if cfg.gpu_ingest:
             # fetch buffers of each device's sources are mirrored on that device once and
             # parsed in place
@@ -156,3 +163,11 @@ class Engine:
 
     def reset_stats(self) -> None:
         self._native.reset_stats()
+
+    def set_ack_log(self, on: bool, capacity: int = 8 << 20) -> None:
+        """Log every acknowledged record (partition, offset, CLOCK_MONOTONIC ns) while on."""
+        self._native.set_ack_log(on, capacity)
+
+    def take_ack_log(self):
+        """(partition, offset, t_ns) numpy arrays of the ack log (and clear it)."""
+        return self._native.take_ack_log()

@@ -189,3 +189,31 @@ class MetricsServer:
     def stop(self) -> None:
         self._httpd.shutdown()
         self._httpd.server_close()
+
+
+def append_to_ack_us(append_log, ack_log):
+    """Record-level latency (microseconds) from a producer's append log and the engine's ack
+    log, both on CLOCK_MONOTONIC: ``append_log`` = (partition, base_offset, records, t_ns) per
+    appended batch (``kafka.RateFeeder.take_log``), ``ack_log`` = (partition, offset, t_ns) per
+    acknowledged output (``Engine.take_ack_log``). Each acknowledged record is matched to the
+    batch that contains its offset; records appended outside the log are skipped."""
+    import numpy as np
+
+    ap, abase, an, at = (np.asarray(x) for x in append_log)
+    kp, koff, kt = (np.asarray(x) for x in ack_log)
+    out = []
+    for p in np.unique(kp):
+        sel = ap == p
+        if not sel.any():
+            continue
+        base, n, t = abase[sel], an[sel], at[sel]
+        order = np.argsort(base)
+        base, n, t = base[order], n[order], t[order]
+        ks = kp == p
+        off, tk = koff[ks], kt[ks]
+        i = np.searchsorted(base, off, side="right") - 1
+        ok = (i >= 0)
+        i = np.clip(i, 0, len(base) - 1)
+        ok &= off < base[i] + n[i]
+        out.append((tk[ok] - t[i[ok]]) / 1e3)
+    return np.concatenate(out) if out else np.zeros(0)

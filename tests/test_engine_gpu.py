@@ -283,3 +283,52 @@ def test_gpu_engine_two_replicas_on_one_gpu_and_crash(broker):
     assert st["replicas_alive"] == 2
     vals = {r["value"] for r in out}
     assert len(vals) == 1  # identical input -> identical output on both replicas
+
+
+def test_gpu_locality_split_steals_parse_from_host_pinned():
+    """Single-process multi-GPU dispatch on one device (--locality-split 2): two locality slots,
+    each with its own source, batcher and pinned fetch pool mirrored on the GPU. All input is in
+    partition 0 (slot 0's source), so slot 1's replica is idle and steals from slot 0's queue
+    (Storm's load-aware shuffle over every replica, MainTopology.java:62). A stolen record is
+    not resident in slot 1's mirror: its text is DMA'd from the host-pinned fetch buffer, as
+    across GPUs. Every record is answered exactly once and matches the fp32 oracle by key."""
+    net = get_model("resnet20")
+    params = init_params(net, seed=0, calib_batch=16)
+    b = K.Broker()
+    b.start()
+    try:
+        b.create_topic("in", 2)
+        b.create_topic("out", 1)
+        rng = np.random.default_rng(7)
+        distinct = rng.random((48,) + net.input_shape, dtype=np.float32)
+        enc = [C.encode_instances(distinct[i:i + 1]) for i in range(len(distinct))]
+        n = 1500
+        for s in range(0, n, 50):
+            b.append("in", 0, [enc[i % len(enc)] for i in range(s, s + 50)],
+                     [f"k{i}".encode() for i in range(s, s + 50)])
+        cfg = GaleConfig(topology_name="g", input_topic="in", output_topic="out",
+                         bootstrap=f"127.0.0.1:{b.port}", start_offset="earliest",
+                         max_batch=32, max_wait_us=300, output_key="input", replicas=2,
+                         source_parallelism=2, locality_split=2, decode_threads=2)
+        eng = Engine(cfg, devices=[0], max_records=n, params=params)
+        eng.start()
+        assert eng.wait(180), eng.stats()
+        eng.stop()
+        st = eng.stats()
+        reps = eng.replica_stats()
+        out = b.read("out", 0)
+    finally:
+        b.stop()
+    assert st["locality_slots"] == 2 and st["steals"] > 0, st
+    by_slot = {r["slot"]: r for r in reps}
+    assert by_slot[1]["records"] > 0 and by_slot[1]["host_records"] == by_slot[1]["records"]
+    assert by_slot[0]["resident_records"] > 0
+    keys = [r["key"] for r in out]
+    assert len(keys) == n and len(set(keys)) == n  # no loss, no duplicate
+    ref = centered_log(forward(net, fold_params(net, params), torch.from_numpy(distinct)).numpy())
+    worst = 0.0
+    for r in out:
+        i = int(r["key"][1:]) % len(distinct)
+        got = centered_log(json.loads(r["value"])["predictions"])[0]
+        worst = max(worst, np.abs(got - ref[i]).max() / max(np.abs(ref[i]).max(), 1.0))
+    assert worst < 2e-2, worst
