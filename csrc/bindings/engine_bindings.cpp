@@ -43,6 +43,8 @@ EngineConfig config_from_dict(const py::dict& d) {
   opt(d, "rebalance_timeout_ms", c.rebalance_timeout_ms);
   opt(d, "heartbeat_interval_ms", c.heartbeat_interval_ms);
   opt(d, "assignor", c.assignor);
+  opt(d, "lag_rebalance_records", c.lag_rebalance_records);
+  opt(d, "rebalance_cooldown_ms", c.rebalance_cooldown_ms);
   opt(d, "device_cpus", c.device_cpus);
   opt(d, "sink_parallelism", c.sink_parallelism);
   opt(d, "acks", c.acks);

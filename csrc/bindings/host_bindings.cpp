@@ -449,6 +449,25 @@ void bind_host(py::module_& m) {
   });
   k.def("group_assign", &GroupMember::assign, py::arg("assignor"), py::arg("members"),
         py::arg("partitions"));
+  k.def("group_assign_load_aware", [](std::vector<std::string> members, py::dict loads, int n) {
+    // loads: member -> (capacity records/s, [owned partitions])
+    std::map<std::string, MemberLoad> m;
+    for (auto kv : loads) {
+      auto t = kv.second.cast<py::tuple>();
+      MemberLoad ml;
+      ml.capacity = t[0].cast<double>();
+      ml.owned = t[1].cast<std::vector<int32_t>>();
+      m[kv.first.cast<std::string>()] = ml;
+    }
+    return GroupMember::assign_load_aware(members, m, n);
+  }, py::arg("members"), py::arg("loads"), py::arg("partitions"));
+  k.def("member_load_roundtrip", [](double cap, std::vector<int32_t> owned) {
+    MemberLoad ml;
+    ml.capacity = cap;
+    ml.owned = owned;
+    const MemberLoad r = decode_member_load(encode_member_load(ml));
+    return py::make_tuple(r.capacity, r.owned);
+  });
   k.def("crc32c_device_tables", [] {
     std::vector<uint32_t> t(kCrcDeviceTableWords);
     crc32c_device_tables(t.data());

@@ -13,6 +13,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <cmath>
 #include <chrono>
 #include <sstream>
 
@@ -836,11 +837,98 @@ void Consumer::commit(const std::map<int, int64_t>& offsets) {
 // GroupMember
 // ---------------------------------------------------------------------------------------------
 
+std::string encode_member_load(const MemberLoad& m) {
+  Writer w;
+  w.i16(1);  // version
+  w.i64((int64_t)(m.capacity * 1000.0));  // milli-records/s
+  w.array_len((int32_t)m.owned.size());
+  for (int32_t p : m.owned) w.i32(p);
+  return w.buf;
+}
+
+MemberLoad decode_member_load(const std::string& b) {
+  MemberLoad m;
+  if (b.size() < 14) return m;
+  try {
+    Reader r(b);
+    if (r.i16() < 1) return m;
+    m.capacity = (double)r.i64() / 1000.0;
+    const int32_t n = r.i32();
+    for (int32_t i = 0; i < n && r.remaining() >= 4; ++i) m.owned.push_back(r.i32());
+  } catch (const ProtocolError&) {
+    m = MemberLoad();
+  }
+  return m;
+}
+
+std::map<std::string, std::vector<int>> GroupMember::assign_load_aware(
+    std::vector<std::string> members, const std::map<std::string, MemberLoad>& load, int n) {
+  std::sort(members.begin(), members.end());
+  std::map<std::string, std::vector<int>> out;
+  for (const auto& m : members) out[m];
+  if (members.empty() || n <= 0) return out;
+  const size_t k = members.size();
+  std::vector<double> cap(k, 0.0);
+  double known = 0;
+  int nknown = 0;
+  for (size_t i = 0; i < k; ++i) {
+    auto it = load.find(members[i]);
+    if (it != load.end() && it->second.capacity > 0) {
+      cap[i] = it->second.capacity;
+      known += cap[i];
+      ++nknown;
+    }
+  }
+  const double fill = nknown ? known / nknown : 1.0;
+  double total = 0;
+  for (double& c : cap) {
+    if (c <= 0) c = fill;
+    total += c;
+  }
+  // quotas: partitions one at a time to the member whose utilisation (partitions per unit of
+  // capacity) stays lowest after taking it (D'Hondt / Jefferson apportionment): this minimises
+  // the most loaded member's partitions / capacity, so a slow member is never rounded up past
+  // what it can serve while faster members have room (ties: the faster, then the first member)
+  std::vector<int> quota(k, 0);
+  for (int p = 0; p < n; ++p) {
+    size_t best = 0;
+    for (size_t i = 1; i < k; ++i) {
+      const double a = (quota[i] + 1) / cap[i], b = (quota[best] + 1) / cap[best];
+      if (a < b - 1e-12 || (std::abs(a - b) <= 1e-12 && cap[i] > cap[best])) best = i;
+    }
+    ++quota[best];
+  }
+  // sticky fill: current owners keep partitions up to their quota
+  std::vector<int> owner(n, -1), count(k, 0);
+  for (size_t i = 0; i < k; ++i) {
+    auto it = load.find(members[i]);
+    if (it == load.end()) continue;
+    std::vector<int32_t> own = it->second.owned;
+    std::sort(own.begin(), own.end());
+    for (int32_t p : own)
+      if (p >= 0 && p < n && owner[p] < 0 && count[i] < quota[i]) {
+        owner[p] = (int)i;
+        ++count[i];
+      }
+  }
+  for (int p = 0; p < n; ++p) {
+    if (owner[p] >= 0) continue;
+    size_t best = 0;
+    for (size_t i = 1; i < k; ++i)
+      if (quota[i] - count[i] > quota[best] - count[best]) best = i;
+    owner[p] = (int)best;
+    ++count[best];
+  }
+  for (int p = 0; p < n; ++p) out[members[(size_t)owner[p]]].push_back(p);
+  return out;
+}
+
 GroupMember::GroupMember(GroupConfig cfg) : cfg_(std::move(cfg)), cluster_(cfg_) {
   if (cfg_.group_id.empty() || cfg_.topic.empty())
     throw std::invalid_argument("GroupMember needs a group_id and a topic");
-  if (cfg_.assignor != "range" && cfg_.assignor != "roundrobin")
-    throw std::invalid_argument("assignor must be range|roundrobin");
+  if (cfg_.assignor != "range" && cfg_.assignor != "roundrobin" &&
+      cfg_.assignor != "load-aware")
+    throw std::invalid_argument("assignor must be range|roundrobin|load-aware");
   // JoinGroup blocks for up to the rebalance timeout: the socket timeout must outlast it
   ClientConfig cc = cfg_;
   cc.request_timeout_ms = std::max(cfg_.request_timeout_ms, cfg_.rebalance_timeout_ms + 5000);
@@ -884,6 +972,7 @@ std::vector<int> GroupMember::join() {
     jr.member_id = member_id_;
     ConsumerSubscription sub;
     sub.topics = {cfg_.topic};
+    sub.user_data = user_data_;
     jr.protocols.push_back({cfg_.assignor, encode_subscription(sub)});
     Writer w;
     encode_join_group_request(w, jr);
@@ -914,14 +1003,18 @@ std::vector<int> GroupMember::join() {
     sr.member_id = member_id_;
     if (leader_) {
       std::vector<std::string> subscribed;
+      std::map<std::string, MemberLoad> loads;
       for (const GroupMemberMeta& m : resp.members) {
         const ConsumerSubscription s = decode_subscription(m.metadata);
-        if (std::find(s.topics.begin(), s.topics.end(), cfg_.topic) != s.topics.end())
+        if (std::find(s.topics.begin(), s.topics.end(), cfg_.topic) != s.topics.end()) {
           subscribed.push_back(m.member_id);
+          loads[m.member_id] = decode_member_load(s.user_data);
+        }
       }
       cluster_.invalidate();  // the partition count may have grown
       const int n = std::max(0, cluster_.partitions(cfg_.topic));
-      for (auto& kv : assign(resp.protocol, subscribed, n)) {
+      for (auto& kv : resp.protocol == "load-aware" ? assign_load_aware(subscribed, loads, n)
+                                                    : assign(resp.protocol, subscribed, n)) {
         ConsumerAssignment a;
         a.partitions.push_back({cfg_.topic, std::vector<int32_t>(kv.second.begin(),
                                                                  kv.second.end())});

@@ -255,8 +255,18 @@ struct GroupConfig : ClientConfig {
   std::string topic;
   int session_timeout_ms = 6000;
   int rebalance_timeout_ms = 8000;
-  std::string assignor = "range";  // range | roundrobin
+  std::string assignor = "range";  // range | roundrobin | load-aware
 };
+
+// What a member tells the leader in its subscription's user_data under the load-aware assignor:
+// its measured serving capacity (records/s; <= 0 = not measured yet) and the partitions it owns
+// now (the assignment keeps them where the quotas allow, like Kafka's sticky assignor).
+struct MemberLoad {
+  double capacity = 0;
+  std::vector<int32_t> owned;
+};
+std::string encode_member_load(const MemberLoad& m);
+MemberLoad decode_member_load(const std::string& b);  // empty/garbled -> capacity 0
 
 class GroupMember {
  public:
@@ -275,11 +285,21 @@ class GroupMember {
   // The assignors, exposed for tests: member -> partitions of one topic with n partitions
   static std::map<std::string, std::vector<int>> assign(const std::string& assignor,
                                                         std::vector<std::string> members, int n);
+  // Load-aware assignor (Storm's LoadAwareShuffleGrouping at partition granularity): quotas
+  // proportional to the members' capacities c_i, apportioned so the largest partitions / c_i
+  // is minimal (members that have not measured a capacity count as the mean of those that
+  // have), filled first from the partitions each member owns now, then from the unowned ones.
+  // A member whose capacity is far below the others' can get zero partitions.
+  static std::map<std::string, std::vector<int>> assign_load_aware(
+      std::vector<std::string> members, const std::map<std::string, MemberLoad>& load, int n);
+  // user_data sent with the next JoinGroup (load-aware: encode_member_load)
+  void set_user_data(std::string d) { user_data_ = std::move(d); }
 
  private:
   GroupConfig cfg_;
   Cluster cluster_;
   std::string member_id_;
+  std::string user_data_;
   int32_t generation_ = -1;
   bool leader_ = false;
 };

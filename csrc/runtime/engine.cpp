@@ -138,6 +138,8 @@ struct Engine::ReplicaSlot {
   std::mutex mu;  // inflight
   std::deque<std::shared_ptr<Batch>> inflight;
   std::atomic<int64_t> batches{0}, images{0}, records{0};
+  // time with at least one batch in flight (the load-aware assignor's capacity estimate)
+  std::atomic<int64_t> busy_ns{0}, busy_since{0};
 };
 
 // ---------------------------------------------------------------------------------------------
@@ -403,6 +405,16 @@ void Engine::commit(kafka::Consumer& c, const std::vector<int>& parts) {
   }
 }
 
+int64_t Engine::replica_busy_ns() const {
+  const int64_t now = mono_ns();
+  int64_t t = 0;
+  for (const auto& rs : replicas_) {
+    const int64_t since = rs->busy_since.load();
+    t += rs->busy_ns.load() + (since ? now - since : 0);
+  }
+  return t;
+}
+
 // Waits until no fetched record of `parts` is still in the pipeline (or timeout_ms).
 bool Engine::drain_pending(const std::vector<int>& parts, int timeout_ms) {
   const int64_t until = mono_ns() + (int64_t)timeout_ms * 1000000;
@@ -460,6 +472,33 @@ void Engine::group_loop() {
   gc.rebalance_timeout_ms = cfg_.rebalance_timeout_ms;
   gc.assignor = cfg_.assignor;
   std::unique_ptr<kafka::GroupMember> gm;
+  const bool load_aware = cfg_.assignor == "load-aware";
+  const int64_t lag_bound =
+      cfg_.lag_rebalance_records > 0
+          ? cfg_.lag_rebalance_records
+          : 8ll * cfg_.max_batch * std::max<int64_t>(1, (int64_t)replicas_.size());
+  std::vector<int> owned;
+  int64_t s_batches = batches_total_, s_busy = replica_busy_ns(), s_t = mono_ns();
+  int64_t last_join = 0, over_since = 0, lag_at_over = 0;
+  // capacity (images/s): full micro-batches per second of replica busy time, i.e. replicas x
+  // max_batch / (busy time per batch), smoothed over heartbeats; only windows in which the
+  // replicas were busy >= 10 % of the time count. A saturated member runs full batches, so its
+  // estimate is what it serves; a lightly loaded one runs partial batches and is credited with
+  // what full ones would carry (an upper bound - it has headroom)
+  auto sample_capacity = [&] {
+    const int64_t t = mono_ns(), nb = batches_total_, busy = replica_busy_ns();
+    const double dt = (double)(t - s_t), nrep = (double)std::max<size_t>(1, replicas_.size());
+    const double dbusy = (double)(busy - s_busy);
+    if (dt > 0 && dbusy >= 0.1 * dt * nrep && nb > s_batches) {
+      const double per_batch_s = dbusy * 1e-9 / (double)(nb - s_batches);
+      const double inst = nrep * (double)cfg_.max_batch / per_batch_s;
+      const double c = capacity_rps_.load();
+      capacity_rps_ = c > 0 ? 0.7 * c + 0.3 * inst : inst;
+    }
+    s_t = t;
+    s_batches = nb;
+    s_busy = busy;
+  };
   while (!group_stop_) {
     try {
       if (!gm) gm = std::make_unique<kafka::GroupMember>(gc);
@@ -468,7 +507,17 @@ void Engine::group_loop() {
         std::this_thread::sleep_for(std::chrono::milliseconds(cfg_.heartbeat_interval_ms));
         continue;
       }
+      if (load_aware) {
+        sample_capacity();
+        kafka::MemberLoad ml;
+        ml.capacity = capacity_rps_.load();
+        ml.owned.assign(owned.begin(), owned.end());
+        gm->set_user_data(kafka::encode_member_load(ml));
+      }
       const std::vector<int> mine = gm->join();
+      owned = mine;
+      last_join = mono_ns();
+      over_since = 0;
       distribute(mine, gm->generation(), gm->member_id(), cfg_.rebalance_timeout_ms);
       generation_ = gm->generation();
       assigned_partitions_ = (int)mine.size();
@@ -481,7 +530,30 @@ void Engine::group_loop() {
         while (!group_stop_ && !stopping_ && mono_ns() < next)
           std::this_thread::sleep_for(std::chrono::milliseconds(5));
         if (group_stop_) break;
-        if (!gm->heartbeat()) {
+        bool rejoin = false;
+        if (load_aware && !stopping_) {
+          // lag-triggered rebalance: this member cannot keep up with its partitions
+          sample_capacity();
+          int64_t lag = 0;
+          for (const PartitionOffsets& o : partition_offsets()) lag += o.lag;
+          const int64_t now = mono_ns();
+          if (lag > lag_bound) {
+            if (!over_since) {
+              over_since = now;
+              lag_at_over = lag;
+            } else if (now - over_since >= 1000000000ll && lag > lag_at_over &&
+                       now - last_join >= (int64_t)cfg_.rebalance_cooldown_ms * 1000000) {
+              fprintf(stderr, "[gale group] lag %lld > %lld and growing (capacity %.0f "
+                      "images/s): triggering a load-aware rebalance\n", (long long)lag,
+                      (long long)lag_bound, capacity_rps_.load());
+              ++lag_rebalances_;
+              rejoin = true;
+            }
+          } else {
+            over_since = 0;
+          }
+        }
+        if (rejoin || !gm->heartbeat()) {
           if (stopping_) continue;
           // eager rebalance: every partition is revoked (drained and committed) before
           // rejoining. Revocation is a barrier: until every source confirmed, keep the session
@@ -956,6 +1028,7 @@ void Engine::serve(ReplicaSlot* rs) {
           std::lock_guard<std::mutex> lk(rs->mu);
           rs->inflight.push_back(b);
         }
+        if (mine.empty()) rs->busy_since = b->t_submit_ns;  // (submit may do the work)
         try {
           if (crash_at_batch_ > 0 && nb == crash_at_batch_)
             throw std::runtime_error("injected replica crash (fault replica_crash@" +
@@ -995,7 +1068,12 @@ void Engine::serve(ReplicaSlot* rs) {
       trace::Range tr("gale:encode+produce");
       finish_batch(rs, *f);
     }
-    ns_finish_ += mono_ns() - f->t_done_ns;
+    const int64_t t_fin = mono_ns();
+    ns_finish_ += t_fin - f->t_done_ns;
+    if (mine.empty()) {
+      const int64_t since = rs->busy_since.exchange(0);
+      if (since) rs->busy_ns += t_fin - since;
+    }
   }
 }
 
@@ -1280,6 +1358,8 @@ std::map<std::string, double> Engine::stats() const {
   for (auto& r : replicas_) alive += r->alive ? 1 : 0;
   s["replicas_alive"] = alive;
   s["rebalances"] = (double)rebalances_;
+  s["lag_rebalances"] = (double)lag_rebalances_;
+  s["capacity_rps"] = capacity_rps_.load();
   s["generation"] = (double)generation_;
   s["assigned_partitions"] = cfg_.group_membership ? (double)assigned_partitions_
                                                    : (double)partition_offsets().size();

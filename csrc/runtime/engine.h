@@ -69,7 +69,13 @@ struct EngineConfig {
   int session_timeout_ms = 6000;
   int rebalance_timeout_ms = 8000;
   int heartbeat_interval_ms = 500;
-  std::string assignor = "range";  // range | roundrobin
+  std::string assignor = "range";  // range | roundrobin | load-aware
+  // load-aware assignor: every member reports its serving capacity (full micro-batches per busy
+  // replica second, in images/s) and owned partitions in JoinGroup; a member whose own lag stays above
+  // lag_rebalance_records and keeps growing for a second triggers a rebalance (at most once
+  // per rebalance_cooldown_ms), so a slow GPU sheds partitions to faster ones
+  int lag_rebalance_records = 0;   // 0 = 8 x max_batch x replicas
+  int rebalance_cooldown_ms = 10000;
   // NUMA placement: device -> CPUs for the threads serving it (replica workers, the sources of
   // its locality slot); empty = no pinning
   std::map<int, std::vector<int>> device_cpus;
@@ -272,6 +278,9 @@ class Engine {
   // thread time per pipeline stage (summed over threads): where the host spends its cycles
   std::atomic<int64_t> ns_poll_{0}, ns_decode_{0}, ns_take_{0}, ns_submit_{0}, ns_wait_{0},
       ns_finish_{0};
+  int64_t replica_busy_ns() const;  // summed over replicas, up to now
+  std::atomic<double> capacity_rps_{0.0};   // load-aware: measured capacity (images/s)
+  std::atomic<int64_t> lag_rebalances_{0};  // rebalances this member triggered on its lag
   std::atomic<int64_t> t_first_ns_{0}, t_last_ns_{0};
   std::atomic<bool> ack_log_on_{false};
   std::mutex ack_mu_;

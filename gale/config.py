@@ -23,7 +23,7 @@ CHOICES = {
     "value_format": ("json", "json-string"),
     "on_error": ("null", "error-json", "drop"),
     "output_key": ("none", "input"),
-    "assignor": ("range", "roundrobin"),
+    "assignor": ("range", "roundrobin", "load-aware"),
     # compute dtype of the GPU kernels (MFMA bf16 / OCP e4m3 fp8 serving plans; fp32 = the
     # reference-precision plan on the fp32 matrix core, every tensor binary32 like the
     # reference's TF graph, InferenceBolt.java:80-86); inputs and the softmax output are fp32
@@ -52,7 +52,12 @@ class GaleConfig:
     session_timeout_ms: int = 6000
     rebalance_timeout_ms: int = 8000
     heartbeat_interval_ms: int = 500
-    assignor: str = "range"
+    assignor: str = "range"            # range | roundrobin | load-aware (capacity-weighted,
+                                       # sticky; a member lagging behind triggers a rebalance)
+    lag_rebalance_records: int = 0     # load-aware trigger: own lag above this and growing for
+                                       # 1 s (0 = 8 x max_batch x replicas)
+    rebalance_cooldown_ms: int = 10000  # load-aware: at most one lag-triggered rebalance per
+                                        # cooldown
     decode_threads: int = 2            # CRC32C + envelope-scan workers behind each consumer
     check_crcs: bool = True            # Kafka consumer check.crcs
     gpu_ingest: bool = True            # CRC32C + image counts of pinned fetch buffers on the GPU
@@ -166,6 +171,8 @@ class GaleConfig:
             group_membership=self.group_membership, session_timeout_ms=self.session_timeout_ms,
             rebalance_timeout_ms=self.rebalance_timeout_ms,
             heartbeat_interval_ms=self.heartbeat_interval_ms, assignor=self.assignor,
+            lag_rebalance_records=self.lag_rebalance_records,
+            rebalance_cooldown_ms=self.rebalance_cooldown_ms,
             decode_threads=self.decode_threads, check_crcs=self.check_crcs,
             acks=self.acks, sink_mode=self.sink_mode, linger_ms=self.linger_ms,
             value_format=self.value_format, type_id_header=self.type_id_header,

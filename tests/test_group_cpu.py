@@ -34,6 +34,26 @@ def test_assignors():
     assert K.group_assign("range", ["a", "b", "c"], 2) == {"a": [0], "b": [1], "c": []}
 
 
+def test_load_aware_assignor_quotas_and_stickiness():
+    la = K.group_assign_load_aware
+    # capacities 3470 / 3470 / 990 records/s over 12 equal partitions: the slow member gets 1
+    # (utilisation 50 %), not the 2 proportional rounding would give it (101 %)
+    got = la(["a", "b", "c"], {"a": (3470.0, [0, 1, 2, 3]), "b": (3470.0, [4, 5, 6, 7]),
+                               "c": (990.0, [8, 9, 10, 11])}, 12)
+    assert sorted(len(v) for v in got.values()) == [1, 5, 6]
+    assert got["c"] == [8]  # sticky: kept one of its own
+    assert set(got["a"]) >= {0, 1, 2, 3} and set(got["b"]) >= {4, 5, 6, 7}
+    assert sorted(sum(got.values(), [])) == list(range(12))
+    # unmeasured members count as the mean of the measured ones; none measured: even split
+    assert sorted(len(v) for v in la(["a", "b", "c"], {}, 7).values()) == [2, 2, 3]
+    got = la(["a", "b", "c"], {"a": (1000.0, []), "b": (0.0, []), "c": (3000.0, [])}, 12)
+    assert len(got["b"]) == len(got["a"]) + 1 or len(got["b"]) == len(got["a"]) + 2
+    # a member far slower than the rest may get nothing
+    assert la(["a", "b"], {"a": (100.0, []), "b": (1.0, [0, 1])}, 4) == {"a": [0, 1, 2, 3],
+                                                                       "b": []}
+    assert K.member_load_roundtrip(1234.5, [3, 1]) == (1234.5, [3, 1])
+
+
 @pytest.fixture()
 def broker():
     b = K.Broker()
@@ -285,3 +305,74 @@ def test_waiting_members_are_not_expired_during_a_long_join(broker):
     a.leave()
     n.leave()
     d.leave()
+
+
+def _load_run(tmp, assignor, seconds=11.0, rate=6000.0):
+    """Three serving processes in one consumer group over 12 input partitions, stub replicas of
+    capacity ~4000 / ~4000 / ~1000 records/s (one 4x slower), an open-loop producer offering
+    6000 records/s spread evenly over the partitions. Returns each process's metric lines."""
+    b = K.Broker()
+    b.start()
+    procs = {}
+    try:
+        b.create_topic("in", 12)
+        b.create_topic("out", 1)
+        imgs = np.random.default_rng(9).random((64, 28, 28, 1), dtype=np.float32)
+        bset = K.synthetic_batches(imgs, 1, 8, 2)
+        extra = ["--group-membership", "--group-id", "L", "--session-timeout-ms", "3000",
+                 "--heartbeat-interval-ms", "100", "--rebalance-timeout-ms", "3000",
+                 "--assignor", assignor, "--rebalance-cooldown-ms", "2000", "--model", "lenet5",
+                 "--stub-null", "--replicas", "1", "--duration", str(seconds + 8),
+                 "--start-offset", "latest"]
+        for name, delay in (("F1", 4000), ("F2", 4000), ("S", 16000)):
+            procs[name] = _cli(name, b.port, tmp, extra + ["--stub-delay-us", str(delay)])
+        assert wait_for(lambda: len(b.describe_group("L")["members"]) == 3
+                        and b.describe_group("L")["state"] == "Stable", 60)
+        time.sleep(1.0)
+        feeder = K.RateFeeder(b, "in", list(range(12)), bset)
+        feeder.start(rate)
+        time.sleep(seconds)
+        feeder.stop()
+        for p in procs.values():
+            p.wait(60)
+        lines = {}
+        for name in procs:
+            lines[name] = [json.loads(x) for x in open(tmp / f"{name}.jsonl") if x.strip()]
+        return lines
+    finally:
+        for p in procs.values():
+            if p.poll() is None:
+                p.kill()
+        b.stop()
+
+
+def _at(lines, t):
+    """The last metrics line at or before time t (seconds since the first line)."""
+    t0 = lines[0]["ts"]
+    best = lines[0]
+    for ln in lines:
+        if ln["ts"] - t0 <= t:
+            best = ln
+    return best
+
+
+def test_load_aware_assignment_sheds_a_slow_members_partitions(tmp_path):
+    """Storm's load-aware shuffle (MainTopology.java:62,66) at Kafka-partition granularity: the
+    slow member's lag grows past the bound, it rejoins, the leader weights the partitions by
+    the members' measured capacities, and the slow member keeps only what it can serve; the
+    group's lag stays bounded. The control run with the static range assignor shows the slow
+    member's lag growing without bound."""
+    aware = _load_run(tmp_path / "aware", "load-aware") if (tmp_path / "aware").mkdir() is None \
+        else None
+    ctrl = _load_run(tmp_path / "ctrl", "range") if (tmp_path / "ctrl").mkdir() is None else None
+    s_end = aware["S"][-2]  # (the very last line is written after the engine drained)
+    assert aware["S"][-1]["lag_rebalances"] >= 1, aware["S"][-1]
+    assert len(s_end["partitions"]) == 1, s_end  # 500 records/s offered vs ~1000 capacity
+    fast_parts = sum(len(aware[n][-2]["partitions"]) for n in ("F1", "F2"))
+    assert fast_parts >= 10
+    total_lag_aware = sum(aware[n][-2]["lag_records"] for n in aware)
+    ctrl_s = ctrl["S"][-2]
+    assert len(ctrl_s["partitions"]) == 4
+    # static: the slow member falls behind by ~1000 records/s; load-aware: the group keeps up
+    assert ctrl_s["lag_records"] > 5000, ctrl_s
+    assert total_lag_aware < ctrl_s["lag_records"] / 3, (total_lag_aware, ctrl_s)
