@@ -99,12 +99,13 @@ def parse_args(argv=None):
                          "sendfile analogue) instead of writev copies")
     ap.add_argument("--numa-pin", action=argparse.BooleanOptionalAction, default=True,
                     help="pin the host pipeline's threads to the GPU's NUMA node")
-    ap.add_argument("--cpus-per-rank", type=int, default=-1,
+    ap.add_argument("--cpus-per-rank", type=int, default=0,
                     help="with --numa-pin: only this rank's slice of the node's CPUs (0 = the "
-                         "whole NUMA node; -1 = the rank's cgroup CPU quota when one is set, "
-                         "so the pipeline is scheduled on as many CPUs as it may use instead of "
-                         "being frozen by CFS bandwidth throttling whenever its threads burst "
-                         "above the quota)")
+                         "whole NUMA node; -1 = as many CPUs as the rank's cgroup CPU quota). "
+                         "Measured on a 16-CPU-quota box: the quota-sized slice (CPUs 0-15) ran "
+                         "at 0.69-0.81 M img/s against 1.49 M on the whole node, with the "
+                         "consumer's loopback receive costing 2.3x the cores "
+                         "(profiles/r3_pinning_ab.txt); the default stays the whole node")
     ap.add_argument("--gpu-wait-poll-us", type=int, default=20,
                     help="replica workers sleep-poll batch completion every N us (0 = spin)")
     ap.add_argument("--encode-threads", type=int, default=0,
@@ -140,6 +141,8 @@ def parse_args(argv=None):
                          "(BASELINE's latency half); 0 = skip (p50 is then fetch -> ack under "
                          "the backlog, i.e. mostly queueing)")
     ap.add_argument("--latency-warmup-s", type=float, default=1.0)
+    ap.add_argument("--fetch-min-bytes", type=int, default=1,
+                    help="consumer fetch.min.bytes (Kafka default 1)")
     ap.add_argument("--latency-s", type=float, default=2.0)
     ap.add_argument("--timeline", default="",
                     help="write a JSON line every --timeline-ms (completions, per-stage CPU, "
@@ -188,6 +191,9 @@ class Timeline:
         self._t.start()
 
     def _run(self):
+        from gale.utils import name_this_thread
+
+        name_this_thread("py-timeline")
         t0 = time.perf_counter()
         prev_t, prev_c, prev_cpu, prev_cg = t0, self.engine.completed, self.cpu(), _cgroup_cpu_stat()
         prev_b = self.broker.stats() if self.broker is not None else None
@@ -213,7 +219,8 @@ class Timeline:
             other = {}
             for k, v in th.items():
                 if not k[1].startswith(groups):
-                    other[k[1]] = other.get(k[1], 0.0) + v - prev_th.get(k, 0.0)
+                    name = f"{k[1]}:{k[0]}"
+                    other[name] = other.get(name, 0.0) + v - prev_th.get(k, 0.0)
             row["other_top"] = {k: round(v / dt, 2) for k, v in
                                 sorted(other.items(), key=lambda kv: -kv[1])[:4] if v > 0}
             prev_th = th
@@ -247,6 +254,7 @@ class Feeder:
         self._next = 0
         self._stop = threading.Event()
         self._t = threading.Thread(target=self._run, name="feeder", daemon=True)
+        self.native_tid = None
 
     def fill(self, records_per_partition):
         for p in self.parts:
@@ -255,6 +263,9 @@ class Feeder:
             self._next += n
 
     def _run(self):
+        from gale.utils import name_this_thread
+
+        name_this_thread("py-feeder")
         if self.rate > 0:
             t0, sent, i = time.perf_counter(), 0, 0
             while not self._stop.is_set():
@@ -472,7 +483,7 @@ def main(argv=None) -> int:
                      check_crcs=a.check_crcs,
                      output_partition=rank if a.local_output and world > 1 else -1,
                      producer_buffer_mb=a.producer_buffer_mb,
-                     locality_split=a.locality_split,
+                     locality_split=a.locality_split, fetch_min_bytes=a.fetch_min_bytes,
                      producer_request_kb=a.producer_request_kb)
     devices = (list(range(local_gpus)) if local_gpus > 1 else [local_rank]) if use_gpu else None
     # ONE engine: warm-up and timed window are the same steady-state pipeline (connections,
@@ -512,7 +523,7 @@ def main(argv=None) -> int:
     done_records = eng.completed - c0
     st = eng.stats()
     if timeline:
-        timeline.stop()
+        timeline.phase = "latency"
     if not reached:
         raise SystemExit(f"rank {rank}: timed out after {elapsed:.1f}s "
                          f"({done_records}/{a.steps * step_records} records)")
@@ -546,6 +557,8 @@ def main(argv=None) -> int:
             lat_us = np.concatenate([g[0] for g in got])
             lat_achieved = sum(g[1] for g in got)
             lat_unmatched = sum(g[2] for g in got)
+    if timeline:
+        timeline.stop()
     if world > 1:
         dist.barrier()
     feeder.stop()

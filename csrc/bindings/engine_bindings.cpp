@@ -32,6 +32,7 @@ EngineConfig config_from_dict(const py::dict& d) {
   opt(d, "source_parallelism", c.source_parallelism);
   opt(d, "start_offset", c.start_offset);
   opt(d, "fetch_max_wait_ms", c.fetch_max_wait_ms);
+  opt(d, "fetch_min_bytes", c.fetch_min_bytes);
   opt(d, "fetch_max_bytes", c.fetch_max_bytes);
   opt(d, "partition_max_bytes", c.partition_max_bytes);
   opt(d, "check_crcs", c.check_crcs);

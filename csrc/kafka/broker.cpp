@@ -192,19 +192,36 @@ void Broker::stop() {
     std::lock_guard<std::mutex> lk(conn_mu_);
     for (int fd : conn_fds_) shutdown(fd, SHUT_RDWR);  // unblocks recv()/writev()
   }
-  wake();
+  wake_all();
   for (auto& t : conn_threads_) t.join();
   conn_threads_.clear();
   conn_fds_.clear();
 }
 
-// Signals new data to long-polling fetches.
-void Broker::wake() {
-  {
-    std::lock_guard<std::mutex> lk(append_mu_);
-    ++append_seq_;
+// Signals new data on (topic, partition) to the long-polling fetches waiting on it.
+void Broker::wake(const std::string& topic, int partition) {
+  std::lock_guard<std::mutex> lk(append_mu_);
+  auto it = waiters_.find({topic, partition});
+  if (it == waiters_.end()) return;
+  for (Waiter* w : it->second) {
+    {
+      std::lock_guard<std::mutex> wl(w->m);
+      w->flag = true;
+    }
+    w->cv.notify_one();
   }
-  append_cv_.notify_all();
+}
+
+void Broker::wake_all() {
+  std::lock_guard<std::mutex> lk(append_mu_);
+  for (auto& kv : waiters_)
+    for (Waiter* w : kv.second) {
+      {
+        std::lock_guard<std::mutex> wl(w->m);
+        w->flag = true;
+      }
+      w->cv.notify_one();
+    }
 }
 
 bool Broker::create_topic(const std::string& topic, int partitions) {
@@ -299,7 +316,7 @@ int64_t Broker::append(const std::string& topic, int partition, const std::vecto
     if (!log) throw std::invalid_argument("unknown topic/partition " + topic);
     base = append_locked(*log, std::move(bytes), bi);
   }
-  wake();
+  wake(topic, partition);
   return base;
 }
 
@@ -314,7 +331,7 @@ int64_t Broker::append_shared(const std::string& topic, int partition,
     if (!log) throw std::invalid_argument("unknown topic/partition " + topic);
     base = append_locked(*log, std::move(batch), bi);
   }
-  wake();
+  wake(topic, partition);
   return base;
 }
 
@@ -412,7 +429,8 @@ bool read_exact(int fd, char* p, size_t n) {
 }  // namespace
 
 // One thread per client connection: blocking reads, requests answered in order, long-poll
-// Fetch waits on append_cv_ (so concurrent consumers are served by concurrent threads).
+// Fetch waits on its partitions' appends (so concurrent consumers are served by concurrent
+// threads).
 void Broker::serve(int fd) {
   Conn c;
   c.fd = fd;
@@ -438,19 +456,36 @@ void Broker::serve(int fd) {
     }
     if (!ok) break;
     if (c.parked) {
-      uint64_t seq;
+      // register on every requested partition before the first attempt, so an append between
+      // an attempt and the wait sets the flag and is not missed
+      Waiter w;
+      std::vector<std::pair<std::string, int>> keys;
+      for (const FetchTopic& t : c.fetch.topics)
+        for (const FetchPartition& fp : t.partitions) keys.emplace_back(t.name, fp.index);
       {
         std::lock_guard<std::mutex> lk(append_mu_);
-        seq = append_seq_;
+        for (auto& k : keys) waiters_[k].push_back(&w);
       }
       bool final_attempt = c.fetch.max_wait_ms <= 0;
-      while (!try_fetch(c, final_attempt)) {
-        std::unique_lock<std::mutex> lk(append_mu_);
-        append_cv_.wait_until(
-            lk, std::chrono::steady_clock::time_point(std::chrono::milliseconds(c.deadline)),
-            [&] { return append_seq_ != seq || !running_; });
-        seq = append_seq_;
+      for (;;) {
+        {
+          std::lock_guard<std::mutex> wl(w.m);
+          w.flag = false;
+        }
+        if (try_fetch(c, final_attempt)) break;
+        std::unique_lock<std::mutex> wl(w.m);
+        w.cv.wait_until(
+            wl, std::chrono::steady_clock::time_point(std::chrono::milliseconds(c.deadline)),
+            [&] { return w.flag || !running_; });
         final_attempt = now_ms() >= c.deadline || !running_;
+      }
+      std::lock_guard<std::mutex> lk(append_mu_);
+      for (auto& k : keys) {
+        auto it = waiters_.find(k);
+        if (it == waiters_.end()) continue;
+        auto& v = it->second;
+        v.erase(std::remove(v.begin(), v.end(), &w), v.end());
+        if (v.empty()) waiters_.erase(it);
       }
     }
     if (!flush(c)) break;
@@ -703,7 +738,8 @@ bool Broker::handle_request(Conn& c, const uint8_t* p, size_t n) {
           resp.topics.push_back(std::move(tr));
         }
       }
-      wake();
+      for (const ProduceTopic& t : req.topics)
+        for (const ProducePartition& pp : t.partitions) wake(t.name, pp.index);
       if (req.acks == 0) return true;  // Kafka sends no response for acks=0
       encode_produce_response(w, resp);
       break;

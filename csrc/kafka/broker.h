@@ -123,7 +123,8 @@ class Broker {
 
   void accept_loop();
   void serve(int fd);
-  void wake();
+  void wake(const std::string& topic, int partition);
+  void wake_all();
   bool handle_request(Conn& c, const uint8_t* p, size_t n);
   bool try_fetch(Conn& c, bool final_attempt);
   bool flush(Conn& c);
@@ -143,9 +144,16 @@ class Broker {
   std::vector<std::thread> conn_threads_;
   std::deque<std::pair<int64_t, std::shared_ptr<const std::string>>> spliced_grave_;
   std::vector<int> conn_fds_;
-  std::mutex append_mu_;  // long-poll wakeups
-  std::condition_variable append_cv_;
-  uint64_t append_seq_ = 0;
+  // long-poll wakeups: a parked Fetch registers a waiter on each partition it asks for; an
+  // append to a partition wakes only the fetches waiting on it (a wake-everyone scheme woke
+  // every consumer connection per appended batch: 12 x ~19k wakeups/s at 1.2 M img/s offered)
+  struct Waiter {
+    std::mutex m;
+    std::condition_variable cv;
+    bool flag = false;
+  };
+  std::mutex append_mu_;  // waiters_
+  std::map<std::pair<std::string, int>, std::vector<Waiter*>> waiters_;
   std::atomic<bool> running_{false};
   mutable std::mutex mu_;  // topics_, offsets_, cluster_, stats_
   std::map<std::string, std::vector<PartitionLog>> topics_;

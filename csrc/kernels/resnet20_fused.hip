@@ -39,12 +39,32 @@
 namespace gale {
 namespace {
 
+// Padded NHWC image layout in LDS: pixel (h, w) of a padded image starts at h * RP + w * PS
+// elements (PS >= C: a pixel may be followed by unused elements, RP >= Wp * PS).
+template <int PS_, int RP_>
+struct Lay {
+  static constexpr int PS = PS_, RP = RP_;
+};
+// Stage layouts. Stage 3 (bf16) pads each 64-channel pixel to 80 elements (160 B = ten 16-B
+// slots) and each row to 896 elements: the B fragments of a 16-pixel tile (two output rows of
+// 8) then hit 16 distinct 16-B slots of the 256-B bank row in every ds_read_b128 lane group
+// (unpadded: 4-way, 12 extra LDS cycles per read; tools/lds_bank_model.py).
+template <bool F8>
+struct Layouts {
+  typedef Lay<16, 34 * 16> S1;  // 34x34x16
+  typedef Lay<32, 18 * 32> S2;  // 18x18x32
+  typedef Lay<F8 ? 64 : 80, F8 ? 10 * 64 : 896> S3;  // 10x10x64
+};
+
 // element offsets (multiply by EB for bytes)
 constexpr int kR0 = 0;
 constexpr int kR1 = 18496;           // 34*34*16
 constexpr int kElems = 39232;        // kR1 + 2*18*18*32
 constexpr int kT2 = kR1, kX2 = kR1 + 10368;
-constexpr int kT3 = kR0, kX3 = kR0 + 6400;
+constexpr int kT3 = kR0;
+template <bool F8>
+constexpr int x3_offset() { return kR0 + Layouts<F8>::S3::RP * 10; }
+static_assert(2 * 896 * 10 <= kR1, "stage-3 images fit in R0");
 
 template <bool F8>
 struct Ty;
@@ -159,8 +179,8 @@ struct WPf {
   int next_bytes;
 };
 
-// zero the one-pixel border of a padded Hp x Wp x C image (C * EB % 16 == 0)
-template <bool F8, int NW, int HP, int WP, int C>
+// zero the one-pixel border of a padded Hp x Wp x C image in layout L (C * EB % 16 == 0)
+template <bool F8, int NW, int HP, int WP, int C, class L>
 __device__ __forceinline__ void zero_border(typename Ty<F8>::elem* buf) {
   constexpr int V = C * Ty<F8>::EB / 16;  // 16-byte vectors per cell
   constexpr int CELLS = 2 * WP + 2 * (HP - 2);
@@ -170,7 +190,7 @@ __device__ __forceinline__ void zero_border(typename Ty<F8>::elem* buf) {
     if (cell < WP) { h = 0; w = cell; }
     else if (cell < 2 * WP) { h = HP - 1; w = cell - WP; }
     else { const int r = cell - 2 * WP; h = 1 + (r >> 1); w = (r & 1) ? WP - 1 : 0; }
-    *reinterpret_cast<uint4*>(reinterpret_cast<char*>(buf + (h * WP + w) * C) + v * 16) =
+    *reinterpret_cast<uint4*>(reinterpret_cast<char*>(buf + h * L::RP + w * L::PS) + v * 16) =
         make_uint4(0, 0, 0, 0);
   }
 }
@@ -178,7 +198,8 @@ __device__ __forceinline__ void zero_border(typename Ty<F8>::elem* buf) {
 // 3x3 pad-1 convolution LDS -> LDS with the folded-BN bias, optional residual and ReLU.
 // RES: 0 none, 1 identity (same layout as out), 2 option-A shortcut from the previous stage's
 // buffer (stride-2 subsample, channels >= RC are zero).
-template <bool F8, int NW, int CIN, int COUT, int S, int HO, int RES, int RC>
+template <bool F8, int NW, int CIN, int COUT, int S, int HO, int RES, int RC, class LI, class LO,
+          class LR>
 __device__ __forceinline__ void conv3x3(const void* wgv, const float* __restrict__ wscale,
                                         const float* __restrict__ bias, Q q,
                                         const typename Ty<F8>::elem* in,
@@ -187,9 +208,6 @@ __device__ __forceinline__ void conv3x3(const void* wgv, const float* __restrict
   typedef Ty<F8> T;
   typedef typename T::elem elem;
   const elem* wg = static_cast<const elem*>(NW == 8 ? pf.wl : wgv);
-  constexpr int WPI = HO * S + 2;  // padded input width
-  constexpr int WPO = HO + 2;      // padded output width
-  constexpr int RWP = 2 * HO + 2;  // padded width of an option-A residual source
   constexpr int K = 9 * CIN;
   constexpr int KPAD = (K + 31) / 32 * 32;
   constexpr int KS = KPAD / 32;
@@ -213,7 +231,7 @@ __device__ __forceinline__ void conv3x3(const void* wgv, const float* __restrict
     int tap = k / CIN;
     const int ci = k - tap * CIN;
     if (tap >= 9) tap = 0;  // K padding: zero weights, any finite input
-    koff[ks] = ((tap / 3) * WPI + (tap % 3)) * CIN + ci;
+    koff[ks] = (tap / 3) * LI::RP + (tap % 3) * LI::PS + ci;
   }
   const int c0 = ct * 16 + g * 4;  // this lane's 4 output channels
   const float4 bv = *reinterpret_cast<const float4*>(bias + c0);
@@ -238,7 +256,7 @@ __device__ __forceinline__ void conv3x3(const void* wgv, const float* __restrict
       const int m = (pt0 + pg + p) * 16 + col;
       ho[p] = m / HO;
       wo[p] = m - ho[p] * HO;
-      pbase[p] = (ho[p] * S * WPI + wo[p] * S) * CIN;
+      pbase[p] = ho[p] * S * LI::RP + wo[p] * S * LI::PS;
     }
     f32x4 acc[G];
 #pragma unroll
@@ -257,9 +275,9 @@ __device__ __forceinline__ void conv3x3(const void* wgv, const float* __restrict
     for (int p = 0; p < G; ++p) {
       float v0 = acc[p][0] * sc.x + bv.x, v1 = acc[p][1] * sc.y + bv.y;
       float v2 = acc[p][2] * sc.z + bv.z, v3 = acc[p][3] * sc.w + bv.w;
-      const int o = ((ho[p] + 1) * WPO + wo[p] + 1) * COUT + c0;
+      const int o = (ho[p] + 1) * LO::RP + (wo[p] + 1) * LO::PS + c0;
       if (RES == 1 || (RES == 2 && c0 < RC)) {
-        const int ro = RES == 1 ? o : ((2 * ho[p] + 1) * RWP + 2 * wo[p] + 1) * RC + c0;
+        const int ro = RES == 1 ? o : (2 * ho[p] + 1) * LR::RP + (2 * wo[p] + 1) * LR::PS + c0;
         float r[4];
         T::load4(res + ro, q.res, r);
         v0 += r[0]; v1 += r[1]; v2 += r[2]; v3 += r[3];
@@ -345,7 +363,10 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void resnet20_fused_kernel(ResNet2
   elem* T2 = base + kT2;
   elem* X2 = base + kX2;
   elem* T3 = base + kT3;
-  elem* X3 = base + kX3;
+  elem* X3 = base + x3_offset<F8>();
+  typedef typename Layouts<F8>::S1 L1;
+  typedef typename Layouts<F8>::S2 L2;
+  typedef typename Layouts<F8>::S3 L3;
   float* scratch = reinterpret_cast<float*>(base + kR1);
   // 8-wave form: weights of the next conv prefetched into LDS behind the activations
   void* wl = NW == 8 ? static_cast<void*>(smem + kElems * T::EB) : nullptr;
@@ -366,7 +387,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void resnet20_fused_kernel(ResNet2
       const int h = cell / 34, w = cell - h * 34;
       if (h == 0 || h == 33 || w == 0 || w == 33) IN[i] = T::zero();
     }
-    zero_border<F8, NW, 34, 34, 16>(X1);
+    zero_border<F8, NW, 34, 34, 16, L1>(X1);
     const float4* xi = reinterpret_cast<const float4*>(x + (size_t)img * 3072);
     for (int i = threadIdx.x; i < 768; i += 64 * NW) {
       const float4 v = xi[i];
@@ -386,50 +407,50 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void resnet20_fused_kernel(ResNet2
       prefetch_weights<NW>(p.w[1], conv_w_bytes(1, T::EB), wl);
     }
     __syncthreads();
-    zero_border<F8, NW, 34, 34, 16>(T1);  // IN is dead; T1's border overlaps its bytes
+    zero_border<F8, NW, 34, 34, 16, L1>(T1);  // IN is dead; T1's border overlaps its bytes
     // ---- stage 1: 32x32x16 ----
 #pragma unroll 1
     for (int blk = 0; blk < 3; ++blk) {
       const int c1 = 1 + 2 * blk, c2 = c1 + 1;
-      conv3x3<F8, NW, 16, 16, 1, 32, 0, 16>(p.w[c1], p.ws[c1], p.b[c1], conv_q<F8>(p, c1), X1, T1,
+      conv3x3<F8, NW, 16, 16, 1, 32, 0, 16, L1, L1, L1>(p.w[c1], p.ws[c1], p.b[c1], conv_q<F8>(p, c1), X1, T1,
                                         nullptr, pfw(c1));
       __syncthreads();
-      conv3x3<F8, NW, 16, 16, 1, 32, 1, 16>(p.w[c2], p.ws[c2], p.b[c2], conv_q<F8>(p, c2), T1, X1,
+      conv3x3<F8, NW, 16, 16, 1, 32, 1, 16, L1, L1, L1>(p.w[c2], p.ws[c2], p.b[c2], conv_q<F8>(p, c2), T1, X1,
                                         X1, pfw(c2));
       __syncthreads();
     }
     // ---- stage 2: 16x16x32 ----
-    zero_border<F8, NW, 18, 18, 32>(T2);
-    zero_border<F8, NW, 18, 18, 32>(X2);
-    conv3x3<F8, NW, 16, 32, 2, 16, 0, 16>(p.w[7], p.ws[7], p.b[7], conv_q<F8>(p, 7), X1, T2, nullptr, pfw(7));
+    zero_border<F8, NW, 18, 18, 32, L2>(T2);
+    zero_border<F8, NW, 18, 18, 32, L2>(X2);
+    conv3x3<F8, NW, 16, 32, 2, 16, 0, 16, L1, L2, L1>(p.w[7], p.ws[7], p.b[7], conv_q<F8>(p, 7), X1, T2, nullptr, pfw(7));
     __syncthreads();
-    conv3x3<F8, NW, 32, 32, 1, 16, 2, 16>(p.w[8], p.ws[8], p.b[8], conv_q<F8>(p, 8), T2, X2, X1, pfw(8));
+    conv3x3<F8, NW, 32, 32, 1, 16, 2, 16, L2, L2, L1>(p.w[8], p.ws[8], p.b[8], conv_q<F8>(p, 8), T2, X2, X1, pfw(8));
     __syncthreads();
 #pragma unroll 1
     for (int blk = 1; blk < 3; ++blk) {
       const int c1 = 7 + 2 * blk, c2 = c1 + 1;
-      conv3x3<F8, NW, 32, 32, 1, 16, 0, 32>(p.w[c1], p.ws[c1], p.b[c1], conv_q<F8>(p, c1), X2, T2,
+      conv3x3<F8, NW, 32, 32, 1, 16, 0, 32, L2, L2, L2>(p.w[c1], p.ws[c1], p.b[c1], conv_q<F8>(p, c1), X2, T2,
                                         nullptr, pfw(c1));
       __syncthreads();
-      conv3x3<F8, NW, 32, 32, 1, 16, 1, 32>(p.w[c2], p.ws[c2], p.b[c2], conv_q<F8>(p, c2), T2, X2,
+      conv3x3<F8, NW, 32, 32, 1, 16, 1, 32, L2, L2, L2>(p.w[c2], p.ws[c2], p.b[c2], conv_q<F8>(p, c2), T2, X2,
                                         X2, pfw(c2));
       __syncthreads();
     }
     // ---- stage 3: 8x8x64 ----
-    zero_border<F8, NW, 10, 10, 64>(T3);
-    zero_border<F8, NW, 10, 10, 64>(X3);
-    conv3x3<F8, NW, 32, 64, 2, 8, 0, 32>(p.w[13], p.ws[13], p.b[13], conv_q<F8>(p, 13), X2, T3,
+    zero_border<F8, NW, 10, 10, 64, L3>(T3);
+    zero_border<F8, NW, 10, 10, 64, L3>(X3);
+    conv3x3<F8, NW, 32, 64, 2, 8, 0, 32, L2, L3, L2>(p.w[13], p.ws[13], p.b[13], conv_q<F8>(p, 13), X2, T3,
                                      nullptr, pfw(13));
     __syncthreads();
-    conv3x3<F8, NW, 64, 64, 1, 8, 2, 32>(p.w[14], p.ws[14], p.b[14], conv_q<F8>(p, 14), T3, X3, X2, pfw(14));
+    conv3x3<F8, NW, 64, 64, 1, 8, 2, 32, L3, L3, L2>(p.w[14], p.ws[14], p.b[14], conv_q<F8>(p, 14), T3, X3, X2, pfw(14));
     __syncthreads();
 #pragma unroll 1
     for (int blk = 1; blk < 3; ++blk) {
       const int c1 = 13 + 2 * blk, c2 = c1 + 1;
-      conv3x3<F8, NW, 64, 64, 1, 8, 0, 64>(p.w[c1], p.ws[c1], p.b[c1], conv_q<F8>(p, c1), X3, T3,
+      conv3x3<F8, NW, 64, 64, 1, 8, 0, 64, L3, L3, L3>(p.w[c1], p.ws[c1], p.b[c1], conv_q<F8>(p, c1), X3, T3,
                                        nullptr, pfw(c1));
       __syncthreads();
-      conv3x3<F8, NW, 64, 64, 1, 8, 1, 64>(p.w[c2], p.ws[c2], p.b[c2], conv_q<F8>(p, c2), T3, X3,
+      conv3x3<F8, NW, 64, 64, 1, 8, 1, 64, L3, L3, L3>(p.w[c2], p.ws[c2], p.b[c2], conv_q<F8>(p, c2), T3, X3,
                                        X3, pfw(c2));
       __syncthreads();
     }
@@ -442,7 +463,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void resnet20_fused_kernel(ResNet2
       for (int i = 0; i < PPW; ++i) {
         const int pix = qq * PPW + i;
         const int h = pix >> 3, w = pix & 7;
-        s += T::to_f32(X3[((h + 1) * 10 + w + 1) * 64 + c]);
+        s += T::to_f32(X3[(h + 1) * L3::RP + (w + 1) * L3::PS + c]);
       }
       scratch[qq * 64 + c] = s;  // R1 is free in stage 3's last block (X2 is dead)
       __syncthreads();

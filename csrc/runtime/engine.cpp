@@ -600,6 +600,7 @@ void Engine::source_loop(int idx) {
   cc.client_id = cfg_.client_id + "-source-" + std::to_string(idx);
   cc.group_id = cfg_.group_id;
   cc.max_wait_ms = cfg_.fetch_max_wait_ms;
+  cc.min_bytes = std::max(1, cfg_.fetch_min_bytes);
   cc.fetch_max_bytes = cfg_.fetch_max_bytes;
   cc.partition_max_bytes = cfg_.partition_max_bytes;
   // with decode workers the CRC32C check moves off this thread (decode_fetch)

@@ -56,6 +56,8 @@ struct EngineConfig {
   int source_parallelism = 2;      // KAFKA_SPOUT_PARAL (MainTopology.java:26)
   std::string start_offset = "latest";  // latest | earliest | committed
   int fetch_max_wait_ms = 20;
+  int fetch_min_bytes = 1;         // Kafka fetch.min.bytes: a long-poll returns once this much
+                                   // is available (or fetch_max_wait_ms passed)
   int fetch_max_bytes = 16 << 20;
   int partition_max_bytes = 8 << 20;
   bool check_crcs = true;

@@ -131,6 +131,17 @@ def thread_cpu_seconds() -> dict:
     return out
 
 
+def name_this_thread(name: str) -> None:
+    """Set the calling thread's OS name (prctl PR_SET_NAME, <= 15 bytes) so per-thread CPU
+    accounting (thread_cpu_seconds, bench.py --timeline) can tell Python threads apart."""
+    import ctypes
+
+    try:
+        ctypes.CDLL(None).prctl(15, name.encode()[:15], 0, 0, 0)
+    except (OSError, AttributeError):
+        pass
+
+
 def free_port(host: str = "127.0.0.1") -> int:
     """An ephemeral TCP port that was free a moment ago (embedded brokers, rendezvous)."""
     s = socket.socket()
