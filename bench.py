@@ -177,6 +177,7 @@ class Timeline:
         from gale.utils import thread_cpu_by_thread, thread_cpu_seconds
 
         self.per_thread = thread_cpu_by_thread
+        self.main_tid = threading.main_thread().native_id
         self.f = open(path, "w")
         self.dt = interval_ms / 1e3
         self.broker = broker
@@ -219,7 +220,7 @@ class Timeline:
             other = {}
             for k, v in th.items():
                 if not k[1].startswith(groups):
-                    name = f"{k[1]}:{k[0]}"
+                    name = "main" if k[0] == self.main_tid else f"{k[1]}:{k[0]}"
                     other[name] = other.get(name, 0.0) + v - prev_th.get(k, 0.0)
             row["other_top"] = {k: round(v / dt, 2) for k, v in
                                 sorted(other.items(), key=lambda kv: -kv[1])[:4] if v > 0}

@@ -410,6 +410,113 @@ void Producer::send(const std::string& topic, int partition, const std::string* 
   if (b.bytes >= (size_t)cfg_.batch_size || cfg_.linger_ms <= 0) cv_.notify_one();
 }
 
+void Producer::send_group(const std::string& topic, int partition, RecordGroup g,
+                          GroupCallback cb) {
+  const size_t n = g.size();
+  if (n == 0) return;
+  if (partition < 0) {
+    // the partitioner's choice is per record (kafka-clients 0.11: round-robin for null keys,
+    // murmur2 of the key otherwise): split into one sub-group per partition, acknowledged
+    // together once every sub-group is
+    std::vector<int> part(n);
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      if (closing_) throw std::runtime_error("producer is closed");
+      for (size_t i = 0; i < n; ++i) {
+        std::string key;
+        const bool keyed = !g.koff.empty() && !g.key_null[i];
+        if (keyed) key.assign(g.keys, g.koff[i], g.koff[i + 1] - g.koff[i]);
+        part[i] = choose_partition(topic, keyed ? &key : nullptr);
+      }
+    }
+    std::map<int, RecordGroup> subs;
+    for (size_t i = 0; i < n; ++i) {
+      RecordGroup& s = subs[part[i]];
+      if (s.off.empty()) {
+        s.off.push_back(0);
+        if (!g.koff.empty()) s.koff.push_back(0);
+        s.headers = g.headers;
+        s.ts = g.ts;
+      }
+      s.values.append(g.values, g.off[i], g.off[i + 1] - g.off[i]);
+      s.off.push_back((uint32_t)s.values.size());
+      if (!g.null_value.empty()) {
+        if (s.null_value.empty()) s.null_value.assign(s.off.size() - 2, 0);
+        s.null_value.push_back(g.null_value[i]);
+      } else if (!s.null_value.empty()) {
+        s.null_value.push_back(0);
+      }
+      if (!g.koff.empty()) {
+        s.keys.append(g.keys, g.koff[i], g.koff[i + 1] - g.koff[i]);
+        s.koff.push_back((uint32_t)s.keys.size());
+        s.key_null.push_back(g.key_null[i]);
+      }
+    }
+    if (subs.size() > 1) {
+      struct Join {
+        std::mutex mu;
+        size_t left;
+        int16_t err = 0;
+        GroupCallback cb;
+      };
+      auto j = std::make_shared<Join>();
+      j->left = subs.size();
+      j->cb = std::move(cb);
+      for (auto& kv : subs)
+        send_group(topic, kv.first, std::move(kv.second),
+                   [j, n](int16_t err, int32_t, int64_t, size_t) {
+                     bool last;
+                     int16_t e;
+                     {
+                       std::lock_guard<std::mutex> lk(j->mu);
+                       if (err && !j->err) j->err = err;
+                       last = --j->left == 0;
+                       e = j->err;
+                     }
+                     if (last && j->cb) j->cb(e, -1, -1, n);
+                   });
+      return;
+    }
+    partition = subs.begin()->first;
+    g = std::move(subs.begin()->second);
+  }
+  size_t sz = 0;
+  for (size_t i = 0; i < n; ++i) {
+    sz += (size_t)(g.off[i + 1] - g.off[i]) + 36;
+    if (!g.koff.empty()) sz += (size_t)(g.koff[i + 1] - g.koff[i]);
+    for (const Header& h : g.headers) sz += h.key.size() + h.value.size() + 10;
+  }
+  std::unique_lock<std::mutex> lk(mu_);
+  if (closing_) throw std::runtime_error("producer is closed");
+  done_cv_.wait(lk, [&] { return unsent_bytes_ < cfg_.buffer_memory || closing_; });
+  Pending p;
+  p.ts = g.ts >= 0 ? g.ts : wall_ms();
+  p.group = std::make_unique<RecordGroup>(std::move(g));
+  p.gcb = std::move(cb);
+  PartBatch& b = acc_[{topic, partition}];
+  if (b.recs.empty()) b.first_ms = mono_ms();
+  b.bytes += sz;
+  b.recs.push_back(std::move(p));
+  unsent_bytes_ += (int64_t)sz;
+  outstanding_ += (int64_t)n;
+  stats_.records_sent += (int64_t)n;
+  if (b.bytes >= (size_t)cfg_.batch_size || cfg_.linger_ms <= 0) cv_.notify_one();
+}
+
+// bytes an entry was charged to unsent_bytes_ (and to its chunk)
+static size_t pending_bound(const std::string& key, const std::string& value,
+                            const std::vector<Header>& headers, const RecordGroup* g) {
+  if (!g) return record_bound(key, value, headers);
+  size_t sz = 0;
+  const size_t n = g->size();
+  for (size_t i = 0; i < n; ++i) {
+    sz += (size_t)(g->off[i + 1] - g->off[i]) + 36;
+    if (!g->koff.empty()) sz += (size_t)(g->koff[i + 1] - g->koff[i]);
+    for (const Header& h : g->headers) sz += h.key.size() + h.value.size() + 10;
+  }
+  return sz;
+}
+
 void Producer::flush() {
   std::unique_lock<std::mutex> lk(mu_);
   flush_req_ = true;
@@ -441,22 +548,32 @@ ProducerStats Producer::stats() const {
 void Producer::run() {
   std::deque<InFlight> inflight;
   auto complete = [&](std::vector<Pending>& recs, int16_t err, int part, int64_t base) {
+    int64_t idx = 0;
     for (size_t i = 0; i < recs.size(); ++i) {
-      SendResult r;
-      r.error = err;
-      r.partition = part;
-      r.offset = (err == NONE && base >= 0) ? base + (int64_t)i : -1;
-      if (recs[i].cb) {
+      const int64_t off = (err == NONE && base >= 0) ? base + idx : -1;
+      if (recs[i].group) {
+        if (recs[i].gcb) {
+          try {
+            recs[i].gcb(err, part, off, recs[i].group->size());
+          } catch (...) {
+          }
+        }
+      } else if (recs[i].cb) {
+        SendResult r;
+        r.error = err;
+        r.partition = part;
+        r.offset = off;
         try {
           recs[i].cb(r);
         } catch (...) {
         }
       }
+      idx += (int64_t)recs[i].records();
     }
     std::lock_guard<std::mutex> lk(mu_);
-    outstanding_ -= (int64_t)recs.size();
-    if (err == NONE) stats_.records_acked += (int64_t)recs.size();
-    else stats_.records_failed += (int64_t)recs.size();
+    outstanding_ -= idx;
+    if (err == NONE) stats_.records_acked += idx;
+    else stats_.records_failed += idx;
     done_cv_.notify_all();
   };
   auto read_one = [&]() {
@@ -516,7 +633,7 @@ void Producer::run() {
                                    ? (size_t)cfg_.max_request_size - kRequestOverhead
                                    : (size_t)cfg_.max_request_size / 2;
             for (auto& p : b.recs) {
-              const size_t sz = record_bound(p.key, p.value, p.headers);
+              const size_t sz = pending_bound(p.key, p.value, p.headers, p.group.get());
               if (!chunk.empty() && cbytes + sz > cap) {
                 ready.push_back({it->first, std::move(chunk)});
                 chunk.clear();
@@ -574,15 +691,34 @@ void Producer::run() {
           bool dup = false;
           for (const auto& fb : f.batches) dup |= fb.first == item.first;
           if (dup) break;
-          std::vector<RecordIn> ins(item.second.size());
+          std::vector<RecordIn> ins;
+          ins.reserve(item.second.size());
           for (size_t j = 0; j < item.second.size(); ++j) {
             const Pending& p = item.second[j];
-            ins[j].key = p.key;
-            ins[j].key_null = p.key_null;
-            ins[j].value = p.value;
-            ins[j].value_null = p.value_null;
-            ins[j].timestamp = p.ts;
-            ins[j].headers = p.headers.empty() ? nullptr : &p.headers;
+            if (p.group) {
+              const RecordGroup& g = *p.group;
+              for (size_t i = 0; i < g.size(); ++i) {
+                RecordIn r;
+                r.value = std::string_view(g.values).substr(g.off[i], g.off[i + 1] - g.off[i]);
+                r.value_null = !g.null_value.empty() && g.null_value[i];
+                if (!g.koff.empty() && !g.key_null[i]) {
+                  r.key = std::string_view(g.keys).substr(g.koff[i], g.koff[i + 1] - g.koff[i]);
+                  r.key_null = false;
+                }
+                r.timestamp = p.ts;
+                r.headers = g.headers.empty() ? nullptr : &g.headers;
+                ins.push_back(r);
+              }
+              continue;
+            }
+            RecordIn r;
+            r.key = p.key;
+            r.key_null = p.key_null;
+            r.value = p.value;
+            r.value_null = p.value_null;
+            r.timestamp = p.ts;
+            r.headers = p.headers.empty() ? nullptr : &p.headers;
+            ins.push_back(r);
           }
           Writer bw;
           encode_batch(bw, ins.data(), ins.size(), 0, item.second.front().ts);

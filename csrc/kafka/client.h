@@ -120,6 +120,24 @@ struct SendResult {
 };
 using SendCallback = std::function<void(const SendResult&)>;
 
+// Several records for one partition sent (and acknowledged) as a unit: the serving engine hands
+// each micro-batch's predictions over in one call instead of one send() per record. Record i's
+// value is values[off[i], off[i + 1]) (null when null_value[i] is set); keys likewise from
+// keys / koff / key_null (koff empty = every key null); every record carries `headers`.
+struct RecordGroup {
+  std::string values;
+  std::vector<uint32_t> off;        // n + 1 boundaries
+  std::vector<uint8_t> null_value;  // n flags, or empty (no null values)
+  std::string keys;
+  std::vector<uint32_t> koff;       // n + 1 boundaries, or empty (all keys null)
+  std::vector<uint8_t> key_null;    // n flags (with koff)
+  std::vector<Header> headers;
+  int64_t ts = -1;
+  size_t size() const { return off.empty() ? 0 : off.size() - 1; }
+};
+// (error, partition, offset of the group's first record, records): once per group
+using GroupCallback = std::function<void(int16_t, int32_t, int64_t, size_t)>;
+
 struct ProducerStats {
   int64_t records_sent = 0, records_acked = 0, records_failed = 0, requests = 0, bytes = 0;
 };
@@ -135,6 +153,9 @@ class Producer {
   // (tombstone) - what the reference's JsonSerializer does for a failed tuple.
   void send(const std::string& topic, int partition, const std::string* key, std::string value,
             bool value_null, std::vector<Header> headers, int64_t timestamp, SendCallback cb);
+  // A group of records to one partition (partition < 0: the partitioner picks one for the
+  // whole group), acknowledged together; the records stay in order and in one batch.
+  void send_group(const std::string& topic, int partition, RecordGroup g, GroupCallback cb);
   void flush();  // blocks until every record sent so far is acked or failed
   void close();
   int partitions_for(const std::string& topic);
@@ -149,6 +170,9 @@ class Producer {
     std::vector<Header> headers;
     int64_t ts = -1;
     SendCallback cb;
+    std::unique_ptr<RecordGroup> group;  // set: this entry is a whole group of records
+    GroupCallback gcb;
+    size_t records() const { return group ? group->size() : 1; }
   };
   struct PartBatch {
     std::vector<Pending> recs;

@@ -282,7 +282,28 @@ __device__ __forceinline__ void conv3x3(const void* wgv, const float* __restrict
         T::load4(res + ro, q.res, r);
         v0 += r[0]; v1 += r[1]; v2 += r[2]; v3 += r[3];
       }
-      T::store4(out + o, q.qout, fmaxf(v0, 0.f), fmaxf(v1, 0.f), fmaxf(v2, 0.f), fmaxf(v3, 0.f));
+      if constexpr (!F8) {
+        // The accumulator puts lane (g, col) on channels g*4..+3 of pixel col: a 16-lane
+        // ds_write_b64 group would store one channel quad of 16 pixels, 4-way (8-way for 64-B
+        // pixels) on the 32-bank store rule. Exchange lane bits (2,3) <-> (4,5) first
+        // (ds_bpermute), so a group stores all four quads of 4 consecutive pixels: 128
+        // contiguous bytes for 32-B pixels (stage 1), distinct banks for the padded 160-B
+        // pixels (stage 3), 2-way for 64-B pixels (stage 2).
+        bf16x4 ov;
+        ov[0] = (bf16)fmaxf(v0, 0.f); ov[1] = (bf16)fmaxf(v1, 0.f);
+        ov[2] = (bf16)fmaxf(v2, 0.f); ov[3] = (bf16)fmaxf(v3, 0.f);
+        uint2 w = __builtin_bit_cast(uint2, ov);
+        const int src = (((lane >> 2) & 3) << 4) | (((lane >> 4) & 3) << 2) | (lane & 3);
+        w.x = (unsigned)__builtin_amdgcn_ds_bpermute(src << 2, (int)w.x);
+        w.y = (unsigned)__builtin_amdgcn_ds_bpermute(src << 2, (int)w.y);
+        const int mt = (pt0 + pg + p) * 16 + ((lane >> 4) << 2) + (lane & 3);
+        const int hot = mt / HO, wot = mt - hot * HO;
+        const int ot = (hot + 1) * LO::RP + (wot + 1) * LO::PS + ct * 16 + ((lane >> 2) & 3) * 4;
+        *reinterpret_cast<uint2*>(out + ot) = w;
+      } else {
+        T::store4(out + o, q.qout, fmaxf(v0, 0.f), fmaxf(v1, 0.f), fmaxf(v2, 0.f),
+                  fmaxf(v3, 0.f));
+      }
     }
   }
   // the next conv's weights have landed before the caller's barrier

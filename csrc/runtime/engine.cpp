@@ -393,7 +393,7 @@ void Engine::commit(kafka::Consumer& c, const std::vector<int>& parts) {
     std::lock_guard<std::mutex> lk(pend_mu_);
     for (int p : parts) {
       auto it = pending_.find(p);
-      if (it != pending_.end() && !it->second.empty()) offs[p] = it->second.begin()->first;
+      if (it != pending_.end() && !it->second.empty()) offs[p] = it->second.first();
       else if (next_fetch_.count(p)) offs[p] = next_fetch_[p];
     }
   }
@@ -698,7 +698,7 @@ void Engine::source_loop(int idx) {
       // register before anything can complete, and before the commit position moves past them
       std::lock_guard<std::mutex> lk(pend_mu_);
       for (auto& f : fs)
-        for (const kafka::RecordRef& rr : f.records) pending_[rr.partition][rr.offset] = 1;
+        for (const kafka::RecordRef& rr : f.records) pending_[rr.partition].add(rr.offset);
       for (int p : parts) next_fetch_[p] = cons->position(p);
       for (const auto& kv : cons->high_watermarks())
         if (std::find(parts.begin(), parts.end(), kv.first) != parts.end())
@@ -1170,24 +1170,89 @@ void Engine::finish_batch(ReplicaSlot* rs, Batch& b) {
   rs->records += (int64_t)b.recs.size();
   kafka::Producer* prod = producer_for(rs->index);
   const bool js = cfg_.value_format == "json-string";
+  auto encode_ok = [&](const InRecord& r, int img, std::string& out) {
+    if (b.pred_text)
+      codec::encode_predictions_text(b.pred_text + (size_t)img * cfg_.classes * 16, r.images,
+                                     cfg_.classes, js, out);
+    else
+      codec::encode_predictions(b.probs + (size_t)img * cfg_.classes, r.images, cfg_.classes, js,
+                                out);
+  };
   int img = 0;
   std::string out;
+  // The batch's outputs leave as ONE record group: one producer call and one acknowledgement
+  // for the batch's records, in order (the producer splits the group by partition when its
+  // partitioner chooses per record). Records sent one by one cost ~1 us each in allocations,
+  // producer lock round trips and per-record callbacks, at 1.5 M records/s ~1.5 cores.
+  kafka::RecordGroup g;
+  g.off.reserve(b.recs.size() + 1);
+  g.off.push_back(0);
+  g.values.reserve(b.recs.size() * (size_t)(cfg_.classes * 13 + 24));
+  const bool keyed = cfg_.output_key == "input";
+  if (keyed) g.koff.push_back(0);
+  if (cfg_.type_id_header) g.headers.push_back({"__TypeId__", "java.lang.String", false});
+  auto metas = std::make_shared<std::vector<InRecord>>();
+  metas->reserve(b.recs.size());
   for (size_t i = 0; i < b.recs.size(); ++i) {
     InRecord& r = b.recs[i];
     if (r.status == codec::OK && i < b.dev_status.size()) r.status = b.dev_status[i];
+    InRecord meta;
+    meta.partition = r.partition;
+    meta.offset = r.offset;
+    meta.timestamp_ms = r.timestamp_ms;
+    meta.t_fetch_ns = r.t_fetch_ns;
+    meta.images = r.status == codec::OK ? r.images : 0;
+    bool null_value = false;
     if (r.status != codec::OK) {
-      emit_error(r, r.status, prod);
+      ++errors_;
+      err_by_status_[r.status & 7]++;
+      if (cfg_.on_error == "drop") {
+        ++dropped_;
+        complete_record(meta, true);
+        img += r.images;
+        continue;
+      }
+      if (cfg_.on_error == "null") {
+        null_value = true;
+      } else {
+        codec::encode_error(r.status, "", js, out);
+        g.values += out;
+      }
     } else {
-      if (b.pred_text)
-        codec::encode_predictions_text(b.pred_text + (size_t)img * cfg_.classes * 16, r.images,
-                                       cfg_.classes, js, out);
-      else
-        codec::encode_predictions(b.probs + (size_t)img * cfg_.classes, r.images, cfg_.classes,
-                                  js, out);
-      emit(r, out, false, prod);
+      encode_ok(r, img, out);
+      g.values += out;
     }
     img += r.images;
+    g.off.push_back((uint32_t)g.values.size());
+    if (null_value) {
+      if (g.null_value.empty()) g.null_value.assign(metas->size(), 0);
+      g.null_value.push_back(1);
+    } else if (!g.null_value.empty()) {
+      g.null_value.push_back(0);
+    }
+    if (keyed) {
+      const bool has = r.key_len >= 0 && r.key;
+      if (has) g.keys.append(reinterpret_cast<const char*>(r.key), (size_t)r.key_len);
+      g.koff.push_back((uint32_t)g.keys.size());
+      g.key_null.push_back(has ? 0 : 1);
+    }
+    metas->push_back(meta);
   }
+  if (metas->empty()) return;
+  const bool ff = cfg_.sink_mode == "fire-and-forget";
+  kafka::GroupCallback cb;
+  if (!ff)
+    cb = [this, metas](int16_t err, int32_t, int64_t, size_t) {
+      complete_records(*metas, err == 0);
+    };
+  try {
+    prod->send_group(cfg_.output_topic, cfg_.output_partition, std::move(g), std::move(cb));
+  } catch (const std::exception& e) {
+    fprintf(stderr, "[gale sink] send failed: %s\n", e.what());
+    complete_records(*metas, false);
+    return;
+  }
+  if (ff) complete_records(*metas, true);  // KafkaBolt fire-and-forget acks immediately
   if (cfg_.sink_mode == "sync") prod->flush();
 }
 
@@ -1195,11 +1260,52 @@ void Engine::finish_batch(ReplicaSlot* rs, Batch& b) {
 // sink
 // ---------------------------------------------------------------------------------------------
 
+// A record group's acknowledgement: one pending-window update for all of its records.
+void Engine::complete_records(const std::vector<InRecord>& rs, bool ok) {
+  std::vector<char> good(rs.size());
+  for (size_t i = 0; i < rs.size(); ++i) good[i] = ok && !fault_hit(producer_fail_p_);
+  {
+    std::lock_guard<std::mutex> lk(pend_mu_);
+    for (const InRecord& r : rs) {
+      auto it = pending_.find(r.partition);
+      if (it != pending_.end()) it->second.done(r.offset);
+    }
+  }
+  const int64_t now = mono_ns();
+  const int64_t wall = wall_ms_now();
+  int64_t nok = 0, imgs = 0;
+  for (size_t i = 0; i < rs.size(); ++i) {
+    const InRecord& r = rs[i];
+    if (good[i]) {
+      ++nok;
+      imgs += r.images;
+      h_engine_e2e_us_.add((now - r.t_fetch_ns) / 1000);
+      if (cfg_.slo_p99_ms > 0) h_slo_win_us_.add((now - r.t_fetch_ns) / 1000);
+      if (r.timestamp_ms > 0) h_record_e2e_ms_.add(wall - r.timestamp_ms);
+    }
+  }
+  records_out_ += nok;
+  images_out_ += imgs;
+  produce_failures_ += (int64_t)rs.size() - nok;
+  t_last_ns_ = now;
+  if (ack_log_on_.load(std::memory_order_relaxed)) {
+    std::lock_guard<std::mutex> lk(ack_mu_);
+    for (size_t i = 0; i < rs.size() && ack_log_.size() < ack_cap_; ++i)
+      if (good[i]) ack_log_.push_back({rs[i].partition, rs[i].offset, now});
+  }
+  const int64_t c = completed_ += (int64_t)rs.size();
+  const int64_t target = wait_target_.load(std::memory_order_relaxed);
+  if ((cfg_.max_records > 0 && c >= cfg_.max_records) || (target > 0 && c >= target)) {
+    std::lock_guard<std::mutex> lk(done_mu_);
+    done_cv_.notify_all();
+  }
+}
+
 void Engine::complete_record(const InRecord& r, bool ok) {
   {
     std::lock_guard<std::mutex> lk(pend_mu_);
     auto it = pending_.find(r.partition);
-    if (it != pending_.end()) it->second.erase(r.offset);
+    if (it != pending_.end()) it->second.done(r.offset);
   }
   const int64_t now = mono_ns();
   if (ok) {
@@ -1405,7 +1511,7 @@ std::vector<PartitionOffsets> Engine::partition_offsets() const {
     o.partition = kv.first;
     o.fetched = kv.second;
     auto pit = pending_.find(kv.first);
-    o.committed = (pit != pending_.end() && !pit->second.empty()) ? pit->second.begin()->first
+    o.committed = (pit != pending_.end() && !pit->second.empty()) ? pit->second.first()
                                                                   : kv.second;
     auto hit = high_watermark_.find(kv.first);
     o.high_watermark = hit != high_watermark_.end() ? hit->second : -1;

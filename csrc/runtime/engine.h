@@ -217,6 +217,7 @@ class Engine {
   void emit(InRecord& r, std::string value, bool null_value, kafka::Producer* prod);
   void emit_error(InRecord& r, int status, kafka::Producer* prod);
   void complete_record(const InRecord& r, bool ok);
+  void complete_records(const std::vector<InRecord>& rs, bool ok);
   void commit(kafka::Consumer& c, const std::vector<int>& parts);
   kafka::Producer* producer_for(int i);
   bool fault_hit(double p);
@@ -250,7 +251,42 @@ class Engine {
   std::atomic<int> sources_active_{0};
 
   std::mutex pend_mu_;
-  std::map<int, std::map<int64_t, int>> pending_;  // partition -> offset -> 1
+  // Offsets fetched but not yet acknowledged downstream, per partition: a sliding window over
+  // the offsets (one byte per offset from the oldest pending one), so registering a fetched
+  // record and completing it are O(1) instead of a tree insert / erase per record.
+  struct OffsetWindow {
+    int64_t base = 0;          // offset of st[0]
+    std::deque<uint8_t> st;    // 1 = pending; the front is pending whenever npending > 0
+    int64_t npending = 0;
+    void add(int64_t off) {
+      if (st.empty()) {
+        base = off;
+      } else if (off < base) {  // (a seek back re-fetched older offsets)
+        st.insert(st.begin(), (size_t)(base - off), 0);
+        base = off;
+      }
+      const size_t i = (size_t)(off - base);
+      if (i >= st.size()) st.resize(i + 1, 0);
+      if (!st[i]) {
+        st[i] = 1;
+        ++npending;
+      }
+    }
+    void done(int64_t off) {
+      if (off < base || (size_t)(off - base) >= st.size()) return;
+      uint8_t& f = st[(size_t)(off - base)];
+      if (!f) return;
+      f = 0;
+      --npending;
+      while (!st.empty() && st.front() == 0) {
+        st.pop_front();
+        ++base;
+      }
+    }
+    bool empty() const { return npending == 0; }
+    int64_t first() const { return base; }  // the oldest pending offset (when !empty())
+  };
+  std::map<int, OffsetWindow> pending_;  // partition -> fetched, unacknowledged offsets
   std::map<int, int64_t> next_fetch_;              // partition -> next offset to fetch
   std::map<int, int64_t> high_watermark_;          // partition -> log end (last fetch response)
 
