@@ -48,7 +48,6 @@ struct GemmConvArgs {
   int nkb;         // 64-deep k-steps = KH*KW*Cin / 64
   int cin_blocks;  // Cin / 64
   int relu, has_res, out_f32;
-  int res_prefetch;  // residual rows loaded during the last k-step (GALE_GEMM_RES_PREFETCH)
   int n_tiles, nwg;
 };
 
@@ -63,23 +62,14 @@ __device__ __forceinline__ void glds16(const void* src, void* lds_base) {
 // on 64 input channels) form, which needs no second stage and so fits 4 workgroups per CU
 // instead of 2 - these layers are bound by their epilogue traffic (a 128 x 128 bf16 output tile
 // plus the residual per 16 KB of input), which more resident workgroups overlap.
-// 3 = a ring of three stages with two k-steps of DMA in flight (128 x 64 tiles, 72 KB: still 2
-// workgroups per CU; an A/B variant, see g_gemm_ring). The ring waits with an explicit vmcnt
-// that leaves the younger stage in flight and a bare s_barrier (a __syncthreads would drain
-// every outstanding load).
-// BM = 256: 8 waves (512 threads) as 4 x 2, one workgroup per CU (96 KB of stages): the same
-// waves per SIMD as two 128-pixel workgroups, but each 64-deep k-step stages 48 KB instead of
-// 2 x 32 KB for the same MFMA work (intensity 85 instead of 64 FLOP per staged byte).
-// WM = 2 with BM = 256: 4 waves of 128 x 64 (TM = 8: 128 accumulator registers, one wave per
-// SIMD), 25 % fewer LDS fragment bytes per MFMA than 64 x 64 wave tiles.
-// RS: register staging instead of LDS-DMA (NST 1 and 2): an LDS-DMA wave-instruction costs
-// 60-185 issue cycles among MFMAs (MI355X_MICROARCH.md, per-instruction constants), 8 of them per
-// wave per k-step against 32 MFMAs of 16 cycles; global_load_dwordx4 + ds_write_b128 issue in a
-// few cycles each and hold the next step in 32 VGPRs.
-template <int BM, int BN, bool STEM, int NST, int WM = BM / 64, bool RS = false>
-__global__ __launch_bounds__(WM * 128, NST == 1 ? 4 : (BM == 256 ? 1 : 2))
+// (Variants measured and removed in round 3 - 256 x 128 tiles with 8 waves, a three-stage
+// 128 x 64 ring, register staging instead of LDS-DMA, the single-stage form for 2-4 k-steps: all
+// slower at ResNet-50 batch 256, profiles/r2_resnet50_gemm_ab.txt.)
+template <int BM, int BN, bool STEM, int NST>
+__global__ __launch_bounds__(256, NST == 1 ? 4 : 2)
 void conv_gemm_kernel(GemmConvArgs a) {
-  constexpr int WN = 2;                         // waves as WM (pixels) x 2 (channels)
+  constexpr int WM = BM / 64;                   // waves as WM (pixels) x 2 (channels)
+  constexpr int WN = 2;
   constexpr int NW = WM * WN;                   // waves per workgroup
   constexpr int TM = BM / WM / 16;              // 16-pixel tiles per wave
   constexpr int TN = BN / WN / 16;              // 16-channel tiles per wave
@@ -161,25 +151,6 @@ void conv_gemm_kernel(GemmConvArgs a) {
     for (int j = 0; j < WI; ++j)
       glds16(wsrc[j] + kb * 64, buf + BM * 128 + (wave * WI + j) * 1024);
   };
-  // register staging (RS): global_load_dwordx4 into VGPRs for a later k-step, ds_write_b128
-  // once its buffer is free; the same lane-linear LDS image as the DMA writes
-  constexpr int XR = RS ? XI : 1, WR = RS ? WI : 1;
-  u32x4 xst[XR], wst[WR];
-  auto fetch = [&](int kb) __attribute__((always_inline)) {
-#pragma unroll
-    for (int j = 0; j < XR; ++j) xst[j] = *(const gbl_u32x4_t*)(xsrc(kb, j));
-#pragma unroll
-    for (int j = 0; j < WR; ++j) wst[j] = *(const gbl_u32x4_t*)(wsrc[j] + kb * 64);
-  };
-  auto commit = [&](uint8_t* buf) __attribute__((always_inline)) {
-#pragma unroll
-    for (int j = 0; j < XR; ++j)
-      *(lds_u32x4_t*)(buf + (wave * XI + j) * 1024 + lane * 16) = xst[j];
-#pragma unroll
-    for (int j = 0; j < WR; ++j)
-      *(lds_u32x4_t*)(buf + BM * 128 + (wave * WI + j) * 1024 + lane * 16) = wst[j];
-  };
-
   f32x4 acc[TM][TN];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
@@ -206,8 +177,7 @@ void conv_gemm_kernel(GemmConvArgs a) {
   // add are loaded into registers while the last k-step's MFMAs run, so their DRAM latency is
   // hidden instead of stalling the epilogue (the 1x1 expansion convs with a shortcut were
   // latency-bound at ~3 TB/s, profiles/r2_resnet50_layers_pmc.txt)
-  // (not for 256-pixel tiles: 512-thread workgroups get 128 VGPRs, no room for 32 more)
-  constexpr bool PREF = NST >= 2 && (BM == 128 || WM == 2);
+  constexpr bool PREF = NST >= 2;
   constexpr int CW = BN / WN;      // channels per wave
   constexpr int EPS = CW + 4;      // fp32 row stride (+16 B: conflict-free 16-row writes)
   constexpr int LPR = CW / 8;      // lanes per pixel row on read-back
@@ -229,47 +199,15 @@ void conv_gemm_kernel(GemmConvArgs a) {
       }
   };
 
-  if (RS) {
-    fetch(0);
-    commit(lds);
-    if (NST == 2 && a.nkb > 1) fetch(1);
-  } else {
-    stage(0, lds);
-    if (NST == 3 && a.nkb > 1) stage(1, lds + STAGE);
-  }
+  stage(0, lds);
   for (int kb = 0; kb < a.nkb; ++kb) {
     uint8_t* cur;
-    if (RS && NST == 2) {
-      // step kb is in LDS (written before the barrier); every wave is done reading step kb-1's
-      // buffer, which now takes step kb+1 (loaded into registers during step kb-1); step kb+2's
-      // loads are then in flight during this step's MFMAs
-      __syncthreads();
-      cur = lds + (kb & 1) * STAGE;
-      if (kb + 1 < a.nkb) {
-        commit(lds + ((kb + 1) & 1) * STAGE);
-        if (kb + 2 < a.nkb) fetch(kb + 2);
-      }
-    } else if (NST == 3) {
-      // step kb has landed when at most the XI + WI loads of step kb+1 are still outstanding;
-      // the barrier also means every wave is done reading step kb-1's buffer, refilled below
-      if (kb + 1 < a.nkb)
-        asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(XI + WI) : "memory");
-      else
-        asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-      const int sb = kb % 3;
-      cur = lds + sb * STAGE;
-      if (kb + 2 < a.nkb) stage(kb + 2, lds + (sb == 0 ? 2 : sb - 1) * STAGE);
-    } else if (NST == 1) {
+    if (NST == 1) {
       // single stage, serial: refill only after every wave is done with step kb-1 (the
       // overlap comes from the other resident workgroups of the CU)
       if (kb > 0) {
         __syncthreads();
-        if (RS) {
-          fetch(kb);
-          commit(lds);
-        } else {
-          stage(kb, lds);
-        }
+        stage(kb, lds);
       }
       __syncthreads();  // step kb has landed
       cur = lds;
@@ -278,7 +216,7 @@ void conv_gemm_kernel(GemmConvArgs a) {
       cur = lds + (kb & 1) * STAGE;
       if (kb + 1 < a.nkb) stage(kb + 1, lds + ((kb + 1) & 1) * STAGE);
     }
-    if (PREF && kb + 1 == a.nkb && a.has_res && a.res_prefetch) prefetch_res();
+    if (PREF && kb + 1 == a.nkb && a.has_res) prefetch_res();
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       const int chunk = kk * 4 + fq;
@@ -334,7 +272,7 @@ void conv_gemm_kernel(GemmConvArgs a) {
         float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
         const size_t o = (size_t)m * a.Cout + c0 + cc;
         if (a.has_res) {
-          const bf16x8 rr = (PREF && a.res_prefetch) ? rpre[h][j] : ld_bf16x8(a.res + o);
+          const bf16x8 rr = PREF ? rpre[h][j] : ld_bf16x8(a.res + o);
 #pragma unroll
           for (int e = 0; e < 8; ++e) v[e] += (float)rr[e];
         }
@@ -362,46 +300,6 @@ void conv_gemm_kernel(GemmConvArgs a) {
 
 // 0 auto, 1 never the GEMM path, 2 GEMM path whenever the shape allows (tests / A-B benches)
 static std::atomic<int> g_conv_path{0};
-// single-stage form for K = 64 layers (A/B switch: GALE_GEMM_SINGLE_STAGE=0 turns it off)
-static std::atomic<bool> g_gemm_single_stage{[] {
-  const char* e = getenv("GALE_GEMM_SINGLE_STAGE");
-  return !(e && *e == '0');
-}()};
-// largest k-step count that takes the single-stage form (GALE_GEMM_SS_MAXK, A/B switch; 2 and 4
-// measured 1-3 % slower at ResNet-50 batch 256 than 1)
-static std::atomic<int> g_gemm_ss_maxk{[] {
-  const char* e = getenv("GALE_GEMM_SS_MAXK");
-  return e && *e ? atoi(e) : 1;
-}()};
-static std::atomic<bool> g_gemm_res_prefetch{[] {
-  const char* e = getenv("GALE_GEMM_RES_PREFETCH");
-  return !(e && *e == '0');
-}()};
-// three-stage 128 x 64 ring for layers with >= 3 k-steps, OFF by default (GALE_GEMM_RING=1 on):
-// measured slower at batch 256 (4.86 -> 5.71 ms; batch 64: 1.78 -> 1.74 ms,
-// profiles/r2_resnet50_gemm_ab.txt) - the halved channel tile doubles the im2col traffic per
-// FLOP, which costs more than the extra step of look-ahead gains
-// 256 x 128 tiles for layers with >= 2 k-steps, OFF by default (A/B variants): GALE_GEMM_BM256=1
-// 8 waves of 64 x 64 whenever eligible, 2 the same when the tiles fill the chip twice, 3 four
-// waves of 128 x 64. Measured at ResNet-50 batch 256 (profiles/r2_resnet50_gemm_ab.txt):
-// 4.87 ms default vs 5.34 (2), 5.44 (1), 6.10 (3) - neither fewer staged bytes per FLOP nor
-// larger wave tiles at one wave per SIMD beat two 128 x 128 workgroups per CU
-static std::atomic<int> g_gemm_bm256{[] {
-  const char* e = getenv("GALE_GEMM_BM256");
-  return e && *e ? atoi(e) : 0;
-}()};
-// register-staged tiles (GALE_GEMM_RS): 0 LDS-DMA everywhere, 1 RS for the 2-stage k-loop,
-// 2 also the single-stage K = 64 form, 3 also the stem. OFF by default: ResNet-50 batch 256
-// 5.04 -> 5.23 (1) / 5.46 ms (2, 3), batch 64 1.85 -> 1.82 ms (1), profiles/r2_resnet50_gemm_ab.txt
-// - the DMA's issue cost is not what bounds the k-loop
-static std::atomic<int> g_gemm_rs{[] {
-  const char* e = getenv("GALE_GEMM_RS");
-  return e && *e ? atoi(e) : 0;
-}()};
-static std::atomic<bool> g_gemm_ring{[] {
-  const char* e = getenv("GALE_GEMM_RING");
-  return e && *e == '1';
-}()};
 void set_conv_path(int mode) { g_conv_path = mode; }
 int conv_path() { return g_conv_path; }
 
@@ -430,7 +328,6 @@ hipError_t conv2d_gemm(const ConvDesc& d, int batch, const void* x, const void* 
   a.res = static_cast<const bf16*>(res);
   a.y = y;
   a.out_f32 = d.out_f32;
-  a.res_prefetch = g_gemm_res_prefetch.load(std::memory_order_relaxed) ? 1 : 0;
   a.M = batch * d.Ho * d.Wo;
   a.H = d.H; a.W = d.W; a.Cin = d.Cin; a.HWo = d.Ho * d.Wo; a.Wo = d.Wo; a.Cout = d.Cout;
   a.KW = d.KW; a.stride = d.stride; a.pad = d.pad; a.Kpad = d.Kpad;
@@ -443,60 +340,31 @@ hipError_t conv2d_gemm(const ConvDesc& d, int batch, const void* x, const void* 
   const int m_tiles = (a.M + BM - 1) / BM;
   a.n_tiles = d.Npad / bn;
   a.nwg = m_tiles * a.n_tiles;
-  const bool one = a.nkb <= g_gemm_ss_maxk.load(std::memory_order_relaxed) &&
-                   g_gemm_single_stage.load(std::memory_order_relaxed);
-  const int big = g_gemm_bm256.load(std::memory_order_relaxed);
-  const int rsm = g_gemm_rs.load(std::memory_order_relaxed);
-  const int m256 = (a.M + 255) / 256;
-  if (!d.stem && !one && bn == 128 && big >= 4 && a.nkb >= 3 &&
-      (big == 5 || (long long)m256 * a.n_tiles >= 2 * 256)) {
-    // 8 waves of 64 x 64, three 48 KB stages (two k-steps of DMA in flight), 1 workgroup per CU
-    // (A/B: 5.0 -> 5.22 ms at batch 256, both 4 and 5; deeper look-ahead does not pay either)
-    a.nwg = m256 * a.n_tiles;
-    hipLaunchKernelGGL((conv_gemm_kernel<256, 128, false, 3>), dim3(a.nwg), dim3(512), 0, stream,
-                       a);
-  } else if (!d.stem && !one && bn == 128 && big && big < 4 &&
-      (big == 1 || big == 3 || (long long)m256 * a.n_tiles >= 2 * 256)) {
-    a.nwg = m256 * a.n_tiles;
-    if (big == 3)
-      hipLaunchKernelGGL((conv_gemm_kernel<256, 128, false, 2, 2>), dim3(a.nwg), dim3(256), 0,
-                         stream, a);
-    else
-      hipLaunchKernelGGL((conv_gemm_kernel<256, 128, false, 2>), dim3(a.nwg), dim3(512), 0,
-                         stream, a);
-  } else if (!d.stem && a.nkb >= 3 && g_gemm_ring.load(std::memory_order_relaxed)) {
-    a.n_tiles = d.Npad / 64;  // (Npad % 64 == 0 whenever a 128- or 64-wide tiling is allowed)
-    a.nwg = m_tiles * a.n_tiles;
-    hipLaunchKernelGGL((conv_gemm_kernel<BM, 64, false, 3>), dim3(a.nwg), dim3(256), 0, stream,
-                       a);
-  } else if (d.stem) {
-    const bool rs = rsm >= 3;
+  // per-shape choice: the packed stem; K = 64 (one k-step: 1x1 convs on 64 channels) in the
+  // single-stage form at 4 workgroups per CU; everything else double-buffered; 128-channel
+  // tiles when Npad allows, else 64
+  const bool one = a.nkb == 1;
+  if (d.stem) {
     if (bn == 128)
-      hipLaunchKernelGGL(rs ? (conv_gemm_kernel<BM, 128, true, 2, 2, true>)
-                            : (conv_gemm_kernel<BM, 128, true, 2>),
-                         dim3(a.nwg), dim3(256), 0, stream, a);
+      hipLaunchKernelGGL((conv_gemm_kernel<BM, 128, true, 2>), dim3(a.nwg), dim3(256), 0, stream,
+                         a);
     else
-      hipLaunchKernelGGL(rs ? (conv_gemm_kernel<BM, 64, true, 2, 2, true>)
-                            : (conv_gemm_kernel<BM, 64, true, 2>),
-                         dim3(a.nwg), dim3(256), 0, stream, a);
+      hipLaunchKernelGGL((conv_gemm_kernel<BM, 64, true, 2>), dim3(a.nwg), dim3(256), 0, stream,
+                         a);
   } else if (bn == 128) {
     if (one)
-      hipLaunchKernelGGL(rsm >= 2 ? (conv_gemm_kernel<BM, 128, false, 1, 2, true>)
-                                  : (conv_gemm_kernel<BM, 128, false, 1>),
-                         dim3(a.nwg), dim3(256), 0, stream, a);
+      hipLaunchKernelGGL((conv_gemm_kernel<BM, 128, false, 1>), dim3(a.nwg), dim3(256), 0, stream,
+                         a);
     else
-      hipLaunchKernelGGL(rsm >= 1 ? (conv_gemm_kernel<BM, 128, false, 2, 2, true>)
-                                  : (conv_gemm_kernel<BM, 128, false, 2>),
-                         dim3(a.nwg), dim3(256), 0, stream, a);
+      hipLaunchKernelGGL((conv_gemm_kernel<BM, 128, false, 2>), dim3(a.nwg), dim3(256), 0, stream,
+                         a);
   } else {
     if (one)
-      hipLaunchKernelGGL(rsm >= 2 ? (conv_gemm_kernel<BM, 64, false, 1, 2, true>)
-                                  : (conv_gemm_kernel<BM, 64, false, 1>),
-                         dim3(a.nwg), dim3(256), 0, stream, a);
+      hipLaunchKernelGGL((conv_gemm_kernel<BM, 64, false, 1>), dim3(a.nwg), dim3(256), 0, stream,
+                         a);
     else
-      hipLaunchKernelGGL(rsm >= 1 ? (conv_gemm_kernel<BM, 64, false, 2, 2, true>)
-                                  : (conv_gemm_kernel<BM, 64, false, 2>),
-                         dim3(a.nwg), dim3(256), 0, stream, a);
+      hipLaunchKernelGGL((conv_gemm_kernel<BM, 64, false, 2>), dim3(a.nwg), dim3(256), 0, stream,
+                         a);
   }
   return hipGetLastError();
 }

@@ -19,8 +19,6 @@
 // LDS row r holds 16-byte chunk s ^ ((r >> 1) & 7)). Fragment rows map pixel p of the tile to
 // patch row (p / W + kh) * (W + 2) + p % W + kw; rows past the tile's pixels read a zero row.
 // The epilogue (bias, residual, ReLU) is the same as conv_gemm's, staged through LDS.
-#include <stdlib.h>
-
 #include <algorithm>
 #include <atomic>
 
@@ -57,15 +55,13 @@ struct PatchArgs {
 
 // PRR: patch rows held in LDS (>= PR + 1 for the zero row, a multiple of 8 = one
 // wave-instruction); compile-time so the two stages are static LDS (2 workgroups per CU).
-// WM: waves along the pixels (2: 128 MFMA rows, 4 waves; 4: 256 rows, 8 waves, 1 workgroup per
-// CU - half the weight bytes per pixel, an A/B variant)
-// PB: patch buffers (2: the next block's patch loads during the last tap; 1: loaded at the block
-// boundary, exposed, but with 64-channel tiles the workgroup fits 4 per CU - an A/B variant)
-// TPS: taps per k-step (between two barriers; the weight stage holds TPS taps): 2 halves the
-// barriers per MFMA - the A/B that tests whether the barrier cadence bounds these layers
-template <int BN, int PRR, int WM = 2, int PB = 2, int TPS = 1>
-__global__ __launch_bounds__(WM * 128, WM == 2 ? (PB == 1 && BN == 64 ? (PRR > 200 ? 3 : 4) : 2) : 1)
+// (Variants measured and removed in round 3 - 256-row tiles with 8 waves, 64-channel tiles with
+// one patch buffer at 4 workgroups per CU, two taps per k-step: none faster than these tiles,
+// profiles/r2_conv_patch.txt.)
+template <int BN, int PRR>
+__global__ __launch_bounds__(256, 2)
 void conv_patch_kernel(PatchArgs a) {
+  constexpr int WM = 2, PB = 2, TPS = 1;  // waves along the pixels, patch buffers, taps per step
   constexpr int kBM = WM * 64;       // MFMA rows per tile (pixels P <= kBM; the rest read zeros)
   constexpr int WN = 2, NW = WM * WN;
   constexpr int TM = kBM / WM / 16;  // 16-pixel tiles per wave
@@ -188,10 +184,6 @@ void conv_patch_kernel(PatchArgs a) {
     // on a block's last tap, the previous block's patch buffer) is refilled below
     __syncthreads();
     const int cb = s / SPB, sl = s - cb * SPB;
-    if (PB == 1 && sl == 0 && cb > 0) {  // every wave is done with block cb-1's patch
-      stage_patch(cb, pbuf);
-      __syncthreads();
-    }
     const uint8_t* wcur = wbuf + (s & 1) * WST;
     const uint8_t* pcur = pbuf + (PB == 2 ? (cb & 1) * PST : 0);
     if (s + 1 < a.nsteps) {
@@ -201,7 +193,6 @@ void conv_patch_kernel(PatchArgs a) {
 #pragma unroll
     for (int tt = 0; tt < TPS; ++tt) {
       const int tap = sl * TPS + tt;
-      if (TPS > 1 && tap >= 9) break;  // (a partial last step; TPS = 1 never)
       const uint8_t* wtap = wcur + tt * BN * 128;
       const int kh = tap / 3;
       const int toff = kh * a.PW + (tap - kh * 3);
@@ -284,27 +275,21 @@ void conv_patch_kernel(PatchArgs a) {
   }
 }
 
-// the patch-row capacities compiled (2 workgroups per CU at BN = 128 up to 184 rows; 272 for
-// the 256-row tiles)
-constexpr int kPrr[4] = {152, 184, 240, 272};
+// the patch-row capacities compiled (2 workgroups per CU at BN = 128 up to 184 rows)
+constexpr int kPrr[3] = {152, 184, 240};
 
-int patch_tile_rows(const ConvDesc& d, int bm) {
-  // largest divisor of H whose rows hold <= bm pixels
-  for (int tr = bm / d.W; tr >= 1; --tr)
+int patch_tile_rows(const ConvDesc& d) {
+  // largest divisor of H whose rows hold <= 128 pixels
+  for (int tr = 128 / d.W; tr >= 1; --tr)
     if (d.H % tr == 0) return tr;
   return 0;
 }
 
 // whole images per tile: several when one image's rows fill less than half the tile (7x7: 2 x 49
-// of 128 MFMA rows; GALE_CONV_PATCH_MULTI=0 keeps one image per tile)
-std::atomic<int> g_patch_multi{[] {
-  const char* e = getenv("GALE_CONV_PATCH_MULTI");
-  return !(e && *e == '0');
-}()};
-
-int patch_images(const ConvDesc& d, int bm, int tr) {
-  if (tr != d.H || !g_patch_multi.load(std::memory_order_relaxed)) return 1;
-  return std::max(1, bm / (d.H * d.W));
+// of 128 MFMA rows)
+int patch_images(const ConvDesc& d, int tr) {
+  if (tr != d.H) return 1;
+  return std::max(1, 128 / (d.H * d.W));
 }
 
 int patch_prr(int PR) {
@@ -313,48 +298,15 @@ int patch_prr(int PR) {
   return 0;
 }
 
-// GALE_CONV_PATCH_BM: 256 = 8-wave 256-row tiles for the 128-channel layers (A/B, off: 28x28
-// 77 -> 90 us, 14x14 77 -> 79 us - halving the weight bytes per pixel does not pay for one
-// workgroup per CU; profiles/r2_conv_patch.txt)
-std::atomic<int> g_patch_bm{[] {
-  const char* e = getenv("GALE_CONV_PATCH_BM");
-  return e && *e ? atoi(e) : 128;
-}()};
-
-int patch_bm(int bn) { return bn == 128 && g_patch_bm.load(std::memory_order_relaxed) == 256 ? 256 : 128; }
-
-// GALE_CONV_PATCH_OCC=4: 64-channel tiles with one patch buffer (4 workgroups per CU) for every
-// eligible layer (A/B, off: 14x14 77 -> 80 us, 28x28 and 56x56 unchanged vs the default paths)
-std::atomic<int> g_patch_occ{[] {
-  const char* e = getenv("GALE_CONV_PATCH_OCC");
-  return e && *e ? atoi(e) : 2;
-}()};
-
-// GALE_CONV_PATCH_TPS: 1 = 64-channel tiles everywhere eligible, one tap per k-step; 2 = the same
-// with two taps per k-step (half the barriers per MFMA). The A/B pair for the barrier-cadence
-// question (measured: 103-105 -> 98 us per layer, ~5 %; both below the default 128-channel tiles
-// at 79-81 us, profiles/r2_conv_patch.txt); 0 (default) = neither.
-std::atomic<int> g_patch_tps{[] {
-  const char* e = getenv("GALE_CONV_PATCH_TPS");
-  return e && *e ? atoi(e) : 0;
-}()};
-
-int patch_bn(const ConvDesc& d) {
-  if (g_patch_tps.load(std::memory_order_relaxed) > 0 && d.Npad % 64 == 0) return 64;
-  if (g_patch_occ.load(std::memory_order_relaxed) == 4 && d.Npad % 64 == 0) return 64;
-  return (d.Npad % 128 == 0) ? 128 : 64;
-}
+int patch_bn(const ConvDesc& d) { return (d.Npad % 128 == 0) ? 128 : 64; }
 
 }  // namespace
 
-// GALE_CONV_PATCH: 0 off, 1 (default) the 128-channel tiles (ResNet-50 28x28 and 14x14 conv2:
-// 90 -> 77 us and 86 -> 76 us per layer at batch 256), 2 also the 64-channel tiles (the 56x56
-// conv2 measured 104-110 -> 125-127 us there: one input block per tile leaves the patch load
-// exposed, so those stay on conv_gemm; profiles/r2_conv_patch.txt)
-static std::atomic<int> g_conv_patch{[] {
-  const char* e = getenv("GALE_CONV_PATCH");
-  return e && *e ? atoi(e) : 1;
-}()};
+// conv_patch mode (set_conv_patch): 0 off, 1 (default) the 128-channel tiles (ResNet-50 28x28
+// and 14x14 conv2: 90 -> 77 us and 86 -> 76 us per layer at batch 256), 2 also the 64-channel
+// tiles (the 56x56 conv2 measured 104-110 -> 125-127 us there: one input block per tile leaves
+// the patch load exposed, so those stay on conv_gemm; profiles/r2_conv_patch.txt)
+static std::atomic<int> g_conv_patch{1};
 
 void set_conv_patch(int mode) { g_conv_patch = mode; }
 
@@ -365,21 +317,16 @@ bool conv_patch_supported(const ConvDesc& d, int batch, bool has_res) {
   if (d.Cin % 64 != 0 || d.K != 9 * d.Cin || d.Kpad != d.K) return false;
   if (d.Ho != d.H || d.Wo != d.W || d.W > 128 || d.Cout % 8 != 0) return false;
   const int bn = patch_bn(d);
-  const bool occ4 = g_patch_occ.load(std::memory_order_relaxed) == 4 ||
-                    g_patch_tps.load(std::memory_order_relaxed) > 0;
   if (d.Npad % bn != 0 || d.Npad < d.Cout) return false;
-  if (bn == 64 && !occ4 && g_conv_patch.load(std::memory_order_relaxed) < 2) return false;
+  if (bn == 64 && g_conv_patch.load(std::memory_order_relaxed) < 2) return false;
   if (has_res && (d.res_C != d.Cout || d.res_stride != 1 || d.res_H != d.H || d.res_W != d.W))
     return false;
-  const int bm = patch_bm(bn);
-  const int tr = patch_tile_rows(d, bm);
-  const int img = tr >= 1 ? patch_images(d, bm, tr) : 1;
+  const int tr = patch_tile_rows(d);
+  const int img = tr >= 1 ? patch_images(d, tr) : 1;
   // (a tile below 3/4 of its MFMA rows wastes too much)
-  if (tr < 1 || img * tr * d.W * 4 < bm * 3 - 16) return false;
+  if (tr < 1 || img * tr * d.W * 4 < 128 * 3 - 16) return false;
   const int prr = patch_prr(img * (tr + 2) * (d.W + 2));
-  if (prr == 0 || (bm == 128 && bn == 128 && prr > 184) || (bm == 256 && prr != 272))
-    return false;
-  if (g_patch_tps.load(std::memory_order_relaxed) == 2 && prr > 184) return false;
+  if (prr == 0 || (bn == 128 && prr > 184)) return false;
   return (long long)batch * d.H * d.W * d.Cin < (1ll << 31) &&
          (long long)batch * d.H * d.W * d.Cout < (1ll << 31);
 }
@@ -394,49 +341,28 @@ hipError_t conv2d_patch(const ConvDesc& d, int batch, const void* x, const void*
   a.y = static_cast<bf16*>(y);
   a.H = d.H; a.W = d.W; a.Cin = d.Cin; a.Cout = d.Cout; a.Kpad = d.Kpad;
   const int bn = patch_bn(d);
-  const int bm = patch_bm(bn);
-  a.TR = patch_tile_rows(d, bm);
+  a.TR = patch_tile_rows(d);
   if (a.TR < 1) return hipErrorInvalidValue;
-  a.IMG = patch_images(d, bm, a.TR);
+  a.IMG = patch_images(d, a.TR);
   a.B = batch;
   a.P = a.IMG * a.TR * d.W;
   a.PW = d.W + 2;
   a.PR1 = (a.TR + 2) * a.PW;
   a.PR = a.IMG * a.PR1;
   a.rblocks = d.H / a.TR;
-  const int tps = g_patch_tps.load(std::memory_order_relaxed) == 2 ? 2 : 1;
-  a.nsteps = (tps == 2 ? 5 : 9) * (d.Cin / 64);  // k-steps: ceil(9 / taps per step) per block
+  a.nsteps = 9 * (d.Cin / 64);  // k-steps: one tap of 64 input channels each
   a.relu = d.relu;
   a.has_res = d.has_res && res != nullptr;
   a.n_tiles = d.Npad / bn;
   a.nwg = (batch + a.IMG - 1) / a.IMG * a.rblocks * a.n_tiles;
   const int prr = patch_prr(a.PR);
-  if (a.P > bm || prr == 0) return hipErrorInvalidValue;
-  if (bm == 256) {
-    if (prr != 272) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((conv_patch_kernel<128, 272, 4>), dim3(a.nwg), dim3(512), 0, stream, a);
-  } else if (bn == 128) {
+  if (a.P > 128 || prr == 0) return hipErrorInvalidValue;
+  if (bn == 128) {
     if (prr > 184) return hipErrorInvalidValue;
     if (prr == 152)
       hipLaunchKernelGGL((conv_patch_kernel<128, 152>), dim3(a.nwg), dim3(256), 0, stream, a);
     else
       hipLaunchKernelGGL((conv_patch_kernel<128, 184>), dim3(a.nwg), dim3(256), 0, stream, a);
-  } else if (tps == 2) {
-    if (prr == 152)
-      hipLaunchKernelGGL((conv_patch_kernel<64, 152, 2, 2, 2>), dim3(a.nwg), dim3(256), 0, stream,
-                         a);
-    else if (prr == 184)
-      hipLaunchKernelGGL((conv_patch_kernel<64, 184, 2, 2, 2>), dim3(a.nwg), dim3(256), 0, stream,
-                         a);
-    else
-      return hipErrorInvalidValue;
-  } else if (g_patch_occ.load(std::memory_order_relaxed) == 4) {
-    if (prr == 152)
-      hipLaunchKernelGGL((conv_patch_kernel<64, 152, 2, 1>), dim3(a.nwg), dim3(256), 0, stream, a);
-    else if (prr == 184)
-      hipLaunchKernelGGL((conv_patch_kernel<64, 184, 2, 1>), dim3(a.nwg), dim3(256), 0, stream, a);
-    else
-      hipLaunchKernelGGL((conv_patch_kernel<64, 240, 2, 1>), dim3(a.nwg), dim3(256), 0, stream, a);
   } else {
     if (prr == 152)
       hipLaunchKernelGGL((conv_patch_kernel<64, 152>), dim3(a.nwg), dim3(256), 0, stream, a);

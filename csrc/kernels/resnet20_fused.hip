@@ -31,8 +31,6 @@
 // Reference parity: the model the reference serves is an opaque SavedModel fetched as
 // "output/Softmax:0" (InferenceBolt.java:81-86); numerics equal the layer-by-layer gale plan
 // (same rounding points) and are checked against the fp32 / fp8-emulation oracles in tests.
-#include <stdlib.h>
-
 #include "common.cuh"
 #include "gale/kernels.h"
 
@@ -532,12 +530,7 @@ hipError_t resnet20_fused_forward(const ResNet20Params& p, int batch, const floa
   // 8 waves. bf16 with no more images than CUs: the 8-wave form (each image gets twice the
   // waves, weights prefetched into LDS; measured 62.3 -> 58.0 us at batch 1,
   // profiles/r1_resnet20_waves_ab.txt). fp8 stays on 4 waves (its 8-wave form measured slower).
-  // GALE_R20_WAVES=4|8 pins the choice (A/B benches).
-  static const int forced = [] {
-    const char* e = getenv("GALE_R20_WAVES");
-    return e ? atoi(e) : 0;
-  }();
-  const int nw = forced == 4 || forced == 8 ? forced : (!f8 && batch <= cus ? 8 : 4);
+  const int nw = !f8 && batch <= cus ? 8 : 4;
   const int grid_cap = nw == 8 ? cus : 2 * cus;
   const int grid = batch < grid_cap ? batch : grid_cap;
   const size_t lds = (size_t)kElems * (f8 ? 1 : 2) + (nw == 8 ? (size_t)kWeightLdsBytes : 0);

@@ -1096,25 +1096,16 @@ void Engine::slo_step() {
   // fetch/decode is the tight stage (then the batchers look empty): a latency miss under
   // overload needs capacity (bigger batches), not smaller ones. Unacknowledged records beyond
   // what the replicas hold in flight at the current batch size count as backlog.
-  static const bool use_lag = [] {  // (A/B switch: GALE_SLO_LAG_BACKLOG=0 ignores the lag)
-    const char* e = getenv("GALE_SLO_LAG_BACKLOG");
-    return !(e && *e == '0');
-  }();
   int64_t unacked = 0;
-  if (use_lag)
-    for (const PartitionOffsets& o : partition_offsets()) unacked += o.lag;
+  for (const PartitionOffsets& o : partition_offsets()) unacked += o.lag;
   const int64_t in_flight = (int64_t)b * (int64_t)replicas_.size() * 3;
   const bool backlog =
       (int64_t)queued > (int64_t)b * (int64_t)replicas_.size() || unacked > 2 * in_flight;
   // Batches leaving (nearly) full: they form faster than the window, so the latency is set by
   // the replicas' capacity, not by batching delay - shrinking them would only cut capacity (the
   // fp8 ResNet-20 at 1.0 M img/s fell into that cycle: mean batch 256 -> 110, p99 2 -> 8-60 ms,
-  // profiles/r2_slo_controller_ab.txt). A/B switch: GALE_SLO_FULL_BATCH=0 ignores it.
-  static const bool use_fill = [] {
-    const char* e = getenv("GALE_SLO_FULL_BATCH");
-    return !(e && *e == '0');
-  }();
-  const bool full = use_fill && mean_batch >= 0.9 * b;
+  // profiles/r2_slo_controller_ab.txt).
+  const bool full = mean_batch >= 0.9 * b;
   if (p99_ms > cfg_.slo_p99_ms) {
     if (backlog || full) {
       b = std::min(maxb, b + std::max(1, maxb / 8));  // overload: capacity first

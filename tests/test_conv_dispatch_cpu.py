@@ -1,5 +1,5 @@
 """Host-side conv dispatch rules (no GPU needed): which layer shapes take the LDS halo-patch 3x3
-kernel (conv_patch.hip) under each GALE_CONV_PATCH mode, and which stay on the im2col GEMM."""
+kernel (conv_patch.hip) under each set_conv_patch mode, and which stay on the im2col GEMM."""
 
 import torch
 

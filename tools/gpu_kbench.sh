@@ -47,12 +47,3 @@ for step in ${KB_STEPS2:-}; do
       done ;;
   esac
 done
-for step in ${KB_STEPS3:-}; do
-  case $step in
-    r20waves)
-      for nw in 4 8; do for dt in bf16 fp8; do
-        GALE_R20_WAVES=$nw timeout -k 10 180 python tools/bench_forward.py --model resnet20 --dtype $dt --batches 1,32,128,256,1024,4096 > gpurun_out/kb_r20_w${nw}_$dt.log 2>&1 || { tail -20 gpurun_out/kb_r20_w${nw}_$dt.log; exit 1; }
-        sed "s/^{/{\"waves\": $nw, /" gpurun_out/kb_r20_w${nw}_$dt.log | grep '^{'
-      done; done ;;
-  esac
-done
