@@ -85,6 +85,8 @@ def parse_args(argv=None):
                     help="stub replicas skip parsing (measures the host Kafka/codec path only)")
     ap.add_argument("--gpu-encode", action=argparse.BooleanOptionalAction, default=True,
                     help="format the prediction text (Java Float.toString) on the GPU")
+    ap.add_argument("--graph", action=argparse.BooleanOptionalAction, default=True,
+                    help="replay each batch's forward as a captured hipGraph (else eager)")
     ap.add_argument("--gpu-ingest", action=argparse.BooleanOptionalAction, default=True,
                     help="CRC32C + image counting of fetch buffers on the GPU (host reads only "
                          "Kafka framing)")
@@ -485,6 +487,7 @@ def main(argv=None) -> int:
                      output_partition=rank if a.local_output and world > 1 else -1,
                      producer_buffer_mb=a.producer_buffer_mb,
                      locality_split=a.locality_split, fetch_min_bytes=a.fetch_min_bytes,
+                     use_graph=a.graph,
                      producer_request_kb=a.producer_request_kb)
     devices = (list(range(local_gpus)) if local_gpus > 1 else [local_rank]) if use_gpu else None
     # ONE engine: warm-up and timed window are the same steady-state pipeline (connections,
