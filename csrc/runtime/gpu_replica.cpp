@@ -28,7 +28,6 @@ GpuReplica::GpuReplica(std::shared_ptr<Executor> exec, int H, int W, int C, int 
     throw std::invalid_argument("GpuReplica: executor output is not fp32 [classes]");
   check_hip(hipSetDevice(exec_->device()), "hipSetDevice");
   check_hip(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "hipStreamCreate");
-  check_hip(hipStreamCreateWithFlags(&copy_stream_, hipStreamNonBlocking), "hipStreamCreate");
   const int mb = exec_->max_batch();
   slots_.resize((size_t)exec_->slots());
   for (Slot& s : slots_) {
@@ -42,7 +41,6 @@ GpuReplica::GpuReplica(std::shared_ptr<Executor> exec, int H, int W, int C, int 
     check_hip(hipEventCreateWithFlags(&s.done, hipEventDisableTiming |
                                                    (wait_poll_us_ < 0 ? hipEventBlockingSync : 0)),
               "hipEventCreate");
-    check_hip(hipEventCreateWithFlags(&s.staged, hipEventDisableTiming), "hipEventCreate");
     // initial text capacity: ~12 bytes per number (Java Float.toString + ",") x a full batch
     ensure_device(s, (size_t)mb * H * W * C * 12 + 4096);
     ensure_tiles(s, (int)(((size_t)mb * H * W * C * 12) / kJsonTileBytes) + 2 * mb, 0);
@@ -61,11 +59,6 @@ GpuReplica::~GpuReplica() {
     if (s.h_out) hipHostFree(s.h_out);
     if (s.h_text) hipHostFree(s.h_text);
     if (s.done) hipEventDestroy(s.done);
-    if (s.staged) hipEventDestroy(s.staged);
-  }
-  if (copy_stream_) {
-    hipStreamSynchronize(copy_stream_);
-    hipStreamDestroy(copy_stream_);
   }
   if (stream_) hipStreamDestroy(stream_);
 }
@@ -171,7 +164,7 @@ void GpuReplica::submit(Batch& b) {
   for (size_t i = 0; i < spans.size(); ++i) {
     span_dev[i] = doff;
     check_hip(hipMemcpyAsync(s.d_bytes + doff, spans[i].base + spans[i].lo,
-                             spans[i].hi - spans[i].lo, hipMemcpyHostToDevice, copy_stream_),
+                             spans[i].hi - spans[i].lo, hipMemcpyHostToDevice, stream_),
               "H2D span");
     doff += ((spans[i].hi - spans[i].lo) + 15) & ~(size_t)15;
   }
@@ -222,14 +215,12 @@ void GpuReplica::submit(Batch& b) {
   }
   if (hoff)
     check_hip(hipMemcpyAsync(s.d_bytes + staged_dev, s.h_bytes, hoff, hipMemcpyHostToDevice,
-                             copy_stream_),
+                             stream_),
               "H2D staged");
   const size_t meta = reinterpret_cast<char*>(s.h_tile_rec + ntiles) -
                       reinterpret_cast<char*>(s.h_recs);
-  check_hip(hipMemcpyAsync(s.d_recs, s.h_recs, meta, hipMemcpyHostToDevice, copy_stream_),
+  check_hip(hipMemcpyAsync(s.d_recs, s.h_recs, meta, hipMemcpyHostToDevice, stream_),
             "H2D recs");
-  check_hip(hipEventRecord(s.staged, copy_stream_), "hipEventRecord(staged)");
-  check_hip(hipStreamWaitEvent(stream_, s.staged, 0), "hipStreamWaitEvent");
   check_hip(json_parse_instances(nrec, ntiles, s.d_recs, s.d_tile_rec, s.d_bytes, H_, W_, C_,
                                  s.d_tiles,
                                  static_cast<float*>(exec_->input(slot)), stream_),
@@ -292,7 +283,6 @@ void GpuReplica::recover() {
   // drain whatever the failed batches left queued on both streams, then clear the (non-sticky)
   // error state; a sticky device fault makes these calls fail and the supervisor gives up
   check_hip(hipSetDevice(exec_->device()), "recover: hipSetDevice");
-  check_hip(hipStreamSynchronize(copy_stream_), "recover: copy stream");
   check_hip(hipStreamSynchronize(stream_), "recover: compute stream");
   (void)hipGetLastError();
   next_slot_ = 0;

@@ -139,7 +139,6 @@ class GpuReplica : public Replica {
     float* h_out = nullptr;      // pinned softmax rows
     uint8_t* h_text = nullptr;   // pinned, device-mapped prediction text slots (gpu_encode)
     hipEvent_t done = nullptr;
-    hipEvent_t staged = nullptr;  // H2D of this slot's text finished (copy stream)
     int64_t t_submit_ns = 0;
   };
   void ensure_host(Slot& s, size_t bytes);
@@ -150,8 +149,12 @@ class GpuReplica : public Replica {
   bool use_graph_;
   int wait_poll_us_ = 0;
   bool gpu_encode_ = false;
-  hipStream_t stream_ = nullptr;       // parse + forward + D2H
-  hipStream_t copy_stream_ = nullptr;  // H2D of batch k+1 overlaps compute of batch k
+  // H2D of the batch's metadata (and of any text not already resident) + parse + forward + D2H,
+  // in order on ONE stream: with GPU ingest the text is resident, so a separate copy stream
+  // bought no overlap, and its cross-stream wait (hipStreamWaitEvent) was where rocprofv3's
+  // kernel tracing crashed under the default 6-replica concurrency; overlap comes from the
+  // replicas' streams running side by side
+  hipStream_t stream_ = nullptr;
   std::vector<Slot> slots_;
   int next_slot_ = 0;
   int locality_ = -1;

@@ -26,6 +26,7 @@ from __future__ import annotations
 import argparse
 import json
 import logging
+import os
 import sys
 import time
 from dataclasses import fields
@@ -97,7 +98,12 @@ def cmd_run(argv: List[str]) -> int:
     if cfg.profile:
         import subprocess
 
-        return subprocess.call(profile_command(cfg, argv))
+        # one HW queue per HIP stream in the profiled child: rocprofv3's queue interception
+        # crashed when several of the engine's streams shared a HW queue and submitted
+        # concurrently (GPU_MAX_HW_QUEUES=4 default; profiles/r3_e2e_kernel_stats_default.csv)
+        env = dict(os.environ)
+        env.setdefault("GPU_MAX_HW_QUEUES", "16")
+        return subprocess.call(profile_command(cfg, argv), env=env)
     logging.basicConfig(level=getattr(logging, cfg.log_level.upper(), logging.INFO),
                         format="%(asctime)s %(name)s %(levelname)s %(message)s")
     try:

@@ -89,9 +89,11 @@ class Engine:
         if cfg.gpu_ingest:
             # fetch buffers of each device's sources are mirrored on that device once and
             # parsed in place
+            # one lane (stream + staging) per thread that runs the ingest: the decode workers,
+            # or the sources themselves when there are none
+            lanes = cfg.decode_threads if cfg.decode_threads > 0 else cfg.source_parallelism
             for dev in devs:
-                self._native.enable_gpu_ingest(dev, max(1, cfg.decode_threads) +
-                                               cfg.source_parallelism, 20)
+                self._native.enable_gpu_ingest(dev, max(1, lanes), 20)
 
     def _build_gpu_replicas(self, devices: Optional[Sequence[int]], params: Optional[dict]):
         import torch
