@@ -32,10 +32,8 @@ GpuIngest::~GpuIngest() {
   hipSetDevice(device_);
   for (auto& L : lanes_) {
     if (L->stream) hipStreamSynchronize(L->stream);
-    if (L->h_in) hipHostFree(L->h_in);
-    if (L->d_in) hipFree(L->d_in);
-    if (L->h_out) hipHostFree(L->h_out);
-    if (L->d_out) hipFree(L->d_out);
+    if (L->h_io) hipHostFree(L->h_io);
+    if (L->d_io) hipFree(L->d_io);
     if (L->d_counts) hipFree(L->d_counts);
     if (L->done) hipEventDestroy(L->done);
     if (L->stream) hipStreamDestroy(L->stream);
@@ -43,23 +41,16 @@ GpuIngest::~GpuIngest() {
   if (d_tables_) hipFree(d_tables_);
 }
 
-void GpuIngest::grow(Lane& L, size_t in_bytes, size_t out_bytes, size_t tiles) {
+void GpuIngest::grow(Lane& L, size_t io_bytes, size_t tiles) {
   auto up = [](size_t want, size_t have) {
     return (std::max(want, have * 2) + 4095) & ~(size_t)4095;
   };
-  if (in_bytes > L.in_cap) {
-    if (L.h_in) hipHostFree(L.h_in);
-    if (L.d_in) hipFree(L.d_in);
-    L.in_cap = up(in_bytes, L.in_cap);
-    check_hip(hipHostMalloc(reinterpret_cast<void**>(&L.h_in), L.in_cap), "ingest: h_in");
-    check_hip(hipMalloc(reinterpret_cast<void**>(&L.d_in), L.in_cap), "ingest: d_in");
-  }
-  if (out_bytes > L.out_cap) {
-    if (L.h_out) hipHostFree(L.h_out);
-    if (L.d_out) hipFree(L.d_out);
-    L.out_cap = up(out_bytes, L.out_cap);
-    check_hip(hipHostMalloc(reinterpret_cast<void**>(&L.h_out), L.out_cap), "ingest: h_out");
-    check_hip(hipMalloc(reinterpret_cast<void**>(&L.d_out), L.out_cap), "ingest: d_out");
+  if (io_bytes > L.io_cap) {
+    if (L.h_io) hipHostFree(L.h_io);
+    if (L.d_io) hipFree(L.d_io);
+    L.io_cap = up(io_bytes, L.io_cap);
+    check_hip(hipHostMalloc(reinterpret_cast<void**>(&L.h_io), L.io_cap), "ingest: h_io");
+    check_hip(hipMalloc(reinterpret_cast<void**>(&L.d_io), L.io_cap), "ingest: d_io");
   }
   if (tiles * sizeof(int) > L.counts_cap) {
     if (L.d_counts) hipFree(L.d_counts);
@@ -124,15 +115,16 @@ void GpuIngest::run(int lane, const kafka::Fetched& f, uint8_t* dev, bool check_
   }
   const size_t nc = chunks.size(), nr = rec_of.size();
   if (nc == 0 && nr == 0) return;
-  const size_t in_chunks = align16(nc * sizeof(CrcChunk)), in_recs = align16(nr * sizeof(JsonRecord));
-  const size_t in_bytes = in_chunks + in_recs + (size_t)ntiles * sizeof(int);
-  const size_t out_crc = align16(nc * 4), out_tok = align16(nr * 4);
-  const size_t out_bytes = out_crc + out_tok + nr * sizeof(JsonRecord);
+  const size_t o_tiles = align16(nc * sizeof(CrcChunk));
+  const size_t o_recs = o_tiles + align16((size_t)ntiles * sizeof(int));
+  const size_t o_tok = o_recs + nr * sizeof(JsonRecord);  // (JsonRecord is 32 bytes)
+  const size_t o_crc = o_tok + align16(nr * 4);
+  const size_t io_bytes = o_crc + align16(nc * 4);
   check_hip(hipSetDevice(device_), "ingest: hipSetDevice");
-  grow(L, in_bytes + 16, out_bytes + 16, (size_t)ntiles + 1);
-  CrcChunk* hc = reinterpret_cast<CrcChunk*>(L.h_in);
-  JsonRecord* hr = reinterpret_cast<JsonRecord*>(L.h_in + in_chunks);
-  int* ht = reinterpret_cast<int*>(L.h_in + in_chunks + in_recs);
+  grow(L, io_bytes + 16, (size_t)ntiles + 1);
+  CrcChunk* hc = reinterpret_cast<CrcChunk*>(L.h_io);
+  int* ht = reinterpret_cast<int*>(L.h_io + o_tiles);
+  JsonRecord* hr = reinterpret_cast<JsonRecord*>(L.h_io + o_recs);
   if (nc) memcpy(hc, chunks.data(), nc * sizeof(CrcChunk));
   int tile = 0;
   for (size_t j = 0; j < nr; ++j) {
@@ -149,36 +141,32 @@ void GpuIngest::run(int lane, const kafka::Fetched& f, uint8_t* dev, bool check_
     for (int t = 0; t < nt; ++t) ht[tile + t] = (int)j;
     tile += nt;
   }
-  // ---- device: text span -> mirror, tables, CRC windows, token counts, results back
+  memset(L.h_io + o_tok, 0, nr * 4);  // token counters start at zero (no device memset)
+  // ---- device: text span -> mirror, plan, CRC windows, token counts, results back
   lo &= ~(size_t)15;
   hipStream_t st = L.stream;
   check_hip(hipMemcpyAsync(dev + lo, f.buf.get() + lo, hi - lo, hipMemcpyHostToDevice, st),
             "ingest: H2D text");
-  check_hip(hipMemcpyAsync(L.d_in, L.h_in, in_bytes, hipMemcpyHostToDevice, st),
-            "ingest: H2D plan");
-  uint32_t* d_crc = reinterpret_cast<uint32_t*>(L.d_out);
-  int* d_tok = reinterpret_cast<int*>(L.d_out + out_crc);
-  JsonRecord* d_rec = reinterpret_cast<JsonRecord*>(L.d_in + in_chunks);
-  if (nr) check_hip(hipMemsetAsync(d_tok, 0, nr * 4, st), "ingest: memset");
+  check_hip(hipMemcpyAsync(L.d_io, L.h_io, o_crc, hipMemcpyHostToDevice, st), "ingest: H2D plan");
+  uint32_t* d_crc = reinterpret_cast<uint32_t*>(L.d_io + o_crc);
+  int* d_tok = reinterpret_cast<int*>(L.d_io + o_tok);
+  JsonRecord* d_rec = reinterpret_cast<JsonRecord*>(L.d_io + o_recs);
   if (nc)
-    check_hip(crc32c_chunks(dev, reinterpret_cast<const CrcChunk*>(L.d_in), (int)nc, d_tables_,
+    check_hip(crc32c_chunks(dev, reinterpret_cast<const CrcChunk*>(L.d_io), (int)nc, d_tables_,
                             d_crc, st),
               "ingest: crc32c_chunks");
   if (nr)
     check_hip(json_count_records((int)nr, ntiles, d_rec,
-                                 reinterpret_cast<const int*>(L.d_in + in_chunks + in_recs), dev,
-                                 L.d_counts, d_tok, st),
+                                 reinterpret_cast<const int*>(L.d_io + o_tiles), dev, L.d_counts,
+                                 d_tok, st),
               "ingest: json_count_records");
-  check_hip(hipMemcpyAsync(L.h_out, L.d_out, out_crc + out_tok, hipMemcpyDeviceToHost, st),
+  check_hip(hipMemcpyAsync(L.h_io + o_recs, L.d_io + o_recs, io_bytes - o_recs,
+                           hipMemcpyDeviceToHost, st),
             "ingest: D2H results");
-  if (nr)
-    check_hip(hipMemcpyAsync(L.h_out + out_crc + out_tok, d_rec, nr * sizeof(JsonRecord),
-                             hipMemcpyDeviceToHost, st),
-              "ingest: D2H status");
   check_hip(hipEventRecord(L.done, st), "ingest: event");
   wait(L);
   // ---- host: join the windows of each batch and compare; images from the element counts
-  const uint32_t* crc = reinterpret_cast<const uint32_t*>(L.h_out);
+  const uint32_t* crc = reinterpret_cast<const uint32_t*>(L.h_io + o_crc);
   for (size_t b = 0; b < batch_chunks.size(); ++b) {
     const kafka::BatchSpan& bs = f.batches[b];
     uint32_t raw = 0;
@@ -192,8 +180,8 @@ void GpuIngest::run(int lane, const kafka::Fetched& f, uint8_t* dev, bool check_
     kafka::Reader cr(f.buf.get() + bs.off + kafka::kBatchCrcOffset, 4);
     io.batch_ok[b] = got == cr.u32();
   }
-  const int* tok = reinterpret_cast<const int*>(L.h_out + out_crc);
-  const JsonRecord* rst = reinterpret_cast<const JsonRecord*>(L.h_out + out_crc + out_tok);
+  const int* tok = reinterpret_cast<const int*>(L.h_io + o_tok);
+  const JsonRecord* rst = reinterpret_cast<const JsonRecord*>(L.h_io + o_recs);
   const int64_t per = (int64_t)H * W * C;
   for (size_t j = 0; j < nr; ++j) {
     const size_t i = (size_t)rec_of[j];

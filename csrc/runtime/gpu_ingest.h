@@ -27,16 +27,17 @@ class GpuIngest : public Ingest {
     std::mutex mu;
     hipStream_t stream = nullptr;
     hipEvent_t done = nullptr;
-    uint8_t* h_in = nullptr;  // pinned: [CrcChunk x nc][JsonRecord x nr][tile_rec x nt]
-    uint8_t* d_in = nullptr;
-    size_t in_cap = 0;
-    uint8_t* h_out = nullptr;  // pinned: [crc u32 x nc][tokens i32 x nr][JsonRecord x nr]
-    uint8_t* d_out = nullptr;
-    size_t out_cap = 0;
+    // one pinned staging buffer and its device image:
+    //   [CrcChunk x nc][tile_rec x nt][JsonRecord x nr][tokens i32 x nr][crc u32 x nc]
+    // the host writes the plan and zeroed token counters, ONE H2D copies up to the tokens, ONE
+    // D2H copies back [JsonRecord..crc] (per-record status, element counts, window CRCs)
+    uint8_t* h_io = nullptr;
+    uint8_t* d_io = nullptr;
+    size_t io_cap = 0;
     int* d_counts = nullptr;  // per-tile token counts (scratch)
     size_t counts_cap = 0;
   };
-  void grow(Lane& L, size_t in_bytes, size_t out_bytes, size_t tiles);
+  void grow(Lane& L, size_t io_bytes, size_t tiles);
   void wait(Lane& L);
   int device_, poll_us_;
   uint32_t* d_tables_ = nullptr;
