@@ -417,9 +417,9 @@ def main(argv=None) -> int:
                     if q else 0
             pinned_cpus = pin_to_gpu_numa(local_rank, a.cpus_per_rank)
     if world > 1:
-        nccl = use_gpu and not a.shared_gpu_rehearsal
-        dist.init_process_group(backend="nccl" if nccl else "gloo",
-                                device_id=torch.device("cuda", local_rank) if nccl else None)
+        from gale.parallel.group import init_rank_group
+
+        init_rank_group(local_rank, use_gpu, shared_gpu=a.shared_gpu_rehearsal)
 
     from gale._native import native
     from gale.config import GaleConfig

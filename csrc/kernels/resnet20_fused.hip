@@ -10,15 +10,18 @@
 // fragments.
 //
 // Two instantiations:
-//   bf16: v_mfma_f32_16x16x32_bf16, activations bf16 in LDS (78,464 B -> 2 workgroups per CU)
+//   bf16: v_mfma_f32_16x16x32_bf16, activations bf16 in LDS (76,576 B -> 2 workgroups per CU)
 //   fp8 : v_mfma_f32_16x16x32_fp8_fp8, OCP e4m3 weights (per-channel scale) and activations
-//         (per-tensor scales calibrated offline, gale/models/quant.py) -> 39,232 B of LDS
+//         (per-tensor scales calibrated offline, gale/models/quant.py) -> 38,288 B of LDS
 //         (half the bytes per B fragment). Epilogue: acc*wscale[c]*s_in + bias + res*s_res, ReLU,
 //         requantise with 1/s_out (saturating at +-448).
 // LDS plan (element offsets scale with the element size EB), NHWC with a zero border so the 3x3
-// windows need no bounds checks (padded layouts Hp x Wp x C):
-//   R0 [0, 18496 EB)          X1 34x34x16 (stage-1 block input/output)  | stage 3: T3, X3 10x10x64
-//   R1 [18496, 39232 EB)      IN 34x34x3 (stem input) -> T1 34x34x16    | stage 2: T2, X2 18x18x32
+// windows need no bounds checks (padded layouts Hp x Wp x C, see Layouts):
+//            stage 1                    stage 2                        stage 3
+//   R0 [0, 18496)       X1 34x34x16      X2 18x18x32 (after conv 7)     (X2: conv 14's shortcut)
+//   R1 [18496, ...)     IN 34x34x3->T1   T2 18x18x32, SC 16x16x16       T3, X3 10x10x64
+// SC is the option-A shortcut of block 2.1 (X1 subsampled, channels 0-15), copied out by conv 7
+// so that X1 is dead once conv 7 is done and the padded stage-2 images fit.
 // Block conv2 writes its output in place over its residual (each lane reads the residual of the
 // pixel/channels it then writes, and no other lane reads that buffer in the same conv).
 //
@@ -43,26 +46,39 @@ template <int PS_, int RP_>
 struct Lay {
   static constexpr int PS = PS_, RP = RP_;
 };
-// Stage layouts. Stage 3 (bf16) pads each 64-channel pixel to 80 elements (160 B = ten 16-B
-// slots) and each row to 896 elements: the B fragments of a 16-pixel tile (two output rows of
-// 8) then hit 16 distinct 16-B slots of the 256-B bank row in every ds_read_b128 lane group
-// (unpadded: 4-way, 12 extra LDS cycles per read; tools/lds_bank_model.py).
+// Stage layouts (bf16). The B fragments of a 16-pixel tile are ds_read_b128s whose 16-lane
+// groups must hit 16 distinct 16-B slots of the 256-B bank row (tools/lds_bank_model.py):
+//   stage 2 pads each 32-channel pixel to 48 elements (96 B = six slots) and each row to 872
+//     elements (109 slots): 0 extra cycles for stage 2 and for conv 13's stride-2 reads
+//     (dense 64-B pixels: 4 and 12 extra LDS cycles per read);
+//   stage 3 pads each 64-channel pixel to 80 elements (ten slots) and each row to 896 (dense: 12).
+// The fp8 images stay dense (ds_read_b64 B fragments).
 template <bool F8>
 struct Layouts {
-  typedef Lay<16, 34 * 16> S1;  // 34x34x16
-  typedef Lay<32, 18 * 32> S2;  // 18x18x32
-  typedef Lay<F8 ? 64 : 80, F8 ? 10 * 64 : 896> S3;  // 10x10x64
+  typedef Lay<16, 34 * 16> S1;                        // 34x34x16
+  typedef Lay<F8 ? 32 : 48, F8 ? 18 * 32 : 872> S2;   // 18x18x32
+  typedef Lay<F8 ? 64 : 80, F8 ? 10 * 64 : 896> S3;   // 10x10x64
+  typedef Lay<16, 16 * 16> SC;                        // 16x16x16 shortcut, no border
 };
 
 // element offsets (multiply by EB for bytes)
 constexpr int kR0 = 0;
-constexpr int kR1 = 18496;           // 34*34*16
-constexpr int kElems = 39232;        // kR1 + 2*18*18*32
-constexpr int kT2 = kR1, kX2 = kR1 + 10368;
-constexpr int kT3 = kR0;
+constexpr int kR1 = 18496;  // 34*34*16
 template <bool F8>
-constexpr int x3_offset() { return kR0 + Layouts<F8>::S3::RP * 10; }
-static_assert(2 * 896 * 10 <= kR1, "stage-3 images fit in R0");
+struct Plan {
+  typedef Layouts<F8> Ls;
+  static constexpr int kX2 = kR0, kT2 = kR1;
+  static constexpr int kSC = kT2 + 18 * Ls::S2::RP;
+  static constexpr int kT3 = kR1, kX3 = kR1 + 10 * Ls::S3::RP;
+  static constexpr int kEnd1 = kR1 + 34 * 34 * 16;
+  static constexpr int kEnd2 = kSC + 16 * 16 * 16;
+  static constexpr int kEnd3 = kX3 + 10 * Ls::S3::RP;
+  static_assert(18 * Ls::S2::RP <= kR1, "X2 fits in R0");
+};
+constexpr int cmax(int a, int b) { return a > b ? a : b; }
+// LDS elements per workgroup (the same bound serves both element sizes)
+constexpr int kElems = cmax(cmax(Plan<false>::kEnd1, Plan<false>::kEnd2), Plan<false>::kEnd3);
+static_assert(Plan<true>::kEnd2 <= kElems && Plan<true>::kEnd3 <= kElems, "fp8 plan fits");
 
 template <bool F8>
 struct Ty;
@@ -142,40 +158,68 @@ __device__ __forceinline__ Q conv_q(const ResNet20Params& p, int i) {
   return Q{1.f, 1.f, 1.f};
 }
 
-// ---- weight prefetch into LDS (8-wave form, one workgroup per CU: 82 KB of LDS spare) ----
+// ---- weight prefetch into LDS (8-wave form, one workgroup per CU: 84 KB of LDS spare) ----
 // Every conv starts by hoisting its weights (A fragments) into registers; from global memory that
 // is an L2/HBM round trip that all waves wait for together, ~19 times per image. In the 8-wave
 // form the weights of conv i+1 are copied by LDS-DMA (global_load_lds_dwordx4) while conv i
 // computes, so the hoist reads LDS. One 1 KiB wave-instruction per chunk (lanes past the end of
-// the tensor are masked off; every packed size is a multiple of 16 bytes).
+// the tensor are masked off). The copy pads each weight row: the hoist's ds_read_b128 has lane
+// (g, col) read 16-B unit (row col, k-group g), and with the dense row of 20/36/72 units (a
+// multiple of 4) rows 4 apart land on the same bank quad (2-, 2- and 4-way conflicts,
+// tools/lds_bank_model.py --weights). A row stride of S = 2 (mod 4) units spreads the 16 lanes of
+// every b128 group over 16 distinct quads. LDS-DMA writes lane l of a wave-instruction to unit
+// 64c + l, so the padding is done on the source side: each lane fetches the global unit its LDS
+// unit holds (pad units are masked off and never read).
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 typedef __attribute__((address_space(1))) void* gbl_ptr_t;
 
-constexpr int kWeightLdsBytes = 64 * 576 * 2;  // largest packed conv weight (bf16)
+// padded LDS row stride (16-B units) of a weight row of `upr` units
+__host__ __device__ constexpr int wrow_units(int upr) { return upr + ((2 - upr) & 3); }
 
-// packed weight bytes of conv i (Cout x Kpad x EB)
-__device__ __forceinline__ int conv_w_bytes(int i, int eb) {
-  const int n = i <= 6 ? 16 * 160 : i == 7 ? 32 * 160 : i <= 12 ? 32 * 288 : i == 13 ? 64 * 288
-                                                                                      : 64 * 576;
-  return n * eb;
+// the largest conv weight (64 x 576 bf16) with padded rows
+constexpr int kWeightLdsBytes = 64 * wrow_units(576 * 2 / 16) * 16;
+
+// conv i's packed weight geometry: rows (Cout) and 16-B units per row (Kpad x EB / 16)
+__device__ __forceinline__ int conv_w_rows(int i) { return i <= 6 ? 16 : i <= 12 ? 32 : 64; }
+__device__ __forceinline__ int conv_w_upr(int i, int eb) {
+  return (i <= 7 ? 160 : i <= 13 ? 288 : 576) * eb / 16;
 }
 
 template <int NW>
-__device__ __forceinline__ void prefetch_weights(const void* src, int bytes, void* dst) {
+__device__ __forceinline__ void prefetch_weights(const void* src, int rows, int upr, void* dst) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int chunks = (bytes + 1023) >> 10;
-  for (int c = wave; c < chunks; c += NW)
-    if (c * 1024 + lane * 16 < bytes)
+  const int S = wrow_units(upr);
+  const int units = rows * S;
+  const float inv = 1.f / (float)S;
+  for (int c = wave; c * 64 < units; c += NW) {
+    const int u = c * 64 + lane;
+    int row = (int)((float)u * inv);
+    if (row * S > u) --row;
+    else if ((row + 1) * S <= u) ++row;
+    const int k = u - row * S;
+    if (u < units && k < upr)
       __builtin_amdgcn_global_load_lds(
-          (gbl_ptr_t)(static_cast<const char*>(src) + c * 1024 + lane * 16),
+          (gbl_ptr_t)(static_cast<const char*>(src) + (row * upr + k) * 16),
           (lds_ptr_t)(static_cast<char*>(dst) + c * 1024), 16, 0, 0);
+  }
 }
 
 struct WPf {
   void* wl;          // LDS weight buffer (nullptr: hoist from global, no prefetch)
   const void* next;  // weights of the next conv (nullptr: none)
-  int next_bytes;
+  int next_rows, next_upr;
 };
+
+// MFMA accumulator -> store order: lane (g, col) holds channels g*4..+3 of tile pixel col; after
+// the exchange of lane bits (2,3) <-> (4,5) lane l holds channel quad (l>>2)&3 of tile pixel
+// (l>>4)*4 + (l&3), so each 16-lane ds_write_b64 group stores all quads of 4 pixels
+__device__ __forceinline__ uint2 quad_transpose(uint2 w) {
+  const int lane = threadIdx.x & 63;
+  const int src = (((lane >> 2) & 3) << 4) | (((lane >> 4) & 3) << 2) | (lane & 3);
+  w.x = (unsigned)__builtin_amdgcn_ds_bpermute(src << 2, (int)w.x);
+  w.y = (unsigned)__builtin_amdgcn_ds_bpermute(src << 2, (int)w.y);
+  return w;
+}
 
 // zero the one-pixel border of a padded Hp x Wp x C image in layout L (C * EB % 16 == 0)
 template <bool F8, int NW, int HP, int WP, int C, class L>
@@ -195,7 +239,9 @@ __device__ __forceinline__ void zero_border(typename Ty<F8>::elem* buf) {
 
 // 3x3 pad-1 convolution LDS -> LDS with the folded-BN bias, optional residual and ReLU.
 // RES: 0 none, 1 identity (same layout as out), 2 option-A shortcut from the previous stage's
-// buffer (stride-2 subsample, channels >= RC are zero).
+// buffer (stride-2 subsample, channels >= RC are zero), 3 option-A shortcut from the SC copy
+// (layout LR, no border), 4 none, and copy this stride-2 conv's option-A shortcut (channels
+// < RC of the input at the subsampled pixels) to `res` in layout LR.
 template <bool F8, int NW, int CIN, int COUT, int S, int HO, int RES, int RC, class LI, class LO,
           class LR>
 __device__ __forceinline__ void conv3x3(const void* wgv, const float* __restrict__ wscale,
@@ -208,6 +254,8 @@ __device__ __forceinline__ void conv3x3(const void* wgv, const float* __restrict
   const elem* wg = static_cast<const elem*>(NW == 8 ? pf.wl : wgv);
   constexpr int K = 9 * CIN;
   constexpr int KPAD = (K + 31) / 32 * 32;
+  // weight row stride in elements: dense in global, padded in the LDS copy
+  constexpr int WROW = NW == 8 ? wrow_units(KPAD * T::EB / 16) * 16 / T::EB : KPAD;
   constexpr int KS = KPAD / 32;
   constexpr int CT = COUT / 16;        // channel tiles
   constexpr int PT = HO * HO / 16;     // 16-pixel tiles
@@ -225,7 +273,7 @@ __device__ __forceinline__ void conv3x3(const void* wgv, const float* __restrict
 #pragma unroll
   for (int ks = 0; ks < KS; ++ks) {
     const int k = ks * 32 + g * 8;
-    afr[ks] = T::ld(wg + (ct * 16 + col) * KPAD + k);
+    afr[ks] = T::ld(wg + (ct * 16 + col) * WROW + k);
     int tap = k / CIN;
     const int ci = k - tap * CIN;
     if (tap >= 9) tap = 0;  // K padding: zero weights, any finite input
@@ -243,7 +291,7 @@ __device__ __forceinline__ void conv3x3(const void* wgv, const float* __restrict
     // DMA is in flight), every wave done reading the buffer, then refill it for the next conv
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __syncthreads();
-    if (pf.next) prefetch_weights<NW>(pf.next, pf.next_bytes, pf.wl);
+    if (pf.next) prefetch_weights<NW>(pf.next, pf.next_rows, pf.next_upr, pf.wl);
   }
 
 #pragma unroll 1
@@ -274,11 +322,21 @@ __device__ __forceinline__ void conv3x3(const void* wgv, const float* __restrict
       float v0 = acc[p][0] * sc.x + bv.x, v1 = acc[p][1] * sc.y + bv.y;
       float v2 = acc[p][2] * sc.z + bv.z, v3 = acc[p][3] * sc.w + bv.w;
       const int o = (ho[p] + 1) * LO::RP + (wo[p] + 1) * LO::PS + c0;
-      if (RES == 1 || (RES == 2 && c0 < RC)) {
-        const int ro = RES == 1 ? o : (2 * ho[p] + 1) * LR::RP + (2 * wo[p] + 1) * LR::PS + c0;
+      if (RES == 1 || ((RES == 2 || RES == 3) && c0 < RC)) {
+        const int ro = RES == 1   ? o
+                       : RES == 2 ? (2 * ho[p] + 1) * LR::RP + (2 * wo[p] + 1) * LR::PS + c0
+                                  : ho[p] * LR::RP + wo[p] * LR::PS + c0;
         float r[4];
         T::load4(res + ro, q.res, r);
         v0 += r[0]; v1 += r[1]; v2 += r[2]; v3 += r[3];
+      }
+      if (RES == 4 && c0 < RC) {  // raw copy: same quantisation scale on both sides
+        const elem* src = in + (2 * ho[p] + 1) * LI::RP + (2 * wo[p] + 1) * LI::PS + c0;
+        elem* dst = const_cast<elem*>(res) + ho[p] * LR::RP + wo[p] * LR::PS + c0;
+        if constexpr (F8)
+          *reinterpret_cast<uint32_t*>(dst) = *reinterpret_cast<const uint32_t*>(src);
+        else
+          *reinterpret_cast<uint2*>(dst) = *reinterpret_cast<const uint2*>(src);
       }
       if constexpr (!F8) {
         // The accumulator puts lane (g, col) on channels g*4..+3 of pixel col: a 16-lane
@@ -290,10 +348,7 @@ __device__ __forceinline__ void conv3x3(const void* wgv, const float* __restrict
         bf16x4 ov;
         ov[0] = (bf16)fmaxf(v0, 0.f); ov[1] = (bf16)fmaxf(v1, 0.f);
         ov[2] = (bf16)fmaxf(v2, 0.f); ov[3] = (bf16)fmaxf(v3, 0.f);
-        uint2 w = __builtin_bit_cast(uint2, ov);
-        const int src = (((lane >> 2) & 3) << 4) | (((lane >> 4) & 3) << 2) | (lane & 3);
-        w.x = (unsigned)__builtin_amdgcn_ds_bpermute(src << 2, (int)w.x);
-        w.y = (unsigned)__builtin_amdgcn_ds_bpermute(src << 2, (int)w.y);
+        const uint2 w = quad_transpose(__builtin_bit_cast(uint2, ov));
         const int mt = (pt0 + pg + p) * 16 + ((lane >> 4) << 2) + (lane & 3);
         const int hot = mt / HO, wot = mt - hot * HO;
         const int ot = (hot + 1) * LO::RP + (wot + 1) * LO::PS + ct * 16 + ((lane >> 2) & 3) * 4;
@@ -358,10 +413,20 @@ __device__ __forceinline__ void stem(const void* wgv, const float* __restrict__ 
       acc[p] = T::mma(a, b, f32x4{0.f, 0.f, 0.f, 0.f});
     }
 #pragma unroll
-    for (int p = 0; p < 4; ++p)
-      T::store4(out + ((ho[p] + 1) * 34 + wo[p] + 1) * 16 + g * 4, q.qout,
-                fmaxf(acc[p][0] * sc.x + bv.x, 0.f), fmaxf(acc[p][1] * sc.y + bv.y, 0.f),
-                fmaxf(acc[p][2] * sc.z + bv.z, 0.f), fmaxf(acc[p][3] * sc.w + bv.w, 0.f));
+    for (int p = 0; p < 4; ++p) {
+      const float v0 = fmaxf(acc[p][0] * sc.x + bv.x, 0.f), v1 = fmaxf(acc[p][1] * sc.y + bv.y, 0.f);
+      const float v2 = fmaxf(acc[p][2] * sc.z + bv.z, 0.f), v3 = fmaxf(acc[p][3] * sc.w + bv.w, 0.f);
+      if constexpr (!F8) {  // 128 contiguous bytes per ds_write_b64 group (see quad_transpose)
+        bf16x4 ov;
+        ov[0] = (bf16)v0; ov[1] = (bf16)v1; ov[2] = (bf16)v2; ov[3] = (bf16)v3;
+        const uint2 w = quad_transpose(__builtin_bit_cast(uint2, ov));
+        const int mt = (wave * TPW + pg + p) * 16 + ((lane >> 4) << 2) + (lane & 3);
+        *reinterpret_cast<uint2*>(out + ((mt >> 5) + 1) * 34 * 16 + ((mt & 31) + 1) * 16 +
+                                  ((lane >> 2) & 3) * 4) = w;
+      } else {
+        T::store4(out + ((ho[p] + 1) * 34 + wo[p] + 1) * 16 + g * 4, q.qout, v0, v1, v2, v3);
+      }
+    }
   }
 }
 
@@ -379,21 +444,24 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void resnet20_fused_kernel(ResNet2
   elem* X1 = base + kR0;
   elem* T1 = base + kR1;
   elem* IN = base + kR1;
-  elem* T2 = base + kT2;
-  elem* X2 = base + kX2;
-  elem* T3 = base + kT3;
-  elem* X3 = base + x3_offset<F8>();
+  typedef Plan<F8> PL;
+  elem* T2 = base + PL::kT2;
+  elem* X2 = base + PL::kX2;
+  elem* SC = base + PL::kSC;
+  elem* T3 = base + PL::kT3;
+  elem* X3 = base + PL::kX3;
   typedef typename Layouts<F8>::S1 L1;
   typedef typename Layouts<F8>::S2 L2;
   typedef typename Layouts<F8>::S3 L3;
-  float* scratch = reinterpret_cast<float*>(base + kR1);
+  float* scratch = reinterpret_cast<float*>(base + kR0);
   // 8-wave form: weights of the next conv prefetched into LDS behind the activations
   void* wl = NW == 8 ? static_cast<void*>(smem + kElems * T::EB) : nullptr;
   auto pfw = [&](int i) {
     WPf f;
     f.wl = wl;
     f.next = i < 18 ? p.w[i + 1] : nullptr;
-    f.next_bytes = i < 18 ? conv_w_bytes(i + 1, T::EB) : 0;
+    f.next_rows = i < 18 ? conv_w_rows(i + 1) : 0;
+    f.next_upr = i < 18 ? conv_w_upr(i + 1, T::EB) : 0;
     return f;
   };
   const float in_q = F8 ? 1.f / p.s_in[0] : 1.f;  // quantisation of the fp32 network input
@@ -423,7 +491,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void resnet20_fused_kernel(ResNet2
     stem<F8, NW>(p.w[0], p.ws[0], p.b[0], conv_q<F8>(p, 0), IN, X1);
     if (wl) {  // conv 1's weights land during the barrier below and the border zeroing
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      prefetch_weights<NW>(p.w[1], conv_w_bytes(1, T::EB), wl);
+      prefetch_weights<NW>(p.w[1], conv_w_rows(1), conv_w_upr(1, T::EB), wl);
     }
     __syncthreads();
     zero_border<F8, NW, 34, 34, 16, L1>(T1);  // IN is dead; T1's border overlaps its bytes
@@ -439,11 +507,13 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void resnet20_fused_kernel(ResNet2
       __syncthreads();
     }
     // ---- stage 2: 16x16x32 ----
+    typedef typename Layouts<F8>::SC LS;
     zero_border<F8, NW, 18, 18, 32, L2>(T2);
-    zero_border<F8, NW, 18, 18, 32, L2>(X2);
-    conv3x3<F8, NW, 16, 32, 2, 16, 0, 16, L1, L2, L1>(p.w[7], p.ws[7], p.b[7], conv_q<F8>(p, 7), X1, T2, nullptr, pfw(7));
+    // conv 7 also copies block 2.1's shortcut out of X1 into SC: X1 is dead after it
+    conv3x3<F8, NW, 16, 32, 2, 16, 4, 16, L1, L2, LS>(p.w[7], p.ws[7], p.b[7], conv_q<F8>(p, 7), X1, T2, SC, pfw(7));
     __syncthreads();
-    conv3x3<F8, NW, 32, 32, 1, 16, 2, 16, L2, L2, L1>(p.w[8], p.ws[8], p.b[8], conv_q<F8>(p, 8), T2, X2, X1, pfw(8));
+    zero_border<F8, NW, 18, 18, 32, L2>(X2);  // X2 lives where X1 was
+    conv3x3<F8, NW, 32, 32, 1, 16, 3, 16, L2, L2, LS>(p.w[8], p.ws[8], p.b[8], conv_q<F8>(p, 8), T2, X2, SC, pfw(8));
     __syncthreads();
 #pragma unroll 1
     for (int blk = 1; blk < 3; ++blk) {
@@ -484,7 +554,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void resnet20_fused_kernel(ResNet2
         const int h = pix >> 3, w = pix & 7;
         s += T::to_f32(X3[(h + 1) * L3::RP + (w + 1) * L3::PS + c]);
       }
-      scratch[qq * 64 + c] = s;  // R1 is free in stage 3's last block (X2 is dead)
+      scratch[qq * 64 + c] = s;  // R0 is free in stage 3's last block (X2 is dead)
       __syncthreads();
       if (threadIdx.x < 64) {
         const int lane = threadIdx.x;
@@ -536,12 +606,8 @@ hipError_t resnet20_fused_forward(const ResNet20Params& p, int batch, const floa
   const size_t lds = (size_t)kElems * (f8 ? 1 : 2) + (nw == 8 ? (size_t)kWeightLdsBytes : 0);
   const dim3 block(64 * nw);
   if (f8) {
-    if (nw == 8)
-      hipLaunchKernelGGL((resnet20_fused_kernel<true, 8>), dim3(grid), block, lds, stream, p, x,
-                         out, batch);
-    else
-      hipLaunchKernelGGL((resnet20_fused_kernel<true, 4>), dim3(grid), block, lds, stream, p, x,
-                         out, batch);
+    hipLaunchKernelGGL((resnet20_fused_kernel<true, 4>), dim3(grid), block, lds, stream, p, x,
+                       out, batch);
   } else if (nw == 8) {
     hipLaunchKernelGGL((resnet20_fused_kernel<false, 8>), dim3(grid), block, lds, stream, p, x,
                        out, batch);

@@ -170,12 +170,9 @@ def run_topology(cfg: GaleConfig, stop_event: Optional[threading.Event] = None,
             broker = start_embedded_broker(cfg)
         devices = None
         if world > 1 and not cfg.stub:
-            import torch
-            import torch.distributed as dist
+            from gale.parallel.group import init_rank_group
 
-            torch.cuda.set_device(local_rank)
-            if not dist.is_initialized():
-                dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+            init_rank_group(local_rank, use_gpu=True)
             devices = [local_rank]
         if world > 1 and not cfg.partitions and not cfg.group_membership:
             cfg.partitions = rank_partitions(cfg, rank, world)

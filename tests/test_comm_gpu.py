@@ -43,3 +43,44 @@ def test_replicate_weights_over_rccl():
     for b in bufs:
         assert torch.equal(b.cpu(), src.cpu())
 
+
+_RANK_SCRIPT = r"""
+import torch, torch.distributed as dist
+from gale.models import get_model
+from gale.parallel.group import init_rank_group
+from gale.parallel.weights import materialize_weights
+backend = init_rank_group(0, use_gpu=True)
+assert backend == "nccl" and dist.get_backend() == "nccl", backend
+net = get_model("resnet20")
+buf = materialize_weights(net, torch.device("cuda", 0), seed=5)
+ref = buf.clone()
+dist.broadcast(buf, src=0)          # the weight broadcast bench.py / topology.py issue
+mx = torch.tensor([3.5], dtype=torch.float64, device="cuda")
+dist.all_reduce(mx, op=dist.ReduceOp.MAX)   # bench.py's max-over-ranks timing
+dist.barrier()
+torch.cuda.synchronize()
+assert torch.equal(buf.cpu(), ref.cpu()) and mx.item() == 3.5
+dist.destroy_process_group()
+print("RANK_GROUP_OK")
+"""
+
+
+def test_rank_process_group_is_rccl():
+    """The per-process ranks' group (gale/parallel/group.py, used by bench.py and
+    ``torchrun -m gale``) comes up on the "nccl" backend (RCCL) bound to the rank's GPU, and the
+    broadcast / MAX all-reduce / barrier the bench issues complete. World 1 here (RCCL refuses two
+    ranks on one device); the same code runs per rank at N > 1."""
+    import os
+    import socket
+    import subprocess
+    import sys
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ, RANK="0", LOCAL_RANK="0", WORLD_SIZE="1", LOCAL_WORLD_SIZE="1",
+               MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", _RANK_SCRIPT], env=env, cwd=repo,
+                       capture_output=True, text=True, timeout=100)
+    assert r.returncode == 0 and "RANK_GROUP_OK" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
