@@ -336,7 +336,7 @@ def latency_phase(eng, broker, feeder, bset, parts, rate_img_s, a, ipr):
     cgroup's CPU throttling during the window (CFS quota periods in which the rank's cgroup ran
     out of its share: every thread then waits for the next period, a latency tail source)."""
     from gale._native import native
-    from gale.metrics import append_to_ack_us
+    from gale.metrics import append_to_ack_us, latency_stages_us
 
     feeder.stop()
     t_end = time.perf_counter() + 10.0
@@ -363,9 +363,14 @@ def latency_phase(eng, broker, feeder, bset, parts, rate_img_s, a, ipr):
                 "latency_cg_periods": int(d.get("nr_periods", 0))}
     rf.stop()
     ack = eng.take_ack_log()
-    lat, when = append_to_ack_us(rf.take_log(), ack, with_ack_time=True)
+    app = rf.take_log()
+    lat, when = append_to_ack_us(app, ack, with_ack_time=True)
+    stages = latency_stages_us(app, ack)
+    host["latency_stages_ms"] = {
+        k: [round(float(np.percentile(v, q)) / 1e3, 3) for q in (50, 99)] if len(v) else None
+        for k, v in stages.items()}
     if a.latency_dump and int(os.environ.get("RANK", "0")) == 0:
-        np.savez(a.latency_dump, latency_us=lat, ack_t_ns=when)
+        np.savez(a.latency_dump, latency_us=lat, ack_t_ns=when, **stages)
     return lat, achieved, int(len(ack[0]) - len(lat)), host
 
 

@@ -133,16 +133,24 @@ void bind_engine(py::module_& m) {
       .def("take_ack_log", [](Engine& e) {
         const std::vector<AckSample> v = e.take_ack_log();
         py::array_t<int32_t> p(v.size());
-        py::array_t<int64_t> o(v.size()), t(v.size());
+        py::array_t<int64_t> o(v.size()), t(v.size()), tf(v.size()), tt(v.size()), td(v.size());
         auto pp = p.mutable_unchecked<1>();
         auto po = o.mutable_unchecked<1>();
         auto pt = t.mutable_unchecked<1>();
+        auto pf = tf.mutable_unchecked<1>();
+        auto pk = tt.mutable_unchecked<1>();
+        auto pd = td.mutable_unchecked<1>();
         for (size_t i = 0; i < v.size(); ++i) {
-          pp((py::ssize_t)i) = v[i].partition;
-          po((py::ssize_t)i) = v[i].offset;
-          pt((py::ssize_t)i) = v[i].t_ns;
+          const auto k = (py::ssize_t)i;
+          pp(k) = v[i].partition;
+          po(k) = v[i].offset;
+          pt(k) = v[i].t_ns;
+          pf(k) = v[i].t_fetch_ns;
+          pk(k) = v[i].t_take_ns;
+          pd(k) = v[i].t_done_ns;
         }
-        return py::make_tuple(p, o, t);
+        // (partition, offset, t_ack, t_fetch, t_take, t_done)
+        return py::make_tuple(p, o, t, tf, tt, td);
       })
       .def("replica_stats", [](Engine& e) {
         py::list out;

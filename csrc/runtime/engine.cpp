@@ -1192,6 +1192,8 @@ void Engine::finish_batch(ReplicaSlot* rs, Batch& b) {
     meta.offset = r.offset;
     meta.timestamp_ms = r.timestamp_ms;
     meta.t_fetch_ns = r.t_fetch_ns;
+    meta.t_take_ns = b.t_take_ns;
+    meta.t_done_ns = b.t_done_ns;
     meta.images = r.status == codec::OK ? r.images : 0;
     bool null_value = false;
     if (r.status != codec::OK) {
@@ -1282,7 +1284,9 @@ void Engine::complete_records(const std::vector<InRecord>& rs, bool ok) {
   if (ack_log_on_.load(std::memory_order_relaxed)) {
     std::lock_guard<std::mutex> lk(ack_mu_);
     for (size_t i = 0; i < rs.size() && ack_log_.size() < ack_cap_; ++i)
-      if (good[i]) ack_log_.push_back({rs[i].partition, rs[i].offset, now});
+      if (good[i])
+        ack_log_.push_back({rs[i].partition, rs[i].offset, now, rs[i].t_fetch_ns, rs[i].t_take_ns,
+                            rs[i].t_done_ns});
   }
   const int64_t c = completed_ += (int64_t)rs.size();
   const int64_t target = wait_target_.load(std::memory_order_relaxed);
@@ -1311,7 +1315,8 @@ void Engine::complete_record(const InRecord& r, bool ok) {
   t_last_ns_ = now;
   if (ack_log_on_.load(std::memory_order_relaxed) && ok) {
     std::lock_guard<std::mutex> lk(ack_mu_);
-    if (ack_log_.size() < ack_cap_) ack_log_.push_back({r.partition, r.offset, now});
+    if (ack_log_.size() < ack_cap_)
+      ack_log_.push_back({r.partition, r.offset, now, r.t_fetch_ns, r.t_take_ns, r.t_done_ns});
   }
   const int64_t c = ++completed_;
   const int64_t target = wait_target_.load(std::memory_order_relaxed);

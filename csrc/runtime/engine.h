@@ -118,12 +118,15 @@ struct EngineConfig {
   uint64_t seed = 0;
 };
 
-// One acknowledged output (ack log): input record (partition, offset) and the monotonic time its
-// prediction was acknowledged by the sink (CLOCK_MONOTONIC ns, the clock of mono_ns()).
+// One acknowledged output (ack log): input record (partition, offset), the monotonic time its
+// prediction was acknowledged by the sink (CLOCK_MONOTONIC ns, the clock of mono_ns()) and the
+// times it passed the earlier stages: fetch response received, batch dispatched to a replica,
+// device work done (prediction handed to the producer right after).
 struct AckSample {
   int32_t partition;
   int64_t offset;
   int64_t t_ns;
+  int64_t t_fetch_ns, t_take_ns, t_done_ns;
 };
 
 struct ReplicaStats {

@@ -30,6 +30,7 @@ struct InRecord {
   int64_t offset = -1;
   int64_t timestamp_ms = -1;     // Kafka record CreateTime
   int64_t t_fetch_ns = 0;        // host receive time
+  int64_t t_take_ns = 0, t_done_ns = 0;  // its batch's dispatch / device-done time (sink metas)
   int64_t arr_off = 0, arr_len = 0;  // instances array inside the value (scan result)
   int32_t images = 0;
   int32_t status = 0;            // codec::Status (scan, then device parse)

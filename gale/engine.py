@@ -171,5 +171,6 @@ class Engine:
         self._native.set_ack_log(on, capacity)
 
     def take_ack_log(self):
-        """(partition, offset, t_ns) numpy arrays of the ack log (and clear it)."""
+        """(partition, offset, t_ack_ns, t_fetch_ns, t_take_ns, t_done_ns) numpy arrays of the
+        ack log (and clear it); all CLOCK_MONOTONIC."""
         return self._native.take_ack_log()

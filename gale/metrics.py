@@ -192,18 +192,14 @@ class MetricsServer:
         self._httpd.server_close()
 
 
-def append_to_ack_us(append_log, ack_log, with_ack_time=False):
-    """Record-level latency (microseconds) from a producer's append log and the engine's ack
-    log, both on CLOCK_MONOTONIC: ``append_log`` = (partition, base_offset, records, t_ns) per
-    appended batch (``kafka.RateFeeder.take_log``), ``ack_log`` = (partition, offset, t_ns) per
-    acknowledged output (``Engine.take_ack_log``). Each acknowledged record is matched to the
-    batch that contains its offset; records appended outside the log are skipped. With
-    ``with_ack_time`` returns (latencies, ack t_ns) so a tail can be placed in time."""
+def _match_appends(append_log, ack_log):
+    """For each acknowledged record, the append time of the producer batch that holds its
+    offset: returns (ack indices, append t_ns) for the matched records."""
     import numpy as np
 
     ap, abase, an, at = (np.asarray(x) for x in append_log)
-    kp, koff, kt = (np.asarray(x) for x in ack_log)
-    out, when = [], []
+    kp, koff = np.asarray(ack_log[0]), np.asarray(ack_log[1])
+    idx, tapp = [], []
     for p in np.unique(kp):
         sel = ap == p
         if not sel.any():
@@ -211,15 +207,46 @@ def append_to_ack_us(append_log, ack_log, with_ack_time=False):
         base, n, t = abase[sel], an[sel], at[sel]
         order = np.argsort(base)
         base, n, t = base[order], n[order], t[order]
-        ks = kp == p
-        off, tk = koff[ks], kt[ks]
+        ks = np.nonzero(kp == p)[0]
+        off = koff[ks]
         i = np.searchsorted(base, off, side="right") - 1
         ok = (i >= 0)
         i = np.clip(i, 0, len(base) - 1)
         ok &= off < base[i] + n[i]
-        out.append((tk[ok] - t[i[ok]]) / 1e3)
-        when.append(tk[ok])
-    lat = np.concatenate(out) if out else np.zeros(0)
-    if with_ack_time:
-        return lat, (np.concatenate(when) if when else np.zeros(0, dtype=np.int64))
-    return lat
+        idx.append(ks[ok])
+        tapp.append(t[i[ok]])
+    if not idx:
+        return np.zeros(0, dtype=np.int64), np.zeros(0, dtype=np.int64)
+    return np.concatenate(idx), np.concatenate(tapp)
+
+
+def append_to_ack_us(append_log, ack_log, with_ack_time=False):
+    """Record-level latency (microseconds) from a producer's append log and the engine's ack
+    log, both on CLOCK_MONOTONIC: ``append_log`` = (partition, base_offset, records, t_ns) per
+    appended batch (``kafka.RateFeeder.take_log``), ``ack_log`` = (partition, offset, t_ns, ...)
+    per acknowledged output (``Engine.take_ack_log``). Each acknowledged record is matched to
+    the batch that contains its offset; records appended outside the log are skipped. With
+    ``with_ack_time`` returns (latencies, ack t_ns) so a tail can be placed in time."""
+    import numpy as np
+
+    idx, tapp = _match_appends(append_log, ack_log)
+    tack = np.asarray(ack_log[2])[idx]
+    lat = (tack - tapp) / 1e3
+    return (lat, tack) if with_ack_time else lat
+
+
+def latency_stages_us(append_log, ack_log):
+    """Per-record split of append -> ack into the pipeline stages (microseconds), from an ack
+    log with stage times (``Engine.take_ack_log``: t_ack, t_fetch, t_take, t_done):
+    broker_source = append -> fetch response received (broker residency, fetch wait, socket),
+    queue = fetch -> batch dispatched (decode / GPU ingest and batching), replica = dispatch ->
+    device done (H2D, parse, forward, D2H, completion wait), sink = done -> produce ack
+    (prediction text, produce request, broker ack). Records without stage times are skipped."""
+    import numpy as np
+
+    idx, tapp = _match_appends(append_log, ack_log)
+    tack, tf, tt, td = (np.asarray(ack_log[k])[idx] for k in (2, 3, 4, 5))
+    ok = (tf > 0) & (tt > 0) & (td > 0)
+    tapp, tack, tf, tt, td = tapp[ok], tack[ok], tf[ok], tt[ok], td[ok]
+    return {"broker_source": (tf - tapp) / 1e3, "queue": (tt - tf) / 1e3,
+            "replica": (td - tt) / 1e3, "sink": (tack - td) / 1e3}
