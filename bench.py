@@ -145,6 +145,12 @@ def parse_args(argv=None):
     ap.add_argument("--latency-warmup-s", type=float, default=1.0)
     ap.add_argument("--fetch-min-bytes", type=int, default=1,
                     help="consumer fetch.min.bytes (Kafka default 1)")
+    ap.add_argument("--latency-sweep", default="",
+                    help="after the --latency-load phase, more latency phases at these offered "
+                         "loads (comma list of fractions of the measured throughput), reported "
+                         "as latency_sweep (config 5: max load meeting a p99 SLO)")
+    ap.add_argument("--latency-repeat", type=int, default=1,
+                    help="latency phases per --latency-sweep load")
     ap.add_argument("--latency-dump", default="",
                     help="save rank 0's per-record latencies and ack times (.npz) of the latency "
                          "phase, to place a tail in time against --timeline")
@@ -370,7 +376,10 @@ def latency_phase(eng, broker, feeder, bset, parts, rate_img_s, a, ipr):
         k: [round(float(np.percentile(v, q)) / 1e3, 3) for q in (50, 99)] if len(v) else None
         for k, v in stages.items()}
     if a.latency_dump and int(os.environ.get("RANK", "0")) == 0:
-        np.savez(a.latency_dump, latency_us=lat, ack_t_ns=when, **stages)
+        # every 4th record, float32 microseconds (a 2 s window at 1.25 M img/s is 2.5 M records)
+        np.savez_compressed(a.latency_dump, latency_us=lat[::4].astype(np.float32),
+                            ack_t_ns=when[::4],
+                            **{k: v[::4].astype(np.float32) for k, v in stages.items()})
     return lat, achieved, int(len(ack[0]) - len(lat)), host
 
 
@@ -567,21 +576,38 @@ def main(argv=None) -> int:
     n_gpus = world * local_gpus
     lat_us, lat_achieved, lat_unmatched, lat_host = None, 0.0, 0, {}
     offered = a.latency_load * value  # whole job, images/s
-    if a.latency_load > 0 and a.rate <= 0:
+
+    def measure(load_img_s):
         if world > 1:
             dist.barrier()
-        lat_us, lat_achieved, lat_unmatched, lat_host = latency_phase(
-            eng, broker, feeder, bset, my_parts, offered / world, a, ipr)
+        lu, ach, unm, hst = latency_phase(eng, broker, feeder, bset, my_parts,
+                                          load_img_s / world, a, ipr)
         if world > 1:
             # every rank's samples (subsampled to <= 200k) and achieved rate to rank 0
-            if len(lat_us) > 200_000:
-                lat_us = lat_us[np.random.default_rng(rank).choice(len(lat_us), 200_000,
-                                                                   replace=False)]
+            if len(lu) > 200_000:
+                lu = lu[np.random.default_rng(rank).choice(len(lu), 200_000, replace=False)]
             got = [None] * world
-            dist.all_gather_object(got, (lat_us, lat_achieved, lat_unmatched))
-            lat_us = np.concatenate([g[0] for g in got])
-            lat_achieved = sum(g[1] for g in got)
-            lat_unmatched = sum(g[2] for g in got)
+            dist.all_gather_object(got, (lu, ach, unm))
+            lu = np.concatenate([g[0] for g in got])
+            ach = sum(g[1] for g in got)
+            unm = sum(g[2] for g in got)
+        return lu, ach, unm, hst
+
+    sweep = []
+    if a.latency_load > 0 and a.rate <= 0:
+        lat_us, lat_achieved, lat_unmatched, lat_host = measure(offered)
+        for frac in [float(x) for x in a.latency_sweep.split(",") if x.strip()]:
+            for _ in range(max(1, a.latency_repeat)):
+                lu, ach, unm, hst = measure(frac * value)
+                if len(lu):
+                    sweep.append({"load": frac, "offered_img_s": round(frac * value, 1),
+                                  "achieved_img_s": round(ach, 1),
+                                  "p50_ms": round(float(np.percentile(lu, 50)) / 1e3, 3),
+                                  "p99_ms": round(float(np.percentile(lu, 99)) / 1e3, 3),
+                                  "p999_ms": round(float(np.percentile(lu, 99.9)) / 1e3, 3),
+                                  "samples": int(len(lu)), "unmatched": unm,
+                                  "stages_ms": hst.get("latency_stages_ms"),
+                                  "cg_throttled_ms": hst.get("latency_cg_throttled_ms")})
     if timeline:
         timeline.stop()
     if world > 1:
@@ -647,6 +673,8 @@ def main(argv=None) -> int:
                 "p999_latency_ms": round(float(np.percentile(lat_us, 99.9)) / 1e3, 3),
                 **lat_host,  # rank 0's cgroup during the latency window
             })
+            if sweep:
+                out["latency_sweep"] = sweep
         else:
             out.update({
                 "p50_latency_ms": round(st["e2e_us_p50"] / 1e3, 3),
