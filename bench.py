@@ -145,6 +145,8 @@ def parse_args(argv=None):
     ap.add_argument("--latency-warmup-s", type=float, default=1.0)
     ap.add_argument("--fetch-min-bytes", type=int, default=1,
                     help="consumer fetch.min.bytes (Kafka default 1)")
+    ap.add_argument("--fetch-max-wait-ms", type=int, default=20,
+                    help="consumer fetch.max.wait.ms (long-poll bound when no data is there)")
     ap.add_argument("--latency-sweep", default="",
                     help="after the --latency-load phase, more latency phases at these offered "
                          "loads (comma list of fractions of the measured throughput), reported "
@@ -210,12 +212,17 @@ class Timeline:
         prev_t, prev_c, prev_cpu, prev_cg = t0, self.engine.completed, self.cpu(), _cgroup_cpu_stat()
         prev_b = self.broker.stats() if self.broker is not None else None
         prev_th = self.per_thread()
+        prev_busy = {}
         groups = ("gl-brk", "gl-src", "gl-dec", "gl-rep", "gl-sink", "gl-watchdog")
         while not self._stop.wait(self.dt):
             now, c, cpu, cg = time.perf_counter(), self.engine.completed, self.cpu(), _cgroup_cpu_stat()
             dt = now - prev_t
             st = self.engine.stats()
+            busy = {k: st.get("thread_s_" + k, 0.0) for k in ("poll", "handoff", "decode", "wait")}
             row = {"t": round(now - t0, 3), "mono": round(now, 4), "phase": self.phase,
+                   # engine thread-seconds per second in source polls, source hand-off waits
+                   # (decode queue full), decode and replica completion waits
+                   "busy": {k: round((v - prev_busy.get(k, 0.0)) / dt, 2) for k, v in busy.items()},
                    "rate": round((c - prev_c) / dt),
                    "cores": {k: round((cpu[k] - prev_cpu.get(k, 0.0)) / dt, 2) for k in cpu},
                    "rss_mb": round(_rss_mb()),
@@ -243,7 +250,7 @@ class Timeline:
                 prev_b = b
             self.f.write(json.dumps(row) + "\n")
             self.f.flush()
-            prev_t, prev_c, prev_cpu, prev_cg = now, c, cpu, cg
+            prev_t, prev_c, prev_cpu, prev_cg, prev_busy = now, c, cpu, cg, busy
 
     def stop(self):
         self._stop.set()
@@ -517,6 +524,7 @@ def main(argv=None) -> int:
                      output_partition=rank if a.local_output and world > 1 else -1,
                      producer_buffer_mb=a.producer_buffer_mb,
                      locality_split=a.locality_split, fetch_min_bytes=a.fetch_min_bytes,
+                     fetch_max_wait_ms=a.fetch_max_wait_ms,
                      use_graph=a.graph,
                      producer_request_kb=a.producer_request_kb)
     devices = (list(range(local_gpus)) if local_gpus > 1 else [local_rank]) if use_gpu else None

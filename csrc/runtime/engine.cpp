@@ -722,9 +722,11 @@ void Engine::source_loop(int idx) {
         // restart with start_offset=committed re-reads it)
         if (!good.empty()) batcher.push_many(good, stopping_);
       } else {
+        const int64_t th = mono_ns();
         std::unique_lock<std::mutex> lk(dec_mu_);
         dec_space_cv_.wait(lk, [&] { return dec_q_.size() < (size_t)(4 * cfg_.decode_threads) ||
                                             stopping_; });
+        ns_handoff_ += mono_ns() - th;
         if (stopping_) break;
         dec_q_.push_back(std::move(it));
         dec_cv_.notify_one();
@@ -1472,6 +1474,7 @@ std::map<std::string, double> Engine::stats() const {
   s["eff_max_wait_us"] = (double)eff_wait_ns_ / 1000.0;
   s["slo_adjustments"] = (double)slo_adjustments_;
   s["thread_s_poll"] = ns_poll_ * 1e-9;
+  s["thread_s_handoff"] = ns_handoff_ * 1e-9;
   s["thread_s_decode"] = ns_decode_ * 1e-9;
   s["thread_s_take"] = ns_take_ * 1e-9;
   s["thread_s_submit"] = ns_submit_ * 1e-9;
@@ -1529,7 +1532,7 @@ void Engine::reset_stats() {
   images_out_ = 0;
   records_out_ = 0;
   bytes_in_ = 0;  // (json MB/s of a window = bytes fetched inside it)
-  ns_poll_ = ns_decode_ = ns_take_ = ns_submit_ = ns_wait_ = ns_finish_ = 0;
+  ns_poll_ = ns_decode_ = ns_take_ = ns_submit_ = ns_wait_ = ns_finish_ = ns_handoff_ = 0;
   t_first_ns_ = mono_ns();
   t_last_ns_ = t_first_ns_.load();
 }
