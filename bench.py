@@ -360,11 +360,13 @@ def latency_phase(eng, broker, feeder, bset, parts, rate_img_s, a, ipr):
     rf = native().kafka.RateFeeder(broker, "gale-in", parts, bset)
     rf.start(rate_img_s / ipr, feeder._next)
     time.sleep(a.latency_warmup_s)
+    broker.take_probes()  # (reset)
     eng.set_ack_log(True)
     c0, t0, cg0 = eng.completed, time.perf_counter(), _cgroup_cpu_stat()
     time.sleep(a.latency_s)
     eng.set_ack_log(False)
     dt = time.perf_counter() - t0
+    probes = broker.take_probes()
     achieved = (eng.completed - c0) * ipr / dt
     cg1 = _cgroup_cpu_stat()
     host = {}
@@ -374,6 +376,7 @@ def latency_phase(eng, broker, feeder, bset, parts, rate_img_s, a, ipr):
                 "latency_cg_throttled_ms": round(d.get("throttled_usec", 0) / 1e3, 1),
                 "latency_cg_throttled_periods": int(d.get("nr_throttled", 0)),
                 "latency_cg_periods": int(d.get("nr_periods", 0))}
+    host["latency_broker_probes"] = probes
     rf.stop()
     ack = eng.take_ack_log()
     app = rf.take_log()
@@ -615,7 +618,8 @@ def main(argv=None) -> int:
                                   "p999_ms": round(float(np.percentile(lu, 99.9)) / 1e3, 3),
                                   "samples": int(len(lu)), "unmatched": unm,
                                   "stages_ms": hst.get("latency_stages_ms"),
-                                  "cg_throttled_ms": hst.get("latency_cg_throttled_ms")})
+                                  "cg_throttled_ms": hst.get("latency_cg_throttled_ms"),
+                                  "broker_probes": hst.get("latency_broker_probes")})
     if timeline:
         timeline.stop()
     if world > 1:

@@ -655,7 +655,19 @@ void bind_host(py::module_& m) {
         d["records_in"] = s.records_in;
         d["connections"] = s.connections;
         return d;
-      });
+      })
+      .def("take_probes", [](Broker& b) {
+        const BrokerProbes p = b.take_probes();
+        py::dict d;
+        d["wake_max_us"] = p.wake_max_us;
+        d["wake_slow"] = p.wake_slow;
+        d["flush_max_us"] = p.flush_max_us;
+        d["flush_slow"] = p.flush_slow;
+        d["lock_max_us"] = p.lock_max_us;
+        d["lock_slow"] = p.lock_slow;
+        return d;
+      }, "latency-tail probes since the last call (max us, count > 1 ms): parked-fetch "
+         "wake-up, response write, append lock wait");
 
   py::class_<RateFeeder, std::shared_ptr<RateFeeder>>(k, "RateFeeder")
       .def(py::init<std::shared_ptr<Broker>, std::string, std::vector<int>,

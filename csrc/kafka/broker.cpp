@@ -27,6 +27,12 @@ int64_t now_ms() {
       .count();
 }
 
+int64_t now_ns() {
+  return std::chrono::duration_cast<std::chrono::nanoseconds>(
+             std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+
 int64_t wall_ms() {
   return std::chrono::duration_cast<std::chrono::milliseconds>(
              std::chrono::system_clock::now().time_since_epoch())
@@ -203,9 +209,11 @@ void Broker::wake(const std::string& topic, int partition) {
   std::lock_guard<std::mutex> lk(append_mu_);
   auto it = waiters_.find({topic, partition});
   if (it == waiters_.end()) return;
+  const int64_t t = now_ns();
   for (Waiter* w : it->second) {
     {
       std::lock_guard<std::mutex> wl(w->m);
+      if (!w->flag) w->t_wake_ns = t;
       w->flag = true;
     }
     w->cv.notify_one();
@@ -326,13 +334,26 @@ int64_t Broker::append_shared(const std::string& topic, int partition,
       peek_batch(reinterpret_cast<const uint8_t*>(batch->data()), batch->size(), false);
   int64_t base;
   {
+    const int64_t t0 = now_ns();
     std::lock_guard<std::mutex> lk(mu_);
+    probe_lock_.add(now_ns() - t0);
     PartitionLog* log = find_log(topic, partition);
     if (!log) throw std::invalid_argument("unknown topic/partition " + topic);
     base = append_locked(*log, std::move(batch), bi);
   }
   wake(topic, partition);
   return base;
+}
+
+BrokerProbes Broker::take_probes() {
+  BrokerProbes p;
+  p.wake_max_us = probe_wake_.max_ns.exchange(0) / 1000;
+  p.wake_slow = probe_wake_.slow.exchange(0);
+  p.flush_max_us = probe_flush_.max_ns.exchange(0) / 1000;
+  p.flush_slow = probe_flush_.slow.exchange(0);
+  p.lock_max_us = probe_lock_.max_ns.exchange(0) / 1000;
+  p.lock_slow = probe_lock_.slow.exchange(0);
+  return p;
 }
 
 int64_t Broker::log_start(const std::string& topic, int partition) const {
@@ -455,6 +476,7 @@ void Broker::serve(int fd) {
       ok = false;
     }
     if (!ok) break;
+    const bool fetch = c.parked;
     if (c.parked) {
       // register on every requested partition before the first attempt, so an append between
       // an attempt and the wait sets the flag and is not missed
@@ -467,16 +489,21 @@ void Broker::serve(int fd) {
         for (auto& k : keys) waiters_[k].push_back(&w);
       }
       bool final_attempt = c.fetch.max_wait_ms <= 0;
+      int64_t t_wake = 0;
       for (;;) {
         {
           std::lock_guard<std::mutex> wl(w.m);
           w.flag = false;
         }
-        if (try_fetch(c, final_attempt)) break;
+        if (try_fetch(c, final_attempt)) {
+          if (t_wake) probe_wake_.add(now_ns() - t_wake);
+          break;
+        }
         std::unique_lock<std::mutex> wl(w.m);
         w.cv.wait_until(
             wl, std::chrono::steady_clock::time_point(std::chrono::milliseconds(c.deadline)),
             [&] { return w.flag || !running_; });
+        t_wake = w.flag ? w.t_wake_ns : 0;
         final_attempt = now_ms() >= c.deadline || !running_;
       }
       std::lock_guard<std::mutex> lk(append_mu_);
@@ -488,7 +515,9 @@ void Broker::serve(int fd) {
         if (v.empty()) waiters_.erase(it);
       }
     }
+    const int64_t t0 = fetch ? now_ns() : 0;
     if (!flush(c)) break;
+    if (fetch) probe_flush_.add(now_ns() - t0);
   }
   close(fd);
   if (!c.spliced.empty()) {

@@ -63,6 +63,14 @@ struct BrokerStats {
   int64_t bytes_spliced = 0;  // part of bytes_out sent zero-copy
 };
 
+// Latency-tail probes of the serving path, since the last take_probes(): the worst and the
+// number of > 1 ms cases of (a) a parked fetch's wake-up: append signalled -> response built,
+// (b) writing one response to the socket, (c) an append waiting for the log lock.
+struct BrokerProbes {
+  int64_t wake_max_us = 0, wake_slow = 0, flush_max_us = 0, flush_slow = 0;
+  int64_t lock_max_us = 0, lock_slow = 0;
+};
+
 class Broker {
  public:
   explicit Broker(BrokerConfig cfg);
@@ -97,6 +105,7 @@ class Broker {
                        int64_t max_bytes) const;
   int64_t committed(const std::string& group, const std::string& topic, int partition) const;
   BrokerStats stats() const;
+  BrokerProbes take_probes();
   GroupInfo describe_group(const std::string& group) { return coord_.describe(group); }
 
  public:
@@ -151,7 +160,18 @@ class Broker {
     std::mutex m;
     std::condition_variable cv;
     bool flag = false;
+    int64_t t_wake_ns = 0;  // when the flag was first set (probe)
   };
+  struct Probe {
+    std::atomic<int64_t> max_ns{0}, slow{0};
+    void add(int64_t ns) {
+      int64_t m = max_ns.load(std::memory_order_relaxed);
+      while (ns > m && !max_ns.compare_exchange_weak(m, ns, std::memory_order_relaxed)) {
+      }
+      if (ns > 1000000) slow.fetch_add(1, std::memory_order_relaxed);
+    }
+  };
+  Probe probe_wake_, probe_flush_, probe_lock_;
   std::mutex append_mu_;  // waiters_
   std::map<std::pair<std::string, int>, std::vector<Waiter*>> waiters_;
   std::atomic<bool> running_{false};

@@ -79,3 +79,29 @@ measure("H2D 64KB pinned", h2d)
 measure("D2H 4KB pinned", d2h)
 measure("event record+query", record_query)
 measure("kernel launch", kernel)
+
+
+g = torch.cuda.CUDAGraph()
+x = torch.zeros(1 << 16, device="cuda")
+with torch.cuda.graph(g):
+    for _ in range(8):
+        x.add_(1)
+
+
+def graph(n):
+    for _ in range(n):
+        g.replay()
+
+
+measure("graph replay (8 kernels)", graph)
+
+
+def graph_query(n):
+    for _ in range(n):
+        g.replay()
+        hip.hipEventRecord(ev, ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+        while hip.hipEventQuery(ev) != 0:
+            pass
+
+
+measure("graph replay + event record/query", graph_query)
