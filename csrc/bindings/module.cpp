@@ -288,7 +288,8 @@ PYBIND11_MODULE(_C, m) {
       .def_property_readonly("max_batch", &gale::Executor::max_batch)
       .def_property_readonly("slots", &gale::Executor::slots)
       .def_property_readonly("device", &gale::Executor::device)
-      .def_property_readonly("graphs_captured", &gale::Executor::graphs_captured);
+      .def_property_readonly("graphs_captured", &gale::Executor::graphs_captured)
+      .def_property_readonly("graph_pays", &gale::Executor::graph_pays);
 
   gale::bind_host(m);
 }

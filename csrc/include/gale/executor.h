@@ -86,6 +86,12 @@ class Executor {
 
   // Enqueue the forward for `batch` images of `slot` on `stream`. use_graph replays (capturing on
   // first use) the graph of the smallest bucket >= batch; otherwise launches kernels eagerly.
+  // Plans of at most kMaxDirectOps kernels (the whole-network ResNet-20 kernel) always launch
+  // directly: a graph saves nothing there, runs the padded bucket batch, and every replay costs
+  // CPU on the HIP runtime's worker thread (~0.9 core at the serving rate, -> 0.16 with direct
+  // launches, tools/gpu/r3_probe.sh).
+  static constexpr size_t kMaxDirectOps = 2;
+  bool graph_pays() const { return spec_.ops.size() > kMaxDirectOps; }
   void run(int slot, int batch, hipStream_t stream, bool use_graph);
   // Eager forward on caller-provided device buffers (tests / ops API; no graph).
   void run_on(int batch, const void* in, void* out, hipStream_t stream);

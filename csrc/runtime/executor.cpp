@@ -167,7 +167,7 @@ void Executor::run(int slot, int batch, hipStream_t stream, bool use_graph) {
   if (slot < 0 || slot >= spec_.slots) throw std::invalid_argument("bad slot");
   if (batch <= 0) return;
   if (batch > spec_.max_batch) throw std::invalid_argument("batch > max_batch");
-  if (!use_graph) {
+  if (!use_graph || !graph_pays()) {
     launch_all(batch, bufs_[slot].data(), stream);
     return;
   }
@@ -202,6 +202,7 @@ void Executor::run(int slot, int batch, hipStream_t stream, bool use_graph) {
 }
 
 void Executor::capture_all(hipStream_t stream) {
+  if (!graph_pays()) return;
   for (int s = 0; s < spec_.slots; ++s)
     for (int b : buckets_) run(s, b, stream, true);
   check_hip(hipStreamSynchronize(stream), "capture_all sync");
