@@ -90,6 +90,10 @@ def parse_args(argv=None):
     ap.add_argument("--gpu-ingest", action=argparse.BooleanOptionalAction, default=True,
                     help="CRC32C + image counting of fetch buffers on the GPU (host reads only "
                          "Kafka framing)")
+    ap.add_argument("--text-pack", action=argparse.BooleanOptionalAction, default=False,
+                    help="sources nibble-pack the fetched JSON text for the host->GPU link "
+                         "(expanded on the device; needs AVX-512 VBMI; costs host CPU, "
+                         "profiles/r3_nibble_transport_ab.txt)")
     ap.add_argument("--check-crcs", action=argparse.BooleanOptionalAction, default=True,
                     help="consumer CRC32C verification (Kafka check.crcs; diagnosis only)")
     ap.add_argument("--rate", type=float, default=0.0,
@@ -522,6 +526,7 @@ def main(argv=None) -> int:
                      replicas=a.replicas_per_gpu * local_gpus,
                      decode_threads=a.decode_threads, slo_p99_ms=a.slo_p99_ms,
                      gpu_wait_poll_us=a.gpu_wait_poll_us, gpu_ingest=a.gpu_ingest, gpu_encode=a.gpu_encode,
+                     text_pack=a.text_pack,
                      stub=a.stub, stub_null=a.stub_null, commit_interval_ms=500,
                      check_crcs=a.check_crcs,
                      output_partition=rank if a.local_output and world > 1 else -1,
@@ -708,6 +713,9 @@ def main(argv=None) -> int:
             "step_rates": [round(r) for r in step_rates],
             "warmup_s": round(warm_s, 2), "warmup_rates": [round(r) for r in warm_rates],
             "json_mb_per_s_rank0": round(st["bytes_in"] / elapsed / 1e6, 1),
+            # host -> GPU link bytes per fetched text byte (nibble transport: ~0.5)
+            "link_ratio_rank0": round(st["ingest_link_bytes"] / st["ingest_text_bytes"], 4)
+            if st.get("ingest_text_bytes") else None,
             "cpu_cores_busy_rank0": round(sum(cores.values()), 2),
             "cpu_cores_by_stage_rank0": cores,
             "encode_s": round(t_enc, 1),

@@ -12,6 +12,7 @@
 #include <thread>
 
 #include "../codec/json_codec.h"
+#include "../codec/text_pack.h"
 #include "../kafka/broker.h"
 #include "../kafka/client.h"
 #include "../kafka/protocol.h"
@@ -403,6 +404,63 @@ void bind_host(py::module_& m) {
                                        C, out.mutable_data(), max_images, &images);
     return py::make_tuple(st, out);
   }, py::arg("data"), py::arg("H"), py::arg("W"), py::arg("C"), py::arg("max_images") = -1);
+  // ---- nibble transport (text_pack.h) ----
+  m.def("text_pack_fast", &codec::text_pack_fast);
+  m.def("text_pack", [](py::bytes b, bool force_scalar) {
+    const std::string_view s = view(b);
+    std::string out(codec::pack_bound(s.size()), '\0');
+    py::array_t<uint32_t> tab((py::ssize_t)(2 * codec::pack_groups(s.size())));
+    const size_t n = codec::text_pack(reinterpret_cast<const uint8_t*>(s.data()), s.size(),
+                                      reinterpret_cast<uint8_t*>(out.data()), tab.mutable_data(),
+                                      force_scalar);
+    out.resize(n);
+    return py::make_tuple(py::bytes(out), tab);
+  }, py::arg("data"), py::arg("force_scalar") = false);
+  m.def("text_pack_chunked", [](py::bytes b, std::vector<size_t> cuts) {
+    // resumable packing as a receive loop drives it: progress at every cut, then finish
+    const std::string_view s = view(b);
+    const auto* src = reinterpret_cast<const uint8_t*>(s.data());
+    std::string out(codec::pack_bound(s.size()), '\0');
+    py::array_t<uint32_t> tab((py::ssize_t)(2 * codec::pack_groups(s.size())));
+    codec::PackState st;
+    auto* dst = reinterpret_cast<uint8_t*>(out.data());
+    for (size_t c : cuts)
+      codec::text_pack_blocks(src, std::min(c, s.size()) / codec::kPackBlock, dst,
+                              tab.mutable_data(), st);
+    out.resize(codec::text_pack_finish(src, s.size(), dst, tab.mutable_data(), st));
+    return py::make_tuple(py::bytes(out), tab);
+  });
+  m.def("text_unpack_host", [](py::bytes packed, py::array_t<uint32_t, py::array::c_style> tab,
+                               size_t n) {
+    std::string out(n, '\0');
+    codec::text_unpack_host(reinterpret_cast<const uint8_t*>(view(packed).data()), tab.data(), n,
+                            reinterpret_cast<uint8_t*>(out.data()));
+    return py::bytes(out);
+  });
+  m.def("text_pack_bench_ptr", [](uintptr_t src, size_t n, uintptr_t dst, uintptr_t tab,
+                                  int iters) {
+    // seconds per pass: packing between caller-provided buffers (e.g. pinned vs pageable)
+    size_t out = 0;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int i = 0; i < iters; ++i)
+      out = codec::text_pack(reinterpret_cast<const uint8_t*>(src), n,
+                             reinterpret_cast<uint8_t*>(dst), reinterpret_cast<uint32_t*>(tab));
+    const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    return py::make_tuple(dt / std::max(1, iters), out);
+  });
+  m.def("text_pack_bench", [](py::bytes b, int iters, bool force_scalar) {
+    // seconds per pass over b (host packing throughput)
+    const std::string_view s = view(b);
+    std::vector<uint8_t> out(codec::pack_bound(s.size()) + 64);
+    std::vector<uint32_t> tab(2 * codec::pack_groups(s.size()) + 2);
+    size_t n = 0;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int i = 0; i < iters; ++i)
+      n = codec::text_pack(reinterpret_cast<const uint8_t*>(s.data()), s.size(), out.data(),
+                           tab.data(), force_scalar);
+    const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    return py::make_tuple(dt / std::max(1, iters), n);
+  }, py::arg("data"), py::arg("iters") = 10, py::arg("force_scalar") = false);
   m.def("format_float_java", [](float v) {
     char buf[48];
     return std::string(buf, (size_t)codec::format_float_java(v, buf));

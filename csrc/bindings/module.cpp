@@ -221,6 +221,15 @@ PYBIND11_MODULE(_C, m) {
                                        reinterpret_cast<hipStream_t>(stream)),
               "json_count_records");
         });
+  m.def("text_unpack", [](uintptr_t packed, uintptr_t tab, int64_t n, uintptr_t out,
+                          uintptr_t stream) {
+    if (out % 16 || packed % 8) throw std::invalid_argument("text_unpack: misaligned buffers");
+    gale::check_hip(gale::text_unpack(reinterpret_cast<const uint8_t*>(packed),
+                                      reinterpret_cast<const uint32_t*>(tab), n,
+                                      reinterpret_cast<uint8_t*>(out),
+                                      reinterpret_cast<hipStream_t>(stream)),
+                    "text_unpack");
+  });
   m.def("format_floats_java", [](int n, uintptr_t x, uintptr_t out16, uintptr_t stream) {
     gale::check_hip(gale::format_floats_java(n, reinterpret_cast<const float*>(x),
                                              reinterpret_cast<void*>(out16),

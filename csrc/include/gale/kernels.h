@@ -175,6 +175,12 @@ struct CrcChunk {
 hipError_t crc32c_chunks(const uint8_t* bytes, const CrcChunk* chunks, int n,
                          const uint32_t* tables, uint32_t* out, hipStream_t stream);
 
+// Expands a nibble-packed span (csrc/codec/text_pack.h: 64-byte blocks, per-2-KiB-group
+// {base offset, packed-block mask} pairs in tab) into out[0, n). out must be 16-byte aligned,
+// packed 8-byte aligned.
+hipError_t text_unpack(const uint8_t* packed, const uint32_t* tab, int64_t n, uint8_t* out,
+                       hipStream_t stream);
+
 // ---- prediction text (format.hip) -----------------------------------------------------------
 // n binary32 values -> Java Float.toString text (JDK 19+ shortest-digit rules, the same text as
 // codec::format_float_java), one 16-byte slot per value: characters from byte 0, length in

@@ -116,9 +116,11 @@ void Connection::send_all(const char* p, size_t n) {
   }
 }
 
-void Connection::recv_all(uint8_t* p, size_t n) {
+void Connection::recv_all(uint8_t* p, size_t n, RecvTap* tap) {
+  const uint8_t* base = p;
+  const size_t cap = tap ? std::max<size_t>(4096, tap->chunk_bytes()) : n;
   while (n) {
-    const ssize_t r = ::recv(fd_, p, n, 0);
+    const ssize_t r = ::recv(fd_, p, std::min(n, cap), 0);
     if (r == 0) throw KafkaError(-1, "connection closed by broker " + host_);
     if (r < 0) {
       if (errno == EINTR) continue;
@@ -128,6 +130,7 @@ void Connection::recv_all(uint8_t* p, size_t n) {
     }
     p += r;
     n -= (size_t)r;
+    if (tap) tap->progress((size_t)(p - base));
   }
 }
 
@@ -147,7 +150,8 @@ int32_t Connection::send(ApiKey key, const Writer& body) {
   return h.correlation_id;
 }
 
-std::shared_ptr<uint8_t> Connection::recv(int32_t corr, size_t* size, const BufferAlloc& alloc) {
+std::shared_ptr<uint8_t> Connection::recv(int32_t corr, size_t* size, const BufferAlloc& alloc,
+                                          RecvTap* tap, int64_t* tap_result) {
   uint8_t hdr[8];
   recv_all(hdr, 8);
   Reader r(hdr, 8);
@@ -159,7 +163,9 @@ std::shared_ptr<uint8_t> Connection::recv(int32_t corr, size_t* size, const Buff
                              std::to_string(corr) + ")");
   const size_t n = (size_t)sz - 4;
   std::shared_ptr<uint8_t> buf = alloc(n);
-  recv_all(buf.get(), n);
+  if (tap) tap->begin(buf.get(), n);
+  recv_all(buf.get(), n, tap);
+  if (tap && tap_result) *tap_result = tap->finish();
   *size = n;
   return buf;
 }
@@ -889,7 +895,7 @@ void Consumer::collect(std::vector<Fetched>& out) {
     Fetched f;
     f.crc_checked = cfg_.check_crcs;
     try {
-      f.buf = cluster_.node(inf.node).recv(inf.corr, &f.size, alloc_);
+      f.buf = cluster_.node(inf.node).recv(inf.corr, &f.size, alloc_, tap_.get(), &f.tap_result);
     } catch (...) {
       // these connections are mid-response: reconnect them, forget their in-flight fetches
       for (size_t j = i; j < infs.size(); ++j) cluster_.drop(infs[j].node);

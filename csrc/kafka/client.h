@@ -48,6 +48,19 @@ struct ClientConfig {
 using BufferAlloc = std::function<std::shared_ptr<uint8_t>(size_t bytes)>;
 std::shared_ptr<uint8_t> heap_alloc(size_t bytes);
 
+// Observes a response body while it is received (e.g. to transform the bytes while they are
+// cache-hot). begin(buf, n) before the first byte; progress(done) after every receive call
+// (bytes [0, done) are in place; one call receives at most chunk_bytes()); finish() after the
+// last one, its value is kept in Fetched::tap_result.
+class RecvTap {
+ public:
+  virtual ~RecvTap() = default;
+  virtual void begin(uint8_t* buf, size_t n) = 0;
+  virtual void progress(size_t done) = 0;
+  virtual int64_t finish() = 0;
+  virtual size_t chunk_bytes() const { return 256 << 10; }
+};
+
 class Connection {
  public:
   Connection(const std::string& host, int port, const ClientConfig& cfg);
@@ -58,14 +71,15 @@ class Connection {
   int32_t send(ApiKey key, const Writer& body);  // returns the correlation id
   // Receive the response for `corr` (responses arrive in request order on one connection).
   // The returned buffer starts AFTER the correlation id.
-  std::shared_ptr<uint8_t> recv(int32_t corr, size_t* size, const BufferAlloc& alloc);
+  std::shared_ptr<uint8_t> recv(int32_t corr, size_t* size, const BufferAlloc& alloc,
+                                RecvTap* tap = nullptr, int64_t* tap_result = nullptr);
   std::string request(ApiKey key, const Writer& body);  // send + recv into a string
   const std::string& host() const { return host_; }
   int port() const { return port_; }
 
  private:
   void send_all(const char* p, size_t n);
-  void recv_all(uint8_t* p, size_t n);
+  void recv_all(uint8_t* p, size_t n, RecvTap* tap = nullptr);
   int fd_ = -1;
   std::string host_;
   int port_;
@@ -222,6 +236,7 @@ struct Fetched {
   std::vector<RecordRef> records;
   std::vector<BatchSpan> batches;  // record batches (for deferred CRC checks)
   bool crc_checked = false;
+  int64_t tap_result = -1;  // the consumer's RecvTap::finish() for this body (-1: no tap)
 };
 
 class Consumer {
@@ -246,6 +261,8 @@ class Consumer {
   int64_t committed(int partition);
   std::map<int, int64_t> high_watermarks() const { return hw_; }
   Cluster& cluster() { return cluster_; }
+  // fetch response bodies are shown to this tap while they are received
+  void set_recv_tap(std::shared_ptr<RecvTap> tap) { tap_ = std::move(tap); }
 
  private:
   int64_t list_offset(int partition, int64_t ts);
@@ -259,6 +276,7 @@ class Consumer {
   void drain();  // collect into ready_ (before any other request on a fetch connection)
   ConsumerConfig cfg_;
   BufferAlloc alloc_;
+  std::shared_ptr<RecvTap> tap_;
   Cluster cluster_;
   std::string topic_;
   std::vector<int> parts_;

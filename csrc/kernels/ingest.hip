@@ -70,7 +70,60 @@ __global__ __launch_bounds__(256) void crc32c_chunks_kernel(const uint8_t* bytes
   }
 }
 
+// Nibble-transport expansion (csrc/codec/text_pack.h): one thread per 16 output bytes, so a
+// 64-byte block is four lanes and a 2 KiB group two quarter-waves. A lane finds its block's
+// source from the group's base offset plus the popcount of the packed blocks before it (packed
+// blocks are 32 bytes, raw 64): one 8-byte load becomes 16 characters (one 16-byte store), or a
+// raw piece is copied. Only a raw final partial block stores bytewise. The volume is the fetched
+// text (~54 GB/s at the link's pace): a few us per fetch against 8 TB/s of HBM.
+__global__ __launch_bounds__(256) void text_unpack_kernel(const uint8_t* __restrict__ packed,
+                                                          const uint32_t* __restrict__ tab,
+                                                          int64_t n, uint8_t* __restrict__ out) {
+  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t o = q * 16;
+  if (o >= n) return;
+  const int64_t b = q >> 2;
+  const int sub = (int)(q & 3);
+  const int64_t g = b >> 5;
+  const int k = (int)(b & 31);
+  const uint32_t base = tab[2 * g], mask = tab[2 * g + 1];
+  const int np = __popc(mask & ((1u << k) - 1u));
+  const int64_t src = (int64_t)base + np * 32 + (k - np) * 64;
+  if ((mask >> k) & 1u) {
+    const uint64_t w = *reinterpret_cast<const uint64_t*>(packed + src + sub * 8);
+    uint32_t c[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      uint32_t v = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t nib = (uint32_t)(w >> (16 * i + 4 * j)) & 15u;
+        // codes 10..15 -> "[],-.E"
+        const uint32_t ch = nib < 10 ? 0x30u + nib
+                                     : (uint32_t)(0x452E2D2C5D5Bull >> ((nib - 10) * 8)) & 0xffu;
+        v |= ch << (8 * j);
+      }
+      c[i] = v;
+    }
+    *reinterpret_cast<uint4*>(out + o) = make_uint4(c[0], c[1], c[2], c[3]);
+  } else if (o + 16 <= n) {
+    *reinterpret_cast<uint4*>(out + o) =
+        *reinterpret_cast<const uint4*>(packed + src + sub * 16);
+  } else {
+    for (int64_t j = 0; o + j < n; ++j) out[o + j] = packed[src + sub * 16 + j];
+  }
+}
+
 }  // namespace
+
+hipError_t text_unpack(const uint8_t* packed, const uint32_t* tab, int64_t n, uint8_t* out,
+                       hipStream_t stream) {
+  if (n <= 0) return hipSuccess;
+  const int64_t pieces = (n + 15) / 16;
+  hipLaunchKernelGGL(text_unpack_kernel, dim3((unsigned)((pieces + 255) / 256)), dim3(256), 0,
+                     stream, packed, tab, n, out);
+  return hipGetLastError();
+}
 
 hipError_t crc32c_chunks(const uint8_t* bytes, const CrcChunk* chunks, int n,
                          const uint32_t* tables, uint32_t* out, hipStream_t stream) {

@@ -11,6 +11,7 @@
 #include <sstream>
 
 #include "../codec/json_codec.h"
+#include "pack_tap.h"
 #include "trace.h"
 
 namespace gale {
@@ -287,7 +288,10 @@ void Engine::start() {
     bool gpu = false;
     for (auto& rs : replicas_) gpu |= rs->slot == (int)i && rs->rep->device() >= 0;
     if (!gpu || cfg_.pinned_fetch_bytes <= 0) continue;
-    pools_[i] = std::make_shared<PinnedPool>((size_t)cfg_.fetch_max_bytes + (1 << 20),
+    // packed fetch bodies (pack_tap.h) keep their packed copy in the same chunk
+    const size_t body = (size_t)cfg_.fetch_max_bytes + (1 << 20);
+    const bool pack = cfg_.text_pack && ingest_for((int)i);
+    pools_[i] = std::make_shared<PinnedPool>(pack ? codec::pack_layout_bytes(body) + 4096 : body,
                                              (size_t)cfg_.pinned_fetch_bytes / nslots);
     if (ingest_for((int)i)) pools_[i]->set_mirror_device(slot_dev_[i]);
   }
@@ -620,6 +624,8 @@ void Engine::source_loop(int idx) {
   std::unique_ptr<kafka::Consumer> cons;
   try {
     cons = std::make_unique<kafka::Consumer>(cc, alloc);
+    if (pinned && cfg_.text_pack && ingest_for(slot))
+      cons->set_recv_tap(std::make_shared<PackTap>(pinned));
   } catch (const std::exception& e) {
     fprintf(stderr, "[gale source %d] failed to start: %s\n", idx, e.what());
   }
@@ -1469,6 +1475,17 @@ std::map<std::string, double> Engine::stats() const {
   s["assigned_partitions"] = cfg_.group_membership ? (double)assigned_partitions_
                                                    : (double)partition_offsets().size();
   s["ingested_records"] = (double)ingested_records_;
+  {
+    int64_t text = 0, link = 0;
+    for (auto& kv : ingests_) {
+      int64_t t = 0, l = 0;
+      kv.second->link_bytes(t, l);
+      text += t;
+      link += l;
+    }
+    s["ingest_text_bytes"] = (double)text;
+    s["ingest_link_bytes"] = (double)link;
+  }
   s["thread_s_ingest"] = ingest_ns_ * 1e-9;
   s["eff_max_batch"] = (double)eff_batch_;
   s["eff_max_wait_us"] = (double)eff_wait_ns_ / 1000.0;

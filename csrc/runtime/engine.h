@@ -63,6 +63,9 @@ struct EngineConfig {
   bool check_crcs = true;
   int decode_threads = 2;          // CRC32C + envelope scan workers (0 = on the source thread)
   int64_t pinned_fetch_bytes = 4ll << 30;  // pinned fetch-buffer budget (GPU replicas only)
+  // GPU ingest: sources nibble-pack fetch bodies while receiving them (pack_tap.h) and the text
+  // crosses the host link packed (csrc/codec/text_pack.h)
+  bool text_pack = false;
   int commit_interval_ms = 2000;   // storm-kafka's ZK commit period
   // consumer-group membership (elastic DP, kafka::GroupMember): the input partitions are shared
   // by every engine of group_id; a member that dies or leaves has its partitions moved to the

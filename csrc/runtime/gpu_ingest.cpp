@@ -8,6 +8,7 @@
 #include <thread>
 
 #include "../codec/json_codec.h"
+#include "../codec/text_pack.h"
 #include "gale/executor.h"
 
 namespace gale {
@@ -115,14 +116,25 @@ void GpuIngest::run(int lane, const kafka::Fetched& f, uint8_t* dev, bool check_
   }
   const size_t nc = chunks.size(), nr = rec_of.size();
   if (nc == 0 && nr == 0) return;
-  const size_t o_tiles = align16(nc * sizeof(CrcChunk));
+  // packed body (the source's PackTap, text_pack.h): the whole body crosses the link packed and
+  // is expanded in its device mirror; otherwise the span holding batches and records, raw
+  const bool packed = f.tap_result >= 0;
+  if (packed) {
+    lo = 0;
+    hi = f.size;
+  }
+  lo &= ~(size_t)15;
+  const size_t span = hi - lo;
+  const size_t ng = packed ? codec::pack_groups(span) : 0;
+  const size_t o_chunks = align16(ng * 2 * sizeof(uint32_t));
+  const size_t o_tiles = o_chunks + align16(nc * sizeof(CrcChunk));
   const size_t o_recs = o_tiles + align16((size_t)ntiles * sizeof(int));
   const size_t o_tok = o_recs + nr * sizeof(JsonRecord);  // (JsonRecord is 32 bytes)
   const size_t o_crc = o_tok + align16(nr * 4);
   const size_t io_bytes = o_crc + align16(nc * 4);
   check_hip(hipSetDevice(device_), "ingest: hipSetDevice");
   grow(L, io_bytes + 16, (size_t)ntiles + 1);
-  CrcChunk* hc = reinterpret_cast<CrcChunk*>(L.h_io);
+  CrcChunk* hc = reinterpret_cast<CrcChunk*>(L.h_io + o_chunks);
   int* ht = reinterpret_cast<int*>(L.h_io + o_tiles);
   JsonRecord* hr = reinterpret_cast<JsonRecord*>(L.h_io + o_recs);
   if (nc) memcpy(hc, chunks.data(), nc * sizeof(CrcChunk));
@@ -142,17 +154,33 @@ void GpuIngest::run(int lane, const kafka::Fetched& f, uint8_t* dev, bool check_
     tile += nt;
   }
   memset(L.h_io + o_tok, 0, nr * 4);  // token counters start at zero (no device memset)
-  // ---- device: text span -> mirror, plan, CRC windows, token counts, results back
-  lo &= ~(size_t)15;
+  // ---- device: text span -> mirror (packed: H2D of the packed stream, expanded in place),
+  // plan, CRC windows, token counts, results back
   hipStream_t st = L.stream;
-  check_hip(hipMemcpyAsync(dev + lo, f.buf.get() + lo, hi - lo, hipMemcpyHostToDevice, st),
-            "ingest: H2D text");
+  size_t link = span;
+  if (packed) {
+    link = (size_t)f.tap_result;
+    memcpy(L.h_io, f.buf.get() + codec::tab_offset(span), ng * 2 * sizeof(uint32_t));
+    const size_t po = codec::pack_offset(span);
+    check_hip(hipMemcpyAsync(dev + po, f.buf.get() + po, link, hipMemcpyHostToDevice, st),
+              "ingest: H2D packed text");
+  } else {
+    check_hip(hipMemcpyAsync(dev + lo, f.buf.get() + lo, span, hipMemcpyHostToDevice, st),
+              "ingest: H2D text");
+  }
   check_hip(hipMemcpyAsync(L.d_io, L.h_io, o_crc, hipMemcpyHostToDevice, st), "ingest: H2D plan");
+  if (packed)
+    check_hip(text_unpack(dev + codec::pack_offset(span), reinterpret_cast<const uint32_t*>(L.d_io),
+                          (int64_t)span, dev, st),
+              "ingest: text_unpack");
+  text_bytes_ += (int64_t)span;
+  link_bytes_ += (int64_t)link;
   uint32_t* d_crc = reinterpret_cast<uint32_t*>(L.d_io + o_crc);
   int* d_tok = reinterpret_cast<int*>(L.d_io + o_tok);
   JsonRecord* d_rec = reinterpret_cast<JsonRecord*>(L.d_io + o_recs);
   if (nc)
-    check_hip(crc32c_chunks(dev, reinterpret_cast<const CrcChunk*>(L.d_io), (int)nc, d_tables_,
+    check_hip(crc32c_chunks(dev, reinterpret_cast<const CrcChunk*>(L.d_io + o_chunks), (int)nc,
+                            d_tables_,
                             d_crc, st),
               "ingest: crc32c_chunks");
   if (nr)

@@ -3,6 +3,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <memory>
 #include <mutex>
 #include <vector>
@@ -21,6 +22,10 @@ class GpuIngest : public Ingest {
   int device() const override { return device_; }
   void run(int lane, const kafka::Fetched& f, uint8_t* dev, bool check_crcs, int H, int W, int C,
            IngestIO& io) override;
+  void link_bytes(int64_t& text, int64_t& link) const override {
+    text = text_bytes_.load();
+    link = link_bytes_.load();
+  }
 
  private:
   struct Lane {
@@ -28,7 +33,8 @@ class GpuIngest : public Ingest {
     hipStream_t stream = nullptr;
     hipEvent_t done = nullptr;
     // one pinned staging buffer and its device image:
-    //   [CrcChunk x nc][tile_rec x nt][JsonRecord x nr][tokens i32 x nr][crc u32 x nc]
+    //   [pack tab u32 x 2ng (packed bodies)][CrcChunk x nc][tile_rec x nt][JsonRecord x nr]
+    //   [tokens i32 x nr][crc u32 x nc]
     // the host writes the plan and zeroed token counters, ONE H2D copies up to the tokens, ONE
     // D2H copies back [JsonRecord..crc] (per-record status, element counts, window CRCs)
     uint8_t* h_io = nullptr;
@@ -40,6 +46,7 @@ class GpuIngest : public Ingest {
   void grow(Lane& L, size_t io_bytes, size_t tiles);
   void wait(Lane& L);
   int device_, poll_us_;
+  std::atomic<int64_t> text_bytes_{0}, link_bytes_{0};
   uint32_t* d_tables_ = nullptr;
   std::vector<std::unique_ptr<Lane>> lanes_;
   kafka::CrcShift shift_chunk_;

@@ -35,6 +35,9 @@ class Ingest {
   // dev: device mirror of f.buf (same offsets). Throws on a device error.
   virtual void run(int lane, const kafka::Fetched& f, uint8_t* dev, bool check_crcs, int H, int W,
                    int C, IngestIO& io) = 0;
+  // fetched text bytes staged so far, and the bytes that crossed the host link for them (less
+  // when the text is nibble-packed, csrc/codec/text_pack.h)
+  virtual void link_bytes(int64_t& text, int64_t& link) const { text = link = 0; }
 };
 
 }  // namespace gale

@@ -64,6 +64,10 @@ class GaleConfig:
     check_crcs: bool = True            # Kafka consumer check.crcs
     gpu_ingest: bool = True            # CRC32C + image counts of pinned fetch buffers on the GPU
                                        # (the host reads only Kafka framing; csrc/runtime/ingest.h)
+    text_pack: bool = False            # GPU ingest: sources nibble-pack fetch bodies for the
+                                       # PCIe link, expanded on the device (text_pack.h); needs
+                                       # AVX-512 VBMI; for hosts with idle cores behind a
+                                       # link-bound GPU (profiles/r3_nibble_transport_ab.txt)
     # parallelism (R3)
     workers: int = 8                   # NUM_WORKERS: placement only (one process per GPU here)
     source_parallelism: int = 2        # KAFKA_SPOUT_PARAL
@@ -177,6 +181,7 @@ class GaleConfig:
             lag_rebalance_records=self.lag_rebalance_records,
             rebalance_cooldown_ms=self.rebalance_cooldown_ms,
             decode_threads=self.decode_threads, check_crcs=self.check_crcs,
+            text_pack=bool(self.gpu_ingest and self.text_pack and _pack_fast()),
             acks=self.acks, sink_mode=self.sink_mode, linger_ms=self.linger_ms,
             value_format=self.value_format, type_id_header=self.type_id_header,
             on_error=self.on_error, output_key=self.output_key,
@@ -189,6 +194,12 @@ class GaleConfig:
             watchdog_ms=self.watchdog_ms, max_restarts=self.max_restarts,
             restart_backoff_ms=self.restart_backoff_ms, fault=self.fault, seed=self.seed,
             trace=self.trace)
+
+
+def _pack_fast() -> bool:
+    from gale._native import native
+
+    return bool(native().text_pack_fast())
 
 
 def _coerce(f: dataclasses.Field, raw: Any) -> Any:

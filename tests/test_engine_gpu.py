@@ -163,13 +163,17 @@ def centered_log(p):
 
 
 @pytest.mark.parametrize("model,ingest", [("resnet20", True), ("resnet20", False),
-                                          ("lenet5", True)])
+                                          ("lenet5", True), ("resnet20", "pack")])
 def test_gpu_engine_matches_oracle(broker, model, ingest):
     """Every output record is matched to ITS input by key (output_key=input) and compared on
     logits (centered log-softmax) with a bf16-level relative tolerance: a misrouted batch split
     (image i's row under record j) or a wrong image count cannot pass. ingest=True: CRC32C and
     image counts on the GPU and the parser reading the device-resident fetch buffer; False: the
-    host decode path with per-batch H2D staging."""
+    host decode path with per-batch H2D staging; "pack": GPU ingest of nibble-packed fetch
+    bodies (the source's PackTap, expanded on the device before the CRC / count / parse)."""
+    pack = ingest == "pack"
+    if pack and not C.text_pack_fast():
+        pytest.skip("no AVX-512 VBMI on this host")
     net = get_model(model)
     params = init_params(net, seed=0, calib_batch=16)
     rng = np.random.default_rng(1)
@@ -182,7 +186,8 @@ def test_gpu_engine_matches_oracle(broker, model, ingest):
     broker.append("in", 0, [b'{"instances": [[[[0.5]]]]}'], [b"bad"])  # wrong shape -> null
     cfg = GaleConfig(topology_name="g", input_topic="in", output_topic="out", model=model,
                      bootstrap=f"127.0.0.1:{broker.port}", start_offset="earliest",
-                     max_batch=32, max_wait_us=500, output_key="input", gpu_ingest=ingest)
+                     max_batch=32, max_wait_us=500, output_key="input",
+                     gpu_ingest=bool(ingest), text_pack=pack)
     eng = Engine(cfg, devices=[0], max_records=len(counts) + 1, params=params)
     eng.start()
     assert eng.wait(120), eng.stats()
@@ -203,7 +208,9 @@ def test_gpu_engine_matches_oracle(broker, model, ingest):
     assert worst < 2e-2, worst
     st = eng.stats()
     assert st["errors"] == 1 and st["images_out"] == sum(counts)
-    assert (st["ingested_records"] > 0) == ingest
+    assert (st["ingested_records"] > 0) == bool(ingest)
+    if pack:  # the text crossed the link packed (~0.5 bytes per fetched byte)
+        assert 0 < st["ingest_link_bytes"] < 0.6 * st["ingest_text_bytes"], st
 
 
 def test_gpu_crc32c_chunks_kernel():
