@@ -171,8 +171,107 @@ struct Text {
 // rounding midpoint (one rounding of an exact product: only d == midpoint is ambiguous). Those
 // rare tokens are decided exactly: x is compared with the midpoint (2M+1) * 2^(e-1) as big
 // integers (w * 5^|q| left-aligned in 256 bits against the midpoint's significand), ties to
-// even. Exact for every input with <= 19 significant digits (all of Jackson's float output).
+// even. With dropped digits, w * 10^q < x < (w + 1) * 10^q brackets x; only a midpoint strictly
+// inside that bracket (x within 1e-19 relative of it) needs the dropped digits, and then every
+// digit of the token is compared with the midpoint's finite decimal expansion (<= 115 digits for
+// binary32) - exact for any length, like Java's Float.parseFloat.
 // (The 5^k table and the 256-bit comparison live in exact_decimal.cuh.)
+
+// N *= m (base-1e9 limbs, little-endian; m < 2^32)
+__device__ __forceinline__ void limbs_mul(uint32_t* N, int* nl, uint32_t m) {
+  uint64_t carry = 0;
+  for (int i = 0; i < *nl; ++i) {
+    const uint64_t v = (uint64_t)N[i] * m + carry;
+    N[i] = (uint32_t)(v % 1000000000ull);
+    carry = v / 1000000000ull;
+  }
+  while (carry) {
+    N[(*nl)++] = (uint32_t)(carry % 1000000000ull);
+    carry /= 1000000000ull;
+  }
+}
+
+// Sign of x - K * 2^E, x the decimal token at [i0, end) with all of its digits. K * 2^E is
+// written as N * 10^-s (N = K * 5^-E, s = -E for E < 0; N = K * 2^E, s = 0 otherwise) and its
+// decimal digits are walked against the token's, after comparing the decimal magnitudes.
+__device__ __noinline__ int cmp_token_dyadic(const Text& t, int i0, int end, uint64_t K, int E) {
+  uint32_t N[16];
+  int nl = 0, s = 0;
+  for (uint64_t k = K; k || nl == 0; k /= 1000000000ull) N[nl++] = (uint32_t)(k % 1000000000ull);
+  if (E >= 0) {
+    for (int k = E; k > 0; k -= 29) limbs_mul(N, &nl, 1u << (k < 29 ? k : 29));
+  } else {
+    s = -E;
+    for (int k = s; k > 0; k -= 13) {
+      uint32_t p = 1;
+      for (int j = 0; j < (k < 13 ? k : 13); ++j) p *= 5u;
+      limbs_mul(N, &nl, p);
+    }
+  }
+  int top = 1;
+  for (uint32_t v = N[nl - 1]; v >= 10; v /= 10) ++top;
+  const int nd = 9 * (nl - 1) + top;  // decimal digits of N
+  // token: leading-digit position Lx (x in [10^(Lx-1), 10^Lx)) and exponent
+  int k = i0;
+  if (t.at(k) == '-') ++k;
+  int int_sig = 0, lead_zeros = 0, first = -1;
+  unsigned c = k < end ? t.at(k) : 0u;
+  for (; c >= '0' && c <= '9'; c = ++k < end ? t.at(k) : 0u)
+    if (first >= 0 || c != '0') {
+      if (first < 0) first = k;
+      ++int_sig;
+    }
+  if (c == '.')
+    for (c = ++k < end ? t.at(k) : 0u; c >= '0' && c <= '9'; c = ++k < end ? t.at(k) : 0u)
+      if (first < 0) {
+        if (c == '0') ++lead_zeros;
+        else first = k;
+      }
+  int ex = 0;
+  if (c == 'e' || c == 'E') {
+    c = ++k < end ? t.at(k) : 0u;
+    const bool eneg = c == '-';
+    if (c == '+' || c == '-') c = ++k < end ? t.at(k) : 0u;
+    for (; c >= '0' && c <= '9'; c = ++k < end ? t.at(k) : 0u)
+      if (ex < 100000) ex = ex * 10 + (int)(c - '0');
+    if (eneg) ex = -ex;
+  }
+  if (first < 0) return -1;  // x == 0 < K * 2^E
+  const int Lx = (int_sig > 0 ? int_sig : -lead_zeros) + ex, Lm = nd - s;
+  if (Lx != Lm) return Lx > Lm ? 1 : -1;
+  // digit walk from the leading digits
+  int j = nd - 1;  // next digit of N, from the top
+  for (k = first; k < end; ++k) {
+    c = t.at(k);
+    if (c == '.') continue;
+    if (c < '0' || c > '9') break;
+    int dm = 0;
+    if (j >= 0) {
+      uint32_t v = N[j / 9];
+      for (int r = j % 9; r > 0; --r) v /= 10;
+      dm = (int)(v % 10);
+    }
+    const int dx = (int)(c - '0');
+    if (dx != dm) return dx > dm ? 1 : -1;
+    --j;
+  }
+  for (; j >= 0; --j) {  // the token ended: x < K * 2^E iff N has a nonzero digit left
+    uint32_t v = N[j / 9];
+    for (int r = j % 9; r > 0; --r) v /= 10;
+    if (v % 10) return -1;
+  }
+  return 0;
+}
+
+// sign of x - K * 2^E for x = w * 10^q (+ dropped digits when sticky)
+__device__ __forceinline__ int cmp_x_dyadic(uint64_t w, int q, bool sticky, uint64_t K, int E,
+                                            const Text* tok, int i0, int end) {
+  const int c = cmp_decimal_dyadic(w, q, K, E);
+  if (!sticky) return c;
+  if (c >= 0) return 1;                                    // x > w * 10^q >= midpoint
+  if (cmp_decimal_dyadic(w + 1, q, K, E) <= 0) return -1;  // x < (w + 1) * 10^q <= midpoint
+  return cmp_token_dyadic(*tok, i0, end, K, E);
+}
 
 // binary32 value M * 2^e, 0 <= M <= 2^24 (M = 2^24 at e = 104 stands for +inf)
 __device__ __forceinline__ void f32_split(float f, uint64_t* M, int* e) {
@@ -190,15 +289,15 @@ __device__ __forceinline__ float f32_join(uint64_t M, int e) {
   return __uint_as_float(((uint32_t)(e + 150) << 23) | ((uint32_t)M & 0x7fffff));
 }
 
-__device__ float exact_f32(uint64_t w, int q, bool sticky, double d) {
+__device__ float exact_f32(uint64_t w, int q, bool sticky, double d, const Text* tok, int i0,
+                          int end) {
   float f = (float)d;
   uint64_t M;
   int e;
   f32_split(f, &M, &e);
   for (int it = 0; it < 4; ++it) {
     if (M < (1u << 24)) {  // upper neighbour and the midpoint to it
-      int c = cmp_decimal_dyadic(w, q, 2 * M + 1, e - 1);
-      if (c == 0 && sticky) c = 1;
+      const int c = cmp_x_dyadic(w, q, sticky, 2 * M + 1, e - 1, tok, i0, end);
       if (c > 0 || (c == 0 && (M & 1))) {
         ++M;
         if (M == (1u << 24) && e < 104) { M = 1u << 23; ++e; }
@@ -210,8 +309,7 @@ __device__ float exact_f32(uint64_t w, int q, bool sticky, double d) {
       int ep = e;
       if (M == (1u << 23) && e > -149) { Mp = (1u << 24) - 1; ep = e - 1; }
       if (M == (1u << 24)) { Mp = (1u << 24) - 1; }  // below +inf: FLT_MAX
-      int c = cmp_decimal_dyadic(w, q, 2 * Mp + 1, ep - 1);
-      if (c == 0 && sticky) c = 1;
+      const int c = cmp_x_dyadic(w, q, sticky, 2 * Mp + 1, ep - 1, tok, i0, end);
       if (c < 0 || (c == 0 && (M & 1))) {
         M = Mp;
         e = ep;
@@ -223,7 +321,9 @@ __device__ float exact_f32(uint64_t w, int q, bool sticky, double d) {
   return f32_join(M, e);
 }
 
-__device__ __forceinline__ float scale10(uint64_t w, int q, bool neg, bool sticky) {
+// tok / i0 / end: the token, read again only when sticky and a midpoint is within 1e-19
+__device__ __forceinline__ float scale10(uint64_t w, int q, bool neg, bool sticky,
+                                         const Text* tok = nullptr, int i0 = 0, int end = 0) {
   float r;
   if (w == 0 || q < -66) {
     r = 0.f;
@@ -262,7 +362,7 @@ __device__ __forceinline__ float scale10(uint64_t w, int q, bool neg, bool stick
         ambiguous = fabs(d - lo) <= tol || fabs(d - hi) <= tol;
       }
     }
-    if (ambiguous) r = exact_f32(w, q, sticky, d);
+    if (ambiguous) r = exact_f32(w, q, sticky, d, tok, i0, end);
   }
   return neg ? -r : r;
 }
@@ -336,7 +436,7 @@ __device__ float parse_number(const Text& t, int i0, int end, bool* ok, int* len
   }
   *ok = good;
   *len = i - i0;
-  return good ? scale10(mant, exp10, neg, sticky) : 0.f;
+  return good ? scale10(mant, exp10, neg, sticky, &t, i0, i) : 0.f;
 }
 
 // n / d for n < 2^32, d < 2^20 from a double reciprocal rd = 1/d: the product is below the true

@@ -4,10 +4,10 @@ decimal value to the nearest binary32, ties to even; InferenceBolt.java:76).
 
 The reference value is computed with exact rational arithmetic (fractions.Fraction): NOT
 ``np.float32(float(text))``, which rounds twice (decimal -> double -> float) and is wrong on
-halfway cases. The GPU parser is exact for inputs with <= 19 significant digits; longer
-mantissas are truncated to 19 digits with a sticky bit, which can be one unit in the last place
-off only when the decimal sits within 1e-19 (relative) of a binary32 midpoint - e.g. a midpoint
-written out in full (checked here to stay within that bound).
+halfway cases. The GPU parser is exact for any number of digits: the first 19 decide unless a
+binary32 midpoint lies within 1e-19 (relative) of the token, and then every digit is compared
+with the midpoint's exact decimal expansion (midpoints written out in full, +- one unit in a
+far digit, subnormal midpoints of ~110 digits, integers past 2^64 are checked here).
 """
 
 import random
@@ -71,6 +71,40 @@ TRICKY = [
 ]
 
 
+def dyadic_text(x: Fraction) -> str:
+    """Exact decimal expansion of a dyadic rational (denominator 2^k): k fraction digits."""
+    k = x.denominator.bit_length() - 1
+    assert x.denominator == 1 << k
+    digits = str(x.numerator * 5 ** k).rjust(k + 1, "0")
+    return digits[:-k] + "." + digits[-k:] if k else digits
+
+
+def long_cases(rng, n=300):
+    """Decimals of > 19 significant digits at and around binary32 midpoints."""
+    out = []
+    for i in range(n):
+        kind = i % 3
+        if kind == 0:  # normal range
+            f = np.float32(rng.uniform(1, 2) * 2.0 ** rng.randint(-126, 126))
+        elif kind == 1:  # subnormal: midpoints of up to ~110 significant digits
+            f = np.float32(rng.randint(1, (1 << 23) - 2) * 2.0 ** -149)
+        else:  # integers: midpoints above 2^64
+            f = np.float32(rng.uniform(1, 2) * 2.0 ** rng.randint(64, 126))
+        up = np.nextafter(f, np.float32(np.inf))
+        mid = (Fraction(float(f)) + Fraction(float(up))) / 2
+        t = dyadic_text(mid)
+        out += [t,                                   # exact tie: to even
+                t + ("0000000000" if "." in t else ".0000000000"),  # zeros after the tie
+                dyadic_text(mid + Fraction(1, 1 << 400)) if kind != 2 else t + ".00001",
+                dyadic_text(mid - Fraction(1, 1 << 400)) if kind != 2 else str(int(mid) - 1)]
+        # the same value in exponent form, mantissa digits shifted
+        m = t.replace(".", "").lstrip("0")
+        e = len(t.split(".")[0]) - (len(t.replace(".", "")) - len(m)) - 1
+        out.append(f"{m[0]}.{m[1:]}E{e}")
+        out.append(t[:30])  # truncated
+    return out
+
+
 def gpu_parse_numbers(texts):
     import torch
 
@@ -121,14 +155,12 @@ def test_gpu_json_float_is_correctly_rounded():
         mid = (Fraction(float(f)) + Fraction(float(np.nextafter(f, np.float32(3))))) / 2
         d = f"{float(mid):.18e}"  # 19 significant digits, within 1e-19 of the midpoint
         texts.append(d)
+    texts += long_cases(rng)
+    texts += ["0." + "0" * 40 + "1" + "0" * 60 + "1", "9" * 60, "1" + "0" * 38 + ".5",
+              "0.99999997019767761230468750000000000001", "0.9999999701976776123046874999999999"]
     got, st = gpu_parse_numbers(texts)
     assert st == 0
     want = np.array([f32_correct(t) for t in texts], dtype=np.uint32)
-    short = np.array([sig_digits(t) <= 19 for t in texts])
-    bad = [(texts[i], hex(got[i]), hex(want[i]))
-           for i in np.nonzero((got != want) & short)[0][:10]]
+    assert sum(sig_digits(t) > 19 for t in texts) > 1000
+    bad = [(texts[i], hex(got[i]), hex(want[i])) for i in np.nonzero(got != want)[0][:10]]
     assert not bad, bad
-    # > 19 significant digits (e.g. exact binary32 midpoints written out in full): truncated
-    # with a sticky bit, so at most one unit in the last place off, only at such ties
-    diff = np.abs(got.astype(np.int64) - want.astype(np.int64))
-    assert (diff[~short] <= 1).all()
