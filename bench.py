@@ -100,7 +100,11 @@ def parse_args(argv=None):
                     help="offered load in images/s per GPU: records are appended to the broker "
                          "at this rate while the engine runs (latency under load, BASELINE "
                          "config 5); 0 = a backlog kept ahead of the consumers (max throughput)")
-    ap.add_argument("--broker-zero-copy", action=argparse.BooleanOptionalAction, default=False,
+    # zero-copy fetch responses, as a Kafka broker serves them (sendfile from the page cache):
+    # one host copy less per byte. On boxes whose memory system is loaded it is the difference
+    # between 0.98 M (copying, CPU-bound at 16 of 16 cores) and 1.43-1.52 M img/s; on quiet
+    # boxes both sit near the link (profiles/r3_broker_zero_copy_default.jsonl)
+    ap.add_argument("--broker-zero-copy", action=argparse.BooleanOptionalAction, default=True,
                     help="embedded broker sends fetched batches with vmsplice/splice (Kafka's "
                          "sendfile analogue) instead of writev copies")
     ap.add_argument("--numa-pin", action=argparse.BooleanOptionalAction, default=True,
