@@ -181,6 +181,38 @@ def _cgroup_cpu_stat() -> dict:
         return {}
 
 
+_TCP_KEYS = ("RetransSegs", "TCPTimeouts", "TCPLossProbes", "PruneCalled", "RcvPruned",
+             "TCPRcvQDrop", "TCPBacklogDrop", "TCPZeroWindowDrop", "TCPRcvCollapsed",
+             "TCPWantZeroWindowAdv", "TCPToZeroWindowAdv", "TCPFromZeroWindowAdv",
+             "DelayedACKs", "TCPSpuriousRTOs")
+
+
+def _tcp_counters() -> dict:
+    """Host TCP counters (/proc/net/snmp Tcp + /proc/net/netstat TcpExt) that explain loopback
+    stalls: retransmission timeouts, receive-queue pruning / drops, zero-window episodes."""
+    out = {}
+    for path in ("/proc/net/snmp", "/proc/net/netstat"):
+        try:
+            with open(path) as f:
+                lines = f.read().splitlines()
+        except OSError:
+            continue
+        for names, vals in zip(lines[::2], lines[1::2]):
+            if names.split(":")[0] not in ("Tcp", "TcpExt"):
+                continue
+            for k, v in zip(names.split()[1:], vals.split()[1:]):
+                if k in _TCP_KEYS:
+                    out[k] = int(v)
+    try:  # per-CPU network backlog: packets dropped (a full backlog) and softirq squeezes
+        with open("/proc/net/softnet_stat") as f:
+            rows = [ln.split() for ln in f if ln.strip()]
+        out["softnet_dropped"] = sum(int(r[1], 16) for r in rows)
+        out["softnet_squeezed"] = sum(int(r[2], 16) for r in rows)
+    except (OSError, ValueError, IndexError):
+        pass
+    return out
+
+
 def _rss_mb() -> float:
     try:
         with open("/proc/self/statm") as f:
@@ -370,7 +402,7 @@ def latency_phase(eng, broker, feeder, bset, parts, rate_img_s, a, ipr):
     time.sleep(a.latency_warmup_s)
     broker.take_probes()  # (reset)
     eng.set_ack_log(True)
-    c0, t0, cg0 = eng.completed, time.perf_counter(), _cgroup_cpu_stat()
+    c0, t0, cg0, tcp0 = eng.completed, time.perf_counter(), _cgroup_cpu_stat(), _tcp_counters()
     time.sleep(a.latency_s)
     eng.set_ack_log(False)
     dt = time.perf_counter() - t0
@@ -385,6 +417,8 @@ def latency_phase(eng, broker, feeder, bset, parts, rate_img_s, a, ipr):
                 "latency_cg_throttled_periods": int(d.get("nr_throttled", 0)),
                 "latency_cg_periods": int(d.get("nr_periods", 0))}
     host["latency_broker_probes"] = probes
+    tcp1 = _tcp_counters()
+    host["latency_tcp"] = {k: tcp1[k] - tcp0.get(k, 0) for k in tcp1 if tcp1[k] != tcp0.get(k, 0)}
     rf.stop()
     ack = eng.take_ack_log()
     app = rf.take_log()
@@ -628,7 +662,8 @@ def main(argv=None) -> int:
                                   "samples": int(len(lu)), "unmatched": unm,
                                   "stages_ms": hst.get("latency_stages_ms"),
                                   "cg_throttled_ms": hst.get("latency_cg_throttled_ms"),
-                                  "broker_probes": hst.get("latency_broker_probes")})
+                                  "broker_probes": hst.get("latency_broker_probes"),
+                                  "tcp": hst.get("latency_tcp")})
     if timeline:
         timeline.stop()
     if world > 1:

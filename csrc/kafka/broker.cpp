@@ -536,9 +536,15 @@ void Broker::serve(int fd) {
 namespace {
 constexpr size_t kSpliceMinBytes = 64 << 10;    // smaller stored slices are just written
 constexpr size_t kSpliceKeepBytes = 96ull << 20;
+constexpr size_t kWriteBurstBytes = 1 << 20;
 }  // namespace
 
-int Broker::splice_chunk(Conn& c, const Chunk& f) {
+// more: bytes of this connection's queue follow the chunk. SPLICE_F_MORE (MSG_MORE) lets TCP hold
+// a sub-MSS tail segment for the data that follows; on the LAST piece of a response nothing
+// follows, and a held tail is only released by a later ACK - with nothing else in flight that
+// stalls the fetch response for up to a TCP timer (the 100-200 ms latency tails of zero-copy
+// fetches), so the final piece is spliced without it.
+int Broker::splice_chunk(Conn& c, const Chunk& f, bool more) {
   if (c.pipe_wr < 0) {
     int fds[2];
     if (pipe2(fds, O_CLOEXEC) != 0) return 0;
@@ -560,8 +566,9 @@ int Broker::splice_chunk(Conn& c, const Chunk& f) {
     }
     first = false;
     size_t m = (size_t)n;
+    const unsigned fl = SPLICE_F_MOVE | (more || (size_t)n < left ? SPLICE_F_MORE : 0u);
     while (m) {
-      const ssize_t w = splice(c.pipe_rd, nullptr, c.fd, nullptr, m, SPLICE_F_MOVE | SPLICE_F_MORE);
+      const ssize_t w = splice(c.pipe_rd, nullptr, c.fd, nullptr, m, fl);
       if (w < 0) {
         if (errno == EINTR) continue;
         return -1;
@@ -587,7 +594,7 @@ bool Broker::flush(Conn& c) {
   while (!c.out.empty()) {
     Chunk& head = c.out.front();
     if (cfg_.zero_copy && c.splice_ok && head.shared && head.len >= kSpliceMinBytes) {
-      const int r = splice_chunk(c, head);
+      const int r = splice_chunk(c, head, c.out.size() > 1);
       if (r < 0) return false;
       if (r > 0) {
         std::lock_guard<std::mutex> lk(mu_);
@@ -598,13 +605,20 @@ bool Broker::flush(Conn& c) {
       }
       c.splice_ok = false;  // not supported here: plain writes from now on
     }
+    // at most kWriteBurstBytes per call (the splice path moves one pipe's worth, 1 MiB): the
+    // loopback device queues a sender's segments on its CPU's backlog (netdev_max_backlog
+    // packets), and a multi-MB burst overflows it whenever softirq work is deferred - every
+    // drop is a retransmission, a 10-200 ms latency tail (tools/gpu/r3_tail_tcp.sh)
     iovec iov[64];
     int n = 0;
-    for (auto it = c.out.begin(); it != c.out.end() && n < 64; ++it, ++n) {
+    size_t burst = 0;
+    for (auto it = c.out.begin(); it != c.out.end() && n < 64 && burst < kWriteBurstBytes;
+         ++it, ++n) {
       if (n > 0 && cfg_.zero_copy && c.splice_ok && it->shared && it->len >= kSpliceMinBytes)
         break;  // (the next piece goes zero-copy)
       iov[n].iov_base = const_cast<char*>(it->data());
-      iov[n].iov_len = it->len;
+      iov[n].iov_len = std::min(it->len, kWriteBurstBytes - burst);
+      burst += iov[n].iov_len;
     }
     const ssize_t w = writev(c.fd, iov, n);
     if (w < 0) {

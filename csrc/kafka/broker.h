@@ -137,7 +137,8 @@ class Broker {
   bool handle_request(Conn& c, const uint8_t* p, size_t n);
   bool try_fetch(Conn& c, bool final_attempt);
   bool flush(Conn& c);
-  int splice_chunk(Conn& c, const Chunk& f);  // 1 sent, 0 splice unusable, -1 connection error
+  // 1 sent, 0 splice unusable, -1 connection error
+  int splice_chunk(Conn& c, const Chunk& f, bool more);
   int64_t append_locked(PartitionLog& log, std::shared_ptr<const std::string> batch,
                         const BatchInfo& bi);
   PartitionLog* find_log(const std::string& topic, int partition);
