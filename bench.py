@@ -450,7 +450,8 @@ def main(argv=None) -> int:
     # profiles/r2_configs_1_4_e2e.txt)
     r50 = a.model == "resnet50"
     if a.step_images <= 0:
-        a.step_images = 4096 if r50 else 131072
+        # >= 1 s for 20 steps at each model's rate (LeNet-5 records run at > 4 M img/s)
+        a.step_images = 4096 if r50 else 262144 if a.model == "lenet5" else 131072
     if a.distinct <= 0:
         a.distinct = 256 if r50 else 65536
     if a.max_wait_us < 0:
