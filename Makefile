@@ -48,7 +48,7 @@ clean:
 # linked; GPU sanitizers are not available on this pool).
 SAN_SRC   := csrc/tests/engine_stress.cpp csrc/runtime/engine.cpp csrc/runtime/replica.cpp \
              csrc/runtime/pinned_pool.cpp csrc/runtime/trace.cpp csrc/codec/json_codec.cpp \
-             csrc/codec/text_pack.cpp \
+             csrc/codec/text_pack.cpp csrc/codec/java8_float.cpp \
              $(wildcard csrc/kafka/*.cpp)
 SAN_FLAGS := -O1 -g -fno-omit-frame-pointer -std=c++17 -D__HIP_PLATFORM_AMD__ -I$(ROCM)/include \
              -Icsrc/include -mavx2 -mfma -msse4.2 -mpclmul -mbmi2 -pthread

@@ -461,17 +461,22 @@ void bind_host(py::module_& m) {
     const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     return py::make_tuple(dt / std::max(1, iters), n);
   }, py::arg("data"), py::arg("iters") = 10, py::arg("force_scalar") = false);
+  m.def("format_float_java8", [](float v) {
+    char buf[48];
+    return std::string(buf, (size_t)codec::format_float_java8(v, buf));
+  });
   m.def("format_float_java", [](float v) {
     char buf[48];
     return std::string(buf, (size_t)codec::format_float_java(v, buf));
   });
   m.def("encode_predictions", [](py::array_t<float, py::array::c_style | py::array::forcecast> p,
-                                 bool json_string) {
+                                 bool json_string, bool java8) {
     if (p.ndim() != 2) throw std::invalid_argument("predictions must be [N, classes]");
     std::string out;
-    codec::encode_predictions(p.data(), (int)p.shape(0), (int)p.shape(1), json_string, out);
+    codec::encode_predictions(p.data(), (int)p.shape(0), (int)p.shape(1), json_string, out,
+                              java8);
     return py::bytes(out);
-  }, py::arg("probs"), py::arg("json_string") = false);
+  }, py::arg("probs"), py::arg("json_string") = false, py::arg("java8") = false);
   m.def("encode_predictions_text", [](py::bytes text16, int n, int classes, bool json_string) {
     const std::string t = text16;
     if (n < 0 || classes <= 0 || t.size() != (size_t)n * classes * 16)

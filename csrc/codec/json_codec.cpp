@@ -332,7 +332,7 @@ int format_float_java(float v, char* out) {
 }
 
 void encode_predictions(const float* probs, int n, int classes, bool json_string,
-                        std::string& out) {
+                        std::string& out, bool java8) {
   out.clear();
   out.reserve((size_t)n * classes * 14 + 32);
   const char* q = json_string ? "\\\"" : "\"";
@@ -348,7 +348,8 @@ void encode_predictions(const float* probs, int n, int classes, bool json_string
     out.push_back('[');
     for (int k = 0; k < classes; ++k) {
       if (k) out.push_back(',');
-      out.append(buf, format_float_java(probs[(size_t)i * classes + k], buf));
+      const float v = probs[(size_t)i * classes + k];
+      out.append(buf, java8 ? format_float_java8(v, buf) : format_float_java(v, buf));
     }
     out.push_back(']');
   }

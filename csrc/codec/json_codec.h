@@ -58,12 +58,17 @@ int parse_instances_host(const uint8_t* p, size_t n, int H, int W, int C, float*
 // Java Float.toString formatting (what Jackson emits for float[]): shortest digits
 // that round-trip, decimal for 1e-3 <= |v| < 1e7 ("0.125", "3.0"), else "1.0E-5". Returns length.
 int format_float_java(float v, char* out);
+// Java 8 Float.toString (FloatingDecimal's free-format digit loop, csrc/codec/java8_float.cpp):
+// the reference's runtime; it sometimes prints more digits than the shortest form. Parity with
+// a real Java 8 is unpinned (no JVM here).
+int format_float_java8(float v, char* out);
 
 // {"predictions":[[p00,p01,...],[p10,...]]} (Jackson compact). json_string=true wraps the
 // document in a JSON string literal, which is what spring-kafka's JsonSerializer does to the
 // already-serialized String value (MainTopology.java:115).
+// java8: Java 8 Float.toString digits (format_float_java8) instead of the JDK 19 rule
 void encode_predictions(const float* probs, int n, int classes, bool json_string,
-                        std::string& out);
+                        std::string& out, bool java8 = false);
 // Same output from pre-formatted values: text16 holds n * classes 16-byte slots (characters,
 // length in byte 15; format_floats_java in csrc/kernels/format.hip).
 void encode_predictions_text(const uint8_t* text16, int n, int classes, bool json_string,

@@ -1169,13 +1169,14 @@ void Engine::finish_batch(ReplicaSlot* rs, Batch& b) {
   rs->records += (int64_t)b.recs.size();
   kafka::Producer* prod = producer_for(rs->index);
   const bool js = cfg_.value_format == "json-string";
+  const bool java8 = cfg_.float_format == "java8";
   auto encode_ok = [&](const InRecord& r, int img, std::string& out) {
     if (b.pred_text)
       codec::encode_predictions_text(b.pred_text + (size_t)img * cfg_.classes * 16, r.images,
                                      cfg_.classes, js, out);
     else
       codec::encode_predictions(b.probs + (size_t)img * cfg_.classes, r.images, cfg_.classes, js,
-                                out);
+                                out, java8);
   };
   int img = 0;
   std::string out;

@@ -91,6 +91,9 @@ struct EngineConfig {
   int linger_ms = 0;
   int batch_size = 1 << 20;
   std::string value_format = "json";  // json | json-string (spring JsonSerializer, E8)
+  // prediction digits: "jdk19" (shortest, also on the GPU) | "java8" (the reference runtime's
+  // Float.toString, host-formatted; codec::format_float_java8)
+  std::string float_format = "jdk19";
   bool type_id_header = false;     // __TypeId__: java.lang.String header (E8)
   std::string on_error = "null";   // null | error-json | drop
   // output record key: "none" = unkeyed (the reference, E9: FieldNameBasedTupleToKafkaMapper

@@ -23,6 +23,7 @@ CHOICES = {
     "value_format": ("json", "json-string"),
     "on_error": ("null", "error-json", "drop"),
     "output_key": ("none", "input"),
+    "float_format": ("jdk19", "java8"),
     "assignor": ("range", "roundrobin", "load-aware"),
     # compute dtype of the GPU kernels (MFMA bf16 / OCP e4m3 fp8 serving plans; fp32 = the
     # reference-precision plan on the fp32 matrix core, every tensor binary32 like the
@@ -89,6 +90,9 @@ class GaleConfig:
     linger_ms: int = 0
     on_error: str = "null"             # reference: malformed input -> null record
     output_key: str = "none"           # reference: unkeyed output (E9); "input" = input's key
+    float_format: str = "jdk19"        # prediction digits: jdk19 = shortest round-trip (GPU
+                                       # formatted); java8 = the reference runtime's
+                                       # Float.toString (host formatted, csrc/codec/java8_float.cpp)
     producer_buffer_mb: int = 32       # unsent output bytes per sink producer before the sink
                                        # blocks (Kafka buffer.memory, 32 MB default)
     producer_request_kb: int = 1024    # bytes per produce request (Kafka max.request.size)
@@ -184,7 +188,7 @@ class GaleConfig:
             text_pack=bool(self.gpu_ingest and self.text_pack and _pack_fast()),
             acks=self.acks, sink_mode=self.sink_mode, linger_ms=self.linger_ms,
             value_format=self.value_format, type_id_header=self.type_id_header,
-            on_error=self.on_error, output_key=self.output_key,
+            on_error=self.on_error, output_key=self.output_key, float_format=self.float_format,
             output_partition=self.output_partition,
             producer_buffer_bytes=self.producer_buffer_mb << 20,
             producer_request_bytes=self.producer_request_kb << 10, H=H, W=W, C=C, classes=classes,

@@ -94,6 +94,45 @@ def test_format_float_java_roundtrips(v):
     assert np.float32(float(s)) == np.float32(v)
 
 
+# Java 8 Float.toString (the reference runtime, --float-format java8; csrc/codec/java8_float.cpp).
+# Pinned cases: values whose Java 8 text is widely documented - (float) 2^31 prints
+# "2.14748365E9" and Float.MIN_NORMAL "1.17549435E-38" on Java 8 (JDK 19+: "2.1474836E9",
+# "1.1754944E-38"); everything else is a property (no JVM here to pin more).
+@pytest.mark.parametrize("v,s", [
+    (0.0, "0.0"), (-0.0, "-0.0"), (1.0, "1.0"), (0.1, "0.1"), (0.5, "0.5"), (100.0, "100.0"),
+    (0.001, "0.001"), (0.0001, "1.0E-4"), (1e-5, "1.0E-5"), (1e7, "1.0E7"),
+    (123456.7, "123456.7"), (float("inf"), "Infinity"), (float("nan"), "NaN"),
+    (3.4028235e38, "3.4028235E38"), (1.4e-45, "1.4E-45"), (1 / 3, "0.33333334"),
+    (2.0 ** 31, "2.14748365E9"), (2.0 ** 30, "1.07374182E9"),
+    (1.1754943508222875e-38, "1.17549435E-38"),
+])
+def test_format_float_java8(v, s):
+    assert C.format_float_java8(v) == s
+
+
+def _sig(s):
+    return len(s.lstrip("-").split("E")[0].replace(".", "").strip("0"))
+
+
+@settings(max_examples=500, deadline=None)
+@given(st.floats(width=32, allow_nan=False, allow_infinity=False))
+def test_format_float_java8_roundtrips_and_is_never_shorter(v):
+    s8, s19 = C.format_float_java8(v), C.format_float_java(v)
+    assert np.float32(float(s8)) == np.float32(v)
+    assert _sig(s8) >= _sig(s19)
+
+
+def test_java8_and_jdk19_agree_on_probabilities():
+    """Softmax outputs (0, 1]: the two rules print the same text (200 k samples, incl. tiny)."""
+    rng = np.random.default_rng(3)
+    p = np.concatenate([rng.random(100_000), rng.random(100_000) ** 12]).astype(np.float32)
+    diff = [float(x) for x in p if C.format_float_java8(float(x)) != C.format_float_java(float(x))]
+    assert not diff, diff[:5]
+    big = np.float32(2.0 ** 31)
+    assert C.encode_predictions(np.array([[big]], np.float32), False, True) == \
+        b'{"predictions":[[2.14748365E9]]}'
+
+
 def test_encode_predictions_json_and_json_string():
     p = np.array([[0.5, 0.25, 1e-5], [0.1, 0.2, 0.7]], dtype=np.float32)
     out = C.encode_predictions(p, False)

@@ -97,6 +97,19 @@ def test_error_policies(broker, policy):
     assert eng.stats()["errors"] == 4
 
 
+def test_float_format_java8_output_text(broker):
+    """--float-format java8: the sink's prediction text is Java 8 Float.toString digits (the
+    reference runtime's; csrc/codec/java8_float.cpp), formatted on the host."""
+    imgs = produce_images(broker, [2, 1])
+    _, out = run(broker, 2, float_format="java8")
+    assert len(out) == 2
+    for r in out:
+        p = np.array(json.loads(r["value"])["predictions"], dtype=np.float32)
+        assert C.encode_predictions(p, False, True) == r["value"]  # the java8 digits, exactly
+    got = sorted(len(json.loads(r["value"])["predictions"]) for r in out)
+    assert got == sorted(len(x) for x in imgs)
+
+
 def test_json_string_value_and_type_header(broker):
     produce_images(broker, [2])
     _, out = run(broker, 1, value_format="json-string", type_id_header=True)
