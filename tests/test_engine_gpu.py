@@ -213,6 +213,21 @@ def test_gpu_engine_matches_oracle(broker, model, ingest):
         assert 0 < st["ingest_link_bytes"] < 0.6 * st["ingest_text_bytes"], st
 
 
+def test_gpu_engine_float_format_java8(broker):
+    """--float-format java8 with GPU replicas: the device formatter (JDK 19 rule) is bypassed and
+    the engine prints Java 8 Float.toString digits from the fp32 softmax rows."""
+    rng = np.random.default_rng(5)
+    n = 12
+    for i in range(n):
+        broker.append("in", 0, [C.encode_instances(rng.random((2, 32, 32, 3), dtype=np.float32))])
+    eng, out = run_engine(broker, n, float_format="java8")
+    assert len(out) == n and eng.stats()["errors"] == 0
+    for r in out:
+        p = np.array(json.loads(r["value"])["predictions"], dtype=np.float32)
+        assert p.shape == (2, 10)
+        assert C.encode_predictions(p, False, True) == r["value"]
+
+
 def test_gpu_crc32c_chunks_kernel():
     """The ingest CRC kernel: raw CRCs of arbitrary (misaligned, partial) windows, joined into
     standard CRC32Cs, equal the host's."""
