@@ -111,7 +111,6 @@ class Executor {
   std::map<std::pair<int, int>, hipGraphExec_t> graphs_;
   mutable std::mutex mu_;
   std::mutex capture_mu_;
-  hipStream_t capture_stream_ = nullptr;
 };
 
 void check_hip(hipError_t e, const char* what);

@@ -42,7 +42,6 @@ Executor::Executor(int device, PlanSpec spec) : device_(device), spec_(std::move
     ws_total += (bytes + 255) & ~size_t(255);
   }
   if (ws_total) check_hip(hipMalloc(&shared_ws_, ws_total), "hipMalloc(workspace)");
-  check_hip(hipStreamCreateWithFlags(&capture_stream_, hipStreamNonBlocking), "capture stream");
   bufs_.resize(spec_.slots);
   for (int s = 0; s < spec_.slots; ++s) {
     bufs_[s].assign(nb, nullptr);
@@ -65,7 +64,6 @@ Executor::~Executor() {
     }
   }
   if (shared_ws_) hipFree(shared_ws_);
-  if (capture_stream_) hipStreamDestroy(capture_stream_);
 }
 
 int Executor::bucket_for(int batch) const {
@@ -179,20 +177,29 @@ void Executor::run(int slot, int batch, hipStream_t stream, bool use_graph) {
     if (it != graphs_.end()) exec = it->second;
   }
   if (!exec) {
-    // capture on a private non-blocking stream (the legacy null stream cannot capture); the
-    // instantiated graph is then launched on the caller's stream
+    // capture on a private non-blocking stream (the legacy null stream cannot capture) that
+    // lives only for the capture: serving keeps one stream per replica and per ingest lane, so
+    // every stream can own a hardware queue (GPU_MAX_HW_QUEUES) - rocprofv3's queue
+    // interception crashed on queues shared by concurrently submitting threads. The
+    // instantiated graph is launched on the caller's stream.
     std::lock_guard<std::mutex> cap(capture_mu_);
+    hipStream_t cs = nullptr;
+    check_hip(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking), "capture stream");
     hipGraph_t graph = nullptr;
-    check_hip(hipStreamBeginCapture(capture_stream_, hipStreamCaptureModeThreadLocal),
-              "BeginCapture");
-    try {
-      launch_all(bucket, bufs_[slot].data(), capture_stream_);
-    } catch (...) {
-      hipStreamEndCapture(capture_stream_, &graph);
-      if (graph) hipGraphDestroy(graph);
-      throw;
+    hipError_t e = hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal);
+    if (e == hipSuccess) {
+      try {
+        launch_all(bucket, bufs_[slot].data(), cs);
+      } catch (...) {
+        hipStreamEndCapture(cs, &graph);
+        if (graph) hipGraphDestroy(graph);
+        hipStreamDestroy(cs);
+        throw;
+      }
+      e = hipStreamEndCapture(cs, &graph);
     }
-    check_hip(hipStreamEndCapture(capture_stream_, &graph), "EndCapture");
+    hipStreamDestroy(cs);
+    check_hip(e, "graph capture");
     check_hip(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0), "GraphInstantiate");
     hipGraphDestroy(graph);
     std::lock_guard<std::mutex> lk(mu_);

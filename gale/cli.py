@@ -102,7 +102,7 @@ def cmd_run(argv: List[str]) -> int:
         # crashed when several of the engine's streams shared a HW queue and submitted
         # concurrently (GPU_MAX_HW_QUEUES=4 default; profiles/r3_e2e_kernel_stats_default.csv)
         env = dict(os.environ)
-        env.setdefault("GPU_MAX_HW_QUEUES", "16")
+        env.setdefault("GPU_MAX_HW_QUEUES", "32")
         return subprocess.call(profile_command(cfg, argv), env=env)
     logging.basicConfig(level=getattr(logging, cfg.log_level.upper(), logging.INFO),
                         format="%(asctime)s %(name)s %(levelname)s %(message)s")

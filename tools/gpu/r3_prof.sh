@@ -5,7 +5,7 @@ set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 rm -rf gpurun_out/prof_def
-GPU_MAX_HW_QUEUES=16 timeout -k 10 240 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_def -o run -- \
+GPU_MAX_HW_QUEUES=32 timeout -k 10 240 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_def -o run -- \
   python3 bench.py --steps 10 --warmup 3 --latency-load 0 > gpurun_out/prof_def.log 2>&1
 rc=$?; echo "prof rc=$rc"; grep -A30 "gale crash" gpurun_out/prof_def.log | head -60
 tail -1 gpurun_out/prof_def.log | cut -c1-400
