@@ -113,6 +113,25 @@ struct ResNet20Params {
 hipError_t resnet20_fused_forward(const ResNet20Params& p, int batch, const float* x, float* out,
                                   hipStream_t stream);
 
+// Whole-network MNIST LeNet-5 (csrc/kernels/lenet5_fused.hip): x fp32 [B,28,28,1] -> softmax
+// fp32 [B,10], four images per workgroup with every activation in LDS. Weights are the serving
+// plan's packed bf16 matrices: conv1 [16][32], conv2 [16][224], fc1 [128][416], fc2 [128][128]
+// (fp32 biases of Npad entries), fc3 fp32 [10][88] + [10].
+struct LeNet5Params {
+  const void* w1;
+  const float* b1;
+  const void* w2;
+  const float* b2;
+  const void* w3;
+  const float* b3;
+  const void* w4;
+  const float* b4;
+  const float* w5;
+  const float* b5;
+};
+hipError_t lenet5_fused_forward(const LeNet5Params& p, int batch, const float* x, float* out,
+                                hipStream_t stream);
+
 // Row softmax, fp32 [B, ld] -> fp32 [B, N] (first N columns of each row).
 hipError_t softmax_rows(int batch, int N, int ld, const float* x, float* out, hipStream_t stream);
 

@@ -146,6 +146,23 @@ void Executor::launch_ops(size_t begin, size_t end, int batch, void* const* bufs
                                    static_cast<float*>(out), stream);
         break;
       }
+      case OP_LENET5: {
+        if (op.ptrs.size() != 10u) throw std::invalid_argument("lenet5 op: bad pointer count");
+        LeNet5Params lp{};
+        lp.w1 = op.ptrs[0];
+        lp.b1 = static_cast<const float*>(op.ptrs[1]);
+        lp.w2 = op.ptrs[2];
+        lp.b2 = static_cast<const float*>(op.ptrs[3]);
+        lp.w3 = op.ptrs[4];
+        lp.b3 = static_cast<const float*>(op.ptrs[5]);
+        lp.w4 = op.ptrs[6];
+        lp.b4 = static_cast<const float*>(op.ptrs[7]);
+        lp.w5 = static_cast<const float*>(op.ptrs[8]);
+        lp.b5 = static_cast<const float*>(op.ptrs[9]);
+        e = lenet5_fused_forward(lp, batch, static_cast<const float*>(in),
+                                 static_cast<float*>(out), stream);
+        break;
+      }
       default:
         throw std::invalid_argument("unknown plan op kind");
     }

@@ -391,7 +391,8 @@ def act_scales_from_packed(net: Network, packed: torch.Tensor) -> Dict[str, floa
 # executor plan
 # --------------------------------------------------------------------------------------------
 
-OP_CONV, OP_MAXPOOL, OP_AVGPOOL, OP_HEAD, OP_SOFTMAX, OP_RESNET20, OP_STEM_PACK, OP_BN_ACT = range(8)
+(OP_CONV, OP_MAXPOOL, OP_AVGPOOL, OP_HEAD, OP_SOFTMAX, OP_RESNET20, OP_STEM_PACK, OP_BN_ACT,
+ OP_LENET5) = range(9)
 
 
 def is_cifar_resnet20(net: Network) -> bool:
@@ -401,6 +402,25 @@ def is_cifar_resnet20(net: Network) -> bool:
     ref = resnet20()
     return (net.input_shape == ref.input_shape and net.classes == ref.classes
             and [repr(L) for L in net.layers] == [repr(L) for L in ref.layers])
+
+
+def is_mnist_lenet5(net: Network) -> bool:
+    """True for the exact architecture the fused LeNet-5 kernel implements."""
+    from gale.models.zoo import lenet5
+
+    ref = lenet5()
+    return (net.input_shape == ref.input_shape and net.classes == ref.classes
+            and [repr(L) for L in net.layers] == [repr(L) for L in ref.layers])
+
+
+def _fused_lenet5_plan(net: Network, base_ptr: int) -> Tuple[List[dict], List[int]]:
+    layout, _ = param_layout(net, "bf16")
+    names = ("conv1", "conv2", "fc1", "fc2", "fc3")
+    ptrs = []
+    for nm in names:
+        ptrs += [base_ptr + layout[f"{nm}.w"].offset, base_ptr + layout[f"{nm}.b"].offset]
+    op = dict(kind=OP_LENET5, **{"in": 0}, out=1, ptrs=ptrs)
+    return [op], [_tensor_bytes(net, "input"), net.classes * 4]
 
 
 def _fused_resnet20_plan(net: Network, base_ptr: int, wdtype: str = "bf16",
@@ -436,8 +456,8 @@ def build_plan(net: Network, base_ptr: int, wdtype: str = "bf16",
     Returns (ops, buf_bytes_per_image). Buffer 0 = fp32 input, 1 = fp32 softmax output, >= 2 =
     bf16 (fp8: e4m3) activations assigned by liveness so concurrently-live tensors never share a
     buffer. ``act_scales`` (fp8 only): per-tensor scales, see ``act_scales_from_packed``.
-    ``fused``: the CIFAR ResNet-20 (bf16 or fp8) becomes ONE whole-network kernel (activations
-    resident in LDS). ``fold_bn=False`` (bf16, layer-wise; the buffer from ``pack_params(...,
+    ``fused``: the CIFAR ResNet-20 (bf16 or fp8) and the MNIST LeNet-5 (bf16 weights, fp32
+    math) become ONE whole-network kernel each (activations resident in LDS). ``fold_bn=False`` (bf16, layer-wise; the buffer from ``pack_params(...,
     fold_bn=False)``): every BatchNorm conv is followed by a standalone ``bn_act`` kernel that
     applies the BN affine, the residual and the ReLU in place (the debugging / parity plan).
     ``chunk_layers``: the first ``chunk_layers`` layers may run per batch chunk (the executor's
@@ -452,6 +472,8 @@ def build_plan(net: Network, base_ptr: int, wdtype: str = "bf16",
         raise ValueError("build_plan: the fp8 plan needs the activation scales")
     if fused and fold_bn and is_cifar_resnet20(net) and not f32:
         return _fused_resnet20_plan(net, base_ptr, wdtype, act_scales)
+    if fused and is_mnist_lenet5(net) and wdtype == "bf16":
+        return _fused_lenet5_plan(net, base_ptr)
     layout, _ = param_layout(net, wdtype, fold_bn)
     # liveness: last layer index reading each tensor
     last_use: Dict[str, int] = {}

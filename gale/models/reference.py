@@ -29,7 +29,7 @@ def forward(net: Network, params: Dict[str, torch.Tensor], x_nhwc: torch.Tensor,
             collect: Dict[str, torch.Tensor] | None = None,
             tensors: Dict[str, torch.Tensor] | None = None,
             fp8_scales: Dict[str, float] | None = None,
-            bf16: bool = False) -> torch.Tensor:
+            bf16: bool = False, bf16_acts: bool = True) -> torch.Tensor:
     """fp32 forward. ``folded``: params come from ``fold_params`` (conv bias already has BN).
 
     With ``folded=False`` BatchNorm is applied from its running statistics (or, when ``bn_stats``
@@ -38,7 +38,9 @@ def forward(net: Network, params: Dict[str, torch.Tensor], x_nhwc: torch.Tensor,
     kernel path: e4m3 per-channel weights and every activation rounded to e4m3 at its scale.
     ``bf16`` emulates the bf16 kernel path: conv weights and the network input rounded to bf16,
     every stored activation rounded to bf16 (fp32 accumulation, fp32 bias and head), so the
-    kernels can be held to accumulation-order differences against it.
+    kernels can be held to accumulation-order differences against it. ``bf16_acts=False``
+    rounds only the conv weights (the fused LeNet-5 kernel: bf16 weights, fp32 input and
+    activations).
     """
     if fp8_scales is not None:
         from gale.models.quant import e4m3_round, fake_quant_weight
@@ -47,6 +49,9 @@ def forward(net: Network, params: Dict[str, torch.Tensor], x_nhwc: torch.Tensor,
             s = fp8_scales[name]
             return e4m3_round(v / s) * s
     def rb(v):  # round to bf16 and back
+        return v.to(torch.bfloat16).float() if bf16 and bf16_acts else v
+
+    def rw(v):
         return v.to(torch.bfloat16).float() if bf16 else v
 
     x0 = x_nhwc.float().permute(0, 3, 1, 2)
@@ -58,7 +63,7 @@ def forward(net: Network, params: Dict[str, torch.Tensor], x_nhwc: torch.Tensor,
             w = params[f"{L.name}.weight"]
             if fp8_scales is not None:
                 w = fake_quant_weight(w)
-            w = rb(w)
+            w = rw(w)
             b = params.get(f"{L.name}.bias")
             y = F.conv2d(t[L.inp], w, b, stride=L.stride, padding=L.pad)
             if not folded and L.bn:

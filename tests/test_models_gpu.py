@@ -43,7 +43,8 @@ def test_model_matches_reference(name, batch):
     eager = rep.infer_eager(x).cpu()
     graph = rep.infer(x, use_graph=True, slot=1).cpu()
     torch.cuda.synchronize()
-    emu = forward(net, fold_params(net, params), x, bf16=True)
+    # (the fused LeNet-5 keeps its activations in fp32: only its weights are bf16)
+    emu = forward(net, fold_params(net, params), x, bf16=True, bf16_acts=name != "lenet5")
     assert eager.shape == ref.shape
     err = rel_logit_err(eager, ref).max().item()
     e_emu = rel_logit_err(eager, emu).max().item()
@@ -149,6 +150,37 @@ def test_fp8_model_matches_emulation_and_fp32(name, batch):
     if clear.any():  # (1000-class random-init resnet50 has no clear winner)
         agree = (got.argmax(1)[clear] == ref.argmax(1)[clear]).float().mean().item()
         assert agree >= 0.97, f"{name}: fp8 argmax agreement {agree}"
+
+
+@pytest.mark.parametrize("batch", [1, 13, 257, 1000])
+def test_lenet5_fused_matches_layerwise_and_fp32(batch):
+    """The whole-network LeNet-5 kernel (one image per workgroup, fp32 activations in LDS, bf16
+    weights) against the layer-by-layer bf16 plan on the same packed weights, the weight-only
+    bf16 emulation (tight: same operands, fp32 everywhere else) and the fp32 oracle, at batches
+    across graph buckets."""
+    net = get_model("lenet5")
+    params = init_params(net, seed=19)
+    packed = materialize_weights(net, torch.device("cuda", 0), params=params)
+    fused = ModelReplica(net, packed, max_batch=1024, slots=1, fused=True)
+    layered = ModelReplica(net, packed, max_batch=1024, slots=1, fused=False)
+    assert len(fused.ops) == 1 and len(layered.ops) > 1
+    x = torch.rand((batch, 28, 28, 1), generator=torch.Generator().manual_seed(batch))
+    a = fused.infer(x, use_graph=True).cpu()
+    b = layered.infer(x, use_graph=True).cpu()
+    folded = fold_params(net, params)
+    ref = forward(net, folded, x)
+    emu_w = forward(net, folded, x, bf16=True, bf16_acts=False)
+    emu = forward(net, folded, x, bf16=True)
+    torch.cuda.synchronize()
+    e_w = rel_logit_err(a, emu_w).max().item()
+    e_ab, e_ref = rel_logit_err(a, b).max().item(), rel_logit_err(a, ref).max().item()
+    budget = rel_logit_err(emu, ref).max().item()
+    print(f"\nlenet5 fused vs weight-bf16 emulation {e_w:.2e}, vs layered {e_ab:.2e}, vs fp32 "
+          f"{e_ref:.2e} (bf16 budget {budget:.2e})")
+    assert e_w < 1e-4  # fp32 math on the same bf16 weights: summation order only
+    assert e_ab < 1.5 * budget + 5e-3 and e_ref < 1.5 * budget + 5e-3
+    assert torch.allclose(a.sum(1), torch.ones(batch), atol=1e-5)
+    assert torch.equal(fused.infer_eager(x).cpu(), a)
 
 
 @pytest.mark.parametrize("batch", [1, 37, 600])
