@@ -1,9 +1,9 @@
 #!/bin/bash
-# GPU box: config 1 (LeNet-5) end to end, sink producers 2 vs 4, alternating
+# GPU box: config 1 (LeNet-5) end to end A/B over sink settings (default: producer buffer 32 vs 8 MB)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out
-for args in "--sink-parallelism 2" "--sink-parallelism 4" "--sink-parallelism 2" "--sink-parallelism 4"; do
+for args in ${LENET_ARGS:-"--producer-buffer-mb 32" "--producer-buffer-mb 8"}; do
   timeout -k 10 240 python bench.py --model lenet5 $args > gpurun_out/lenet_sink.log 2>&1 || { tail -20 gpurun_out/lenet_sink.log; exit 1; }
   python3 - "$args" <<'PY' | tee -a gpurun_out/lenet_sink.jsonl
 import json, sys
