@@ -153,6 +153,9 @@ def parse_args(argv=None):
     ap.add_argument("--latency-warmup-s", type=float, default=1.0)
     ap.add_argument("--fetch-min-bytes", type=int, default=1,
                     help="consumer fetch.min.bytes (Kafka default 1)")
+    ap.add_argument("--recv-lowat-kb", type=int, default=0,
+                    help="consumer receive low-water mark per receive call (SO_RCVLOWAT): one "
+                         "wake-up per this many KB of a fetch response; 0 = per segment")
     ap.add_argument("--fetch-max-wait-ms", type=int, default=20,
                     help="consumer fetch.max.wait.ms (long-poll bound when no data is there)")
     ap.add_argument("--latency-sweep", default="",
@@ -571,7 +574,7 @@ def main(argv=None) -> int:
                      output_partition=rank if a.local_output and world > 1 else -1,
                      producer_buffer_mb=a.producer_buffer_mb,
                      locality_split=a.locality_split, fetch_min_bytes=a.fetch_min_bytes,
-                     fetch_max_wait_ms=a.fetch_max_wait_ms,
+                     fetch_max_wait_ms=a.fetch_max_wait_ms, recv_lowat_kb=a.recv_lowat_kb,
                      use_graph=a.graph,
                      producer_request_kb=a.producer_request_kb)
     devices = (list(range(local_gpus)) if local_gpus > 1 else [local_rank]) if use_gpu else None

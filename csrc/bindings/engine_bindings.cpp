@@ -40,6 +40,7 @@ EngineConfig config_from_dict(const py::dict& d) {
   opt(d, "pinned_fetch_bytes", c.pinned_fetch_bytes);
   opt(d, "text_pack", c.text_pack);
   opt(d, "float_format", c.float_format);
+  opt(d, "recv_lowat", c.recv_lowat);
   opt(d, "commit_interval_ms", c.commit_interval_ms);
   opt(d, "group_membership", c.group_membership);
   opt(d, "session_timeout_ms", c.session_timeout_ms);

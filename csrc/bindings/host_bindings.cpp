@@ -818,8 +818,10 @@ void bind_host(py::module_& m) {
   py::class_<Consumer, std::shared_ptr<Consumer>>(k, "Consumer")
       .def(py::init([](const std::string& bootstrap, const std::string& group_id, int max_wait_ms,
                        int fetch_max_bytes, int partition_max_bytes, bool check_crcs,
-                       const std::string& auto_offset_reset, const std::string& client_id) {
+                       const std::string& auto_offset_reset, const std::string& client_id,
+                       int recv_lowat) {
              ConsumerConfig c;
+             c.recv_lowat = recv_lowat;
              c.bootstrap = bootstrap;
              c.group_id = group_id;
              c.max_wait_ms = max_wait_ms;
@@ -833,7 +835,7 @@ void bind_host(py::module_& m) {
            py::arg("bootstrap"), py::arg("group_id") = "", py::arg("max_wait_ms") = 100,
            py::arg("fetch_max_bytes") = 64 << 20, py::arg("partition_max_bytes") = 16 << 20,
            py::arg("check_crcs") = true, py::arg("auto_offset_reset") = "latest",
-           py::arg("client_id") = "gale-consumer")
+           py::arg("client_id") = "gale-consumer", py::arg("recv_lowat") = 0)
       .def("assign", [](Consumer& c, const std::string& topic, std::vector<int> parts) {
         py::gil_scoped_release nogil;
         c.assign(topic, parts);

@@ -63,7 +63,9 @@ std::shared_ptr<uint8_t> heap_alloc(size_t bytes) {
 // ---------------------------------------------------------------------------------------------
 
 Connection::Connection(const std::string& host, int port, const ClientConfig& cfg)
-    : host_(host), port_(port), client_id_(cfg.client_id) {
+    : lowat_cap_(std::max(0, cfg.recv_lowat)), timeout_ms_(cfg.request_timeout_ms), host_(host),
+      port_(port),
+      client_id_(cfg.client_id) {
   addrinfo hints{}, *res = nullptr;
   hints.ai_family = AF_INET;
   hints.ai_socktype = SOCK_STREAM;
@@ -120,10 +122,26 @@ void Connection::recv_all(uint8_t* p, size_t n, RecvTap* tap) {
   const uint8_t* base = p;
   const size_t cap = tap ? std::max<size_t>(4096, tap->chunk_bytes()) : n;
   while (n) {
-    const ssize_t r = ::recv(fd_, p, std::min(n, cap), 0);
+    const size_t want = std::min(n, cap);
+    int flags = 0;
+    if (lowat_cap_ > 0) {
+      const int lw = (int)std::min<size_t>(want, (size_t)lowat_cap_);
+      if (lw != lowat_cur_ && setsockopt(fd_, SOL_SOCKET, SO_RCVLOWAT, &lw, sizeof(lw)) == 0)
+        lowat_cur_ = lw;
+      pollfd pf{fd_, POLLIN, 0};
+      const int pr = ::poll(&pf, 1, timeout_ms_);
+      if (pr == 0) throw KafkaError(REQUEST_TIMED_OUT, "request timed out on " + host_);
+      if (pr < 0) {
+        if (errno == EINTR) continue;
+        throw KafkaError(-1, std::string("poll failed: ") + strerror(errno));
+      }
+      flags = MSG_DONTWAIT;
+    }
+    const ssize_t r = ::recv(fd_, p, want, flags);
     if (r == 0) throw KafkaError(-1, "connection closed by broker " + host_);
     if (r < 0) {
       if (errno == EINTR) continue;
+      if (flags && (errno == EAGAIN || errno == EWOULDBLOCK)) continue;  // (raced the mark)
       if (errno == EAGAIN || errno == EWOULDBLOCK)
         throw KafkaError(REQUEST_TIMED_OUT, "request timed out on " + host_);
       throw KafkaError(-1, std::string("recv failed: ") + strerror(errno));

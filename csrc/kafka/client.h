@@ -41,6 +41,12 @@ struct ClientConfig {
   std::string client_id = "gale";
   int request_timeout_ms = 30000;
   int connect_timeout_ms = 10000;
+  // > 0: each receive waits (poll) until min(this, bytes still wanted) bytes are queued
+  // (SO_RCVLOWAT, set per call so the last piece of a response never waits for more), then
+  // takes them without blocking: one wake-up per ~this many bytes of a large response instead of
+  // one per arriving segment. (A blocking recv cannot be used with it: after a partial copy the
+  // kernel compares only the still-unread bytes with the mark, and the reader sleeps on.)
+  int recv_lowat = 0;
 };
 
 // Response buffers: the body of a response frame (after the 4-byte size) is received into
@@ -81,6 +87,7 @@ class Connection {
   void send_all(const char* p, size_t n);
   void recv_all(uint8_t* p, size_t n, RecvTap* tap = nullptr);
   int fd_ = -1;
+  int lowat_cap_ = 0, lowat_cur_ = 1, timeout_ms_ = 30000;
   std::string host_;
   int port_;
   int32_t next_corr_ = 1;

@@ -607,6 +607,7 @@ void Engine::source_loop(int idx) {
   cc.min_bytes = std::max(1, cfg_.fetch_min_bytes);
   cc.fetch_max_bytes = cfg_.fetch_max_bytes;
   cc.partition_max_bytes = cfg_.partition_max_bytes;
+  cc.recv_lowat = cfg_.recv_lowat;
   // with decode workers the CRC32C check moves off this thread (decode_fetch)
   cc.check_crcs = cfg_.check_crcs && cfg_.decode_threads <= 0;
   cc.auto_offset_reset = cfg_.start_offset == "earliest" ? "earliest" : "latest";

@@ -66,6 +66,8 @@ struct EngineConfig {
   // GPU ingest: sources nibble-pack fetch bodies while receiving them (pack_tap.h) and the text
   // crosses the host link packed (csrc/codec/text_pack.h)
   bool text_pack = false;
+  // consumers' receive low-water mark (kafka::ClientConfig::recv_lowat), bytes; 0 = off
+  int recv_lowat = 0;
   int commit_interval_ms = 2000;   // storm-kafka's ZK commit period
   // consumer-group membership (elastic DP, kafka::GroupMember): the input partitions are shared
   // by every engine of group_id; a member that dies or leaves has its partitions moved to the

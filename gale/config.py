@@ -49,6 +49,8 @@ class GaleConfig:
     commit_interval_ms: int = 2000
     fetch_min_bytes: int = 1           # Kafka fetch.min.bytes of the consumers (long-poll size)
     fetch_max_wait_ms: int = 20        # Kafka fetch.max.wait.ms
+    recv_lowat_kb: int = 0             # consumers wake per this many KB of a large fetch
+                                       # response (SO_RCVLOWAT per receive call); 0 = per segment
     # elastic data parallelism: every process of the group shares the input partitions through
     # Kafka consumer-group membership; dead members' partitions move to the survivors
     group_membership: bool = False
@@ -179,6 +181,7 @@ class GaleConfig:
             source_parallelism=self.source_parallelism, start_offset=self.start_offset,
             commit_interval_ms=self.commit_interval_ms, sink_parallelism=self.sink_parallelism,
             fetch_min_bytes=self.fetch_min_bytes, fetch_max_wait_ms=self.fetch_max_wait_ms,
+            recv_lowat=self.recv_lowat_kb << 10,
             group_membership=self.group_membership, session_timeout_ms=self.session_timeout_ms,
             rebalance_timeout_ms=self.rebalance_timeout_ms,
             heartbeat_interval_ms=self.heartbeat_interval_ms, assignor=self.assignor,

@@ -5,6 +5,7 @@ input, InferenceBolt.java:70-99) and the new capabilities (micro-batching, error
 fault injection, offset commits / resume)."""
 
 import json
+import time
 
 import numpy as np
 import pytest
@@ -108,6 +109,18 @@ def test_float_format_java8_output_text(broker):
         assert C.encode_predictions(p, False, True) == r["value"]  # the java8 digits, exactly
     got = sorted(len(json.loads(r["value"])["predictions"]) for r in out)
     assert got == sorted(len(x) for x in imgs)
+
+
+@pytest.mark.parametrize("lowat_kb", [1, 1024])
+def test_recv_lowat_never_waits_past_a_response(broker, lowat_kb):
+    """SO_RCVLOWAT is set per receive call to min(cap, bytes still wanted): responses smaller
+    than the low-water mark, and the tails of larger ones, complete without waiting."""
+    counts = [1, 2, 1, 3] * 4
+    produce_images(broker, counts)
+    t0 = time.perf_counter()
+    eng, out = run(broker, len(counts), recv_lowat_kb=lowat_kb)
+    assert len(out) == len(counts) and eng.stats()["errors"] == 0
+    assert time.perf_counter() - t0 < 20
 
 
 def test_json_string_value_and_type_header(broker):
