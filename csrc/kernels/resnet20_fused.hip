@@ -52,12 +52,18 @@ struct Lay {
 //     elements (109 slots): 0 extra cycles for stage 2 and for conv 13's stride-2 reads
 //     (dense 64-B pixels: 4 and 12 extra LDS cycles per read);
 //   stage 3 pads each 64-channel pixel to 80 elements (ten slots) and each row to 896 (dense: 12).
-// The fp8 images stay dense (ds_read_b64 B fragments).
+// fp8 uses the same element counts, i.e. half the bytes: its B fragments are ds_read_b64s whose
+// 32-lane halves (lane groups g = 0,1 and 2,3 x 16 pixels) read a 16-B window per pixel, and
+// pixel strides of 48 / 80 B (3 / 5 x 16 B, odd) put the 16 windows of a row on 16 distinct 16-B
+// positions of the 256-B bank row; the row strides (872 B = 109 x 8 B: two rows for conv 13's
+// stride-2 reads land on the other half of the positions; 896 B = 128 mod 256: stage 3's second
+// tile row) keep multi-row tiles disjoint too. (Dense fp8 pixels of 32 / 64 B: 2- and 4-way, 14
+// extra LDS cycles per LDS instruction measured, profiles/r3_resnet20_fp8_lds.txt.)
 template <bool F8>
 struct Layouts {
-  typedef Lay<16, 34 * 16> S1;                        // 34x34x16
-  typedef Lay<F8 ? 32 : 48, F8 ? 18 * 32 : 872> S2;   // 18x18x32
-  typedef Lay<F8 ? 64 : 80, F8 ? 10 * 64 : 896> S3;   // 10x10x64
+  typedef Lay<16, 34 * 16> S1;  // 34x34x16
+  typedef Lay<48, 872> S2;      // 18x18x32
+  typedef Lay<80, 896> S3;      // 10x10x64
   typedef Lay<16, 16 * 16> SC;                        // 16x16x16 shortcut, no border
 };
 
@@ -221,10 +227,13 @@ __device__ __forceinline__ uint2 quad_transpose(uint2 w) {
   return w;
 }
 
-// zero the one-pixel border of a padded Hp x Wp x C image in layout L (C * EB % 16 == 0)
+// zero the one-pixel border of a padded Hp x Wp x C image in layout L (C * EB % 16 == 0); 8-B
+// vectors when a row or pixel stride is not a multiple of 16 B (fp8 stage 2: 872-B rows)
 template <bool F8, int NW, int HP, int WP, int C, class L>
 __device__ __forceinline__ void zero_border(typename Ty<F8>::elem* buf) {
-  constexpr int V = C * Ty<F8>::EB / 16;  // 16-byte vectors per cell
+  constexpr int EB = Ty<F8>::EB;
+  constexpr int VB = (L::RP * EB) % 16 == 0 && (L::PS * EB) % 16 == 0 ? 16 : 8;
+  constexpr int V = C * EB / VB;  // vectors per cell
   constexpr int CELLS = 2 * WP + 2 * (HP - 2);
   for (int i = threadIdx.x; i < CELLS * V; i += 64 * NW) {
     const int cell = i / V, v = i - cell * V;
@@ -232,8 +241,11 @@ __device__ __forceinline__ void zero_border(typename Ty<F8>::elem* buf) {
     if (cell < WP) { h = 0; w = cell; }
     else if (cell < 2 * WP) { h = HP - 1; w = cell - WP; }
     else { const int r = cell - 2 * WP; h = 1 + (r >> 1); w = (r & 1) ? WP - 1 : 0; }
-    *reinterpret_cast<uint4*>(reinterpret_cast<char*>(buf + h * L::RP + w * L::PS) + v * 16) =
-        make_uint4(0, 0, 0, 0);
+    char* dst = reinterpret_cast<char*>(buf + h * L::RP + w * L::PS) + v * VB;
+    if constexpr (VB == 16)
+      *reinterpret_cast<uint4*>(dst) = make_uint4(0, 0, 0, 0);
+    else
+      *reinterpret_cast<uint2*>(dst) = make_uint2(0, 0);
   }
 }
 
@@ -599,7 +611,9 @@ hipError_t resnet20_fused_forward(const ResNet20Params& p, int batch, const floa
   // of LDS would allow 4, but the hoisted A fragments need more than 128 VGPRs per lane), or 1 of
   // 8 waves. bf16 with no more images than CUs: the 8-wave form (each image gets twice the
   // waves, weights prefetched into LDS; measured 62.3 -> 58.0 us at batch 1,
-  // profiles/r1_resnet20_waves_ab.txt). fp8 stays on 4 waves (its 8-wave form measured slower).
+  // profiles/r1_resnet20_waves_ab.txt). fp8 stays on 4 waves (its 8-wave form measured slower in
+  // round 1 and equal after the round-3 LDS layout fix: 50.9 / 53.1 vs 50.7 / 52.7 us at batch
+  // 64 / 256, profiles/r3_resnet20_fp8_lds.txt).
   const int nw = !f8 && batch <= cus ? 8 : 4;
   const int grid_cap = nw == 8 ? cus : 2 * cus;
   const int grid = batch < grid_cap ? batch : grid_cap;
