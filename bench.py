@@ -22,10 +22,10 @@ What one rank (= one GPU, launched by torch.distributed.run for N > 1) does:
 
 Steady state: warm-up is W steps AND at least ``--min-warmup-s`` seconds AND until the last
 four 500 ms rate windows (2 s) all lie within 5 % of their mean (capped at ``--max-warmup-s``). A step is
-``--step-images`` images per GPU (default 131072: 512 micro-batches of 256) completing the whole
-path (acknowledged by the broker), so the default K = 20 steps is a >= 1 s window on one
-MI355X (1.7 s at 1.5 M img/s; 65536-image steps fell to 0.86 s once the pipeline passed
-1.5 M img/s). The K timed steps are bracketed by a barrier + ``torch.cuda.synchronize()``; ``value``
+``--step-images`` images per GPU (default 262144: 1024 micro-batches of 256) completing the whole
+path (acknowledged by the broker), so the default K = 20 steps is a ~3.5 s window on one
+MI355X at 1.5 M img/s (65536-image steps fell below 1 s once the pipeline passed 1.5 M img/s;
+131072-image steps let single host hiccups swing a step's rate by 10-20 %). The K timed steps are bracketed by a barrier + ``torch.cuda.synchronize()``; ``value``
 is the whole-job images/s (sum over ranks of the images completed in the window / the slowest
 rank's window). The per-step rates give the within-run spread.
 """
@@ -55,7 +55,7 @@ def parse_args(argv=None):
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--step-images", type=int, default=0,
                     help="images per GPU per step (the unit of --steps / --warmup); default "
-                         "131072 (4096 for resnet50)")
+                         "262144 (4096 for resnet50)")
     ap.add_argument("--min-warmup-s", type=float, default=2.0)
     ap.add_argument("--max-warmup-s", type=float, default=20.0)
     ap.add_argument("--model", default="resnet20", choices=["lenet5", "resnet20", "resnet50"])
@@ -453,8 +453,11 @@ def main(argv=None) -> int:
     # profiles/r2_configs_1_4_e2e.txt)
     r50 = a.model == "resnet50"
     if a.step_images <= 0:
-        # >= 1 s for 20 steps at each model's rate (LeNet-5 records run at > 4 M img/s)
-        a.step_images = 4096 if r50 else 262144 if a.model == "lenet5" else 131072
+        # 262144-image steps: ~0.18 s each at 1.5 M img/s (20 steps ~3.6 s), long enough that a
+        # single 10-50 ms host hiccup (scheduler, page-cache, neighbour tenants) moves a step's
+        # rate by a few percent rather than 10-20 % (131072-image steps: spread 9-20 %,
+        # profiles/r3_final_check_session2.jsonl); LeNet-5 runs at > 4 M img/s
+        a.step_images = 4096 if r50 else 262144
     if a.distinct <= 0:
         a.distinct = 256 if r50 else 65536
     if a.max_wait_us < 0:
