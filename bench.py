@@ -475,7 +475,10 @@ def main(argv=None) -> int:
         else:
             a.partitions = 2 * a.replicas_per_gpu if big else a.replicas_per_gpu
     if a.decode_threads <= 0:
-        a.decode_threads = 4 if big else 2
+        # 6 GPU-ingest workers keep more H2D copies in flight on the host link than 4 (higher
+        # throughput in 5 of 6 interleaved pairs on two boxes, p50 unchanged; see
+        # profiles/r3_decode_threads_ab.txt)
+        a.decode_threads = 6 if big else 2
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
