@@ -46,6 +46,11 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "images/sec (whole node) + p50 latency, CIFAR-10 ResNet-20 at 1/2/4/8 GPUs"
+# the headline metric is BASELINE.json's (ResNet-20); the other BASELINE configs report the same
+# quantity under their own model's name
+METRICS = {"resnet20": METRIC,
+           "lenet5": "images/sec (whole node) + p50 latency, MNIST LeNet-5",
+           "resnet50": "images/sec (whole node) + p50 latency, ImageNet ResNet-50"}
 
 
 def parse_args(argv=None):
@@ -438,8 +443,74 @@ def latency_phase(eng, broker, feeder, bset, parts, rate_img_s, a, ipr):
     return lat, achieved, int(len(ack[0]) - len(lat)), host
 
 
+def pipeline_path(a, st) -> str:
+    """What the timed window actually ran, from the engine's own counters (not the flags)."""
+    if a.stub:
+        return "kafka-fetch->host-scan->cpu-stub-replica->kafka-produce"
+    hops = ["kafka-fetch"]
+    if st.get("ingested_records", 0) > 0:
+        hops.append("gpu-ingest(crc32c+count%s)" % (",nibble-link" if a.text_pack else ""))
+    else:
+        hops.append("host-scan+crc32c")
+    batches = max(1.0, st.get("batches", 0))
+    step_g = st.get("graph_step_batches", 0) / batches
+    fwd_g = st.get("graph_forward_batches", 0) / batches
+    if step_g > 0.5:
+        hops.append("hipgraph-step(json-parse+forward%s+status)" %
+                    ("+format" if a.gpu_encode else ""))
+    else:
+        hops.append("gpu-json-parse")
+        hops.append("hipgraph-forward" if fwd_g > 0.5 else "forward(direct-launch)")
+        if a.gpu_encode:
+            hops.append("gpu-format")
+    hops.append("kafka-produce")
+    return "->".join(hops)
+
+
+def _free_port() -> int:
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(a, argv) -> int:
+    """``bench.py --gpus N`` (N > 1) started as a plain process: this process stays GPU-untouched
+    (device_count() only, which initialises no device on this image), starts
+    ``torch.distributed.run`` with one rank per GPU as a CHILD process (never an exec), lets rank
+    0's JSON line through on the shared stdout and exits with the child's status. Under an
+    external torchrun (WORLD_SIZE set) this is skipped and the process is one rank."""
+    if not a.stub and not a.shared_gpu_rehearsal:
+        import torch
+
+        have = torch.cuda.device_count()
+        if a.gpus > have:
+            print(f"bench.py: --gpus {a.gpus} but {have} GPU(s) visible (use "
+                  "--shared-gpu-rehearsal for a multi-rank rehearsal on fewer GPUs)",
+                  file=sys.stderr)
+            return 2
+    import subprocess
+
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={a.gpus}", "--master-addr", "127.0.0.1",
+           "--master-port", str(_free_port()), os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", HSA_ENABLE_IPC_MODE_LEGACY="0",
+               GALE_BENCH_LAUNCHED="1")
+    env.setdefault("OMP_NUM_THREADS", "1")
+    p = subprocess.Popen(cmd, cwd=ROOT, env=env)
+    try:
+        return p.wait()
+    except KeyboardInterrupt:
+        p.terminate()
+        return p.wait()
+
+
 def main(argv=None) -> int:
+    argv = list(sys.argv[1:] if argv is None else argv)
     a = parse_args(argv)
+    if a.gpus > 1 and not a.single_process and "WORLD_SIZE" not in os.environ:
+        return launch_ranks(a, argv)
     from gale.utils import host_cpus_per_rank, thread_cpu_seconds
 
     # Host pipeline sizing from the rank's CPU share. Throughput is bound by per-connection
@@ -486,6 +557,8 @@ def main(argv=None) -> int:
     local_gpus = a.gpus if a.single_process else 1
     if a.single_process and world > 1:
         raise SystemExit("bench.py: --single-process runs as ONE process (no torchrun)")
+    if world > 1 and world != a.gpus:
+        raise SystemExit(f"bench.py: --gpus {a.gpus} but the launcher started {world} ranks")
     import torch
     import torch.distributed as dist
 
@@ -698,7 +771,8 @@ def main(argv=None) -> int:
         med = statistics.median(step_rates)
         cores = {k: round((cpu1[k] - cpu0[k]) / elapsed, 2) for k in cpu1}
         out = {
-            "metric": METRIC, "value": round(value, 1), "unit": "images/s", "n_gpus": n_gpus,
+            "metric": METRICS[a.model], "value": round(value, 1), "unit": "images/s",
+            "n_gpus": n_gpus,
             "steps": a.steps, "warmup": a.warmup,
             "ms_per_step": round(elapsed_max / a.steps * 1e3, 4),
             "higher_is_better": True,
@@ -710,15 +784,21 @@ def main(argv=None) -> int:
                     "rank 0",
             "step": f"{a.step_images} images per GPU through fetch->parse->forward->produce-ack",
             "config": {"model": a.model,
-                       "global_batch": a.batch * a.replicas_per_gpu * n_gpus,
+                       # images per timed step over the whole job (the unit ms_per_step times);
+                       # each forward launch runs a micro-batch of <= max_batch images
+                       "global_batch": a.step_images * n_gpus,
                        "seq_len": None, "parallelism": f"dp{n_gpus}",
                        "processes": world,
+                       "launcher": ("torch.distributed.run child of bench.py"
+                                    if os.environ.get("GALE_BENCH_LAUNCHED") else
+                                    "torch.distributed.run" if world > 1 else
+                                    "single process"),
                        "images_per_record": ipr, "max_batch": a.batch,
                        "max_wait_us": a.max_wait_us, "replicas_per_gpu": a.replicas_per_gpu,
                        "decode_threads": a.decode_threads,
                        "locality_split": a.locality_split,
                        "partitions": n_parts, "step_images_per_gpu": a.step_images,
-                       "path": "kafka-fetch->gpu-json-parse->hipgraph-forward->kafka-produce"},
+                       "path": pipeline_path(a, st)},
             "load": (f"offered {a.rate:.0f} images/s per GPU" if a.rate > 0
                      else "value: backlog kept ahead of the consumers (max throughput); "
                           "latency: a second phase at a fixed offered load"),

@@ -65,10 +65,35 @@ def test_bench_stub_torchrun_world2():
     r = lines[0]
     assert r["n_gpus"] == 2 and r["steps"] == 4 and r["value"] > 0
     # a step = one 32-image micro-batch per replica (4 per GPU by default), on both ranks
-    assert r["config"]["parallelism"] == "dp2" and r["config"]["global_batch"] == 32 * 4 * 2
+    assert r["config"]["parallelism"] == "dp2" and r["config"]["global_batch"] == 512 * 2
     # one input topic shared by the two ranks' broker cluster, one partition per replica
     assert r["config"]["partitions"] == 8
     assert r["step_rate_spread"]["min"] > 0 and r["timed_s"] > 0
+
+
+def test_bench_plain_entry_launches_ranks():
+    """The driver's plain ``python bench.py --gpus 2`` (no torchrun around it): bench.py starts
+    one rank per GPU itself (a torch.distributed.run child) and rank 0 reports n_gpus = 2."""
+    cmd = [sys.executable, "bench.py", "--gpus", "2", "--stub", "--steps", "3", "--warmup", "1",
+           "--batch", "32", "--distinct", "64", "--replicas-per-gpu", "2",
+           "--step-images", "256", "--min-warmup-s", "0.2", "--stub-null", "--timeout", "120"]
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    out = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=300,
+                         env=dict(env, OMP_NUM_THREADS="1"))
+    assert out.returncode == 0, out.stderr[-3000:]
+    (r,) = [json.loads(x) for x in out.stdout.splitlines() if x.startswith("{")]
+    assert r["n_gpus"] == 2 and r["config"]["processes"] == 2
+    assert r["config"]["parallelism"] == "dp2"
+    assert r["config"]["launcher"].startswith("torch.distributed.run child")
+
+
+def test_bench_plain_entry_too_many_gpus_fails():
+    """More GPUs than visible (none here) fails loudly instead of silently running fewer."""
+    out = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--steps", "1"], cwd=ROOT,
+                         capture_output=True, text=True, timeout=120)
+    assert out.returncode != 0 and "GPU(s) visible" in out.stderr
+    assert not [x for x in out.stdout.splitlines() if x.startswith("{")]
 
 
 def test_bench_stub_rate_mode():

@@ -2,8 +2,9 @@
 """Scaling curve of the headline benchmark (BASELINE.json: whole-node images/s + p50 latency,
 CIFAR-10 ResNet-20 at 1/2/4/8 GPUs).
 
-Runs ``bench.py`` once per GPU count N on ONE node -- N = 1 as a plain process, N > 1 under
-``torch.distributed.run`` (one rank per GPU, RCCL over xGMI, rendezvous on 127.0.0.1) -- and
+Runs ``bench.py --gpus N`` once per GPU count N on ONE node, exactly as the round driver does:
+a plain process, which for N > 1 starts ``torch.distributed.run`` itself (one rank per GPU, RCCL
+over xGMI, rendezvous on 127.0.0.1; bench.py ``launch_ranks``) -- and
 prints one JSON line per N plus a summary with the per-N images/s, p50/p99 latency and the
 weak-scaling efficiency value(N) / (N * value(1)). Every run is a child process (never an exec),
 bounded by ``--timeout``; the sweep stops at the first failing N.
@@ -19,28 +20,18 @@ from __future__ import annotations
 import argparse
 import json
 import os
-import socket
 import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def free_port() -> int:
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
-
-
 def bench_cmd(n: int, steps: int, warmup: int, extra: list, stub: bool = False,
               single_process: bool = False) -> list:
     args = [os.path.join(ROOT, "bench.py"), "--gpus", str(n), "--steps", str(steps),
             "--warmup", str(warmup)] + (["--stub"] if stub else []) + list(extra)
-    if n == 1 or single_process:  # one process drives all n GPUs
-        return [sys.executable] + args + (["--single-process"] if single_process else [])
-    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
-            f"--nproc-per-node={n}", "--master-addr", "127.0.0.1",
-            "--master-port", str(free_port())] + args
+    # n > 1 per-process: bench.py launches its own ranks (the driver's entry point)
+    return [sys.executable] + args + (["--single-process"] if single_process else [])
 
 
 def last_json(text: str):
