@@ -35,7 +35,7 @@ $(OBJ)/%.o: csrc/%.cpp $(HDRS)
 	$(CXX) $(CXX_FLAGS) -c $< -o $@
 
 gale/_C.so: $(HIP_OBJ) $(CXX_OBJ)
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -L$(ROCM)/lib -lamdhip64 -lrccl -lrocprofiler-sdk-roctx -pthread \
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -L$(ROCM)/lib -lamdhip64 -lrccl -lrocprofiler-sdk-roctx -lz -ldl -pthread \
 	    -Wl,-rpath,$(ROCM)/lib
 
 clean:
@@ -52,7 +52,7 @@ SAN_SRC   := csrc/tests/engine_stress.cpp csrc/runtime/engine.cpp csrc/runtime/r
              $(wildcard csrc/kafka/*.cpp)
 SAN_FLAGS := -O1 -g -fno-omit-frame-pointer -std=c++17 -D__HIP_PLATFORM_AMD__ -I$(ROCM)/include \
              -Icsrc/include -mavx2 -mfma -msse4.2 -mpclmul -mbmi2 -pthread
-SAN_LIBS  := -L$(ROCM)/lib -lamdhip64 -lrocprofiler-sdk-roctx -Wl,-rpath,$(ROCM)/lib
+SAN_LIBS  := -L$(ROCM)/lib -lamdhip64 -lrocprofiler-sdk-roctx -lz -ldl -Wl,-rpath,$(ROCM)/lib
 # LLVM's sanitizer runtimes (ROCm's clang): gcc-11's libtsan does not intercept
 # pthread_cond_clockwait, which libstdc++'s condition_variable uses, and reports false races
 SAN_CXX   ?= $(ROCM)/lib/llvm/bin/clang++

@@ -54,6 +54,7 @@ EngineConfig config_from_dict(const py::dict& d) {
   opt(d, "acks", c.acks);
   opt(d, "sink_mode", c.sink_mode);
   opt(d, "linger_ms", c.linger_ms);
+  opt(d, "compression", c.compression);
   opt(d, "batch_size", c.batch_size);
   opt(d, "value_format", c.value_format);
   opt(d, "type_id_header", c.type_id_header);

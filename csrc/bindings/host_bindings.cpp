@@ -15,6 +15,7 @@
 #include "../codec/text_pack.h"
 #include "../kafka/broker.h"
 #include "../kafka/client.h"
+#include "../kafka/compress.h"
 #include "../kafka/protocol.h"
 #include "../kafka/wire.h"
 
@@ -54,9 +55,28 @@ py::list records_to_py(const uint8_t* base, const std::vector<RecordRef>& recs) 
       hs.append(py::make_tuple(h.key, h.value_null ? py::object(py::none())
                                                    : py::object(py::bytes(h.value))));
     d["headers"] = hs;
+    if (r.poison) d["poison"] = true;
     out.append(d);
   }
   return out;
+}
+
+// decode_records, falling back to the consumer's normalisation (compress.h) for compressed /
+// legacy / corrupt blobs; `hold` keeps the normalised bytes the records point into
+const uint8_t* decode_any(const std::string_view s, int64_t min_offset, bool check_crc,
+                          std::string& hold, std::vector<RecordRef>& recs) {
+  const uint8_t* base = reinterpret_cast<const uint8_t*>(s.data());
+  try {
+    decode_records(base, 0, s.size(), min_offset, check_crc, recs);
+    return base;
+  } catch (const ProtocolError&) {
+    recs.clear();
+    NormalizeStats st;
+    hold = normalize_records(base, s.size(), min_offset, check_crc, (size_t)1 << 30, st);
+    const uint8_t* hb = reinterpret_cast<const uint8_t*>(hold.data());
+    decode_records(hb, 0, hold.size(), min_offset, false, recs, nullptr, true);
+    return hb;
+  }
 }
 
 std::vector<Header> headers_from_py(const py::object& o) {
@@ -581,9 +601,69 @@ void bind_host(py::module_& m) {
   k.def("decode_records", [](py::bytes b, int64_t min_offset, bool check_crc) {
     const std::string_view s = view(b);
     std::vector<RecordRef> recs;
-    decode_records(reinterpret_cast<const uint8_t*>(s.data()), 0, s.size(), min_offset, check_crc,
-                   recs);
-    return records_to_py(reinterpret_cast<const uint8_t*>(s.data()), recs);
+    std::string hold;
+    const uint8_t* base = decode_any(s, min_offset, check_crc, hold, recs);
+    return records_to_py(base, recs);
+  }, py::arg("data"), py::arg("min_offset") = 0, py::arg("check_crc") = true,
+     "records of a records blob (any message format / compression; undecodable batches come "
+     "back as {'poison': True, 'value': None} records)");
+  // ---- compression codecs and message-format conversion (kafka/compress.h)
+  k.def("codec_available", [](const std::string& c) { return codec_available(codec_from_name(c)); });
+  k.def("compress", [](const std::string& c, py::bytes data) {
+    const std::string_view s = view(data);
+    std::string out;
+    {
+      py::gil_scoped_release nogil;
+      out = compress(codec_from_name(c), reinterpret_cast<const uint8_t*>(s.data()), s.size());
+    }
+    return py::bytes(out);
+  }, py::arg("codec"), py::arg("data"));
+  k.def("decompress", [](const std::string& c, py::bytes data, size_t limit) {
+    const std::string_view s = view(data);
+    std::string out, err;
+    if (!decompress(codec_from_name(c), reinterpret_cast<const uint8_t*>(s.data()), s.size(), out,
+                    limit, &err))
+      throw std::runtime_error(err.empty() ? "corrupt " + c + " data" : err);
+    return py::bytes(out);
+  }, py::arg("codec"), py::arg("data"), py::arg("limit") = (size_t)1 << 30);
+  k.def("snappy_compress_raw", [](py::bytes data) {
+    const std::string_view s = view(data);
+    return py::bytes(snappy_compress_raw(reinterpret_cast<const uint8_t*>(s.data()), s.size()));
+  });
+  k.def("xxh32", [](py::bytes data, uint32_t seed) {
+    const std::string_view s = view(data);
+    return xxh32(reinterpret_cast<const uint8_t*>(s.data()), s.size(), seed);
+  }, py::arg("data"), py::arg("seed") = 0);
+  k.def("compress_batch", [](py::bytes batch, const std::string& c) {
+    return py::bytes(compress_batch(std::string(view(batch)), codec_from_name(c)));
+  }, py::arg("batch"), py::arg("codec"));
+  k.def("encode_message_set", [](int magic, py::list values, int64_t base_offset,
+                                 const std::string& c, py::object keys, int64_t timestamp) {
+    std::vector<LegacyRecord> recs(values.size());
+    for (size_t i = 0; i < values.size(); ++i) {
+      if (values[i].is_none()) recs[i].value_null = true;
+      else recs[i].value = std::string(view(values[i].cast<py::bytes>()));
+      if (!keys.is_none() && !keys.cast<py::list>()[i].is_none()) {
+        recs[i].key = std::string(view(keys.cast<py::list>()[i].cast<py::bytes>()));
+        recs[i].key_null = false;
+      }
+      recs[i].timestamp = timestamp;
+    }
+    return py::bytes(encode_message_set(magic, recs, base_offset, codec_from_name(c)));
+  }, py::arg("magic"), py::arg("values"), py::arg("base_offset") = 0, py::arg("codec") = "none",
+     py::arg("keys") = py::none(), py::arg("timestamp") = -1);
+  k.def("normalize_records", [](py::bytes data, int64_t min_offset, bool check_crc) {
+    const std::string_view s = view(data);
+    NormalizeStats st;
+    const std::string out = normalize_records(reinterpret_cast<const uint8_t*>(s.data()),
+                                              s.size(), min_offset, check_crc, (size_t)1 << 30,
+                                              st);
+    py::dict d;
+    d["converted_batches"] = st.converted_batches;
+    d["poison_batches"] = st.poison_batches;
+    d["poison_records"] = st.poison_records;
+    d["last_error"] = st.last_error;
+    return py::make_tuple(py::bytes(out), d);
   }, py::arg("data"), py::arg("min_offset") = 0, py::arg("check_crc") = true);
   k.def("encode", &py_encode);
   k.def("decode", &py_decode);
@@ -652,6 +732,24 @@ void bind_host(py::module_& m) {
         py::gil_scoped_release nogil;
         return b.append(topic, partition, ins);
       }, py::arg("topic"), py::arg("partition"), py::arg("values"), py::arg("keys") = py::none())
+      .def("append_legacy", [](Broker& b, const std::string& topic, int partition, int magic,
+                               py::list values, const std::string& codec, py::object keys,
+                               int64_t timestamp) {
+        std::vector<LegacyRecord> recs(values.size());
+        for (size_t i = 0; i < values.size(); ++i) {
+          if (values[i].is_none()) recs[i].value_null = true;
+          else recs[i].value = std::string(view(values[i].cast<py::bytes>()));
+          if (!keys.is_none() && !keys.cast<py::list>()[i].is_none()) {
+            recs[i].key = std::string(view(keys.cast<py::list>()[i].cast<py::bytes>()));
+            recs[i].key_null = false;
+          }
+          recs[i].timestamp = timestamp;
+        }
+        py::gil_scoped_release nogil;
+        return b.append_legacy(topic, partition, magic, recs, codec_from_name(codec));
+      }, py::arg("topic"), py::arg("partition"), py::arg("magic"), py::arg("values"),
+         py::arg("codec") = "none", py::arg("keys") = py::none(), py::arg("timestamp") = -1,
+         "append one old-format message set (magic 0/1, optionally compressed)")
       .def("append_batch_repeated", [](Broker& b, const std::string& topic, int partition,
                                        py::bytes batch, int64_t times) {
         // append one pre-encoded batch `times` times, sharing its bytes (bench preloading)
@@ -700,10 +798,10 @@ void bind_host(py::module_& m) {
                       int64_t max_bytes) {
         const std::string raw = b.read_raw(topic, partition, offset, max_bytes);
         std::vector<RecordRef> recs;
-        decode_records(reinterpret_cast<const uint8_t*>(raw.data()), 0, raw.size(), offset, true,
-                       recs);
+        std::string hold;
+        const uint8_t* base = decode_any(raw, offset, true, hold, recs);
         for (auto& r : recs) r.partition = partition;
-        return records_to_py(reinterpret_cast<const uint8_t*>(raw.data()), recs);
+        return records_to_py(base, recs);
       }, py::arg("topic"), py::arg("partition"), py::arg("offset") = 0,
          py::arg("max_bytes") = 64ll << 20)
       .def("stats", [](Broker& b) {
@@ -748,8 +846,9 @@ void bind_host(py::module_& m) {
   py::class_<Producer, std::shared_ptr<Producer>>(k, "Producer")
       .def(py::init([](const std::string& bootstrap, int acks, int linger_ms, int batch_size,
                        const std::string& client_id, int request_timeout_ms, int max_in_flight,
-                       int max_request_size) {
+                       int max_request_size, const std::string& compression) {
              ProducerConfig c;
+             c.compression = codec_from_name(compression);
              c.max_request_size = max_request_size;
              c.bootstrap = bootstrap;
              c.acks = acks;
@@ -764,7 +863,7 @@ void bind_host(py::module_& m) {
            py::arg("bootstrap"), py::arg("acks") = 1, py::arg("linger_ms") = 0,
            py::arg("batch_size") = 16384, py::arg("client_id") = "gale-producer",
            py::arg("request_timeout_ms") = 30000, py::arg("max_in_flight") = 5,
-           py::arg("max_request_size") = 64 << 20)
+           py::arg("max_request_size") = 64 << 20, py::arg("compression") = "none")
       .def("send", [](Producer& p, const std::string& topic, py::object value, py::object key,
                       int partition, py::object headers, int64_t timestamp, py::object callback) {
         std::string v;
@@ -847,6 +946,14 @@ void bind_host(py::module_& m) {
       })
       .def("seek", &Consumer::seek)
       .def("position", &Consumer::position)
+      .def("format_stats", [](Consumer& c) {
+        py::dict d;
+        d["converted_batches"] = c.converted_batches();
+        d["poison_batches"] = c.poison_batches();
+        d["poison_records"] = c.poison_records();
+        return d;
+      }, "record-format conversion counters: compressed / legacy batches rewritten, "
+         "undecodable batches skipped as poison records")
       .def("poll", [](Consumer& c) {
         std::vector<Fetched> fs;
         {

@@ -20,6 +20,7 @@ const char* status_name(int s) {
     case BAD_NUMBER: return "bad_number";
     case NULL_INSTANCES: return "null_instances";
     case TOO_LARGE: return "too_large";
+    case CORRUPT: return "corrupt";
     default: return "unknown";
   }
 }
@@ -206,6 +207,25 @@ Scan scan_envelope(const uint8_t* p, size_t n) {
   s.arr_off = (int64_t)beg;
   s.arr_len = (int64_t)(j - beg);  // up to and including the closing ']'
   return s;
+}
+
+bool split_instances(const uint8_t* arr, size_t len,
+                     std::vector<std::pair<uint32_t, uint32_t>>& spans) {
+  spans.clear();
+  if (len < 2 || arr[0] != '[' || arr[len - 1] != ']') return false;
+  int depth = 0;
+  uint32_t start = 0;
+  for (size_t i = 0; i < len; ++i) {
+    const uint8_t c = arr[i];
+    if (c == '[') {
+      if (++depth == 2) start = (uint32_t)i;
+    } else if (c == ']') {
+      if (depth == 2) spans.emplace_back(start, (uint32_t)(i + 1));
+      if (--depth < 0) return false;
+      if (depth == 0 && i != len - 1) return false;
+    }
+  }
+  return depth == 0;
 }
 
 Scan scan_instances(const uint8_t* p, size_t n, int H, int W, int C) {

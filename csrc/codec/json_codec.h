@@ -18,6 +18,8 @@
 #include <stdint.h>
 
 #include <string>
+#include <utility>
+#include <vector>
 
 namespace gale {
 namespace codec {
@@ -31,7 +33,10 @@ enum Status : int {
   BAD_NUMBER = 5,     // malformed JSON number / non-number element
   NULL_INSTANCES = 6, // "instances": null
   TOO_LARGE = 7,      // more images than the caller allows
+  CORRUPT = 8,        // the Kafka batch holding the record could not be decoded (unknown codec,
+                      // corrupt compressed data, CRC mismatch; kafka/compress.h poison records)
 };
+constexpr int kStatusCount = 9;
 
 const char* status_name(int s);
 
@@ -49,6 +54,12 @@ Scan scan_envelope(const uint8_t* p, size_t n);
 
 // Envelope validation + image count (the per-number work is left to the GPU parser).
 Scan scan_instances(const uint8_t* p, size_t n, int H, int W, int C);
+
+// Byte spans [begin, end) of the top-level elements (the images) of the instances array
+// `arr[0..len)` (its outer '[' ... ']'), for splitting a record with more images than one
+// micro-batch holds. false when the bracket structure is broken.
+bool split_instances(const uint8_t* arr, size_t len,
+                     std::vector<std::pair<uint32_t, uint32_t>>& spans);
 
 // Full host decoder: validates structure and parses every number into out[N*H*W*C].
 // Returns the status; *images receives N. out may be null to validate only.

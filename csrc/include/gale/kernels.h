@@ -114,7 +114,7 @@ hipError_t resnet20_fused_forward(const ResNet20Params& p, int batch, const floa
                                   hipStream_t stream);
 
 // Whole-network MNIST LeNet-5 (csrc/kernels/lenet5_fused.hip): x fp32 [B,28,28,1] -> softmax
-// fp32 [B,10], four images per workgroup with every activation in LDS. Weights are the serving
+// fp32 [B,10], one image per 256-thread workgroup (grid = batch) with every activation in LDS. Weights are the serving
 // plan's packed bf16 matrices: conv1 [16][32], conv2 [16][224], fc1 [128][416], fc2 [128][128]
 // (fp32 biases of Npad entries), fc3 fp32 [10][88] + [10].
 struct LeNet5Params {

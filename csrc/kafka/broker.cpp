@@ -269,13 +269,14 @@ const Broker::PartitionLog* Broker::find_log(const std::string& topic, int parti
 }
 
 int64_t Broker::append_locked(PartitionLog& log, std::shared_ptr<const std::string> batch,
-                              const BatchInfo& bi) {
+                              bool legacy, const BatchInfo& bi) {
   Segment s;
   s.base = log.end;
   s.next = log.end + bi.last_offset_delta + 1;
   s.max_ts = bi.max_timestamp;
   s.bytes = std::move(batch);
-  if (cfg_.log_append_time) {
+  s.legacy = legacy;
+  if (cfg_.log_append_time && !legacy) {
     // the stored bytes may be shared (preloaded by reference): the stamp lives in the segment
     const uint8_t* b = reinterpret_cast<const uint8_t*>(s.bytes->data());
     const size_t n = kBatchMaxTsOffset + 8 - kBatchAttrOffset;
@@ -322,7 +323,28 @@ int64_t Broker::append(const std::string& topic, int partition, const std::vecto
     std::lock_guard<std::mutex> lk(mu_);
     PartitionLog* log = find_log(topic, partition);
     if (!log) throw std::invalid_argument("unknown topic/partition " + topic);
-    base = append_locked(*log, std::move(bytes), bi);
+    base = append_locked(*log, std::move(bytes), false, bi);
+  }
+  wake(topic, partition);
+  return base;
+}
+
+int64_t Broker::append_legacy(const std::string& topic, int partition, int magic,
+                              const std::vector<LegacyRecord>& recs, int codec) {
+  if (recs.empty()) return log_end(topic, partition);
+  int64_t base;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    PartitionLog* log = find_log(topic, partition);
+    if (!log) throw std::invalid_argument("unknown topic/partition " + topic);
+    base = log->end;
+    auto bytes = std::make_shared<const std::string>(encode_message_set(magic, recs, base, codec));
+    BatchInfo bi;
+    bi.base_offset = base;
+    bi.records = (int32_t)recs.size();
+    bi.last_offset_delta = (int32_t)recs.size() - 1;
+    bi.max_timestamp = recs.back().timestamp;
+    append_locked(*log, std::move(bytes), true, bi);
   }
   wake(topic, partition);
   return base;
@@ -339,7 +361,7 @@ int64_t Broker::append_shared(const std::string& topic, int partition,
     probe_lock_.add(now_ns() - t0);
     PartitionLog* log = find_log(topic, partition);
     if (!log) throw std::invalid_argument("unknown topic/partition " + topic);
-    base = append_locked(*log, std::move(batch), bi);
+    base = append_locked(*log, std::move(batch), false, bi);
   }
   wake(topic, partition);
   return base;
@@ -391,6 +413,7 @@ std::string Broker::read_raw(const std::string& topic, int partition, int64_t of
     if (!out.empty() && (int64_t)(out.size() + s.bytes->size()) > max_bytes) break;
     const size_t at = out.size();
     out += *s.bytes;
+    if (s.legacy) continue;  // (offsets inside, as written)
     Writer::put_be(&out[at], &s.base, 8);
     if (s.stamped) {
       Writer::put_be(&out[at + kBatchCrcOffset], &s.crc, 4);
@@ -488,6 +511,23 @@ void Broker::serve(int fd) {
         std::lock_guard<std::mutex> lk(append_mu_);
         for (auto& k : keys) waiters_[k].push_back(&w);
       }
+      // unregistered on every exit path (a throwing try_fetch included): wake() must never see
+      // a pointer to this stack frame after it is gone
+      struct Unregister {
+        Broker* b;
+        Waiter* w;
+        const std::vector<std::pair<std::string, int>>& keys;
+        ~Unregister() {
+          std::lock_guard<std::mutex> lk(b->append_mu_);
+          for (auto& k : keys) {
+            auto it = b->waiters_.find(k);
+            if (it == b->waiters_.end()) continue;
+            auto& v = it->second;
+            v.erase(std::remove(v.begin(), v.end(), w), v.end());
+            if (v.empty()) b->waiters_.erase(it);
+          }
+        }
+      } unregister{this, &w, keys};
       bool final_attempt = c.fetch.max_wait_ms <= 0;
       int64_t t_wake = 0;
       for (;;) {
@@ -505,14 +545,6 @@ void Broker::serve(int fd) {
             [&] { return w.flag || !running_; });
         t_wake = w.flag ? w.t_wake_ns : 0;
         final_attempt = now_ms() >= c.deadline || !running_;
-      }
-      std::lock_guard<std::mutex> lk(append_mu_);
-      for (auto& k : keys) {
-        auto it = waiters_.find(k);
-        if (it == waiters_.end()) continue;
-        auto& v = it->second;
-        v.erase(std::remove(v.begin(), v.end(), &w), v.end());
-        if (v.empty()) waiters_.erase(it);
       }
     }
     const int64_t t0 = fetch ? now_ns() : 0;
@@ -771,7 +803,7 @@ bool Broker::handle_request(Conn& c, const uint8_t* p, size_t n) {
                       reinterpret_cast<const char*>(blob + bs[k].first), (size_t)bs[k].second.length);
                   const int64_t base = log->end;
                   Writer::put_be(&(*copy)[0], &base, 8);
-                  append_locked(*log, std::move(copy), bs[k].second);
+                  append_locked(*log, std::move(copy), false, bs[k].second);
                   if (k == 0) pr.base_offset = base;
                 }
               }
@@ -970,6 +1002,10 @@ bool Broker::try_fetch(Conn& c, bool final_attempt) {
         if (!sel.empty()) first_data = false;
         rb.w.i32((int32_t)pbytes);
         for (const Segment* s : sel) {
+          if (s->legacy) {  // legacy message set: its own offsets, verbatim
+            rb.shared(s->bytes, 0, s->bytes->size());
+            continue;
+          }
           rb.w.i64(s->base);
           if (s->stamped) {  // batchLength, leaderEpoch, magic | crc | attrs .. maxTimestamp
             rb.w.raw(s->bytes->data() + kBatchLengthOffset, kBatchCrcOffset - kBatchLengthOffset);

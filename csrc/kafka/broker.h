@@ -29,6 +29,7 @@
 
 #include "group_coordinator.h"
 #include "protocol.h"
+#include "compress.h"
 #include "wire.h"
 
 namespace gale {
@@ -96,6 +97,12 @@ class Broker {
   // Local (in-process) producer: appends one batch; returns its base offset.
   int64_t append(const std::string& topic, int partition, const std::vector<RecordIn>& recs);
   // Append a pre-encoded batch shared by reference (bench preloading of repeated payloads).
+  // Old message format (log.message.format.version < 0.11): `recs` appended as ONE legacy
+  // message set of magic 0 or 1, wrapped in a `codec`-compressed message when codec != 0. The
+  // bytes are stored and served as such (consumers must read the old format). Returns the first
+  // offset.
+  int64_t append_legacy(const std::string& topic, int partition, int magic,
+                        const std::vector<LegacyRecord>& recs, int codec);
   int64_t append_shared(const std::string& topic, int partition,
                         std::shared_ptr<const std::string> batch);
   int64_t log_start(const std::string& topic, int partition) const;
@@ -121,6 +128,8 @@ class Broker {
     bool stamped = false;
     uint32_t crc = 0;
     uint8_t hdr[22] = {};
+    // a legacy message set (magic 0/1, kafka/compress.h): served verbatim, offsets included
+    bool legacy = false;
   };
   struct PartitionLog {
     std::vector<Segment> segs;
@@ -139,7 +148,7 @@ class Broker {
   bool flush(Conn& c);
   // 1 sent, 0 splice unusable, -1 connection error
   int splice_chunk(Conn& c, const Chunk& f, bool more);
-  int64_t append_locked(PartitionLog& log, std::shared_ptr<const std::string> batch,
+  int64_t append_locked(PartitionLog& log, std::shared_ptr<const std::string> batch, bool legacy,
                         const BatchInfo& bi);
   PartitionLog* find_log(const std::string& topic, int partition);
   const PartitionLog* find_log(const std::string& topic, int partition) const;

@@ -2,7 +2,10 @@
 #include "client.h"
 #include "gale/thread_name.h"
 
+#include "compress.h"
+
 #include <arpa/inet.h>
+#include <stdio.h>
 #include <errno.h>
 #include <fcntl.h>
 #include <netdb.h>
@@ -746,6 +749,7 @@ void Producer::run() {
           }
           Writer bw;
           encode_batch(bw, ins.data(), ins.size(), 0, item.second.front().ts);
+          if (cfg_.compression != CODEC_NONE) bw.buf = compress_batch(bw.buf, cfg_.compression);
           if (bytes && bytes + bw.size() > (size_t)cfg_.max_request_size) break;
           bytes += bw.size();
           ProduceTopic* pt = nullptr;
@@ -922,6 +926,13 @@ void Consumer::collect(std::vector<Fetched>& out) {
     }
     Reader r(f.buf.get(), f.size);
     const FetchResponse m = decode_fetch_response(r);
+    // partitions whose records are not plain v2 batches: normalised copies (compress.h),
+    // appended behind the response body once every partition was looked at
+    struct Conv {
+      int partition;
+      std::string blob;
+    };
+    std::vector<Conv> convs;
     for (auto& t : m.topics)
       for (auto& p : t.partitions) {
         auto it = inf.from.find(p.index);
@@ -936,12 +947,58 @@ void Consumer::collect(std::vector<Fetched>& out) {
         }
         hw_[p.index] = p.high_watermark;
         if (p.records_len <= 0) continue;
-        const size_t before = f.records.size();
-        decode_records(f.buf.get(), p.records_off, (size_t)p.records_len, pos_[p.index],
-                       cfg_.check_crcs, f.records, &f.batches);
+        const size_t before = f.records.size(), bbefore = f.batches.size();
+        try {
+          decode_records(f.buf.get(), p.records_off, (size_t)p.records_len, pos_[p.index],
+                         cfg_.check_crcs, f.records, &f.batches);
+        } catch (const ProtocolError&) {
+          // compressed / legacy / corrupt: never thrown out of poll (that would retry the same
+          // position forever); the partition's records are rewritten as plain v2 batches, with
+          // undecodable batches as poison records that advance the position
+          f.records.resize(before);
+          f.batches.resize(bbefore);
+          NormalizeStats ns;
+          std::string blob = normalize_records(f.buf.get() + p.records_off, (size_t)p.records_len,
+                                               pos_[p.index], cfg_.check_crcs,
+                                               cfg_.max_decompressed_bytes, ns);
+          converted_batches_ += ns.converted_batches;
+          poison_batches_ += ns.poison_batches;
+          poison_records_ += ns.poison_records;
+          if (ns.poison_batches && poison_logged_ < 16) {
+            ++poison_logged_;
+            fprintf(stderr, "[gale consumer] %s-%d: %lld undecodable batch(es) from offset %lld "
+                    "skipped as %lld poison record(s): %s\n", topic_.c_str(), p.index,
+                    (long long)ns.poison_batches, (long long)pos_[p.index],
+                    (long long)ns.poison_records, ns.last_error.c_str());
+          }
+          if (!blob.empty()) convs.push_back({p.index, std::move(blob)});
+          continue;
+        }
         for (size_t k = before; k < f.records.size(); ++k) f.records[k].partition = p.index;
         if (f.records.size() > before) pos_[p.index] = f.records.back().offset + 1;
       }
+    if (!convs.empty()) {
+      // one buffer: [response body][normalised blobs], so every record still points into ONE
+      // buffer (pinned when the pool's chunk fits it; the device-side packed copy of the body,
+      // if any, does not describe the new buffer)
+      size_t total = (f.size + 15) & ~(size_t)15;
+      for (const Conv& c : convs) total += (c.blob.size() + 15) & ~(size_t)15;
+      std::shared_ptr<uint8_t> nb = alloc_(total);
+      memcpy(nb.get(), f.buf.get(), f.size);
+      size_t at = (f.size + 15) & ~(size_t)15;
+      f.buf = nb;
+      f.tap_result = -1;
+      for (const Conv& c : convs) {
+        memcpy(nb.get() + at, c.blob.data(), c.blob.size());
+        const size_t before = f.records.size();
+        decode_records(nb.get(), at, c.blob.size(), pos_[c.partition], false, f.records,
+                       &f.batches, /*honor_poison=*/true);
+        for (size_t k = before; k < f.records.size(); ++k) f.records[k].partition = c.partition;
+        if (f.records.size() > before) pos_[c.partition] = f.records.back().offset + 1;
+        at += (c.blob.size() + 15) & ~(size_t)15;
+      }
+      f.size = at;
+    }
     if (!f.records.empty()) out.push_back(std::move(f));
   }
   if (stale) cluster_.invalidate();

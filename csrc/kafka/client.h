@@ -132,6 +132,7 @@ struct ProducerConfig : ClientConfig {
   int max_request_size = 64 << 20;
   int max_in_flight = 5;
   int64_t buffer_memory = 1ll << 30;  // send() blocks while more than this is unsent
+  int compression = 0;  // compression.type (compress.h Codec; kafka-clients default none)
 };
 
 struct SendResult {
@@ -234,6 +235,8 @@ struct ConsumerConfig : ClientConfig {
   // keep the next fetch of every leader in flight while the application processes the previous
   // response (the Java consumer's fetcher does the same): the broker's send overlaps our work
   bool prefetch = true;
+  // bound on one decompressed batch (compressed batches / legacy wrappers, compress.h)
+  size_t max_decompressed_bytes = (size_t)256 << 20;
 };
 
 // One fetch round: records point into `buf` (the response body).
@@ -268,6 +271,11 @@ class Consumer {
   int64_t committed(int partition);
   std::map<int, int64_t> high_watermarks() const { return hw_; }
   Cluster& cluster() { return cluster_; }
+  // record-format conversion counters (compress.h): batches rewritten from a compressed or
+  // legacy format, undecodable batches skipped as poison records
+  int64_t converted_batches() const { return converted_batches_; }
+  int64_t poison_batches() const { return poison_batches_; }
+  int64_t poison_records() const { return poison_records_; }
   // fetch response bodies are shown to this tap while they are received
   void set_recv_tap(std::shared_ptr<RecvTap> tap) { tap_ = std::move(tap); }
 
@@ -292,6 +300,8 @@ class Consumer {
   std::vector<Fetched> ready_;  // drained responses not yet returned by poll()
   int32_t generation_ = -1;
   std::string member_id_;
+  std::atomic<int64_t> converted_batches_{0}, poison_batches_{0}, poison_records_{0};
+  int poison_logged_ = 0;
 };
 
 // Consumer-group membership (Kafka's eager rebalance protocol): JoinGroup -> (leader computes

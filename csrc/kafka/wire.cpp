@@ -348,7 +348,7 @@ BatchInfo peek_batch(const uint8_t* p, size_t avail, bool check_crc) {
 
 size_t decode_records(const uint8_t* base, size_t off, size_t len, int64_t min_offset,
                       bool check_crc, std::vector<RecordRef>& out,
-                      std::vector<BatchSpan>* spans) {
+                      std::vector<BatchSpan>* spans, bool honor_poison) {
   size_t added = 0;
   size_t pos = off;
   const size_t end = off + len;
@@ -360,6 +360,7 @@ size_t decode_records(const uint8_t* base, size_t off, size_t len, int64_t min_o
     const BatchInfo b = peek_batch(base + pos, end - pos, check_crc);
     if (b.attributes & 0x7) throw ProtocolError("compressed record batches are not supported");
     const bool control = (b.attributes & 0x20) != 0;
+    const bool poison = honor_poison && (b.attributes & 0x4000) != 0;  // kAttrGalePoison
     const size_t first = out.size();
     if (!control) {
       Reader r(base + pos + kBatchHeaderBytes, (size_t)b.length - kBatchHeaderBytes);
@@ -387,6 +388,7 @@ size_t decode_records(const uint8_t* base, size_t off, size_t len, int64_t min_o
         if (rlen < 0 || consumed > (size_t)rlen) throw ProtocolError("bad record length");
         r.skip((size_t)rlen - consumed);
         rr.headers_len = (int64_t)(rbase + r.pos()) - rr.headers_off;
+        rr.poison = poison;
         if (rr.offset >= min_offset) {
           out.push_back(rr);
           ++added;

@@ -219,6 +219,9 @@ struct RecordRef {
   int32_t header_count = 0;
   int64_t headers_off = 0;  // raw header bytes (decode with decode_headers)
   int64_t headers_len = 0;
+  // a marker for a record the consumer could not decode (compress.h poison batches): the value
+  // is null and the engine applies --on-error with status CORRUPT
+  bool poison = false;
 };
 
 struct BatchInfo {
@@ -244,9 +247,12 @@ struct BatchSpan {
   size_t off = 0, len = 0;
   size_t first_rec = 0, nrec = 0;
 };
+// Throws ProtocolError on anything but plain v2 batches (compressed / legacy formats, CRC
+// mismatches, malformed records): the consumer then normalises the blob (compress.h) and decodes
+// that with honor_poison, which marks the records of poison batches.
 size_t decode_records(const uint8_t* base, size_t off, size_t len, int64_t min_offset,
                       bool check_crc, std::vector<RecordRef>& out,
-                      std::vector<BatchSpan>* spans = nullptr);
+                      std::vector<BatchSpan>* spans = nullptr, bool honor_poison = false);
 
 std::vector<Header> decode_headers(const uint8_t* base, const RecordRef& r);
 

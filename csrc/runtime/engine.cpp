@@ -4,6 +4,7 @@
 
 #include <hip/hip_runtime.h>
 #include <stdio.h>
+#include <string.h>
 #include <sched.h>
 #include <sys/prctl.h>
 
@@ -11,6 +12,7 @@
 #include <sstream>
 
 #include "../codec/json_codec.h"
+#include "../kafka/compress.h"
 #include "pack_tap.h"
 #include "trace.h"
 
@@ -143,6 +145,16 @@ struct Engine::ReplicaSlot {
   std::atomic<int64_t> busy_ns{0}, busy_since{0};
 };
 
+struct SplitRecord {
+  InRecord parent;   // the input record (its fetch buffer released; the key copied below)
+  std::string key;
+  int parts = 0;
+  std::mutex mu;
+  std::vector<std::string> rows;  // per fragment: its prediction rows "[..],[..]"
+  int done = 0;
+  int status = codec::OK;         // the first failing fragment's status
+};
+
 // ---------------------------------------------------------------------------------------------
 
 Engine::Engine(EngineConfig cfg) : cfg_(std::move(cfg)), rng_(cfg_.seed) {
@@ -239,6 +251,7 @@ void Engine::start() {
     pc.batch_size = cfg_.batch_size;
     pc.buffer_memory = cfg_.producer_buffer_bytes;
     pc.max_request_size = (int)cfg_.producer_request_bytes;
+    pc.compression = kafka::codec_from_name(cfg_.compression);
     producers_.push_back(std::make_unique<kafka::Producer>(pc));
   }
   // static mode: resolve the input partitions and split them over the source threads now;
@@ -657,6 +670,9 @@ void Engine::source_loop(int idx) {
       for (int p : parts) {
         next_fetch_.erase(p);
         high_watermark_.erase(p);
+        // (records still in flight complete against a missing entry, which is a no-op; a
+        // partition assigned back later starts a fresh window)
+        pending_.erase(p);
       }
     }
     parts = want;
@@ -675,6 +691,7 @@ void Engine::source_loop(int idx) {
     ctl.cv.notify_all();
   };
   int64_t last_commit = mono_ns();
+  int64_t seen_conv = 0, seen_poison = 0, seen_poison_recs = 0;
   std::vector<InRecord> good;
   while (cons && !stopping_) {
     try {
@@ -695,6 +712,17 @@ void Engine::source_loop(int idx) {
       trace::Range tr("gale:fetch");
       fs = cons->poll();
       ns_poll_ += mono_ns() - t0;
+      // record-format conversion (compressed / legacy batches) and poison batches
+      const int64_t cb = cons->converted_batches(), pb = cons->poison_batches(),
+                    pr = cons->poison_records();
+      if (cb != seen_conv || pb != seen_poison) {
+        converted_batches_ += cb - seen_conv;
+        poison_batches_ += pb - seen_poison;
+        poison_records_ += pr - seen_poison_recs;
+        seen_conv = cb;
+        seen_poison = pb;
+        seen_poison_recs = pr;
+      }
     } catch (const std::exception& e) {
       fprintf(stderr, "[gale source %d] fetch failed: %s\n", idx, e.what());
       std::this_thread::sleep_for(std::chrono::milliseconds(100));
@@ -796,6 +824,10 @@ bool Engine::ingest_fetch(FetchItem& it, std::vector<InRecord>& good, int lane) 
   io.arr_len.assign(n, 0);
   for (size_t i = 0; i < n; ++i) {
     const kafka::RecordRef& rr = f.records[i];
+    if (rr.poison) {
+      io.status[i] = codec::CORRUPT;  // stands for a record of an undecodable batch
+      continue;
+    }
     if (rr.value_len < 0) {
       io.status[i] = codec::BAD_ENVELOPE;  // null value (Jackson would throw)
       continue;
@@ -835,13 +867,15 @@ bool Engine::ingest_fetch(FetchItem& it, std::vector<InRecord>& good, int lane) 
     r.dev_locality = slot_key_[(size_t)it.slot];
     ++records_in_;
     if (r.len >= 0) bytes_in_ += r.len;
-    r.status = corrupt[i] ? (int)codec::BAD_ENVELOPE : io.status[i];
+    r.status = corrupt[i] ? (int)codec::CORRUPT : io.status[i];
     r.arr_off = io.arr_off[i];
     r.arr_len = io.arr_len[i];
     r.images = io.images[i];
-    if (r.status == codec::OK && r.images > cfg_.max_batch) r.status = codec::TOO_LARGE;
     if (r.status == codec::OK && fault_hit(parse_error_p_)) r.status = codec::BAD_ENVELOPE;
-    if (r.status == codec::OK) {
+    if (r.status == codec::OK && r.images > cfg_.max_batch) {
+      images_in_ += r.images;
+      if (!split_record(r, good)) emit_error(r, codec::BAD_SHAPE, prod);
+    } else if (r.status == codec::OK) {
       images_in_ += r.images;
       good.push_back(std::move(r));
     } else {
@@ -910,8 +944,10 @@ void Engine::decode_fetch(FetchItem& it, std::vector<InRecord>& good, int lane) 
     r.t_fetch_ns = it.t_fetch_ns;
     r.source = it.source;
     ++records_in_;
-    if (!corrupt.empty() && corrupt[i]) {
-      r.status = codec::BAD_ENVELOPE;  // corrupt Kafka batch (CRC32C mismatch)
+    if (rr.poison) {
+      r.status = codec::CORRUPT;  // a record of a batch the consumer could not decode
+    } else if (!corrupt.empty() && corrupt[i]) {
+      r.status = codec::CORRUPT;  // corrupt Kafka batch (CRC32C mismatch)
     } else if (r.len < 0) {
       r.status = codec::BAD_ENVELOPE;  // null value (Jackson would throw)
     } else {
@@ -924,10 +960,12 @@ void Engine::decode_fetch(FetchItem& it, std::vector<InRecord>& good, int lane) 
       r.arr_off = s.arr_off;
       r.arr_len = s.arr_len;
       r.images = s.images;
-      if (r.status == codec::OK && r.images > cfg_.max_batch) r.status = codec::TOO_LARGE;
       if (r.status == codec::OK && fault_hit(parse_error_p_)) r.status = codec::BAD_ENVELOPE;
     }
-    if (r.status == codec::OK) {
+    if (r.status == codec::OK && r.images > cfg_.max_batch) {
+      images_in_ += r.images;
+      if (!split_record(r, good)) emit_error(r, codec::BAD_SHAPE, prod);
+    } else if (r.status == codec::OK) {
       images_in_ += r.images;
       good.push_back(std::move(r));
     } else {
@@ -1171,13 +1209,13 @@ void Engine::finish_batch(ReplicaSlot* rs, Batch& b) {
   kafka::Producer* prod = producer_for(rs->index);
   const bool js = cfg_.value_format == "json-string";
   const bool java8 = cfg_.float_format == "java8";
-  auto encode_ok = [&](const InRecord& r, int img, std::string& out) {
+  auto encode_ok = [&](const InRecord& r, int img, std::string& out, bool jstr) {
     if (b.pred_text)
       codec::encode_predictions_text(b.pred_text + (size_t)img * cfg_.classes * 16, r.images,
-                                     cfg_.classes, js, out);
+                                     cfg_.classes, jstr, out);
     else
-      codec::encode_predictions(b.probs + (size_t)img * cfg_.classes, r.images, cfg_.classes, js,
-                                out, java8);
+      codec::encode_predictions(b.probs + (size_t)img * cfg_.classes, r.images, cfg_.classes,
+                                jstr, out, java8);
   };
   int img = 0;
   std::string out;
@@ -1197,6 +1235,16 @@ void Engine::finish_batch(ReplicaSlot* rs, Batch& b) {
   for (size_t i = 0; i < b.recs.size(); ++i) {
     InRecord& r = b.recs[i];
     if (r.status == codec::OK && i < b.dev_status.size()) r.status = b.dev_status[i];
+    if (r.split) {  // a fragment of an oversized record: its rows join the others'
+      std::string rows;
+      if (r.status == codec::OK) {
+        encode_ok(r, img, out, false);
+        rows.assign(out, 16, out.size() - 18);  // {"predictions":[ rows ]}
+      }
+      fragment_done(r, std::move(rows), r.status, prod);
+      img += r.images;
+      continue;
+    }
     InRecord meta;
     meta.partition = r.partition;
     meta.offset = r.offset;
@@ -1208,7 +1256,7 @@ void Engine::finish_batch(ReplicaSlot* rs, Batch& b) {
     bool null_value = false;
     if (r.status != codec::OK) {
       ++errors_;
-      err_by_status_[r.status & 7]++;
+      err_by_status_[r.status & 15]++;
       if (cfg_.on_error == "drop") {
         ++dropped_;
         complete_record(meta, true);
@@ -1222,7 +1270,7 @@ void Engine::finish_batch(ReplicaSlot* rs, Batch& b) {
         g.values += out;
       }
     } else {
-      encode_ok(r, img, out);
+      encode_ok(r, img, out, js);
       g.values += out;
     }
     img += r.images;
@@ -1395,9 +1443,96 @@ void Engine::emit(InRecord& r, std::string value, bool null_value, kafka::Produc
   if (ff) complete_record(meta, true);  // KafkaBolt fire-and-forget acks immediately
 }
 
+bool Engine::split_record(InRecord& r, std::vector<InRecord>& good) {
+  std::vector<std::pair<uint32_t, uint32_t>> spans;
+  const uint8_t* arr = r.value + r.arr_off;
+  if (!codec::split_instances(arr, (size_t)r.arr_len, spans) || (int)spans.size() != r.images)
+    return false;
+  const int mb = cfg_.max_batch;
+  const int parts = (r.images + mb - 1) / mb;
+  auto sp = std::make_shared<SplitRecord>();
+  sp->parent = r;
+  sp->parent.buf.reset();
+  sp->parent.value = nullptr;
+  sp->parent.dev_value = nullptr;
+  if (r.key && r.key_len >= 0) {
+    sp->key.assign(reinterpret_cast<const char*>(r.key), (size_t)r.key_len);
+    sp->parent.key = reinterpret_cast<const uint8_t*>(sp->key.data());
+  }
+  sp->parts = parts;
+  sp->rows.resize((size_t)parts);
+  for (int k = 0; k < parts; ++k) {
+    const int i0 = k * mb, i1 = std::min(r.images, i0 + mb);
+    const size_t b = spans[(size_t)i0].first, e = spans[(size_t)i1 - 1].second;
+    // a complete InstObj of its own: {"instances":[ images ]}
+    static const char kHead[] = "{\"instances\":[";
+    const size_t hl = sizeof(kHead) - 1;
+    const size_t n = hl + (e - b) + 2;
+    std::shared_ptr<uint8_t> buf = kafka::heap_alloc(n);
+    memcpy(buf.get(), kHead, hl);
+    memcpy(buf.get() + hl, arr + b, e - b);
+    buf.get()[n - 2] = ']';
+    buf.get()[n - 1] = '}';
+    InRecord f;
+    f.buf = std::move(buf);
+    f.value = f.buf.get();
+    f.len = (int32_t)n;
+    f.arr_off = (int64_t)hl - 1;
+    f.arr_len = (int64_t)(e - b) + 2;
+    f.images = i1 - i0;
+    f.status = codec::OK;
+    f.partition = r.partition;
+    f.offset = r.offset;
+    f.timestamp_ms = r.timestamp_ms;
+    f.t_fetch_ns = r.t_fetch_ns;
+    f.source = r.source;
+    f.split = sp;
+    f.split_index = k;
+    good.push_back(std::move(f));
+  }
+  ++split_records_;
+  split_fragments_ += parts;
+  return true;
+}
+
+void Engine::fragment_done(const InRecord& frag, std::string rows, int status,
+                           kafka::Producer* prod) {
+  SplitRecord& sp = *frag.split;
+  {
+    std::lock_guard<std::mutex> lk(sp.mu);
+    if (status != codec::OK && sp.status == codec::OK) sp.status = status;
+    sp.rows[(size_t)frag.split_index] = std::move(rows);
+    if (++sp.done < sp.parts) return;
+  }
+  // the last fragment: one output record for the input record, rows in image order
+  if (sp.status != codec::OK) {
+    emit_error(sp.parent, sp.status, prod);
+    return;
+  }
+  const bool js = cfg_.value_format == "json-string";
+  const char* q = js ? "\\\"" : "\"";
+  size_t total = 32;
+  for (const std::string& x : sp.rows) total += x.size() + 1;
+  std::string v;
+  v.reserve(total);
+  if (js) v.push_back('"');
+  v += '{';
+  v += q;
+  v += "predictions";
+  v += q;
+  v += ":[";
+  for (size_t k = 0; k < sp.rows.size(); ++k) {
+    if (k) v.push_back(',');
+    v += sp.rows[k];
+  }
+  v += "]}";
+  if (js) v.push_back('"');
+  emit(sp.parent, std::move(v), false, prod);
+}
+
 void Engine::emit_error(InRecord& r, int status, kafka::Producer* prod) {
   ++errors_;
-  err_by_status_[status & 7]++;
+  err_by_status_[status & 15]++;
   if (cfg_.on_error == "drop") {
     ++dropped_;
     InRecord meta = r;
@@ -1433,6 +1568,11 @@ std::map<std::string, double> Engine::stats() const {
   s["replica_failures"] = (double)replica_failures_;
   s["replica_restarts"] = (double)replica_restarts_;
   s["commits"] = (double)commits_;
+  s["converted_batches"] = (double)converted_batches_;
+  s["poison_batches"] = (double)poison_batches_;
+  s["poison_records"] = (double)poison_records_;
+  s["split_records"] = (double)split_records_;
+  s["split_fragments"] = (double)split_fragments_;
   {
     int64_t lag = 0, fetch_lag = 0, lag_max = 0;
     for (const PartitionOffsets& o : partition_offsets()) {
@@ -1450,7 +1590,7 @@ std::map<std::string, double> Engine::stats() const {
   s["queue_records"] = (double)queued;
   s["locality_slots"] = (double)batchers_.size();
   s["steals"] = (double)steals_;
-  for (int i = 1; i < 8; ++i)
+  for (int i = 1; i < codec::kStatusCount; ++i)
     s[std::string("err_") + codec::status_name(i)] = (double)err_by_status_[i];
   const double el = (double)(t_last_ns_ - t_first_ns_) * 1e-9;
   s["elapsed_s"] = el > 0 ? el : 0;

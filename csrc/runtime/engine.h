@@ -31,6 +31,7 @@
 #include <memory>
 #include <mutex>
 #include <random>
+#include <set>
 #include <string>
 #include <thread>
 #include <vector>
@@ -92,6 +93,7 @@ struct EngineConfig {
   std::string sink_mode = "async"; // async | sync | fire-and-forget (KafkaBolt.java:186-197)
   int linger_ms = 0;
   int batch_size = 1 << 20;
+  std::string compression = "none";  // sink compression.type (kafka/compress.h codecs)
   std::string value_format = "json";  // json | json-string (spring JsonSerializer, E8)
   // prediction digits: "jdk19" (shortest, also on the GPU) | "java8" (the reference runtime's
   // Float.toString, host-formatted; codec::format_float_java8)
@@ -155,6 +157,75 @@ struct PartitionOffsets {
   int64_t high_watermark = -1, fetched = -1, committed = -1;
   int64_t lag = 0;        // high_watermark - committed
   int64_t fetch_lag = 0;  // high_watermark - fetched
+};
+
+// Offsets fetched but not yet acknowledged downstream, per partition: a sliding window over
+// the offsets (one byte per offset from the oldest pending one), so registering a fetched
+// record and completing it are O(1) instead of a tree insert / erase per record. The window
+// spans at most kMaxSpan offsets: an offset further away (a forward seek past records still
+// pending, a record that is never acknowledged while the log moves on) goes to a sparse set,
+// and the window re-bases onto the set once it drains - the span, and the memory, stay bounded.
+struct OffsetWindow {
+  static constexpr int64_t kMaxSpan = 1 << 22;
+  int64_t base = 0;          // offset of st[0]
+  std::deque<uint8_t> st;    // 1 = pending; the front is pending whenever npending > 0
+  int64_t npending = 0;
+  std::set<int64_t> sparse;  // pending offsets outside the window
+  void add(int64_t off) {
+    if (npending == 0 && sparse.empty()) {
+      st.clear();
+      base = off;
+    }
+    if (off < base) {
+      if (base - off > kMaxSpan || (int64_t)st.size() + (base - off) > kMaxSpan) {
+        sparse.insert(off);
+        return;
+      }
+      st.insert(st.begin(), (size_t)(base - off), 0);  // (a seek back re-fetched them)
+      base = off;
+    }
+    if (off - base >= kMaxSpan) {
+      sparse.insert(off);
+      return;
+    }
+    const size_t i = (size_t)(off - base);
+    if (i >= st.size()) st.resize(i + 1, 0);
+    if (!st[i]) {
+      st[i] = 1;
+      ++npending;
+    }
+  }
+  void done(int64_t off) {
+    if (off < base || (size_t)(off - base) >= st.size()) {
+      sparse.erase(off);
+    } else {
+      uint8_t& f = st[(size_t)(off - base)];
+      if (!f) return;
+      f = 0;
+      --npending;
+      while (!st.empty() && st.front() == 0) {
+        st.pop_front();
+        ++base;
+      }
+    }
+    if (npending == 0 && !sparse.empty()) {  // re-base the window onto the sparse offsets
+      st.clear();
+      base = *sparse.begin();
+      while (!sparse.empty() && *sparse.begin() - base < kMaxSpan) {
+        const int64_t o = *sparse.begin();
+        sparse.erase(sparse.begin());
+        const size_t i = (size_t)(o - base);
+        if (i >= st.size()) st.resize(i + 1, 0);
+        st[i] = 1;
+        ++npending;
+      }
+    }
+  }
+  bool empty() const { return npending == 0 && sparse.empty(); }
+  int64_t first() const {  // the oldest pending offset (when !empty())
+    if (npending == 0) return *sparse.begin();
+    return sparse.empty() ? base : std::min(base, *sparse.begin());
+  }
 };
 
 class Engine {
@@ -226,6 +297,10 @@ class Engine {
   void slo_step();
   void finish_batch(ReplicaSlot* rs, Batch& b);
   void emit(InRecord& r, std::string value, bool null_value, kafka::Producer* prod);
+  // an oversized record -> fragments of <= max_batch images appended to `good` (false: the
+  // array could not be split; the record keeps its status for the error policy)
+  bool split_record(InRecord& r, std::vector<InRecord>& good);
+  void fragment_done(const InRecord& frag, std::string rows, int status, kafka::Producer* prod);
   void emit_error(InRecord& r, int status, kafka::Producer* prod);
   void complete_record(const InRecord& r, bool ok);
   void complete_records(const std::vector<InRecord>& rs, bool ok);
@@ -262,41 +337,6 @@ class Engine {
   std::atomic<int> sources_active_{0};
 
   std::mutex pend_mu_;
-  // Offsets fetched but not yet acknowledged downstream, per partition: a sliding window over
-  // the offsets (one byte per offset from the oldest pending one), so registering a fetched
-  // record and completing it are O(1) instead of a tree insert / erase per record.
-  struct OffsetWindow {
-    int64_t base = 0;          // offset of st[0]
-    std::deque<uint8_t> st;    // 1 = pending; the front is pending whenever npending > 0
-    int64_t npending = 0;
-    void add(int64_t off) {
-      if (st.empty()) {
-        base = off;
-      } else if (off < base) {  // (a seek back re-fetched older offsets)
-        st.insert(st.begin(), (size_t)(base - off), 0);
-        base = off;
-      }
-      const size_t i = (size_t)(off - base);
-      if (i >= st.size()) st.resize(i + 1, 0);
-      if (!st[i]) {
-        st[i] = 1;
-        ++npending;
-      }
-    }
-    void done(int64_t off) {
-      if (off < base || (size_t)(off - base) >= st.size()) return;
-      uint8_t& f = st[(size_t)(off - base)];
-      if (!f) return;
-      f = 0;
-      --npending;
-      while (!st.empty() && st.front() == 0) {
-        st.pop_front();
-        ++base;
-      }
-    }
-    bool empty() const { return npending == 0; }
-    int64_t first() const { return base; }  // the oldest pending offset (when !empty())
-  };
   std::map<int, OffsetWindow> pending_;  // partition -> fetched, unacknowledged offsets
   std::map<int, int64_t> next_fetch_;              // partition -> next offset to fetch
   std::map<int, int64_t> high_watermark_;          // partition -> log end (last fetch response)
@@ -317,7 +357,9 @@ class Engine {
   std::atomic<int64_t> records_in_{0}, images_in_{0}, records_out_{0}, images_out_{0};
   std::atomic<int64_t> bytes_in_{0}, errors_{0}, produce_failures_{0}, dropped_{0};
   std::atomic<int64_t> requeued_{0}, replica_failures_{0}, replica_restarts_{0}, commits_{0};
-  std::atomic<int64_t> err_by_status_[8] = {};
+  std::atomic<int64_t> err_by_status_[16] = {};
+  std::atomic<int64_t> converted_batches_{0}, poison_batches_{0}, poison_records_{0};
+  std::atomic<int64_t> split_records_{0}, split_fragments_{0};
   Histogram h_queue_us_, h_device_us_, h_engine_e2e_us_, h_record_e2e_ms_, h_batch_images_;
   Histogram h_slo_win_us_;  // e2e latency of the SLO controller's current window
   Histogram h_slo_batch_;   // batch sizes (images) of the SLO controller's current window

@@ -20,6 +20,12 @@
 
 namespace gale {
 
+struct InRecord;
+// A record with more images than one micro-batch holds (InstObj N > max_batch): it is served as
+// consecutive fragments of <= max_batch images, each a record of its own in the batcher, and the
+// prediction rows are joined back into ONE {"predictions": [...]} record for the input offset.
+struct SplitRecord;
+
 struct InRecord {
   std::shared_ptr<uint8_t> buf;  // keeps the fetch buffer alive
   const uint8_t* value = nullptr;
@@ -40,6 +46,9 @@ struct InRecord {
   // the fetch pool of locality slot dev_locality (its key: the device, or the split slot)
   const uint8_t* dev_value = nullptr;
   int32_t dev_locality = -1;
+  // fragment `split_index` of an oversized record (null for ordinary records)
+  std::shared_ptr<SplitRecord> split;
+  int32_t split_index = -1;
 };
 
 struct Batch {

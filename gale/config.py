@@ -25,6 +25,7 @@ CHOICES = {
     "output_key": ("none", "input"),
     "float_format": ("jdk19", "java8"),
     "assignor": ("range", "roundrobin", "load-aware"),
+    "compression": ("none", "gzip", "snappy", "lz4", "zstd"),
     # compute dtype of the GPU kernels (MFMA bf16 / OCP e4m3 fp8 serving plans; fp32 = the
     # reference-precision plan on the fp32 matrix core, every tensor binary32 like the
     # reference's TF graph, InferenceBolt.java:80-86); inputs and the softmax output are fp32
@@ -90,6 +91,9 @@ class GaleConfig:
     value_format: str = "json"         # json-string = spring JsonSerializer double encoding
     type_id_header: bool = False       # add __TypeId__: java.lang.String (spring JsonSerializer)
     linger_ms: int = 0
+    compression: str = "none"          # sink compression.type: none | gzip | snappy | lz4 | zstd
+                                       # (kafka-clients default none; the input side decodes
+                                       # every codec and the old message formats regardless)
     on_error: str = "null"             # reference: malformed input -> null record
     output_key: str = "none"           # reference: unkeyed output (E9); "input" = input's key
     float_format: str = "jdk19"        # prediction digits: jdk19 = shortest round-trip (GPU
@@ -190,6 +194,7 @@ class GaleConfig:
             decode_threads=self.decode_threads, check_crcs=self.check_crcs,
             text_pack=bool(self.gpu_ingest and self.text_pack and _pack_fast()),
             acks=self.acks, sink_mode=self.sink_mode, linger_ms=self.linger_ms,
+            compression=self.compression,
             value_format=self.value_format, type_id_header=self.type_id_header,
             on_error=self.on_error, output_key=self.output_key, float_format=self.float_format,
             output_partition=self.output_partition,

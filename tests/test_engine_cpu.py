@@ -245,7 +245,7 @@ def test_corrupt_batch_crc_marks_its_records(broker):
     vals = [r["value"] for r in out]
     assert sum(b"predictions" in v for v in vals) == 3
     errs = [json.loads(v)["error"] for v in vals if b"predictions" not in v]
-    assert errs == ["bad_envelope"] * 3
+    assert errs == ["corrupt"] * 3
 
 
 def test_output_key_input_correlates_every_record(broker):
@@ -392,3 +392,42 @@ def test_output_partition_pins_every_output_record():
     with pytest.raises(ValueError):
         GaleConfig(topology_name="t", input_topic="in", output_topic="out",
                    output_partition=-2).validate()
+
+
+@pytest.mark.parametrize("value_format", ["json", "json-string"])
+def test_record_larger_than_max_batch_is_split_and_reassembled(broker, value_format):
+    """InstObj N > max_batch (InstObj.java:8 float[N][H][W][C]; SURVEY §2.3 P7 keeps per-message
+    N >= 1): the record is served as fragments of <= max_batch images on consecutive
+    micro-batches and ONE {"predictions": [N rows]} record comes back, rows in image order."""
+    rng = np.random.default_rng(11)
+    small1 = rng.random((2, H, W, CH), dtype=np.float32)
+    big = rng.random((40, H, W, CH), dtype=np.float32)  # max_batch 16 -> 3 fragments
+    small2 = rng.random((1, H, W, CH), dtype=np.float32)
+    broker.append("in", 0, [C.encode_instances(x) for x in (small1, big, small2)],
+                  [b"s1", b"big", b"s2"])
+    eng, out = run(broker, 3, output_key="input", value_format=value_format)
+    assert len(out) == 3
+    by_key = {}
+    for r in out:
+        v = json.loads(r["value"])
+        by_key[r["key"]] = json.loads(v) if value_format == "json-string" else v
+    for k, x in ((b"s1", small1), (b"big", big), (b"s2", small2)):
+        got = np.array(by_key[k]["predictions"])
+        assert got.shape == (len(x), CLASSES)
+        np.testing.assert_allclose(got, stub_probs(x), rtol=1e-5, atol=1e-6)
+    st = eng.stats()
+    assert st["split_records"] == 1 and st["split_fragments"] == 3
+    assert st["errors"] == 0 and st["images_out"] == 43
+
+
+def test_split_record_with_a_bad_fragment_is_one_error(broker):
+    """A malformed image inside an oversized record: the whole record gets the error policy
+    once (one output for the one input), not one per fragment."""
+    rng = np.random.default_rng(12)
+    txt = C.encode_instances(rng.random((20, H, W, CH), dtype=np.float32))
+    k = txt.index(b",", len(txt) * 3 // 4)
+    bad = txt[:k] + b",x" + txt[k + 1:]  # a non-number in the last fragment
+    broker.append("in", 0, [bad], [b"big"])
+    eng, out = run(broker, 1, output_key="input", on_error="error-json")
+    assert len(out) == 1 and json.loads(out[0]["value"])["error"] in ("bad_number", "bad_shape")
+    assert eng.stats()["errors"] == 1

@@ -276,7 +276,7 @@ def test_gpu_ingest_rejects_corrupt_batch_and_counts_images(broker):
     vals = [r["value"] for r in out]
     assert sum(b"predictions" in v for v in vals) == 3
     assert [json.loads(v)["error"] for v in vals if b"predictions" not in v] == \
-        ["bad_envelope"] * 3
+        ["corrupt"] * 3
     st = eng.stats()
     assert st["ingested_records"] == 6 and st["images_out"] == 6
 
@@ -354,3 +354,37 @@ def test_gpu_locality_split_steals_parse_from_host_pinned():
         got = centered_log(json.loads(r["value"])["predictions"])[0]
         worst = max(worst, np.abs(got - ref[i]).max() / max(np.abs(ref[i]).max(), 1.0))
     assert worst < 2e-2, worst
+
+
+@pytest.mark.parametrize("ingest", [True, False])
+def test_gpu_engine_record_over_max_batch(broker, ingest):
+    """A 300-image CIFAR record between small ones (max_batch 128): split over consecutive
+    micro-batches on the GPU replicas and reassembled into ONE prediction record, every row
+    matched to the fp32 oracle in image order; no TOO_LARGE."""
+    net = get_model("resnet20")
+    params = init_params(net, seed=0, calib_batch=16)
+    rng = np.random.default_rng(7)
+    xs = {b"a": rng.random((3, 32, 32, 3), dtype=np.float32),
+          b"big": rng.random((300, 32, 32, 3), dtype=np.float32),
+          b"b": rng.random((1, 32, 32, 3), dtype=np.float32)}
+    for k, x in xs.items():
+        broker.append("in", 0, [C.encode_instances(x)], [k])
+    cfg = GaleConfig(topology_name="g", input_topic="in", output_topic="out",
+                     bootstrap=f"127.0.0.1:{broker.port}", start_offset="earliest",
+                     max_batch=128, max_wait_us=500, output_key="input", gpu_ingest=ingest)
+    eng = Engine(cfg, devices=[0], max_records=3, params=params)
+    eng.start()
+    assert eng.wait(120), eng.stats()
+    eng.stop()
+    out = {r["key"]: r["value"] for r in broker.read("out", 0)}
+    assert set(out) == set(xs)
+    folded = fold_params(net, params)
+    for k, x in xs.items():
+        ref = centered_log(forward(net, folded, torch.from_numpy(x)).numpy())
+        got = centered_log(json.loads(out[k])["predictions"])
+        assert got.shape == ref.shape, k
+        rel = np.abs(got - ref).max() / max(np.abs(ref).max(), 1.0)
+        assert rel < 2e-2, (k, rel)
+    st = eng.stats()
+    assert st["split_records"] == 1 and st["split_fragments"] == 3
+    assert st["errors"] == 0 and st["images_out"] == 304 and st["err_too_large"] == 0
