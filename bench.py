@@ -92,6 +92,9 @@ def parse_args(argv=None):
                     help="format the prediction text (Java Float.toString) on the GPU")
     ap.add_argument("--graph", action=argparse.BooleanOptionalAction, default=True,
                     help="replay each batch's forward as a captured hipGraph (else eager)")
+    ap.add_argument("--graph-step", action=argparse.BooleanOptionalAction, default=True,
+                    help="run each batch step (metadata H2D, parse, forward, format, status D2H) "
+                         "as one replay of a captured per-slot hipGraph (whole-network plans)")
     ap.add_argument("--gpu-ingest", action=argparse.BooleanOptionalAction, default=True,
                     help="CRC32C + image counting of fetch buffers on the GPU (host reads only "
                          "Kafka framing)")
@@ -654,7 +657,7 @@ def main(argv=None) -> int:
                      producer_buffer_mb=a.producer_buffer_mb,
                      locality_split=a.locality_split, fetch_min_bytes=a.fetch_min_bytes,
                      fetch_max_wait_ms=a.fetch_max_wait_ms, recv_lowat_kb=a.recv_lowat_kb,
-                     use_graph=a.graph,
+                     use_graph=a.graph, graph_step=a.graph_step,
                      producer_request_kb=a.producer_request_kb)
     devices = (list(range(local_gpus)) if local_gpus > 1 else [local_rank]) if use_gpu else None
     # ONE engine: warm-up and timed window are the same steady-state pipeline (connections,

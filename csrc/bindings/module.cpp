@@ -164,14 +164,18 @@ PYBIND11_MODULE(_C, m) {
         });
   m.def("json_parse_instances",
         [](int nrec, int ntiles, uintptr_t recs, uintptr_t tile_rec, uintptr_t bytes, int H,
-           int W, int C, uintptr_t tile_counts, uintptr_t out, uintptr_t stream) {
+           int W, int C, uintptr_t tile_counts, uintptr_t out, uintptr_t stream,
+           bool count_pass) {
           chk(gale::json_parse_instances(nrec, ntiles, static_cast<gale::JsonRecord*>(P(recs)),
                                          static_cast<const int*>(P(tile_rec)),
                                          static_cast<const uint8_t*>(P(bytes)), H, W, C,
                                          static_cast<int*>(P(tile_counts)),
-                                         static_cast<float*>(P(out)), S(stream)),
+                                         static_cast<float*>(P(out)), S(stream), count_pass),
               "json_parse_instances");
-        });
+        },
+        py::arg("nrec"), py::arg("ntiles"), py::arg("recs"), py::arg("tile_rec"),
+        py::arg("bytes"), py::arg("H"), py::arg("W"), py::arg("C"), py::arg("tile_counts"),
+        py::arg("out"), py::arg("stream"), py::arg("count_pass") = true);
   m.def("json_tile_count", &gale::json_tile_count);
   py::module_ comm = m.def_submodule("comm", "in-process RCCL communicator (ncclCommInitAll)");
   py::class_<gale::CommGroup, std::shared_ptr<gale::CommGroup>>(comm, "CommGroup")
@@ -208,6 +212,22 @@ PYBIND11_MODULE(_C, m) {
                                               reinterpret_cast<uint32_t*>(out),
                                               reinterpret_cast<hipStream_t>(stream)),
                           "crc32c_chunks");
+        });
+  m.def("ingest_crc_count",
+        [](uintptr_t bytes, uintptr_t chunks, int nchunks, uintptr_t tables, uintptr_t crc_out,
+           int nrec, int ntiles, uintptr_t recs, uintptr_t tile_rec, uintptr_t counts,
+           uintptr_t rec_tokens, uintptr_t stream) {
+          gale::check_hip(
+              gale::ingest_crc_count(reinterpret_cast<const uint8_t*>(bytes),
+                                     reinterpret_cast<const gale::CrcChunk*>(chunks), nchunks,
+                                     reinterpret_cast<const uint32_t*>(tables),
+                                     reinterpret_cast<uint32_t*>(crc_out), nrec, ntiles,
+                                     reinterpret_cast<gale::JsonRecord*>(recs),
+                                     reinterpret_cast<const int*>(tile_rec),
+                                     reinterpret_cast<int*>(counts),
+                                     reinterpret_cast<int*>(rec_tokens),
+                                     reinterpret_cast<hipStream_t>(stream)),
+              "ingest_crc_count");
         });
   m.def("json_count_records",
         [](int nrec, int ntiles, uintptr_t recs, uintptr_t tile_rec, uintptr_t bytes,

@@ -98,12 +98,19 @@ class Executor {
   void run_on(int batch, const void* in, void* out, hipStream_t stream);
   void capture_all(hipStream_t stream);  // pre-capture every (bucket, slot) graph
   int graphs_captured() const;
+  // Plans whose every op reads its image count from device memory (the whole-network kernels):
+  // launch_device_batch enqueues the forward of `slot` sized for max_batch images, the count
+  // taken from *d_batch when the kernels run - what a captured per-slot step graph replays
+  // for every batch size (GpuReplica step graphs).
+  bool device_batch_ok() const;
+  void launch_device_batch(int slot, const int* d_batch, hipStream_t stream);
 
  private:
-  void launch_all(int batch, void* const* bufs, hipStream_t stream);
+  void launch_all(int batch, void* const* bufs, hipStream_t stream,
+                  const int* d_batch = nullptr);
   // ops [begin, end) for images [c0, c0 + batch) of the buffers (c0 > 0: a chunk)
   void launch_ops(size_t begin, size_t end, int batch, void* const* bufs, hipStream_t stream,
-                  int c0 = 0);
+                  int c0 = 0, const int* d_batch = nullptr);
   int device_;
   PlanSpec spec_;
   std::vector<int> buckets_;

@@ -109,6 +109,9 @@ struct ResNet20Params {
   int fp8;
   const float* ws[19];
   float s_in[19], s_out[19], s_res[19];
+  // non-null: the image count is read from device memory at run time (images <= the `batch`
+  // the launch is sized for) - a captured step graph replays one launch for every batch size
+  const int* batch_dev;
 };
 hipError_t resnet20_fused_forward(const ResNet20Params& p, int batch, const float* x, float* out,
                                   hipStream_t stream);
@@ -128,6 +131,7 @@ struct LeNet5Params {
   const float* b4;
   const float* w5;
   const float* b5;
+  const int* batch_dev;  // as ResNet20Params::batch_dev
 };
 hipError_t lenet5_fused_forward(const LeNet5Params& p, int batch, const float* x, float* out,
                                 hipStream_t stream);
@@ -162,14 +166,24 @@ struct JsonRecord {
   int32_t images;   // images in this record (from the host '[' count)
   int32_t status;   // raised by the kernel
   int32_t tile0;    // first global tile of this record
-  int32_t pad_;
+  // 1: the record's per-tile token counts are already on the device at bytes + cnt_off (the GPU
+  // ingest pass counted them and left them in the fetch buffer's device mirror), so the parse
+  // skips its own counting pass over this record's text
+  int32_t has_cnt;
+  int64_t cnt_off;
+  int64_t pad_;
 };
+static_assert(sizeof(JsonRecord) == 48, "JsonRecord layout (host <-> device tables)");
 int json_tile_count(int64_t off, int32_t len);
 // tile_rec[t]: index of the record owning global tile t. tile_counts: device scratch of
 // >= ntiles ints.
+// count_pass = false: every record has_cnt (the counting kernel is not launched at all).
+// d_ntiles non-null: the kernels read the tile count from device memory (ntiles = the most the
+// launch is sized for; waves past the device count exit) - the captured step graph's form.
 hipError_t json_parse_instances(int nrec, int ntiles, JsonRecord* recs, const int* tile_rec,
                                 const uint8_t* bytes, int H, int W, int C, int* tile_counts,
-                                float* out, hipStream_t stream);
+                                float* out, hipStream_t stream, bool count_pass = true,
+                                const int* d_ntiles = nullptr);
 
 // Ingest pass over a Kafka fetch buffer already on the device: json_count_records counts the
 // number tokens of every record's instances array (rec_tokens[i] += tokens of record i, host
@@ -194,6 +208,14 @@ struct CrcChunk {
 hipError_t crc32c_chunks(const uint8_t* bytes, const CrcChunk* chunks, int n,
                          const uint32_t* tables, uint32_t* out, hipStream_t stream);
 
+// The GPU ingest pass of one fetch buffer in ONE launch: workgroups [0, crc blocks) fold the CRC
+// windows (crc32c_chunks), the rest count the records' number tokens (json_count_records,
+// tile_counts[t] = tokens of tile t, rec_tokens[i] += tokens of record i).
+hipError_t ingest_crc_count(const uint8_t* bytes, const CrcChunk* chunks, int nchunks,
+                            const uint32_t* tables, uint32_t* crc_out, int nrec, int ntiles,
+                            JsonRecord* recs, const int* tile_rec, int* tile_counts,
+                            int* rec_tokens, hipStream_t stream);
+
 // Expands a nibble-packed span (csrc/codec/text_pack.h: 64-byte blocks, per-2-KiB-group
 // {base offset, packed-block mask} pairs in tab) into out[0, n). out must be 16-byte aligned,
 // packed 8-byte aligned.
@@ -206,5 +228,8 @@ hipError_t text_unpack(const uint8_t* packed, const uint32_t* tab, int64_t n, ui
 // byte 15 (at most 14 characters).
 constexpr int kFloatTextSlot = 16;
 hipError_t format_floats_java(int n, const float* x, void* out16, hipStream_t stream);
+// n = (*d_count) * per values (n <= max_n, the launch size): the step graph's form
+hipError_t format_floats_java_dev(int max_n, const int* d_count, int per, const float* x,
+                                  void* out16, hipStream_t stream);
 
 }  // namespace gale

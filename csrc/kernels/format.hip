@@ -229,9 +229,11 @@ __device__ Text16 format_java(float v, int* len_out) {
   return t;
 }
 
-__global__ __launch_bounds__(256) void format_floats_kernel(int n, const float* __restrict__ x,
+__global__ __launch_bounds__(256) void format_floats_kernel(int n, const int* d_count, int per,
+                                                            const float* __restrict__ x,
                                                             uint4* __restrict__ out) {
   const int i = blockIdx.x * 256 + threadIdx.x;
+  if (d_count) n = min(n, *d_count * per);
   if (i >= n) return;
   int len = 0;
   Text16 t = format_java(x[i], &len);
@@ -245,7 +247,15 @@ __global__ __launch_bounds__(256) void format_floats_kernel(int n, const float* 
 hipError_t format_floats_java(int n, const float* x, void* out16, hipStream_t stream) {
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(format_floats_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
-                     stream, n, x, static_cast<uint4*>(out16));
+                     stream, n, nullptr, 1, x, static_cast<uint4*>(out16));
+  return hipGetLastError();
+}
+
+hipError_t format_floats_java_dev(int max_n, const int* d_count, int per, const float* x,
+                                  void* out16, hipStream_t stream) {
+  if (max_n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(format_floats_kernel, dim3((unsigned)((max_n + 255) / 256)), dim3(256), 0,
+                     stream, max_n, d_count, per, x, static_cast<uint4*>(out16));
   return hipGetLastError();
 }
 

@@ -13,61 +13,19 @@
 // bytes do not change a raw CRC, so a window shorter than 4 KiB simply leaves its first lanes
 // empty. Misaligned ends are folded byte by byte; everything else uses aligned dword loads.
 #include "common.cuh"
+#include "crc32c.cuh"
 #include "gale/kernels.h"
 
 namespace gale {
 namespace {
 
-constexpr int kCrcWaves = 4;
-constexpr int kTableWords = 1024 + 64;
-constexpr uint32_t kPoly = 0x82f63b78u;  // CRC-32C, reflected
-
-__device__ __forceinline__ uint32_t crc_byte(const uint32_t* T, uint32_t c, uint32_t b) {
-  return (c >> 8) ^ T[(c ^ b) & 0xffu];
-}
-
-__device__ __forceinline__ uint32_t crc_word(const uint32_t* T, uint32_t c, uint32_t w) {
-  const uint32_t x = c ^ w;  // byte 0 (first in the stream) is advanced the most
-  return T[768 + (x & 0xffu)] ^ T[512 + ((x >> 8) & 0xffu)] ^ T[256 + ((x >> 16) & 0xffu)] ^
-         T[x >> 24];
-}
-
-// a * b mod P, reflected domain (bit 31 = x^0): the host's poly_mulmod (csrc/kafka/wire.cpp)
-__device__ __forceinline__ uint32_t gf2_mulmod(uint32_t a, uint32_t b) {
-  uint32_t r = 0;
-#pragma unroll
-  for (int i = 0; i < 32; ++i) {
-    r ^= b & (0u - ((a >> (31 - i)) & 1u));
-    b = (b >> 1) ^ (kPoly & (0u - (b & 1u)));
-  }
-  return r;
-}
-
 __global__ __launch_bounds__(256) void crc32c_chunks_kernel(const uint8_t* bytes,
                                                             const CrcChunk* chunks, int n,
                                                             const uint32_t* tables,
                                                             uint32_t* out) {
-  __shared__ uint32_t T[kTableWords];
-  for (int i = threadIdx.x; i < kTableWords; i += blockDim.x) T[i] = tables[i];
-  __syncthreads();
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  for (int c = blockIdx.x * kCrcWaves + wave; c < n; c += gridDim.x * kCrcWaves) {
-    const CrcChunk ch = chunks[c];
-    const int64_t cs = ch.end - ch.len;
-    const int64_t wa = ch.end - (int64_t)64 * (64 - lane);  // this lane's piece [wa, wa + 64)
-    const int64_t hi = wa + 64;
-    int64_t q = wa > cs ? wa : cs;
-    uint32_t crc = 0;
-    if (q < hi) {
-      while (q < hi && (q & 3)) crc = crc_byte(T, crc, bytes[q++]);
-      for (; q + 4 <= hi; q += 4) crc = crc_word(T, crc, *reinterpret_cast<const uint32_t*>(bytes + q));
-      while (q < hi) crc = crc_byte(T, crc, bytes[q++]);
-    }
-    crc = gf2_mulmod(crc, T[1024 + lane]);  // over the 64 * (63 - lane) bytes that follow
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) crc ^= __shfl_xor(crc, o, 64);
-    if (lane == 0) out[c] = crc;
-  }
+  __shared__ uint32_t T[crc::kTableWords];
+  crc::crc_stage_tables(tables, T);
+  crc::crc_windows(bytes, chunks, n, T, out, blockIdx.x, gridDim.x);
 }
 
 // Nibble-transport expansion (csrc/codec/text_pack.h): one thread per 16 output bytes, so a
@@ -128,9 +86,9 @@ hipError_t text_unpack(const uint8_t* packed, const uint32_t* tab, int64_t n, ui
 hipError_t crc32c_chunks(const uint8_t* bytes, const CrcChunk* chunks, int n,
                          const uint32_t* tables, uint32_t* out, hipStream_t stream) {
   if (n <= 0) return hipSuccess;
-  int blocks = (n + kCrcWaves - 1) / kCrcWaves;
+  int blocks = (n + crc::kCrcWaves - 1) / crc::kCrcWaves;
   if (blocks > 1024) blocks = 1024;  // waves loop: the 28 KB table load is amortised
-  hipLaunchKernelGGL(crc32c_chunks_kernel, dim3(blocks), dim3(64 * kCrcWaves), 0, stream, bytes,
+  hipLaunchKernelGGL(crc32c_chunks_kernel, dim3(blocks), dim3(64 * crc::kCrcWaves), 0, stream, bytes,
                      chunks, n, tables, out);
   return hipGetLastError();
 }

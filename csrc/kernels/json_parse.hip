@@ -33,6 +33,7 @@
 // Each record's bytes start 16-byte aligned; the buffer must be readable 16 bytes past the last
 // record. Positions below are record-relative: 0 = the record's 16-byte-aligned start.
 #include "common.cuh"
+#include "crc32c.cuh"
 #include "gale/kernels.h"
 #include "exact_decimal.cuh"
 
@@ -580,14 +581,15 @@ __device__ __forceinline__ bool gap_window(const uint8_t* text, int x, int k) {
   return prev - '0' < 10u;
 }
 
-__global__ __launch_bounds__(256) void json_count_kernel(JsonRecord* recs, const int* tile_rec,
-                                                         int ntiles, const uint8_t* bytes,
-                                                         int* counts, int* rec_tokens) {
+// Tokens of global tile t (one wave): counts[t], rec_tokens[record] += (ingest), invalid bytes
+// raise the record's status to 2. A record whose counts the ingest pass already left on the
+// device (has_cnt) is skipped by the parse's counting pass.
+__device__ __forceinline__ void count_tile(JsonRecord* recs, const int* tile_rec, int t,
+                                           const uint8_t* bytes, int* counts, int* rec_tokens) {
   const int lane = threadIdx.x & 63;
-  const int t = blockIdx.x * kWaves + (threadIdx.x >> 6);
-  if (t >= ntiles) return;  // (no workgroup barriers in this kernel)
   const int ri = tile_rec[t];
   const JsonRecord r = recs[ri];
+  if (!rec_tokens && r.has_cnt) return;
   const int64_t abeg = r.off & ~(int64_t)15;
   const uint8_t* rb = bytes + abeg;
   const int beg = (int)(r.off - abeg), end = beg + r.len;
@@ -614,15 +616,43 @@ __global__ __launch_bounds__(256) void json_count_kernel(JsonRecord* recs, const
   if (bad) atomicMax(&recs[ri].status, 2);
 }
 
+__global__ __launch_bounds__(256) void json_count_kernel(JsonRecord* recs, const int* tile_rec,
+                                                         int ntiles, const uint8_t* bytes,
+                                                         int* counts, int* rec_tokens,
+                                                         const int* d_ntiles) {
+  const int t = blockIdx.x * kWaves + (threadIdx.x >> 6);
+  if (d_ntiles) ntiles = min(ntiles, *d_ntiles);
+  if (t >= ntiles) return;  // (no workgroup barriers in this kernel)
+  count_tile(recs, tile_rec, t, bytes, counts, rec_tokens);
+}
+
+// The ingest pass of a fetch buffer in one launch: CRC window workgroups first (they stage the
+// CRC tables in LDS behind one barrier; the branch is uniform per workgroup), then counting.
+__global__ __launch_bounds__(256) void ingest_crc_count_kernel(
+    const uint8_t* bytes, const CrcChunk* chunks, int nchunks, const uint32_t* tables,
+    uint32_t* crc_out, int crc_blocks, JsonRecord* recs, const int* tile_rec, int ntiles,
+    int* counts, int* rec_tokens) {
+  if ((int)blockIdx.x < crc_blocks) {
+    __shared__ uint32_t T[crc::kTableWords];
+    crc::crc_stage_tables(tables, T);
+    crc::crc_windows(bytes, chunks, nchunks, T, crc_out, blockIdx.x, crc_blocks);
+    return;
+  }
+  const int t = ((int)blockIdx.x - crc_blocks) * kWaves + (threadIdx.x >> 6);
+  if (t >= ntiles) return;
+  count_tile(recs, tile_rec, t, bytes, counts, rec_tokens);
+}
+
 __global__ __launch_bounds__(256) void json_parse_kernel(JsonRecord* recs, const int* tile_rec,
                                                          int ntiles, const uint8_t* bytes, int H,
                                                          int W, int C, const int* counts,
-                                                         float* out) {
+                                                         float* out, const int* d_ntiles) {
   __shared__ __attribute__((aligned(16))) uint8_t lds_text[kWaves][kText];
   __shared__ uint16_t lds_tok[kWaves][kMaxTok];
   __shared__ uint32_t lds_cm[kWaves][kTile / 16 + 1];  // packed masks of the tile's chunks + 1
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int t = blockIdx.x * kWaves + wave;
+  if (d_ntiles) ntiles = min(ntiles, *d_ntiles);
   if (t >= ntiles) return;  // (waves only share LDS regions of their own: no barriers)
   uint8_t* text = lds_text[wave];
   uint16_t* tok = lds_tok[wave];
@@ -651,7 +681,12 @@ __global__ __launch_bounds__(256) void json_parse_kernel(JsonRecord* recs, const
 
   // first element index of this tile: the token counts of the record's earlier tiles
   int part = 0;
-  for (int k = r.tile0 + lane; k < t; k += 64) part += counts[k];
+  if (r.has_cnt) {  // counted by the ingest pass, left next to the fetch buffer's device mirror
+    const int* rc = reinterpret_cast<const int*>(bytes + r.cnt_off);
+    for (int k = lane; k < tl; k += 64) part += rc[k];
+  } else {
+    for (int k = r.tile0 + lane; k < t; k += 64) part += counts[k];
+  }
   const int base = wave_sum_i(part);
   wave_lds_sync();
 
@@ -744,7 +779,7 @@ hipError_t json_count_records(int nrec, int ntiles, JsonRecord* recs, const int*
   if (nrec <= 0 || ntiles <= 0) return hipSuccess;
   const int blocks = (ntiles + kWaves - 1) / kWaves;
   hipLaunchKernelGGL(json_count_kernel, dim3(blocks), dim3(64 * kWaves), 0, stream, recs,
-                     tile_rec, ntiles, bytes, tile_counts, rec_tokens);
+                     tile_rec, ntiles, bytes, tile_counts, rec_tokens, nullptr);
   return hipGetLastError();
 }
 
@@ -754,16 +789,33 @@ int json_tile_count(int64_t off, int32_t len) {
   return (int)((off + len - abeg + kJsonTileBytes - 1) / kJsonTileBytes);
 }
 
+hipError_t ingest_crc_count(const uint8_t* bytes, const CrcChunk* chunks, int nchunks,
+                            const uint32_t* tables, uint32_t* crc_out, int nrec, int ntiles,
+                            JsonRecord* recs, const int* tile_rec, int* tile_counts,
+                            int* rec_tokens, hipStream_t stream) {
+  if (nrec <= 0) ntiles = 0;
+  int crc_blocks = (nchunks + crc::kCrcWaves - 1) / crc::kCrcWaves;
+  if (crc_blocks > 1024) crc_blocks = 1024;  // (windows loop: the table load is amortised)
+  const int cnt_blocks = (ntiles + kWaves - 1) / kWaves;
+  if (crc_blocks + cnt_blocks == 0) return hipSuccess;
+  hipLaunchKernelGGL(ingest_crc_count_kernel, dim3(crc_blocks + cnt_blocks), dim3(256), 0, stream,
+                     bytes, chunks, nchunks, tables, crc_out, crc_blocks, recs, tile_rec, ntiles,
+                     tile_counts, rec_tokens);
+  return hipGetLastError();
+}
+
 hipError_t json_parse_instances(int nrec, int ntiles, JsonRecord* recs, const int* tile_rec,
                                 const uint8_t* bytes, int H, int W, int C, int* tile_counts,
-                                float* out, hipStream_t stream) {
+                                float* out, hipStream_t stream, bool count_pass,
+                                const int* d_ntiles) {
   if (nrec <= 0 || ntiles <= 0) return hipSuccess;
   if (H <= 0 || W <= 0 || C <= 0) return hipErrorInvalidValue;
   const int blocks = (ntiles + kWaves - 1) / kWaves;
-  hipLaunchKernelGGL(json_count_kernel, dim3(blocks), dim3(64 * kWaves), 0, stream, recs,
-                     tile_rec, ntiles, bytes, tile_counts, nullptr);
+  if (count_pass)
+    hipLaunchKernelGGL(json_count_kernel, dim3(blocks), dim3(64 * kWaves), 0, stream, recs,
+                       tile_rec, ntiles, bytes, tile_counts, nullptr, d_ntiles);
   hipLaunchKernelGGL(json_parse_kernel, dim3(blocks), dim3(64 * kWaves), 0, stream, recs,
-                     tile_rec, ntiles, bytes, H, W, C, tile_counts, out);
+                     tile_rec, ntiles, bytes, H, W, C, tile_counts, out, d_ntiles);
   return hipGetLastError();
 }
 

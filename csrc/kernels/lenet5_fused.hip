@@ -54,6 +54,7 @@ __global__ __launch_bounds__(kT) void lenet5_fused_kernel(LeNet5Params p, int n,
   __shared__ float s_w2[16 * 150], s_b2[16];  // [c][(ky*5 + kx)*6 + ci]
   const int t = threadIdx.x;
   const int img = blockIdx.x;
+  if (p.batch_dev && img >= *p.batch_dev) return;  // (uniform per workgroup, before any barrier)
   const bf16* w1 = static_cast<const bf16*>(p.w1);
   const bf16* w2 = static_cast<const bf16*>(p.w2);
   for (int i = t; i < 150; i += kT) s_w1[i] = (float)w1[(i / 25) * 32 + i % 25];

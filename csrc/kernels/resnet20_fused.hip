@@ -478,6 +478,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void resnet20_fused_kernel(ResNet2
   };
   const float in_q = F8 ? 1.f / p.s_in[0] : 1.f;  // quantisation of the fp32 network input
 
+  if (p.batch_dev) batch = min(batch, *p.batch_dev);  // (a captured step graph's batch size)
   for (int img = blockIdx.x; img < batch; img += gridDim.x) {
     __syncthreads();  // the previous image's head is done with R0/R1
     // ---- stage the fp32 input image into the zero-bordered 34x34x3 IN ----

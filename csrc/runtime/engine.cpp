@@ -838,7 +838,8 @@ bool Engine::ingest_fetch(FetchItem& it, std::vector<InRecord>& good, int lane) 
     io.arr_len[i] = s.arr_len;
   }
   try {
-    ingest->run(lane, f, dev, cfg_.check_crcs && !f.crc_checked, cfg_.H, cfg_.W, cfg_.C, io);
+    ingest->run(lane, f, dev, pools_[(size_t)it.slot]->chunk_bytes(),
+                cfg_.check_crcs && !f.crc_checked, cfg_.H, cfg_.W, cfg_.C, io);
   } catch (const std::exception& e) {
     if (!ingest_failed_.exchange(true))
       fprintf(stderr, "[gale decode] GPU ingest failed (%s): host decode from now on\n", e.what());
@@ -865,6 +866,7 @@ bool Engine::ingest_fetch(FetchItem& it, std::vector<InRecord>& good, int lane) 
     r.source = it.source;
     r.dev_value = dev + rr.value_off;
     r.dev_locality = slot_key_[(size_t)it.slot];
+    if (io.cnt_off[i] >= 0) r.dev_counts = dev + io.cnt_off[i];
     ++records_in_;
     if (r.len >= 0) bytes_in_ += r.len;
     r.status = corrupt[i] ? (int)codec::CORRUPT : io.status[i];
@@ -1617,6 +1619,15 @@ std::map<std::string, double> Engine::stats() const {
   s["assigned_partitions"] = cfg_.group_membership ? (double)assigned_partitions_
                                                    : (double)partition_offsets().size();
   s["ingested_records"] = (double)ingested_records_;
+  {
+    int64_t step = 0, fwd = 0;
+    for (auto& r : replicas_) {
+      step += r->rep->graph_step_batches();
+      fwd += r->rep->graph_forward_batches();
+    }
+    s["graph_step_batches"] = (double)step;
+    s["graph_forward_batches"] = (double)fwd;
+  }
   {
     int64_t text = 0, link = 0;
     for (auto& kv : ingests_) {

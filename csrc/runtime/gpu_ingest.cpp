@@ -77,12 +77,13 @@ namespace {
 size_t align16(size_t n) { return (n + 15) & ~(size_t)15; }
 }  // namespace
 
-void GpuIngest::run(int lane, const kafka::Fetched& f, uint8_t* dev, bool check_crcs, int H,
-                    int W, int C, IngestIO& io) {
+void GpuIngest::run(int lane, const kafka::Fetched& f, uint8_t* dev, size_t dev_cap,
+                    bool check_crcs, int H, int W, int C, IngestIO& io) {
   Lane& L = *lanes_[(size_t)lane % lanes_.size()];
   std::lock_guard<std::mutex> lk(L.mu);
   const size_t nrec_all = f.records.size();
   io.images.assign(nrec_all, 0);
+  io.cnt_off.assign(nrec_all, -1);
   io.batch_ok.assign(f.batches.size(), 1);
   // ---- plan: CRC windows (aligned to each batch's end) and the records to count
   std::vector<CrcChunk> chunks;
@@ -129,7 +130,7 @@ void GpuIngest::run(int lane, const kafka::Fetched& f, uint8_t* dev, bool check_
   const size_t o_chunks = align16(ng * 2 * sizeof(uint32_t));
   const size_t o_tiles = o_chunks + align16(nc * sizeof(CrcChunk));
   const size_t o_recs = o_tiles + align16((size_t)ntiles * sizeof(int));
-  const size_t o_tok = o_recs + nr * sizeof(JsonRecord);  // (JsonRecord is 32 bytes)
+  const size_t o_tok = o_recs + nr * sizeof(JsonRecord);  // (JsonRecord is 48 bytes)
   const size_t o_crc = o_tok + align16(nr * 4);
   const size_t io_bytes = o_crc + align16(nc * 4);
   check_hip(hipSetDevice(device_), "ingest: hipSetDevice");
@@ -148,6 +149,8 @@ void GpuIngest::run(int lane, const kafka::Fetched& f, uint8_t* dev, bool check_
     jr.images = 0;
     jr.status = 0;
     jr.tile0 = tile;
+    jr.has_cnt = 0;
+    jr.cnt_off = 0;
     jr.pad_ = 0;
     const int nt = json_tile_count(jr.off, jr.len);
     for (int t = 0; t < nt; ++t) ht[tile + t] = (int)j;
@@ -178,16 +181,24 @@ void GpuIngest::run(int lane, const kafka::Fetched& f, uint8_t* dev, bool check_
   uint32_t* d_crc = reinterpret_cast<uint32_t*>(L.d_io + o_crc);
   int* d_tok = reinterpret_cast<int*>(L.d_io + o_tok);
   JsonRecord* d_rec = reinterpret_cast<JsonRecord*>(L.d_io + o_recs);
-  if (nc)
-    check_hip(crc32c_chunks(dev, reinterpret_cast<const CrcChunk*>(L.d_io + o_chunks), (int)nc,
-                            d_tables_,
-                            d_crc, st),
-              "ingest: crc32c_chunks");
-  if (nr)
-    check_hip(json_count_records((int)nr, ntiles, d_rec,
-                                 reinterpret_cast<const int*>(L.d_io + o_tiles), dev, L.d_counts,
-                                 d_tok, st),
-              "ingest: json_count_records");
+  // the per-tile token counts stay with the fetch buffer: at the end of its device mirror when
+  // they fit behind the text (and the packed stream), so the replica that later parses these
+  // records reuses them instead of counting again
+  int* d_cnt = L.d_counts;
+  int64_t cnt_base = -1;
+  if (ntiles > 0) {
+    const size_t used = packed ? codec::pack_offset(span) + link : hi;
+    const size_t cb = ((size_t)ntiles * sizeof(int) + 255) & ~(size_t)255;
+    if (dev_cap > cb + 256 && ((dev_cap - cb) & ~(size_t)255) >= ((used + 64 + 255) & ~(size_t)255)) {
+      cnt_base = (int64_t)((dev_cap - cb) & ~(size_t)255);
+      d_cnt = reinterpret_cast<int*>(dev + cnt_base);
+    }
+  }
+  // CRC windows and token counts: one launch, one pass of workgroups over the buffer
+  check_hip(ingest_crc_count(dev, reinterpret_cast<const CrcChunk*>(L.d_io + o_chunks), (int)nc,
+                             d_tables_, d_crc, (int)nr, ntiles, d_rec,
+                             reinterpret_cast<const int*>(L.d_io + o_tiles), d_cnt, d_tok, st),
+            "ingest: crc32c + count");
   check_hip(hipMemcpyAsync(L.h_io + o_recs, L.d_io + o_recs, io_bytes - o_recs,
                            hipMemcpyDeviceToHost, st),
             "ingest: D2H results");
@@ -221,6 +232,7 @@ void GpuIngest::run(int lane, const kafka::Fetched& f, uint8_t* dev, bool check_
       io.status[i] = codec::BAD_SHAPE;
     } else {
       io.images[i] = (int32_t)(tok[j] / per);
+      if (cnt_base >= 0) io.cnt_off[i] = cnt_base + (int64_t)hr[j].tile0 * (int64_t)sizeof(int);
     }
   }
 }

@@ -20,8 +20,8 @@ class GpuIngest : public Ingest {
   GpuIngest(int device, int lanes, int poll_us);
   ~GpuIngest() override;
   int device() const override { return device_; }
-  void run(int lane, const kafka::Fetched& f, uint8_t* dev, bool check_crcs, int H, int W, int C,
-           IngestIO& io) override;
+  void run(int lane, const kafka::Fetched& f, uint8_t* dev, size_t dev_cap, bool check_crcs,
+           int H, int W, int C, IngestIO& io) override;
   void link_bytes(int64_t& text, int64_t& link) const override {
     text = text_bytes_.load();
     link = link_bytes_.load();

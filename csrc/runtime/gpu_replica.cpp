@@ -19,9 +19,11 @@ namespace gale {
 // ---------------------------------------------------------------------------------------------
 
 GpuReplica::GpuReplica(std::shared_ptr<Executor> exec, int H, int W, int C, int classes,
-                       bool use_graph, int wait_poll_us, bool gpu_encode, int locality)
+                       bool use_graph, int wait_poll_us, bool gpu_encode, int locality,
+                       bool step_graph)
     : exec_(std::move(exec)), H_(H), W_(W), C_(C), classes_(classes), use_graph_(use_graph),
       wait_poll_us_(wait_poll_us), gpu_encode_(gpu_encode), locality_(locality) {
+  step_graph_ = step_graph && use_graph && exec_->device_batch_ok();
   if (exec_->input_bytes_per_image() != (long long)H * W * C * 4)
     throw std::invalid_argument("GpuReplica: executor input is not fp32 [H, W, C]");
   if (exec_->output_bytes_per_image() != (long long)classes * 4)
@@ -51,10 +53,11 @@ GpuReplica::~GpuReplica() {
   hipSetDevice(exec_->device());
   if (stream_) hipStreamSynchronize(stream_);
   for (Slot& s : slots_) {
+    drop_steps(s);
     if (s.h_bytes) hipHostFree(s.h_bytes);
     if (s.d_bytes) hipFree(s.d_bytes);
-    if (s.h_recs) hipHostFree(s.h_recs);
-    if (s.d_recs) hipFree(s.d_recs);
+    if (s.h_hdr) hipHostFree(s.h_hdr);
+    if (s.d_hdr) hipFree(s.d_hdr);
     if (s.d_tiles) hipFree(s.d_tiles);
     if (s.h_out) hipHostFree(s.h_out);
     if (s.h_text) hipHostFree(s.h_text);
@@ -76,25 +79,38 @@ void GpuReplica::ensure_host(Slot& s, size_t bytes) {
   s.h_cap = cap;
 }
 
-// Per-slot parser metadata: [JsonRecord x max_batch][tile -> record index x tiles_cap], pinned
-// on the host and mirrored on the device (one H2D per batch), plus the per-tile token counts.
-// Growing keeps the first `keep` records already written into the host copy.
+void GpuReplica::drop_steps(Slot& s) {
+  for (hipGraphExec_t& g : s.step) {
+    if (g) hipGraphExecDestroy(g);
+    g = nullptr;
+  }
+}
+
+// Per-slot parser metadata: [header][JsonRecord x max_batch][tile -> record index x tiles_cap],
+// pinned on the host and mirrored on the device (one H2D per batch), plus the per-tile token
+// counts. Growing keeps the first `keep` records already written into the host copy.
 void GpuReplica::ensure_tiles(Slot& s, int ntiles, int keep) {
   if (ntiles <= s.tiles_cap) return;
   const int cap = std::max(ntiles, s.tiles_cap * 2);
   const size_t rec_bytes = sizeof(JsonRecord) * (size_t)exec_->max_batch();
-  const size_t bytes = rec_bytes + sizeof(int) * (size_t)cap;
-  if (s.h_recs) check_hip(hipEventSynchronize(s.done), "hipEventSynchronize");
-  JsonRecord* h = nullptr;
+  const size_t bytes = kMetaHdr + rec_bytes + sizeof(int) * (size_t)cap;
+  if (s.h_hdr) check_hip(hipEventSynchronize(s.done), "hipEventSynchronize");
+  uint8_t* h = nullptr;
   check_hip(hipHostMalloc(reinterpret_cast<void**>(&h), bytes), "hipHostMalloc(meta)");
-  if (s.h_recs) {
-    memcpy(h, s.h_recs, sizeof(JsonRecord) * (size_t)keep);
-    hipHostFree(s.h_recs);
-    hipFree(s.d_recs);
+  memset(h, 0, kMetaHdr);
+  if (s.h_hdr) {
+    memcpy(h + kMetaHdr, s.h_recs, sizeof(JsonRecord) * (size_t)keep);
+    drop_steps(s);
+    hipHostFree(s.h_hdr);
+    hipFree(s.d_hdr);
     hipFree(s.d_tiles);
   }
-  s.h_recs = h;
-  check_hip(hipMalloc(reinterpret_cast<void**>(&s.d_recs), bytes), "hipMalloc(meta)");
+  uint8_t* d = nullptr;
+  check_hip(hipMalloc(reinterpret_cast<void**>(&d), bytes), "hipMalloc(meta)");
+  s.h_hdr = reinterpret_cast<int32_t*>(h);
+  s.d_hdr = reinterpret_cast<int32_t*>(d);
+  s.h_recs = reinterpret_cast<JsonRecord*>(h + kMetaHdr);
+  s.d_recs = reinterpret_cast<JsonRecord*>(d + kMetaHdr);
   check_hip(hipMalloc(reinterpret_cast<void**>(&s.d_tiles), sizeof(int) * cap),
             "hipMalloc(tiles)");
   s.h_tile_rec = reinterpret_cast<int*>(reinterpret_cast<char*>(s.h_recs) + rec_bytes);
@@ -107,6 +123,7 @@ void GpuReplica::ensure_device(Slot& s, size_t bytes) {
   const size_t cap = (std::max(bytes, s.d_cap * 2) + 4095) & ~(size_t)4095;
   if (s.d_bytes) {
     check_hip(hipEventSynchronize(s.done), "hipEventSynchronize");
+    drop_steps(s);
     hipFree(s.d_bytes);
   }
   check_hip(hipMalloc(reinterpret_cast<void**>(&s.d_bytes), cap), "hipMalloc(bytes)");
@@ -171,6 +188,7 @@ void GpuReplica::submit(Batch& b) {
   const size_t staged_dev = doff;
   size_t hoff = 0;
   int nrec = 0, img = 0, ntiles = 0;
+  bool count_pass = false;
   for (const InRecord& r : b.recs) {
     JsonRecord& jr = s.h_recs[nrec++];
     const uint8_t* base = r.buf.get();
@@ -195,7 +213,15 @@ void GpuReplica::submit(Batch& b) {
     jr.images = r.images;
     jr.status = 0;
     jr.tile0 = ntiles;
+    jr.has_cnt = 0;
+    jr.cnt_off = 0;
     jr.pad_ = 0;
+    if (resident(r) && r.dev_counts) {  // counted by the ingest pass: no counting pass here
+      jr.has_cnt = 1;
+      jr.cnt_off = (int64_t)(r.dev_counts - s.d_bytes);
+    } else {
+      count_pass = true;
+    }
     ntiles += json_tile_count(jr.off, jr.len);
     img += r.images;
   }
@@ -217,15 +243,29 @@ void GpuReplica::submit(Batch& b) {
     check_hip(hipMemcpyAsync(s.d_bytes + staged_dev, s.h_bytes, hoff, hipMemcpyHostToDevice,
                              stream_),
               "H2D staged");
+  if (step_graph_) {
+    // ONE launch for the whole step: the captured graph copies the metadata (header included)
+    // and its kernels take the record / tile / image counts from the header
+    s.h_hdr[0] = nrec;
+    s.h_hdr[1] = ntiles;
+    s.h_hdr[2] = img;
+    hipGraphExec_t g = step_for(s, slot, count_pass);
+    check_hip(hipGraphLaunch(g, stream_), "hipGraphLaunch(step)");
+    ++step_batches_;
+    check_hip(hipEventRecord(s.done, stream_), "hipEventRecord");
+    s.t_submit_ns = mono_ns();
+    return;
+  }
   const size_t meta = reinterpret_cast<char*>(s.h_tile_rec + ntiles) -
                       reinterpret_cast<char*>(s.h_recs);
   check_hip(hipMemcpyAsync(s.d_recs, s.h_recs, meta, hipMemcpyHostToDevice, stream_),
             "H2D recs");
   check_hip(json_parse_instances(nrec, ntiles, s.d_recs, s.d_tile_rec, s.d_bytes, H_, W_, C_,
                                  s.d_tiles,
-                                 static_cast<float*>(exec_->input(slot)), stream_),
+                                 static_cast<float*>(exec_->input(slot)), stream_, count_pass),
             "json_parse_instances");
   exec_->run(slot, img, stream_, use_graph_);
+  if (use_graph_ && exec_->graph_pays()) ++fwd_graph_batches_;
   if (gpu_encode_) {
     // the prediction text (Java Float.toString per value) is formatted on the stream and comes
     // back instead of the probabilities, so the emitting thread only concatenates slots
@@ -244,6 +284,53 @@ void GpuReplica::submit(Batch& b) {
             "D2H status");
   check_hip(hipEventRecord(s.done, stream_), "hipEventRecord");
   s.t_submit_ns = mono_ns();
+}
+
+// The slot's step graph, captured on first use (and after its buffers moved). Sized for the
+// largest batch: the parse covers tiles_cap tiles and the forward max_batch images, their waves
+// past the header's counts exit at once; the status copy-back is max_batch records.
+hipGraphExec_t GpuReplica::step_for(Slot& s, int slot, bool count_pass) {
+  hipGraphExec_t& g = s.step[count_pass ? 1 : 0];
+  if (g) return g;
+  const int mb = exec_->max_batch();
+  const size_t meta = kMetaHdr + sizeof(JsonRecord) * (size_t)mb + sizeof(int) * s.tiles_cap;
+  // capture on a private stream (as Executor::run does), replayed on the replica's stream
+  hipStream_t cs = nullptr;
+  check_hip(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking), "capture stream");
+  hipGraph_t graph = nullptr;
+  hipError_t e = hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal);
+  if (e == hipSuccess) {
+    hipError_t c = hipMemcpyAsync(s.d_hdr, s.h_hdr, meta, hipMemcpyHostToDevice, cs);
+    if (c == hipSuccess)
+      c = json_parse_instances(mb, s.tiles_cap, s.d_recs, s.d_tile_rec, s.d_bytes, H_, W_, C_,
+                               s.d_tiles, static_cast<float*>(exec_->input(slot)), cs,
+                               count_pass, s.d_hdr + 1);
+    if (c == hipSuccess) {
+      try {
+        exec_->launch_device_batch(slot, s.d_hdr + 2, cs);
+      } catch (const std::exception&) {
+        c = hipErrorLaunchFailure;
+      }
+    }
+    if (c == hipSuccess)
+      c = gpu_encode_
+              ? format_floats_java_dev(mb * classes_, s.d_hdr + 2, classes_,
+                                       static_cast<const float*>(exec_->output(slot)), s.h_text,
+                                       cs)
+              : hipMemcpyAsync(s.h_out, exec_->output(slot), sizeof(float) * mb * classes_,
+                               hipMemcpyDeviceToHost, cs);
+    if (c == hipSuccess)
+      c = hipMemcpyAsync(s.h_recs, s.d_recs, sizeof(JsonRecord) * mb, hipMemcpyDeviceToHost, cs);
+    e = hipStreamEndCapture(cs, &graph);
+    if (e == hipSuccess) e = c;
+  }
+  hipStreamDestroy(cs);
+  if (e != hipSuccess && graph) hipGraphDestroy(graph);
+  check_hip(e, "step graph capture");
+  e = hipGraphInstantiate(&g, graph, nullptr, nullptr, 0);
+  hipGraphDestroy(graph);
+  check_hip(e, "step graph instantiate");
+  return g;
 }
 
 void GpuReplica::wait(Batch& b) {

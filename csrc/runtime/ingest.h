@@ -23,6 +23,9 @@ struct IngestIO {
   std::vector<int32_t> status;
   std::vector<int64_t> arr_off, arr_len;
   std::vector<int32_t> images;
+  // out: per record, where the device left its per-tile token counts (offset from the device
+  // mirror's base; -1: not kept) - the replica's parse then skips its own counting pass
+  std::vector<int64_t> cnt_off;
   // out: per Fetched::batches entry, false when its CRC32C did not match (check_crcs)
   std::vector<char> batch_ok;
 };
@@ -32,9 +35,9 @@ class Ingest {
   virtual ~Ingest() = default;
   virtual int device() const = 0;
   // lane: the calling decode thread (each lane owns its stream and staging buffers).
-  // dev: device mirror of f.buf (same offsets). Throws on a device error.
-  virtual void run(int lane, const kafka::Fetched& f, uint8_t* dev, bool check_crcs, int H, int W,
-                   int C, IngestIO& io) = 0;
+  // dev: device mirror of f.buf (same offsets), dev_cap bytes. Throws on a device error.
+  virtual void run(int lane, const kafka::Fetched& f, uint8_t* dev, size_t dev_cap,
+                   bool check_crcs, int H, int W, int C, IngestIO& io) = 0;
   // fetched text bytes staged so far, and the bytes that crossed the host link for them (less
   // when the text is nibble-packed, csrc/codec/text_pack.h)
   virtual void link_bytes(int64_t& text, int64_t& link) const { text = link = 0; }

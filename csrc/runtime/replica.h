@@ -46,6 +46,8 @@ struct InRecord {
   // the fetch pool of locality slot dev_locality (its key: the device, or the split slot)
   const uint8_t* dev_value = nullptr;
   int32_t dev_locality = -1;
+  // its per-tile token counts, left on the device by the ingest pass (null: none)
+  const uint8_t* dev_counts = nullptr;
   // fragment `split_index` of an oversized record (null for ordinary records)
   std::shared_ptr<SplitRecord> split;
   int32_t split_index = -1;
@@ -82,6 +84,10 @@ class Replica {
   // mirror of its own locality slot) vs. copied over the host link (pinned or staged)
   virtual int64_t resident_records() const { return 0; }
   virtual int64_t host_records() const { return 0; }
+  // batches run as ONE captured step graph (parse + forward + format + status) / with a
+  // graph-captured forward only (the rest launched directly)
+  virtual int64_t graph_step_batches() const { return 0; }
+  virtual int64_t graph_forward_batches() const { return 0; }
 };
 
 // CPU stub (SURVEY.md §4 "stub replica for plumbing tests on GPU-less hosts"): parses on the
@@ -121,8 +127,13 @@ class GpuReplica : public Replica {
   // slot - a steal - are not resident for this replica even on the same device: their text is
   // DMA'd from the host-pinned fetch buffer, as it would be across GPUs (--locality-split
   // exercises the multi-GPU dispatch on one device)
+  // step_graph: with use_graph and a whole-network plan (Executor::device_batch_ok), each batch
+  // is ONE hipGraphLaunch of the slot's captured step: metadata H2D -> JSON parse -> forward ->
+  // prediction text (or probabilities D2H) -> status D2H, the kernels reading the batch's record /
+  // tile / image counts from the metadata header, so one graph per slot serves every batch size
   GpuReplica(std::shared_ptr<Executor> exec, int H, int W, int C, int classes, bool use_graph,
-             int wait_poll_us = 0, bool gpu_encode = false, int locality = -1);
+             int wait_poll_us = 0, bool gpu_encode = false, int locality = -1,
+             bool step_graph = true);
   ~GpuReplica() override;
   std::string name() const override;
   int max_images() const override { return exec_->max_batch(); }
@@ -134,14 +145,21 @@ class GpuReplica : public Replica {
   void recover() override;
   int64_t resident_records() const override { return resident_; }
   int64_t host_records() const override { return host_; }
+  int64_t graph_step_batches() const override { return step_batches_; }
+  int64_t graph_forward_batches() const override { return fwd_graph_batches_; }
+  bool step_graph() const { return step_graph_; }
 
  private:
+  static constexpr size_t kMetaHdr = 64;  // [nrec, ntiles, images, ...] ahead of the records
   struct Slot {
     uint8_t* h_bytes = nullptr;  // pinned staging for records that arrived in pageable memory
     uint8_t* d_bytes = nullptr;  // device copy of the batch's JSON text
     size_t h_cap = 0, d_cap = 0;
+    int32_t* h_hdr = nullptr;      // metadata header (pinned) and its device mirror:
+    int32_t* d_hdr = nullptr;      // [kMetaHdr][records][tile map], one allocation each
     JsonRecord* h_recs = nullptr;  // [max_batch records][tile -> record map] (pinned)
     JsonRecord* d_recs = nullptr;  // device mirror
+    hipGraphExec_t step[2] = {nullptr, nullptr};  // captured steps (without / with count pass)
     int* h_tile_rec = nullptr;
     int* d_tile_rec = nullptr;
     int* d_tiles = nullptr;      // per-tile token counts (parser scratch)
@@ -154,6 +172,8 @@ class GpuReplica : public Replica {
   void ensure_host(Slot& s, size_t bytes);
   void ensure_device(Slot& s, size_t bytes);
   void ensure_tiles(Slot& s, int ntiles, int keep);
+  void drop_steps(Slot& s);  // (buffers moved: the captured steps point at the old ones)
+  hipGraphExec_t step_for(Slot& s, int slot, bool count_pass);
   std::shared_ptr<Executor> exec_;
   int H_, W_, C_, classes_;
   bool use_graph_;
@@ -169,6 +189,8 @@ class GpuReplica : public Replica {
   int next_slot_ = 0;
   int locality_ = -1;
   std::atomic<int64_t> resident_{0}, host_{0};
+  std::atomic<int64_t> step_batches_{0}, fwd_graph_batches_{0};
+  bool step_graph_ = false;
   int64_t expect_ns_ = 0;  // running average of submit -> done (adaptive sleep-poll)
 };
 

@@ -117,6 +117,9 @@ class GaleConfig:
     slo_p99_ms: float = 0.0            # latency-SLO mode (config 5): adapt batch/wait to a p99
     queue_depth: int = 8192
     use_graph: bool = True
+    graph_step: bool = True            # whole-network plans: each batch step (metadata H2D,
+                                       # parse, forward, format, status D2H) is ONE replay of a
+                                       # per-slot captured hipGraph (else launched op by op)
     gpu_wait_poll_us: int = 20         # > 0: replicas sleep-poll their batch events (0: spin)
     gpu_encode: bool = True            # prediction text (Float.toString) formatted on the GPU
     fold_bn: bool = True               # False: standalone BatchNorm kernels (bf16 / fp32)

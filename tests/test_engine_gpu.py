@@ -19,7 +19,8 @@ pytestmark = pytest.mark.gpu
 C = native()
 K = C.kafka
 REC = np.dtype([("off", "<i8"), ("len", "<i4"), ("slot", "<i4"), ("images", "<i4"),
-                ("status", "<i4"), ("tile0", "<i4"), ("pad", "<i4")])
+                ("status", "<i4"), ("tile0", "<i4"), ("has_cnt", "<i4"), ("cnt_off", "<i8"),
+                ("pad", "<i8")])
 assert REC.itemsize == C.JSON_RECORD_BYTES
 
 
@@ -29,7 +30,7 @@ def stage(arrays):
     recs = np.zeros(len(arrays), dtype=REC)
     slot = tiles = 0
     for i, (txt, images) in enumerate(arrays):
-        recs[i] = (len(buf), len(txt), slot, images, 0, tiles, 0)
+        recs[i] = (len(buf), len(txt), slot, images, 0, tiles, 0, 0, 0)
         tiles += C.json_tile_count(len(buf), len(txt))
         buf += txt + b" " * ((-len(txt)) % 16)
         slot += images
@@ -261,6 +262,70 @@ def test_gpu_crc32c_chunks_kernel():
         assert std == K.crc32c(buf[s0:s0 + ln]), (s0, ln)
 
 
+def test_gpu_fused_ingest_kernel_matches_separate_passes():
+    """ingest_crc_count (CRC windows + token counts in ONE launch) produces the raw window CRCs
+    of crc32c_chunks and the per-tile / per-record counts of json_count_records; the parse then
+    reuses those tile counts (has_cnt, no counting launch) and decodes the same tensor."""
+    import os
+
+    rng = np.random.default_rng(8)
+    H, Wd, Cc = 32, 32, 3
+    xs = [rng.random((n, H, Wd, Cc), dtype=np.float32) for n in (1, 3, 2)]
+    arrays = [array_text(C.encode_instances(x), H, Wd, Cc) for x in xs]
+    raw, recs, total, tiles = stage(arrays)
+    buf = bytes(raw) + os.urandom(5000)
+    tile_rec = np.zeros(tiles, dtype=np.int32)
+    for i, r in enumerate(recs):
+        n = C.json_tile_count(int(r["off"]), int(r["len"]))
+        tile_rec[r["tile0"]:r["tile0"] + n] = i
+    wins = [(len(buf) - 4096 * k, 4096) for k in range(len(buf) // 4096)][::-1]
+    wins = [(len(buf) - 4096 * len(wins), len(buf) % 4096)] + wins if len(buf) % 4096 else wins
+    ch = np.zeros(len(wins), dtype=[("end", "<i8"), ("len", "<i4"), ("pad", "<i4")])
+    for i, (e, ln) in enumerate(wins):
+        ch[i] = (e, ln, 0)
+    d = torch.frombuffer(bytearray(buf + bytes(64)), dtype=torch.uint8).cuda()
+    tables = torch.tensor(np.array(K.crc32c_device_tables(), dtype=np.uint32).view(np.int32),
+                          device="cuda")
+    dch = torch.from_numpy(ch.view(np.uint8).copy()).cuda()
+    dmap = torch.from_numpy(tile_rec).cuda()
+    s = torch.cuda.current_stream().cuda_stream
+
+    def run(fused):
+        drec = torch.from_numpy(recs.view(np.uint8).copy()).cuda()
+        crc = torch.zeros(len(wins), dtype=torch.int32, device="cuda")
+        cnt = torch.full((tiles,), -1, dtype=torch.int32, device="cuda")
+        tok = torch.zeros(len(recs), dtype=torch.int32, device="cuda")
+        if fused:
+            C.ingest_crc_count(d.data_ptr(), dch.data_ptr(), len(wins), tables.data_ptr(),
+                               crc.data_ptr(), len(recs), tiles, drec.data_ptr(),
+                               dmap.data_ptr(), cnt.data_ptr(), tok.data_ptr(), s)
+        else:
+            C.crc32c_chunks(d.data_ptr(), dch.data_ptr(), len(wins), tables.data_ptr(),
+                            crc.data_ptr(), s)
+            C.json_count_records(len(recs), tiles, drec.data_ptr(), dmap.data_ptr(),
+                                 d.data_ptr(), cnt.data_ptr(), tok.data_ptr(), s)
+        torch.cuda.synchronize()
+        return crc.cpu().numpy(), cnt.cpu().numpy(), tok.cpu().numpy()
+
+    a, b = run(True), run(False)
+    for u, v in zip(a, b):
+        np.testing.assert_array_equal(u, v)
+    assert list(a[2]) == [len(x) * H * Wd * Cc for x in xs]
+    # parse with the ingest counts (has_cnt, cnt_off relative to the text base), no count pass
+    cnt_dev = torch.from_numpy(a[1].copy()).cuda()
+    recs2 = recs.copy()
+    recs2["has_cnt"] = 1
+    recs2["cnt_off"] = [cnt_dev.data_ptr() + 4 * int(r["tile0"]) - d.data_ptr() for r in recs]
+    drec = torch.from_numpy(recs2.view(np.uint8).copy()).cuda()
+    out = torch.full((total, H, Wd, Cc), -7.0, device="cuda")
+    scratch = torch.full((tiles,), 123456, dtype=torch.int32, device="cuda")  # must be unused
+    C.json_parse_instances(len(recs), tiles, drec.data_ptr(), dmap.data_ptr(), d.data_ptr(), H,
+                           Wd, Cc, scratch.data_ptr(), out.data_ptr(), s, count_pass=False)
+    torch.cuda.synchronize()
+    assert list(drec.cpu().numpy().view(REC)["status"]) == [0, 0, 0]
+    np.testing.assert_array_equal(out.cpu().numpy(), np.concatenate(xs))
+
+
 def test_gpu_ingest_rejects_corrupt_batch_and_counts_images(broker):
     """GPU ingest: a bit flip inside a record batch fails its device-computed CRC32C, so all of
     its records get the error policy; records of intact batches are counted (N = 2 images
@@ -388,3 +453,41 @@ def test_gpu_engine_record_over_max_batch(broker, ingest):
     st = eng.stats()
     assert st["split_records"] == 1 and st["split_fragments"] == 3
     assert st["errors"] == 0 and st["images_out"] == 304 and st["err_too_large"] == 0
+
+
+@pytest.mark.parametrize("model", ["resnet20", "lenet5"])
+def test_gpu_step_graph_equals_eager(model):
+    """The captured per-slot step graph (metadata H2D, parse, forward, format, status D2H in one
+    hipGraphLaunch, counts read from the metadata header) produces byte-identical output records
+    to the op-by-op launches, over batches of every size and with a malformed record inside."""
+    net = get_model(model)
+    params = init_params(net, seed=0, calib_batch=16)
+    rng = np.random.default_rng(21)
+    recs = []
+    for i in range(40):
+        x = rng.random((1 + i % 5,) + net.input_shape, dtype=np.float32)
+        recs.append((f"r{i}".encode(), C.encode_instances(x)))
+    recs.insert(17, (b"bad", b'{"instances": [[[[0.5, x]]]]}'))
+    outs = {}
+    for step in (True, False):
+        b = K.Broker()
+        b.start()
+        b.create_topic("in", 1)
+        b.create_topic("out", 1)
+        for k, v in recs:
+            b.append("in", 0, [v], [k])
+        cfg = GaleConfig(topology_name="s", input_topic="in", output_topic="out", model=model,
+                         bootstrap=f"127.0.0.1:{b.port}", start_offset="earliest",
+                         max_batch=32, max_wait_us=300, output_key="input", graph_step=step,
+                         on_error="error-json")
+        eng = Engine(cfg, devices=[0], max_records=len(recs), params=params)
+        eng.start()
+        assert eng.wait(120), eng.stats()
+        eng.stop()
+        st = eng.stats()
+        assert (st["graph_step_batches"] == st["batches"]) if step else \
+            st["graph_step_batches"] == 0
+        outs[step] = {r["key"]: r["value"] for r in b.read("out", 0)}
+        b.stop()
+    assert outs[True] == outs[False] and len(outs[True]) == len(recs)
+    assert b"error" in outs[True][b"bad"]

@@ -111,9 +111,10 @@ def gpu_parse_numbers(texts):
     arr = ("[[[" + ",".join(f"[{t}]" for t in texts) + "]]]").encode()
     n = len(texts)
     rec = np.zeros(1, dtype=[("off", "<i8"), ("len", "<i4"), ("slot", "<i4"), ("images", "<i4"),
-                             ("status", "<i4"), ("tile0", "<i4"), ("pad", "<i4")])
+                             ("status", "<i4"), ("tile0", "<i4"), ("has_cnt", "<i4"),
+                             ("cnt_off", "<i8"), ("pad", "<i8")])
     tiles = C.json_tile_count(0, len(arr))
-    rec[0] = (0, len(arr), 0, 1, 0, 0, 0)
+    rec[0] = (0, len(arr), 0, 1, 0, 0, 0, 0, 0)
     raw = np.frombuffer(arr + b" " * (16 + (-len(arr)) % 16), dtype=np.uint8)
     d_raw = torch.from_numpy(raw.copy()).cuda()
     d_rec = torch.from_numpy(rec.view(np.uint8).copy()).cuda()
