@@ -1230,11 +1230,35 @@ std::vector<int> GroupMember::join() {
       }
       cluster_.invalidate();  // the partition count may have grown
       const int n = std::max(0, cluster_.partitions(cfg_.topic));
-      for (auto& kv : resp.protocol == "load-aware" ? assign_load_aware(subscribed, loads, n)
-                                                    : assign(resp.protocol, subscribed, n)) {
+      const bool la = resp.protocol == "load-aware";
+      // load-aware: every member learns its capacity share (unmeasured members count as the
+      // mean of the measured ones, as in the assignor), so it can tell whether its lag is out
+      // of proportion - only then can a new assignment help
+      std::map<std::string, double> share;
+      if (la) {
+        double known = 0, total = 0;
+        int nknown = 0;
+        for (const auto& m : subscribed)
+          if (loads[m].capacity > 0) {
+            known += loads[m].capacity;
+            ++nknown;
+          }
+        const double fill = nknown ? known / nknown : 1.0;
+        for (const auto& m : subscribed) total += loads[m].capacity > 0 ? loads[m].capacity : fill;
+        for (const auto& m : subscribed)
+          share[m] = (loads[m].capacity > 0 ? loads[m].capacity : fill) / std::max(total, 1e-9);
+      }
+      for (auto& kv : la ? assign_load_aware(subscribed, loads, n)
+                         : assign(resp.protocol, subscribed, n)) {
         ConsumerAssignment a;
         a.partitions.push_back({cfg_.topic, std::vector<int32_t>(kv.second.begin(),
                                                                  kv.second.end())});
+        if (la) {
+          Writer u;
+          u.i16(1);  // version
+          u.i64((int64_t)(share[kv.first] * 1e9));
+          a.user_data = u.buf;
+        }
         sr.assignments.push_back({kv.first, encode_assignment(a)});
       }
       for (const GroupMemberMeta& m : resp.members)  // members not on this topic: nothing
@@ -1261,11 +1285,71 @@ std::vector<int> GroupMember::join() {
     if (sresp.error != NONE)
       throw KafkaError(sresp.error, std::string("SyncGroup: ") + error_name(sresp.error));
     std::vector<int> mine;
-    for (const auto& tp : decode_assignment(sresp.assignment).partitions)
+    const ConsumerAssignment asg = decode_assignment(sresp.assignment);
+    for (const auto& tp : asg.partitions)
       if (tp.first == cfg_.topic) mine.insert(mine.end(), tp.second.begin(), tp.second.end());
     std::sort(mine.begin(), mine.end());
+    capacity_share_ = -1;
+    if (asg.user_data.size() >= 10) {
+      Reader u(asg.user_data);
+      if (u.i16() == 1) capacity_share_ = (double)u.i64() * 1e-9;
+    }
     return mine;
   }
+}
+
+std::map<int, int64_t> GroupMember::partition_lags() {
+  std::map<int, int64_t> lag;
+  const int n = cluster_.partitions(cfg_.topic);
+  if (n <= 0) return lag;
+  // committed offsets (one OffsetFetch to the coordinator)
+  OffsetFetchRequest fr;
+  fr.group_id = cfg_.group_id;
+  CommitTopic ct;
+  ct.name = cfg_.topic;
+  for (int p = 0; p < n; ++p) {
+    CommitPartition cp;
+    cp.index = p;
+    ct.partitions.push_back(cp);
+  }
+  fr.topics.push_back(std::move(ct));
+  Writer w;
+  encode_offset_fetch_request(w, fr);
+  std::map<int, int64_t> committed;
+  {
+    const std::string resp = cluster_.coordinator(cfg_.group_id).request(OFFSET_FETCH, w);
+    Reader r(resp);
+    for (auto& t : decode_offset_fetch_response(r))
+      for (auto& p : t.partitions) committed[p.index] = p.offset;
+  }
+  // log ends and starts (ListOffsets per partition leader)
+  std::map<int32_t, std::vector<int>> by_leader;
+  for (int p = 0; p < n; ++p) by_leader[cluster_.leader(cfg_.topic, p)].push_back(p);
+  std::map<int, int64_t> end, start;
+  for (auto& kv : by_leader) {
+    for (int64_t ts : {kLatest, kEarliest}) {
+      ListOffsetsRequest lr;
+      ListOffsetsTopic lt;
+      lt.name = cfg_.topic;
+      for (int p : kv.second) lt.partitions.push_back({p, ts});
+      lr.topics.push_back(std::move(lt));
+      Writer lw;
+      encode_list_offsets_request(lw, lr);
+      const std::string resp = cluster_.node(kv.first).request(LIST_OFFSETS, lw);
+      Reader r(resp);
+      for (auto& t : decode_list_offsets_response(r).topics)
+        for (auto& p : t.partitions)
+          if (p.error == NONE) (ts == kLatest ? end : start)[p.index] = p.offset;
+    }
+  }
+  for (int p = 0; p < n; ++p) {
+    auto e = end.find(p);
+    if (e == end.end()) continue;
+    auto c = committed.find(p);
+    const int64_t from = c != committed.end() && c->second >= 0 ? c->second : start[p];
+    lag[p] = std::max<int64_t>(0, e->second - from);
+  }
+  return lag;
 }
 
 bool GroupMember::heartbeat() {

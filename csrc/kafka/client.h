@@ -353,6 +353,12 @@ class GroupMember {
       std::vector<std::string> members, const std::map<std::string, MemberLoad>& load, int n);
   // user_data sent with the next JoinGroup (load-aware: encode_member_load)
   void set_user_data(std::string d) { user_data_ = std::move(d); }
+  // load-aware: this member's share of the group's capacity as the leader weighed it for the
+  // current assignment (carried in the assignment's user_data; -1 = unknown / other assignor)
+  double capacity_share() const { return capacity_share_; }
+  // per-partition lag of the group on its topic (log end - committed offset; partitions with
+  // no commit yet count from the log start): what decides whether a rebalance can help
+  std::map<int, int64_t> partition_lags();
 
  private:
   GroupConfig cfg_;
@@ -361,6 +367,7 @@ class GroupMember {
   std::string user_data_;
   int32_t generation_ = -1;
   bool leader_ = false;
+  double capacity_share_ = -1;
 };
 
 }  // namespace kafka

@@ -560,11 +560,37 @@ void Engine::group_loop() {
               lag_at_over = lag;
             } else if (now - over_since >= 1000000000ll && lag > lag_at_over &&
                        now - last_join >= (int64_t)cfg_.rebalance_cooldown_ms * 1000000) {
-              fprintf(stderr, "[gale group] lag %lld > %lld and growing (capacity %.0f "
-                      "images/s): triggering a load-aware rebalance\n", (long long)lag,
-                      (long long)lag_bound, capacity_rps_.load());
-              ++lag_rebalances_;
-              rejoin = true;
+              // a rebalance only helps when this member's lag is out of proportion to its
+              // capacity share; when the whole group is overloaded every member's lag grows in
+              // proportion, no assignment adds capacity, and an eager rebalance would only
+              // stop the world. The group's lags come from the broker (log ends -
+              // committed offsets), this member's share from the leader's assignment.
+              const double share = gm->capacity_share();
+              double frac = -1;
+              if (share > 0) {
+                try {
+                  int64_t total = 0, own = 0;
+                  for (const auto& kv : gm->partition_lags()) {
+                    total += kv.second;
+                    if (std::find(owned.begin(), owned.end(), kv.first) != owned.end())
+                      own += kv.second;
+                  }
+                  if (total > 0) frac = (double)own / (double)total;
+                } catch (const std::exception&) {
+                }
+              }
+              if (frac < 0 || frac > std::min(0.95, 1.5 * share)) {
+                fprintf(stderr, "[gale group] lag %lld > %lld and growing (capacity %.0f "
+                        "images/s, %.0f%% of the group's lag at a %.0f%% capacity share): "
+                        "triggering a load-aware rebalance\n", (long long)lag,
+                        (long long)lag_bound, capacity_rps_.load(), 100 * frac, 100 * share);
+                ++lag_rebalances_;
+                rejoin = true;
+              } else {
+                ++lag_rebalances_skipped_;  // group-wide overload: re-arm, keep the assignment
+                over_since = now;
+                lag_at_over = lag;
+              }
             }
           } else {
             over_since = 0;
@@ -1614,6 +1640,7 @@ std::map<std::string, double> Engine::stats() const {
   s["replicas_alive"] = alive;
   s["rebalances"] = (double)rebalances_;
   s["lag_rebalances"] = (double)lag_rebalances_;
+  s["lag_rebalances_skipped"] = (double)lag_rebalances_skipped_;
   s["capacity_rps"] = capacity_rps_.load();
   s["generation"] = (double)generation_;
   s["assigned_partitions"] = cfg_.group_membership ? (double)assigned_partitions_

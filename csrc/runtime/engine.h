@@ -373,6 +373,7 @@ class Engine {
   int64_t replica_busy_ns() const;  // summed over replicas, up to now
   std::atomic<double> capacity_rps_{0.0};   // load-aware: measured capacity (images/s)
   std::atomic<int64_t> lag_rebalances_{0};  // rebalances this member triggered on its lag
+  std::atomic<int64_t> lag_rebalances_skipped_{0};  // lag over the bound, but group-wide
   std::atomic<int64_t> t_first_ns_{0}, t_last_ns_{0};
   std::atomic<bool> ack_log_on_{false};
   std::mutex ack_mu_;

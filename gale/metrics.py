@@ -27,7 +27,9 @@ KEYS = ("records_in", "records_out", "images_out", "errors", "produce_failures",
         "e2e_us_p50", "e2e_us_p99", "queue_us_p50", "device_us_p50", "device_us_p99",
         "record_e2e_ms_p50", "record_e2e_ms_p99", "batch_images_mean", "rebalances",
         "generation", "assigned_partitions", "eff_max_batch", "eff_max_wait_us",
-        "lag_rebalances", "capacity_rps", "steals")
+        "lag_rebalances", "lag_rebalances_skipped", "capacity_rps", "steals",
+        "converted_batches", "poison_batches", "poison_records", "split_records",
+        "graph_step_batches")
 
 
 class Reporter:

@@ -307,7 +307,8 @@ def test_waiting_members_are_not_expired_during_a_long_join(broker):
     d.leave()
 
 
-def _load_run(tmp, assignor, seconds=11.0, rate=6000.0):
+def _load_run(tmp, assignor, seconds=11.0, rate=6000.0,
+              delays=(("F1", 4000), ("F2", 4000), ("S", 16000))):
     """Three serving processes in one consumer group over 12 input partitions, stub replicas of
     capacity ~4000 / ~4000 / ~1000 records/s (one 4x slower), an open-loop producer offering
     6000 records/s spread evenly over the partitions. Returns each process's metric lines."""
@@ -324,7 +325,7 @@ def _load_run(tmp, assignor, seconds=11.0, rate=6000.0):
                  "--assignor", assignor, "--rebalance-cooldown-ms", "2000", "--model", "lenet5",
                  "--stub-null", "--replicas", "1", "--duration", str(seconds + 8),
                  "--start-offset", "latest"]
-        for name, delay in (("F1", 4000), ("F2", 4000), ("S", 16000)):
+        for name, delay in delays:
             procs[name] = _cli(name, b.port, tmp, extra + ["--stub-delay-us", str(delay)])
         assert wait_for(lambda: len(b.describe_group("L")["members"]) == 3
                         and b.describe_group("L")["state"] == "Stable", 60)
@@ -377,3 +378,15 @@ def test_load_aware_assignment_sheds_a_slow_members_partitions(tmp_path):
     # the feeder and the stubs share the CPUs); load-aware: the group keeps up
     assert ctrl_s["lag_records"] > 3000, ctrl_s
     assert total_lag_aware < ctrl_s["lag_records"] / 3, (total_lag_aware, ctrl_s)
+
+
+def test_load_aware_no_rebalance_when_the_whole_group_is_overloaded(tmp_path):
+    """Every member at ~1000 records/s against 2000 offered each: all lags grow in proportion
+    to the members' capacity shares, no assignment can add capacity, so the lag trigger must
+    not keep forcing stop-the-world rebalances: it re-arms instead."""
+    lines = _load_run(tmp_path, "load-aware", seconds=9.0,
+                      delays=(("A", 16000), ("B", 16000), ("C", 16000)))
+    last = {n: v[-1] for n, v in lines.items()}
+    assert sum(v["lag_rebalances"] for v in last.values()) == 0, last
+    assert sum(v.get("lag_rebalances_skipped", 0) for v in last.values()) >= 1, last
+    assert sum(v["lag_records"] for v in (lines[n][-2] for n in lines)) > 3000  # overloaded
