@@ -102,6 +102,9 @@ def parse_args(argv=None):
                     help="sources nibble-pack the fetched JSON text for the host->GPU link "
                          "(expanded on the device; needs AVX-512 VBMI; costs host CPU, "
                          "profiles/r3_nibble_transport_ab.txt)")
+    ap.add_argument("--text-pack-bounce", action=argparse.BooleanOptionalAction, default=True,
+                    help="with --text-pack: receive through a cache-resident window, keep only "
+                         "the packed text + a sparse framing copy in pinned memory")
     ap.add_argument("--check-crcs", action=argparse.BooleanOptionalAction, default=True,
                     help="consumer CRC32C verification (Kafka check.crcs; diagnosis only)")
     ap.add_argument("--rate", type=float, default=0.0,
@@ -650,7 +653,7 @@ def main(argv=None) -> int:
                      replicas=a.replicas_per_gpu * local_gpus,
                      decode_threads=a.decode_threads, slo_p99_ms=a.slo_p99_ms,
                      gpu_wait_poll_us=a.gpu_wait_poll_us, gpu_ingest=a.gpu_ingest, gpu_encode=a.gpu_encode,
-                     text_pack=a.text_pack,
+                     text_pack=a.text_pack, text_pack_bounce=a.text_pack_bounce,
                      stub=a.stub, stub_null=a.stub_null, commit_interval_ms=500,
                      check_crcs=a.check_crcs,
                      output_partition=rank if a.local_output and world > 1 else -1,

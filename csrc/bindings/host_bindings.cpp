@@ -16,6 +16,8 @@
 #include "../kafka/broker.h"
 #include "../kafka/client.h"
 #include "../kafka/compress.h"
+#include "../kafka/fetch_framing.h"
+#include "../runtime/pack_tap.h"
 #include "../kafka/protocol.h"
 #include "../kafka/wire.h"
 
@@ -918,7 +920,7 @@ void bind_host(py::module_& m) {
       .def(py::init([](const std::string& bootstrap, const std::string& group_id, int max_wait_ms,
                        int fetch_max_bytes, int partition_max_bytes, bool check_crcs,
                        const std::string& auto_offset_reset, const std::string& client_id,
-                       int recv_lowat) {
+                       int recv_lowat, bool bounce_pack, int bounce_window_kb) {
              ConsumerConfig c;
              c.recv_lowat = recv_lowat;
              c.bootstrap = bootstrap;
@@ -929,12 +931,24 @@ void bind_host(py::module_& m) {
              c.check_crcs = check_crcs;
              c.auto_offset_reset = auto_offset_reset;
              c.client_id = client_id;
-             return std::make_shared<Consumer>(c);
+             if (!bounce_pack) return std::make_shared<Consumer>(c);
+             // the bounce receive (runtime/pack_tap.h) over heap "chunks" sized like the
+             // engine's pinned pool, for host-side tests of the sparse body + packed text
+             c.check_crcs = false;  // (the host copy is sparse: the GPU checks the CRCs)
+             const size_t chunk =
+                 gale::codec::pack_layout_bytes((size_t)c.fetch_max_bytes + (1 << 20)) + 4096;
+             auto cons = std::make_shared<Consumer>(
+                 c, [chunk](size_t n) { return heap_alloc(std::max(n, chunk)); });
+             cons->set_recv_tap(std::make_shared<gale::BouncePackTap>(
+                 chunk, [](const uint8_t*) { return true; }, 1,
+                 (size_t)std::max(1, bounce_window_kb) << 10));
+             return cons;
            }),
            py::arg("bootstrap"), py::arg("group_id") = "", py::arg("max_wait_ms") = 100,
            py::arg("fetch_max_bytes") = 64 << 20, py::arg("partition_max_bytes") = 16 << 20,
            py::arg("check_crcs") = true, py::arg("auto_offset_reset") = "latest",
-           py::arg("client_id") = "gale-consumer", py::arg("recv_lowat") = 0)
+           py::arg("client_id") = "gale-consumer", py::arg("recv_lowat") = 0,
+           py::arg("bounce_pack") = false, py::arg("bounce_window_kb") = 256)
       .def("assign", [](Consumer& c, const std::string& topic, std::vector<int> parts) {
         py::gil_scoped_release nogil;
         c.assign(topic, parts);
@@ -961,8 +975,60 @@ void bind_host(py::module_& m) {
           fs = c.poll();
         }
         py::list out;
-        for (auto& f : fs)
+        for (auto& f : fs) {
+          f.restore();  // (a sparse body: the values are read here)
           for (auto item : records_to_py(f.buf.get(), f.records)) out.append(item);
+        }
+        return out;
+      })
+      .def("poll_bodies", [](Consumer& c) {
+        // per fetch response: the host copy as received (sparse under the bounce receive), the
+        // text expanded from its packed stream, and the records decoded from the host copy
+        std::vector<Fetched> fs;
+        {
+          py::gil_scoped_release nogil;
+          fs = c.poll();
+        }
+        py::list out;
+        for (auto& f : fs) {
+          py::dict d;
+          d["size"] = f.size;
+          d["packed_bytes"] = f.tap_result;
+          d["sparse"] = f.sparse;
+          d["host"] = py::bytes(reinterpret_cast<const char*>(f.buf.get()), f.size);
+          py::list recs;
+          for (const RecordRef& r : f.records) {
+            py::dict x;
+            x["partition"] = r.partition;
+            x["offset"] = r.offset;
+            x["timestamp"] = r.timestamp;
+            x["key"] = opt_bytes(f.buf.get(), r.key_off, r.key_len);
+            x["value_off"] = r.value_off;
+            x["value_len"] = r.value_len;
+            py::list hs;
+            for (const Header& h : decode_headers(f.buf.get(), r))
+              hs.append(py::make_tuple(h.key, h.value_null ? py::object(py::none())
+                                                           : py::object(py::bytes(h.value))));
+            x["headers"] = hs;
+            if (r.value_len >= 0) {
+              const gale::codec::Scan sc = gale::codec::scan_envelope(
+                  f.buf.get() + r.value_off, (size_t)r.value_len, gale::kafka::FramingWalker::kHead,
+                  gale::kafka::FramingWalker::kTail);
+              x["scan"] = py::make_tuple(sc.status, sc.arr_off, sc.arr_len);
+            }
+            recs.append(x);
+          }
+          d["records"] = recs;
+          if (f.tap_result >= 0) {
+            std::string full(f.size, '\0');
+            gale::codec::text_unpack_host(
+                f.buf.get() + gale::codec::pack_offset(f.size),
+                reinterpret_cast<const uint32_t*>(f.buf.get() + gale::codec::tab_offset(f.size)),
+                f.size, reinterpret_cast<uint8_t*>(&full[0]));
+            d["unpacked"] = py::bytes(full);
+          }
+          out.append(d);
+        }
         return out;
       })
       .def("poll_count", [](Consumer& c) {

@@ -1,6 +1,8 @@
 // Host JSON codec for the InstObj/PredObj contract (see json_codec.h).
 #include "json_codec.h"
 
+#include <algorithm>
+
 #include <immintrin.h>
 #include <math.h>
 #include <string.h>
@@ -164,8 +166,10 @@ void sci_digits(float a, int precision, char* dig, int* nd, int* e) {
 
 }  // namespace
 
-Scan scan_envelope(const uint8_t* p, size_t n) {
+Scan scan_envelope(const uint8_t* p, size_t full_n, size_t head_limit, size_t tail_limit) {
   Scan s;
+  // forward scans stay inside the head window, the backward scan inside the tail window
+  const size_t n = std::min(full_n, head_limit);
   size_t i = skip_ws(p, 0, n);
   if (i >= n || p[i] != '{') { s.status = BAD_ENVELOPE; return s; }
   i = skip_ws(p, i + 1, n);
@@ -195,12 +199,13 @@ Scan scan_envelope(const uint8_t* p, size_t n) {
   if (i >= n || p[i] != '[') { s.status = BAD_ENVELOPE; return s; }
   const size_t beg = i;
   // trailing "] ws } ws"
-  size_t j = n;
-  while (j > beg && is_ws(p[j - 1])) --j;
-  if (j == beg || p[j - 1] != '}') { s.status = BAD_ENVELOPE; return s; }
+  const size_t lo = std::max(beg, full_n > tail_limit ? full_n - tail_limit : (size_t)0);
+  size_t j = full_n;
+  while (j > lo && is_ws(p[j - 1])) --j;
+  if (j == lo || p[j - 1] != '}') { s.status = BAD_ENVELOPE; return s; }
   --j;
-  while (j > beg && is_ws(p[j - 1])) --j;
-  if (j == beg || p[j - 1] != ']') {
+  while (j > lo && is_ws(p[j - 1])) --j;
+  if (j == lo || p[j - 1] != ']') {
     s.status = (j > beg) ? UNKNOWN_KEY : BAD_ENVELOPE;  // e.g. {"instances":[..],"k":1}
     return s;
   }

@@ -17,6 +17,8 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include <cstdint>
+
 #include <string>
 #include <utility>
 #include <vector>
@@ -50,7 +52,11 @@ struct Scan {
 // Bounded envelope check: the {"instances": ... } prefix and the "] }" suffix only (reads a
 // few bytes at each end; the array's interior, its image count and any key hidden inside it are
 // left to the device ingest / parser). images stays 0.
-Scan scan_envelope(const uint8_t* p, size_t n);
+// head_limit / tail_limit: only the first / last that many bytes of the value are read (a sparse
+// host copy holds nothing else, kafka/fetch_framing.h); an envelope reaching beyond them is
+// rejected as BAD_ENVELOPE (documented limit: <= ~200 bytes of whitespace around it).
+Scan scan_envelope(const uint8_t* p, size_t n, size_t head_limit = SIZE_MAX,
+                   size_t tail_limit = SIZE_MAX);
 
 // Envelope validation + image count (the per-number work is left to the GPU parser).
 Scan scan_instances(const uint8_t* p, size_t n, int H, int W, int C);

@@ -37,10 +37,11 @@ inline void close_block(uint32_t* tab, PackState& st, bool packed) {
     tab[2 * (st.block / kPackGroupBlocks - 1) + 1] = st.mask;
 }
 
-void pack_scalar(const uint8_t* src, size_t upto, uint8_t* dst, uint32_t* tab, PackState& st) {
+void pack_scalar(const uint8_t* src, size_t upto, uint8_t* dst, uint32_t* tab, PackState& st,
+                 size_t src_base) {
   for (; st.block < upto;) {
     open_block(tab, st);
-    const uint8_t* s = src + st.block * kPackBlock;
+    const uint8_t* s = src + (st.block * kPackBlock - src_base);
     uint8_t bad = 0;
     for (int i = 0; i < kPackBlock; ++i) bad |= kLut[s[i]];
     const bool packed = !(bad & 0x80);
@@ -61,7 +62,8 @@ void pack_scalar(const uint8_t* src, size_t upto, uint8_t* dst, uint32_t* tab, P
 __attribute__((target("avx512f,avx512bw,avx512vbmi"))) void pack_avx512(const uint8_t* src,
                                                                         size_t upto, uint8_t* dst,
                                                                         uint32_t* tab,
-                                                                        PackState& st) {
+                                                                        PackState& st,
+                                                                        size_t src_base) {
   const __m512i t0 = _mm512_loadu_si512(kLut.data());
   const __m512i t1 = _mm512_loadu_si512(kLut.data() + 64);
   const __m512i pair = _mm512_set1_epi16(0x1001);  // bytes (1, 16)
@@ -74,7 +76,7 @@ __attribute__((target("avx512f,avx512bw,avx512vbmi"))) void pack_avx512(const ui
       mask = 0;
     }
     const size_t gend = std::min(upto, (g + 1) * kPackGroupBlocks);
-    const uint8_t* s = src + b * kPackBlock;
+    const uint8_t* s = src + (b * kPackBlock - src_base);
     for (; b < gend; ++b, s += kPackBlock) {
       const __m512i v = _mm512_loadu_si512(s);
       const __m512i c = _mm512_permutex2var_epi8(t0, v, t1);
@@ -104,21 +106,22 @@ bool text_pack_fast() {
 }
 
 void text_pack_blocks(const uint8_t* src, size_t upto, uint8_t* dst, uint32_t* tab,
-                      PackState& st) {
+                      PackState& st, size_t src_base) {
   if (upto <= st.block) return;
   if (text_pack_fast())
-    pack_avx512(src, upto, dst, tab, st);
+    pack_avx512(src, upto, dst, tab, st, src_base);
   else
-    pack_scalar(src, upto, dst, tab, st);
+    pack_scalar(src, upto, dst, tab, st, src_base);
 }
 
-size_t text_pack_finish(const uint8_t* src, size_t n, uint8_t* dst, uint32_t* tab, PackState& st) {
+size_t text_pack_finish(const uint8_t* src, size_t n, uint8_t* dst, uint32_t* tab, PackState& st,
+                        size_t src_base) {
   const size_t full = n / kPackBlock;
-  text_pack_blocks(src, full, dst, tab, st);
+  text_pack_blocks(src, full, dst, tab, st, src_base);
   const size_t r = n - full * kPackBlock;
   if (r) {  // the partial tail block: raw
     open_block(tab, st);
-    memcpy(dst + st.out, src + full * kPackBlock, r);
+    memcpy(dst + st.out, src + (full * kPackBlock - src_base), r);
     st.out += r;
     st.mask &= ~(1u << (full % kPackGroupBlocks));
   }
@@ -130,7 +133,7 @@ size_t text_pack_finish(const uint8_t* src, size_t n, uint8_t* dst, uint32_t* ta
 size_t text_pack(const uint8_t* src, size_t n, uint8_t* dst, uint32_t* tab, bool force_scalar) {
   PackState st;
   if (force_scalar) {
-    pack_scalar(src, n / kPackBlock, dst, tab, st);
+    pack_scalar(src, n / kPackBlock, dst, tab, st, 0);
     st.block = n / kPackBlock;  // (text_pack_finish sees every full block done)
   }
   return text_pack_finish(src, n, dst, tab, st);

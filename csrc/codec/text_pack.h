@@ -53,9 +53,12 @@ struct PackState {
   size_t out = 0;     // packed bytes written so far
   uint32_t mask = 0;  // packed-block bits of the open group
 };
+// src_base: the span offset src points at (src holds bytes [src_base, ...) of the span: a
+// receive window sliding over it); blocks before src_base must already be packed.
 void text_pack_blocks(const uint8_t* src, size_t upto, uint8_t* dst, uint32_t* tab,
-                      PackState& st);
-size_t text_pack_finish(const uint8_t* src, size_t n, uint8_t* dst, uint32_t* tab, PackState& st);
+                      PackState& st, size_t src_base = 0);
+size_t text_pack_finish(const uint8_t* src, size_t n, uint8_t* dst, uint32_t* tab, PackState& st,
+                        size_t src_base = 0);
 
 // True when the host has the vector path (AVX-512 VBMI byte permutes); the scalar path is exact
 // but ~10x slower, so the engine only packs by default when this holds.

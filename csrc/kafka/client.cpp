@@ -184,8 +184,22 @@ std::shared_ptr<uint8_t> Connection::recv(int32_t corr, size_t* size, const Buff
                              std::to_string(corr) + ")");
   const size_t n = (size_t)sz - 4;
   std::shared_ptr<uint8_t> buf = alloc(n);
-  if (tap) tap->begin(buf.get(), n);
-  recv_all(buf.get(), n, tap);
+  const bool bounce = tap && tap->begin(buf.get(), n);
+  if (bounce) {
+    // the tap's window takes the bytes; the tap writes what it keeps into buf
+    size_t left = n;
+    while (left) {
+      size_t room = 0;
+      uint8_t* w = tap->window(&room);
+      if (!w || room == 0) throw KafkaError(-1, "receive tap without a window");
+      const size_t want = std::min(left, room);
+      recv_all(w, want, nullptr);
+      tap->received(want);
+      left -= want;
+    }
+  } else {
+    recv_all(buf.get(), n, tap);
+  }
   if (tap && tap_result) *tap_result = tap->finish();
   *size = n;
   return buf;
@@ -918,6 +932,10 @@ void Consumer::collect(std::vector<Fetched>& out) {
     f.crc_checked = cfg_.check_crcs;
     try {
       f.buf = cluster_.node(inf.node).recv(inf.corr, &f.size, alloc_, tap_.get(), &f.tap_result);
+      if (tap_ && tap_->sparse()) {
+        f.sparse = true;
+        f.restorer = tap_;
+      }
     } catch (...) {
       // these connections are mid-response: reconnect them, forget their in-flight fetches
       for (size_t j = i; j < infs.size(); ++j) cluster_.drop(infs[j].node);
@@ -957,6 +975,7 @@ void Consumer::collect(std::vector<Fetched>& out) {
           // undecodable batches as poison records that advance the position
           f.records.resize(before);
           f.batches.resize(bbefore);
+          f.restore();  // (the rewrite copies values: they must be whole on the host)
           NormalizeStats ns;
           std::string blob = normalize_records(f.buf.get() + p.records_off, (size_t)p.records_len,
                                                pos_[p.index], cfg_.check_crcs,
@@ -988,6 +1007,7 @@ void Consumer::collect(std::vector<Fetched>& out) {
       size_t at = (f.size + 15) & ~(size_t)15;
       f.buf = nb;
       f.tap_result = -1;
+      f.sparse = false;
       for (const Conv& c : convs) {
         memcpy(nb.get() + at, c.blob.data(), c.blob.size());
         const size_t before = f.records.size();

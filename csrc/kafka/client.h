@@ -58,13 +58,29 @@ std::shared_ptr<uint8_t> heap_alloc(size_t bytes);
 // cache-hot). begin(buf, n) before the first byte; progress(done) after every receive call
 // (bytes [0, done) are in place; one call receives at most chunk_bytes()); finish() after the
 // last one, its value is kept in Fetched::tap_result.
+//
+// Bounce mode: a tap whose begin() returns true takes the body over - it is received piece by
+// piece into the tap's own (cache-resident) window (window(&room) -> receive -> received(bytes))
+// and buf gets only what the tap writes into it; finish() then says what buf holds.
 class RecvTap {
  public:
   virtual ~RecvTap() = default;
-  virtual void begin(uint8_t* buf, size_t n) = 0;
+  virtual bool begin(uint8_t* buf, size_t n) = 0;  // true: bounce mode for this body
   virtual void progress(size_t done) = 0;
   virtual int64_t finish() = 0;
   virtual size_t chunk_bytes() const { return 256 << 10; }
+  virtual uint8_t* window(size_t* room) {
+    *room = 0;
+    return nullptr;
+  }
+  virtual void received(size_t bytes) { (void)bytes; }
+  // the last body was kept sparse (bounce mode: framing only on the host, text packed)
+  virtual bool sparse() const { return false; }
+  // a sparse body -> its full bytes in place (host fallback paths; buf, n as in begin)
+  virtual void restore(const std::shared_ptr<uint8_t>& buf, size_t n) {
+    (void)buf;
+    (void)n;
+  }
 };
 
 class Connection {
@@ -247,6 +263,16 @@ struct Fetched {
   std::vector<BatchSpan> batches;  // record batches (for deferred CRC checks)
   bool crc_checked = false;
   int64_t tap_result = -1;  // the consumer's RecvTap::finish() for this body (-1: no tap)
+  // the host copy of the body holds Kafka framing and the ends of each value only (bounce
+  // receive, csrc/runtime/pack_tap.h): the full text is the packed stream in the same buffer.
+  // restore() rebuilds it in place for the host paths.
+  bool sparse = false;
+  std::shared_ptr<RecvTap> restorer;
+  void restore() {
+    if (!sparse) return;
+    restorer->restore(buf, size);
+    sparse = false;
+  }
 };
 
 class Consumer {

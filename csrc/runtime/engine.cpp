@@ -14,6 +14,7 @@
 #include "../codec/json_codec.h"
 #include "../kafka/compress.h"
 #include "pack_tap.h"
+#include "../kafka/fetch_framing.h"
 #include "trace.h"
 
 namespace gale {
@@ -664,8 +665,16 @@ void Engine::source_loop(int idx) {
   std::unique_ptr<kafka::Consumer> cons;
   try {
     cons = std::make_unique<kafka::Consumer>(cc, alloc);
-    if (pinned && cfg_.text_pack && ingest_for(slot))
-      cons->set_recv_tap(std::make_shared<PackTap>(pinned));
+    if (pinned && cfg_.text_pack && ingest_for(slot)) {
+      // the bounce receive leaves only framing on the host: the CRC check must be the GPU's
+      if (cfg_.text_pack_bounce && cfg_.decode_threads > 0) {
+        std::shared_ptr<PinnedPool> pool = pinned;
+        cons->set_recv_tap(std::make_shared<BouncePackTap>(
+            pool->chunk_bytes(), [pool](const uint8_t* p) { return pool->owns(p); }));
+      } else {
+        cons->set_recv_tap(std::make_shared<PackTap>(pinned));
+      }
+    }
   } catch (const std::exception& e) {
     fprintf(stderr, "[gale source %d] failed to start: %s\n", idx, e.what());
   }
@@ -771,6 +780,7 @@ void Engine::source_loop(int idx) {
     }
     for (auto& f : fs) {
       FetchItem it;
+      if (f.sparse) ++sparse_fetches_;
       it.pinned = pinned && pinned->owns(f.buf.get());
       it.f = std::move(f);
       it.source = idx;
@@ -858,7 +868,11 @@ bool Engine::ingest_fetch(FetchItem& it, std::vector<InRecord>& good, int lane) 
       io.status[i] = codec::BAD_ENVELOPE;  // null value (Jackson would throw)
       continue;
     }
-    const codec::Scan s = codec::scan_envelope(f.buf.get() + rr.value_off, (size_t)rr.value_len);
+    // (a sparse host copy holds only the ends of each value: the scan stays inside them)
+    const codec::Scan s =
+        f.sparse ? codec::scan_envelope(f.buf.get() + rr.value_off, (size_t)rr.value_len,
+                                        kafka::FramingWalker::kHead, kafka::FramingWalker::kTail)
+                 : codec::scan_envelope(f.buf.get() + rr.value_off, (size_t)rr.value_len);
     io.status[i] = s.status;
     io.arr_off[i] = s.arr_off;
     io.arr_len[i] = s.arr_len;
@@ -902,6 +916,10 @@ bool Engine::ingest_fetch(FetchItem& it, std::vector<InRecord>& good, int lane) 
     if (r.status == codec::OK && fault_hit(parse_error_p_)) r.status = codec::BAD_ENVELOPE;
     if (r.status == codec::OK && r.images > cfg_.max_batch) {
       images_in_ += r.images;
+      if (f.sparse) {  // the split copies the record's text on the host: make it whole
+        f.restore();
+        ++restored_fetches_;
+      }
       if (!split_record(r, good)) emit_error(r, codec::BAD_SHAPE, prod);
     } else if (r.status == codec::OK) {
       images_in_ += r.images;
@@ -920,6 +938,10 @@ bool Engine::ingest_fetch(FetchItem& it, std::vector<InRecord>& good, int lane) 
 void Engine::decode_fetch(FetchItem& it, std::vector<InRecord>& good, int lane) {
   if (ingest_fetch(it, good, lane)) return;
   kafka::Fetched& f = it.f;
+  if (f.sparse) {  // the host path reads the text: expand the packed stream in place first
+    f.restore();
+    ++restored_fetches_;
+  }
   std::vector<char> corrupt;
   // CRC32C and envelope scan fused in one pass: the batch CRC is chained record by record
   // (crc32c(b, crc32c(a)) == crc32c(a ++ b)) and each record is scanned right after its bytes
@@ -1070,7 +1092,8 @@ void Engine::serve(ReplicaSlot* rs) {
       {
         trace::Range tr("gale:batch");
         const int maxb = eff_batch_.load(std::memory_order_relaxed);
-        const bool steal = batchers_.size() > 1;
+        // (no steals with the text packed: a stolen record's host copy is sparse)
+        const bool steal = batchers_.size() > 1 && !cfg_.text_pack;
         open = batchers_[(size_t)rs->slot]->take(maxb,
                                                  eff_wait_ns_.load(std::memory_order_relaxed),
                                                  !mine.empty(), b->recs, images,
@@ -1600,6 +1623,8 @@ std::map<std::string, double> Engine::stats() const {
   s["poison_batches"] = (double)poison_batches_;
   s["poison_records"] = (double)poison_records_;
   s["split_records"] = (double)split_records_;
+  s["sparse_fetches"] = (double)sparse_fetches_;
+  s["restored_fetches"] = (double)restored_fetches_;
   s["split_fragments"] = (double)split_fragments_;
   {
     int64_t lag = 0, fetch_lag = 0, lag_max = 0;

@@ -67,6 +67,10 @@ struct EngineConfig {
   // GPU ingest: sources nibble-pack fetch bodies while receiving them (pack_tap.h) and the text
   // crosses the host link packed (csrc/codec/text_pack.h)
   bool text_pack = false;
+  // with text_pack: receive each fetch body through a cache-resident window and keep only its
+  // packed text + a sparse framing copy in the pinned chunk (BouncePackTap, pack_tap.h); false:
+  // the body lands in the chunk whole and is packed behind it (PackTap)
+  bool text_pack_bounce = true;
   // consumers' receive low-water mark (kafka::ClientConfig::recv_lowat), bytes; 0 = off
   int recv_lowat = 0;
   int commit_interval_ms = 2000;   // storm-kafka's ZK commit period
@@ -360,6 +364,7 @@ class Engine {
   std::atomic<int64_t> err_by_status_[16] = {};
   std::atomic<int64_t> converted_batches_{0}, poison_batches_{0}, poison_records_{0};
   std::atomic<int64_t> split_records_{0}, split_fragments_{0};
+  std::atomic<int64_t> sparse_fetches_{0}, restored_fetches_{0};  // bounce receive (pack_tap.h)
   Histogram h_queue_us_, h_device_us_, h_engine_e2e_us_, h_record_e2e_ms_, h_batch_images_;
   Histogram h_slo_win_us_;  // e2e latency of the SLO controller's current window
   Histogram h_slo_batch_;   // batch sizes (images) of the SLO controller's current window

@@ -72,6 +72,9 @@ class GaleConfig:
                                        # PCIe link, expanded on the device (text_pack.h); needs
                                        # AVX-512 VBMI; for hosts with idle cores behind a
                                        # link-bound GPU (profiles/r3_nibble_transport_ab.txt)
+    text_pack_bounce: bool = True      # with text_pack: fetch bodies go through a cache-resident
+                                       # window; the pinned chunk gets the packed text and a
+                                       # sparse framing copy only (csrc/runtime/pack_tap.h)
     # parallelism (R3)
     workers: int = 8                   # NUM_WORKERS: placement only (one process per GPU here)
     source_parallelism: int = 2        # KAFKA_SPOUT_PARAL
@@ -196,6 +199,7 @@ class GaleConfig:
             rebalance_cooldown_ms=self.rebalance_cooldown_ms,
             decode_threads=self.decode_threads, check_crcs=self.check_crcs,
             text_pack=bool(self.gpu_ingest and self.text_pack and _pack_fast()),
+            text_pack_bounce=self.text_pack_bounce,
             acks=self.acks, sink_mode=self.sink_mode, linger_ms=self.linger_ms,
             compression=self.compression,
             value_format=self.value_format, type_id_header=self.type_id_header,

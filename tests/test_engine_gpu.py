@@ -164,7 +164,8 @@ def centered_log(p):
 
 
 @pytest.mark.parametrize("model,ingest", [("resnet20", True), ("resnet20", False),
-                                          ("lenet5", True), ("resnet20", "pack")])
+                                          ("lenet5", True), ("resnet20", "pack"),
+                                          ("resnet20", "pack-inplace"), ("lenet5", "pack")])
 def test_gpu_engine_matches_oracle(broker, model, ingest):
     """Every output record is matched to ITS input by key (output_key=input) and compared on
     logits (centered log-softmax) with a bf16-level relative tolerance: a misrouted batch split
@@ -172,7 +173,7 @@ def test_gpu_engine_matches_oracle(broker, model, ingest):
     image counts on the GPU and the parser reading the device-resident fetch buffer; False: the
     host decode path with per-batch H2D staging; "pack": GPU ingest of nibble-packed fetch
     bodies (the source's PackTap, expanded on the device before the CRC / count / parse)."""
-    pack = ingest == "pack"
+    pack = ingest in ("pack", "pack-inplace")
     if pack and not C.text_pack_fast():
         pytest.skip("no AVX-512 VBMI on this host")
     net = get_model(model)
@@ -188,7 +189,8 @@ def test_gpu_engine_matches_oracle(broker, model, ingest):
     cfg = GaleConfig(topology_name="g", input_topic="in", output_topic="out", model=model,
                      bootstrap=f"127.0.0.1:{broker.port}", start_offset="earliest",
                      max_batch=32, max_wait_us=500, output_key="input",
-                     gpu_ingest=bool(ingest), text_pack=pack)
+                     gpu_ingest=bool(ingest), text_pack=pack,
+                     text_pack_bounce=ingest != "pack-inplace")
     eng = Engine(cfg, devices=[0], max_records=len(counts) + 1, params=params)
     eng.start()
     assert eng.wait(120), eng.stats()
@@ -212,6 +214,9 @@ def test_gpu_engine_matches_oracle(broker, model, ingest):
     assert (st["ingested_records"] > 0) == bool(ingest)
     if pack:  # the text crossed the link packed (~0.5 bytes per fetched byte)
         assert 0 < st["ingest_link_bytes"] < 0.6 * st["ingest_text_bytes"], st
+        # the bounce receive left sparse host copies (nothing needed the text on the host)
+        assert (st["sparse_fetches"] > 0) == (ingest == "pack"), st
+        assert st["restored_fetches"] == 0, st
 
 
 def test_gpu_engine_float_format_java8(broker):
