@@ -98,10 +98,13 @@ def parse_args(argv=None):
     ap.add_argument("--gpu-ingest", action=argparse.BooleanOptionalAction, default=True,
                     help="CRC32C + image counting of fetch buffers on the GPU (host reads only "
                          "Kafka framing)")
-    ap.add_argument("--text-pack", action=argparse.BooleanOptionalAction, default=False,
+    ap.add_argument("--text-pack", action=argparse.BooleanOptionalAction, default=True,
                     help="sources nibble-pack the fetched JSON text for the host->GPU link "
-                         "(expanded on the device; needs AVX-512 VBMI; costs host CPU, "
-                         "profiles/r3_nibble_transport_ab.txt)")
+                         "through a cache-resident receive window (expanded on the device; needs "
+                         "AVX-512 VBMI): half the link and pinned-memory bytes, "
+                         "profiles/r4_ab_step_graph_text_pack.jsonl")
+    ap.add_argument("--text-pack-window-kb", type=int, default=256,
+                    help="bounce receive window per source thread")
     ap.add_argument("--text-pack-bounce", action=argparse.BooleanOptionalAction, default=True,
                     help="with --text-pack: receive through a cache-resident window, keep only "
                          "the packed text + a sparse framing copy in pinned memory")
@@ -654,6 +657,7 @@ def main(argv=None) -> int:
                      decode_threads=a.decode_threads, slo_p99_ms=a.slo_p99_ms,
                      gpu_wait_poll_us=a.gpu_wait_poll_us, gpu_ingest=a.gpu_ingest, gpu_encode=a.gpu_encode,
                      text_pack=a.text_pack, text_pack_bounce=a.text_pack_bounce,
+                     text_pack_window_kb=a.text_pack_window_kb,
                      stub=a.stub, stub_null=a.stub_null, commit_interval_ms=500,
                      check_crcs=a.check_crcs,
                      output_partition=rank if a.local_output and world > 1 else -1,

@@ -40,6 +40,7 @@ EngineConfig config_from_dict(const py::dict& d) {
   opt(d, "pinned_fetch_bytes", c.pinned_fetch_bytes);
   opt(d, "text_pack", c.text_pack);
   opt(d, "text_pack_bounce", c.text_pack_bounce);
+  opt(d, "text_pack_window_kb", c.text_pack_window_kb);
   opt(d, "float_format", c.float_format);
   opt(d, "recv_lowat", c.recv_lowat);
   opt(d, "commit_interval_ms", c.commit_interval_ms);

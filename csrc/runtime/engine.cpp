@@ -670,7 +670,8 @@ void Engine::source_loop(int idx) {
       if (cfg_.text_pack_bounce && cfg_.decode_threads > 0) {
         std::shared_ptr<PinnedPool> pool = pinned;
         cons->set_recv_tap(std::make_shared<BouncePackTap>(
-            pool->chunk_bytes(), [pool](const uint8_t* p) { return pool->owns(p); }));
+            pool->chunk_bytes(), [pool](const uint8_t* p) { return pool->owns(p); }, 64 << 10,
+            (size_t)std::max(4, cfg_.text_pack_window_kb) << 10));
       } else {
         cons->set_recv_tap(std::make_shared<PackTap>(pinned));
       }

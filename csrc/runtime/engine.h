@@ -71,6 +71,7 @@ struct EngineConfig {
   // packed text + a sparse framing copy in the pinned chunk (BouncePackTap, pack_tap.h); false:
   // the body lands in the chunk whole and is packed behind it (PackTap)
   bool text_pack_bounce = true;
+  int text_pack_window_kb = 256;   // the bounce receive window per source (L2 resident)
   // consumers' receive low-water mark (kafka::ClientConfig::recv_lowat), bytes; 0 = off
   int recv_lowat = 0;
   int commit_interval_ms = 2000;   // storm-kafka's ZK commit period

@@ -68,13 +68,14 @@ class GaleConfig:
     check_crcs: bool = True            # Kafka consumer check.crcs
     gpu_ingest: bool = True            # CRC32C + image counts of pinned fetch buffers on the GPU
                                        # (the host reads only Kafka framing; csrc/runtime/ingest.h)
-    text_pack: bool = False            # GPU ingest: sources nibble-pack fetch bodies for the
+    text_pack: bool = True             # GPU ingest: sources nibble-pack fetch bodies for the
                                        # PCIe link, expanded on the device (text_pack.h); needs
                                        # AVX-512 VBMI; for hosts with idle cores behind a
                                        # link-bound GPU (profiles/r3_nibble_transport_ab.txt)
     text_pack_bounce: bool = True      # with text_pack: fetch bodies go through a cache-resident
                                        # window; the pinned chunk gets the packed text and a
                                        # sparse framing copy only (csrc/runtime/pack_tap.h)
+    text_pack_window_kb: int = 256     # that window, per source thread
     # parallelism (R3)
     workers: int = 8                   # NUM_WORKERS: placement only (one process per GPU here)
     source_parallelism: int = 2        # KAFKA_SPOUT_PARAL
@@ -199,7 +200,7 @@ class GaleConfig:
             rebalance_cooldown_ms=self.rebalance_cooldown_ms,
             decode_threads=self.decode_threads, check_crcs=self.check_crcs,
             text_pack=bool(self.gpu_ingest and self.text_pack and _pack_fast()),
-            text_pack_bounce=self.text_pack_bounce,
+            text_pack_bounce=self.text_pack_bounce, text_pack_window_kb=self.text_pack_window_kb,
             acks=self.acks, sink_mode=self.sink_mode, linger_ms=self.linger_ms,
             compression=self.compression,
             value_format=self.value_format, type_id_header=self.type_id_header,
