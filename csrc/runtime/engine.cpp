@@ -305,8 +305,13 @@ void Engine::start() {
     // packed fetch bodies (pack_tap.h) keep their packed copy in the same chunk
     const size_t body = (size_t)cfg_.fetch_max_bytes + (1 << 20);
     const bool pack = cfg_.text_pack && ingest_for((int)i);
+    // a packed chunk holds the body's layout twice over (text region + packed stream): the same
+    // number of fetches in flight needs twice the budget - with the round-3 budget ResNet-50's
+    // 1.7 MB records ran the pool dry and 77 % of them fell back to heap buffers (host staging,
+    // 21.6 vs 31.3 k img/s, profiles/r4_ab_resnet50_lenet_sink.jsonl)
+    const size_t budget = (size_t)cfg_.pinned_fetch_bytes * (pack ? 2 : 1) / nslots;
     pools_[i] = std::make_shared<PinnedPool>(pack ? codec::pack_layout_bytes(body) + 4096 : body,
-                                             (size_t)cfg_.pinned_fetch_bytes / nslots);
+                                             budget);
     if (ingest_for((int)i)) pools_[i]->set_mirror_device(slot_dev_[i]);
   }
   running_ = true;
@@ -1094,7 +1099,7 @@ void Engine::serve(ReplicaSlot* rs) {
         trace::Range tr("gale:batch");
         const int maxb = eff_batch_.load(std::memory_order_relaxed);
         // (no steals with the text packed: a stolen record's host copy is sparse)
-        const bool steal = batchers_.size() > 1 && !cfg_.text_pack;
+        const bool steal = batchers_.size() > 1 && !(cfg_.text_pack && !ingests_.empty());
         open = batchers_[(size_t)rs->slot]->take(maxb,
                                                  eff_wait_ns_.load(std::memory_order_relaxed),
                                                  !mine.empty(), b->recs, images,
@@ -1393,10 +1398,10 @@ void Engine::complete_records(const std::vector<InRecord>& rs, bool ok) {
   t_last_ns_ = now;
   if (ack_log_on_.load(std::memory_order_relaxed)) {
     std::lock_guard<std::mutex> lk(ack_mu_);
-    for (size_t i = 0; i < rs.size() && ack_log_.size() < ack_cap_; ++i)
+    for (size_t i = 0; i < rs.size() && ack_n_ < ack_cap_; ++i)
       if (good[i])
-        ack_log_.push_back({rs[i].partition, rs[i].offset, now, rs[i].t_fetch_ns, rs[i].t_take_ns,
-                            rs[i].t_done_ns});
+        ack_push({rs[i].partition, rs[i].offset, now, rs[i].t_fetch_ns, rs[i].t_take_ns,
+                  rs[i].t_done_ns});
   }
   const int64_t c = completed_ += (int64_t)rs.size();
   const int64_t target = wait_target_.load(std::memory_order_relaxed);
@@ -1425,8 +1430,8 @@ void Engine::complete_record(const InRecord& r, bool ok) {
   t_last_ns_ = now;
   if (ack_log_on_.load(std::memory_order_relaxed) && ok) {
     std::lock_guard<std::mutex> lk(ack_mu_);
-    if (ack_log_.size() < ack_cap_)
-      ack_log_.push_back({r.partition, r.offset, now, r.t_fetch_ns, r.t_take_ns, r.t_done_ns});
+    if (ack_n_ < ack_cap_)
+      ack_push({r.partition, r.offset, now, r.t_fetch_ns, r.t_take_ns, r.t_done_ns});
   }
   const int64_t c = ++completed_;
   const int64_t target = wait_target_.load(std::memory_order_relaxed);
@@ -1439,17 +1444,32 @@ void Engine::complete_record(const InRecord& r, bool ok) {
 void Engine::set_ack_log(bool on, size_t capacity) {
   std::lock_guard<std::mutex> lk(ack_mu_);
   if (on) {
-    ack_log_.clear();
+    ack_n_ = 0;
     ack_cap_ = capacity;
-    ack_log_.reserve(std::min<size_t>(capacity, 4u << 20));
+    // blocks allocated and touched now, before the window: no page faults or copies inside it
+    const size_t nb = (std::min<size_t>(capacity, 16u << 20) + kAckBlock - 1) / kAckBlock;
+    while (ack_blocks_.size() < nb) {
+      ack_blocks_.emplace_back(new AckSample[kAckBlock]);
+      memset(ack_blocks_.back().get(), 0, sizeof(AckSample) * kAckBlock);
+    }
   }
   ack_log_on_ = on;
 }
 
+void Engine::ack_push(const AckSample& a) {
+  const size_t b = ack_n_ / kAckBlock;
+  if (b >= ack_blocks_.size()) ack_blocks_.emplace_back(new AckSample[kAckBlock]);
+  ack_blocks_[b][ack_n_ % kAckBlock] = a;
+  ++ack_n_;
+}
+
 std::vector<AckSample> Engine::take_ack_log() {
   std::lock_guard<std::mutex> lk(ack_mu_);
-  std::vector<AckSample> out;
-  out.swap(ack_log_);
+  std::vector<AckSample> out(ack_n_);
+  for (size_t i = 0; i < ack_n_; i += kAckBlock)
+    memcpy(out.data() + i, ack_blocks_[i / kAckBlock].get(),
+           sizeof(AckSample) * std::min(kAckBlock, ack_n_ - i));
+  ack_n_ = 0;
   return out;
 }
 
@@ -1626,6 +1646,23 @@ std::map<std::string, double> Engine::stats() const {
   s["split_records"] = (double)split_records_;
   s["sparse_fetches"] = (double)sparse_fetches_;
   s["restored_fetches"] = (double)restored_fetches_;
+  {
+    PinnedPool::Stats ps;
+    for (const auto& pool : pools_)
+      if (pool) {
+        const PinnedPool::Stats q = pool->stats();
+        ps.chunks += q.chunks;
+        ps.in_use_max += q.in_use_max;
+        ps.heap_too_large += q.heap_too_large;
+        ps.heap_budget += q.heap_budget;
+        ps.no_mirror += q.no_mirror;
+      }
+    s["pinned_chunks"] = (double)ps.chunks;
+    s["pinned_in_use_max"] = (double)ps.in_use_max;
+    s["pinned_heap_too_large"] = (double)ps.heap_too_large;
+    s["pinned_heap_budget"] = (double)ps.heap_budget;
+    s["pinned_no_mirror"] = (double)ps.no_mirror;
+  }
   s["split_fragments"] = (double)split_fragments_;
   {
     int64_t lag = 0, fetch_lag = 0, lag_max = 0;

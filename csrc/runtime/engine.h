@@ -383,8 +383,14 @@ class Engine {
   std::atomic<int64_t> t_first_ns_{0}, t_last_ns_{0};
   std::atomic<bool> ack_log_on_{false};
   std::mutex ack_mu_;
-  std::vector<AckSample> ack_log_;
+  // fixed-size blocks, never reallocated: a growing vector copied hundreds of MB under ack_mu_
+  // mid-window (at 4 M samples) and stalled every produce callback for ~50 ms - the LeNet-5
+  // "sink tail" of round 3 was that measurement artifact
+  static constexpr size_t kAckBlock = 1 << 16;
+  std::vector<std::unique_ptr<AckSample[]>> ack_blocks_;
+  size_t ack_n_ = 0;
   size_t ack_cap_ = 0;
+  void ack_push(const AckSample& a);  // under ack_mu_
 };
 
 }  // namespace gale

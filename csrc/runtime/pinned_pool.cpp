@@ -3,6 +3,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <unordered_map>
 
 #include "../kafka/client.h"
@@ -17,6 +18,7 @@ struct PinnedPool::State {
   int mirror_device = -1;
   size_t chunk = 0, max_bytes = 0;
   bool closed = false;
+  int64_t in_use = 0, in_use_max = 0, heap_too_large = 0, heap_budget = 0, no_mirror = 0;
   ~State() {
     for (uint8_t* p : all) hipHostFree(p);
     if (mirror_device >= 0 && hipSetDevice(mirror_device) == hipSuccess)
@@ -44,6 +46,17 @@ PinnedPool::PinnedPool(size_t chunk_bytes, size_t max_bytes)
 PinnedPool::~PinnedPool() {
   std::lock_guard<std::mutex> lk(st_->mu);
   st_->closed = true;  // outstanding buffers keep State alive and are freed with it
+}
+
+PinnedPool::Stats PinnedPool::stats() const {
+  std::lock_guard<std::mutex> lk(st_->mu);
+  Stats s;
+  s.chunks = (int64_t)st_->all.size();
+  s.in_use_max = st_->in_use_max;
+  s.heap_too_large = st_->heap_too_large;
+  s.heap_budget = st_->heap_budget;
+  s.no_mirror = st_->no_mirror;
+  return s;
 }
 
 size_t PinnedPool::pinned_bytes() const {
@@ -75,9 +88,16 @@ std::shared_ptr<uint8_t> PinnedPool::alloc(size_t n, bool* pinned) {
           if (st_->mirror_device >= 0 && hipSetDevice(st_->mirror_device) == hipSuccess &&
               hipMalloc(reinterpret_cast<void**>(&d), st_->chunk) == hipSuccess)
             st_->mirrors[p] = d;  // (no mirror: this chunk's records take the host path)
+          else if (st_->mirror_device >= 0)
+            ++st_->no_mirror;
         } else {
           p = nullptr;
         }
+      }
+      if (p) {
+        st_->in_use_max = std::max(st_->in_use_max, ++st_->in_use);
+      } else {
+        ++st_->heap_budget;
       }
     }
     if (p) {
@@ -86,8 +106,12 @@ std::shared_ptr<uint8_t> PinnedPool::alloc(size_t n, bool* pinned) {
       return std::shared_ptr<uint8_t>(p, [st](uint8_t* q) {
         std::lock_guard<std::mutex> lk(st->mu);
         st->free.push_back(q);
+        --st->in_use;
       });
     }
+  } else {
+    std::lock_guard<std::mutex> lk(st_->mu);
+    ++st_->heap_too_large;
   }
   *pinned = false;
   return kafka::heap_alloc(n);

@@ -28,6 +28,11 @@ class PinnedPool {
   size_t chunk_bytes() const { return chunk_; }
   bool owns(const uint8_t* p) const;  // p is the base of one of this pool's pinned chunks
   size_t pinned_bytes() const;
+  // heap fallbacks: requests larger than a chunk / requests past the budget with no chunk free
+  struct Stats {
+    int64_t chunks = 0, in_use_max = 0, heap_too_large = 0, heap_budget = 0, no_mirror = 0;
+  };
+  Stats stats() const;
   // Device mirrors (GPU ingest, ingest.h): every pinned chunk gets a same-size buffer on
   // `device`, at the same offsets. Set before the first alloc. mirror(base) -> nullptr when base
   // is not a pinned chunk of this pool (or mirrors are off).
