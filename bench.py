@@ -117,7 +117,7 @@ def parse_args(argv=None):
     # zero-copy fetch responses, as a Kafka broker serves them (sendfile from the page cache):
     # one host copy less per byte. On boxes whose memory system is loaded it is the difference
     # between 0.98 M (copying, CPU-bound at 16 of 16 cores) and 1.43-1.52 M img/s; on quiet
-    # boxes both sit near the link (profiles/r3_broker_zero_copy_default.jsonl)
+    # boxes both sit near the link (profiles/archive/r3_broker_zero_copy_default.jsonl)
     ap.add_argument("--broker-zero-copy", action=argparse.BooleanOptionalAction, default=True,
                     help="embedded broker sends fetched batches with vmsplice/splice (Kafka's "
                          "sendfile analogue) instead of writev copies")
@@ -129,7 +129,7 @@ def parse_args(argv=None):
                          "Measured on a 16-CPU-quota box: the quota-sized slice (CPUs 0-15) ran "
                          "at 0.69-0.81 M img/s against 1.49 M on the whole node, with the "
                          "consumer's loopback receive costing 2.3x the cores "
-                         "(profiles/r3_pinning_ab.txt); the default stays the whole node")
+                         "(profiles/archive/r3_pinning_ab.txt); the default stays the whole node")
     ap.add_argument("--gpu-wait-poll-us", type=int, default=20,
                     help="replica workers sleep-poll batch completion every N us (0 = spin)")
     ap.add_argument("--encode-threads", type=int, default=0,
@@ -526,17 +526,17 @@ def main(argv=None) -> int:
     # copy bandwidth and GPU-ingest round trips, not by the total core count: with >= 16 cores
     # per GPU, 12 input partitions (TCP connections), 6 replica streams and 4 ingest workers
     # saturate the share (1.47 M img/s vs 0.97 M with 4/4/2 on one MI355X box,
-    # profiles/r2_host_pipeline_shape_ab.txt); smaller shares keep ~4 cores per replica.
+    # profiles/archive/r2_host_pipeline_shape_ab.txt); smaller shares keep ~4 cores per replica.
     # ResNet-50 records are 1.7 MB of JSON each: the GPU, not the host, sets the pace unless the
     # batches are full, so fewer replicas wait longer for full 256-image batches while 12
     # partitions keep the fetches parallel (29.0 k img/s vs 23.8 k with the CIFAR sizing,
-    # profiles/r2_configs_1_4_e2e.txt)
+    # profiles/archive/r2_configs_1_4_e2e.txt)
     r50 = a.model == "resnet50"
     if a.step_images <= 0:
         # 262144-image steps: ~0.18 s each at 1.5 M img/s (20 steps ~3.6 s), long enough that a
         # single 10-50 ms host hiccup (scheduler, page-cache, neighbour tenants) moves a step's
         # rate by a few percent rather than 10-20 % (131072-image steps: spread 9-20 %,
-        # profiles/r3_final_check_session2.jsonl); LeNet-5 runs at > 4 M img/s
+        # profiles/archive/r3_final_check_session2.jsonl); LeNet-5 runs at > 4 M img/s
         a.step_images = 4096 if r50 else 262144
     if a.distinct <= 0:
         a.distinct = 256 if r50 else 65536
@@ -557,7 +557,7 @@ def main(argv=None) -> int:
     if a.decode_threads <= 0:
         # 6 GPU-ingest workers keep more H2D copies in flight on the host link than 4 (higher
         # throughput in 5 of 6 interleaved pairs on two boxes, p50 unchanged; see
-        # profiles/r3_decode_threads_ab.txt)
+        # profiles/archive/r3_decode_threads_ab.txt)
         a.decode_threads = 6 if big else 2
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))

@@ -5,7 +5,7 @@
 //     0 1 2 3 4 5 6 7 8 9 [ ] , - . E
 // so a 4-bit code carries it losslessly. On one MI355X the headline path is bound by the PCIe
 // link (the fetched text crosses it once, 54 of ~55.5 GB/s measured pinned H2D at 1.56 M img/s,
-// profiles/r3_bench_session2_start.jsonl); packing the text 2:1 on the host before the DMA and
+// profiles/archive/r3_bench_session2_start.jsonl); packing the text 2:1 on the host before the DMA and
 // expanding it on the device (text_unpack in csrc/kernels/ingest.hip) halves the link bytes at
 // the price of one more host pass (opt-in, see csrc/runtime/pack_tap.h for the measured trade). The
 // device then holds the exact fetched bytes again: the batch CRC32Cs are checked over the

@@ -90,7 +90,7 @@ class Executor {
   // Plans of at most kMaxDirectOps kernels (the whole-network ResNet-20 kernel) always launch
   // directly: a graph saves nothing there, runs the padded bucket batch, and every replay costs
   // CPU on the HIP runtime's worker thread (~0.9 core at the serving rate, -> 0.16 with direct
-  // launches, tools/gpu/r3_probe.sh).
+  // launches, measured in round 3).
   static constexpr size_t kMaxDirectOps = 2;
   bool graph_pays() const { return spec_.ops.size() > kMaxDirectOps; }
   void run(int slot, int batch, hipStream_t stream, bool use_graph);

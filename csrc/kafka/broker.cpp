@@ -640,7 +640,7 @@ bool Broker::flush(Conn& c) {
     // at most kWriteBurstBytes per call (the splice path moves one pipe's worth, 1 MiB): the
     // loopback device queues a sender's segments on its CPU's backlog (netdev_max_backlog
     // packets), and a multi-MB burst overflows it whenever softirq work is deferred - every
-    // drop is a retransmission, a 10-200 ms latency tail (tools/gpu/r3_tail_tcp.sh)
+    // drop is a retransmission, a 10-200 ms latency tail (profiles/archive/r3_tail_tcp.txt)
     iovec iov[64];
     int n = 0;
     size_t burst = 0;

@@ -666,7 +666,7 @@ void Producer::run() {
             // accumulated behind a busy sender leaves in request-sized batches, so a request
             // (and the bytes awaiting acks, max_in_flight of them) stays bounded instead of
             // growing with the backlog (one 30 MB batch per request was 0.5-1 s of ack latency
-            // at saturation, profiles/r2_producer_request_ab.txt)
+            // at saturation, profiles/archive/r2_producer_request_ab.txt)
             size_t total = 0;
             std::vector<Pending> chunk;
             size_t cbytes = 0;

@@ -64,7 +64,7 @@ __device__ __forceinline__ void glds16(const void* src, void* lds_base) {
 // plus the residual per 16 KB of input), which more resident workgroups overlap.
 // (Variants measured and removed in round 3 - 256 x 128 tiles with 8 waves, a three-stage
 // 128 x 64 ring, register staging instead of LDS-DMA, the single-stage form for 2-4 k-steps: all
-// slower at ResNet-50 batch 256, profiles/r2_resnet50_gemm_ab.txt.)
+// slower at ResNet-50 batch 256, profiles/archive/r2_resnet50_gemm_ab.txt.)
 template <int BM, int BN, bool STEM, int NST>
 __global__ __launch_bounds__(256, NST == 1 ? 4 : 2)
 void conv_gemm_kernel(GemmConvArgs a) {
@@ -176,7 +176,7 @@ void conv_gemm_kernel(GemmConvArgs a) {
   // epilogue geometry (see below) and the residual prefetch: the residual rows this lane will
   // add are loaded into registers while the last k-step's MFMAs run, so their DRAM latency is
   // hidden instead of stalling the epilogue (the 1x1 expansion convs with a shortcut were
-  // latency-bound at ~3 TB/s, profiles/r2_resnet50_layers_pmc.txt)
+  // latency-bound at ~3 TB/s, profiles/archive/r2_resnet50_layers_pmc.txt)
   constexpr bool PREF = NST >= 2;
   constexpr int CW = BN / WN;      // channels per wave
   constexpr int EPS = CW + 4;      // fp32 row stride (+16 B: conflict-free 16-row writes)
@@ -314,7 +314,7 @@ bool conv_gemm_supported(const ConvDesc& d, int batch, bool has_res) {
   if (has_res && (d.res_C != d.Cout || d.res_stride != 1 || d.res_H != d.Ho || d.res_W != d.Wo))
     return false;
   // 32-bit element offsets inside the kernel. (No minimum size: measured faster than conv_mfma
-  // from ResNet-50 batch 64 up, including the 98-tile stage-4 layers, profiles/r1_resnet50_*.)
+  // from ResNet-50 batch 64 up, including the 98-tile stage-4 layers, profiles/archive/r1_resnet50_*.)
   const long long m = (long long)batch * d.Ho * d.Wo;
   return m < (1ll << 31) && (long long)batch * d.H * d.W * d.Cin < (1ll << 31);
 }

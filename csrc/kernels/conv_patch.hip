@@ -4,7 +4,7 @@
 // Why: in conv_gemm.hip every k-step stages the im2col rows of ONE tap, so each input pixel
 // crosses the vector-memory return path (TA/TD -> LDS) nine times per 64 input channels. The
 // per-layer counters show that path, not the MFMA, binding those layers: TD busy 0.6-0.75 of
-// the CU cycles against MFMA busy 22-28 % (profiles/r2_resnet50_layers_mem_pmc.txt).
+// the CU cycles against MFMA busy 22-28 % (profiles/archive/r2_resnet50_layers_mem_pmc.txt).
 //
 // Here a workgroup owns TR whole output rows of one image (TR*W <= 128 pixels: 2 x 56,
 // 4 x 28, 7 x 14) and BN output channels. Per 64-channel input block it stages the
@@ -57,7 +57,7 @@ struct PatchArgs {
 // wave-instruction); compile-time so the two stages are static LDS (2 workgroups per CU).
 // (Variants measured and removed in round 3 - 256-row tiles with 8 waves, 64-channel tiles with
 // one patch buffer at 4 workgroups per CU, two taps per k-step: none faster than these tiles,
-// profiles/r2_conv_patch.txt.)
+// profiles/archive/r2_conv_patch.txt.)
 template <int BN, int PRR>
 __global__ __launch_bounds__(256, 2)
 void conv_patch_kernel(PatchArgs a) {
@@ -305,7 +305,7 @@ int patch_bn(const ConvDesc& d) { return (d.Npad % 128 == 0) ? 128 : 64; }
 // conv_patch mode (set_conv_patch): 0 off, 1 (default) the 128-channel tiles (ResNet-50 28x28
 // and 14x14 conv2: 90 -> 77 us and 86 -> 76 us per layer at batch 256), 2 also the 64-channel
 // tiles (the 56x56 conv2 measured 104-110 -> 125-127 us there: one input block per tile leaves
-// the patch load exposed, so those stay on conv_gemm; profiles/r2_conv_patch.txt)
+// the patch load exposed, so those stay on conv_gemm; profiles/archive/r2_conv_patch.txt)
 static std::atomic<int> g_conv_patch{1};
 
 void set_conv_patch(int mode) { g_conv_patch = mode; }

@@ -58,7 +58,7 @@ struct Lay {
 // positions of the 256-B bank row; the row strides (872 B = 109 x 8 B: two rows for conv 13's
 // stride-2 reads land on the other half of the positions; 896 B = 128 mod 256: stage 3's second
 // tile row) keep multi-row tiles disjoint too. (Dense fp8 pixels of 32 / 64 B: 2- and 4-way, 14
-// extra LDS cycles per LDS instruction measured, profiles/r3_resnet20_fp8_lds.txt.)
+// extra LDS cycles per LDS instruction measured, profiles/archive/r3_resnet20_fp8_lds.txt.)
 template <bool F8>
 struct Layouts {
   typedef Lay<16, 34 * 16> S1;  // 34x34x16
@@ -612,9 +612,9 @@ hipError_t resnet20_fused_forward(const ResNet20Params& p, int batch, const floa
   // of LDS would allow 4, but the hoisted A fragments need more than 128 VGPRs per lane), or 1 of
   // 8 waves. bf16 with no more images than CUs: the 8-wave form (each image gets twice the
   // waves, weights prefetched into LDS; measured 62.3 -> 58.0 us at batch 1,
-  // profiles/r1_resnet20_waves_ab.txt). fp8 stays on 4 waves (its 8-wave form measured slower in
+  // profiles/archive/r1_resnet20_waves_ab.txt). fp8 stays on 4 waves (its 8-wave form measured slower in
   // round 1 and equal after the round-3 LDS layout fix: 50.9 / 53.1 vs 50.7 / 52.7 us at batch
-  // 64 / 256, profiles/r3_resnet20_fp8_lds.txt).
+  // 64 / 256, profiles/archive/r3_resnet20_fp8_lds.txt).
   const int nw = !f8 && batch <= cus ? 8 : 4;
   const int grid_cap = nw == 8 ? cus : 2 * cus;
   const int grid = batch < grid_cap ? batch : grid_cap;

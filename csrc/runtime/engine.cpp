@@ -313,6 +313,7 @@ void Engine::start() {
     pools_[i] = std::make_shared<PinnedPool>(pack ? codec::pack_layout_bytes(body) + 4096 : body,
                                              budget);
     if (ingest_for((int)i)) pools_[i]->set_mirror_device(slot_dev_[i]);
+    pools_[i]->set_wait_ms(200);
   }
   running_ = true;
   stopping_ = false;
@@ -1208,7 +1209,7 @@ void Engine::slo_step() {
   // Batches leaving (nearly) full: they form faster than the window, so the latency is set by
   // the replicas' capacity, not by batching delay - shrinking them would only cut capacity (the
   // fp8 ResNet-20 at 1.0 M img/s fell into that cycle: mean batch 256 -> 110, p99 2 -> 8-60 ms,
-  // profiles/r2_slo_controller_ab.txt).
+  // profiles/archive/r2_slo_controller_ab.txt).
   const bool full = mean_batch >= 0.9 * b;
   if (p99_ms > cfg_.slo_p99_ms) {
     if (backlog || full) {
@@ -1656,12 +1657,16 @@ std::map<std::string, double> Engine::stats() const {
         ps.heap_too_large += q.heap_too_large;
         ps.heap_budget += q.heap_budget;
         ps.no_mirror += q.no_mirror;
+        ps.waits += q.waits;
+        ps.wait_us += q.wait_us;
       }
     s["pinned_chunks"] = (double)ps.chunks;
     s["pinned_in_use_max"] = (double)ps.in_use_max;
     s["pinned_heap_too_large"] = (double)ps.heap_too_large;
     s["pinned_heap_budget"] = (double)ps.heap_budget;
     s["pinned_no_mirror"] = (double)ps.no_mirror;
+    s["pinned_waits"] = (double)ps.waits;
+    s["pinned_wait_s"] = (double)ps.wait_us * 1e-6;
   }
   s["split_fragments"] = (double)split_fragments_;
   {

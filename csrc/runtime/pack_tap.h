@@ -7,7 +7,7 @@
 //
 // Off by default (EngineConfig::text_pack): it halves the PCIe bytes, but on the bench's 16-CPU
 // share, which also runs the embedded broker, the extra pass makes the pipeline CPU-bound
-// (1.21-1.26 vs 1.55 M img/s, profiles/r3_nibble_transport_ab.txt). It is for hosts with cores
+// (1.21-1.26 vs 1.55 M img/s, profiles/archive/r3_nibble_transport_ab.txt). It is for hosts with cores
 // to spare behind a link-bound GPU (a remote Kafka cluster leaves ~10 of 16 cores idle).
 #pragma once
 #include <string.h>

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <unordered_map>
 
 #include "../kafka/client.h"
@@ -12,6 +13,9 @@ namespace gale {
 
 struct PinnedPool::State {
   std::mutex mu;
+  std::condition_variable freed;
+  int wait_ms = 0;
+  int64_t waits = 0, wait_us = 0;
   std::vector<uint8_t*> free;
   std::vector<uint8_t*> all;
   std::unordered_map<const uint8_t*, uint8_t*> mirrors;  // pinned chunk -> device mirror
@@ -25,6 +29,11 @@ struct PinnedPool::State {
       for (auto& kv : mirrors) hipFree(kv.second);
   }
 };
+
+void PinnedPool::set_wait_ms(int ms) {
+  std::lock_guard<std::mutex> lk(st_->mu);
+  st_->wait_ms = ms;
+}
 
 void PinnedPool::set_mirror_device(int device) {
   std::lock_guard<std::mutex> lk(st_->mu);
@@ -46,6 +55,7 @@ PinnedPool::PinnedPool(size_t chunk_bytes, size_t max_bytes)
 PinnedPool::~PinnedPool() {
   std::lock_guard<std::mutex> lk(st_->mu);
   st_->closed = true;  // outstanding buffers keep State alive and are freed with it
+  st_->freed.notify_all();
 }
 
 PinnedPool::Stats PinnedPool::stats() const {
@@ -56,6 +66,8 @@ PinnedPool::Stats PinnedPool::stats() const {
   s.heap_too_large = st_->heap_too_large;
   s.heap_budget = st_->heap_budget;
   s.no_mirror = st_->no_mirror;
+  s.waits = st_->waits;
+  s.wait_us = st_->wait_us;
   return s;
 }
 
@@ -75,7 +87,20 @@ std::shared_ptr<uint8_t> PinnedPool::alloc(size_t n, bool* pinned) {
   if (n + 64 <= chunk_) {
     uint8_t* p = nullptr;
     {
-      std::lock_guard<std::mutex> lk(st_->mu);
+      std::unique_lock<std::mutex> lk(st_->mu);
+      if (st_->free.empty() && (st_->all.size() + 1) * st_->chunk > st_->max_bytes &&
+          st_->wait_ms > 0 && !st_->closed) {
+        // budget spent: wait for a release rather than stage this fetch through the heap (a
+        // heap buffer takes the host decode path, which is slower and so holds records, and
+        // with them chunks, longer - the pool would not recover)
+        const auto t0 = std::chrono::steady_clock::now();
+        ++st_->waits;
+        st_->freed.wait_for(lk, std::chrono::milliseconds(st_->wait_ms),
+                            [&] { return !st_->free.empty() || st_->closed; });
+        st_->wait_us += std::chrono::duration_cast<std::chrono::microseconds>(
+                            std::chrono::steady_clock::now() - t0)
+                            .count();
+      }
       if (!st_->free.empty()) {
         p = st_->free.back();
         st_->free.pop_back();
@@ -104,9 +129,12 @@ std::shared_ptr<uint8_t> PinnedPool::alloc(size_t n, bool* pinned) {
       *pinned = true;
       std::shared_ptr<State> st = st_;
       return std::shared_ptr<uint8_t>(p, [st](uint8_t* q) {
-        std::lock_guard<std::mutex> lk(st->mu);
-        st->free.push_back(q);
-        --st->in_use;
+        {
+          std::lock_guard<std::mutex> lk(st->mu);
+          st->free.push_back(q);
+          --st->in_use;
+        }
+        st->freed.notify_one();
       });
     }
   } else {

@@ -10,6 +10,7 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include <condition_variable>
 #include <memory>
 #include <mutex>
 #include <vector>
@@ -31,12 +32,16 @@ class PinnedPool {
   // heap fallbacks: requests larger than a chunk / requests past the budget with no chunk free
   struct Stats {
     int64_t chunks = 0, in_use_max = 0, heap_too_large = 0, heap_budget = 0, no_mirror = 0;
+    int64_t waits = 0, wait_us = 0;
   };
   Stats stats() const;
   // Device mirrors (GPU ingest, ingest.h): every pinned chunk gets a same-size buffer on
   // `device`, at the same offsets. Set before the first alloc. mirror(base) -> nullptr when base
   // is not a pinned chunk of this pool (or mirrors are off).
   void set_mirror_device(int device);
+  // Backpressure: with the budget spent and no chunk free, alloc waits up to `ms` for one to be
+  // released before it falls back to the heap (0 = fall back at once).
+  void set_wait_ms(int ms);
   uint8_t* mirror(const uint8_t* base) const;
 
  private:

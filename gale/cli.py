@@ -100,7 +100,7 @@ def cmd_run(argv: List[str]) -> int:
 
         # one HW queue per HIP stream in the profiled child: rocprofv3's queue interception
         # crashed when several of the engine's streams shared a HW queue and submitted
-        # concurrently (GPU_MAX_HW_QUEUES=4 default; profiles/r3_e2e_kernel_stats_default.csv)
+        # concurrently (GPU_MAX_HW_QUEUES=4 default; profiles/archive/r3_e2e_kernel_stats_default.csv)
         env = dict(os.environ)
         env.setdefault("GPU_MAX_HW_QUEUES", "32")
         return subprocess.call(profile_command(cfg, argv), env=env)

@@ -52,6 +52,10 @@ class GaleConfig:
     fetch_max_wait_ms: int = 20        # Kafka fetch.max.wait.ms
     recv_lowat_kb: int = 0             # consumers wake per this many KB of a large fetch
                                        # response (SO_RCVLOWAT per receive call); 0 = per segment
+    fetch_max_kb: int = 16384          # Kafka fetch.max.bytes (per fetch response)
+    partition_max_kb: int = 8192       # Kafka max.partition.fetch.bytes
+    pinned_fetch_mb: int = 4096        # pinned fetch-buffer budget per GPU (x2 with text_pack);
+                                       # when it is spent the sources wait for a free buffer
     # elastic data parallelism: every process of the group shares the input partitions through
     # Kafka consumer-group membership; dead members' partitions move to the survivors
     group_membership: bool = False
@@ -71,7 +75,7 @@ class GaleConfig:
     text_pack: bool = True             # GPU ingest: sources nibble-pack fetch bodies for the
                                        # PCIe link, expanded on the device (text_pack.h); needs
                                        # AVX-512 VBMI; for hosts with idle cores behind a
-                                       # link-bound GPU (profiles/r3_nibble_transport_ab.txt)
+                                       # link-bound GPU (profiles/archive/r3_nibble_transport_ab.txt)
     text_pack_bounce: bool = True      # with text_pack: fetch bodies go through a cache-resident
                                        # window; the pinned chunk gets the packed text and a
                                        # sparse framing copy only (csrc/runtime/pack_tap.h)
@@ -193,6 +197,9 @@ class GaleConfig:
             commit_interval_ms=self.commit_interval_ms, sink_parallelism=self.sink_parallelism,
             fetch_min_bytes=self.fetch_min_bytes, fetch_max_wait_ms=self.fetch_max_wait_ms,
             recv_lowat=self.recv_lowat_kb << 10,
+            fetch_max_bytes=self.fetch_max_kb << 10,
+            partition_max_bytes=self.partition_max_kb << 10,
+            pinned_fetch_bytes=self.pinned_fetch_mb << 20,
             group_membership=self.group_membership, session_timeout_ms=self.session_timeout_ms,
             rebalance_timeout_ms=self.rebalance_timeout_ms,
             heartbeat_interval_ms=self.heartbeat_interval_ms, assignor=self.assignor,

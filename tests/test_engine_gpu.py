@@ -496,3 +496,41 @@ def test_gpu_step_graph_equals_eager(model):
         b.stop()
     assert outs[True] == outs[False] and len(outs[True]) == len(recs)
     assert b"error" in outs[True][b"bad"]
+
+
+def test_gpu_pinned_pool_backpressure(broker):
+    """A pinned-fetch budget of two buffers: when both are held by queued records the sources
+    wait for one to be released instead of staging fetches through the heap (which would send
+    those records down the host path and, under load, keep the pool exhausted - the ResNet-50
+    regression of profiles/r4_ab_resnet50_lenet_sink.jsonl). Every record is still served by GPU
+    ingest, correctly."""
+    if not C.text_pack_fast():
+        pytest.skip("no AVX-512 VBMI on this host")
+    net = get_model("resnet20")
+    params = init_params(net, seed=0, calib_batch=16)
+    rng = np.random.default_rng(5)
+    xs = {}
+    for i in range(120):
+        x = rng.random((1 + i % 3,) + net.input_shape, dtype=np.float32)
+        xs[f"b{i}".encode()] = x
+        broker.append("in", 0, [C.encode_instances(x)], [f"b{i}".encode()])
+    # 128 KB fetches: a packed chunk is 2.37 MB, so 3 MB (x2 with the pack) = 2 chunks
+    cfg = GaleConfig(topology_name="g", input_topic="in", output_topic="out", model="resnet20",
+                     bootstrap=f"127.0.0.1:{broker.port}", start_offset="earliest",
+                     max_batch=32, max_wait_us=500, output_key="input", gpu_ingest=True,
+                     text_pack=True, fetch_max_kb=128, partition_max_kb=128, pinned_fetch_mb=3)
+    eng = Engine(cfg, devices=[0], max_records=len(xs), params=params)
+    eng.start()
+    assert eng.wait(120), eng.stats()
+    eng.stop()
+    st = eng.stats()
+    out = {r["key"]: r["value"] for r in broker.read("out", 0)}
+    assert set(out) == set(xs)
+    folded = fold_params(net, params)
+    for k in list(xs)[::7]:
+        ref = centered_log(forward(net, folded, torch.from_numpy(xs[k])).numpy())
+        got = centered_log(json.loads(out[k])["predictions"])
+        assert np.abs(got - ref).max() / max(np.abs(ref).max(), 1.0) < 2e-2, k
+    assert st["pinned_chunks"] <= 2, st
+    assert st["pinned_heap_budget"] == 0 and st["pinned_heap_too_large"] == 0, st
+    assert st["ingested_records"] == st["records_in"] == len(xs), st
