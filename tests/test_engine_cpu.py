@@ -431,3 +431,26 @@ def test_split_record_with_a_bad_fragment_is_one_error(broker):
     eng, out = run(broker, 1, output_key="input", on_error="error-json")
     assert len(out) == 1 and json.loads(out[0]["value"])["error"] in ("bad_number", "bad_shape")
     assert eng.stats()["errors"] == 1
+
+
+def test_ack_log_spans_blocks(broker):
+    """The produce-ack log (the latency join's engine side) is kept in fixed 64 Ki-sample blocks
+    allocated before the window, so a long window never reallocates under the ack lock (a 4 M
+    sample realloc was a 50 ms stall, the LeNet-5 p99 of round 3). 150 000 acks span three blocks
+    and all come back, once each."""
+    batch = K.encode_batch([(None, b"x", -1, None)] * 1000, 0, 0)
+    broker.append_batch_repeated("in", 0, batch, 75)
+    broker.append_batch_repeated("in", 1, batch, 75)
+    n = 150_000
+    eng = Engine(make_cfg(broker, queue_depth=4096, max_batch=256), max_records=n)
+    eng.set_ack_log(True, capacity=1 << 20)
+    eng.start()
+    assert eng.wait(120), eng.stats()
+    eng.stop()
+    part, off, t_ack = (np.asarray(v) for v in eng.take_ack_log()[:3])
+    assert len(part) == n
+    for p in (0, 1):
+        o = off[part == p]
+        assert sorted(o.tolist()) == list(range(75_000)), p
+    assert np.all(t_ack > 0)
+    assert len(eng.take_ack_log()[0]) == 0  # taken: the log is empty again

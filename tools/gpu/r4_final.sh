@@ -1,8 +1,9 @@
 #!/bin/bash
 # Round-4 evidence on ONE box: every BASELINE config 3 runs back to back (the README tables are
 # the medians of these), GPU tests + smoke, the plain multi-GPU entry point, a kernel trace.
-#   PART=a  pytest -m gpu, smoke, config 2 (ResNet-20 bf16) x3, config 5 (fp8) x3
-#   PART=b  config 1 (LeNet-5) x3, config 4 (ResNet-50) x3, bench.py --gpus 2 (rehearsal / refusal),
+#   PART=a  pytest -m gpu, smoke, config 2 (ResNet-20 bf16) x3, config 1 (LeNet-5) x3
+#   PART=b  config 5 (p99 SLO 2 ms) fp8 x3 and bf16 x3, config 4 (ResNet-50) x3,
+#           bench.py --gpus 2 (rehearsal / refusal),
 #           kernel trace of the default bench, forward-alone ResNet-50 / ResNet-20
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
@@ -35,9 +36,12 @@ if [ "${PART:-a}" = a ]; then
       > $out/smoke.log 2>&1 || { tail -20 $out/smoke.log; exit 1; }
   tail -1 $out/smoke.log
   for i in 1 2 3; do one c2_bf16_$i 240 --steps 20 --warmup 5 || exit 1; done
-  for i in 1 2 3; do one c5_fp8_$i 240 --steps 20 --warmup 5 --dtype fp8 || exit 1; done
-else
   for i in 1 2 3; do one c1_lenet5_$i 240 --model lenet5 --steps 20 --warmup 5 --latency-load 0.9 || exit 1; done
+else
+  for i in 1 2 3; do  # fp8 and bf16 interleaved
+    one c5_fp8_slo2_$i 240 --steps 20 --warmup 5 --dtype fp8 --slo-p99-ms 2 || exit 1
+    one c5_bf16_slo2_$i 240 --steps 20 --warmup 5 --slo-p99-ms 2 || exit 1
+  done
   for i in 1 2 3; do one c4_resnet50_$i 300 --model resnet50 --steps 10 --warmup 3 || exit 1; done
   # the driver's multi-GPU entry point on a 1-GPU box: more ranks than GPUs must be refused,
   # and the same entry point with --shared-gpu-rehearsal runs both ranks (gloo, one GPU)
