@@ -103,6 +103,8 @@ def parse_args(argv=None):
                          "through a cache-resident receive window (expanded on the device; needs "
                          "AVX-512 VBMI): half the link and pinned-memory bytes, "
                          "profiles/r4_ab_step_graph_text_pack.jsonl")
+    ap.add_argument("--pinned-fetch-mb", type=int, default=4096,
+                    help="pinned fetch-buffer budget per GPU (doubled with --text-pack)")
     ap.add_argument("--text-pack-window-kb", type=int, default=256,
                     help="bounce receive window per source thread")
     ap.add_argument("--text-pack-bounce", action=argparse.BooleanOptionalAction, default=True,
@@ -658,6 +660,7 @@ def main(argv=None) -> int:
                      gpu_wait_poll_us=a.gpu_wait_poll_us, gpu_ingest=a.gpu_ingest, gpu_encode=a.gpu_encode,
                      text_pack=a.text_pack, text_pack_bounce=a.text_pack_bounce,
                      text_pack_window_kb=a.text_pack_window_kb,
+                     pinned_fetch_mb=a.pinned_fetch_mb,
                      stub=a.stub, stub_null=a.stub_null, commit_interval_ms=500,
                      check_crcs=a.check_crcs,
                      output_partition=rank if a.local_output and world > 1 else -1,

@@ -27,6 +27,10 @@ def main():
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp8"])
     ap.add_argument("--conv-path", type=int, default=0,
                     help="0 auto, 1 conv_mfma only, 2 GEMM conv wherever the shape allows")
+    ap.add_argument("--streams", type=int, default=1,
+                    help="batches in flight at once, one replica slot and HIP stream each (the "
+                         "serving engine keeps 2 per replica): whole-GPU throughput when a "
+                         "memory-bound layer of one batch overlaps a compute-bound one of another")
     ap.add_argument("--chunk", default="",
                     help="LAYER:N - layers before LAYER run per chunk of N images "
                          "(PlanSpec::chunk_ops)")
@@ -41,22 +45,27 @@ def main():
     if a.chunk:
         name, n = a.chunk.split(":")
         chunk = ([L.name for L in net.layers].index(name), int(n))
-    rep = ModelReplica(net, packed, max_batch=max(bs), slots=1, buckets=bs, wdtype=a.dtype,
+    ns = max(1, a.streams)
+    rep = ModelReplica(net, packed, max_batch=max(bs), slots=ns, buckets=bs, wdtype=a.dtype,
                        chunk=chunk)
-    s = torch.cuda.current_stream().cuda_stream
+    streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(ns - 1)]
+    ss = [st.cuda_stream for st in streams]
     res = []
     for b in bs:
         for _ in range(3):
-            rep.executor.run(0, b, s, not a.eager)
+            for k in range(ns):
+                rep.executor.run(k, b, ss[k], not a.eager)
         torch.cuda.synchronize()
         t = time.perf_counter()
         for _ in range(a.iters):
-            rep.executor.run(0, b, s, not a.eager)
+            for k in range(ns):
+                rep.executor.run(k, b, ss[k], not a.eager)
         torch.cuda.synchronize()
-        dt = (time.perf_counter() - t) / a.iters
+        dt = (time.perf_counter() - t) / a.iters / ns  # per batch
         flops = 2 * net.macs_per_image() * b
         r = dict(model=a.model, dtype=a.dtype, conv_path=a.conv_path, batch=b, ms=dt * 1e3,
-                 img_s=b / dt, tflops=flops / dt / 1e12, graph=not a.eager, chunk=a.chunk)
+                 img_s=b / dt, tflops=flops / dt / 1e12, graph=not a.eager, chunk=a.chunk,
+                 streams=ns)
         res.append(r)
         print(json.dumps(r), flush=True)
 

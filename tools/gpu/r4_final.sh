@@ -5,6 +5,7 @@
 #   PART=b  config 5 (p99 SLO 2 ms) fp8 x3 and bf16 x3, config 4 (ResNet-50) x3,
 #           bench.py --gpus 2 (rehearsal / refusal),
 #           kernel trace of the default bench, forward-alone ResNet-50 / ResNet-20
+#   PART=c  only the kernel trace and the forward-alone runs
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 out=gpurun_out/final
@@ -37,7 +38,7 @@ if [ "${PART:-a}" = a ]; then
   tail -1 $out/smoke.log
   for i in 1 2 3; do one c2_bf16_$i 240 --steps 20 --warmup 5 || exit 1; done
   for i in 1 2 3; do one c1_lenet5_$i 240 --model lenet5 --steps 20 --warmup 5 --latency-load 0.9 || exit 1; done
-else
+elif [ "$PART" = b ]; then
   for i in 1 2 3; do  # fp8 and bf16 interleaved
     one c5_fp8_slo2_$i 240 --steps 20 --warmup 5 --dtype fp8 --slo-p99-ms 2 || exit 1
     one c5_bf16_slo2_$i 240 --steps 20 --warmup 5 --slo-p99-ms 2 || exit 1
@@ -50,13 +51,24 @@ else
   fi
   tail -2 $out/gpus2_refused.log
   one rehearsal_world2 300 --gpus 2 --shared-gpu-rehearsal --steps 10 --warmup 3 || exit 1
+fi
+if [ "${PART:-a}" = b ] || [ "${PART:-a}" = c ]; then
   export TMPDIR=/tmp
+  # one hardware queue per HIP stream under the profiler: its queue interception crashed when
+  # the engine's streams (replicas + ingest lanes, > 4 from several threads) shared HIP's
+  # default 4 (a SIGSEGV inside librocprofiler-sdk under GpuIngest::run,
+  # gpurun_out/final/prof_bench.log); the same setting gale's --profile uses
+  export GPU_MAX_HW_QUEUES=32
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out/prof -o run -- \
       python bench.py --steps 10 --warmup 3 --latency-load 0 > $out/prof_bench.log 2>&1 || exit 1
-  python tools/prof_summary.py $(find $out/prof -name '*.db' | head -1) --top 14 > $out/kernel_stats.txt
-  head -8 $out/kernel_stats.txt
+  db=$(find $out/prof -name '*.db' | head -1)
+  python tools/prof_summary.py $db --top 14 > $out/kernel_stats.txt
+  python tools/prof_summary.py $db --busy --top 14 > $out/kernel_busy.txt
+  head -8 $out/kernel_stats.txt; cat $out/kernel_busy.txt
   timeout -k 10 240 python tools/bench_forward.py --model resnet50 --batches 64,256 --iters 30 \
       > $out/forward_resnet50.jsonl 2> $out/forward.err || exit 1
+  timeout -k 10 240 python tools/bench_forward.py --model resnet50 --batches 256 --iters 30 \
+      --streams 2 >> $out/forward_resnet50.jsonl 2>> $out/forward.err || exit 1
   timeout -k 10 240 python tools/bench_forward.py --model resnet20 --batches 256,4096 --iters 50 \
       > $out/forward_resnet20.jsonl 2>> $out/forward.err || exit 1
   timeout -k 10 240 python tools/bench_forward.py --model resnet20 --dtype fp8 --batches 256,4096 \

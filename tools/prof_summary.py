@@ -7,14 +7,53 @@ import argparse
 import sqlite3
 
 
+def busy(c, top):
+    ev = []
+    for name, st, en in c.execute("select name, start, end from kernels where end > start"):
+        ev.append((st, 1, name))
+        ev.append((en, -1, name))
+    if not ev:
+        print("no kernels")
+        return
+    ev.sort(key=lambda e: (e[0], e[1]))
+    active = {}
+    share = {}
+    busy_ns = 0
+    t_prev = ev[0][0]
+    for t, d, name in ev:
+        k = sum(active.values())
+        if k and t > t_prev:
+            seg = t - t_prev
+            busy_ns += seg
+            for n, m in active.items():
+                share[n] = share.get(n, 0.0) + seg * m / k
+        t_prev = t
+        active[name] = active.get(name, 0) + d
+        if active[name] == 0:
+            del active[name]
+    span = ev[-1][0] - ev[0][0]
+    print(f"span_ms,{span / 1e6:.1f},busy_ms,{busy_ns / 1e6:.1f},busy_pct,{100 * busy_ns / span:.1f}")
+    print("kernel,attributed_us,pct_of_busy")
+    for name, v in sorted(share.items(), key=lambda kv: -kv[1])[:top]:
+        short = name if len(name) < 110 else name[:107] + "..."
+        print(f'"{short}",{v / 1e3:.1f},{100 * v / busy_ns:.1f}')
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("db")
     ap.add_argument("--top", type=int, default=25)
     ap.add_argument("--by-grid", action="store_true",
                     help="one row per (kernel, grid size): per-layer view of a plan")
+    ap.add_argument("--busy", action="store_true",
+                    help="GPU busy share of the traced span, and each kernel's share of the "
+                         "busy time with concurrent kernels splitting a time slice evenly (the "
+                         "per-kernel durations double-count overlap when streams run together)")
     a = ap.parse_args()
     c = sqlite3.connect(a.db)
+    if a.busy:
+        busy(c, a.top)
+        return
     key = "name || ' grid=' || grid_x || 'x' || grid_y" if a.by_grid else "name"
     rows = c.execute(
         f"select {key}, count(*), sum(end-start), avg(end-start), min(end-start), max(end-start) "
