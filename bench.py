@@ -693,13 +693,21 @@ def main(argv=None) -> int:
     cpu0 = thread_cpu_seconds()
     c0 = eng.completed
     t0 = time.perf_counter()
-    marks = []
+    m0 = time.clock_gettime_ns(time.CLOCK_MONOTONIC)
+    marks = []  # (s since t0, records completed): step boundaries for the per-step rates
     reached = True
     for k in range(1, a.steps + 1):
         if not eng.wait_completed(c0 + k * step_records, a.timeout):
             reached = False
             break
-        marks.append((time.perf_counter(), eng.completed))
+        # the completing thread's own clock reading of the crossing: this thread's wake-up runs
+        # late by a varying few ms on a saturated host, and a late mark shortens the next step
+        # (an alternating fast / slow pattern that is the measurement, not the pipeline)
+        ns, c = eng.last_wait()
+        if ns > 0:
+            marks.append(((ns - m0) * 1e-9, c))
+        else:
+            marks.append((time.perf_counter() - t0, eng.completed))
     if use_gpu:
         torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
@@ -775,7 +783,7 @@ def main(argv=None) -> int:
     if rank == 0:
         # per-step rates from (time, completed) marks; a completion burst can cross several step
         # boundaries at once, so intervals shorter than half a mean step are merged with the next
-        step_rates, ta, ca = [], t0, c0
+        step_rates, ta, ca = [], 0.0, c0
         for tb, cb in marks:
             if tb - ta >= 0.5 * elapsed / max(1, len(marks)) and cb > ca:
                 step_rates.append((cb - ca) * ipr / (tb - ta))

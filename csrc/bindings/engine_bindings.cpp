@@ -124,6 +124,7 @@ void bind_engine(py::module_& m) {
              return e.wait(timeout_ms);
            },
            py::arg("timeout_ms") = -1)
+      .def("last_wait", &Engine::last_wait)
       .def("wait_completed",
            [](Engine& e, int64_t n, int64_t timeout_ms) {
              py::gil_scoped_release nogil;

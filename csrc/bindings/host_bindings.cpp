@@ -153,6 +153,13 @@ class RateFeeder {
     if (records_per_s <= 0) throw std::invalid_argument("RateFeeder: rate must be > 0");
     stop_ = false;
     next_ = start_batch;
+    {
+      // room for a long window up front: the appends are timestamped, a growth copy would
+      // delay the next ones
+      std::lock_guard<std::mutex> lk(mu_);
+      for (auto* v : {&lp_, &ln_}) v->reserve(1 << 18);
+      for (auto* v : {&lbase_, &lt_}) v->reserve(1 << 18);
+    }
     t_ = std::thread([this, records_per_s] { run(records_per_s); });
   }
   void stop() {

@@ -215,32 +215,23 @@ PYBIND11_MODULE(_C, m) {
         });
   m.def("ingest_crc_count",
         [](uintptr_t bytes, uintptr_t chunks, int nchunks, uintptr_t tables, uintptr_t crc_out,
-           int nrec, int ntiles, uintptr_t recs, uintptr_t tile_rec, uintptr_t counts,
+           int nrec, int ngroups, uintptr_t recs, uintptr_t groups, uintptr_t counts,
            uintptr_t rec_tokens, uintptr_t stream) {
           gale::check_hip(
               gale::ingest_crc_count(reinterpret_cast<const uint8_t*>(bytes),
                                      reinterpret_cast<const gale::CrcChunk*>(chunks), nchunks,
                                      reinterpret_cast<const uint32_t*>(tables),
-                                     reinterpret_cast<uint32_t*>(crc_out), nrec, ntiles,
+                                     reinterpret_cast<uint32_t*>(crc_out), nrec, ngroups,
                                      reinterpret_cast<gale::JsonRecord*>(recs),
-                                     reinterpret_cast<const int*>(tile_rec),
+                                     reinterpret_cast<const int2*>(groups),
                                      reinterpret_cast<int*>(counts),
                                      reinterpret_cast<int*>(rec_tokens),
                                      reinterpret_cast<hipStream_t>(stream)),
               "ingest_crc_count");
-        });
-  m.def("json_count_records",
-        [](int nrec, int ntiles, uintptr_t recs, uintptr_t tile_rec, uintptr_t bytes,
-           uintptr_t counts, uintptr_t rec_tokens, uintptr_t stream) {
-          gale::check_hip(
-              gale::json_count_records(nrec, ntiles, reinterpret_cast<gale::JsonRecord*>(recs),
-                                       reinterpret_cast<const int*>(tile_rec),
-                                       reinterpret_cast<const uint8_t*>(bytes),
-                                       reinterpret_cast<int*>(counts),
-                                       reinterpret_cast<int*>(rec_tokens),
-                                       reinterpret_cast<hipStream_t>(stream)),
-              "json_count_records");
-        });
+        },
+        "groups: int32 (record, first tile) pairs, kGroupTiles tiles each; counts: per record "
+        "tile0 + grp0 -> [tile counts][group sums]");
+  m.attr("GROUP_TILES") = gale::kGroupTiles;
   m.def("text_unpack", [](uintptr_t packed, uintptr_t tab, int64_t n, uintptr_t out,
                           uintptr_t stream) {
     if (out % 16 || packed % 8) throw std::invalid_argument("text_unpack: misaligned buffers");

@@ -159,6 +159,7 @@ hipError_t cast_f32_bf16(int64_t n, float scale, float shift, const float* x, vo
 // The kernel raises each record's status (host zeroes it): 0 ok, 1 number-count mismatch,
 // 2 malformed number / element, 3 bad structure (ragged / wrong rank).
 constexpr int kJsonTileBytes = 2048;
+constexpr int kGroupTiles = 16;  // tiles per ingest counting wave / per group sum
 struct JsonRecord {
   int64_t off;      // byte offset of the instances array inside the staged byte buffer
   int32_t len;      // array length in bytes
@@ -166,12 +167,14 @@ struct JsonRecord {
   int32_t images;   // images in this record (from the host '[' count)
   int32_t status;   // raised by the kernel
   int32_t tile0;    // first global tile of this record
-  // 1: the record's per-tile token counts are already on the device at bytes + cnt_off (the GPU
-  // ingest pass counted them and left them in the fetch buffer's device mirror), so the parse
-  // skips its own counting pass over this record's text
+  // 1: the record's count block is already on the device at bytes + cnt_off (the GPU ingest pass
+  // counted it and left it in the fetch buffer's device mirror): its nt tile token counts, then
+  // one sum per group of kGroupTiles tiles. The parse skips its counting pass over this record.
   int32_t has_cnt;
   int64_t cnt_off;
-  int64_t pad_;
+  // ingest_crc_count only: groups in the records before this one, so the record's count block
+  // starts at counts + tile0 + grp0
+  int64_t grp0;
 };
 static_assert(sizeof(JsonRecord) == 48, "JsonRecord layout (host <-> device tables)");
 int json_tile_count(int64_t off, int32_t len);
@@ -184,14 +187,6 @@ hipError_t json_parse_instances(int nrec, int ntiles, JsonRecord* recs, const in
                                 const uint8_t* bytes, int H, int W, int C, int* tile_counts,
                                 float* out, hipStream_t stream, bool count_pass = true,
                                 const int* d_ntiles = nullptr);
-
-// Ingest pass over a Kafka fetch buffer already on the device: json_count_records counts the
-// number tokens of every record's instances array (rec_tokens[i] += tokens of record i, host
-// zeroes it; invalid bytes raise recs[i].status to 2) so the host learns each record's image
-// count without reading its text.
-hipError_t json_count_records(int nrec, int ntiles, JsonRecord* recs, const int* tile_rec,
-                              const uint8_t* bytes, int* tile_counts, int* rec_tokens,
-                              hipStream_t stream);
 
 // Raw (zero initial state, no final inversion) CRC32C of byte windows [end - len, end) of a
 // device buffer, one wave per window (len <= kCrcChunkBytes): each lane folds 64 bytes with
@@ -209,12 +204,16 @@ hipError_t crc32c_chunks(const uint8_t* bytes, const CrcChunk* chunks, int n,
                          const uint32_t* tables, uint32_t* out, hipStream_t stream);
 
 // The GPU ingest pass of one fetch buffer in ONE launch: workgroups [0, crc blocks) fold the CRC
-// windows (crc32c_chunks), the rest count the records' number tokens (json_count_records,
-// tile_counts[t] = tokens of tile t, rec_tokens[i] += tokens of record i).
+// windows (crc32c_chunks), the rest count the records' number tokens so the host learns each
+// record's image count without reading its text: one wave per tile group, groups[g] = (record,
+// record-relative first tile), kGroupTiles tiles each (a record's last group may be shorter).
+// Record i's count block at counts + tile0 + grp0 gets its tile counts and group sums (see
+// JsonRecord::has_cnt); rec_tokens[i] += its tokens (host zeroes it); invalid bytes raise
+// recs[i].status to 2.
 hipError_t ingest_crc_count(const uint8_t* bytes, const CrcChunk* chunks, int nchunks,
-                            const uint32_t* tables, uint32_t* crc_out, int nrec, int ntiles,
-                            JsonRecord* recs, const int* tile_rec, int* tile_counts,
-                            int* rec_tokens, hipStream_t stream);
+                            const uint32_t* tables, uint32_t* crc_out, int nrec, int ngroups,
+                            JsonRecord* recs, const int2* groups, int* counts, int* rec_tokens,
+                            hipStream_t stream);
 
 // Expands a nibble-packed span (csrc/codec/text_pack.h: 64-byte blocks, per-2-KiB-group
 // {base offset, packed-block mask} pairs in tab) into out[0, n). out must be 16-byte aligned,

@@ -581,19 +581,15 @@ __device__ __forceinline__ bool gap_window(const uint8_t* text, int x, int k) {
   return prev - '0' < 10u;
 }
 
-// Tokens of global tile t (one wave): counts[t], rec_tokens[record] += (ingest), invalid bytes
-// raise the record's status to 2. A record whose counts the ingest pass already left on the
-// device (has_cnt) is skipped by the parse's counting pass.
-__device__ __forceinline__ void count_tile(JsonRecord* recs, const int* tile_rec, int t,
-                                           const uint8_t* bytes, int* counts, int* rec_tokens) {
+// Number tokens of record-relative tile tl of record r (one wave, the count on every lane);
+// *bad: the tile holds a byte outside the number / delimiter alphabet.
+__device__ __forceinline__ int tile_tokens(const JsonRecord& r, int tl, const uint8_t* bytes,
+                                           bool* bad) {
   const int lane = threadIdx.x & 63;
-  const int ri = tile_rec[t];
-  const JsonRecord r = recs[ri];
-  if (!rec_tokens && r.has_cnt) return;
   const int64_t abeg = r.off & ~(int64_t)15;
   const uint8_t* rb = bytes + abeg;
   const int beg = (int)(r.off - abeg), end = beg + r.len;
-  const int o = (t - r.tile0) * kTile + kLaneBytes * lane;
+  const int o = tl * kTile + kLaneBytes * lane;
   uint4 v[kChunks];
 #pragma unroll
   for (int i = 0; i < kChunks; ++i)
@@ -603,34 +599,76 @@ __device__ __forceinline__ void count_tile(JsonRecord* recs, const int* tile_rec
   if (lane == 0 && o - 1 >= beg) prevb = rb[o - 1];
   const bool pd = (o - 1 < beg) || is_delim(prevb);
   uint32_t st[kChunks], cm[kChunks];
-  bool bad;
-  token_starts(v, o, beg, end, pd, st, cm, &bad);
+  token_starts(v, o, beg, end, pd, st, cm, bad);
   int lc = 0;
 #pragma unroll
   for (int i = 0; i < kChunks; ++i) lc += __builtin_popcount(st[i]);
-  const int cnt = wave_sum_i(lc);
-  if (lane == 0) {
-    counts[t] = cnt;
-    if (rec_tokens) atomicAdd(&rec_tokens[ri], cnt);  // ingest: the record's element count
-  }
+  return wave_sum_i(lc);
+}
+
+// tiles of a record: json_tile_count on the device
+__device__ __forceinline__ int record_tiles(const JsonRecord& r) {
+  const int64_t abeg = r.off & ~(int64_t)15;
+  return (int)((r.off + r.len - abeg + kTile - 1) / kTile);
+}
+
+// The parse's counting pass for global tile t (one wave): counts[t]. A record whose counts the
+// ingest pass already left on the device (has_cnt) is skipped.
+__device__ __forceinline__ void count_tile(JsonRecord* recs, const int* tile_rec, int t,
+                                           const uint8_t* bytes, int* counts) {
+  const int ri = tile_rec[t];
+  const JsonRecord r = recs[ri];
+  if (r.has_cnt) return;
+  bool bad;
+  const int cnt = tile_tokens(r, t - r.tile0, bytes, &bad);
+  if ((threadIdx.x & 63) == 0) counts[t] = cnt;
   if (bad) atomicMax(&recs[ri].status, 2);
+}
+
+// The ingest pass's counting of one group of up to kGroupTiles consecutive tiles of a record
+// (one wave, the tiles in turn). The record's count block (at counts + tile0 + grp0) holds its
+// nt tile counts, then one sum per group: the parse finds a tile's first element index from at
+// most nt / kGroupTiles group sums plus < kGroupTiles tile counts, and the record's token total
+// takes one atomic per group - per-tile atomics on one counter serialise (an ImageNet record is
+// ~850 tiles: 80 of the 92 us of a 15 MB fetch's ingest launch, tools/bench_ingest.py).
+__device__ __forceinline__ void count_group(JsonRecord* recs, const int2* groups, int g,
+                                            const uint8_t* bytes, int* counts, int* rec_tokens) {
+  const int2 gr = groups[g];  // (record, record-relative first tile)
+  const JsonRecord r = recs[gr.x];
+  const int nt = record_tiles(r);
+  const int n = min(kGroupTiles, nt - gr.y);
+  int* blk = counts + r.tile0 + (int)r.grp0;
+  int acc = 0;
+  bool any_bad = false;
+  for (int i = 0; i < n; ++i) {
+    bool bad;
+    const int cnt = tile_tokens(r, gr.y + i, bytes, &bad);
+    any_bad |= bad;
+    acc += cnt;
+    if ((threadIdx.x & 63) == 0) blk[gr.y + i] = cnt;
+  }
+  if ((threadIdx.x & 63) == 0) {
+    blk[nt + gr.y / kGroupTiles] = acc;
+    atomicAdd(&rec_tokens[gr.x], acc);
+  }
+  if (any_bad) atomicMax(&recs[gr.x].status, 2);
 }
 
 __global__ __launch_bounds__(256) void json_count_kernel(JsonRecord* recs, const int* tile_rec,
                                                          int ntiles, const uint8_t* bytes,
-                                                         int* counts, int* rec_tokens,
-                                                         const int* d_ntiles) {
+                                                         int* counts, const int* d_ntiles) {
   const int t = blockIdx.x * kWaves + (threadIdx.x >> 6);
   if (d_ntiles) ntiles = min(ntiles, *d_ntiles);
   if (t >= ntiles) return;  // (no workgroup barriers in this kernel)
-  count_tile(recs, tile_rec, t, bytes, counts, rec_tokens);
+  count_tile(recs, tile_rec, t, bytes, counts);
 }
 
 // The ingest pass of a fetch buffer in one launch: CRC window workgroups first (they stage the
-// CRC tables in LDS behind one barrier; the branch is uniform per workgroup), then counting.
+// CRC tables in LDS behind one barrier; the branch is uniform per workgroup), then counting,
+// one wave per tile group.
 __global__ __launch_bounds__(256) void ingest_crc_count_kernel(
     const uint8_t* bytes, const CrcChunk* chunks, int nchunks, const uint32_t* tables,
-    uint32_t* crc_out, int crc_blocks, JsonRecord* recs, const int* tile_rec, int ntiles,
+    uint32_t* crc_out, int crc_blocks, JsonRecord* recs, const int2* groups, int ngroups,
     int* counts, int* rec_tokens) {
   if ((int)blockIdx.x < crc_blocks) {
     __shared__ uint32_t T[crc::kTableWords];
@@ -638,9 +676,9 @@ __global__ __launch_bounds__(256) void ingest_crc_count_kernel(
     crc::crc_windows(bytes, chunks, nchunks, T, crc_out, blockIdx.x, crc_blocks);
     return;
   }
-  const int t = ((int)blockIdx.x - crc_blocks) * kWaves + (threadIdx.x >> 6);
-  if (t >= ntiles) return;
-  count_tile(recs, tile_rec, t, bytes, counts, rec_tokens);
+  const int g = ((int)blockIdx.x - crc_blocks) * kWaves + (threadIdx.x >> 6);
+  if (g >= ngroups) return;
+  count_group(recs, groups, g, bytes, counts, rec_tokens);
 }
 
 __global__ __launch_bounds__(256) void json_parse_kernel(JsonRecord* recs, const int* tile_rec,
@@ -681,9 +719,13 @@ __global__ __launch_bounds__(256) void json_parse_kernel(JsonRecord* recs, const
 
   // first element index of this tile: the token counts of the record's earlier tiles
   int part = 0;
-  if (r.has_cnt) {  // counted by the ingest pass, left next to the fetch buffer's device mirror
+  if (r.has_cnt) {  // counted by the ingest pass, left next to the fetch buffer's device mirror:
+    // the sums of the whole tile groups before this tile, then its group's earlier tiles
     const int* rc = reinterpret_cast<const int*>(bytes + r.cnt_off);
-    for (int k = lane; k < tl; k += 64) part += rc[k];
+    const int* gs = rc + record_tiles(r);
+    const int gi = tl / kGroupTiles;
+    for (int k = lane; k < gi; k += 64) part += gs[k];
+    if (lane < tl - gi * kGroupTiles) part += rc[gi * kGroupTiles + lane];
   } else {
     for (int k = r.tile0 + lane; k < t; k += 64) part += counts[k];
   }
@@ -773,15 +815,7 @@ __global__ __launch_bounds__(256) void json_parse_kernel(JsonRecord* recs, const
 
 }  // namespace
 
-hipError_t json_count_records(int nrec, int ntiles, JsonRecord* recs, const int* tile_rec,
-                              const uint8_t* bytes, int* tile_counts, int* rec_tokens,
-                              hipStream_t stream) {
-  if (nrec <= 0 || ntiles <= 0) return hipSuccess;
-  const int blocks = (ntiles + kWaves - 1) / kWaves;
-  hipLaunchKernelGGL(json_count_kernel, dim3(blocks), dim3(64 * kWaves), 0, stream, recs,
-                     tile_rec, ntiles, bytes, tile_counts, rec_tokens, nullptr);
-  return hipGetLastError();
-}
+
 
 int json_tile_count(int64_t off, int32_t len) {
   if (len <= 0) return 0;
@@ -790,17 +824,17 @@ int json_tile_count(int64_t off, int32_t len) {
 }
 
 hipError_t ingest_crc_count(const uint8_t* bytes, const CrcChunk* chunks, int nchunks,
-                            const uint32_t* tables, uint32_t* crc_out, int nrec, int ntiles,
-                            JsonRecord* recs, const int* tile_rec, int* tile_counts,
-                            int* rec_tokens, hipStream_t stream) {
-  if (nrec <= 0) ntiles = 0;
+                            const uint32_t* tables, uint32_t* crc_out, int nrec, int ngroups,
+                            JsonRecord* recs, const int2* groups, int* counts, int* rec_tokens,
+                            hipStream_t stream) {
+  if (nrec <= 0) ngroups = 0;
   int crc_blocks = (nchunks + crc::kCrcWaves - 1) / crc::kCrcWaves;
   if (crc_blocks > 1024) crc_blocks = 1024;  // (windows loop: the table load is amortised)
-  const int cnt_blocks = (ntiles + kWaves - 1) / kWaves;
+  const int cnt_blocks = (ngroups + kWaves - 1) / kWaves;
   if (crc_blocks + cnt_blocks == 0) return hipSuccess;
   hipLaunchKernelGGL(ingest_crc_count_kernel, dim3(crc_blocks + cnt_blocks), dim3(256), 0, stream,
-                     bytes, chunks, nchunks, tables, crc_out, crc_blocks, recs, tile_rec, ntiles,
-                     tile_counts, rec_tokens);
+                     bytes, chunks, nchunks, tables, crc_out, crc_blocks, recs, groups, ngroups,
+                     counts, rec_tokens);
   return hipGetLastError();
 }
 
@@ -813,7 +847,7 @@ hipError_t json_parse_instances(int nrec, int ntiles, JsonRecord* recs, const in
   const int blocks = (ntiles + kWaves - 1) / kWaves;
   if (count_pass)
     hipLaunchKernelGGL(json_count_kernel, dim3(blocks), dim3(64 * kWaves), 0, stream, recs,
-                       tile_rec, ntiles, bytes, tile_counts, nullptr, d_ntiles);
+                       tile_rec, ntiles, bytes, tile_counts, d_ntiles);
   hipLaunchKernelGGL(json_parse_kernel, dim3(blocks), dim3(64 * kWaves), 0, stream, recs,
                      tile_rec, ntiles, bytes, H, W, C, tile_counts, out, d_ntiles);
   return hipGetLastError();

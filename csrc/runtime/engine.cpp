@@ -1404,10 +1404,18 @@ void Engine::complete_records(const std::vector<InRecord>& rs, bool ok) {
         ack_push({rs[i].partition, rs[i].offset, now, rs[i].t_fetch_ns, rs[i].t_take_ns,
                   rs[i].t_done_ns});
   }
-  const int64_t c = completed_ += (int64_t)rs.size();
+  note_completed(completed_ += (int64_t)rs.size(), now);
+}
+
+void Engine::note_completed(int64_t c, int64_t now) {
   const int64_t target = wait_target_.load(std::memory_order_relaxed);
   if ((cfg_.max_records > 0 && c >= cfg_.max_records) || (target > 0 && c >= target)) {
     std::lock_guard<std::mutex> lk(done_mu_);
+    if (target > 0 && c >= target && hit_target_ != target) {
+      hit_target_ = target;
+      hit_ns_ = now;
+      hit_c_ = c;
+    }
     done_cv_.notify_all();
   }
 }
@@ -1434,12 +1442,7 @@ void Engine::complete_record(const InRecord& r, bool ok) {
     if (ack_n_ < ack_cap_)
       ack_push({r.partition, r.offset, now, r.t_fetch_ns, r.t_take_ns, r.t_done_ns});
   }
-  const int64_t c = ++completed_;
-  const int64_t target = wait_target_.load(std::memory_order_relaxed);
-  if ((cfg_.max_records > 0 && c >= cfg_.max_records) || (target > 0 && c >= target)) {
-    std::lock_guard<std::mutex> lk(done_mu_);
-    done_cv_.notify_all();
-  }
+  note_completed(++completed_, now);
 }
 
 void Engine::set_ack_log(bool on, size_t capacity) {
@@ -1481,6 +1484,8 @@ bool Engine::wait_completed(int64_t n, int64_t timeout_ms) {
   if (timeout_ms < 0) done_cv_.wait(lk, pred);
   else done_cv_.wait_for(lk, std::chrono::milliseconds(timeout_ms), pred);
   wait_target_ = 0;
+  last_wait_ns_ = hit_target_ == n ? hit_ns_ : 0;
+  last_wait_c_ = hit_target_ == n ? hit_c_ : 0;
   return completed_.load() >= n;
 }
 

@@ -33,6 +33,7 @@
 #include <random>
 #include <set>
 #include <string>
+#include <utility>
 #include <thread>
 #include <vector>
 
@@ -254,6 +255,13 @@ class Engine {
   // Block (without stopping anything) until at least n records completed; false on timeout or
   // when the engine stopped first.
   bool wait_completed(int64_t n, int64_t timeout_ms);
+  // CLOCK_MONOTONIC ns of the completion that reached the last wait_completed target (0 = it
+  // was reached before the wait started): the waiting thread's own wake-up can run late on a
+  // busy host, so step times taken from it alias into an alternating fast/slow pattern
+  std::pair<int64_t, int64_t> last_wait() const {  // (ns, records completed by then)
+    std::lock_guard<std::mutex> lk(done_mu_);
+    return {last_wait_ns_, last_wait_c_};
+  }
   bool running() const { return running_; }
   int64_t completed() const { return completed_.load(); }
 
@@ -346,7 +354,9 @@ class Engine {
   std::map<int, int64_t> next_fetch_;              // partition -> next offset to fetch
   std::map<int, int64_t> high_watermark_;          // partition -> log end (last fetch response)
 
-  std::mutex done_mu_;
+  mutable std::mutex done_mu_;
+  int64_t hit_target_ = 0, hit_ns_ = 0, hit_c_ = 0, last_wait_ns_ = 0, last_wait_c_ = 0;
+  void note_completed(int64_t c, int64_t now);
   std::condition_variable done_cv_;
   std::atomic<int64_t> completed_{0};
   std::atomic<int64_t> wait_target_{0};

@@ -106,12 +106,14 @@ void GpuIngest::run(int lane, const kafka::Fetched& f, uint8_t* dev, size_t dev_
     }
   }
   std::vector<int> rec_of;  // JsonRecord j -> record index
-  int ntiles = 0;
+  int ntiles = 0, ngroups = 0;
   for (size_t i = 0; i < nrec_all; ++i) {
     if (io.status[i] != codec::OK) continue;
     const kafka::RecordRef& rr = f.records[i];
     rec_of.push_back((int)i);
-    ntiles += json_tile_count(rr.value_off + io.arr_off[i], (int32_t)io.arr_len[i]);
+    const int nt = json_tile_count(rr.value_off + io.arr_off[i], (int32_t)io.arr_len[i]);
+    ntiles += nt;
+    ngroups += (nt + kGroupTiles - 1) / kGroupTiles;
     lo = std::min(lo, (size_t)rr.value_off);
     hi = std::max(hi, (size_t)(rr.value_off + rr.value_len));
   }
@@ -128,18 +130,20 @@ void GpuIngest::run(int lane, const kafka::Fetched& f, uint8_t* dev, size_t dev_
   const size_t span = hi - lo;
   const size_t ng = packed ? codec::pack_groups(span) : 0;
   const size_t o_chunks = align16(ng * 2 * sizeof(uint32_t));
-  const size_t o_tiles = o_chunks + align16(nc * sizeof(CrcChunk));
-  const size_t o_recs = o_tiles + align16((size_t)ntiles * sizeof(int));
+  const size_t o_groups = o_chunks + align16(nc * sizeof(CrcChunk));
+  const size_t o_recs = o_groups + align16((size_t)ngroups * sizeof(int2));
   const size_t o_tok = o_recs + nr * sizeof(JsonRecord);  // (JsonRecord is 48 bytes)
   const size_t o_crc = o_tok + align16(nr * 4);
   const size_t io_bytes = o_crc + align16(nc * 4);
   check_hip(hipSetDevice(device_), "ingest: hipSetDevice");
-  grow(L, io_bytes + 16, (size_t)ntiles + 1);
+  // count blocks: per record its tile counts then its group sums (ntiles + ngroups ints)
+  const size_t ncnt = (size_t)ntiles + (size_t)ngroups;
+  grow(L, io_bytes + 16, ncnt + 1);
   CrcChunk* hc = reinterpret_cast<CrcChunk*>(L.h_io + o_chunks);
-  int* ht = reinterpret_cast<int*>(L.h_io + o_tiles);
+  int2* hg = reinterpret_cast<int2*>(L.h_io + o_groups);
   JsonRecord* hr = reinterpret_cast<JsonRecord*>(L.h_io + o_recs);
   if (nc) memcpy(hc, chunks.data(), nc * sizeof(CrcChunk));
-  int tile = 0;
+  int tile = 0, grp = 0;
   for (size_t j = 0; j < nr; ++j) {
     const size_t i = (size_t)rec_of[j];
     JsonRecord& jr = hr[j];
@@ -151,9 +155,13 @@ void GpuIngest::run(int lane, const kafka::Fetched& f, uint8_t* dev, size_t dev_
     jr.tile0 = tile;
     jr.has_cnt = 0;
     jr.cnt_off = 0;
-    jr.pad_ = 0;
+    jr.grp0 = grp;
     const int nt = json_tile_count(jr.off, jr.len);
-    for (int t = 0; t < nt; ++t) ht[tile + t] = (int)j;
+    for (int t0 = 0; t0 < nt; t0 += kGroupTiles) {
+      hg[grp].x = (int)j;
+      hg[grp].y = t0;
+      ++grp;
+    }
     tile += nt;
   }
   memset(L.h_io + o_tok, 0, nr * 4);  // token counters start at zero (no device memset)
@@ -188,7 +196,7 @@ void GpuIngest::run(int lane, const kafka::Fetched& f, uint8_t* dev, size_t dev_
   int64_t cnt_base = -1;
   if (ntiles > 0) {
     const size_t used = packed ? codec::pack_offset(span) + link : hi;
-    const size_t cb = ((size_t)ntiles * sizeof(int) + 255) & ~(size_t)255;
+    const size_t cb = (ncnt * sizeof(int) + 255) & ~(size_t)255;
     if (dev_cap > cb + 256 && ((dev_cap - cb) & ~(size_t)255) >= ((used + 64 + 255) & ~(size_t)255)) {
       cnt_base = (int64_t)((dev_cap - cb) & ~(size_t)255);
       d_cnt = reinterpret_cast<int*>(dev + cnt_base);
@@ -196,8 +204,8 @@ void GpuIngest::run(int lane, const kafka::Fetched& f, uint8_t* dev, size_t dev_
   }
   // CRC windows and token counts: one launch, one pass of workgroups over the buffer
   check_hip(ingest_crc_count(dev, reinterpret_cast<const CrcChunk*>(L.d_io + o_chunks), (int)nc,
-                             d_tables_, d_crc, (int)nr, ntiles, d_rec,
-                             reinterpret_cast<const int*>(L.d_io + o_tiles), d_cnt, d_tok, st),
+                             d_tables_, d_crc, (int)nr, ngroups, d_rec,
+                             reinterpret_cast<const int2*>(L.d_io + o_groups), d_cnt, d_tok, st),
             "ingest: crc32c + count");
   check_hip(hipMemcpyAsync(L.h_io + o_recs, L.d_io + o_recs, io_bytes - o_recs,
                            hipMemcpyDeviceToHost, st),
@@ -232,7 +240,8 @@ void GpuIngest::run(int lane, const kafka::Fetched& f, uint8_t* dev, size_t dev_
       io.status[i] = codec::BAD_SHAPE;
     } else {
       io.images[i] = (int32_t)(tok[j] / per);
-      if (cnt_base >= 0) io.cnt_off[i] = cnt_base + (int64_t)hr[j].tile0 * (int64_t)sizeof(int);
+      if (cnt_base >= 0)
+        io.cnt_off[i] = cnt_base + (hr[j].tile0 + hr[j].grp0) * (int64_t)sizeof(int);
     }
   }
 }

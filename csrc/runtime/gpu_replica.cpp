@@ -215,7 +215,7 @@ void GpuReplica::submit(Batch& b) {
     jr.tile0 = ntiles;
     jr.has_cnt = 0;
     jr.cnt_off = 0;
-    jr.pad_ = 0;
+    jr.grp0 = 0;
     if (resident(r) && r.dev_counts) {  // counted by the ingest pass: no counting pass here
       jr.has_cnt = 1;
       jr.cnt_off = (int64_t)(r.dev_counts - s.d_bytes);

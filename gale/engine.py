@@ -146,6 +146,12 @@ class Engine:
         """Block until >= n records completed (the engine keeps running)."""
         return self._native.wait_completed(n, -1 if timeout_s is None else int(timeout_s * 1000))
 
+    def last_wait(self):
+        """(CLOCK_MONOTONIC ns, records completed) of the completion that reached the last
+        wait_completed target, taken by the completing thread; (0, 0) if the target was already
+        reached when the wait began."""
+        return tuple(self._native.last_wait())
+
     @property
     def running(self) -> bool:
         return self._native.running

@@ -267,68 +267,95 @@ def test_gpu_crc32c_chunks_kernel():
         assert std == K.crc32c(buf[s0:s0 + ln]), (s0, ln)
 
 
+def host_tile_tokens(buf, off, ln):
+    """Number tokens starting in each 2 KiB tile of the record text at [off, off + ln) (tiles
+    counted from the 16-byte-aligned start, as json_tile_count)."""
+    abeg = off & ~15
+    b = np.frombuffer(buf, dtype=np.uint8)[abeg:off + ln].copy()
+    beg = off - abeg
+    delim = np.isin(b, np.frombuffer(b"[], \t\r\n", dtype=np.uint8))
+    delim[:beg] = True
+    prev = np.concatenate([[True], delim[:-1]])
+    start = ~delim & prev
+    nt = C.json_tile_count(off, ln)
+    T = C.JSON_TILE_BYTES
+    return np.array([start[k * T:(k + 1) * T].sum() for k in range(nt)], dtype=np.int64)
+
+
 def test_gpu_fused_ingest_kernel_matches_separate_passes():
-    """ingest_crc_count (CRC windows + token counts in ONE launch) produces the raw window CRCs
-    of crc32c_chunks and the per-tile / per-record counts of json_count_records; the parse then
-    reuses those tile counts (has_cnt, no counting launch) and decodes the same tensor."""
+    """ingest_crc_count (CRC windows + token counts in ONE launch, one wave per group of
+    GROUP_TILES tiles) produces the raw window CRCs of crc32c_chunks, every record's count block
+    (tile token counts as counted on the host, then one sum per tile group) and the per-record
+    totals; the parse then reuses those blocks (has_cnt, no counting launch) and decodes the same
+    tensor. Records of 1-3 CIFAR images and one ImageNet image (~850 tiles, 54 groups)."""
     import os
 
     rng = np.random.default_rng(8)
-    H, Wd, Cc = 32, 32, 3
-    xs = [rng.random((n, H, Wd, Cc), dtype=np.float32) for n in (1, 3, 2)]
-    arrays = [array_text(C.encode_instances(x), H, Wd, Cc) for x in xs]
-    raw, recs, total, tiles = stage(arrays)
-    buf = bytes(raw) + os.urandom(5000)
-    tile_rec = np.zeros(tiles, dtype=np.int32)
-    for i, r in enumerate(recs):
-        n = C.json_tile_count(int(r["off"]), int(r["len"]))
-        tile_rec[r["tile0"]:r["tile0"] + n] = i
-    wins = [(len(buf) - 4096 * k, 4096) for k in range(len(buf) // 4096)][::-1]
-    wins = [(len(buf) - 4096 * len(wins), len(buf) % 4096)] + wins if len(buf) % 4096 else wins
-    ch = np.zeros(len(wins), dtype=[("end", "<i8"), ("len", "<i4"), ("pad", "<i4")])
-    for i, (e, ln) in enumerate(wins):
-        ch[i] = (e, ln, 0)
-    d = torch.frombuffer(bytearray(buf + bytes(64)), dtype=torch.uint8).cuda()
-    tables = torch.tensor(np.array(K.crc32c_device_tables(), dtype=np.uint32).view(np.int32),
-                          device="cuda")
-    dch = torch.from_numpy(ch.view(np.uint8).copy()).cuda()
-    dmap = torch.from_numpy(tile_rec).cuda()
-    s = torch.cuda.current_stream().cuda_stream
-
-    def run(fused):
+    G = C.GROUP_TILES
+    cases = [(32, 32, 3, (1, 3, 2)), (224, 224, 3, (1,))]
+    for H, Wd, Cc, ns in cases:
+        xs = [rng.random((n, H, Wd, Cc), dtype=np.float32) for n in ns]
+        arrays = [array_text(C.encode_instances(x), H, Wd, Cc) for x in xs]
+        raw, recs, total, tiles = stage(arrays)
+        buf = bytes(raw) + os.urandom(5000)
+        wins = [(len(buf) - 4096 * k, 4096) for k in range(len(buf) // 4096)][::-1]
+        wins = [(len(buf) - 4096 * len(wins), len(buf) % 4096)] + wins if len(buf) % 4096 else wins
+        ch = np.zeros(len(wins), dtype=[("end", "<i8"), ("len", "<i4"), ("pad", "<i4")])
+        for i, (e, ln) in enumerate(wins):
+            ch[i] = (e, ln, 0)
+        groups, grp0 = [], []
+        for i, r in enumerate(recs):
+            grp0.append(len(groups))
+            nt = C.json_tile_count(int(r["off"]), int(r["len"]))
+            groups += [(i, t0) for t0 in range(0, nt, G)]
+        recs["pad"] = grp0  # JsonRecord::grp0
+        d = torch.frombuffer(bytearray(buf + bytes(64)), dtype=torch.uint8).cuda()
+        tables = torch.tensor(np.array(K.crc32c_device_tables(), dtype=np.uint32).view(np.int32),
+                              device="cuda")
+        dch = torch.from_numpy(ch.view(np.uint8).copy()).cuda()
+        dgrp = torch.tensor(np.array(groups, dtype=np.int32).reshape(-1), device="cuda")
+        s = torch.cuda.current_stream().cuda_stream
         drec = torch.from_numpy(recs.view(np.uint8).copy()).cuda()
         crc = torch.zeros(len(wins), dtype=torch.int32, device="cuda")
-        cnt = torch.full((tiles,), -1, dtype=torch.int32, device="cuda")
+        cnt = torch.full((tiles + len(groups),), -1, dtype=torch.int32, device="cuda")
         tok = torch.zeros(len(recs), dtype=torch.int32, device="cuda")
-        if fused:
-            C.ingest_crc_count(d.data_ptr(), dch.data_ptr(), len(wins), tables.data_ptr(),
-                               crc.data_ptr(), len(recs), tiles, drec.data_ptr(),
-                               dmap.data_ptr(), cnt.data_ptr(), tok.data_ptr(), s)
-        else:
-            C.crc32c_chunks(d.data_ptr(), dch.data_ptr(), len(wins), tables.data_ptr(),
-                            crc.data_ptr(), s)
-            C.json_count_records(len(recs), tiles, drec.data_ptr(), dmap.data_ptr(),
-                                 d.data_ptr(), cnt.data_ptr(), tok.data_ptr(), s)
+        C.ingest_crc_count(d.data_ptr(), dch.data_ptr(), len(wins), tables.data_ptr(),
+                           crc.data_ptr(), len(recs), len(groups), drec.data_ptr(),
+                           dgrp.data_ptr(), cnt.data_ptr(), tok.data_ptr(), s)
+        crc2 = torch.zeros(len(wins), dtype=torch.int32, device="cuda")
+        C.crc32c_chunks(d.data_ptr(), dch.data_ptr(), len(wins), tables.data_ptr(),
+                        crc2.data_ptr(), s)
         torch.cuda.synchronize()
-        return crc.cpu().numpy(), cnt.cpu().numpy(), tok.cpu().numpy()
-
-    a, b = run(True), run(False)
-    for u, v in zip(a, b):
-        np.testing.assert_array_equal(u, v)
-    assert list(a[2]) == [len(x) * H * Wd * Cc for x in xs]
-    # parse with the ingest counts (has_cnt, cnt_off relative to the text base), no count pass
-    cnt_dev = torch.from_numpy(a[1].copy()).cuda()
-    recs2 = recs.copy()
-    recs2["has_cnt"] = 1
-    recs2["cnt_off"] = [cnt_dev.data_ptr() + 4 * int(r["tile0"]) - d.data_ptr() for r in recs]
-    drec = torch.from_numpy(recs2.view(np.uint8).copy()).cuda()
-    out = torch.full((total, H, Wd, Cc), -7.0, device="cuda")
-    scratch = torch.full((tiles,), 123456, dtype=torch.int32, device="cuda")  # must be unused
-    C.json_parse_instances(len(recs), tiles, drec.data_ptr(), dmap.data_ptr(), d.data_ptr(), H,
-                           Wd, Cc, scratch.data_ptr(), out.data_ptr(), s, count_pass=False)
-    torch.cuda.synchronize()
-    assert list(drec.cpu().numpy().view(REC)["status"]) == [0, 0, 0]
-    np.testing.assert_array_equal(out.cpu().numpy(), np.concatenate(xs))
+        np.testing.assert_array_equal(crc.cpu().numpy(), crc2.cpu().numpy())
+        assert list(tok.cpu().numpy()) == [len(x) * H * Wd * Cc for x in xs]
+        assert list(drec.cpu().numpy().view(REC)["status"]) == [0] * len(recs)
+        c = cnt.cpu().numpy()
+        for i, r in enumerate(recs):
+            want = host_tile_tokens(buf, int(r["off"]), int(r["len"]))
+            nt = len(want)
+            blk = c[int(r["tile0"]) + grp0[i]:]
+            np.testing.assert_array_equal(blk[:nt], want)
+            sums = [want[t0:t0 + G].sum() for t0 in range(0, nt, G)]
+            np.testing.assert_array_equal(blk[nt:nt + len(sums)], sums)
+        # parse with the ingest blocks (has_cnt, cnt_off = block start), no count pass
+        recs2 = recs.copy()
+        recs2["has_cnt"] = 1
+        recs2["cnt_off"] = [cnt.data_ptr() + 4 * (int(r["tile0"]) + grp0[i]) - d.data_ptr()
+                            for i, r in enumerate(recs)]
+        drec = torch.from_numpy(recs2.view(np.uint8).copy()).cuda()
+        tile_rec = np.zeros(tiles, dtype=np.int32)
+        for i, r in enumerate(recs):
+            n = C.json_tile_count(int(r["off"]), int(r["len"]))
+            tile_rec[r["tile0"]:r["tile0"] + n] = i
+        dmap = torch.from_numpy(tile_rec).cuda()
+        out = torch.full((total, H, Wd, Cc), -7.0, device="cuda")
+        scratch = torch.full((tiles,), 123456, dtype=torch.int32, device="cuda")  # unused
+        C.json_parse_instances(len(recs), tiles, drec.data_ptr(), dmap.data_ptr(), d.data_ptr(),
+                               H, Wd, Cc, scratch.data_ptr(), out.data_ptr(), s,
+                               count_pass=False)
+        torch.cuda.synchronize()
+        assert list(drec.cpu().numpy().view(REC)["status"]) == [0] * len(recs)
+        np.testing.assert_array_equal(out.cpu().numpy(), np.concatenate(xs))
 
 
 def test_gpu_ingest_rejects_corrupt_batch_and_counts_images(broker):

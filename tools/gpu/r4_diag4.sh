@@ -32,3 +32,4 @@ timeout -k 10 300 rocprofv3 --kernel-trace -d $d/prof -o run -- \
     python bench.py --model resnet50 --steps 10 --warmup 3 --latency-load 0 > $d/prof.log 2>&1 || exit 1
 python tools/prof_summary.py $(find $d/prof -name '*.db' | head -1) --busy --top 14 > $d/busy.txt
 cat $d/busy.txt
+rm -rf $d/prof

@@ -65,6 +65,7 @@ if [ "${PART:-a}" = b ] || [ "${PART:-a}" = c ]; then
   python tools/prof_summary.py $db --top 14 > $out/kernel_stats.txt
   python tools/prof_summary.py $db --busy --top 14 > $out/kernel_busy.txt
   head -8 $out/kernel_stats.txt; cat $out/kernel_busy.txt
+  rm -rf $out/prof  # (the trace database: too large to bring back)
   timeout -k 10 240 python tools/bench_forward.py --model resnet50 --batches 64,256 --iters 30 \
       > $out/forward_resnet50.jsonl 2> $out/forward.err || exit 1
   timeout -k 10 240 python tools/bench_forward.py --model resnet50 --batches 256 --iters 30 \
@@ -74,4 +75,7 @@ if [ "${PART:-a}" = b ] || [ "${PART:-a}" = c ]; then
   timeout -k 10 240 python tools/bench_forward.py --model resnet20 --dtype fp8 --batches 256,4096 \
       --iters 50 >> $out/forward_resnet20.jsonl 2>> $out/forward.err || exit 1
   cat $out/forward_resnet50.jsonl $out/forward_resnet20.jsonl
+  timeout -k 10 240 python tools/bench_ingest.py > $out/ingest_kernels.jsonl 2> $out/ingest.err \
+      || { tail -5 $out/ingest.err; exit 1; }
+  cat $out/ingest_kernels.jsonl
 fi

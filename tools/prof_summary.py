@@ -7,9 +7,13 @@ import argparse
 import sqlite3
 
 
-def busy(c, top):
+def busy(c, top, tail_s=0.0):
     ev = []
-    for name, st, en in c.execute("select name, start, end from kernels where end > start"):
+    lo = 0
+    if tail_s > 0:
+        lo = c.execute("select max(end) from kernels").fetchone()[0] - int(tail_s * 1e9)
+    for name, st, en in c.execute("select name, start, end from kernels where end > start "
+                                  "and start >= ?", (lo,)):
         ev.append((st, 1, name))
         ev.append((en, -1, name))
     if not ev:
@@ -49,10 +53,13 @@ def main():
                     help="GPU busy share of the traced span, and each kernel's share of the "
                          "busy time with concurrent kernels splitting a time slice evenly (the "
                          "per-kernel durations double-count overlap when streams run together)")
+    ap.add_argument("--tail-s", type=float, default=0.0,
+                    help="with --busy: only the kernels of the trace's last S seconds (the timed "
+                         "window of a bench run, without its start-up)")
     a = ap.parse_args()
     c = sqlite3.connect(a.db)
     if a.busy:
-        busy(c, a.top)
+        busy(c, a.top, a.tail_s)
         return
     key = "name || ' grid=' || grid_x || 'x' || grid_y" if a.by_grid else "name"
     rows = c.execute(
