@@ -216,7 +216,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("ingest_crc_count",
         [](uintptr_t bytes, uintptr_t chunks, int nchunks, uintptr_t tables, uintptr_t crc_out,
            int nrec, int ngroups, uintptr_t recs, uintptr_t groups, uintptr_t counts,
-           uintptr_t rec_tokens, uintptr_t stream) {
+           uintptr_t gsum, uintptr_t stream) {
           gale::check_hip(
               gale::ingest_crc_count(reinterpret_cast<const uint8_t*>(bytes),
                                      reinterpret_cast<const gale::CrcChunk*>(chunks), nchunks,
@@ -225,12 +225,12 @@ PYBIND11_MODULE(_C, m) {
                                      reinterpret_cast<gale::JsonRecord*>(recs),
                                      reinterpret_cast<const int2*>(groups),
                                      reinterpret_cast<int*>(counts),
-                                     reinterpret_cast<int*>(rec_tokens),
+                                     reinterpret_cast<int*>(gsum),
                                      reinterpret_cast<hipStream_t>(stream)),
               "ingest_crc_count");
         },
-        "groups: int32 (record, first tile) pairs, kGroupTiles tiles each; counts: per record "
-        "tile0 + grp0 -> [tile counts][group sums]");
+        "groups: int32 (record, first tile) pairs, GROUP_TILES tiles each; counts: per record "
+        "tile0 + grp0 -> [tile counts][group sums]; gsum: one int per group");
   m.attr("GROUP_TILES") = gale::kGroupTiles;
   m.def("text_unpack", [](uintptr_t packed, uintptr_t tab, int64_t n, uintptr_t out,
                           uintptr_t stream) {

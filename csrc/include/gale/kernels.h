@@ -159,7 +159,7 @@ hipError_t cast_f32_bf16(int64_t n, float scale, float shift, const float* x, vo
 // The kernel raises each record's status (host zeroes it): 0 ok, 1 number-count mismatch,
 // 2 malformed number / element, 3 bad structure (ragged / wrong rank).
 constexpr int kJsonTileBytes = 2048;
-constexpr int kGroupTiles = 16;  // tiles per ingest counting wave / per group sum
+constexpr int kGroupTiles = 4;  // tiles per ingest counting workgroup (one per wave) / group sum
 struct JsonRecord {
   int64_t off;      // byte offset of the instances array inside the staged byte buffer
   int32_t len;      // array length in bytes
@@ -205,14 +205,14 @@ hipError_t crc32c_chunks(const uint8_t* bytes, const CrcChunk* chunks, int n,
 
 // The GPU ingest pass of one fetch buffer in ONE launch: workgroups [0, crc blocks) fold the CRC
 // windows (crc32c_chunks), the rest count the records' number tokens so the host learns each
-// record's image count without reading its text: one wave per tile group, groups[g] = (record,
-// record-relative first tile), kGroupTiles tiles each (a record's last group may be shorter).
-// Record i's count block at counts + tile0 + grp0 gets its tile counts and group sums (see
-// JsonRecord::has_cnt); rec_tokens[i] += its tokens (host zeroes it); invalid bytes raise
-// recs[i].status to 2.
+// record's image count without reading its text: one workgroup per tile group, groups[g] =
+// (record, record-relative first tile), kGroupTiles tiles each (a record's last group may be
+// shorter). Record i's count block at counts + tile0 + grp0 gets its tile counts and group sums
+// (see JsonRecord::has_cnt); gsum[g] = the tokens of group g (the host adds a record's groups);
+// invalid bytes raise recs[i].status to 2.
 hipError_t ingest_crc_count(const uint8_t* bytes, const CrcChunk* chunks, int nchunks,
                             const uint32_t* tables, uint32_t* crc_out, int nrec, int ngroups,
-                            JsonRecord* recs, const int2* groups, int* counts, int* rec_tokens,
+                            JsonRecord* recs, const int2* groups, int* counts, int* gsum,
                             hipStream_t stream);
 
 // Expands a nibble-packed span (csrc/codec/text_pack.h: 64-byte blocks, per-2-KiB-group

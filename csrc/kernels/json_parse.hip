@@ -625,33 +625,37 @@ __device__ __forceinline__ void count_tile(JsonRecord* recs, const int* tile_rec
   if (bad) atomicMax(&recs[ri].status, 2);
 }
 
-// The ingest pass's counting of one group of up to kGroupTiles consecutive tiles of a record
-// (one wave, the tiles in turn). The record's count block (at counts + tile0 + grp0) holds its
-// nt tile counts, then one sum per group: the parse finds a tile's first element index from at
-// most nt / kGroupTiles group sums plus < kGroupTiles tile counts, and the record's token total
-// takes one atomic per group - per-tile atomics on one counter serialise (an ImageNet record is
-// ~850 tiles: 80 of the 92 us of a 15 MB fetch's ingest launch, tools/bench_ingest.py).
+// The ingest pass's counting of one tile group (one workgroup: wave w counts tile tl0 + w of the
+// record, up to kGroupTiles = kWaves tiles). The record's count block (at counts + tile0 + grp0)
+// gets its nt tile counts, then one sum per group; gsum[g] (contiguous, read back by the host)
+// gets the group's sum too, and the host adds a record's group sums for its image count. The
+// parse finds a tile's first element index from nt / kGroupTiles group sums plus < kGroupTiles
+// tile counts. (Per-tile atomics on one record counter serialise: an ImageNet record is ~850
+// tiles, 80 of the 92 us of a 15 MB fetch's ingest launch, tools/bench_ingest.py.)
 __device__ __forceinline__ void count_group(JsonRecord* recs, const int2* groups, int g,
-                                            const uint8_t* bytes, int* counts, int* rec_tokens) {
+                                            const uint8_t* bytes, int* counts, int* gsum,
+                                            int* lds4) {
+  const int wave = threadIdx.x >> 6;
   const int2 gr = groups[g];  // (record, record-relative first tile)
   const JsonRecord r = recs[gr.x];
   const int nt = record_tiles(r);
-  const int n = min(kGroupTiles, nt - gr.y);
-  int* blk = counts + r.tile0 + (int)r.grp0;
-  int acc = 0;
-  bool any_bad = false;
-  for (int i = 0; i < n; ++i) {
+  const int tl = gr.y + wave;
+  int cnt = 0;
+  if (tl < nt) {
     bool bad;
-    const int cnt = tile_tokens(r, gr.y + i, bytes, &bad);
-    any_bad |= bad;
-    acc += cnt;
-    if ((threadIdx.x & 63) == 0) blk[gr.y + i] = cnt;
+    cnt = tile_tokens(r, tl, bytes, &bad);
+    if ((threadIdx.x & 63) == 0) counts[r.tile0 + (int)r.grp0 + tl] = cnt;
+    if (bad) atomicMax(&recs[gr.x].status, 2);
   }
-  if ((threadIdx.x & 63) == 0) {
-    blk[nt + gr.y / kGroupTiles] = acc;
-    atomicAdd(&rec_tokens[gr.x], acc);
+  if ((threadIdx.x & 63) == 0) lds4[wave] = cnt;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int acc = 0;
+#pragma unroll
+    for (int w = 0; w < kGroupTiles; ++w) acc += lds4[w];
+    counts[r.tile0 + (int)r.grp0 + nt + gr.y / kGroupTiles] = acc;
+    gsum[g] = acc;
   }
-  if (any_bad) atomicMax(&recs[gr.x].status, 2);
 }
 
 __global__ __launch_bounds__(256) void json_count_kernel(JsonRecord* recs, const int* tile_rec,
@@ -664,21 +668,22 @@ __global__ __launch_bounds__(256) void json_count_kernel(JsonRecord* recs, const
 }
 
 // The ingest pass of a fetch buffer in one launch: CRC window workgroups first (they stage the
-// CRC tables in LDS behind one barrier; the branch is uniform per workgroup), then counting,
-// one wave per tile group.
+// CRC tables in LDS behind one barrier), then one workgroup per tile group (the branches are
+// uniform per workgroup).
+static_assert(kGroupTiles == kWaves, "one tile group per counting workgroup");
 __global__ __launch_bounds__(256) void ingest_crc_count_kernel(
     const uint8_t* bytes, const CrcChunk* chunks, int nchunks, const uint32_t* tables,
     uint32_t* crc_out, int crc_blocks, JsonRecord* recs, const int2* groups, int ngroups,
-    int* counts, int* rec_tokens) {
+    int* counts, int* gsum) {
+  __shared__ uint32_t T[crc::kTableWords];
   if ((int)blockIdx.x < crc_blocks) {
-    __shared__ uint32_t T[crc::kTableWords];
     crc::crc_stage_tables(tables, T);
     crc::crc_windows(bytes, chunks, nchunks, T, crc_out, blockIdx.x, crc_blocks);
     return;
   }
-  const int g = ((int)blockIdx.x - crc_blocks) * kWaves + (threadIdx.x >> 6);
+  const int g = (int)blockIdx.x - crc_blocks;
   if (g >= ngroups) return;
-  count_group(recs, groups, g, bytes, counts, rec_tokens);
+  count_group(recs, groups, g, bytes, counts, gsum, reinterpret_cast<int*>(T));
 }
 
 __global__ __launch_bounds__(256) void json_parse_kernel(JsonRecord* recs, const int* tile_rec,
@@ -825,16 +830,15 @@ int json_tile_count(int64_t off, int32_t len) {
 
 hipError_t ingest_crc_count(const uint8_t* bytes, const CrcChunk* chunks, int nchunks,
                             const uint32_t* tables, uint32_t* crc_out, int nrec, int ngroups,
-                            JsonRecord* recs, const int2* groups, int* counts, int* rec_tokens,
+                            JsonRecord* recs, const int2* groups, int* counts, int* gsum,
                             hipStream_t stream) {
   if (nrec <= 0) ngroups = 0;
   int crc_blocks = (nchunks + crc::kCrcWaves - 1) / crc::kCrcWaves;
   if (crc_blocks > 1024) crc_blocks = 1024;  // (windows loop: the table load is amortised)
-  const int cnt_blocks = (ngroups + kWaves - 1) / kWaves;
-  if (crc_blocks + cnt_blocks == 0) return hipSuccess;
-  hipLaunchKernelGGL(ingest_crc_count_kernel, dim3(crc_blocks + cnt_blocks), dim3(256), 0, stream,
+  if (crc_blocks + ngroups == 0) return hipSuccess;
+  hipLaunchKernelGGL(ingest_crc_count_kernel, dim3(crc_blocks + ngroups), dim3(256), 0, stream,
                      bytes, chunks, nchunks, tables, crc_out, crc_blocks, recs, groups, ngroups,
-                     counts, rec_tokens);
+                     counts, gsum);
   return hipGetLastError();
 }
 

@@ -132,8 +132,8 @@ void GpuIngest::run(int lane, const kafka::Fetched& f, uint8_t* dev, size_t dev_
   const size_t o_chunks = align16(ng * 2 * sizeof(uint32_t));
   const size_t o_groups = o_chunks + align16(nc * sizeof(CrcChunk));
   const size_t o_recs = o_groups + align16((size_t)ngroups * sizeof(int2));
-  const size_t o_tok = o_recs + nr * sizeof(JsonRecord);  // (JsonRecord is 48 bytes)
-  const size_t o_crc = o_tok + align16(nr * 4);
+  const size_t o_gsum = o_recs + nr * sizeof(JsonRecord);  // (JsonRecord is 48 bytes)
+  const size_t o_crc = o_gsum + align16((size_t)ngroups * 4);
   const size_t io_bytes = o_crc + align16(nc * 4);
   check_hip(hipSetDevice(device_), "ingest: hipSetDevice");
   // count blocks: per record its tile counts then its group sums (ntiles + ngroups ints)
@@ -164,7 +164,6 @@ void GpuIngest::run(int lane, const kafka::Fetched& f, uint8_t* dev, size_t dev_
     }
     tile += nt;
   }
-  memset(L.h_io + o_tok, 0, nr * 4);  // token counters start at zero (no device memset)
   // ---- device: text span -> mirror (packed: H2D of the packed stream, expanded in place),
   // plan, CRC windows, token counts, results back
   hipStream_t st = L.stream;
@@ -187,7 +186,7 @@ void GpuIngest::run(int lane, const kafka::Fetched& f, uint8_t* dev, size_t dev_
   text_bytes_ += (int64_t)span;
   link_bytes_ += (int64_t)link;
   uint32_t* d_crc = reinterpret_cast<uint32_t*>(L.d_io + o_crc);
-  int* d_tok = reinterpret_cast<int*>(L.d_io + o_tok);
+  int* d_gsum = reinterpret_cast<int*>(L.d_io + o_gsum);
   JsonRecord* d_rec = reinterpret_cast<JsonRecord*>(L.d_io + o_recs);
   // the per-tile token counts stay with the fetch buffer: at the end of its device mirror when
   // they fit behind the text (and the packed stream), so the replica that later parses these
@@ -205,7 +204,7 @@ void GpuIngest::run(int lane, const kafka::Fetched& f, uint8_t* dev, size_t dev_
   // CRC windows and token counts: one launch, one pass of workgroups over the buffer
   check_hip(ingest_crc_count(dev, reinterpret_cast<const CrcChunk*>(L.d_io + o_chunks), (int)nc,
                              d_tables_, d_crc, (int)nr, ngroups, d_rec,
-                             reinterpret_cast<const int2*>(L.d_io + o_groups), d_cnt, d_tok, st),
+                             reinterpret_cast<const int2*>(L.d_io + o_groups), d_cnt, d_gsum, st),
             "ingest: crc32c + count");
   check_hip(hipMemcpyAsync(L.h_io + o_recs, L.d_io + o_recs, io_bytes - o_recs,
                            hipMemcpyDeviceToHost, st),
@@ -227,19 +226,23 @@ void GpuIngest::run(int lane, const kafka::Fetched& f, uint8_t* dev, size_t dev_
     kafka::Reader cr(f.buf.get() + bs.off + kafka::kBatchCrcOffset, 4);
     io.batch_ok[b] = got == cr.u32();
   }
-  const int* tok = reinterpret_cast<const int*>(L.h_io + o_tok);
+  // a record's tokens: the sums of its tile groups
+  const int* gsum = reinterpret_cast<const int*>(L.h_io + o_gsum);
   const JsonRecord* rst = reinterpret_cast<const JsonRecord*>(L.h_io + o_recs);
   const int64_t per = (int64_t)H * W * C;
   for (size_t j = 0; j < nr; ++j) {
     const size_t i = (size_t)rec_of[j];
+    const int64_t g1 = j + 1 < nr ? rst[j + 1].grp0 : ngroups;
+    int64_t tok = 0;
+    for (int64_t g = rst[j].grp0; g < g1; ++g) tok += gsum[g];
     if (rst[j].status != 0) {
       io.status[i] = codec::BAD_NUMBER;
-    } else if (tok[j] == 0) {
+    } else if (tok == 0) {
       io.status[i] = codec::EMPTY;
-    } else if (tok[j] % per != 0) {
+    } else if (tok % per != 0) {
       io.status[i] = codec::BAD_SHAPE;
     } else {
-      io.images[i] = (int32_t)(tok[j] / per);
+      io.images[i] = (int32_t)(tok / per);
       if (cnt_base >= 0)
         io.cnt_off[i] = cnt_base + (hr[j].tile0 + hr[j].grp0) * (int64_t)sizeof(int);
     }

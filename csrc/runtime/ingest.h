@@ -4,7 +4,7 @@
 // count its images before micro-batching: ~35 KB of host reads per CIFAR image on top of the
 // socket receive. With an Ingest attached, a pinned fetch buffer is instead DMA'd once to its
 // device mirror (PinnedPool::mirror) and the GPU computes the batch CRCs and the per-record
-// element counts (csrc/kernels/ingest.hip, json_count_records). The host reads only Kafka framing
+// element counts in one launch (ingest_crc_count, csrc/kernels/json_parse.hip). The host reads only Kafka framing
 // and a bounded prefix/suffix of each record (codec::scan_envelope); the GPU replica later parses
 // the records straight from the device mirror, so the JSON text crosses PCIe once and is never
 // read by a host core.

@@ -283,11 +283,12 @@ def host_tile_tokens(buf, off, ln):
 
 
 def test_gpu_fused_ingest_kernel_matches_separate_passes():
-    """ingest_crc_count (CRC windows + token counts in ONE launch, one wave per group of
+    """ingest_crc_count (CRC windows + token counts in ONE launch, one workgroup per group of
     GROUP_TILES tiles) produces the raw window CRCs of crc32c_chunks, every record's count block
-    (tile token counts as counted on the host, then one sum per tile group) and the per-record
-    totals; the parse then reuses those blocks (has_cnt, no counting launch) and decodes the same
-    tensor. Records of 1-3 CIFAR images and one ImageNet image (~850 tiles, 54 groups)."""
+    (tile token counts as counted on the host, then one sum per tile group) and the group sums
+    the host adds per record; the parse then reuses those blocks (has_cnt, no counting launch)
+    and decodes the same tensor. Records of 1-3 CIFAR images and one ImageNet image (~850
+    tiles)."""
     import os
 
     rng = np.random.default_rng(8)
@@ -318,16 +319,19 @@ def test_gpu_fused_ingest_kernel_matches_separate_passes():
         drec = torch.from_numpy(recs.view(np.uint8).copy()).cuda()
         crc = torch.zeros(len(wins), dtype=torch.int32, device="cuda")
         cnt = torch.full((tiles + len(groups),), -1, dtype=torch.int32, device="cuda")
-        tok = torch.zeros(len(recs), dtype=torch.int32, device="cuda")
+        gsum = torch.full((len(groups),), -1, dtype=torch.int32, device="cuda")
         C.ingest_crc_count(d.data_ptr(), dch.data_ptr(), len(wins), tables.data_ptr(),
                            crc.data_ptr(), len(recs), len(groups), drec.data_ptr(),
-                           dgrp.data_ptr(), cnt.data_ptr(), tok.data_ptr(), s)
+                           dgrp.data_ptr(), cnt.data_ptr(), gsum.data_ptr(), s)
         crc2 = torch.zeros(len(wins), dtype=torch.int32, device="cuda")
         C.crc32c_chunks(d.data_ptr(), dch.data_ptr(), len(wins), tables.data_ptr(),
                         crc2.data_ptr(), s)
         torch.cuda.synchronize()
         np.testing.assert_array_equal(crc.cpu().numpy(), crc2.cpu().numpy())
-        assert list(tok.cpu().numpy()) == [len(x) * H * Wd * Cc for x in xs]
+        gs = gsum.cpu().numpy()
+        bounds = grp0 + [len(groups)]
+        assert [gs[bounds[i]:bounds[i + 1]].sum() for i in range(len(recs))] == \
+            [len(x) * H * Wd * Cc for x in xs]
         assert list(drec.cpu().numpy().view(REC)["status"]) == [0] * len(recs)
         c = cnt.cpu().numpy()
         for i, r in enumerate(recs):
@@ -337,6 +341,7 @@ def test_gpu_fused_ingest_kernel_matches_separate_passes():
             np.testing.assert_array_equal(blk[:nt], want)
             sums = [want[t0:t0 + G].sum() for t0 in range(0, nt, G)]
             np.testing.assert_array_equal(blk[nt:nt + len(sums)], sums)
+            np.testing.assert_array_equal(gs[bounds[i]:bounds[i + 1]], sums)
         # parse with the ingest blocks (has_cnt, cnt_off = block start), no count pass
         recs2 = recs.copy()
         recs2["has_cnt"] = 1

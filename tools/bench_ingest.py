@@ -86,23 +86,24 @@ def main():
         drec = torch.from_numpy(recs.view(np.uint8).copy()).cuda()
         crc = torch.zeros(len(ch), dtype=torch.int32, device="cuda")
         cnt = torch.zeros(tiles + len(groups), dtype=torch.int32, device="cuda")
-        tok = torch.zeros(nrec, dtype=torch.int32, device="cuda")
+        cnt_p = torch.zeros(tiles, dtype=torch.int32, device="cuda")  # the parse's own pass
+        gsum = torch.zeros(max(1, len(groups)), dtype=torch.int32, device="cuda")
         H, W, Cc = shape
         out = torch.empty((nrec, H, W, Cc), device="cuda")
 
         def ingest():
             C.ingest_crc_count(d.data_ptr(), dch.data_ptr(), len(ch), tables.data_ptr(),
                                crc.data_ptr(), nrec, len(groups), drec.data_ptr(),
-                               dgrp.data_ptr(), cnt.data_ptr(), tok.data_ptr(), s)
+                               dgrp.data_ptr(), cnt.data_ptr(), gsum.data_ptr(), s)
 
         def crc_only():
             C.ingest_crc_count(d.data_ptr(), dch.data_ptr(), len(ch), tables.data_ptr(),
                                crc.data_ptr(), 0, 0, drec.data_ptr(), dgrp.data_ptr(),
-                               cnt.data_ptr(), tok.data_ptr(), s)
+                               cnt.data_ptr(), gsum.data_ptr(), s)
 
         def parse():
             C.json_parse_instances(nrec, tiles, drec.data_ptr(), dmap.data_ptr(), d.data_ptr(), H,
-                                   W, Cc, cnt.data_ptr(), out.data_ptr(), s, count_pass=True)
+                                   W, Cc, cnt_p.data_ptr(), out.data_ptr(), s, count_pass=True)
 
         # the replica's parse of ingested records: the ingest pass's count blocks, no count pass
         ingest()
@@ -114,7 +115,8 @@ def main():
 
         def parse_cnt():
             C.json_parse_instances(nrec, tiles, drec2.data_ptr(), dmap.data_ptr(), d.data_ptr(),
-                                   H, W, Cc, cnt.data_ptr(), out.data_ptr(), s, count_pass=False)
+                                   H, W, Cc, cnt_p.data_ptr(), out.data_ptr(), s,
+                                   count_pass=False)
 
         for kname, fn in (("crc+count", ingest), ("crc", crc_only), ("count+parse", parse),
                           ("parse(ingest counts)", parse_cnt)):
