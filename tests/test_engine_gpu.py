@@ -433,7 +433,8 @@ def test_gpu_locality_split_steals_parse_from_host_pinned():
         cfg = GaleConfig(topology_name="g", input_topic="in", output_topic="out",
                          bootstrap=f"127.0.0.1:{b.port}", start_offset="earliest",
                          max_batch=32, max_wait_us=300, output_key="input", replicas=2,
-                         source_parallelism=2, locality_split=2, decode_threads=2)
+                         source_parallelism=2, locality_split=2, decode_threads=2,
+                         text_pack=False)  # (a stolen record is parsed from its host text)
         eng = Engine(cfg, devices=[0], max_records=n, params=params)
         eng.start()
         assert eng.wait(180), eng.stats()
