@@ -21,9 +21,16 @@ GpuIngest::GpuIngest(int device, int lanes, int poll_us)
   check_hip(hipMalloc(reinterpret_cast<void**>(&d_tables_), t.size() * 4), "ingest: tables");
   check_hip(hipMemcpy(d_tables_, t.data(), t.size() * 4, hipMemcpyHostToDevice),
             "ingest: tables H2D");
+  // ingest lanes at the highest stream priority: their kernels are short, and a fetch waits on
+  // them synchronously while its pinned buffer is held - behind a replica's forward kernels the
+  // decode queue (and the buffers in it) would grow
+  int prio_least = 0, prio_greatest = 0;
+  if (hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest) != hipSuccess)
+    prio_greatest = prio_least = 0;
   for (int i = 0; i < std::max(1, lanes); ++i) {
     auto L = std::make_unique<Lane>();
-    check_hip(hipStreamCreateWithFlags(&L->stream, hipStreamNonBlocking), "ingest: stream");
+    check_hip(hipStreamCreateWithPriority(&L->stream, hipStreamNonBlocking, prio_greatest),
+              "ingest: stream");
     check_hip(hipEventCreateWithFlags(&L->done, hipEventDisableTiming), "ingest: event");
     lanes_.push_back(std::move(L));
   }
