@@ -691,6 +691,7 @@ def main(argv=None) -> int:
         torch.cuda.synchronize()
     eng.reset_stats()
     cpu0 = thread_cpu_seconds()
+    cgt0 = _cgroup_cpu_stat()
     c0 = eng.completed
     t0 = time.perf_counter()
     m0 = time.clock_gettime_ns(time.CLOCK_MONOTONIC)
@@ -712,6 +713,17 @@ def main(argv=None) -> int:
         torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     cpu1 = thread_cpu_seconds()
+    cgt1 = _cgroup_cpu_stat()
+    # cgroup CPU accounting of the timed window: at the CPU quota the CFS bandwidth controller
+    # stops the whole group for the rest of each 100 ms period, which alternates fast and slow
+    # steps (the step spread) without changing the mean
+    cg_timed = {}
+    if cgt0 and cgt1:
+        d = {k: cgt1.get(k, 0) - cgt0.get(k, 0) for k in cgt1}
+        cg_timed = {"cores": round(d.get("usage_usec", 0) / 1e6 / max(elapsed, 1e-9), 2),
+                    "throttled_ms": round(d.get("throttled_usec", 0) / 1e3, 1),
+                    "throttled_periods": int(d.get("nr_throttled", 0)),
+                    "periods": int(d.get("nr_periods", 0))}
     done_records = eng.completed - c0
     st = eng.stats()
     if timeline:
@@ -861,6 +873,7 @@ def main(argv=None) -> int:
                                  "range_pct": round(100 * (max(step_rates) - min(step_rates))
                                                     / med, 1)},
             "step_rates": [round(r) for r in step_rates],
+            "timed_cgroup_rank0": cg_timed,
             "warmup_s": round(warm_s, 2), "warmup_rates": [round(r) for r in warm_rates],
             "json_mb_per_s_rank0": round(st["bytes_in"] / elapsed / 1e6, 1),
             # host -> GPU link bytes per fetched text byte (nibble transport: ~0.5)

@@ -21,16 +21,12 @@ GpuIngest::GpuIngest(int device, int lanes, int poll_us)
   check_hip(hipMalloc(reinterpret_cast<void**>(&d_tables_), t.size() * 4), "ingest: tables");
   check_hip(hipMemcpy(d_tables_, t.data(), t.size() * 4, hipMemcpyHostToDevice),
             "ingest: tables H2D");
-  // ingest lanes at the highest stream priority: their kernels are short, and a fetch waits on
-  // them synchronously while its pinned buffer is held - behind a replica's forward kernels the
-  // decode queue (and the buffers in it) would grow
-  int prio_least = 0, prio_greatest = 0;
-  if (hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest) != hipSuccess)
-    prio_greatest = prio_least = 0;
+  // (ingest lanes at the highest stream priority were measured and dropped: the replicas' batch
+  // kernels then queue behind every fetch's ingest, ResNet-20 device time per batch 0.4 -> 2 ms,
+  // profiles/r4_ab_ingest_priority.jsonl)
   for (int i = 0; i < std::max(1, lanes); ++i) {
     auto L = std::make_unique<Lane>();
-    check_hip(hipStreamCreateWithPriority(&L->stream, hipStreamNonBlocking, prio_greatest),
-              "ingest: stream");
+    check_hip(hipStreamCreateWithFlags(&L->stream, hipStreamNonBlocking), "ingest: stream");
     check_hip(hipEventCreateWithFlags(&L->done, hipEventDisableTiming), "ingest: event");
     lanes_.push_back(std::move(L));
   }
