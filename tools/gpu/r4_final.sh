@@ -6,6 +6,7 @@
 #           bench.py --gpus 2 (rehearsal / refusal),
 #           kernel trace of the default bench, forward-alone ResNet-50 / ResNet-20
 #   PART=c  only the kernel trace and the forward-alone runs
+#   PART=b2 config 4 x3, then PART=c
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 out=gpurun_out/final
@@ -51,8 +52,10 @@ elif [ "$PART" = b ]; then
   fi
   tail -2 $out/gpus2_refused.log
   one rehearsal_world2 300 --gpus 2 --shared-gpu-rehearsal --steps 10 --warmup 3 || exit 1
+elif [ "$PART" = b2 ]; then
+  for i in 1 2 3; do one c4_resnet50_$i 300 --model resnet50 --steps 10 --warmup 3 || exit 1; done
 fi
-if [ "${PART:-a}" = b ] || [ "${PART:-a}" = c ]; then
+if [ "${PART:-a}" = b ] || [ "${PART:-a}" = c ] || [ "${PART:-a}" = b2 ]; then
   export TMPDIR=/tmp
   # one hardware queue per HIP stream under the profiler: its queue interception crashed when
   # the engine's streams (replicas + ingest lanes, > 4 from several threads) shared HIP's
