@@ -567,3 +567,48 @@ def test_gpu_pinned_pool_backpressure(broker):
     assert st["pinned_chunks"] <= 2, st
     assert st["pinned_heap_budget"] == 0 and st["pinned_heap_too_large"] == 0, st
     assert st["ingested_records"] == st["records_in"] == len(xs), st
+
+
+@pytest.mark.parametrize("pack", [True, False])
+def test_gpu_engine_resnet50_imagenet_records(broker, pack):
+    """ImageNet-size records (224x224x3, ~1.7 MB of JSON per image, ~850 parse tiles) through the
+    whole engine: the bounce receive + device text expansion (pack) or raw fetch bodies, the
+    grouped ingest count (a record spans many 4-tile groups; the parse takes each tile's first
+    element index from the group sums), the parse and the ResNet-50 forward. Outputs are
+    key-matched to the same replica's forward of the original float32 tensors."""
+    from gale.parallel.weights import materialize_weights
+    from gale.runtime.replica import ModelReplica
+
+    if pack and not C.text_pack_fast():
+        pytest.skip("no AVX-512 VBMI on this host")
+    net = get_model("resnet50")
+    params = init_params(net, seed=3, calib_batch=4)
+    rng = np.random.default_rng(4)
+    xs = {}
+    for i, n in enumerate([1, 2, 1]):
+        x = rng.random((n,) + net.input_shape, dtype=np.float32)
+        xs[f"i{i}".encode()] = x
+        broker.append("in", 0, [C.encode_instances(x)], [f"i{i}".encode()])
+    cfg = GaleConfig(topology_name="g", input_topic="in", output_topic="out", model="resnet50",
+                     bootstrap=f"127.0.0.1:{broker.port}", start_offset="earliest",
+                     max_batch=8, max_wait_us=2000, output_key="input", gpu_ingest=True,
+                     text_pack=pack)
+    eng = Engine(cfg, devices=[0], max_records=len(xs), params=params)
+    eng.start()
+    assert eng.wait(180), eng.stats()
+    eng.stop()
+    st = eng.stats()
+    assert st["errors"] == 0 and st["ingested_records"] == len(xs), st
+    if pack:
+        assert st["sparse_fetches"] > 0 and st["restored_fetches"] == 0, st
+    out = {r["key"]: r["value"] for r in broker.read("out", 0)}
+    assert set(out) == set(xs)
+    rep = ModelReplica(net, materialize_weights(net, torch.device("cuda", 0), params=params),
+                       max_batch=8, slots=1)
+    for k, x in xs.items():
+        want = rep.infer_eager(torch.from_numpy(x)).cpu().numpy()
+        got = np.array(json.loads(out[k])["predictions"], dtype=np.float32)
+        assert got.shape == want.shape, k
+        # same kernels, the same floats in (the GPU parse is exact): equal up to a kernel
+        # choice that may differ with the batch size
+        np.testing.assert_allclose(got, want, rtol=2e-3, atol=1e-6, err_msg=k.decode())
