@@ -7,6 +7,8 @@
 #include <fcntl.h>
 #include <netinet/in.h>
 #include <netinet/tcp.h>
+#include <pthread.h>
+#include <signal.h>
 #include <sys/socket.h>
 #include <sys/uio.h>
 #include <unistd.h>
@@ -183,6 +185,14 @@ void Broker::start() {
   running_ = true;
   thread_ = std::thread([this] {
     name_thread("gl-brk-acc");
+    // writev() / splice() to a socket whose peer has gone raise SIGPIPE, which would kill an
+    // embedding process that does not ignore it (Python does, a C++ host need not): block it in
+    // the accept thread, whose mask the connection threads inherit, so the calls just fail
+    // with EPIPE and the connection closes
+    sigset_t pipe_set;
+    sigemptyset(&pipe_set);
+    sigaddset(&pipe_set, SIGPIPE);
+    pthread_sigmask(SIG_BLOCK, &pipe_set, nullptr);
     accept_loop();
   });
 }

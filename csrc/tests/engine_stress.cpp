@@ -9,6 +9,10 @@
 //   2. faults:   a replica crash (its in-flight batches re-queue to the survivors), injected
 //                parse errors and producer failures -> every record still accounted for
 //   3. stop while busy: Engine::stop() with records still queued (drain + commit path)
+//   4. bounce receive: four consumer threads at once receive through the bounce tap
+//      (runtime/pack_tap.h: L2 window, framing walker, nibble packing) over plain, lz4- and
+//      gzip-compressed and legacy magic-1 batches; every value restored from the packed stream
+//      equals what was appended
 // The reference's only concurrency primitive is `synchronized (collector)` in the producer
 // callback (KafkaBolt.java:129-143); gale's queues and callbacks are what this exercises.
 //
@@ -20,9 +24,15 @@
 #include <string>
 #include <vector>
 
+#include <thread>
+
 #include "../codec/json_codec.h"
+#include "../codec/text_pack.h"
 #include "../kafka/broker.h"
+#include "../kafka/client.h"
+#include "../kafka/compress.h"
 #include "../runtime/engine.h"
+#include "../runtime/pack_tap.h"
 
 using namespace gale;
 
@@ -98,6 +108,83 @@ void add_stubs(Engine& e, int n, int delay_us) {
     e.add_replica(std::make_shared<StubReplica>(H, W, C, CLASSES, 32, delay_us, true));
 }
 
+// Scenario 4: the values appended to partition p of `topic`, by offset.
+std::vector<std::vector<std::string>> preload_formats(kafka::Broker& b, const std::string& topic,
+                                                      int parts, int per_part, uint64_t seed) {
+  std::mt19937_64 rng(seed);
+  std::uniform_real_distribution<float> u(0.f, 1.f);
+  std::vector<std::vector<std::string>> vals((size_t)parts);
+  for (int p = 0; p < parts; ++p) {
+    int k = 0;
+    while (k < per_part) {
+      const int n = std::min(per_part - k, 5 + (int)(rng() % 20));
+      std::vector<std::string> v;
+      for (int i = 0; i < n; ++i) {
+        const int imgs = 1 + (int)(rng() % 2);
+        std::vector<float> x((size_t)imgs * 32 * 32 * 3);  // ~35 KB of text per image
+        for (float& f : x) f = u(rng);
+        std::string sv;
+        codec::encode_instances(x.data(), imgs, 32, 32, 3, sv);
+        v.push_back(std::move(sv));
+      }
+      // plain, lz4, gzip, legacy magic 1 (partition 0 plain only: sparse fetches throughout)
+      const int kind = p == 0 ? 0 : (int)(rng() % 4);
+      if (kind == 3) {
+        std::vector<kafka::LegacyRecord> lr(v.size());
+        for (size_t i = 0; i < v.size(); ++i) {
+          lr[i].value = v[i];
+          lr[i].timestamp = 1000 + (int64_t)i;
+        }
+        b.append_legacy(topic, p, 1, lr, kafka::CODEC_NONE);
+      } else {
+        std::vector<kafka::RecordIn> recs(v.size());
+        for (size_t i = 0; i < v.size(); ++i) recs[i].value = v[i];
+        kafka::Writer w;
+        kafka::encode_batch(w, recs.data(), recs.size(), 0, 1000);
+        const int codec = kind == 1 ? kafka::CODEC_LZ4 : kind == 2 ? kafka::CODEC_GZIP
+                                                                   : kafka::CODEC_NONE;
+        b.append_shared(topic, p,
+                        std::make_shared<const std::string>(kafka::compress_batch(w.buf, codec)));
+      }
+      for (auto& sv : v) vals[(size_t)p].push_back(std::move(sv));
+      k += n;
+    }
+  }
+  return vals;
+}
+
+void consume_bounce(int port, const std::string& topic, int p,
+                    const std::vector<std::string>& want, int* bad, int64_t* sparse) {
+  kafka::ConsumerConfig cc;
+  cc.bootstrap = "127.0.0.1:" + std::to_string(port);
+  cc.max_wait_ms = 20;
+  cc.fetch_max_bytes = 1 << 20;
+  cc.partition_max_bytes = 600 << 10;
+  cc.check_crcs = false;  // (the host copy of a bounce-received body is sparse)
+  const size_t chunk = codec::pack_layout_bytes((size_t)cc.fetch_max_bytes + (1 << 20)) + 4096;
+  kafka::Consumer cons(cc, [chunk](size_t n) { return kafka::heap_alloc(std::max(n, chunk)); });
+  cons.set_recv_tap(std::make_shared<BouncePackTap>(
+      chunk, [](const uint8_t*) { return true; }, 1, (size_t)(8 + 8 * p) << 10));
+  cons.assign(topic, {p});
+  cons.seek_to("earliest");
+  size_t got = 0;
+  for (int round = 0; round < 4000 && got < want.size(); ++round) {
+    for (kafka::Fetched& f : cons.poll()) {
+      if (f.sparse) ++*sparse;
+      f.restore();
+      for (const kafka::RecordRef& r : f.records) {
+        const std::string v(reinterpret_cast<const char*>(f.buf.get()) + r.value_off,
+                            r.value_len > 0 ? (size_t)r.value_len : 0);
+        if (r.offset < 0 || (size_t)r.offset >= want.size() || r.poison ||
+            v != want[(size_t)r.offset])
+          ++*bad;
+        ++got;
+      }
+    }
+  }
+  if (got != want.size()) ++*bad;
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -158,6 +245,28 @@ int main(int argc, char** argv) {
     CHECK(!e.running(), "engine still running after stop()");
     fprintf(stderr, "[stress] stop-while-busy: completed %lld before stop\n",
             (long long)e.completed());
+  }
+  if (codec::text_pack_fast()) {  // 4. bounce receive over plain / compressed / legacy batches
+    const int parts = 4;
+    broker.create_topic("bounce", parts);
+    const auto want = preload_formats(broker, "bounce", parts, std::max(40, n / 40), 11);
+    std::vector<int> bad((size_t)parts, 0);
+    std::vector<int64_t> sparse((size_t)parts, 0);
+    std::vector<std::thread> ts;
+    for (int p = 0; p < parts; ++p)
+      ts.emplace_back(consume_bounce, broker.port(), "bounce", p, std::cref(want[(size_t)p]),
+                      &bad[(size_t)p], &sparse[(size_t)p]);
+    for (auto& t : ts) t.join();
+    int64_t nbad = 0, nsparse = 0;
+    for (int p = 0; p < parts; ++p) {
+      nbad += bad[(size_t)p];
+      nsparse += sparse[(size_t)p];
+    }
+    CHECK(nbad == 0, "%lld bounce-received values differ from what was appended",
+          (long long)nbad);
+    CHECK(nsparse > 0, "no fetch was received sparse");
+    fprintf(stderr, "[stress] bounce receive: %lld sparse fetches, values OK\n",
+            (long long)nsparse);
   }
   broker.stop();
   if (failures) {
