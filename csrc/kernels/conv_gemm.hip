@@ -335,7 +335,11 @@ hipError_t conv2d_gemm(const ConvDesc& d, int batch, const void* x, const void* 
   a.cin_blocks = d.stem ? 1 : d.Cin / 64;
   a.relu = d.relu;
   a.has_res = d.has_res && res != nullptr;
-  const int bn = (d.Npad % 128 == 0) ? 128 : 64;
+  // 64-channel tiles for the single-k-step (K = 64) 1x1 convs: these are bound by their
+  // epilogue traffic, and half-width tiles (24 KB of LDS, 91 VGPRs) put 5 workgroups on a CU
+  // instead of 4 (ResNet-50 batch 256: 4.87 -> 4.81 ms; at K = 128 / 256 / 512 the same change
+  // costs 0.6 / 1.6 / 2.6 %, profiles/r4_resnet50_layers.txt)
+  const int bn = (d.Npad % 128 == 0 && !(d.K == 64 && d.KH == 1 && !d.stem)) ? 128 : 64;
   constexpr int BM = 128;
   const int m_tiles = (a.M + BM - 1) / BM;
   a.n_tiles = d.Npad / bn;
