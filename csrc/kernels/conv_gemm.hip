@@ -347,8 +347,8 @@ hipError_t conv2d_gemm(const ConvDesc& d, int batch, const void* x, const void* 
   a.n_tiles = d.Npad / bn;
   a.nwg = m_tiles * a.n_tiles;
   // per-shape choice: the packed stem; K = 64 (one k-step: 1x1 convs on 64 channels) in the
-  // single-stage form at 4 workgroups per CU; everything else double-buffered; 128-channel
-  // tiles when Npad allows, else 64
+  // single-stage form with 64-channel tiles, 5 workgroups per CU; everything else
+  // double-buffered, 128-channel tiles when Npad allows, else 64
   const bool one = a.nkb == 1;
   if (d.stem) {
     if (bn == 128)
