@@ -340,7 +340,7 @@ hipError_t conv2d_gemm(const ConvDesc& d, int batch, const void* x, const void* 
   // instead of 4 (ResNet-50 batch 256: 4.87 -> 4.81 ms; at K = 128 / 256 / 512 the same change
   // costs 0.6 / 1.6 / 2.6 %, profiles/r4_resnet50_layers.txt)
   // (the single-stage form for the K = 128 1x1 convs, with 64- or 128-channel tiles, measured
-  // 0.4 / 2.2 % slower in round 4)
+  // 0.4 / 2.2 % slower in round 4; for the 64-channel K = 256 ones, within noise)
   const int bn = (d.Npad % 128 == 0 && !(d.K == 64 && d.KH == 1 && !d.stem)) ? 128 : 64;
   constexpr int BM = 128;
   const int m_tiles = (a.M + BM - 1) / BM;
