@@ -169,9 +169,11 @@ def parse_args(argv=None):
     ap.add_argument("--latency-warmup-s", type=float, default=1.0)
     ap.add_argument("--fetch-min-bytes", type=int, default=1,
                     help="consumer fetch.min.bytes (Kafka default 1)")
-    ap.add_argument("--recv-lowat-kb", type=int, default=0,
+    ap.add_argument("--recv-lowat-kb", type=int, default=-1,
                     help="consumer receive low-water mark per receive call (SO_RCVLOWAT): one "
-                         "wake-up per this many KB of a fetch response; 0 = per segment")
+                         "wake-up per this many KB of a fetch response; 0 = per segment, -1 = "
+                         "the bounce window with the bounce receive (profiles/"
+                         "r4_ab_recv_lowat.jsonl)")
     ap.add_argument("--fetch-max-wait-ms", type=int, default=20,
                     help="consumer fetch.max.wait.ms (long-poll bound when no data is there)")
     ap.add_argument("--latency-sweep", default="",

@@ -73,8 +73,9 @@ struct EngineConfig {
   // the body lands in the chunk whole and is packed behind it (PackTap)
   bool text_pack_bounce = true;
   int text_pack_window_kb = 256;   // the bounce receive window per source (L2 resident)
-  // consumers' receive low-water mark (kafka::ClientConfig::recv_lowat), bytes; 0 = off
-  int recv_lowat = 0;
+  // consumers' receive low-water mark (kafka::ClientConfig::recv_lowat), bytes; 0 = off,
+  // < 0 = auto (the bounce window when the bounce receive is on, else off)
+  int recv_lowat = -1;
   int commit_interval_ms = 2000;   // storm-kafka's ZK commit period
   // consumer-group membership (elastic DP, kafka::GroupMember): the input partitions are shared
   // by every engine of group_id; a member that dies or leaves has its partitions moved to the

@@ -50,8 +50,9 @@ class GaleConfig:
     commit_interval_ms: int = 2000
     fetch_min_bytes: int = 1           # Kafka fetch.min.bytes of the consumers (long-poll size)
     fetch_max_wait_ms: int = 20        # Kafka fetch.max.wait.ms
-    recv_lowat_kb: int = 0             # consumers wake per this many KB of a large fetch
-                                       # response (SO_RCVLOWAT per receive call); 0 = per segment
+    recv_lowat_kb: int = -1            # consumers wake per this many KB of a large fetch
+                                       # response (SO_RCVLOWAT per receive call); 0 = per segment,
+                                       # -1 = the bounce window with the bounce receive, else 0
     fetch_max_kb: int = 16384          # Kafka fetch.max.bytes (per fetch response)
     partition_max_kb: int = 8192       # Kafka max.partition.fetch.bytes
     pinned_fetch_mb: int = 4096        # pinned fetch-buffer budget per GPU (x2 with text_pack);
@@ -196,7 +197,7 @@ class GaleConfig:
             source_parallelism=self.source_parallelism, start_offset=self.start_offset,
             commit_interval_ms=self.commit_interval_ms, sink_parallelism=self.sink_parallelism,
             fetch_min_bytes=self.fetch_min_bytes, fetch_max_wait_ms=self.fetch_max_wait_ms,
-            recv_lowat=self.recv_lowat_kb << 10,
+            recv_lowat=self.recv_lowat_kb << 10 if self.recv_lowat_kb >= 0 else -1,
             fetch_max_bytes=self.fetch_max_kb << 10,
             partition_max_bytes=self.partition_max_kb << 10,
             pinned_fetch_bytes=self.pinned_fetch_mb << 20,
