@@ -7,6 +7,7 @@
 #           kernel trace of the default bench, forward-alone ResNet-50 / ResNet-20
 #   PART=c  only the kernel trace and the forward-alone runs
 #   PART=b2 config 4 x3, then PART=c
+#   PART=b5 config 5 only
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 out=gpurun_out/final
@@ -52,6 +53,11 @@ elif [ "$PART" = b ]; then
   fi
   tail -2 $out/gpus2_refused.log
   one rehearsal_world2 300 --gpus 2 --shared-gpu-rehearsal --steps 10 --warmup 3 || exit 1
+elif [ "$PART" = b5 ]; then
+  for i in 1 2 3; do  # fp8 and bf16 interleaved
+    one c5_fp8_slo2_$i 240 --steps 20 --warmup 5 --dtype fp8 --slo-p99-ms 2 || exit 1
+    one c5_bf16_slo2_$i 240 --steps 20 --warmup 5 --slo-p99-ms 2 || exit 1
+  done
 elif [ "$PART" = b2 ]; then
   for i in 1 2 3; do one c4_resnet50_$i 300 --model resnet50 --steps 10 --warmup 3 || exit 1; done
 fi
