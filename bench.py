@@ -559,7 +559,11 @@ def main(argv=None) -> int:
         if r50:
             a.partitions = 12 if big else 4
         else:
-            a.partitions = 2 * a.replicas_per_gpu if big else a.replicas_per_gpu
+            # 10 source threads: with the bounce receive each one packs at ~7 GB/s of text, and
+            # 10 of them sustain the rate with less contention than 12 (1.99 vs 1.81 M img/s,
+            # 3 interleaved pairs; 8 starve the pipeline at p99, 16 lose 12 %,
+            # profiles/r4_ab_partitions.jsonl)
+            a.partitions = 10 if big else a.replicas_per_gpu
     if a.decode_threads <= 0:
         # 6 GPU-ingest workers keep more H2D copies in flight on the host link than 4 (higher
         # throughput in 5 of 6 interleaved pairs on two boxes, p50 unchanged; see

@@ -5,8 +5,8 @@ set -o pipefail
 d=gpurun_out/parts
 mkdir -p $d
 : > $d/runs.jsonl
-for r in 1 2; do
-for us in 12 16 8; do
+for r in ${REPS:-1 2}; do
+for us in ${VALS:-12 16 8}; do
   timeout -k 10 240 python bench.py --steps 20 --warmup 5 --partitions $us > $d/one.jsonl 2> $d/err.log || { tail -5 $d/err.log; exit 1; }
   python - $us <<'PY'
 import json, sys
