@@ -39,7 +39,7 @@ if [ "${PART:-a}" = a ]; then
       > $out/smoke.log 2>&1 || { tail -20 $out/smoke.log; exit 1; }
   tail -1 $out/smoke.log
   for i in 1 2 3; do one c2_bf16_$i 240 --steps 20 --warmup 5 || exit 1; done
-  for i in 1 2 3; do one c1_lenet5_$i 240 --model lenet5 --steps 20 --warmup 5 --latency-load 0.9 || exit 1; done
+  for i in 1 2 3; do one c1_lenet5_$i 240 --model lenet5 --steps 20 --warmup 5 || exit 1; done
 elif [ "$PART" = b ]; then
   for i in 1 2 3; do  # fp8 and bf16 interleaved
     one c5_fp8_slo2_$i 240 --steps 20 --warmup 5 --dtype fp8 --slo-p99-ms 2 || exit 1
@@ -53,6 +53,8 @@ elif [ "$PART" = b ]; then
   fi
   tail -2 $out/gpus2_refused.log
   one rehearsal_world2 300 --gpus 2 --shared-gpu-rehearsal --steps 10 --warmup 3 || exit 1
+elif [ "$PART" = c1 ]; then
+  for i in 1 2 3; do one c1_lenet5_$i 240 --model lenet5 --steps 20 --warmup 5 || exit 1; done
 elif [ "$PART" = b5 ]; then
   for i in 1 2 3; do  # fp8 and bf16 interleaved
     one c5_fp8_slo2_$i 240 --steps 20 --warmup 5 --dtype fp8 --slo-p99-ms 2 || exit 1
