@@ -563,8 +563,11 @@ def main(argv=None) -> int:
             # 10 of them sustain the rate with less contention than 12 (1.99 vs 1.81 M img/s,
             # 3 interleaved pairs; 8 starve the pipeline at p99, 16 lose 12 %,
             # profiles/r4_ab_partitions.jsonl); a larger CPU share per rank (an 8-GPU node
-            # without a per-job quota) keeps 12
-            a.partitions = (10 if cpus < 24 else 12) if big else a.replicas_per_gpu
+            # without a per-job quota) keeps 12, and so does LeNet-5, whose 10 KB records at
+            # 4+ M img/s pushed its latency phase into retransmissions with 10 (p99 6-112 ms,
+            # profiles/r4_ab_lenet_partitions.jsonl)
+            a.partitions = (10 if cpus < 24 and a.model != "lenet5" else 12) if big \
+                else a.replicas_per_gpu
     if a.decode_threads <= 0:
         # 6 GPU-ingest workers keep more H2D copies in flight on the host link than 4 (higher
         # throughput in 5 of 6 interleaved pairs on two boxes, p50 unchanged; see
