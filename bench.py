@@ -542,7 +542,7 @@ def main(argv=None) -> int:
         # rate by a few percent rather than 10-20 % (131072-image steps: spread 9-20 %,
         # profiles/archive/r3_final_check_session2.jsonl). LeNet-5 runs at ~4 M img/s: its
         # 262144-image steps were 65 ms, shorter than one 100 ms CFS period, and at the cgroup
-        # quota they spread by ~100 % (profiles/r4_final_config1_box1.jsonl notes): 4x longer steps
+        # quota they spread by ~100 % (round 4, 3 runs on one box): 4x longer steps
         a.step_images = 4096 if r50 else (1048576 if a.model == "lenet5" else 262144)
     if a.distinct <= 0:
         a.distinct = 256 if r50 else 65536
