@@ -559,14 +559,14 @@ def main(argv=None) -> int:
         if r50:
             a.partitions = 12 if big else 4
         else:
-            # 10 source threads: with the bounce receive each one packs at ~7 GB/s of text, and
-            # 10 of them sustain the rate with less contention than 12 (1.99 vs 1.81 M img/s,
-            # 3 interleaved pairs; 8 starve the pipeline at p99, 16 lose 12 %,
-            # profiles/r4_ab_partitions.jsonl); a larger CPU share per rank (an 8-GPU node
-            # without a per-job quota) keeps 12, and so does LeNet-5, whose 10 KB records at
-            # 4+ M img/s pushed its latency phase into retransmissions with 10 (p99 6-112 ms,
-            # profiles/r4_ab_lenet_partitions.jsonl)
-            a.partitions = (10 if cpus < 24 and a.model != "lenet5" else 12) if big \
+            # 11 source threads: with the bounce receive each one packs at ~7 GB/s of text, and
+            # fewer threads than 12 contend less at the 16-CPU quota (10: 1.99 vs 1.81 M img/s
+            # over 3 interleaved pairs; 9 / 10 / 11: 2.15 / 2.08 / 1.99 M). Below 11 the latency
+            # phase, at 0.8 x the higher rate, runs into loopback retransmissions (p99 8-37 ms
+            # in some runs against 0.9-1.0 ms with 11; profiles/r4_ab_partitions.jsonl). A larger
+            # CPU share per rank (an 8-GPU node without a per-job quota) keeps 12, and so does
+            # LeNet-5 (p99 6-112 ms with 10, profiles/r4_ab_lenet_partitions.jsonl)
+            a.partitions = (11 if cpus < 24 and a.model != "lenet5" else 12) if big \
                 else a.replicas_per_gpu
     if a.decode_threads <= 0:
         # 6 GPU-ingest workers keep more H2D copies in flight on the host link than 4 (higher
