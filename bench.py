@@ -127,11 +127,20 @@ def parse_args(argv=None):
                     help="pin the host pipeline's threads to the GPU's NUMA node")
     ap.add_argument("--cpus-per-rank", type=int, default=0,
                     help="with --numa-pin: only this rank's slice of the node's CPUs (0 = the "
-                         "whole NUMA node; -1 = as many CPUs as the rank's cgroup CPU quota). "
-                         "Measured on a 16-CPU-quota box: the quota-sized slice (CPUs 0-15) ran "
-                         "at 0.69-0.81 M img/s against 1.49 M on the whole node, with the "
-                         "consumer's loopback receive costing 2.3x the cores "
-                         "(profiles/archive/r3_pinning_ab.txt); the default stays the whole node")
+                         "whole NUMA node at N = 1, the rank's --rank-slices share at N > 1; "
+                         "-1 = as many CPUs as the rank's cgroup CPU quota). Round-4 code on a "
+                         "16-CPU-quota box, 3 interleaved runs each: whole node 2.08 M img/s, "
+                         "16 physical cores 1.83 M (88 %%), 16 cores + SMT siblings 1.78 M "
+                         "(85 %%; profiles/r5_slices_ab.jsonl)")
+    ap.add_argument("--rank-slices", action=argparse.BooleanOptionalAction, default=True,
+                    help="N > 1 with --cpus-per-rank 0: each rank gets a disjoint slice of its "
+                         "GPU's NUMA node (the node's CPUs split evenly among the ranks on it, "
+                         "whole cores with their SMT siblings: 16 + 16 per rank with 4 GPUs per "
+                         "64-core socket) instead of every rank floating over the whole node")
+    ap.add_argument("--slice-smt", action="store_true",
+                    help="with --cpus-per-rank N: the slice is N/2 whole physical cores with "
+                         "their SMT siblings (what each of 4 ranks owns on a 64-core socket), "
+                         "not the N lowest CPU ids")
     ap.add_argument("--gpu-wait-poll-us", type=int, default=20,
                     help="replica workers sleep-poll batch completion every N us (0 = spin)")
     ap.add_argument("--encode-threads", type=int, default=0,
@@ -191,6 +200,9 @@ def parse_args(argv=None):
                          "cgroup throttling, RSS, queue depth, lag) to this file (rank 0)")
     ap.add_argument("--timeline-ms", type=int, default=100)
     ap.add_argument("--timeout", type=float, default=600.0)
+    ap.add_argument("--print-config", action="store_true",
+                    help="print the per-rank configuration (pipeline sizing, CPU slices) this "
+                         "command would run, then exit without running it")
     return ap.parse_args(argv)
 
 
@@ -480,6 +492,21 @@ def pipeline_path(a, st) -> str:
     return "->".join(hops)
 
 
+def _cpulist(cpus) -> str:
+    """Compact CPU list text: {0,1,2,5} -> "0-2,5"."""
+    out, run = [], []
+    for c in sorted(cpus):
+        if run and c == run[-1] + 1:
+            run.append(c)
+            continue
+        if run:
+            out.append(f"{run[0]}-{run[-1]}" if len(run) > 1 else str(run[0]))
+        run = [c]
+    if run:
+        out.append(f"{run[0]}-{run[-1]}" if len(run) > 1 else str(run[0]))
+    return ",".join(out)
+
+
 def _free_port() -> int:
     import socket
 
@@ -519,22 +546,8 @@ def launch_ranks(a, argv) -> int:
         return p.wait()
 
 
-def main(argv=None) -> int:
-    argv = list(sys.argv[1:] if argv is None else argv)
-    a = parse_args(argv)
-    if a.gpus > 1 and not a.single_process and "WORLD_SIZE" not in os.environ:
-        return launch_ranks(a, argv)
-    from gale.utils import host_cpus_per_rank, thread_cpu_seconds
-
-    # Host pipeline sizing from the rank's CPU share. Throughput is bound by per-connection
-    # copy bandwidth and GPU-ingest round trips, not by the total core count: with >= 16 cores
-    # per GPU, 12 input partitions (TCP connections), 6 replica streams and 4 ingest workers
-    # saturate the share (1.47 M img/s vs 0.97 M with 4/4/2 on one MI355X box,
-    # profiles/archive/r2_host_pipeline_shape_ab.txt); smaller shares keep ~4 cores per replica.
-    # ResNet-50 records are 1.7 MB of JSON each: the GPU, not the host, sets the pace unless the
-    # batches are full, so fewer replicas wait longer for full 256-image batches while 12
-    # partitions keep the fetches parallel (29.0 k img/s vs 23.8 k with the CIFAR sizing,
-    # profiles/archive/r2_configs_1_4_e2e.txt)
+def size_pipeline(a, cpus: float) -> None:
+    """Fill the per-GPU host pipeline sizing left at 0 / -1 from the rank's CPU share."""
     r50 = a.model == "resnet50"
     if a.step_images <= 0:
         # 262144-image steps: ~0.18 s each at 1.5 M img/s (20 steps ~3.6 s), long enough that a
@@ -548,7 +561,6 @@ def main(argv=None) -> int:
         a.distinct = 256 if r50 else 65536
     if a.max_wait_us < 0:
         a.max_wait_us = 20000 if r50 else 2000
-    cpus = host_cpus_per_rank()
     big = cpus >= 16
     if a.replicas_per_gpu <= 0:
         if r50:
@@ -573,6 +585,56 @@ def main(argv=None) -> int:
         # throughput in 5 of 6 interleaved pairs on two boxes, p50 unchanged; see
         # profiles/archive/r3_decode_threads_ab.txt)
         a.decode_threads = 6 if big else 2
+
+
+def print_config(a) -> int:
+    """--print-config: the per-rank configuration this command would run at --gpus N (sizing
+    from the rank's CPU share, the per-rank CPU slices), without running it."""
+    from gale.utils import gpu_numa_node, host_cpus_per_rank, node_cpus, plan_rank_slices
+
+    os.environ.setdefault("LOCAL_WORLD_SIZE", str(1 if a.single_process else a.gpus))
+    cpus = host_cpus_per_rank()
+    size_pipeline(a, cpus)
+    slices = None
+    if a.gpus > 1 and a.rank_slices and a.cpus_per_rank == 0 and not a.single_process:
+        import torch
+
+        ndev = torch.cuda.device_count()
+        if ndev >= a.gpus:
+            nodes = [gpu_numa_node(r) for r in range(a.gpus)]
+            slices = [_cpulist(x) for x in
+                      plan_rank_slices(nodes, {n: node_cpus(n) for n in set(nodes)})]
+    print(json.dumps({"n_gpus": a.gpus, "model": a.model, "dtype": a.dtype,
+                      "processes": 1 if a.single_process else a.gpus,
+                      "host_cpus_per_rank": round(cpus, 2),
+                      "replicas_per_gpu": a.replicas_per_gpu,
+                      "partitions_per_gpu": a.partitions, "decode_threads": a.decode_threads,
+                      "max_batch": a.batch, "max_wait_us": a.max_wait_us,
+                      "step_images_per_gpu": a.step_images, "steps": a.steps,
+                      "warmup": a.warmup, "rank_cpu_slices": slices}), flush=True)
+    return 0
+
+
+def main(argv=None) -> int:
+    argv = list(sys.argv[1:] if argv is None else argv)
+    a = parse_args(argv)
+    if a.print_config:
+        return print_config(a)
+    if a.gpus > 1 and not a.single_process and "WORLD_SIZE" not in os.environ:
+        return launch_ranks(a, argv)
+    from gale.utils import (cpu_time_split, host_cpus_per_rank, thread_cpu_seconds,
+                            thread_ctx_switches)
+
+    # Host pipeline sizing from the rank's CPU share. Throughput is bound by per-connection
+    # copy bandwidth and GPU-ingest round trips, not by the total core count: with >= 16 cores
+    # per GPU, 12 input partitions (TCP connections), 6 replica streams and 4 ingest workers
+    # saturate the share (1.47 M img/s vs 0.97 M with 4/4/2 on one MI355X box,
+    # profiles/archive/r2_host_pipeline_shape_ab.txt); smaller shares keep ~4 cores per replica.
+    # ResNet-50 records are 1.7 MB of JSON each: the GPU, not the host, sets the pace unless the
+    # batches are full, so fewer replicas wait longer for full 256-image batches while 12
+    # partitions keep the fetches parallel (29.0 k img/s vs 23.8 k with the CIFAR sizing,
+    # profiles/archive/r2_configs_1_4_e2e.txt)
+    size_pipeline(a, host_cpus_per_rank())
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -591,19 +653,30 @@ def main(argv=None) -> int:
     if use_gpu and local_gpus > torch.cuda.device_count():
         raise SystemExit(f"bench.py: {local_gpus} GPUs requested, "
                          f"{torch.cuda.device_count()} visible")
+    rank_index = local_rank  # (the rank's index on this node, also in the rehearsal)
     if use_gpu and a.shared_gpu_rehearsal:
         local_rank %= torch.cuda.device_count()
     pinned_cpus = set()
     if use_gpu:
         torch.cuda.set_device(local_rank)
         if a.numa_pin and local_gpus == 1:
-            from gale.utils import cgroup_cpu_quota, pin_to_gpu_numa
+            from gale.utils import (cgroup_cpu_quota, gpu_numa_node, node_cpus, pin_cpus,
+                                    pin_to_gpu_numa, plan_rank_slices)
 
+            local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
             if a.cpus_per_rank < 0:
                 q = cgroup_cpu_quota()
-                a.cpus_per_rank = int(q // max(1, int(os.environ.get("LOCAL_WORLD_SIZE", "1")))) \
-                    if q else 0
-            pinned_cpus = pin_to_gpu_numa(local_rank, a.cpus_per_rank)
+                a.cpus_per_rank = int(q // max(1, local_world)) if q else 0
+            if a.cpus_per_rank == 0 and local_world > 1 and a.rank_slices:
+                # disjoint per-rank slices of each GPU's NUMA node (profiles/r5_slices_ab.jsonl,
+                # profiles/r5_host_budget.txt); the rehearsal's ranks share GPU 0's node
+                ndev = torch.cuda.device_count()
+                nodes = [gpu_numa_node(r % ndev if a.shared_gpu_rehearsal else r)
+                         for r in range(local_world)]
+                plan = plan_rank_slices(nodes, {n: node_cpus(n) for n in set(nodes)})
+                pinned_cpus = pin_cpus(plan[rank_index])
+            else:
+                pinned_cpus = pin_to_gpu_numa(local_rank, a.cpus_per_rank, smt=a.slice_smt)
     if world > 1:
         from gale.parallel.group import init_rank_group
 
@@ -703,6 +776,7 @@ def main(argv=None) -> int:
         torch.cuda.synchronize()
     eng.reset_stats()
     cpu0 = thread_cpu_seconds()
+    ctx0, split0 = thread_ctx_switches(), cpu_time_split(pinned_cpus)
     cgt0 = _cgroup_cpu_stat()
     c0 = eng.completed
     t0 = time.perf_counter()
@@ -725,6 +799,7 @@ def main(argv=None) -> int:
         torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     cpu1 = thread_cpu_seconds()
+    ctx1, split1 = thread_ctx_switches(), cpu_time_split(pinned_cpus)
     cgt1 = _cgroup_cpu_stat()
     # cgroup CPU accounting of the timed window: at the CPU quota the CFS bandwidth controller
     # stops the whole group for the rest of each 100 ms period, which alternates fast and slow
@@ -752,8 +827,18 @@ def main(argv=None) -> int:
         sm = tt.clone()
         dist.all_reduce(sm, op=dist.ReduceOp.SUM)
         elapsed_max, total_images = float(mx[0]), float(sm[1])
+        # every rank's own view, for the JSON line: its partitions, output partition, window,
+        # images, host slice and busy cores (imbalance between ranks shows up here)
+        mine = {"rank": rank, "partitions": my_parts, "output_partition": cfg.output_partition,
+                "timed_s": round(elapsed, 4), "images": int(images),
+                "img_s": round(images / max(elapsed, 1e-9), 1),
+                "cpus": _cpulist(pinned_cpus),
+                "cores": round(sum(cpu1[k] - cpu0[k] for k in cpu1) / max(elapsed, 1e-9), 2)}
+        per_rank = [None] * world
+        dist.all_gather_object(per_rank, mine)
     else:
         elapsed_max, total_images = elapsed, float(images)
+        per_rank = None
     value = total_images / elapsed_max
     n_gpus = world * local_gpus
     lat_us, lat_achieved, lat_unmatched, lat_host = None, 0.0, 0, {}
@@ -849,6 +934,8 @@ def main(argv=None) -> int:
                           "latency: a second phase at a fixed offered load"),
             "timed_s": round(elapsed_max, 3),
         }
+        if per_rank:
+            out["ranks"] = per_rank
         if lat_us is not None and len(lat_us):
             out.update({
                 "p50_latency_ms": round(float(np.percentile(lat_us, 50)) / 1e3, 3),
@@ -895,6 +982,16 @@ def main(argv=None) -> int:
             "cpu_cores_by_stage_rank0": cores,
             "encode_s": round(t_enc, 1),
             "cpus_pinned_rank0": len(pinned_cpus),
+            "cpu_slice_rank0": _cpulist(pinned_cpus),
+            # per stage, thousands of context switches per second: [voluntary, involuntary]
+            "ctx_k_per_s_rank0": {k: [round((ctx1[k][0] - ctx0[k][0]) / elapsed / 1e3, 1),
+                                      round((ctx1[k][1] - ctx0[k][1]) / elapsed / 1e3, 1)]
+                                  for k in ctx1 if k in ctx0},
+            # the pinned CPUs' time by /proc/stat category (whole machine when unpinned), in
+            # cores: softirq is the loopback receive processing, charged to no thread
+            "slice_cores_rank0": {k: round((split1[k] - split0.get(k, 0.0)) / elapsed, 2)
+                                  for k in ("user", "system", "softirq", "irq", "idle")
+                                  if k in split1},
             "steals": int(st.get("steals", 0)),
             "warmup_records": warm_done,
         })

@@ -207,12 +207,17 @@ struct OffsetWindow {
       sparse.erase(off);
     } else {
       uint8_t& f = st[(size_t)(off - base)];
-      if (!f) return;
-      f = 0;
-      --npending;
-      while (!st.empty() && st.front() == 0) {
-        st.pop_front();
-        ++base;
+      if (!f) {
+        // not pending in the window: it may be a sparse offset that the window grew over
+        // after it was set aside (add() past kMaxSpan while base was stalled, then base moved)
+        sparse.erase(off);
+      } else {
+        f = 0;
+        --npending;
+        while (!st.empty() && st.front() == 0) {
+          st.pop_front();
+          ++base;
+        }
       }
     }
     if (npending == 0 && !sparse.empty()) {  // re-base the window onto the sparse offsets

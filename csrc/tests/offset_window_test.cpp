@@ -9,7 +9,27 @@
 
 #include "../runtime/engine.h"
 
+// A sparse offset that the window later grows over (base stalled, a record set aside past
+// kMaxSpan, base moves on, a new add() resizes the window across it) must still complete.
+static int sparse_overlap_case() {
+  const int64_t S = gale::OffsetWindow::kMaxSpan;
+  gale::OffsetWindow w;
+  for (int64_t o = 0; o <= 10; ++o) w.add(o);  // offset 0: the stalled record at base
+  w.add(S + 5);     // >= kMaxSpan past base: set aside in the sparse set
+  for (int64_t o = 0; o < 10; ++o) w.done(o);  // base moves to 10 (still pending)
+  w.add(S + 8);     // inside the window now: st grows over S + 5
+  w.done(S + 5);    // must leave the sparse set although its window slot is 0
+  w.done(10);
+  w.done(S + 8);
+  if (!w.empty()) {
+    fprintf(stderr, "sparse overlap: window not empty (first %lld)\n", (long long)w.first());
+    return 1;
+  }
+  return 0;
+}
+
 int main() {
+  if (sparse_overlap_case()) return 1;
   std::mt19937_64 rng(42);
   for (int round = 0; round < 200; ++round) {
     gale::OffsetWindow w;

@@ -16,9 +16,11 @@
 (roctx ranges on every host pipeline stage, ``--trace``); ``GALE_ROCTX=1`` turns the ranges on
 for an externally launched profiler.
 
-Multi-GPU, one process per GPU: ``python -m torch.distributed.run --nproc-per-node 8
---master-addr 127.0.0.1 -m gale NAME IN OUT ...`` — rank r consumes the input partitions
-p % WORLD_SIZE == r and weights are RCCL-broadcast from rank 0.
+Multi-GPU, one process per GPU: ``python -m gale NAME IN OUT --ranks 8`` starts and supervises
+one rank process per GPU and respawns a rank that dies (Storm's supervisors, gale/supervisor.py);
+``python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 -m gale NAME IN OUT
+...`` runs the same ranks without respawning. Rank r consumes the input partitions
+p % WORLD_SIZE == r (or its consumer-group share) and weights are RCCL-broadcast from rank 0.
 """
 
 from __future__ import annotations
@@ -92,9 +94,18 @@ def profile_command(cfg: GaleConfig, argv: List[str]) -> List[str]:
 
 
 def cmd_run(argv: List[str]) -> int:
-    from gale.topology import AlreadyAliveError, InvalidTopologyError, run_topology
+    from gale.topology import (AlreadyAliveError, InvalidTopologyError, RankFailedError,
+                               run_topology)
 
     cfg = parse_topology_args(argv)
+    if cfg.ranks > 0 and not os.environ.get("GALE_SUPERVISED"):
+        # the supervisor: one child process per rank, respawned when it dies (never touches
+        # a GPU itself; gale/supervisor.py)
+        from gale.supervisor import run_supervised
+
+        logging.basicConfig(level=getattr(logging, cfg.log_level.upper(), logging.INFO),
+                            format="%(asctime)s %(name)s %(levelname)s %(message)s")
+        return run_supervised(cfg, argv)
     if cfg.profile:
         import subprocess
 
@@ -114,6 +125,9 @@ def cmd_run(argv: List[str]) -> int:
     except InvalidTopologyError as e:
         logging.getLogger("gale").error("invalid topology: %s", e)
         return 2
+    except RankFailedError as e:  # replaced by the rank supervisor (--ranks)
+        logging.getLogger("gale").error("%s", e)
+        return 3
     print(json.dumps({k: v for k, v in final.items() if k != "final"}), file=sys.stderr)
     return 0
 

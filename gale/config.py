@@ -141,6 +141,14 @@ class GaleConfig:
     # recovered and rejoins after restart_backoff_ms, up to max_restarts times (0 = stays dead)
     max_restarts: int = 3
     restart_backoff_ms: int = 500
+    # rank supervisor (gale/supervisor.py; Storm supervisors respawn dead worker JVMs,
+    # MainTopology.java:25,65-66): > 0 = this command starts and supervises that many rank
+    # processes (one per GPU), respawning a dead one after rank_restart_backoff_ms, at most
+    # rank_max_restarts times per rank (-1 = always)
+    ranks: int = 0
+    rank_max_restarts: int = 10
+    rank_restart_backoff_ms: int = 1000
+    rank_start_timeout_s: float = 300.0
     fault: str = ""                    # replica_crash@N,parse_error@P,producer_fail@P
     trace: bool = False                # roctx ranges around pipeline stages (rocprofv3)
     profile: str = ""                  # run under rocprofv3 --kernel-trace --marker-trace --stats
@@ -176,6 +184,8 @@ class GaleConfig:
             raise ValueError("slo_p99_ms must be >= 0")
         if self.replicas < 0 or self.gpus < 0:
             raise ValueError("replicas/gpus must be >= 0")
+        if self.ranks < 0 or self.rank_restart_backoff_ms < 0:
+            raise ValueError("--ranks / --rank-restart-backoff-ms must be >= 0")
         if self.locality_split < 1:
             raise ValueError("locality_split must be >= 1")
         if not self.topology_name:

@@ -8,6 +8,9 @@ one device) and the CPU stub engine.
 
 from __future__ import annotations
 
+import os
+from datetime import timedelta
+
 import torch
 import torch.distributed as dist
 
@@ -19,10 +22,16 @@ def init_rank_group(local_rank: int, use_gpu: bool, shared_gpu: bool = False) ->
     collective."""
     if dist.is_initialized():
         return dist.get_backend()
+    # fault injection for the failure-path tests: this rank's group init fails
+    if os.environ.get("GALE_FAULT_INIT_RANK", "") == os.environ.get("RANK", "0"):
+        raise RuntimeError("injected process-group init failure (GALE_FAULT_INIT_RANK)")
+    # bounded: a peer that never arrives fails the rendezvous instead of hanging the job
+    timeout = timedelta(seconds=float(os.environ.get("GALE_PG_TIMEOUT_S", "300")))
     nccl = use_gpu and not shared_gpu
     if nccl:
         torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank),
+                                timeout=timeout)
     else:
-        dist.init_process_group("gloo")
+        dist.init_process_group("gloo", timeout=timeout)
     return "nccl" if nccl else "gloo"

@@ -48,6 +48,11 @@ class InvalidTopologyError(TopologyError):
     pass
 
 
+class RankFailedError(TopologyError):
+    """Every replica of this rank is dead (e.g. a hung device the watchdog gave up on): the
+    process exits non-zero so the rank supervisor (--ranks) replaces it."""
+
+
 def _alive(pid: int) -> bool:
     try:
         os.kill(pid, 0)
@@ -169,16 +174,28 @@ def run_topology(cfg: GaleConfig, stop_event: Optional[threading.Event] = None,
         if cfg.embedded_broker and rank == 0:
             broker = start_embedded_broker(cfg)
         devices = None
+        incarnation = int(os.environ.get("GALE_RANK_INCARNATION", "0"))
+        supervised = bool(os.environ.get("GALE_SUPERVISED"))
         if world > 1 and not cfg.stub:
-            from gale.parallel.group import init_rank_group
-
-            init_rank_group(local_rank, use_gpu=True)
             devices = [local_rank]
+            if incarnation == 0:
+                from gale.parallel.group import init_rank_group
+
+                init_rank_group(local_rank, use_gpu=True)
+            # a respawned rank (incarnation > 0) has no group to join: it materialises the
+            # weights itself from the same seed / --weights file (Storm's prepare() reload)
         if world > 1 and not cfg.partitions and not cfg.group_membership:
             cfg.partitions = rank_partitions(cfg, rank, world)
         if cfg.numa_pin and not cfg.stub:
             _pin_single_gpu(cfg, devices)
         engine = Engine(cfg, devices=devices)
+        if supervised and world > 1:
+            # the group existed for the one-time weight broadcast: a supervised rank may die and
+            # be respawned later, so no rank keeps a communicator with a peer that can vanish
+            import torch.distributed as dist
+
+            if dist.is_initialized():
+                dist.destroy_process_group()
         if install_signals and threading.current_thread() is threading.main_thread():
             for sig in (signal.SIGTERM, signal.SIGINT):
                 old_handlers[sig] = signal.signal(sig, lambda *_: stop_event.set())
@@ -186,23 +203,33 @@ def run_topology(cfg: GaleConfig, stop_event: Optional[threading.Event] = None,
         log.info("topology %s running: %s -> %s on %s (model %s, %d replica(s))", name,
                  cfg.input_topic, cfg.output_topic, cfg.bootstrap, cfg.model,
                  len(engine.replica_stats()))
+        ready = os.environ.get("GALE_READY_FILE")
+        if ready:  # the supervisor's start-up barrier
+            with open(ready + ".tmp", "w") as fh:
+                json.dump({"rank": rank, "pid": os.getpid(), "incarnation": incarnation}, fh)
+            os.replace(ready + ".tmp", ready)
+        labels = {"topology": name, "rank": rank}
+        if supervised:
+            labels["rank_restarts"] = incarnation
         reporter = Reporter(engine.stats, cfg.metrics_interval, path=cfg.metrics_file,
-                            labels={"topology": name, "rank": rank},
+                            labels=labels,
                             extra_fn=lambda: {"partitions": sorted(
                                 o["partition"] for o in engine.partition_offsets())}).start()
         http = None
         if cfg.metrics_port >= 0:
             port = cfg.metrics_port + local_rank if cfg.metrics_port > 0 else 0
-            http = MetricsServer(engine, port, labels={"topology": name, "rank": rank}).start()
+            http = MetricsServer(engine, port, labels=labels).start()
             log.info("metrics: http://127.0.0.1:%d/metrics (Prometheus), /stats (JSON)",
                      http.port)
-        stop_event.wait(cfg.duration if cfg.duration > 0 else None)
+        failed = _serve_until_done(engine, cfg, stop_event)
         if http is not None:
             http.stop()
         reporter.stop(final=False, close=False)
         engine.stop()
         final = reporter.report()
         reporter.close()
+        if failed:
+            raise RankFailedError(f"rank {rank}: every replica is dead ({failed})")
         return dict(engine.stats(), final=final)
     finally:
         if engine is not None and engine.running:
@@ -212,6 +239,27 @@ def run_topology(cfg: GaleConfig, stop_event: Optional[threading.Event] = None,
         for sig, h in old_handlers.items():
             signal.signal(sig, h)
         registry.unregister(name)
+
+
+def _serve_until_done(engine, cfg: GaleConfig, stop_event: threading.Event) -> str:
+    """Serve until the duration elapses or ``stop_event`` is set; returns "" then, or why the
+    rank can no longer serve: no replica alive for longer than a replica restart could take
+    (the watchdog killed them on a hung device, or they failed past --max-restarts)."""
+    deadline = time.monotonic() + cfg.duration if cfg.duration > 0 else None
+    grace = max(2.0, 2 * cfg.restart_backoff_ms / 1e3 + 1.0)
+    dead_since = None
+    while True:
+        wait = 0.25 if deadline is None else min(0.25, max(0.0, deadline - time.monotonic()))
+        if stop_event.wait(wait) or (deadline is not None and time.monotonic() >= deadline):
+            return ""
+        alive = engine.stats().get("replicas_alive", 1)
+        if alive > 0:
+            dead_since = None
+            continue
+        now = time.monotonic()
+        dead_since = dead_since or now
+        if now - dead_since >= grace:
+            return f"replicas_alive 0 for {now - dead_since:.1f} s"
 
 
 def rank_partitions(cfg: GaleConfig, rank: int, world: int) -> str:

@@ -56,15 +56,106 @@ def gpu_numa_node(device: int) -> int:
         return -1
 
 
-def pin_to_gpu_numa(device: int, cpus_per_rank: int = 0) -> set:
+def core_groups(cpus, sysfs: str = "/sys/devices/system/cpu") -> list:
+    """The CPUs of ``cpus`` grouped by physical core (SMT siblings together), cores ordered by
+    their lowest CPU id: [[0, 128], [1, 129], ...] on a 2-way SMT EPYC. A CPU whose topology
+    cannot be read is its own core."""
+    cpus = set(cpus)
+    seen, out = set(), []
+    for c in sorted(cpus):
+        if c in seen:
+            continue
+        try:
+            with open(f"{sysfs}/cpu{c}/topology/thread_siblings_list") as f:
+                sib = sorted(_parse_cpulist(f.read()) & cpus)
+        except (OSError, ValueError):
+            sib = [c]
+        if c not in sib:
+            sib = [c] + sib
+        seen.update(sib)
+        out.append(sib)
+    return out
+
+
+def numa_slice(cpus, slot: int, cpus_per_rank: int, smt: bool = False,
+               sysfs: str = "/sys/devices/system/cpu") -> set:
+    """Slot ``slot``'s disjoint share of a NUMA node's CPUs.
+
+    * ``smt=False``: the ``cpus_per_rank`` lowest CPU ids after the earlier slots' (physical
+      cores before their SMT siblings on Linux's numbering);
+    * ``smt=True``: whole physical cores with their SMT siblings, ``cpus_per_rank`` hardware
+      threads per slot (16 cores + 16 siblings for 32): what each of 4 ranks on a 64-core,
+      128-thread socket owns, and the slice a loopback sender and receiver can share a core's
+      L2 in.
+
+    Returns an empty set when the node has fewer CPUs than the slot needs."""
+    if cpus_per_rank <= 0:
+        return set(cpus)
+    if not smt:
+        ordered = sorted(cpus)
+        part = ordered[slot * cpus_per_rank:(slot + 1) * cpus_per_rank]
+        return set(part) if len(part) == cpus_per_rank else set()
+    cores = core_groups(cpus, sysfs)
+    tpc = max(1, max(len(g) for g in cores)) if cores else 1
+    ncores = max(1, cpus_per_rank // tpc)
+    part = cores[slot * ncores:(slot + 1) * ncores]
+    if len(part) < ncores:
+        return set()
+    return {c for g in part for c in g}
+
+
+def plan_rank_slices(gpu_nodes, node_cpus: dict, smt: bool = True,
+                     sysfs: str = "/sys/devices/system/cpu") -> list:
+    """Disjoint host CPU slices for the ranks of one node: ``gpu_nodes[i]`` is the NUMA node of
+    rank i's GPU, ``node_cpus`` maps a node to its CPUs. The ranks on a node split it evenly,
+    in rank order, as whole physical cores with their SMT siblings (``smt``) - on a 2-socket
+    64-core EPYC with 4 GPUs per socket, 16 cores + 16 siblings per rank, each slice inside
+    its own L3 domains. A rank whose node is unknown (-1) gets an empty set (left unpinned)."""
+    out = []
+    for i, node in enumerate(gpu_nodes):
+        cpus = node_cpus.get(node, set())
+        peers = [j for j, n in enumerate(gpu_nodes) if n == node]
+        if node < 0 or not cpus:
+            out.append(set())
+            continue
+        per = len(cpus) // len(peers)
+        if smt:
+            cores = core_groups(cpus, sysfs)
+            tpc = max(len(g) for g in cores)
+            per = (per // tpc) * tpc
+        out.append(numa_slice(cpus, peers.index(i), per, smt, sysfs) if per > 0 else set())
+    return out
+
+
+def node_cpus(node: int) -> set:
+    """CPUs of a NUMA node within this process's affinity (empty when unknown)."""
+    if node < 0:
+        return set()
+    try:
+        with open(f"/sys/devices/system/node/node{node}/cpulist") as f:
+            return _parse_cpulist(f.read()) & os.sched_getaffinity(0)
+    except OSError:
+        return set()
+
+
+def pin_cpus(cpus) -> set:
+    """Restrict this process's future threads to ``cpus`` (no-op when empty)."""
+    cpus = set(cpus)
+    if cpus:
+        os.sched_setaffinity(0, cpus)
+    return cpus
+
+
+def pin_to_gpu_numa(device: int, cpus_per_rank: int = 0, smt: bool = False) -> set:
     """Restrict this process's future threads to the CPUs of the GPU's NUMA node (within the
     current affinity). The host pipeline moves ~35 KB of JSON per image through fetch buffers
     that are DMA sources for this GPU: keeping its threads and their first-touch memory on the
     GPU's socket avoids cross-socket copies. ``cpus_per_rank`` > 0 narrows it to this GPU's
-    own slice of the node (lowest CPU ids first: physical cores before their SMT siblings;
-    GPUs of one node take disjoint slices in device order), so the threads stop migrating over
-    the whole socket. Returns the CPU set used (empty: left unpinned). Call before the engine
-    starts its threads (they inherit the creator's affinity)."""
+    own slice of the node (``numa_slice``: lowest CPU ids, or whole cores with their SMT
+    siblings with ``smt``; GPUs of one node take disjoint slices in device order), so the
+    threads stop migrating over the whole socket. Returns the CPU set used (empty: left
+    unpinned). Call before the engine starts its threads (they inherit the creator's
+    affinity)."""
     node = gpu_numa_node(device)
     if node < 0:
         return set()
@@ -75,13 +166,65 @@ def pin_to_gpu_numa(device: int, cpus_per_rank: int = 0) -> set:
         return set()
     if cpus and cpus_per_rank > 0:
         slot = sum(1 for d in range(device) if gpu_numa_node(d) == node)
-        ordered = sorted(cpus)
-        part = ordered[slot * cpus_per_rank:(slot + 1) * cpus_per_rank]
-        if len(part) == cpus_per_rank:
-            cpus = set(part)
+        part = numa_slice(cpus, slot, cpus_per_rank, smt)
+        if part:
+            cpus = part
     if cpus:
         os.sched_setaffinity(0, cpus)
     return cpus
+
+
+def thread_ctx_switches() -> dict:
+    """Voluntary / involuntary context switches of this process's live threads, summed per
+    pipeline stage: {stage: [voluntary, involuntary]} (``/proc/self/task/<tid>/status``). A
+    voluntary switch is a thread blocking (a wake-up per socket read, queue wait or poll
+    sleep); an involuntary one is preemption by another runnable thread - the cost of more
+    runnable threads than CPUs in the slice."""
+    out = {g: [0, 0] for _, g in THREAD_GROUPS}
+    out["other"] = [0, 0]
+    base = "/proc/self/task"
+    for tid in os.listdir(base):
+        try:
+            with open(f"{base}/{tid}/status") as f:
+                txt = f.read()
+        except OSError:
+            continue
+        name, vol, inv = "", 0, 0
+        for ln in txt.splitlines():
+            if ln.startswith("Name:"):
+                name = ln.split(None, 1)[1] if len(ln.split(None, 1)) > 1 else ""
+            elif ln.startswith("voluntary_ctxt_switches:"):
+                vol = int(ln.split()[1])
+            elif ln.startswith("nonvoluntary_ctxt_switches:"):
+                inv = int(ln.split()[1])
+        group = next((g for pre, g in THREAD_GROUPS if name.startswith(pre)), "other")
+        out[group][0] += vol
+        out[group][1] += inv
+    return out
+
+
+def cpu_time_split(cpus) -> dict:
+    """Seconds per /proc/stat category summed over ``cpus`` (all CPUs when empty): user, system,
+    irq, softirq, idle. Loopback TCP receive processing runs as softirq on the sending CPU (or
+    in ksoftirqd when deferred), outside any thread's utime/stime of this process."""
+    tick = os.sysconf("SC_CLK_TCK")
+    want = set(cpus) if cpus else None
+    keys = ("user", "nice", "system", "idle", "iowait", "irq", "softirq")
+    out = {k: 0.0 for k in keys}
+    try:
+        with open("/proc/stat") as f:
+            for ln in f:
+                if not ln.startswith("cpu") or ln.startswith("cpu "):
+                    continue
+                parts = ln.split()
+                c = int(parts[0][3:])
+                if want is not None and c not in want:
+                    continue
+                for k, v in zip(keys, parts[1:8]):
+                    out[k] += int(v) / tick
+    except (OSError, ValueError):
+        return {}
+    return out
 
 
 THREAD_GROUPS = (("gl-brk", "broker"), ("gl-src", "source"), ("gl-dec", "decode"),

@@ -8,6 +8,7 @@ import socket
 import subprocess
 import sys
 
+import pytest
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
@@ -142,3 +143,67 @@ def test_scaling_driver_single_process_mode():
     assert [r["n_gpus"] for r in lines[:2]] == [1, 2]
     assert lines[1]["config"]["processes"] == 1 and lines[1]["config"]["partitions"] == 4
     assert lines[-1]["mode"] == "single-process"
+
+
+def _bench_stub(n, extra=(), env_extra=None, timeout=300):
+    cmd = [sys.executable, "bench.py", "--gpus", str(n), "--stub", "--steps", "3", "--warmup",
+           "1", "--batch", "32", "--distinct", "64", "--replicas-per-gpu", "2",
+           "--step-images", "256", "--min-warmup-s", "0.2", "--stub-null", "--timeout", "120",
+           *extra]
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    return subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=timeout,
+                          env=dict(env, OMP_NUM_THREADS="1", **(env_extra or {})))
+
+
+def test_bench_plain_entry_world4_per_rank_view():
+    """The driver's ``python bench.py --gpus 4`` at world 4 (gloo stub ranks): every rank leads
+    and consumes its own input partitions (p % 4 == rank), produces to its own output partition,
+    the reported window is the slowest rank's and ``value`` the sum over ranks / that window."""
+    out = _bench_stub(4)
+    assert out.returncode == 0, out.stderr[-3000:]
+    (r,) = [json.loads(x) for x in out.stdout.splitlines() if x.startswith("{")]
+    assert r["n_gpus"] == 4 and r["config"]["processes"] == 4
+    assert r["config"]["parallelism"] == "dp4" and r["config"]["partitions"] == 8
+    ranks = r["ranks"]
+    assert [x["rank"] for x in ranks] == [0, 1, 2, 3]
+    for x in ranks:
+        assert x["partitions"] == [p for p in range(8) if p % 4 == x["rank"]]
+        assert x["output_partition"] == x["rank"]
+        assert x["images"] >= 3 * 256
+    assert r["timed_s"] == pytest.approx(max(x["timed_s"] for x in ranks), abs=2e-3)
+    total = sum(x["images"] for x in ranks)
+    assert r["value"] == pytest.approx(total / max(x["timed_s"] for x in ranks), rel=2e-3)
+
+
+def test_bench_rank_init_failure_fails_the_job_fast():
+    """A rank whose process-group init fails (injected in rank 2 of 3) makes the whole
+    ``bench.py --gpus 3`` exit non-zero promptly: no rank is left hanging in the rendezvous and
+    no JSON line is printed."""
+    import time
+
+    t0 = time.time()
+    out = _bench_stub(3, env_extra={"GALE_FAULT_INIT_RANK": "2", "GALE_PG_TIMEOUT_S": "60"},
+                      timeout=240)
+    assert out.returncode != 0
+    assert "injected process-group init failure" in out.stderr
+    assert not [x for x in out.stdout.splitlines() if x.startswith("{")]
+    assert time.time() - t0 < 120
+
+
+def test_scaling_dry_run_prints_per_n_config():
+    """tools/scaling.py --dry-run: the command and per-rank config of every N, nothing run; the
+    N = 1 sizing is pinned for every larger N (weak scaling at equal per-GPU work)."""
+    out = subprocess.run([sys.executable, "tools/scaling.py", "--gpus", "1,2,4,8", "--dry-run"],
+                         cwd=ROOT, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [json.loads(x) for x in out.stdout.splitlines() if x.startswith("{")]
+    assert [r["n_gpus"] for r in lines] == [1, 2, 4, 8]
+    one = lines[0]["config"]
+    for r in lines[1:]:
+        assert f"--gpus {r['n_gpus']}" in r["cmd"]
+        c = r["config"]
+        assert c["processes"] == r["n_gpus"]
+        for k in ("replicas_per_gpu", "partitions_per_gpu", "decode_threads",
+                  "step_images_per_gpu"):
+            assert c[k] == one[k], k

@@ -62,6 +62,9 @@ def main(argv=None) -> int:
                     choices=["per-process", "single-process", "both"],
                     help="per-process: one torch.distributed rank per GPU; single-process: one "
                          "engine driving every GPU (bench.py --single-process)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="print, per N, the command and per-rank configuration the sweep would "
+                         "run (bench.py --print-config), without running anything")
     ap.add_argument("extra", nargs=argparse.REMAINDER, help="-- extra bench.py arguments")
     a = ap.parse_args(argv)
     extra = a.extra[1:] if a.extra[:1] == ["--"] else a.extra
@@ -70,8 +73,43 @@ def main(argv=None) -> int:
     modes = ["per-process", "single-process"] if a.mode == "both" else [a.mode]
     rc = 0
     for mode in modes:
-        rc |= sweep(a, counts, extra, env, mode)
+        rc |= (dry_run if a.dry_run else sweep)(a, counts, extra, env, mode)
     return rc
+
+
+def _pin_from(cfg: dict, extra: list) -> list:
+    """The N = 1 run's per-GPU sizing as bench.py flags, pinned for every larger N."""
+    pinned = []
+    for flag, key in (("--partitions", "partitions_per_gpu"),
+                      ("--replicas-per-gpu", "replicas_per_gpu"),
+                      ("--decode-threads", "decode_threads"), ("--batch", "max_batch"),
+                      ("--step-images", "step_images_per_gpu")):
+        if cfg.get(key) and flag not in extra:
+            pinned += [flag, str(cfg[key])]
+    return pinned
+
+
+def dry_run(a, counts, extra, env, mode) -> int:
+    """--dry-run: one line per N with the exact bench.py command and its per-rank config."""
+    pinned: list = []
+    for n in counts:
+        cmd = bench_cmd(n, a.steps, a.warmup, extra + pinned, a.stub,
+                        single_process=mode == "single-process")
+        p = subprocess.run(cmd + ["--print-config"], cwd=ROOT, env=env, capture_output=True,
+                           text=True, timeout=300)
+        cfg = None
+        for line in p.stdout.splitlines():
+            if line.startswith("{"):
+                cfg = json.loads(line)
+        if p.returncode != 0 or cfg is None:
+            print(json.dumps({"n_gpus": n, "error": f"rc={p.returncode}",
+                              "tail": p.stderr[-2000:]}))
+            return 1
+        if not pinned:
+            pinned = _pin_from(cfg, extra)
+        print(json.dumps({"mode": mode, "n_gpus": n, "cmd": " ".join(cmd[1:]), "config": cfg}),
+              flush=True)
+    return 0
 
 
 def sweep(a, counts, extra, env, mode) -> int:
