@@ -661,19 +661,20 @@ void bind_host(py::module_& m) {
     return py::bytes(encode_message_set(magic, recs, base_offset, codec_from_name(c)));
   }, py::arg("magic"), py::arg("values"), py::arg("base_offset") = 0, py::arg("codec") = "none",
      py::arg("keys") = py::none(), py::arg("timestamp") = -1);
-  k.def("normalize_records", [](py::bytes data, int64_t min_offset, bool check_crc) {
+  k.def("normalize_records", [](py::bytes data, int64_t min_offset, bool check_crc, size_t limit) {
     const std::string_view s = view(data);
     NormalizeStats st;
     const std::string out = normalize_records(reinterpret_cast<const uint8_t*>(s.data()),
-                                              s.size(), min_offset, check_crc, (size_t)1 << 30,
-                                              st);
+                                              s.size(), min_offset, check_crc, limit, st);
     py::dict d;
     d["converted_batches"] = st.converted_batches;
     d["poison_batches"] = st.poison_batches;
     d["poison_records"] = st.poison_records;
+    d["poison_unknown_span"] = st.poison_unknown_span;
     d["last_error"] = st.last_error;
     return py::make_tuple(py::bytes(out), d);
-  }, py::arg("data"), py::arg("min_offset") = 0, py::arg("check_crc") = true);
+  }, py::arg("data"), py::arg("min_offset") = 0, py::arg("check_crc") = true,
+     py::arg("limit") = (size_t)1 << 30);
   k.def("encode", &py_encode);
   k.def("decode", &py_decode);
   k.def("api_version", [](int key) { return kVersion((ApiKey)key); });
@@ -972,6 +973,7 @@ void bind_host(py::module_& m) {
         d["converted_batches"] = c.converted_batches();
         d["poison_batches"] = c.poison_batches();
         d["poison_records"] = c.poison_records();
+        d["poison_unknown_span"] = c.poison_unknown_span();
         return d;
       }, "record-format conversion counters: compressed / legacy batches rewritten, "
          "undecodable batches skipped as poison records")

@@ -3,6 +3,7 @@
 // Kernels take raw device pointers (torch tensors' data_ptr()) and a hipStream_t handle
 // (torch.cuda.current_stream().cuda_stream), so they interoperate with PyTorch-ROCm tensors
 // without linking libtorch. Long-running calls release the GIL.
+#include <pybind11/numpy.h>
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
@@ -94,7 +95,39 @@ namespace gale {
 void install_crash_handler();  // runtime/crash.cpp
 }
 
+namespace {
+// Host-mapped pinned memory (hipHostMallocMapped) for tests of the zero-copy kernel paths: the
+// GPU ingest reads its plan and the packed text from, and writes its results to, such memory.
+struct MappedBuffer {
+  uint8_t* p = nullptr;
+  size_t n = 0;
+  explicit MappedBuffer(size_t bytes) : n(bytes) {
+    gale::check_hip(hipHostMalloc(reinterpret_cast<void**>(&p), bytes ? bytes : 1,
+                                  hipHostMallocMapped),
+                    "hipHostMalloc(mapped)");
+    void* dp = nullptr;
+    gale::check_hip(hipHostGetDevicePointer(&dp, p, 0), "hipHostGetDevicePointer");
+    if (dp != p) throw std::runtime_error("mapped buffer: device address differs from host");
+  }
+  ~MappedBuffer() {
+    if (p) hipHostFree(p);
+  }
+};
+}  // namespace
+
 PYBIND11_MODULE(_C, m) {
+  py::class_<MappedBuffer, std::shared_ptr<MappedBuffer>>(
+      m, "MappedBuffer", "host-mapped pinned buffer (same address on the host and the GPU)")
+      .def(py::init<size_t>())
+      .def_property_readonly("ptr", [](const MappedBuffer& b) { return (uintptr_t)b.p; })
+      .def_property_readonly("size", [](const MappedBuffer& b) { return b.n; })
+      .def("numpy", [](std::shared_ptr<MappedBuffer> b) {
+        // a uint8 view that keeps the buffer alive
+        return py::array_t<uint8_t>({(py::ssize_t)b->n}, {1}, b->p,
+                                    py::capsule(new std::shared_ptr<MappedBuffer>(b), [](void* c) {
+                                      delete static_cast<std::shared_ptr<MappedBuffer>*>(c);
+                                    }));
+      });
   m.doc() = "gale native library: gfx950 kernels, plan executor, host runtime";
   gale::install_crash_handler();
 
@@ -216,7 +249,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("ingest_crc_count",
         [](uintptr_t bytes, uintptr_t chunks, int nchunks, uintptr_t tables, uintptr_t crc_out,
            int nrec, int ngroups, uintptr_t recs, uintptr_t groups, uintptr_t counts,
-           uintptr_t gsum, uintptr_t stream) {
+           uintptr_t gsum, uintptr_t stream, uintptr_t gbad) {
           gale::check_hip(
               gale::ingest_crc_count(reinterpret_cast<const uint8_t*>(bytes),
                                      reinterpret_cast<const gale::CrcChunk*>(chunks), nchunks,
@@ -226,9 +259,14 @@ PYBIND11_MODULE(_C, m) {
                                      reinterpret_cast<const int2*>(groups),
                                      reinterpret_cast<int*>(counts),
                                      reinterpret_cast<int*>(gsum),
+                                     reinterpret_cast<int*>(gbad),
                                      reinterpret_cast<hipStream_t>(stream)),
               "ingest_crc_count");
         },
+        py::arg("bytes"), py::arg("chunks"), py::arg("nchunks"), py::arg("tables"),
+        py::arg("crc_out"), py::arg("nrec"), py::arg("ngroups"), py::arg("recs"),
+        py::arg("groups"), py::arg("counts"), py::arg("gsum"), py::arg("stream"),
+        py::arg("gbad") = 0,
         "groups: int32 (record, first tile) pairs, GROUP_TILES tiles each; counts: per record "
         "tile0 + grp0 -> [tile counts][group sums]; gsum: one int per group");
   m.attr("GROUP_TILES") = gale::kGroupTiles;

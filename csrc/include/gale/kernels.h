@@ -183,10 +183,14 @@ int json_tile_count(int64_t off, int32_t len);
 // count_pass = false: every record has_cnt (the counting kernel is not launched at all).
 // d_ntiles non-null: the kernels read the tile count from device memory (ntiles = the most the
 // launch is sized for; waves past the device count exit) - the captured step graph's form.
+// status non-null: the verdicts are raised in status[record] (device memory) instead of
+// recs[record].status, and recs / tile_rec / d_ntiles are only read - they may then be
+// host-mapped pinned memory (the step graph reads the batch's metadata where the host wrote it,
+// with no copy node).
 hipError_t json_parse_instances(int nrec, int ntiles, JsonRecord* recs, const int* tile_rec,
                                 const uint8_t* bytes, int H, int W, int C, int* tile_counts,
                                 float* out, hipStream_t stream, bool count_pass = true,
-                                const int* d_ntiles = nullptr);
+                                const int* d_ntiles = nullptr, int* status = nullptr);
 
 // Raw (zero initial state, no final inversion) CRC32C of byte windows [end - len, end) of a
 // device buffer, one wave per window (len <= kCrcChunkBytes): each lane folds 64 bytes with
@@ -209,15 +213,20 @@ hipError_t crc32c_chunks(const uint8_t* bytes, const CrcChunk* chunks, int n,
 // (record, record-relative first tile), kGroupTiles tiles each (a record's last group may be
 // shorter). Record i's count block at counts + tile0 + grp0 gets its tile counts and group sums
 // (see JsonRecord::has_cnt); gsum[g] = the tokens of group g (the host adds a record's groups);
-// invalid bytes raise recs[i].status to 2.
+// invalid bytes raise recs[i].status to 2, or, with gbad non-null, set gbad[g] = 2 (else 0) by a
+// plain store and leave recs untouched - chunks, recs, groups, crc_out, gsum and gbad may then
+// be host-mapped pinned memory (read and written over the link, no copies); bytes, tables and
+// counts are device memory.
 hipError_t ingest_crc_count(const uint8_t* bytes, const CrcChunk* chunks, int nchunks,
                             const uint32_t* tables, uint32_t* crc_out, int nrec, int ngroups,
                             JsonRecord* recs, const int2* groups, int* counts, int* gsum,
-                            hipStream_t stream);
+                            int* gbad, hipStream_t stream);
 
 // Expands a nibble-packed span (csrc/codec/text_pack.h: 64-byte blocks, per-2-KiB-group
 // {base offset, packed-block mask} pairs in tab) into out[0, n). out must be 16-byte aligned,
-// packed 8-byte aligned.
+// packed 8-byte aligned. packed and tab may be host-mapped pinned memory (the GPU ingest reads the
+// small group table from the source's pinned chunk; the packed stream itself is DMA'd first:
+// kernel loads over the link expand it ~15x slower than the SDMA copy plus a device pass).
 hipError_t text_unpack(const uint8_t* packed, const uint32_t* tab, int64_t n, uint8_t* out,
                        hipStream_t stream);
 
@@ -230,5 +239,12 @@ hipError_t format_floats_java(int n, const float* x, void* out16, hipStream_t st
 // n = (*d_count) * per values (n <= max_n, the launch size): the step graph's form
 hipError_t format_floats_java_dev(int max_n, const int* d_count, int per, const float* x,
                                   void* out16, hipStream_t stream);
+// The step graph's last node: format_floats_java_dev, and the batch's parse verdicts handed
+// back - status_out[i] = status[i], status[i] = 0 for i < *d_nrec (status: the parse's device
+// array, cleared for the slot's next batch; status_out: host-mapped), so the step needs no
+// status copy node. max_n must cover max_nrec values (the launch's threads do both).
+hipError_t format_floats_java_step(int max_n, const int* d_count, int per, const float* x,
+                                   void* out16, const int* d_nrec, int* status, int* status_out,
+                                   hipStream_t stream);
 
 }  // namespace gale

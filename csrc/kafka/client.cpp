@@ -983,6 +983,7 @@ void Consumer::collect(std::vector<Fetched>& out) {
           converted_batches_ += ns.converted_batches;
           poison_batches_ += ns.poison_batches;
           poison_records_ += ns.poison_records;
+          poison_unknown_span_ += ns.poison_unknown_span;
           if (ns.poison_batches && poison_logged_ < 16) {
             ++poison_logged_;
             fprintf(stderr, "[gale consumer] %s-%d: %lld undecodable batch(es) from offset %lld "

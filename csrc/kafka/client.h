@@ -302,6 +302,7 @@ class Consumer {
   int64_t converted_batches() const { return converted_batches_; }
   int64_t poison_batches() const { return poison_batches_; }
   int64_t poison_records() const { return poison_records_; }
+  int64_t poison_unknown_span() const { return poison_unknown_span_; }
   // fetch response bodies are shown to this tap while they are received
   void set_recv_tap(std::shared_ptr<RecvTap> tap) { tap_ = std::move(tap); }
 
@@ -327,6 +328,7 @@ class Consumer {
   int32_t generation_ = -1;
   std::string member_id_;
   std::atomic<int64_t> converted_batches_{0}, poison_batches_{0}, poison_records_{0};
+  std::atomic<int64_t> poison_unknown_span_{0};
   int poison_logged_ = 0;
 };
 

@@ -831,6 +831,15 @@ std::string normalize_records(const uint8_t* p, size_t len, int64_t min_offset, 
   size_t pos = 0;
   std::vector<Rec> legacy_run;           // consecutive plain legacy messages -> one v2 batch
   std::deque<std::string> hold;  // (deque: elements never move, records point into them)
+  // `limit` bounds the decompressed bytes of the whole call, not just of each batch: a
+  // partition fetch of highly compressible batches must not grow the consumer by gigabytes.
+  // Once it is spent, conversion stops and the next fetch resumes at the first batch not
+  // converted; a batch that fails with budget already spent is retried there with the whole
+  // budget before it can become poison.
+  size_t spent = 0;
+  // offset after the previous entry of this response (a failed legacy wrapper's inner records
+  // are the offsets from here to the wrapper's own, its last inner record's)
+  int64_t prev_end = min_offset;
   auto flush_legacy = [&] {
     std::vector<Rec> keep;
     for (const Rec& r : legacy_run)
@@ -864,6 +873,7 @@ std::string normalize_records(const uint8_t* p, size_t len, int64_t min_offset, 
           continue;
         }
         const bool control = (bi.attributes & 0x20) != 0;
+        if (compressed && !control && spent >= limit) break;  // (budget spent: next fetch)
         if (!compressed || control) {
           // verify the records parse, then copy the batch through verbatim
           std::vector<Rec> probe;
@@ -876,8 +886,11 @@ std::string normalize_records(const uint8_t* p, size_t len, int64_t min_offset, 
           std::string plain;
           std::string err;
           if (!decompress(bi.attributes & 7, p + pos + kBatchHeaderBytes,
-                          (size_t)bi.length - kBatchHeaderBytes, plain, limit, &err))
+                          (size_t)bi.length - kBatchHeaderBytes, plain, limit - spent, &err)) {
+            if (spent > 0) break;  // (maybe only the remaining budget: retried next fetch)
             throw ProtocolError(err.empty() ? "corrupt compressed batch" : err);
+          }
+          spent += plain.size();
           std::vector<Rec> probe;
           parse_v2_records(reinterpret_cast<const uint8_t*>(plain.data()), plain.size(),
                            bi.records, base, bi.base_timestamp, bi.max_timestamp,
@@ -902,17 +915,35 @@ std::string normalize_records(const uint8_t* p, size_t len, int64_t min_offset, 
         else
           append_poison(out, base, base, 1, min_offset, st, e.what());
       }
+      prev_end = base + (have_hdr ? bi.last_offset_delta : 0) + 1;
     } else if (magic == 0 || magic == 1) {
+      const int attrs = (int8_t)p[pos + 17];
+      if ((attrs & 7) != 0 && spent >= limit) break;  // (budget spent: next fetch)
+      const size_t held = hold.size();
       try {
         std::vector<Rec> recs;
         size_t used = 0;
-        legacy_records(p + pos, len - pos, true, limit, hold, recs, &used);
+        legacy_records(p + pos, len - pos, true, limit - spent, hold, recs, &used);
+        for (size_t h = held; h < hold.size(); ++h) spent += hold[h].size();
         legacy_run.insert(legacy_run.end(), recs.begin(), recs.end());
         ++st.converted_batches;
       } catch (const ProtocolError& e) {
+        if (spent > 0 && (attrs & 7) != 0) break;  // (maybe only the remaining budget)
         if (!legacy_run.empty()) flush_legacy();
-        append_poison(out, base, base, 1, min_offset, st, e.what());
+        // the wrapper's offset is its LAST inner record's; the inner count is unreadable, so
+        // every offset from the previous entry's end up to it becomes one poison record (for
+        // a compacted log some of those offsets may not exist: poison_unknown_span counts the
+        // records poisoned on that estimate)
+        const int64_t first = std::max(prev_end, min_offset);
+        if ((attrs & 7) != 0 && first < base) {
+          const int64_t n = std::min<int64_t>(base - first + 1, 1 << 20);
+          append_poison(out, base - n + 1, base, (int32_t)n, min_offset, st, e.what());
+          st.poison_unknown_span += n;
+        } else {
+          append_poison(out, base, base, 1, min_offset, st, e.what());
+        }
       }
+      prev_end = base + 1;
     } else {
       // unreadable format: its offsets end where the next entry begins (when the response holds
       // one); otherwise one poison record at the position, which then advances by one per fetch
@@ -928,6 +959,7 @@ std::string normalize_records(const uint8_t* p, size_t len, int64_t min_offset, 
       append_poison(out, first, last, (int32_t)std::min<int64_t>(last - first + 1, 1 << 20),
                     min_offset, st,
                     "unsupported message format (magic " + std::to_string(magic) + ")");
+      prev_end = last + 1;
     }
     pos += entry;
   }

@@ -61,13 +61,18 @@ struct NormalizeStats {
   int64_t converted_batches = 0;  // compressed v2 batches and legacy messages rewritten
   int64_t poison_batches = 0;
   int64_t poison_records = 0;
+  // poison records of failed compressed legacy wrappers, whose inner record count cannot be
+  // read: the offsets from the previous entry's end to the wrapper's (its last inner record's)
+  int64_t poison_unknown_span = 0;
   std::string last_error;
 };
 
 // Rewrite a records blob (a Fetch response's records field) as plain v2 batches (see above).
 // Batches wholly below min_offset are dropped. Original CRCs of converted batches are always
 // verified (their bytes do not survive the conversion); plain v2 batches are copied verbatim
-// (CRC left to the caller's deferred check unless check_crc). limit bounds each decompression.
+// (CRC left to the caller's deferred check unless check_crc). limit bounds the decompressed bytes
+// of the whole call: once spent, the blob ends before the next compressed batch (the caller's
+// next fetch resumes there).
 std::string normalize_records(const uint8_t* p, size_t len, int64_t min_offset, bool check_crc,
                               size_t limit, NormalizeStats& st);
 

@@ -231,8 +231,14 @@ __device__ Text16 format_java(float v, int* len_out) {
 
 __global__ __launch_bounds__(256) void format_floats_kernel(int n, const int* d_count, int per,
                                                             const float* __restrict__ x,
-                                                            uint4* __restrict__ out) {
+                                                            uint4* __restrict__ out,
+                                                            const int* d_nrec, int* status,
+                                                            int* status_out) {
   const int i = blockIdx.x * 256 + threadIdx.x;
+  if (d_nrec && i < *d_nrec) {  // the parse verdicts: to the host, cleared for the next batch
+    status_out[i] = status[i];
+    status[i] = 0;
+  }
   if (d_count) n = min(n, *d_count * per);
   if (i >= n) return;
   int len = 0;
@@ -247,7 +253,8 @@ __global__ __launch_bounds__(256) void format_floats_kernel(int n, const int* d_
 hipError_t format_floats_java(int n, const float* x, void* out16, hipStream_t stream) {
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(format_floats_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
-                     stream, n, nullptr, 1, x, static_cast<uint4*>(out16));
+                     stream, n, nullptr, 1, x, static_cast<uint4*>(out16), nullptr, nullptr,
+                     nullptr);
   return hipGetLastError();
 }
 
@@ -255,7 +262,19 @@ hipError_t format_floats_java_dev(int max_n, const int* d_count, int per, const 
                                   void* out16, hipStream_t stream) {
   if (max_n <= 0) return hipSuccess;
   hipLaunchKernelGGL(format_floats_kernel, dim3((unsigned)((max_n + 255) / 256)), dim3(256), 0,
-                     stream, max_n, d_count, per, x, static_cast<uint4*>(out16));
+                     stream, max_n, d_count, per, x, static_cast<uint4*>(out16), nullptr, nullptr,
+                     nullptr);
+  return hipGetLastError();
+}
+
+hipError_t format_floats_java_step(int max_n, const int* d_count, int per, const float* x,
+                                   void* out16, const int* d_nrec, int* status, int* status_out,
+                                   hipStream_t stream) {
+  if (max_n <= 0) return hipSuccess;
+  if (!d_nrec || !status || !status_out) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(format_floats_kernel, dim3((unsigned)((max_n + 255) / 256)), dim3(256), 0,
+                     stream, max_n, d_count, per, x, static_cast<uint4*>(out16), d_nrec, status,
+                     status_out);
   return hipGetLastError();
 }
 

@@ -615,14 +615,14 @@ __device__ __forceinline__ int record_tiles(const JsonRecord& r) {
 // The parse's counting pass for global tile t (one wave): counts[t]. A record whose counts the
 // ingest pass already left on the device (has_cnt) is skipped.
 __device__ __forceinline__ void count_tile(JsonRecord* recs, const int* tile_rec, int t,
-                                           const uint8_t* bytes, int* counts) {
+                                           const uint8_t* bytes, int* counts, int* status) {
   const int ri = tile_rec[t];
   const JsonRecord r = recs[ri];
   if (r.has_cnt) return;
   bool bad;
   const int cnt = tile_tokens(r, t - r.tile0, bytes, &bad);
   if ((threadIdx.x & 63) == 0) counts[t] = cnt;
-  if (bad) atomicMax(&recs[ri].status, 2);
+  if (bad) atomicMax(status ? &status[ri] : &recs[ri].status, 2);
 }
 
 // The ingest pass's counting of one tile group (one workgroup: wave w counts tile tl0 + w of the
@@ -632,39 +632,52 @@ __device__ __forceinline__ void count_tile(JsonRecord* recs, const int* tile_rec
 // parse finds a tile's first element index from nt / kGroupTiles group sums plus < kGroupTiles
 // tile counts. (Per-tile atomics on one record counter serialise: an ImageNet record is ~850
 // tiles, 80 of the 92 us of a 15 MB fetch's ingest launch, tools/bench_ingest.py.)
+// gbad non-null: the group's verdict goes to gbad[g] (0 / 2) with a plain store instead of an
+// atomic on the record's status - the plan and the results may then live in host memory (the
+// GPU ingest reads them over the link and writes them back without copies; device atomics on
+// fine-grained host memory are not something to rely on).
 __device__ __forceinline__ void count_group(JsonRecord* recs, const int2* groups, int g,
                                             const uint8_t* bytes, int* counts, int* gsum,
-                                            int* lds4) {
+                                            int* gbad, int* lds8) {
   const int wave = threadIdx.x >> 6;
   const int2 gr = groups[g];  // (record, record-relative first tile)
   const JsonRecord r = recs[gr.x];
   const int nt = record_tiles(r);
   const int tl = gr.y + wave;
   int cnt = 0;
+  bool bad = false;
   if (tl < nt) {
-    bool bad;
-    cnt = tile_tokens(r, tl, bytes, &bad);
+    cnt = tile_tokens(r, tl, bytes, &bad);  // (bad: this lane's bytes)
     if ((threadIdx.x & 63) == 0) counts[r.tile0 + (int)r.grp0 + tl] = cnt;
-    if (bad) atomicMax(&recs[gr.x].status, 2);
+    if (bad && !gbad) atomicMax(&recs[gr.x].status, 2);
+    bad = __ballot(bad) != 0;  // the wave's verdict, for lane 0 below
   }
-  if ((threadIdx.x & 63) == 0) lds4[wave] = cnt;
+  if ((threadIdx.x & 63) == 0) {
+    lds8[wave] = cnt;
+    lds8[kGroupTiles + wave] = bad ? 1 : 0;
+  }
   __syncthreads();
   if (threadIdx.x == 0) {
-    int acc = 0;
+    int acc = 0, nbad = 0;
 #pragma unroll
-    for (int w = 0; w < kGroupTiles; ++w) acc += lds4[w];
+    for (int w = 0; w < kGroupTiles; ++w) {
+      acc += lds8[w];
+      nbad += lds8[kGroupTiles + w];
+    }
     counts[r.tile0 + (int)r.grp0 + nt + gr.y / kGroupTiles] = acc;
     gsum[g] = acc;
+    if (gbad) gbad[g] = nbad ? 2 : 0;
   }
 }
 
 __global__ __launch_bounds__(256) void json_count_kernel(JsonRecord* recs, const int* tile_rec,
                                                          int ntiles, const uint8_t* bytes,
-                                                         int* counts, const int* d_ntiles) {
+                                                         int* counts, const int* d_ntiles,
+                                                         int* status) {
   const int t = blockIdx.x * kWaves + (threadIdx.x >> 6);
   if (d_ntiles) ntiles = min(ntiles, *d_ntiles);
   if (t >= ntiles) return;  // (no workgroup barriers in this kernel)
-  count_tile(recs, tile_rec, t, bytes, counts);
+  count_tile(recs, tile_rec, t, bytes, counts, status);
 }
 
 // The ingest pass of a fetch buffer in one launch: CRC window workgroups first (they stage the
@@ -674,7 +687,7 @@ static_assert(kGroupTiles == kWaves, "one tile group per counting workgroup");
 __global__ __launch_bounds__(256) void ingest_crc_count_kernel(
     const uint8_t* bytes, const CrcChunk* chunks, int nchunks, const uint32_t* tables,
     uint32_t* crc_out, int crc_blocks, JsonRecord* recs, const int2* groups, int ngroups,
-    int* counts, int* gsum) {
+    int* counts, int* gsum, int* gbad) {
   __shared__ uint32_t T[crc::kTableWords];
   if ((int)blockIdx.x < crc_blocks) {
     crc::crc_stage_tables(tables, T);
@@ -683,13 +696,14 @@ __global__ __launch_bounds__(256) void ingest_crc_count_kernel(
   }
   const int g = (int)blockIdx.x - crc_blocks;
   if (g >= ngroups) return;
-  count_group(recs, groups, g, bytes, counts, gsum, reinterpret_cast<int*>(T));
+  count_group(recs, groups, g, bytes, counts, gsum, gbad, reinterpret_cast<int*>(T));
 }
 
 __global__ __launch_bounds__(256) void json_parse_kernel(JsonRecord* recs, const int* tile_rec,
                                                          int ntiles, const uint8_t* bytes, int H,
                                                          int W, int C, const int* counts,
-                                                         float* out, const int* d_ntiles) {
+                                                         float* out, const int* d_ntiles,
+                                                         int* status) {
   __shared__ __attribute__((aligned(16))) uint8_t lds_text[kWaves][kText];
   __shared__ uint16_t lds_tok[kWaves][kMaxTok];
   __shared__ uint32_t lds_cm[kWaves][kTile / 16 + 1];  // packed masks of the tile's chunks + 1
@@ -815,7 +829,7 @@ __global__ __launch_bounds__(256) void json_parse_kernel(JsonRecord* recs, const
     if (idx < expected) dst[idx] = val;
   }
   if (last_tile && lane == 0 && base + ntok != expected) bad = max(bad, 1);
-  if (bad) atomicMax(&recs[ri].status, bad);
+  if (bad) atomicMax(status ? &status[ri] : &recs[ri].status, bad);
 }
 
 }  // namespace
@@ -831,29 +845,29 @@ int json_tile_count(int64_t off, int32_t len) {
 hipError_t ingest_crc_count(const uint8_t* bytes, const CrcChunk* chunks, int nchunks,
                             const uint32_t* tables, uint32_t* crc_out, int nrec, int ngroups,
                             JsonRecord* recs, const int2* groups, int* counts, int* gsum,
-                            hipStream_t stream) {
+                            int* gbad, hipStream_t stream) {
   if (nrec <= 0) ngroups = 0;
   int crc_blocks = (nchunks + crc::kCrcWaves - 1) / crc::kCrcWaves;
   if (crc_blocks > 1024) crc_blocks = 1024;  // (windows loop: the table load is amortised)
   if (crc_blocks + ngroups == 0) return hipSuccess;
   hipLaunchKernelGGL(ingest_crc_count_kernel, dim3(crc_blocks + ngroups), dim3(256), 0, stream,
                      bytes, chunks, nchunks, tables, crc_out, crc_blocks, recs, groups, ngroups,
-                     counts, gsum);
+                     counts, gsum, gbad);
   return hipGetLastError();
 }
 
 hipError_t json_parse_instances(int nrec, int ntiles, JsonRecord* recs, const int* tile_rec,
                                 const uint8_t* bytes, int H, int W, int C, int* tile_counts,
                                 float* out, hipStream_t stream, bool count_pass,
-                                const int* d_ntiles) {
+                                const int* d_ntiles, int* status) {
   if (nrec <= 0 || ntiles <= 0) return hipSuccess;
   if (H <= 0 || W <= 0 || C <= 0) return hipErrorInvalidValue;
   const int blocks = (ntiles + kWaves - 1) / kWaves;
   if (count_pass)
     hipLaunchKernelGGL(json_count_kernel, dim3(blocks), dim3(64 * kWaves), 0, stream, recs,
-                       tile_rec, ntiles, bytes, tile_counts, d_ntiles);
+                       tile_rec, ntiles, bytes, tile_counts, d_ntiles, status);
   hipLaunchKernelGGL(json_parse_kernel, dim3(blocks), dim3(64 * kWaves), 0, stream, recs,
-                     tile_rec, ntiles, bytes, H, W, C, tile_counts, out, d_ntiles);
+                     tile_rec, ntiles, bytes, H, W, C, tile_counts, out, d_ntiles, status);
   return hipGetLastError();
 }
 

@@ -738,7 +738,7 @@ void Engine::source_loop(int idx) {
     ctl.cv.notify_all();
   };
   int64_t last_commit = mono_ns();
-  int64_t seen_conv = 0, seen_poison = 0, seen_poison_recs = 0;
+  int64_t seen_conv = 0, seen_poison = 0, seen_poison_recs = 0, seen_unknown = 0;
   std::vector<InRecord> good;
   while (cons && !stopping_) {
     try {
@@ -761,14 +761,16 @@ void Engine::source_loop(int idx) {
       ns_poll_ += mono_ns() - t0;
       // record-format conversion (compressed / legacy batches) and poison batches
       const int64_t cb = cons->converted_batches(), pb = cons->poison_batches(),
-                    pr = cons->poison_records();
+                    pr = cons->poison_records(), pu = cons->poison_unknown_span();
       if (cb != seen_conv || pb != seen_poison) {
         converted_batches_ += cb - seen_conv;
         poison_batches_ += pb - seen_poison;
         poison_records_ += pr - seen_poison_recs;
+        poison_unknown_span_ += pu - seen_unknown;
         seen_conv = cb;
         seen_poison = pb;
         seen_poison_recs = pr;
+        seen_unknown = pu;
       }
     } catch (const std::exception& e) {
       fprintf(stderr, "[gale source %d] fetch failed: %s\n", idx, e.what());
@@ -1654,6 +1656,7 @@ std::map<std::string, double> Engine::stats() const {
   s["converted_batches"] = (double)converted_batches_;
   s["poison_batches"] = (double)poison_batches_;
   s["poison_records"] = (double)poison_records_;
+  s["poison_unknown_span"] = (double)poison_unknown_span_;
   s["split_records"] = (double)split_records_;
   s["sparse_fetches"] = (double)sparse_fetches_;
   s["restored_fetches"] = (double)restored_fetches_;

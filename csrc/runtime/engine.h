@@ -380,6 +380,7 @@ class Engine {
   std::atomic<int64_t> requeued_{0}, replica_failures_{0}, replica_restarts_{0}, commits_{0};
   std::atomic<int64_t> err_by_status_[16] = {};
   std::atomic<int64_t> converted_batches_{0}, poison_batches_{0}, poison_records_{0};
+  std::atomic<int64_t> poison_unknown_span_{0};  // legacy wrapper poison on an estimated span
   std::atomic<int64_t> split_records_{0}, split_fragments_{0};
   std::atomic<int64_t> sparse_fetches_{0}, restored_fetches_{0};  // bounce receive (pack_tap.h)
   Histogram h_queue_us_, h_device_us_, h_engine_e2e_us_, h_record_e2e_ms_, h_batch_images_;

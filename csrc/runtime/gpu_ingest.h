@@ -32,13 +32,12 @@ class GpuIngest : public Ingest {
     std::mutex mu;
     hipStream_t stream = nullptr;
     hipEvent_t done = nullptr;
-    // one pinned staging buffer and its device image:
-    //   [pack tab u32 x 2ng (packed bodies)][CrcChunk x nc][tile_rec x nt][JsonRecord x nr]
-    //   [tokens i32 x nr][crc u32 x nc]
-    // the host writes the plan and zeroed token counters, ONE H2D copies up to the tokens, ONE
-    // D2H copies back [JsonRecord..crc] (per-record status, element counts, window CRCs)
+    // one host-mapped pinned buffer, no device image:
+    //   [CrcChunk x nc][int2 group x ng][JsonRecord x nr][group sum i32 x ng][crc u32 x nc]
+    //   [group verdict i32 x ng]
+    // the host writes the plan, ingest_crc_count reads it over the link and stores the results
+    // (group sums and verdicts, window CRCs) back into it; no copies either way
     uint8_t* h_io = nullptr;
-    uint8_t* d_io = nullptr;
     size_t io_cap = 0;
     int* d_counts = nullptr;  // per-tile token counts (scratch)
     size_t counts_cap = 0;

@@ -39,6 +39,10 @@ GpuReplica::GpuReplica(std::shared_ptr<Executor> exec, int H, int W, int C, int 
       const size_t tb = (size_t)kFloatTextSlot * mb * classes;
       check_hip(hipHostMalloc(reinterpret_cast<void**>(&s.h_text), tb, hipHostMallocMapped),
                 "hipHostMalloc(text)");
+      check_hip(hipMalloc(reinterpret_cast<void**>(&s.d_status), sizeof(int) * mb),
+                "hipMalloc(status)");
+      check_hip(hipMemset(s.d_status, 0, sizeof(int) * mb), "hipMemset(status)");
+      s.h_status = static_cast<int*>(mapped_alloc(sizeof(int) * mb, "status"));
     }
     check_hip(hipEventCreateWithFlags(&s.done, hipEventDisableTiming |
                                                    (wait_poll_us_ < 0 ? hipEventBlockingSync : 0)),
@@ -61,12 +65,29 @@ GpuReplica::~GpuReplica() {
     if (s.d_tiles) hipFree(s.d_tiles);
     if (s.h_out) hipHostFree(s.h_out);
     if (s.h_text) hipHostFree(s.h_text);
+    if (s.h_status) hipHostFree(s.h_status);
+    if (s.d_status) hipFree(s.d_status);
     if (s.done) hipEventDestroy(s.done);
   }
   if (stream_) hipStreamDestroy(stream_);
 }
 
 std::string GpuReplica::name() const { return "gpu" + std::to_string(exec_->device()); }
+
+// Host-mapped pinned memory that kernels address with the host pointer (ROCm maps it at the
+// same virtual address; anything else is refused rather than silently copied).
+void* GpuReplica::mapped_alloc(size_t bytes, const char* what) {
+  void* h = nullptr;
+  check_hip(hipHostMalloc(&h, bytes, hipHostMallocMapped), what);
+  void* d = nullptr;
+  check_hip(hipHostGetDevicePointer(&d, h, 0), what);
+  if (d != h) {
+    hipHostFree(h);
+    throw std::runtime_error(std::string("GpuReplica: mapped ") + what +
+                             " buffer has another device address");
+  }
+  return h;
+}
 
 void GpuReplica::ensure_host(Slot& s, size_t bytes) {
   if (bytes <= s.h_cap) return;
@@ -95,8 +116,8 @@ void GpuReplica::ensure_tiles(Slot& s, int ntiles, int keep) {
   const size_t rec_bytes = sizeof(JsonRecord) * (size_t)exec_->max_batch();
   const size_t bytes = kMetaHdr + rec_bytes + sizeof(int) * (size_t)cap;
   if (s.h_hdr) check_hip(hipEventSynchronize(s.done), "hipEventSynchronize");
-  uint8_t* h = nullptr;
-  check_hip(hipHostMalloc(reinterpret_cast<void**>(&h), bytes), "hipHostMalloc(meta)");
+  // host-mapped: the copy-free step graph's kernels read the metadata from here
+  uint8_t* h = static_cast<uint8_t*>(mapped_alloc(bytes, "meta"));
   memset(h, 0, kMetaHdr);
   if (s.h_hdr) {
     memcpy(h + kMetaHdr, s.h_recs, sizeof(JsonRecord) * (size_t)keep);
@@ -251,6 +272,7 @@ void GpuReplica::submit(Batch& b) {
     s.h_hdr[2] = img;
     hipGraphExec_t g = step_for(s, slot, count_pass);
     check_hip(hipGraphLaunch(g, stream_), "hipGraphLaunch(step)");
+    b.step_graph = true;
     ++step_batches_;
     check_hip(hipEventRecord(s.done, stream_), "hipEventRecord");
     s.t_submit_ns = mono_ns();
@@ -299,7 +321,31 @@ hipGraphExec_t GpuReplica::step_for(Slot& s, int slot, bool count_pass) {
   check_hip(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking), "capture stream");
   hipGraph_t graph = nullptr;
   hipError_t e = hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal);
-  if (e == hipSuccess) {
+  if (e == hipSuccess && gpu_encode_) {
+    // copy-free step: [count] -> parse -> forward -> format (+ verdicts to the host). The
+    // kernels read the header, records and tile map where the host wrote them (host-mapped;
+    // a record and a tile index per parse wave, one count per forward workgroup), and the last
+    // node stores text and verdicts into host-mapped slots. The r4 step also had a metadata
+    // H2D and a status D2H node, each run as a CU blit kernel on this runtime (2 per batch,
+    // 68 us average under the serving load, profiles/r5_ingest_zero_copy_ab.txt).
+    hipError_t c = json_parse_instances(mb, s.tiles_cap, s.h_recs, s.h_tile_rec, s.d_bytes, H_,
+                                        W_, C_, s.d_tiles,
+                                        static_cast<float*>(exec_->input(slot)), cs, count_pass,
+                                        s.h_hdr + 1, s.d_status);
+    if (c == hipSuccess) {
+      try {
+        exec_->launch_device_batch(slot, s.h_hdr + 2, cs);
+      } catch (const std::exception&) {
+        c = hipErrorLaunchFailure;
+      }
+    }
+    if (c == hipSuccess)
+      c = format_floats_java_step(std::max(mb * classes_, mb), s.h_hdr + 2, classes_,
+                                  static_cast<const float*>(exec_->output(slot)), s.h_text,
+                                  s.h_hdr, s.d_status, s.h_status, cs);
+    e = hipStreamEndCapture(cs, &graph);
+    if (e == hipSuccess) e = c;
+  } else if (e == hipSuccess) {
     hipError_t c = hipMemcpyAsync(s.d_hdr, s.h_hdr, meta, hipMemcpyHostToDevice, cs);
     if (c == hipSuccess)
       c = json_parse_instances(mb, s.tiles_cap, s.d_recs, s.d_tile_rec, s.d_bytes, H_, W_, C_,
@@ -357,8 +403,9 @@ void GpuReplica::wait(Batch& b) {
     check_hip(hipEventSynchronize(s.done), "hipEventSynchronize(batch)");
   }
   b.dev_status.assign(b.recs.size(), codec::OK);
+  const bool copy_free = b.step_graph && gpu_encode_;
   for (size_t i = 0; i < b.recs.size(); ++i) {
-    const int st = s.h_recs[i].status;
+    const int st = copy_free ? s.h_status[i] : s.h_recs[i].status;
     if (st == 1 || st == 3) b.dev_status[i] = codec::BAD_SHAPE;
     else if (st == 2) b.dev_status[i] = codec::BAD_NUMBER;
   }

@@ -105,12 +105,16 @@ std::shared_ptr<uint8_t> PinnedPool::alloc(size_t n, bool* pinned) {
         p = st_->free.back();
         st_->free.pop_back();
       } else if ((st_->all.size() + 1) * st_->chunk <= st_->max_bytes) {
-        // portable: usable as a DMA source by every GPU of the process
-        if (hipHostMalloc(reinterpret_cast<void**>(&p), st_->chunk, hipHostMallocPortable) ==
-            hipSuccess) {
+        // portable + mapped: a DMA source for every GPU of the process, and directly readable
+        // by kernels at the same address (the GPU ingest expands the packed text from here)
+        if (hipHostMalloc(reinterpret_cast<void**>(&p), st_->chunk,
+                          hipHostMallocPortable | hipHostMallocMapped) == hipSuccess) {
           st_->all.push_back(p);
           uint8_t* d = nullptr;
-          if (st_->mirror_device >= 0 && hipSetDevice(st_->mirror_device) == hipSuccess &&
+          void* dp = nullptr;
+          const bool same = hipHostGetDevicePointer(&dp, p, 0) == hipSuccess && dp == p;
+          if (st_->mirror_device >= 0 && same &&
+              hipSetDevice(st_->mirror_device) == hipSuccess &&
               hipMalloc(reinterpret_cast<void**>(&d), st_->chunk) == hipSuccess)
             st_->mirrors[p] = d;  // (no mirror: this chunk's records take the host path)
           else if (st_->mirror_device >= 0)

@@ -63,6 +63,7 @@ struct Batch {
   const uint8_t* pred_text = nullptr;
   std::vector<int32_t> dev_status;  // per-record codec::Status found by the replica's parser
   int64_t t_take_ns = 0, t_submit_ns = 0, t_done_ns = 0;
+  bool step_graph = false;  // (GpuReplica) submitted as one replay of the slot's step graph
 };
 
 class Replica {
@@ -128,9 +129,10 @@ class GpuReplica : public Replica {
   // DMA'd from the host-pinned fetch buffer, as it would be across GPUs (--locality-split
   // exercises the multi-GPU dispatch on one device)
   // step_graph: with use_graph and a whole-network plan (Executor::device_batch_ok), each batch
-  // is ONE hipGraphLaunch of the slot's captured step: metadata H2D -> JSON parse -> forward ->
-  // prediction text (or probabilities D2H) -> status D2H, the kernels reading the batch's record /
-  // tile / image counts from the metadata header, so one graph per slot serves every batch size
+  // is ONE hipGraphLaunch of the slot's captured step: JSON parse -> forward -> prediction text +
+  // parse verdicts, the kernels reading the batch's record / tile / image counts and records from
+  // the host-mapped metadata (no copy nodes; without gpu_encode: metadata H2D -> parse -> forward
+  // -> probabilities D2H -> status D2H), so one graph per slot serves every batch size
   GpuReplica(std::shared_ptr<Executor> exec, int H, int W, int C, int classes, bool use_graph,
              int wait_poll_us = 0, bool gpu_encode = false, int locality = -1,
              bool step_graph = true);
@@ -166,6 +168,10 @@ class GpuReplica : public Replica {
     int tiles_cap = 0;
     float* h_out = nullptr;      // pinned softmax rows
     uint8_t* h_text = nullptr;   // pinned, device-mapped prediction text slots (gpu_encode)
+    // copy-free step graph (gpu_encode): the kernels read the metadata from h_hdr (host-mapped)
+    // and raise verdicts in d_status; the format node hands them to h_status (host-mapped)
+    int* d_status = nullptr;
+    int* h_status = nullptr;
     hipEvent_t done = nullptr;
     int64_t t_submit_ns = 0;
   };
@@ -174,6 +180,7 @@ class GpuReplica : public Replica {
   void ensure_tiles(Slot& s, int ntiles, int keep);
   void drop_steps(Slot& s);  // (buffers moved: the captured steps point at the old ones)
   hipGraphExec_t step_for(Slot& s, int slot, bool count_pass);
+  static void* mapped_alloc(size_t bytes, const char* what);
   std::shared_ptr<Executor> exec_;
   int H_, W_, C_, classes_;
   bool use_graph_;

@@ -28,7 +28,8 @@ KEYS = ("records_in", "records_out", "images_out", "errors", "produce_failures",
         "record_e2e_ms_p50", "record_e2e_ms_p99", "batch_images_mean", "rebalances",
         "generation", "assigned_partitions", "eff_max_batch", "eff_max_wait_us",
         "lag_rebalances", "lag_rebalances_skipped", "capacity_rps", "steals",
-        "converted_batches", "poison_batches", "poison_records", "split_records",
+        "converted_batches", "poison_batches", "poison_records", "poison_unknown_span",
+        "split_records",
         "graph_step_batches", "sparse_fetches", "restored_fetches", "pinned_chunks",
         "pinned_waits", "pinned_heap_budget")
 

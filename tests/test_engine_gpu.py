@@ -363,6 +363,81 @@ def test_gpu_fused_ingest_kernel_matches_separate_passes():
         np.testing.assert_array_equal(out.cpu().numpy(), np.concatenate(xs))
 
 
+def test_gpu_ingest_zero_copy_plan_and_group_verdicts():
+    """The engine's zero-copy form of ingest_crc_count: windows, records and groups are read from
+    host-mapped pinned memory, CRCs / group sums / group verdicts are stored back into it (no
+    copies, no atomics on host memory). A record with a byte outside the number alphabet gets
+    verdict 2 on exactly the group holding that byte; the others stay 0 and their sums match."""
+    import os
+
+    rng = np.random.default_rng(11)
+    G = C.GROUP_TILES
+    H, Wd, Cc = 32, 32, 3
+    xs = [rng.random((n, H, Wd, Cc), dtype=np.float32) for n in (2, 1, 3)]
+    arrays = [array_text(C.encode_instances(x), H, Wd, Cc) for x in xs]
+    raw, recs, total, tiles = stage(arrays)
+    raw = bytearray(raw)
+    bad_pos = int(recs[1]["off"]) + 9000  # inside record 1, tile 4 (group 1)
+    while raw[bad_pos] not in b"0123456789":
+        bad_pos += 1
+    raw[bad_pos] = ord("x")
+    buf = bytes(raw) + os.urandom(3000)
+    wins = [(len(buf) - 4096 * k, 4096) for k in range(len(buf) // 4096)][::-1]
+    if len(buf) % 4096:
+        wins = [(len(buf) - 4096 * len(wins), len(buf) % 4096)] + wins
+    groups, grp0 = [], []
+    for i, r in enumerate(recs):
+        grp0.append(len(groups))
+        nt = C.json_tile_count(int(r["off"]), int(r["len"]))
+        groups += [(i, t0) for t0 in range(0, nt, G)]
+    recs["pad"] = grp0
+    ch = np.zeros(len(wins), dtype=[("end", "<i8"), ("len", "<i4"), ("pad", "<i4")])
+    for i, (e, ln) in enumerate(wins):
+        ch[i] = (e, ln, 0)
+    # plan and results in ONE host-mapped buffer, as GpuIngest lays them out
+    parts = [np.frombuffer(a.tobytes(), dtype=np.uint8)
+             for a in (ch, np.array(groups, dtype=np.int32), recs)]
+    offs, o = [], 0
+    for a in parts:
+        offs.append(o)
+        o += (a.nbytes + 15) & ~15
+    o_gsum = o
+    o_crc = o_gsum + ((4 * len(groups) + 15) & ~15)
+    o_gbad = o_crc + ((4 * len(wins) + 15) & ~15)
+    mb = C.MappedBuffer(o_gbad + 4 * len(groups) + 16)
+    v = mb.numpy()
+    for a, off in zip(parts, offs):
+        v[off:off + a.nbytes] = a
+    v[o_gsum:] = 0xEE  # (results must overwrite this)
+    d = torch.frombuffer(bytearray(buf + bytes(64)), dtype=torch.uint8).cuda()
+    tables = torch.tensor(np.array(K.crc32c_device_tables(), dtype=np.uint32).view(np.int32),
+                          device="cuda")
+    cnt = torch.full((tiles + len(groups),), -1, dtype=torch.int32, device="cuda")
+    s = torch.cuda.current_stream().cuda_stream
+    C.ingest_crc_count(d.data_ptr(), mb.ptr + offs[0], len(wins), tables.data_ptr(),
+                       mb.ptr + o_crc, len(recs), len(groups), mb.ptr + offs[2],
+                       mb.ptr + offs[1], cnt.data_ptr(), mb.ptr + o_gsum, s,
+                       gbad=mb.ptr + o_gbad)
+    torch.cuda.synchronize()
+    gbad = v[o_gbad:o_gbad + 4 * len(groups)].view(np.int32)
+    gsum = v[o_gsum:o_gsum + 4 * len(groups)].view(np.int32)
+    want_bad = [2 if (i == 1 and t0 == 4) else 0 for i, t0 in groups]
+    assert list(gbad) == want_bad
+    assert list(v[offs[2]:offs[2] + recs.nbytes].view(REC)["status"]) == [0, 0, 0]  # untouched
+    for i, r in enumerate(recs):
+        if i == 1:
+            continue
+        g0, g1 = grp0[i], (grp0[i + 1] if i + 1 < len(recs) else len(groups))
+        assert gsum[g0:g1].sum() == len(xs[i]) * H * Wd * Cc
+    crc = v[o_crc:o_crc + 4 * len(wins)].view(np.int32)
+    crc2 = torch.zeros(len(wins), dtype=torch.int32, device="cuda")
+    dch = torch.from_numpy(ch.view(np.uint8).copy()).cuda()
+    C.crc32c_chunks(d.data_ptr(), dch.data_ptr(), len(wins), tables.data_ptr(), crc2.data_ptr(),
+                    s)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(crc, crc2.cpu().numpy())
+
+
 def test_gpu_ingest_rejects_corrupt_batch_and_counts_images(broker):
     """GPU ingest: a bit flip inside a record batch fails its device-computed CRC32C, so all of
     its records get the error policy; records of intact batches are counted (N = 2 images

@@ -224,6 +224,53 @@ def test_poison_batches_become_marked_records():
     assert st["poison_batches"] == 3 and st["poison_records"] == 18
 
 
+def test_decompression_budget_is_per_fetch_not_per_batch():
+    """the decompression limit bounds the whole normalisation of a partition fetch.
+    Five gzip batches of ~20 KB plain each under a 50 KB budget: the blob ends after the batches
+    the budget covers (no poison), and normalising again from the next offset - the consumer's
+    next fetch - continues where it stopped."""
+    recs = [(None, b"0" * 2000, 0, None) for _ in range(10)]
+    zs = [K.compress_batch(K.encode_batch(recs, 10 * i, 0), "gzip") for i in range(5)]
+    blob_in = b"".join(zs)
+    got_all = []
+    pos = 0
+    calls = 0
+    while pos < 50:
+        blob, st = K.normalize_records(blob_in, pos, True, limit=50_000)
+        assert st["poison_batches"] == 0
+        offs = [r["offset"] for r in K.decode_records(blob, 0, True)]
+        assert offs and offs[0] == pos and len(offs) <= 30  # <= 2-3 batches per call
+        got_all += offs
+        pos = offs[-1] + 1
+        calls += 1
+    assert got_all == list(range(50)) and calls >= 2
+    # with the budget spent by earlier batches, a batch over the remaining budget is not poison
+    blob, st = K.normalize_records(blob_in, 0, True, limit=30_000)
+    assert st["poison_batches"] == 0 and len(K.decode_records(blob, 0, True)) == 10
+    # one batch over the whole budget alone is
+    _, st = K.normalize_records(zs[0], 0, True, limit=10_000)
+    assert st["poison_batches"] == 1
+
+
+def test_failed_legacy_wrapper_poisons_its_inner_span():
+    """a compressed magic-1 wrapper that cannot be decoded covers the offsets after the
+    previous entry up to its own (its last inner record's); each becomes a poison record (counted
+    in poison_unknown_span, since the inner count itself is unreadable)."""
+    vals = [b'{"instances": [[[[1.0]]]]}'] * 4
+    first = K.encode_message_set(1, vals, 10, "none")  # offsets 10-13, plain
+    bad = bytearray(K.encode_message_set(1, vals, 14, "gzip"))  # wrapper offset 17
+    mid = 16 + (len(bad) - 16) // 2
+    bad[mid:mid + 6] = b"\xff" * 6  # corrupt the compressed payload ...
+    import zlib
+    body = bytes(bad[16:])  # ... and fix the message CRC (magic .. value)
+    bad[12:16] = struct.pack(">I", zlib.crc32(body))
+    _, st = K.normalize_records(first + bytes(bad), 10, True)
+    got = K.decode_records(first + bytes(bad), 10, True)
+    assert [r["offset"] for r in got] == list(range(10, 18))
+    assert [r["offset"] for r in got if r.get("poison")] == [14, 15, 16, 17]
+    assert st["poison_records"] == 4 and st["poison_unknown_span"] == 4
+
+
 # ---- through the broker and the consumer ---------------------------------------------------------
 
 @pytest.fixture()

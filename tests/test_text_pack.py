@@ -90,3 +90,25 @@ def test_device_unpack_matches_host(name, data):
     got = bytes(out.cpu().numpy())
     assert got[:len(data)] == data
     assert got[len(data):] == b"\xa5" * 64
+
+
+@pytest.mark.gpu
+def test_device_unpack_reads_host_mapped_packed_text():
+    """The GPU ingest's zero-copy form: the packed stream and its group table stay in host-mapped
+    pinned memory (the source's pinned chunk) and the kernel reads them over the link."""
+    import torch
+
+    data = _jackson_text(3) + b"\x00tail bytes \xff" + _jackson_text(1)
+    packed, tab = N.text_pack(data)
+    tb = tab.astype(np.uint32).tobytes()
+    buf = N.MappedBuffer(len(packed) + 16 + len(tb))
+    v = buf.numpy()
+    v[:len(packed)] = np.frombuffer(packed, dtype=np.uint8)
+    toff = (len(packed) + 15) & ~15
+    v[toff:toff + len(tb)] = np.frombuffer(tb, dtype=np.uint8)
+    dev = torch.device("cuda", 0)
+    out = torch.full((len(data) + 64,), 0xA5, dtype=torch.uint8, device=dev)
+    s = torch.cuda.current_stream(dev)
+    N.text_unpack(buf.ptr, buf.ptr + toff, len(data), out.data_ptr(), s.cuda_stream)
+    got = bytes(out.cpu().numpy())
+    assert got[:len(data)] == data and got[len(data):] == b"\xa5" * 64
