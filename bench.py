@@ -103,6 +103,10 @@ def parse_args(argv=None):
                          "through a cache-resident receive window (expanded on the device; needs "
                          "AVX-512 VBMI): half the link and pinned-memory bytes, "
                          "profiles/r4_ab_step_graph_text_pack.jsonl")
+    ap.add_argument("--pack-nt", action=argparse.BooleanOptionalAction, default=True,
+                    help="the sources write the packed text with non-temporal stores (no "
+                         "read-for-ownership of the pinned destination lines, the receive window "
+                         "stays in L2)")
     ap.add_argument("--pinned-fetch-mb", type=int, default=4096,
                     help="pinned fetch-buffer budget per GPU (doubled with --text-pack)")
     ap.add_argument("--text-pack-window-kb", type=int, default=256,
@@ -689,6 +693,7 @@ def main(argv=None) -> int:
     from gale.models import get_model
 
     net = get_model(a.model)
+    native().set_pack_stream_stores(a.pack_nt)
     K = native().kafka
     ipr = a.images_per_record
     parts_per_rank = a.partitions * local_gpus

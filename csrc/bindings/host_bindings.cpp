@@ -435,6 +435,8 @@ void bind_host(py::module_& m) {
   }, py::arg("data"), py::arg("H"), py::arg("W"), py::arg("C"), py::arg("max_images") = -1);
   // ---- nibble transport (text_pack.h) ----
   m.def("text_pack_fast", &codec::text_pack_fast);
+  m.def("set_pack_stream_stores", &codec::set_pack_stream_stores,
+        "non-temporal stores for the packed stream (default on; A/B switch)");
   m.def("text_pack", [](py::bytes b, bool force_scalar) {
     const std::string_view s = view(b);
     std::string out(codec::pack_bound(s.size()), '\0');

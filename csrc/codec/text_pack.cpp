@@ -6,6 +6,7 @@
 
 #include <algorithm>
 #include <array>
+#include <atomic>
 
 namespace gale {
 namespace codec {
@@ -59,6 +60,21 @@ void pack_scalar(const uint8_t* src, size_t upto, uint8_t* dst, uint32_t* tab, P
 // of (code | byte) rejects the block, a multiply-add of byte pairs by (1, 16) forms the packed
 // bytes in 16-bit lanes and a word -> byte narrowing stores them. The group's block mask and the
 // output offset stay in registers (one table store per 2 KiB).
+// Stores: the packed stream goes to pinned memory that only the GPU's DMA reads next, so it is
+// written with non-temporal stores (NT = true): full 64-byte lines leave through the write-
+// combining buffers without a read-for-ownership of each destination line and without evicting
+// the L2-resident receive window (two 32-byte halves of a line are written back to back: a
+// packed block is 32 bytes, a raw one two 32-byte halves, every block 32-byte aligned).
+template <bool NT>
+__attribute__((target("avx512f,avx512bw,avx512vbmi"), always_inline)) inline void store32(
+    uint8_t* p, __m256i v) {
+  if (NT)
+    _mm256_stream_si256(reinterpret_cast<__m256i*>(p), v);
+  else
+    _mm256_storeu_si256(reinterpret_cast<__m256i*>(p), v);
+}
+
+template <bool NT>
 __attribute__((target("avx512f,avx512bw,avx512vbmi"))) void pack_avx512(const uint8_t* src,
                                                                         size_t upto, uint8_t* dst,
                                                                         uint32_t* tab,
@@ -82,11 +98,12 @@ __attribute__((target("avx512f,avx512bw,avx512vbmi"))) void pack_avx512(const ui
       const __m512i c = _mm512_permutex2var_epi8(t0, v, t1);
       if (__builtin_expect(_mm512_movepi8_mask(_mm512_or_si512(c, v)) == 0, 1)) {
         const __m512i w = _mm512_maddubs_epi16(c, pair);
-        _mm256_storeu_si256(reinterpret_cast<__m256i*>(dst + o), _mm512_cvtepi16_epi8(w));
+        store32<NT>(dst + o, _mm512_cvtepi16_epi8(w));
         mask |= 1u << (b % kPackGroupBlocks);
         o += kPackBlock / 2;
       } else {
-        _mm512_storeu_si512(dst + o, v);
+        store32<NT>(dst + o, _mm512_castsi512_si256(v));
+        store32<NT>(dst + o + 32, _mm512_extracti64x4_epi64(v, 1));
         o += kPackBlock;
       }
     }
@@ -96,6 +113,17 @@ __attribute__((target("avx512f,avx512bw,avx512vbmi"))) void pack_avx512(const ui
   st.out = o;
   st.mask = mask;
 }
+
+std::atomic<bool> g_pack_nt{true};
+
+}  // namespace
+
+void set_pack_stream_stores(bool on) { g_pack_nt = on; }
+bool pack_stream_stores() { return g_pack_nt.load(std::memory_order_relaxed); }
+
+namespace {
+
+__attribute__((target("sse2"))) inline void store_fence() { _mm_sfence(); }
 
 }  // namespace
 
@@ -108,10 +136,13 @@ bool text_pack_fast() {
 void text_pack_blocks(const uint8_t* src, size_t upto, uint8_t* dst, uint32_t* tab,
                       PackState& st, size_t src_base) {
   if (upto <= st.block) return;
-  if (text_pack_fast())
-    pack_avx512(src, upto, dst, tab, st, src_base);
-  else
+  if (!text_pack_fast()) {
     pack_scalar(src, upto, dst, tab, st, src_base);
+  } else if ((reinterpret_cast<uintptr_t>(dst) & 31) == 0 && pack_stream_stores()) {
+    pack_avx512<true>(src, upto, dst, tab, st, src_base);
+  } else {
+    pack_avx512<false>(src, upto, dst, tab, st, src_base);
+  }
 }
 
 size_t text_pack_finish(const uint8_t* src, size_t n, uint8_t* dst, uint32_t* tab, PackState& st,
@@ -127,6 +158,7 @@ size_t text_pack_finish(const uint8_t* src, size_t n, uint8_t* dst, uint32_t* ta
   }
   if (st.block % kPackGroupBlocks != 0 || r)  // an open group: its mask
     tab[2 * (full / kPackGroupBlocks) + 1] = st.mask;
+  store_fence();  // the streamed stores are globally visible before the stream is handed on
   return st.out;
 }
 

@@ -64,6 +64,11 @@ size_t text_pack_finish(const uint8_t* src, size_t n, uint8_t* dst, uint32_t* ta
 // but ~10x slower, so the engine only packs by default when this holds.
 bool text_pack_fast();
 
+// Non-temporal stores for the packed stream (default on; a 32-byte-aligned destination): the
+// pinned chunk is read next by the GPU's DMA, not by this core. Process-wide switch for A/B.
+void set_pack_stream_stores(bool on);
+bool pack_stream_stores();
+
 // Packs src[0, n) into dst (>= pack_bound(n) bytes) and tab (2 * pack_groups(n) words).
 // Returns the packed size. force_scalar selects the reference path (tests).
 size_t text_pack(const uint8_t* src, size_t n, uint8_t* dst, uint32_t* tab,

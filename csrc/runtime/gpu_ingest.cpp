@@ -37,6 +37,7 @@ GpuIngest::~GpuIngest() {
   for (auto& L : lanes_) {
     if (L->stream) hipStreamSynchronize(L->stream);
     if (L->h_io) hipHostFree(L->h_io);
+    if (L->d_io) hipFree(L->d_io);
     if (L->d_counts) hipFree(L->d_counts);
     if (L->done) hipEventDestroy(L->done);
     if (L->stream) hipStreamDestroy(L->stream);
@@ -50,8 +51,10 @@ void GpuIngest::grow(Lane& L, size_t io_bytes, size_t tiles) {
   };
   if (io_bytes > L.io_cap) {
     if (L.h_io) hipHostFree(L.h_io);
+    if (L.d_io) hipFree(L.d_io);
     L.io_cap = up(io_bytes, L.io_cap);
-    // the plan and the results: host-mapped, read and written by the kernels over the link
+    check_hip(hipMalloc(reinterpret_cast<void**>(&L.d_io), L.io_cap), "ingest: d_io");
+    // the plan (DMA'd to d_io) and the results (stored here by the kernel): host-mapped
     check_hip(hipHostMalloc(reinterpret_cast<void**>(&L.h_io), L.io_cap, hipHostMallocMapped),
               "ingest: h_io");
     void* dp = nullptr;
@@ -133,7 +136,8 @@ void GpuIngest::run(int lane, const kafka::Fetched& f, uint8_t* dev, size_t dev_
   }
   lo &= ~(size_t)15;
   const size_t span = hi - lo;
-  const size_t o_chunks = 0;
+  const size_t ng = packed ? codec::pack_groups(span) : 0;
+  const size_t o_chunks = align16(ng * 2 * sizeof(uint32_t));  // (the pack group table first)
   const size_t o_groups = o_chunks + align16(nc * sizeof(CrcChunk));
   const size_t o_recs = o_groups + align16((size_t)ngroups * sizeof(int2));
   const size_t o_gsum = o_recs + nr * sizeof(JsonRecord);  // (JsonRecord is 48 bytes)
@@ -170,33 +174,36 @@ void GpuIngest::run(int lane, const kafka::Fetched& f, uint8_t* dev, size_t dev_
     tile += nt;
   }
   // ---- device: text span -> mirror (packed: ONE H2D of the packed stream, expanded in place),
-  // CRC windows, token counts. The bulk copy stays a DMA (SDMA engine, no CU time): expanding
-  // straight from the host-mapped chunk (kernel loads over the link) made text_unpack 15x slower
-  // and device time per batch 0.34 -> 2.9 ms (profiles/r5_ingest_zero_copy_ab.txt). The small
-  // parts go without copies: text_unpack reads the group table from the chunk and
-  // ingest_crc_count reads the plan from / stores its results into the lane's mapped buffer
-  // (r4: two more DMAs per fetch, the plan H2D and the results D2H).
+  // plan H2D, CRC windows, token counts; the kernel stores its results (window CRCs, group sums
+  // and verdicts) straight into the lane's host-mapped buffer, so no D2H copy follows. Both
+  // copies are DMAs (SDMA engines, no CU time). Kernel READS of host memory stay out of this
+  // path: under the serving load the link is busy with these DMAs and every read waits behind
+  // them - expanding the packed text straight from the host-mapped chunk made text_unpack 15x
+  // slower (device time per batch 0.34 -> 2.9 ms), and reading only the plan and the step's
+  // metadata that way still stretched every kernel by 25-40 % (profiles/r5_step_ab.txt).
   hipStream_t st = L.stream;
   size_t link = span;
   if (packed) {
     link = (size_t)f.tap_result;
+    memcpy(L.h_io, f.buf.get() + codec::tab_offset(span), ng * 2 * sizeof(uint32_t));
     const size_t po = codec::pack_offset(span);
     check_hip(hipMemcpyAsync(dev + po, f.buf.get() + po, link, hipMemcpyHostToDevice, st),
               "ingest: H2D packed text");
-    check_hip(text_unpack(dev + po,
-                          reinterpret_cast<const uint32_t*>(f.buf.get() + codec::tab_offset(span)),
-                          (int64_t)span, dev, st),
-              "ingest: text_unpack");
   } else {
     check_hip(hipMemcpyAsync(dev + lo, f.buf.get() + lo, span, hipMemcpyHostToDevice, st),
               "ingest: H2D text");
   }
+  check_hip(hipMemcpyAsync(L.d_io, L.h_io, o_gsum, hipMemcpyHostToDevice, st), "ingest: H2D plan");
+  if (packed)
+    check_hip(text_unpack(dev + codec::pack_offset(span), reinterpret_cast<const uint32_t*>(L.d_io),
+                          (int64_t)span, dev, st),
+              "ingest: text_unpack");
   text_bytes_ += (int64_t)span;
   link_bytes_ += (int64_t)link;
-  uint32_t* d_crc = reinterpret_cast<uint32_t*>(L.h_io + o_crc);
+  uint32_t* d_crc = reinterpret_cast<uint32_t*>(L.h_io + o_crc);   // (host-mapped results)
   int* d_gsum = reinterpret_cast<int*>(L.h_io + o_gsum);
   int* d_gbad = reinterpret_cast<int*>(L.h_io + o_gbad);
-  JsonRecord* d_rec = reinterpret_cast<JsonRecord*>(L.h_io + o_recs);
+  JsonRecord* d_rec = reinterpret_cast<JsonRecord*>(L.d_io + o_recs);
   // the per-tile token counts stay with the fetch buffer: at the end of its device mirror when
   // they fit behind the text (and the packed stream), so the replica that later parses these
   // records reuses them instead of counting again
@@ -211,9 +218,9 @@ void GpuIngest::run(int lane, const kafka::Fetched& f, uint8_t* dev, size_t dev_
     }
   }
   // CRC windows and token counts: one launch, one pass of workgroups over the buffer
-  check_hip(ingest_crc_count(dev, reinterpret_cast<const CrcChunk*>(L.h_io + o_chunks), (int)nc,
+  check_hip(ingest_crc_count(dev, reinterpret_cast<const CrcChunk*>(L.d_io + o_chunks), (int)nc,
                              d_tables_, d_crc, (int)nr, ngroups, d_rec,
-                             reinterpret_cast<const int2*>(L.h_io + o_groups), d_cnt, d_gsum,
+                             reinterpret_cast<const int2*>(L.d_io + o_groups), d_cnt, d_gsum,
                              d_gbad, st),
             "ingest: crc32c + count");
   check_hip(hipEventRecord(L.done, st), "ingest: event");

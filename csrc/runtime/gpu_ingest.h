@@ -32,12 +32,14 @@ class GpuIngest : public Ingest {
     std::mutex mu;
     hipStream_t stream = nullptr;
     hipEvent_t done = nullptr;
-    // one host-mapped pinned buffer, no device image:
-    //   [CrcChunk x nc][int2 group x ng][JsonRecord x nr][group sum i32 x ng][crc u32 x nc]
-    //   [group verdict i32 x ng]
-    // the host writes the plan, ingest_crc_count reads it over the link and stores the results
-    // (group sums and verdicts, window CRCs) back into it; no copies either way
+    // one host-mapped pinned buffer and a device image of its plan part:
+    //   [pack tab u32 x 2 per 2 KiB group][CrcChunk x nc][int2 group x ng][JsonRecord x nr]
+    //   [group sum i32 x ng][crc u32 x nc][group verdict i32 x ng]
+    // the host writes the plan, ONE H2D copies it (up to the group sums) into d_io, and
+    // ingest_crc_count stores the results (group sums and verdicts, window CRCs) straight into
+    // the host buffer: no D2H copy
     uint8_t* h_io = nullptr;
+    uint8_t* d_io = nullptr;
     size_t io_cap = 0;
     int* d_counts = nullptr;  // per-tile token counts (scratch)
     size_t counts_cap = 0;

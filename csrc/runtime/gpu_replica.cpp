@@ -271,6 +271,14 @@ void GpuReplica::submit(Batch& b) {
     s.h_hdr[1] = ntiles;
     s.h_hdr[2] = img;
     hipGraphExec_t g = step_for(s, slot, count_pass);
+    if (gpu_encode_) {
+      // the metadata this batch uses (header, its records, its tile map) as one DMA
+      const size_t rec_bytes = sizeof(JsonRecord) * (size_t)exec_->max_batch();
+      const size_t used = ntiles > 0 ? kMetaHdr + rec_bytes + sizeof(int) * (size_t)ntiles
+                                     : kMetaHdr + sizeof(JsonRecord) * (size_t)nrec;
+      check_hip(hipMemcpyAsync(s.d_hdr, s.h_hdr, used, hipMemcpyHostToDevice, stream_),
+                "H2D step metadata");
+    }
     check_hip(hipGraphLaunch(g, stream_), "hipGraphLaunch(step)");
     b.step_graph = true;
     ++step_batches_;
@@ -322,27 +330,28 @@ hipGraphExec_t GpuReplica::step_for(Slot& s, int slot, bool count_pass) {
   hipGraph_t graph = nullptr;
   hipError_t e = hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal);
   if (e == hipSuccess && gpu_encode_) {
-    // copy-free step: [count] -> parse -> forward -> format (+ verdicts to the host). The
-    // kernels read the header, records and tile map where the host wrote them (host-mapped;
-    // a record and a tile index per parse wave, one count per forward workgroup), and the last
-    // node stores text and verdicts into host-mapped slots. The r4 step also had a metadata
-    // H2D and a status D2H node, each run as a CU blit kernel on this runtime (2 per batch,
-    // 68 us average under the serving load, profiles/r5_ingest_zero_copy_ab.txt).
-    hipError_t c = json_parse_instances(mb, s.tiles_cap, s.h_recs, s.h_tile_rec, s.d_bytes, H_,
+    // kernels-only step: [count] -> parse -> forward -> format (+ verdicts to the host). The
+    // batch's metadata is DMA'd just before the replay (submit(): an SDMA copy of the used part
+    // only), and the last node stores the text and the parse verdicts into host-mapped slots.
+    // The r4 step captured a metadata H2D and a status D2H as graph nodes, which this runtime
+    // runs as CU blit kernels (two per batch, 68 us average under the serving load); reading
+    // the metadata from host memory instead stretched every kernel by 25-40 % under the link's
+    // DMA load (profiles/r5_step_ab.txt).
+    hipError_t c = json_parse_instances(mb, s.tiles_cap, s.d_recs, s.d_tile_rec, s.d_bytes, H_,
                                         W_, C_, s.d_tiles,
                                         static_cast<float*>(exec_->input(slot)), cs, count_pass,
-                                        s.h_hdr + 1, s.d_status);
+                                        s.d_hdr + 1, s.d_status);
     if (c == hipSuccess) {
       try {
-        exec_->launch_device_batch(slot, s.h_hdr + 2, cs);
+        exec_->launch_device_batch(slot, s.d_hdr + 2, cs);
       } catch (const std::exception&) {
         c = hipErrorLaunchFailure;
       }
     }
     if (c == hipSuccess)
-      c = format_floats_java_step(std::max(mb * classes_, mb), s.h_hdr + 2, classes_,
+      c = format_floats_java_step(std::max(mb * classes_, mb), s.d_hdr + 2, classes_,
                                   static_cast<const float*>(exec_->output(slot)), s.h_text,
-                                  s.h_hdr, s.d_status, s.h_status, cs);
+                                  s.d_hdr, s.d_status, s.h_status, cs);
     e = hipStreamEndCapture(cs, &graph);
     if (e == hipSuccess) e = c;
   } else if (e == hipSuccess) {
