@@ -249,7 +249,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("ingest_crc_count",
         [](uintptr_t bytes, uintptr_t chunks, int nchunks, uintptr_t tables, uintptr_t crc_out,
            int nrec, int ngroups, uintptr_t recs, uintptr_t groups, uintptr_t counts,
-           uintptr_t gsum, uintptr_t stream, uintptr_t gbad) {
+           uintptr_t gsum, uintptr_t stream, uintptr_t gbad, uintptr_t packed, uintptr_t tab,
+           uintptr_t text_out) {
           gale::check_hip(
               gale::ingest_crc_count(reinterpret_cast<const uint8_t*>(bytes),
                                      reinterpret_cast<const gale::CrcChunk*>(chunks), nchunks,
@@ -260,13 +261,16 @@ PYBIND11_MODULE(_C, m) {
                                      reinterpret_cast<int*>(counts),
                                      reinterpret_cast<int*>(gsum),
                                      reinterpret_cast<int*>(gbad),
-                                     reinterpret_cast<hipStream_t>(stream)),
+                                     reinterpret_cast<hipStream_t>(stream),
+                                     reinterpret_cast<const uint8_t*>(packed),
+                                     reinterpret_cast<const uint32_t*>(tab),
+                                     reinterpret_cast<uint8_t*>(text_out)),
               "ingest_crc_count");
         },
         py::arg("bytes"), py::arg("chunks"), py::arg("nchunks"), py::arg("tables"),
         py::arg("crc_out"), py::arg("nrec"), py::arg("ngroups"), py::arg("recs"),
         py::arg("groups"), py::arg("counts"), py::arg("gsum"), py::arg("stream"),
-        py::arg("gbad") = 0,
+        py::arg("gbad") = 0, py::arg("packed") = 0, py::arg("tab") = 0, py::arg("text_out") = 0,
         "groups: int32 (record, first tile) pairs, GROUP_TILES tiles each; counts: per record "
         "tile0 + grp0 -> [tile counts][group sums]; gsum: one int per group");
   m.attr("GROUP_TILES") = gale::kGroupTiles;

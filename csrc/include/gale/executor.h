@@ -102,15 +102,19 @@ class Executor {
   // launch_device_batch enqueues the forward of `slot` sized for max_batch images, the count
   // taken from *d_batch when the kernels run - what a captured per-slot step graph replays
   // for every batch size (GpuReplica step graphs).
+  // so (optional): the step outputs the forward kernel writes in its own epilogue (prediction
+  // text, parse verdicts; gale/kernels.h StepOut) - only when step_out_ok()
   bool device_batch_ok() const;
-  void launch_device_batch(int slot, const int* d_batch, hipStream_t stream);
+  bool step_out_ok() const { return device_batch_ok() && spec_.ops.size() == 1; }
+  void launch_device_batch(int slot, const int* d_batch, hipStream_t stream,
+                           const StepOut* so = nullptr);
 
  private:
   void launch_all(int batch, void* const* bufs, hipStream_t stream,
-                  const int* d_batch = nullptr);
+                  const int* d_batch = nullptr, const StepOut* so = nullptr);
   // ops [begin, end) for images [c0, c0 + batch) of the buffers (c0 > 0: a chunk)
   void launch_ops(size_t begin, size_t end, int batch, void* const* bufs, hipStream_t stream,
-                  int c0 = 0, const int* d_batch = nullptr);
+                  int c0 = 0, const int* d_batch = nullptr, const StepOut* so = nullptr);
   int device_;
   PlanSpec spec_;
   std::vector<int> buckets_;

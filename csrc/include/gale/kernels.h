@@ -97,6 +97,18 @@ hipError_t head_pool_dense_softmax(int batch, int HW, int C, int N, const void* 
                                    hipStream_t stream);
 
 // Whole-network CIFAR-10 ResNet-20 (csrc/kernels/resnet20_fused.hip): x fp32 [B,32,32,3] ->
+// The step graph's outputs written by a whole-network forward itself (all null: none): each
+// softmax value also as a Java Float.toString slot (kFloatTextSlot bytes, as format_floats_java)
+// in text, and, by workgroup 0 before anything else, the batch's parse verdicts handed over:
+// status_out[i] = status[i], status[i] = 0 for i < *nrec (status: the parse's device array;
+// text and status_out: host-mapped). The replica's step is then parse -> forward, two nodes.
+struct StepOut {
+  void* text = nullptr;
+  int* status = nullptr;
+  int* status_out = nullptr;
+  const int* nrec = nullptr;
+};
+
 // softmax fp32 [B,10], one workgroup per image with every activation in LDS. w/b: the 19 convs
 // in network order (packed [Npad][Kpad] + folded-BN fp32 bias), fc_w fp32 [10][64].
 // fp8: w are e4m3 codes with per-channel scales ws; s_in / s_out / s_res are the per-tensor
@@ -112,6 +124,7 @@ struct ResNet20Params {
   // non-null: the image count is read from device memory at run time (images <= the `batch`
   // the launch is sized for) - a captured step graph replays one launch for every batch size
   const int* batch_dev;
+  StepOut so;  // (prediction text + verdict hand-off in the epilogue)
 };
 hipError_t resnet20_fused_forward(const ResNet20Params& p, int batch, const float* x, float* out,
                                   hipStream_t stream);
@@ -132,6 +145,7 @@ struct LeNet5Params {
   const float* w5;
   const float* b5;
   const int* batch_dev;  // as ResNet20Params::batch_dev
+  StepOut so;            // as ResNet20Params::so
 };
 hipError_t lenet5_fused_forward(const LeNet5Params& p, int batch, const float* x, float* out,
                                 hipStream_t stream);
@@ -217,10 +231,15 @@ hipError_t crc32c_chunks(const uint8_t* bytes, const CrcChunk* chunks, int n,
 // plain store and leave recs untouched - chunks, recs, groups, crc_out, gsum and gbad may then
 // be host-mapped pinned memory (read and written over the link, no copies); bytes, tables and
 // counts are device memory.
+// packed non-null: the fetch body is the nibble-packed stream `packed` with its group table
+// `tab` (both device memory; csrc/codec/text_pack.h) instead of text at `bytes`: the CRC
+// windows and counting waves expand it in registers and the counting waves store every record's
+// text (its 16-byte-aligned extent) into text_out - text_unpack folded into this launch.
 hipError_t ingest_crc_count(const uint8_t* bytes, const CrcChunk* chunks, int nchunks,
                             const uint32_t* tables, uint32_t* crc_out, int nrec, int ngroups,
                             JsonRecord* recs, const int2* groups, int* counts, int* gsum,
-                            int* gbad, hipStream_t stream);
+                            int* gbad, hipStream_t stream, const uint8_t* packed = nullptr,
+                            const uint32_t* tab = nullptr, uint8_t* text_out = nullptr);
 
 // Expands a nibble-packed span (csrc/codec/text_pack.h: 64-byte blocks, per-2-KiB-group
 // {base offset, packed-block mask} pairs in tab) into out[0, n). out must be 16-byte aligned,

@@ -36,6 +36,7 @@
 #include "crc32c.cuh"
 #include "gale/kernels.h"
 #include "exact_decimal.cuh"
+#include "text_expand.cuh"
 
 namespace gale {
 namespace {
@@ -606,6 +607,38 @@ __device__ __forceinline__ int tile_tokens(const JsonRecord& r, int tl, const ui
   return wave_sum_i(lc);
 }
 
+// tile_tokens over a nibble-packed fetch buffer (the fused GPU ingest): each lane expands its
+// chunks from the packed stream in registers, stores them into the text image at `bytes` (the
+// mirror the parse reads later; tiles of a record are disjoint and cover its 16-byte-aligned
+// extent, so every byte the parse reads is stored exactly once) and counts as tile_tokens.
+__device__ __forceinline__ int tile_tokens_packed(const JsonRecord& r, int tl, uint8_t* bytes,
+                                                  const PackedText& pt, bool* bad) {
+  const int lane = threadIdx.x & 63;
+  const int64_t abeg = r.off & ~(int64_t)15;
+  uint8_t* rb = bytes + abeg;
+  const int beg = (int)(r.off - abeg), end = beg + r.len;
+  const int o = tl * kTile + kLaneBytes * lane;
+  uint4 v[kChunks];
+#pragma unroll
+  for (int i = 0; i < kChunks; ++i) {
+    if (o + 16 * i < end) {
+      v[i] = expand16(pt, abeg + o + 16 * i);
+      *reinterpret_cast<uint4*>(rb + o + 16 * i) = v[i];
+    } else {
+      v[i] = make_uint4(0, 0, 0, 0);
+    }
+  }
+  unsigned prevb = __shfl_up(v[kChunks - 1].w >> 24, 1, 64);
+  if (lane == 0 && o - 1 >= beg) prevb = expand16(pt, abeg + o - 16).w >> 24;  // (another tile's)
+  const bool pd = (o - 1 < beg) || is_delim(prevb);
+  uint32_t st[kChunks], cm[kChunks];
+  token_starts(v, o, beg, end, pd, st, cm, bad);
+  int lc = 0;
+#pragma unroll
+  for (int i = 0; i < kChunks; ++i) lc += __builtin_popcount(st[i]);
+  return wave_sum_i(lc);
+}
+
 // tiles of a record: json_tile_count on the device
 __device__ __forceinline__ int record_tiles(const JsonRecord& r) {
   const int64_t abeg = r.off & ~(int64_t)15;
@@ -636,9 +669,10 @@ __device__ __forceinline__ void count_tile(JsonRecord* recs, const int* tile_rec
 // atomic on the record's status - the plan and the results may then live in host memory (the
 // GPU ingest reads them over the link and writes them back without copies; device atomics on
 // fine-grained host memory are not something to rely on).
+template <bool PACKED>
 __device__ __forceinline__ void count_group(JsonRecord* recs, const int2* groups, int g,
-                                            const uint8_t* bytes, int* counts, int* gsum,
-                                            int* gbad, int* lds8) {
+                                            uint8_t* bytes, const PackedText& pt, int* counts,
+                                            int* gsum, int* gbad, int* lds8) {
   const int wave = threadIdx.x >> 6;
   const int2 gr = groups[g];  // (record, record-relative first tile)
   const JsonRecord r = recs[gr.x];
@@ -647,7 +681,8 @@ __device__ __forceinline__ void count_group(JsonRecord* recs, const int2* groups
   int cnt = 0;
   bool bad = false;
   if (tl < nt) {
-    cnt = tile_tokens(r, tl, bytes, &bad);  // (bad: this lane's bytes)
+    cnt = PACKED ? tile_tokens_packed(r, tl, bytes, pt, &bad)
+                 : tile_tokens(r, tl, bytes, &bad);  // (bad: this lane's bytes)
     if ((threadIdx.x & 63) == 0) counts[r.tile0 + (int)r.grp0 + tl] = cnt;
     if (bad && !gbad) atomicMax(&recs[gr.x].status, 2);
     bad = __ballot(bad) != 0;  // the wave's verdict, for lane 0 below
@@ -680,23 +715,85 @@ __global__ __launch_bounds__(256) void json_count_kernel(JsonRecord* recs, const
   count_tile(recs, tile_rec, t, bytes, counts, status);
 }
 
+// crc::crc_windows over a packed span: a lane's 64-byte piece [wa, wa + 64) is assembled from
+// the (at most five) 16-byte-aligned chunks covering it, expanded in registers, shifted into place
+// (wa % 16 is the same on every lane of a window: pieces are 64 bytes apart, ending at the
+// window's end) and folded as sixteen 32-bit words. Bytes before the window start are zeroed:
+// with a zero initial register, leading zero bytes leave the raw CRC unchanged.
+__device__ __forceinline__ void crc_windows_packed(const PackedText& pt, const CrcChunk* chunks,
+                                                   int n, const uint32_t* T, uint32_t* out,
+                                                   int block, int nblocks) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int c = block * crc::kCrcWaves + wave; c < n; c += nblocks * crc::kCrcWaves) {
+    const CrcChunk ch = chunks[c];
+    const int64_t cs = ch.end - ch.len;
+    const int64_t wa = ch.end - (int64_t)64 * (64 - lane);  // this lane's piece [wa, wa + 64)
+    const int64_t hi = wa + 64;
+    uint32_t crc = 0;
+    if (hi > cs) {
+      const int64_t b16 = wa & ~(int64_t)15;
+      uint32_t w[20];
+#pragma unroll
+      for (int j = 0; j < 5; ++j) {
+        const int64_t p = b16 + 16 * j;
+        const uint4 v = (p < hi && p + 16 > cs) ? expand16(pt, p) : make_uint4(0, 0, 0, 0);
+        w[4 * j] = v.x;
+        w[4 * j + 1] = v.y;
+        w[4 * j + 2] = v.z;
+        w[4 * j + 3] = v.w;
+      }
+      const uint32_t sh = (uint32_t)(wa & 3);
+      uint32_t x[16];
+      switch ((int)((wa & 15) >> 2)) {  // (wave-uniform)
+#define GALE_ALIGN_WORDS(D)                                                       \
+  _Pragma("unroll") for (int t = 0; t < 16; ++t) x[t] =                           \
+      __builtin_amdgcn_alignbyte(w[t + (D) + 1], w[t + (D)], sh);
+        case 0: GALE_ALIGN_WORDS(0) break;
+        case 1: GALE_ALIGN_WORDS(1) break;
+        case 2: GALE_ALIGN_WORDS(2) break;
+        default: GALE_ALIGN_WORDS(3) break;
+#undef GALE_ALIGN_WORDS
+      }
+#pragma unroll
+      for (int t = 0; t < 16; ++t) {
+        const int64_t at = wa + 4 * t;  // word t = bytes [at, at + 4)
+        uint32_t v = x[t];
+        if (at + 4 <= cs) v = 0;
+        else if (at < cs) v &= 0xffffffffu << (8 * (uint32_t)(cs - at));
+        crc = crc::crc_word(T, crc, v);
+      }
+    }
+    crc = crc::gf2_mulmod(crc, T[1024 + lane]);  // over the 64 * (63 - lane) bytes that follow
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) crc ^= __shfl_xor(crc, o, 64);
+    if (lane == 0) out[c] = crc;
+  }
+}
+
 // The ingest pass of a fetch buffer in one launch: CRC window workgroups first (they stage the
 // CRC tables in LDS behind one barrier), then one workgroup per tile group (the branches are
 // uniform per workgroup).
 static_assert(kGroupTiles == kWaves, "one tile group per counting workgroup");
+// PACKED: the buffer's text is the nibble-packed stream pt (the fetch body crossed the link
+// packed); CRC windows and counting waves expand it in registers, and the counting waves store
+// the record text into `bytes` for the parse - the separate text_unpack pass is folded in.
+template <bool PACKED>
 __global__ __launch_bounds__(256) void ingest_crc_count_kernel(
-    const uint8_t* bytes, const CrcChunk* chunks, int nchunks, const uint32_t* tables,
+    uint8_t* bytes, PackedText pt, const CrcChunk* chunks, int nchunks, const uint32_t* tables,
     uint32_t* crc_out, int crc_blocks, JsonRecord* recs, const int2* groups, int ngroups,
     int* counts, int* gsum, int* gbad) {
   __shared__ uint32_t T[crc::kTableWords];
   if ((int)blockIdx.x < crc_blocks) {
     crc::crc_stage_tables(tables, T);
-    crc::crc_windows(bytes, chunks, nchunks, T, crc_out, blockIdx.x, crc_blocks);
+    if (PACKED)
+      crc_windows_packed(pt, chunks, nchunks, T, crc_out, blockIdx.x, crc_blocks);
+    else
+      crc::crc_windows(bytes, chunks, nchunks, T, crc_out, blockIdx.x, crc_blocks);
     return;
   }
   const int g = (int)blockIdx.x - crc_blocks;
   if (g >= ngroups) return;
-  count_group(recs, groups, g, bytes, counts, gsum, gbad, reinterpret_cast<int*>(T));
+  count_group<PACKED>(recs, groups, g, bytes, pt, counts, gsum, gbad, reinterpret_cast<int*>(T));
 }
 
 __global__ __launch_bounds__(256) void json_parse_kernel(JsonRecord* recs, const int* tile_rec,
@@ -845,14 +942,25 @@ int json_tile_count(int64_t off, int32_t len) {
 hipError_t ingest_crc_count(const uint8_t* bytes, const CrcChunk* chunks, int nchunks,
                             const uint32_t* tables, uint32_t* crc_out, int nrec, int ngroups,
                             JsonRecord* recs, const int2* groups, int* counts, int* gsum,
-                            int* gbad, hipStream_t stream) {
+                            int* gbad, hipStream_t stream, const uint8_t* packed,
+                            const uint32_t* tab, uint8_t* text_out) {
   if (nrec <= 0) ngroups = 0;
   int crc_blocks = (nchunks + crc::kCrcWaves - 1) / crc::kCrcWaves;
   if (crc_blocks > 1024) crc_blocks = 1024;  // (windows loop: the table load is amortised)
   if (crc_blocks + ngroups == 0) return hipSuccess;
-  hipLaunchKernelGGL(ingest_crc_count_kernel, dim3(crc_blocks + ngroups), dim3(256), 0, stream,
-                     bytes, chunks, nchunks, tables, crc_out, crc_blocks, recs, groups, ngroups,
-                     counts, gsum, gbad);
+  if (packed) {
+    if (!tab || !text_out || (reinterpret_cast<uintptr_t>(packed) & 7) ||
+        (reinterpret_cast<uintptr_t>(text_out) & 15))
+      return hipErrorInvalidValue;
+    hipLaunchKernelGGL(ingest_crc_count_kernel<true>, dim3(crc_blocks + ngroups), dim3(256), 0,
+                       stream, text_out, PackedText{packed, tab}, chunks, nchunks, tables,
+                       crc_out, crc_blocks, recs, groups, ngroups, counts, gsum, gbad);
+  } else {
+    hipLaunchKernelGGL(ingest_crc_count_kernel<false>, dim3(crc_blocks + ngroups), dim3(256), 0,
+                       stream, const_cast<uint8_t*>(bytes), PackedText{nullptr, nullptr}, chunks,
+                       nchunks, tables, crc_out, crc_blocks, recs, groups, ngroups, counts, gsum,
+                       gbad);
+  }
   return hipGetLastError();
 }
 

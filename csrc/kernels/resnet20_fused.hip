@@ -36,6 +36,7 @@
 // (same rounding points) and are checked against the fp32 / fp8-emulation oracles in tests.
 #include "common.cuh"
 #include "gale/kernels.h"
+#include "java_float.cuh"
 
 namespace gale {
 namespace {
@@ -478,6 +479,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void resnet20_fused_kernel(ResNet2
   };
   const float in_q = F8 ? 1.f / p.s_in[0] : 1.f;  // quantisation of the fp32 network input
 
+  if (p.so.status_out && blockIdx.x == 0) step_verdicts(p.so);  // (the parse is done)
   if (p.batch_dev) batch = min(batch, *p.batch_dev);  // (a captured step graph's batch size)
   for (int img = blockIdx.x; img < batch; img += gridDim.x) {
     __syncthreads();  // the previous image's head is done with R0/R1
@@ -584,7 +586,13 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void resnet20_fused_kernel(ResNet2
         const float mx = wave_max(lane < 10 ? logit : -3.0e38f);
         const float e = lane < 10 ? __expf(logit - mx) : 0.f;
         const float sum = wave_sum(e);
-        if (lane < 10) out[(size_t)img * 10 + lane] = e / sum;
+        if (lane < 10) {
+          const float prob = e / sum;
+          out[(size_t)img * 10 + lane] = prob;
+          // the prediction text in the epilogue (no separate formatting launch per batch)
+          if (p.so.text)
+            static_cast<uint4*>(p.so.text)[(size_t)img * 10 + lane] = java_float_slot(prob);
+        }
       }
     }
   }

@@ -194,10 +194,6 @@ void GpuIngest::run(int lane, const kafka::Fetched& f, uint8_t* dev, size_t dev_
               "ingest: H2D text");
   }
   check_hip(hipMemcpyAsync(L.d_io, L.h_io, o_gsum, hipMemcpyHostToDevice, st), "ingest: H2D plan");
-  if (packed)
-    check_hip(text_unpack(dev + codec::pack_offset(span), reinterpret_cast<const uint32_t*>(L.d_io),
-                          (int64_t)span, dev, st),
-              "ingest: text_unpack");
   text_bytes_ += (int64_t)span;
   link_bytes_ += (int64_t)link;
   uint32_t* d_crc = reinterpret_cast<uint32_t*>(L.h_io + o_crc);   // (host-mapped results)
@@ -217,11 +213,17 @@ void GpuIngest::run(int lane, const kafka::Fetched& f, uint8_t* dev, size_t dev_
       d_cnt = reinterpret_cast<int*>(dev + cnt_base);
     }
   }
-  // CRC windows and token counts: one launch, one pass of workgroups over the buffer
+  // CRC windows and token counts: one launch, one pass of workgroups over the buffer. Packed,
+  // the same launch expands the text: CRC and counting waves read the packed stream, and the
+  // counting waves store each record's text into the mirror for the parse (r4 ran a separate
+  // text_unpack pass over the whole body first: a third of the ingest launches, 16 % of the
+  // GPU's busy time under the serving load, profiles/r5_step_ab.txt)
   check_hip(ingest_crc_count(dev, reinterpret_cast<const CrcChunk*>(L.d_io + o_chunks), (int)nc,
                              d_tables_, d_crc, (int)nr, ngroups, d_rec,
                              reinterpret_cast<const int2*>(L.d_io + o_groups), d_cnt, d_gsum,
-                             d_gbad, st),
+                             d_gbad, st, packed ? dev + codec::pack_offset(span) : nullptr,
+                             packed ? reinterpret_cast<const uint32_t*>(L.d_io) : nullptr,
+                             packed ? dev : nullptr),
             "ingest: crc32c + count");
   check_hip(hipEventRecord(L.done, st), "ingest: event");
   wait(L);

@@ -341,14 +341,22 @@ hipGraphExec_t GpuReplica::step_for(Slot& s, int slot, bool count_pass) {
                                         W_, C_, s.d_tiles,
                                         static_cast<float*>(exec_->input(slot)), cs, count_pass,
                                         s.d_hdr + 1, s.d_status);
+    // a whole-network forward writes the prediction text and hands the verdicts over in its
+    // own epilogue (two nodes per step); other plans end with the formatting kernel
+    const bool fused = exec_->step_out_ok();
+    StepOut so;
+    so.text = s.h_text;
+    so.status = s.d_status;
+    so.status_out = s.h_status;
+    so.nrec = s.d_hdr;
     if (c == hipSuccess) {
       try {
-        exec_->launch_device_batch(slot, s.d_hdr + 2, cs);
+        exec_->launch_device_batch(slot, s.d_hdr + 2, cs, fused ? &so : nullptr);
       } catch (const std::exception&) {
         c = hipErrorLaunchFailure;
       }
     }
-    if (c == hipSuccess)
+    if (c == hipSuccess && !fused)
       c = format_floats_java_step(std::max(mb * classes_, mb), s.d_hdr + 2, classes_,
                                   static_cast<const float*>(exec_->output(slot)), s.h_text,
                                   s.d_hdr, s.d_status, s.h_status, cs);

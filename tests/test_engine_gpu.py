@@ -363,6 +363,79 @@ def test_gpu_fused_ingest_kernel_matches_separate_passes():
         np.testing.assert_array_equal(out.cpu().numpy(), np.concatenate(xs))
 
 
+@pytest.mark.parametrize("tail", [5000, 4097, 61])
+def test_gpu_fused_packed_ingest_matches_plain(tail):
+    """ingest_crc_count over a nibble-packed body (text_unpack folded in): the window CRCs
+    equal crc32c_chunks over the plain text, the count blocks and group sums equal the plain
+    pass's, and every record's 16-byte-aligned extent is stored into the text image (what the
+    parse reads) byte for byte. Random bytes after the records make raw blocks, and the body
+    length leaves a raw partial final block."""
+    import os
+
+    rng = np.random.default_rng(12)
+    G = C.GROUP_TILES
+    H, Wd, Cc = 32, 32, 3
+    xs = [rng.random((n, H, Wd, Cc), dtype=np.float32) for n in (1, 3, 2, 1)]
+    arrays = [array_text(C.encode_instances(x), H, Wd, Cc) for x in xs]
+    raw, recs, total, tiles = stage(arrays)
+    buf = os.urandom(48) + bytes(raw) + os.urandom(tail)
+    recs["off"] += 48
+    recs["tile0"] = np.cumsum([0] + [C.json_tile_count(int(r["off"]), int(r["len"]))
+                                     for r in recs][:-1])
+    tiles = sum(C.json_tile_count(int(r["off"]), int(r["len"])) for r in recs)
+    wins = [(len(buf) - 4096 * k, 4096) for k in range(len(buf) // 4096)][::-1]
+    if len(buf) % 4096:
+        wins = [(len(buf) - 4096 * len(wins), len(buf) % 4096)] + wins
+    wins = [(1000, 900), (2000, 5)] + wins  # unaligned short windows too
+    groups, grp0 = [], []
+    for i, r in enumerate(recs):
+        grp0.append(len(groups))
+        nt = C.json_tile_count(int(r["off"]), int(r["len"]))
+        groups += [(i, t0) for t0 in range(0, nt, G)]
+    recs["pad"] = grp0
+    ch = np.zeros(len(wins), dtype=[("end", "<i8"), ("len", "<i4"), ("pad", "<i4")])
+    for i, (e, ln) in enumerate(wins):
+        ch[i] = (e, ln, 0)
+    packed, tab = C.text_pack(buf)
+    s = torch.cuda.current_stream().cuda_stream
+    tables = torch.tensor(np.array(K.crc32c_device_tables(), dtype=np.uint32).view(np.int32),
+                          device="cuda")
+    dch = torch.from_numpy(ch.view(np.uint8).copy()).cuda()
+    dgrp = torch.tensor(np.array(groups, dtype=np.int32).reshape(-1), device="cuda")
+    dp = torch.frombuffer(bytearray(packed + bytes(64)), dtype=torch.uint8).cuda()
+    dt = torch.from_numpy(tab.astype(np.int64)).to(torch.int32).cuda()
+    out = torch.full((len(buf) + 64,), 0xA5, dtype=torch.uint8, device="cuda")
+    results = {}
+    for mode in ("plain", "packed"):
+        d = torch.frombuffer(bytearray(buf + bytes(64)), dtype=torch.uint8).cuda()
+        drec = torch.from_numpy(recs.view(np.uint8).copy()).cuda()
+        crc = torch.zeros(len(wins), dtype=torch.int32, device="cuda")
+        cnt = torch.full((tiles + len(groups),), -1, dtype=torch.int32, device="cuda")
+        gsum = torch.full((len(groups),), -1, dtype=torch.int32, device="cuda")
+        gbad = torch.full((len(groups),), -1, dtype=torch.int32, device="cuda")
+        kw = dict(gbad=gbad.data_ptr())
+        if mode == "packed":
+            kw.update(packed=dp.data_ptr(), tab=dt.data_ptr(), text_out=out.data_ptr())
+        C.ingest_crc_count(d.data_ptr(), dch.data_ptr(), len(wins), tables.data_ptr(),
+                           crc.data_ptr(), len(recs), len(groups), drec.data_ptr(),
+                           dgrp.data_ptr(), cnt.data_ptr(), gsum.data_ptr(), s, **kw)
+        torch.cuda.synchronize()
+        results[mode] = [t.cpu().numpy() for t in (crc, cnt, gsum, gbad)]
+    for a, b in zip(results["plain"], results["packed"]):
+        np.testing.assert_array_equal(a, b)
+    assert (results["packed"][3] == 0).all()
+    raw_w = results["packed"][0].view(np.uint32)
+    for i, (e, ln) in enumerate(wins):  # (the plain pass's CRCs are right: checked elsewhere)
+        std = int(raw_w[i]) ^ K.crc32c_shift(0xFFFFFFFF, ln) ^ 0xFFFFFFFF
+        assert std == K.crc32c(buf[e - ln:e]), (e, ln)
+    got = out.cpu().numpy()
+    src = np.frombuffer(buf, dtype=np.uint8)
+    for r in recs:
+        a0 = int(r["off"]) & ~15
+        a1 = (int(r["off"]) + int(r["len"]) + 15) & ~15
+        np.testing.assert_array_equal(got[a0:a1], src[a0:a1])
+
+
 def test_gpu_ingest_zero_copy_plan_and_group_verdicts():
     """The engine's zero-copy form of ingest_crc_count: windows, records and groups are read from
     host-mapped pinned memory, CRCs / group sums / group verdicts are stored back into it (no
