@@ -145,6 +145,8 @@ def parse_args(argv=None):
                     help="with --cpus-per-rank N: the slice is N/2 whole physical cores with "
                          "their SMT siblings (what each of 4 ranks owns on a 64-core socket), "
                          "not the N lowest CPU ids")
+    ap.add_argument("--replica-priority", default="normal", choices=["normal", "high"],
+                    help="stream priority of the replicas' step graphs")
     ap.add_argument("--gpu-wait-poll-us", type=int, default=20,
                     help="replica workers sleep-poll batch completion every N us (0 = spin)")
     ap.add_argument("--encode-threads", type=int, default=0,
@@ -748,6 +750,7 @@ def main(argv=None) -> int:
                      replicas=a.replicas_per_gpu * local_gpus,
                      decode_threads=a.decode_threads, slo_p99_ms=a.slo_p99_ms,
                      gpu_wait_poll_us=a.gpu_wait_poll_us, gpu_ingest=a.gpu_ingest, gpu_encode=a.gpu_encode,
+                     replica_priority=a.replica_priority,
                      text_pack=a.text_pack, text_pack_bounce=a.text_pack_bounce,
                      text_pack_window_kb=a.text_pack_window_kb,
                      pinned_fetch_mb=a.pinned_fetch_mb,

@@ -20,7 +20,7 @@ namespace gale {
 
 GpuReplica::GpuReplica(std::shared_ptr<Executor> exec, int H, int W, int C, int classes,
                        bool use_graph, int wait_poll_us, bool gpu_encode, int locality,
-                       bool step_graph)
+                       bool step_graph, bool high_priority)
     : exec_(std::move(exec)), H_(H), W_(W), C_(C), classes_(classes), use_graph_(use_graph),
       wait_poll_us_(wait_poll_us), gpu_encode_(gpu_encode), locality_(locality) {
   step_graph_ = step_graph && use_graph && exec_->device_batch_ok();
@@ -29,7 +29,14 @@ GpuReplica::GpuReplica(std::shared_ptr<Executor> exec, int H, int W, int C, int 
   if (exec_->output_bytes_per_image() != (long long)classes * 4)
     throw std::invalid_argument("GpuReplica: executor output is not fp32 [classes]");
   check_hip(hipSetDevice(exec_->device()), "hipSetDevice");
-  check_hip(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "hipStreamCreate");
+  if (high_priority) {
+    int least = 0, greatest = 0;
+    check_hip(hipDeviceGetStreamPriorityRange(&least, &greatest), "stream priority range");
+    check_hip(hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, greatest),
+              "hipStreamCreateWithPriority");
+  } else {
+    check_hip(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "hipStreamCreate");
+  }
   const int mb = exec_->max_batch();
   slots_.resize((size_t)exec_->slots());
   for (Slot& s : slots_) {

@@ -133,9 +133,11 @@ class GpuReplica : public Replica {
   // parse verdicts, the kernels reading the batch's record / tile / image counts and records from
   // the host-mapped metadata (no copy nodes; without gpu_encode: metadata H2D -> parse -> forward
   // -> probabilities D2H -> status D2H), so one graph per slot serves every batch size
+  // high_priority: the replica's stream at the device's highest stream priority, so its step
+  // kernels are dispatched ahead of the GPU ingest's when both wait for CUs
   GpuReplica(std::shared_ptr<Executor> exec, int H, int W, int C, int classes, bool use_graph,
              int wait_poll_us = 0, bool gpu_encode = false, int locality = -1,
-             bool step_graph = true);
+             bool step_graph = true, bool high_priority = false);
   ~GpuReplica() override;
   std::string name() const override;
   int max_images() const override { return exec_->max_batch(); }

@@ -18,6 +18,7 @@ from dataclasses import dataclass, field, fields
 from typing import Any, Dict, List, Optional
 
 CHOICES = {
+    "replica_priority": ("normal", "high"),
     "sink_mode": ("async", "sync", "fire-and-forget"),
     "start_offset": ("latest", "earliest", "committed"),
     "value_format": ("json", "json-string"),
@@ -130,6 +131,8 @@ class GaleConfig:
                                        # parse, forward, format, status D2H) is ONE replay of a
                                        # per-slot captured hipGraph (else launched op by op)
     gpu_wait_poll_us: int = 20         # > 0: replicas sleep-poll their batch events (0: spin)
+    replica_priority: str = "normal"   # high: replica streams at the top stream priority (their
+                                       # step kernels dispatch ahead of the GPU ingest's)
     gpu_encode: bool = True            # prediction text (Float.toString) formatted on the GPU
     fold_bn: bool = True               # False: standalone BatchNorm kernels (bf16 / fp32)
     stub: bool = False                 # CPU stub replicas (plumbing without a GPU)
