@@ -321,6 +321,19 @@ class Timeline:
                     other[name] = other.get(name, 0.0) + v - prev_th.get(k, 0.0)
             row["other_top"] = {k: round(v / dt, 2) for k, v in
                                 sorted(other.items(), key=lambda kv: -kv[1])[:4] if v > 0}
+            # what the busiest unnamed thread is doing (its current syscall and wait channel):
+            # the HIP / HSA runtime's helper threads carry the process name
+            busiest = max(other.items(), key=lambda kv: kv[1], default=(None, 0.0))[0]
+            if busiest and ":" in busiest:
+                tid = busiest.rsplit(":", 1)[1]
+                probe = {}
+                for f in ("syscall", "wchan"):
+                    try:
+                        with open(f"/proc/self/task/{tid}/{f}") as fh:
+                            probe[f] = fh.read().split()[0] if f == "syscall" else fh.read()
+                    except (OSError, IndexError):
+                        pass
+                row["other_probe"] = probe
             prev_th = th
             if prev_b is not None:
                 b = self.broker.stats()

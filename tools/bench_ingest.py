@@ -96,6 +96,25 @@ def main():
                                crc.data_ptr(), nrec, len(groups), drec.data_ptr(),
                                dgrp.data_ptr(), cnt.data_ptr(), gsum.data_ptr(), s)
 
+        packed, tab = C.text_pack(buf[:n])
+        dp = torch.frombuffer(bytearray(packed + bytes(64)), dtype=torch.uint8).cuda()
+        dt = torch.from_numpy(tab.astype(np.int64)).to(torch.int32).cuda()
+        text = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
+        gbad = torch.zeros(max(1, len(groups)), dtype=torch.int32, device="cuda")
+
+        def ingest_packed():  # the engine's form: the packed body, expansion folded in
+            C.ingest_crc_count(d.data_ptr(), dch.data_ptr(), len(ch), tables.data_ptr(),
+                               crc.data_ptr(), nrec, len(groups), drec.data_ptr(),
+                               dgrp.data_ptr(), cnt.data_ptr(), gsum.data_ptr(), s,
+                               gbad=gbad.data_ptr(), packed=dp.data_ptr(), tab=dt.data_ptr(),
+                               text_out=text.data_ptr())
+
+        def unpack_then_ingest():  # round 4: text_unpack pass, then crc+count on the text
+            C.text_unpack(dp.data_ptr(), dt.data_ptr(), n, text.data_ptr(), s)
+            C.ingest_crc_count(text.data_ptr(), dch.data_ptr(), len(ch), tables.data_ptr(),
+                               crc.data_ptr(), nrec, len(groups), drec.data_ptr(),
+                               dgrp.data_ptr(), cnt.data_ptr(), gsum.data_ptr(), s)
+
         def crc_only():
             C.ingest_crc_count(d.data_ptr(), dch.data_ptr(), len(ch), tables.data_ptr(),
                                crc.data_ptr(), 0, 0, drec.data_ptr(), dgrp.data_ptr(),
@@ -118,8 +137,10 @@ def main():
                                    H, W, Cc, cnt_p.data_ptr(), out.data_ptr(), s,
                                    count_pass=False)
 
-        for kname, fn in (("crc+count", ingest), ("crc", crc_only), ("count+parse", parse),
-                          ("parse(ingest counts)", parse_cnt)):
+        for kname, fn in (("crc+count", ingest), ("crc", crc_only),
+                          ("crc+count+expand(packed)", ingest_packed),
+                          ("unpack;crc+count (r4)", unpack_then_ingest),
+                          ("count+parse", parse), ("parse(ingest counts)", parse_cnt)):
             us = timed(fn, a.iters)
             print(json.dumps(dict(case=name, kernel=kname, records=nrec, text_mb=round(n / 1e6, 2),
                                   us=round(us, 1), gb_s=round(n / us / 1e3, 1))), flush=True)
