@@ -145,6 +145,11 @@ def parse_args(argv=None):
                     help="with --cpus-per-rank N: the slice is N/2 whole physical cores with "
                          "their SMT siblings (what each of 4 ranks owns on a 64-core socket), "
                          "not the N lowest CPU ids")
+    ap.add_argument("--step-launch", default="direct", choices=["graph", "direct"],
+                    help="the per-batch step (parse -> forward, text + verdicts in the forward's "
+                         "epilogue) as direct kernel launches or as one hipGraph replay (the "
+                         "replay kept a HIP runtime helper thread spinning at ~0.8 core: 2.10 vs "
+                         "2.18 M img/s, profiles/r5_ab_step_launch.jsonl)")
     ap.add_argument("--replica-priority", default="normal", choices=["normal", "high"],
                     help="stream priority of the replicas' step graphs")
     ap.add_argument("--gpu-wait-poll-us", type=int, default=20,
@@ -500,8 +505,9 @@ def pipeline_path(a, st) -> str:
     step_g = st.get("graph_step_batches", 0) / batches
     fwd_g = st.get("graph_forward_batches", 0) / batches
     if step_g > 0.5:
-        hops.append("hipgraph-step(json-parse+forward%s+status)" %
-                    ("+format" if a.gpu_encode else ""))
+        hops.append("%s(json-parse+forward%s+status)" %
+                    ("hipgraph-step" if a.step_launch == "graph" else "step", "+format"
+                     if a.gpu_encode else ""))
     else:
         hops.append("gpu-json-parse")
         hops.append("hipgraph-forward" if fwd_g > 0.5 else "forward(direct-launch)")
@@ -763,7 +769,7 @@ def main(argv=None) -> int:
                      replicas=a.replicas_per_gpu * local_gpus,
                      decode_threads=a.decode_threads, slo_p99_ms=a.slo_p99_ms,
                      gpu_wait_poll_us=a.gpu_wait_poll_us, gpu_ingest=a.gpu_ingest, gpu_encode=a.gpu_encode,
-                     replica_priority=a.replica_priority,
+                     replica_priority=a.replica_priority, step_launch=a.step_launch,
                      text_pack=a.text_pack, text_pack_bounce=a.text_pack_bounce,
                      text_pack_window_kb=a.text_pack_window_kb,
                      pinned_fetch_mb=a.pinned_fetch_mb,

@@ -95,16 +95,17 @@ void bind_engine(py::module_& m) {
            py::arg("locality") = -1)
       .def("add_gpu_replica",
            [](Engine& e, std::shared_ptr<Executor> exec, bool use_graph, int wait_poll_us,
-              bool gpu_encode, int locality, bool step_graph, bool high_priority) {
+              bool gpu_encode, int locality, bool step_graph, bool high_priority,
+              bool step_direct) {
              const EngineConfig& c = e.config();
              e.add_replica(std::make_shared<GpuReplica>(std::move(exec), c.H, c.W, c.C,
                                                         c.classes, use_graph, wait_poll_us,
                                                         gpu_encode, locality, step_graph,
-                                                        high_priority));
+                                                        high_priority, step_direct));
            },
            py::arg("executor"), py::arg("use_graph") = true, py::arg("wait_poll_us") = 0,
            py::arg("gpu_encode") = false, py::arg("locality") = -1, py::arg("step_graph") = true,
-           py::arg("high_priority") = false)
+           py::arg("high_priority") = false, py::arg("step_direct") = false)
       .def("enable_gpu_ingest",
            [](Engine& e, int device, int lanes, int poll_us) {
              e.set_ingest(std::make_shared<GpuIngest>(device, lanes, poll_us));

@@ -20,9 +20,10 @@ namespace gale {
 
 GpuReplica::GpuReplica(std::shared_ptr<Executor> exec, int H, int W, int C, int classes,
                        bool use_graph, int wait_poll_us, bool gpu_encode, int locality,
-                       bool step_graph, bool high_priority)
+                       bool step_graph, bool high_priority, bool step_direct)
     : exec_(std::move(exec)), H_(H), W_(W), C_(C), classes_(classes), use_graph_(use_graph),
-      wait_poll_us_(wait_poll_us), gpu_encode_(gpu_encode), locality_(locality) {
+      wait_poll_us_(wait_poll_us), gpu_encode_(gpu_encode), locality_(locality),
+      step_direct_(step_direct) {
   step_graph_ = step_graph && use_graph && exec_->device_batch_ok();
   if (exec_->input_bytes_per_image() != (long long)H * W * C * 4)
     throw std::invalid_argument("GpuReplica: executor input is not fp32 [H, W, C]");
@@ -277,7 +278,7 @@ void GpuReplica::submit(Batch& b) {
     s.h_hdr[0] = nrec;
     s.h_hdr[1] = ntiles;
     s.h_hdr[2] = img;
-    hipGraphExec_t g = step_for(s, slot, count_pass);
+    hipGraphExec_t g = (gpu_encode_ && step_direct_) ? nullptr : step_for(s, slot, count_pass);
     if (gpu_encode_) {
       // the metadata this batch uses (header, its records, its tile map) as one DMA
       const size_t rec_bytes = sizeof(JsonRecord) * (size_t)exec_->max_batch();
@@ -286,7 +287,10 @@ void GpuReplica::submit(Batch& b) {
       check_hip(hipMemcpyAsync(s.d_hdr, s.h_hdr, used, hipMemcpyHostToDevice, stream_),
                 "H2D step metadata");
     }
-    check_hip(hipGraphLaunch(g, stream_), "hipGraphLaunch(step)");
+    if (g)
+      check_hip(hipGraphLaunch(g, stream_), "hipGraphLaunch(step)");
+    else  // (the same kernels launched directly: no graph-launch bookkeeping in the runtime)
+      check_hip(enqueue_step(s, slot, count_pass, stream_), "step launch");
     b.step_graph = true;
     ++step_batches_;
     check_hip(hipEventRecord(s.done, stream_), "hipEventRecord");
@@ -323,6 +327,39 @@ void GpuReplica::submit(Batch& b) {
   s.t_submit_ns = mono_ns();
 }
 
+// The kernels-only step (gpu_encode): [count] -> parse -> forward (+ prediction text and
+// verdicts in its epilogue; other plans end with the formatting kernel). The batch's metadata
+// is DMA'd just before (submit(): an SDMA copy of the used part only), and the kernels read the
+// record / tile / image counts from its header. The r4 step captured a metadata H2D and a status
+// D2H as graph nodes, which this runtime runs as CU blit kernels (two per batch, 68 us average
+// under the serving load); reading the metadata from host memory instead stretched every kernel
+// by 25-40 % under the link's DMA load (profiles/r5_step_ab.txt). Captured once per slot into
+// the step graph, or enqueued directly (step_direct).
+hipError_t GpuReplica::enqueue_step(Slot& s, int slot, bool count_pass, hipStream_t st) {
+  const int mb = exec_->max_batch();
+  hipError_t c = json_parse_instances(mb, s.tiles_cap, s.d_recs, s.d_tile_rec, s.d_bytes, H_, W_,
+                                      C_, s.d_tiles, static_cast<float*>(exec_->input(slot)), st,
+                                      count_pass, s.d_hdr + 1, s.d_status);
+  const bool fused = exec_->step_out_ok();
+  StepOut so;
+  so.text = s.h_text;
+  so.status = s.d_status;
+  so.status_out = s.h_status;
+  so.nrec = s.d_hdr;
+  if (c == hipSuccess) {
+    try {
+      exec_->launch_device_batch(slot, s.d_hdr + 2, st, fused ? &so : nullptr);
+    } catch (const std::exception&) {
+      c = hipErrorLaunchFailure;
+    }
+  }
+  if (c == hipSuccess && !fused)
+    c = format_floats_java_step(std::max(mb * classes_, mb), s.d_hdr + 2, classes_,
+                                static_cast<const float*>(exec_->output(slot)), s.h_text,
+                                s.d_hdr, s.d_status, s.h_status, st);
+  return c;
+}
+
 // The slot's step graph, captured on first use (and after its buffers moved). Sized for the
 // largest batch: the parse covers tiles_cap tiles and the forward max_batch images, their waves
 // past the header's counts exit at once; the status copy-back is max_batch records.
@@ -337,36 +374,7 @@ hipGraphExec_t GpuReplica::step_for(Slot& s, int slot, bool count_pass) {
   hipGraph_t graph = nullptr;
   hipError_t e = hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal);
   if (e == hipSuccess && gpu_encode_) {
-    // kernels-only step: [count] -> parse -> forward -> format (+ verdicts to the host). The
-    // batch's metadata is DMA'd just before the replay (submit(): an SDMA copy of the used part
-    // only), and the last node stores the text and the parse verdicts into host-mapped slots.
-    // The r4 step captured a metadata H2D and a status D2H as graph nodes, which this runtime
-    // runs as CU blit kernels (two per batch, 68 us average under the serving load); reading
-    // the metadata from host memory instead stretched every kernel by 25-40 % under the link's
-    // DMA load (profiles/r5_step_ab.txt).
-    hipError_t c = json_parse_instances(mb, s.tiles_cap, s.d_recs, s.d_tile_rec, s.d_bytes, H_,
-                                        W_, C_, s.d_tiles,
-                                        static_cast<float*>(exec_->input(slot)), cs, count_pass,
-                                        s.d_hdr + 1, s.d_status);
-    // a whole-network forward writes the prediction text and hands the verdicts over in its
-    // own epilogue (two nodes per step); other plans end with the formatting kernel
-    const bool fused = exec_->step_out_ok();
-    StepOut so;
-    so.text = s.h_text;
-    so.status = s.d_status;
-    so.status_out = s.h_status;
-    so.nrec = s.d_hdr;
-    if (c == hipSuccess) {
-      try {
-        exec_->launch_device_batch(slot, s.d_hdr + 2, cs, fused ? &so : nullptr);
-      } catch (const std::exception&) {
-        c = hipErrorLaunchFailure;
-      }
-    }
-    if (c == hipSuccess && !fused)
-      c = format_floats_java_step(std::max(mb * classes_, mb), s.d_hdr + 2, classes_,
-                                  static_cast<const float*>(exec_->output(slot)), s.h_text,
-                                  s.d_hdr, s.d_status, s.h_status, cs);
+    const hipError_t c = enqueue_step(s, slot, count_pass, cs);
     e = hipStreamEndCapture(cs, &graph);
     if (e == hipSuccess) e = c;
   } else if (e == hipSuccess) {

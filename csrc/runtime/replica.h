@@ -137,7 +137,7 @@ class GpuReplica : public Replica {
   // kernels are dispatched ahead of the GPU ingest's when both wait for CUs
   GpuReplica(std::shared_ptr<Executor> exec, int H, int W, int C, int classes, bool use_graph,
              int wait_poll_us = 0, bool gpu_encode = false, int locality = -1,
-             bool step_graph = true, bool high_priority = false);
+             bool step_graph = true, bool high_priority = false, bool step_direct = false);
   ~GpuReplica() override;
   std::string name() const override;
   int max_images() const override { return exec_->max_batch(); }
@@ -182,6 +182,7 @@ class GpuReplica : public Replica {
   void ensure_tiles(Slot& s, int ntiles, int keep);
   void drop_steps(Slot& s);  // (buffers moved: the captured steps point at the old ones)
   hipGraphExec_t step_for(Slot& s, int slot, bool count_pass);
+  hipError_t enqueue_step(Slot& s, int slot, bool count_pass, hipStream_t st);
   static void* mapped_alloc(size_t bytes, const char* what);
   std::shared_ptr<Executor> exec_;
   int H_, W_, C_, classes_;
@@ -200,6 +201,7 @@ class GpuReplica : public Replica {
   std::atomic<int64_t> resident_{0}, host_{0};
   std::atomic<int64_t> step_batches_{0}, fwd_graph_batches_{0};
   bool step_graph_ = false;
+  bool step_direct_ = false;  // the kernels-only step launched directly, not as a graph replay
   int64_t expect_ns_ = 0;  // running average of submit -> done (adaptive sleep-poll)
 };
 

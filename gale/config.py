@@ -19,6 +19,7 @@ from typing import Any, Dict, List, Optional
 
 CHOICES = {
     "replica_priority": ("normal", "high"),
+    "step_launch": ("graph", "direct"),
     "sink_mode": ("async", "sync", "fire-and-forget"),
     "start_offset": ("latest", "earliest", "committed"),
     "value_format": ("json", "json-string"),
@@ -131,6 +132,11 @@ class GaleConfig:
                                        # parse, forward, format, status D2H) is ONE replay of a
                                        # per-slot captured hipGraph (else launched op by op)
     gpu_wait_poll_us: int = 20         # > 0: replicas sleep-poll their batch events (0: spin)
+    step_launch: str = "direct"        # the kernels-only batch step (parse -> forward) launched
+                                       # kernel by kernel ("direct") or as a hipGraph replay
+                                       # ("graph": the runtime's graph-launch bookkeeping kept a
+                                       # helper thread spinning at ~0.8 of a core,
+                                       # profiles/r5_ab_step_launch.jsonl)
     replica_priority: str = "normal"   # high: replica streams at the top stream priority (their
                                        # step kernels dispatch ahead of the GPU ingest's)
     gpu_encode: bool = True            # prediction text (Float.toString) formatted on the GPU

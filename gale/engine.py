@@ -85,7 +85,8 @@ class Engine:
             # Java 8 digits are formatted on the host (the GPU formatter is the JDK 19 rule)
             self._native.add_gpu_replica(rep.executor, cfg.use_graph, cfg.gpu_wait_poll_us,
                                          cfg.gpu_encode and cfg.float_format == "jdk19", loc,
-                                         cfg.graph_step, cfg.replica_priority == "high")
+                                         cfg.graph_step, cfg.replica_priority == "high",
+                                         cfg.step_launch == "direct")
             self.model_replicas.append(rep)
             self.devices.append(dev)
         if cfg.gpu_ingest:
