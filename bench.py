@@ -136,11 +136,13 @@ def parse_args(argv=None):
                          "16-CPU-quota box, 3 interleaved runs each: whole node 2.08 M img/s, "
                          "16 physical cores 1.83 M (88 %%), 16 cores + SMT siblings 1.78 M "
                          "(85 %%; profiles/r5_slices_ab.jsonl)")
-    ap.add_argument("--rank-slices", action=argparse.BooleanOptionalAction, default=True,
+    ap.add_argument("--rank-slices", action=argparse.BooleanOptionalAction, default=False,
                     help="N > 1 with --cpus-per-rank 0: each rank gets a disjoint slice of its "
                          "GPU's NUMA node (the node's CPUs split evenly among the ranks on it, "
                          "whole cores with their SMT siblings: 16 + 16 per rank with 4 GPUs per "
-                         "64-core socket) instead of every rank floating over the whole node")
+                         "64-core socket) instead of every rank floating over the whole node. "
+                         "Off by default: the 2-rank rehearsal on one box ran 3.6 %% slower with "
+                         "slices (profiles/r5_rehearsal_world2_slices.jsonl), so no win is shown")
     ap.add_argument("--slice-smt", action="store_true",
                     help="with --cpus-per-rank N: the slice is N/2 whole physical cores with "
                          "their SMT siblings (what each of 4 ranks owns on a 64-core socket), "
