@@ -102,7 +102,7 @@ def parse_args(argv=None):
                     help="sources nibble-pack the fetched JSON text for the host->GPU link "
                          "through a cache-resident receive window (expanded on the device; needs "
                          "AVX-512 VBMI): half the link and pinned-memory bytes, "
-                         "profiles/r4_ab_step_graph_text_pack.jsonl")
+                         "profiles/archive/r4_ab_step_graph_text_pack.jsonl")
     ap.add_argument("--pack-nt", action=argparse.BooleanOptionalAction, default=True,
                     help="the sources write the packed text with non-temporal stores (no "
                          "read-for-ownership of the pinned destination lines, the receive window "
@@ -602,9 +602,9 @@ def size_pipeline(a, cpus: float) -> None:
             # fewer threads than 12 contend less at the 16-CPU quota (10: 1.99 vs 1.81 M img/s
             # over 3 interleaved pairs; 9 / 10 / 11: 2.15 / 2.08 / 1.99 M). Below 11 the latency
             # phase, at 0.8 x the higher rate, runs into loopback retransmissions (p99 8-37 ms
-            # in some runs against 0.9-1.0 ms with 11; profiles/r4_ab_partitions.jsonl). A larger
+            # in some runs against 0.9-1.0 ms with 11; profiles/archive/r4_ab_partitions.jsonl). A larger
             # CPU share per rank (an 8-GPU node without a per-job quota) keeps 12, and so does
-            # LeNet-5 (p99 6-112 ms with 10, profiles/r4_ab_lenet_partitions.jsonl)
+            # LeNet-5 (p99 6-112 ms with 10, profiles/archive/r4_ab_lenet_partitions.jsonl)
             a.partitions = (11 if cpus < 24 and a.model != "lenet5" else 12) if big \
                 else a.replicas_per_gpu
     if a.decode_threads <= 0:

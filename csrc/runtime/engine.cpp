@@ -308,7 +308,7 @@ void Engine::start() {
     // a packed chunk holds the body's layout twice over (text region + packed stream): the same
     // number of fetches in flight needs twice the budget - with the round-3 budget ResNet-50's
     // 1.7 MB records ran the pool dry and 77 % of them fell back to heap buffers (host staging,
-    // 21.6 vs 31.3 k img/s, profiles/r4_ab_resnet50_lenet_sink.jsonl)
+    // 21.6 vs 31.3 k img/s, profiles/archive/r4_ab_resnet50_lenet_sink.jsonl)
     const size_t budget = (size_t)cfg_.pinned_fetch_bytes * (pack ? 2 : 1) / nslots;
     pools_[i] = std::make_shared<PinnedPool>(pack ? codec::pack_layout_bytes(body) + 4096 : body,
                                              budget);
@@ -659,7 +659,7 @@ void Engine::source_loop(int idx) {
   const bool bounce = packing && cfg_.text_pack_bounce && cfg_.decode_threads > 0;
   const size_t window = (size_t)std::max(4, cfg_.text_pack_window_kb) << 10;
   // recv_lowat < 0 (auto): with the bounce receive, wake per window of a large response instead
-  // of per segment (+6 % img/s in 5 of 5 interleaved pairs, profiles/r4_ab_recv_lowat.jsonl)
+  // of per segment (+6 % img/s in 5 of 5 interleaved pairs, profiles/archive/r4_ab_recv_lowat.jsonl)
   cc.recv_lowat = cfg_.recv_lowat >= 0 ? cfg_.recv_lowat : bounce ? (int)window : 0;
   // with decode workers the CRC32C check moves off this thread (decode_fetch)
   cc.check_crcs = cfg_.check_crcs && cfg_.decode_threads <= 0;

@@ -23,7 +23,7 @@ GpuIngest::GpuIngest(int device, int lanes, int poll_us)
             "ingest: tables H2D");
   // (ingest lanes at the highest stream priority were measured and dropped: the replicas' batch
   // kernels then queue behind every fetch's ingest, ResNet-20 device time per batch 0.4 -> 2 ms,
-  // profiles/r4_ab_ingest_priority.jsonl)
+  // profiles/archive/r4_ab_ingest_priority.jsonl)
   for (int i = 0; i < std::max(1, lanes); ++i) {
     auto L = std::make_unique<Lane>();
     check_hip(hipStreamCreateWithFlags(&L->stream, hipStreamNonBlocking), "ingest: stream");

@@ -683,7 +683,7 @@ def test_gpu_pinned_pool_backpressure(broker):
     """A pinned-fetch budget of two buffers: when both are held by queued records the sources
     wait for one to be released instead of staging fetches through the heap (which would send
     those records down the host path and, under load, keep the pool exhausted - the ResNet-50
-    regression of profiles/r4_ab_resnet50_lenet_sink.jsonl). Every record is still served by GPU
+    regression of profiles/archive/r4_ab_resnet50_lenet_sink.jsonl). Every record is still served by GPU
     ingest, correctly."""
     if not C.text_pack_fast():
         pytest.skip("no AVX-512 VBMI on this host")
