@@ -141,6 +141,25 @@ PYBIND11_MODULE(_C, m) {
         },
         py::arg("desc"), py::arg("batch"), py::arg("x"), py::arg("w"), py::arg("bias"),
         py::arg("wscale"), py::arg("res"), py::arg("y"), py::arg("stream"));
+  m.def("bottleneck56",
+        [](int batch, uintptr_t x, uintptr_t w1, uintptr_t b1, uintptr_t w2, uintptr_t b2,
+           uintptr_t w3, uintptr_t b3, uintptr_t wd, uintptr_t bd, uintptr_t y, int cin,
+           int down, uintptr_t stream) {
+          gale::BottleneckParams bp;
+          bp.w1 = P(w1); bp.w2 = P(w2); bp.w3 = P(w3); bp.wd = P(wd);
+          bp.b1 = static_cast<const float*>(P(b1));
+          bp.b2 = static_cast<const float*>(P(b2));
+          bp.b3 = static_cast<const float*>(P(b3));
+          bp.bd = static_cast<const float*>(P(bd));
+          bp.cin = cin;
+          bp.down = down;
+          chk(gale::bottleneck56(bp, batch, P(x), P(y), S(stream)), "bottleneck56");
+        },
+        py::arg("batch"), py::arg("x"), py::arg("w1"), py::arg("b1"), py::arg("w2"),
+        py::arg("b2"), py::arg("w3"), py::arg("b3"), py::arg("wd"), py::arg("bd"), py::arg("y"),
+        py::arg("cin"), py::arg("down"), py::arg("stream"));
+  m.def("bottleneck56_supported", &gale::bottleneck56_supported, py::arg("H"), py::arg("W"),
+        py::arg("cin"), py::arg("cmid"), py::arg("cout"), py::arg("down"));
   m.def("stem_pack",
         [](int batch, int H, int W, int C, int Wp, int lp, uintptr_t x, uintptr_t y,
            uintptr_t stream) {

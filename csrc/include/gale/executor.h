@@ -30,6 +30,8 @@ enum OpKind : int {
   OP_BN_ACT = 7,    // p[0..7] = HW, Wo, C, relu, res_H, res_W, res_C, res_stride; w = BN scale,
                     // bias = BN shift (unfolded-BN plan: standalone BatchNorm + add + ReLU)
   OP_LENET5 = 8,    // whole-network fused MNIST LeNet-5; ptrs = w1 b1 w2 b2 w3 b3 w4 b4 w5 b5
+  OP_BOTTLENECK = 9,  // one whole ResNet-50 56x56 bottleneck (bottleneck56); ptrs = w1 b1 w2 b2
+                      // w3 b3 [wd bd]; p[0] = cin, p[1] = down (projection shortcut)
 };
 
 // Buffer ids: 0 = network input (fp32 NHWC), 1 = network output (fp32 [B, classes]),

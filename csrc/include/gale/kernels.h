@@ -75,6 +75,26 @@ void set_conv_patch(int mode);
 hipError_t conv2d_patch(const ConvDesc& d, int batch, const void* x, const void* w,
                         const float* bias, const void* res, void* y, hipStream_t stream);
 
+// One whole ResNet-50 56x56 bottleneck per launch (bottleneck_fused.hip), bf16 NHWC:
+// y = relu(conv3(relu(conv2(relu(conv1(x))))) + shortcut), shortcut = x (cin 256) or, with
+// down = 1 (block 0, cin 64), the 1x1 projection bf16(wd . x + bd). Packed weights as conv2d's:
+// w1 [64][cin], w2 [64][576], w3 / wd [256][64]; biases fp32 with BatchNorm folded in.
+struct BottleneckParams {
+  const void* w1 = nullptr;
+  const void* w2 = nullptr;
+  const void* w3 = nullptr;
+  const void* wd = nullptr;
+  const float* b1 = nullptr;
+  const float* b2 = nullptr;
+  const float* b3 = nullptr;
+  const float* bd = nullptr;
+  int cin = 256;
+  int down = 0;
+};
+bool bottleneck56_supported(int H, int W, int cin, int cmid, int cout, int down);
+hipError_t bottleneck56(const BottleneckParams& p, int batch, const void* x, void* y,
+                        hipStream_t stream);
+
 // fp32 NHWC [B][H][W][C<=4] -> bf16 [B][H][Wp][4] with `lp` zero columns on the left (and zeros
 // up to Wp on the right, channels >= C zero): the input of a packed-stem conv (ConvDesc::stem).
 hipError_t stem_pack(int batch, int H, int W, int C, int Wp, int lp, const float* x, void* y,

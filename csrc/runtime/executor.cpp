@@ -183,6 +183,26 @@ void Executor::launch_ops(size_t begin, size_t end, int batch, void* const* bufs
                                  static_cast<float*>(out), stream);
         break;
       }
+      case OP_BOTTLENECK: {
+        const bool down = op.p[1] != 0;
+        if (op.ptrs.size() != (down ? 8u : 6u))
+          throw std::invalid_argument("bottleneck op: bad pointer count");
+        BottleneckParams bp;
+        bp.w1 = op.ptrs[0];
+        bp.b1 = static_cast<const float*>(op.ptrs[1]);
+        bp.w2 = op.ptrs[2];
+        bp.b2 = static_cast<const float*>(op.ptrs[3]);
+        bp.w3 = op.ptrs[4];
+        bp.b3 = static_cast<const float*>(op.ptrs[5]);
+        if (down) {
+          bp.wd = op.ptrs[6];
+          bp.bd = static_cast<const float*>(op.ptrs[7]);
+        }
+        bp.cin = op.p[0];
+        bp.down = down ? 1 : 0;
+        e = bottleneck56(bp, batch, in, out, stream);
+        break;
+      }
       default:
         throw std::invalid_argument("unknown plan op kind");
     }

@@ -15,6 +15,7 @@ whose only pinned contract is ``input:0`` (NHWC float) -> ``output/Softmax:0`` (
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Tuple, Union
 
@@ -392,7 +393,7 @@ def act_scales_from_packed(net: Network, packed: torch.Tensor) -> Dict[str, floa
 # --------------------------------------------------------------------------------------------
 
 (OP_CONV, OP_MAXPOOL, OP_AVGPOOL, OP_HEAD, OP_SOFTMAX, OP_RESNET20, OP_STEM_PACK, OP_BN_ACT,
- OP_LENET5) = range(9)
+ OP_LENET5, OP_BOTTLENECK) = range(10)
 
 
 def is_cifar_resnet20(net: Network) -> bool:
@@ -447,10 +448,69 @@ def _tensor_bytes(net: Network, name: str, wdtype: str = "bf16") -> int:
     return h * w * stored_channels(c) * {"fp8": 1, "bf16": 2, "fp32": 4}[wdtype]
 
 
+def _is_conv(op: dict, kh: int, cin: int, cout: int, relu: int, res: bool, hw: int = 56) -> bool:
+    if op["kind"] != OP_CONV:
+        return False
+    d = op["conv"]
+    return (d["KH"] == kh and d["KW"] == kh and d["stride"] == 1 and d["H"] == hw
+            and d["W"] == hw and d["Cin"] == cin and d["Cout"] == cout and d["Npad"] == cout
+            and d["relu"] == relu and bool(d.get("has_res", 0)) == res
+            and not d.get("stem") and not d.get("fp8") and not d.get("f32")
+            and not d.get("in_f32") and not d.get("out_f32")
+            and (kh == 1 or d["pad"] == 1))
+
+
+def fuse_bottlenecks(ops: List[dict]) -> List[dict]:
+    """Replace every ResNet-50 56x56 bottleneck of a bf16 plan - conv1 / conv2 / conv3 (+ the
+    block-0 projection before them) - by ONE ``OP_BOTTLENECK`` (csrc/kernels/bottleneck_fused.hip:
+    the 64-channel intermediates stay in LDS). A chain is fused only when its intermediate
+    tensors are read by nothing after it."""
+    def live_after(k: int, buf: int) -> bool:
+        # buffers are reused by liveness: the tensor in `buf` is live at op k when an op from k
+        # on reads `buf` before one overwrites it
+        for o in ops[k:]:
+            if o.get("in") == buf or o.get("res", -1) == buf:
+                return True
+            if o.get("out") == buf:
+                return False
+        return False
+
+    out: List[dict] = []
+    i = 0
+    while i < len(ops):
+        down = None
+        j = i
+        if (i + 3 < len(ops) and _is_conv(ops[i], 1, 64, 256, 0, False)
+                and _is_conv(ops[i + 1], 1, 64, 64, 1, False) and ops[i + 1]["in"] == ops[i]["in"]):
+            down, j = ops[i], i + 1
+        if (j + 2 < len(ops) and (down is not None or _is_conv(ops[j], 1, 256, 64, 1, False))
+                and _is_conv(ops[j + 1], 3, 64, 64, 1, False)
+                and _is_conv(ops[j + 2], 1, 64, 256, 1, True)
+                and ops[j + 1]["in"] == ops[j]["out"] and ops[j + 2]["in"] == ops[j + 1]["out"]
+                and ops[j + 2]["conv"].get("res_stride", 1) == 1
+                and ops[j + 2]["res"] == (down["out"] if down is not None else ops[j]["in"])
+                and ops[j + 2]["out"] != ops[j]["in"]
+                and not live_after(j + 2, ops[j]["out"]) and not live_after(j + 3, ops[j + 1]["out"])
+                and (down is None or not live_after(j + 3, down["out"]))):
+            c1, c2, c3 = ops[j], ops[j + 1], ops[j + 2]
+            ptrs = [c1["w"], c1["bias"], c2["w"], c2["bias"], c3["w"], c3["bias"]]
+            if down is not None:
+                ptrs += [down["w"], down["bias"]]
+            out.append(dict(kind=OP_BOTTLENECK, **{"in": c1["in"]}, out=c3["out"], res=-1,
+                            p=[c1["conv"]["Cin"], int(down is not None)], ptrs=ptrs,
+                            bpi=[c1["bpi"][0], c3["bpi"][1], 0], layer=c3.get("layer", 0)))
+            i = j + 3
+            continue
+        out.append(ops[i])
+        i += 1
+    return out
+
+
 def build_plan(net: Network, base_ptr: int, wdtype: str = "bf16",
                act_scales: Optional[Dict[str, float]] = None,
                fused: bool = True, fold_bn: bool = True,
-               chunk_layers: int = 0) -> Tuple[List[dict], List[int]]:
+               chunk_layers: int = 0,
+               fuse_blocks: Optional[bool] = None) -> Tuple[List[dict], List[int]]:
     """Executor plan for a packed parameter buffer living at device address ``base_ptr``.
 
     Returns (ops, buf_bytes_per_image). Buffer 0 = fp32 input, 1 = fp32 softmax output, >= 2 =
@@ -460,6 +520,8 @@ def build_plan(net: Network, base_ptr: int, wdtype: str = "bf16",
     math) become ONE whole-network kernel each (activations resident in LDS). ``fold_bn=False`` (bf16, layer-wise; the buffer from ``pack_params(...,
     fold_bn=False)``): every BatchNorm conv is followed by a standalone ``bn_act`` kernel that
     applies the BN affine, the residual and the ReLU in place (the debugging / parity plan).
+    ``fuse_blocks`` (bf16, folded BN, no chunking; default on, ``GALE_FUSE_BLOCKS=0`` off): the
+    ResNet-50 56x56 bottlenecks run as one kernel each (``fuse_bottlenecks``).
     ``chunk_layers``: the first ``chunk_layers`` layers may run per batch chunk (the executor's
     PlanSpec::chunk_ops; every op carries ``layer``, its layer index): each tensor they produce
     that is still read after them gets a buffer of its own, so a later chunk cannot overwrite an
@@ -596,4 +658,8 @@ def build_plan(net: Network, base_ptr: int, wdtype: str = "bf16",
             if lu == i and t in buf_of and buf_of[t] >= 2:
                 free.append(buf_of[t])
                 del last_use[t]
+    if fuse_blocks is None:
+        fuse_blocks = os.environ.get("GALE_FUSE_BLOCKS", "1") != "0"
+    if fuse_blocks and fused and wdtype == "bf16" and fold_bn and chunk_layers == 0:
+        ops = fuse_bottlenecks(ops)
     return ops, buf_bytes

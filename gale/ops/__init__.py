@@ -80,6 +80,43 @@ def conv2d(x: torch.Tensor, w_packed: torch.Tensor, bias: torch.Tensor, geom: di
     return y
 
 
+def bottleneck56(x: torch.Tensor, w1: torch.Tensor, b1: torch.Tensor, w2: torch.Tensor,
+                 b2: torch.Tensor, w3: torch.Tensor, b3: torch.Tensor,
+                 wd: Optional[torch.Tensor] = None,
+                 bd: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """One whole ResNet-50 56x56 bottleneck in one kernel (bottleneck_fused.hip).
+
+    x: [B,56,56,256] bf16 (identity shortcut) or [B,56,56,64] with the projection (wd, bd) of
+    block 0. Weights packed by ``pack_conv`` (w1 1x1 -> 64, w2 3x3 64 -> 64, w3 / wd 1x1 -> 256).
+    Returns relu(conv3(relu(conv2(relu(conv1(x))))) + shortcut), bf16 [B,56,56,256].
+    """
+    B, H, W, C = x.shape
+    down = wd is not None
+    if not native().bottleneck56_supported(H, W, C, 64, 256, int(down)):
+        raise ValueError(f"bottleneck56: unsupported input {tuple(x.shape)} (down={down})")
+    _check(x, torch.bfloat16, "x")
+    shapes = {"w1": (w1, (64, C)), "w2": (w2, (64, 576)), "w3": (w3, (256, 64))}
+    if down:
+        if bd is None:
+            raise ValueError("bottleneck56: wd needs bd")
+        shapes["wd"] = (wd, (256, 64))
+    for name, (t, shp) in shapes.items():
+        _check(t, torch.bfloat16, name)
+        if tuple(t.shape) != shp:
+            raise ValueError(f"bottleneck56: {name} must be {shp}, got {tuple(t.shape)}")
+    for name, t, n in (("b1", b1, 64), ("b2", b2, 64), ("b3", b3, 256)) + \
+            ((("bd", bd, 256),) if down else ()):
+        _check(t, torch.float32, name)
+        if t.numel() != n:
+            raise ValueError(f"bottleneck56: {name} must have {n} entries")
+    y = torch.empty(B, H, W, 256, device=x.device, dtype=torch.bfloat16)
+    native().bottleneck56(B, x.data_ptr(), w1.data_ptr(), b1.data_ptr(), w2.data_ptr(),
+                          b2.data_ptr(), w3.data_ptr(), b3.data_ptr(),
+                          wd.data_ptr() if down else 0, bd.data_ptr() if down else 0,
+                          y.data_ptr(), C, int(down), _stream())
+    return y
+
+
 def maxpool2d(x: torch.Tensor, k: int, s: int, p: int = 0) -> torch.Tensor:
     _check(x, torch.bfloat16, "x")
     B, H, W, C = x.shape

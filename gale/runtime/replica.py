@@ -19,7 +19,7 @@ class ModelReplica:
     def __init__(self, net: Network, packed: torch.Tensor, max_batch: int = 256, slots: int = 2,
                  buckets: Optional[Sequence[int]] = None, wdtype: str = "bf16",
                  fused: bool = True, fold_bn: bool = True,
-                 chunk: Optional[Tuple[int, int]] = None):
+                 chunk: Optional[Tuple[int, int]] = None, fuse_blocks: Optional[bool] = None):
         if not packed.is_cuda:
             raise RuntimeError("ModelReplica needs the packed weights on a GPU")
         self.net = net
@@ -31,7 +31,8 @@ class ModelReplica:
         # (PlanSpec::chunk_ops, executor.h), the rest over the whole batch
         cl, ci = chunk if chunk is not None else (0, 0)
         ops, buf_bytes = build_plan(net, packed.data_ptr(), wdtype, self.act_scales, fused=fused,
-                                    fold_bn=fold_bn, chunk_layers=cl if ci > 0 else 0)
+                                    fold_bn=fold_bn, chunk_layers=cl if ci > 0 else 0,
+                                    fuse_blocks=fuse_blocks)
         co = sum(1 for op in ops if op.get("layer", len(net.layers)) < cl) if ci > 0 else 0
         self.ops = ops
         self.buf_bytes = buf_bytes

@@ -182,3 +182,33 @@ def test_chunked_plan_keeps_live_out_tensors(end):
         plain, _ = build_plan(net, 0)
         with pytest.raises(AssertionError):
             _simulate_chunked(plain, n, batch=7, chunk=3)
+
+
+def test_resnet50_plan_fuses_56x56_bottlenecks():
+    """fuse_bottlenecks: the three 56x56 blocks (block 0 with its projection) become one
+    OP_BOTTLENECK each, wired from the block input to the block output buffer; other stages,
+    fp8 and the unfused switch keep the layered ops."""
+    from gale.models.graph import OP_BOTTLENECK, OP_CONV
+
+    net = get_model("resnet50")
+    layered, bufs = build_plan(net, 1 << 20, fuse_blocks=False)
+    fused, bufs2 = build_plan(net, 1 << 20, fuse_blocks=True)
+    assert bufs == bufs2
+    bn = [op for op in fused if op["kind"] == OP_BOTTLENECK]
+    assert [op["p"][:2] for op in bn] == [[64, 1], [256, 0], [256, 0]]
+    assert len(fused) == len(layered) - 4 - 3 - 3 + 3
+    # block 0 reads the max-pool output and writes what l1.1 reads; each block feeds the next
+    assert bn[0]["in"] == layered[2]["out"]  # stem_pack, stem, maxpool -> p0
+    assert bn[1]["in"] == bn[0]["out"] and bn[2]["in"] == bn[1]["out"]
+    assert all(op["in"] != op["out"] for op in bn)
+    nxt = fused[fused.index(bn[2]) + 1]
+    assert nxt["kind"] == OP_CONV and nxt["in"] == bn[2]["out"]  # l2.0.down reads l1's output
+    assert len(bn[0]["ptrs"]) == 8 and len(bn[1]["ptrs"]) == 6
+    # pointers are the layered convs' own packed weights / biases
+    l1 = [op for op in layered[3:13]]
+    assert bn[0]["ptrs"][:6] == [l1[1]["w"], l1[1]["bias"], l1[2]["w"], l1[2]["bias"],
+                                 l1[3]["w"], l1[3]["bias"]]
+    assert bn[0]["ptrs"][6:] == [l1[0]["w"], l1[0]["bias"]]
+    # other models / dtypes untouched
+    r20 = build_plan(get_model("resnet20"), 1 << 20, fused=False, fuse_blocks=True)[0]
+    assert not any(op["kind"] == OP_BOTTLENECK for op in r20)

@@ -34,6 +34,9 @@ def main():
     ap.add_argument("--chunk", default="",
                     help="LAYER:N - layers before LAYER run per chunk of N images "
                          "(PlanSpec::chunk_ops)")
+    ap.add_argument("--no-fuse-blocks", action="store_true",
+                    help="run the ResNet-50 56x56 bottlenecks layer by layer (A/B of "
+                         "bottleneck_fused.hip)")
     a = ap.parse_args()
     from gale._native import native
     native().set_conv_path(a.conv_path)
@@ -47,7 +50,7 @@ def main():
         chunk = ([L.name for L in net.layers].index(name), int(n))
     ns = max(1, a.streams)
     rep = ModelReplica(net, packed, max_batch=max(bs), slots=ns, buckets=bs, wdtype=a.dtype,
-                       chunk=chunk)
+                       chunk=chunk, fuse_blocks=not a.no_fuse_blocks)
     streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(ns - 1)]
     ss = [st.cuda_stream for st in streams]
     res = []
@@ -65,7 +68,7 @@ def main():
         flops = 2 * net.macs_per_image() * b
         r = dict(model=a.model, dtype=a.dtype, conv_path=a.conv_path, batch=b, ms=dt * 1e3,
                  img_s=b / dt, tflops=flops / dt / 1e12, graph=not a.eager, chunk=a.chunk,
-                 streams=ns)
+                 streams=ns, fuse_blocks=not a.no_fuse_blocks)
         res.append(r)
         print(json.dumps(r), flush=True)
 
