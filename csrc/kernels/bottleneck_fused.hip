@@ -16,11 +16,12 @@
 //       later H2, conv2's output for the TR x W tile (same rows, so no extra space);
 //   W2: the nine 64 x 64 conv2 taps (LDS-DMA at the start, landing during phase 1); later W3
 //       (and Wd, the block-0 projection) for phase 3.
-// Every 128-B LDS row stores its 16-B chunk c at slot c ^ ((row >> 1) & 7): 16 lanes reading one
-// chunk of 16 consecutive rows hit 16 distinct 4-bank groups (as conv_gemm / conv_patch).
+// Every 128-B LDS row stores its 16-B chunk c at slot c ^ rkey(row) (see rkey): 16 lanes reading
+// 16 consecutive rows hit 16 distinct 4-bank groups.
 //   phase 1: conv1 on the 10 x 56 halo pixels: per wave up to 5 tiles of 16 pixels x all 64
-//            channels; the input fragments (the only HBM stream) and conv1's weights (L2) are
-//            loaded straight into registers, one k-step ahead; bias + ReLU -> bf16 -> H1.
+//            channels; the input fragments (the only HBM stream; 4 k-steps ahead) and conv1's
+//            weights (L2; 1 step ahead) are loaded straight into registers; bias + ReLU -> bf16
+//            -> H1.
 //   phase 2: conv2 from H1 (taps = shifted patch rows) x W2, 4 x 2 waves of 112 pixels x 32
 //            channels; the residual (or block-0 input) fragments of phase 3 are issued first so
 //            their HBM latency hides under the MFMAs; bias + ReLU -> bf16 -> H2 over H1.
@@ -71,8 +72,13 @@ struct BneckArgs {
   int dbg;         // timing experiments only (GALE_BNECK_DBG): bits skip work, output invalid
 };
 
+// XOR key of 128-B LDS row `row`: even values only, so a ds_read_b128 lane group - which mixes
+// chunks c and c ^ 1 (fq = 0 / 1 lanes) - never has two lanes on one 4-bank group for ANY 16
+// consecutive rows, not just 16-aligned ones: the conv2 taps read the patch at row offsets
+// +1 / +2 (bank model: 6.9 -> 4.6 LDS cycles per fragment read, 4 = conflict-free)
+__device__ __forceinline__ int rkey(int row) { return ((row >> 1) & 3) << 1; }
 // byte offset of 16-B chunk c of 128-B LDS row `row`
-__device__ __forceinline__ int swz(int row, int c) { return row * 128 + ((c ^ ((row >> 1) & 7)) << 4); }
+__device__ __forceinline__ int swz(int row, int c) { return row * 128 + ((c ^ rkey(row)) << 4); }
 
 __device__ __forceinline__ bf16x8 lds16(const uint8_t* lds, int off) {
   return *reinterpret_cast<const bf16x8*>(lds + off);
@@ -100,7 +106,7 @@ __global__ __launch_bounds__(512, 1) void bottleneck56_kernel(BneckArgs a) {
     const int wi = wave * 9 + j;
     const int rg = wi * 8 + (lane >> 3);  // tap * 64 + output channel
     const int tap = rg >> 6, row = rg & 63;
-    const int c = (lane & 7) ^ ((row >> 1) & 7);
+    const int c = (lane & 7) ^ rkey(row);
     glds16(a.w2 + row * (9 * kCM) + tap * kCM + c * 8, wreg + wi * 1024);
   }
   // zero padding columns of the patch (slots r * 58 and r * 58 + 57)
@@ -132,25 +138,33 @@ __global__ __launch_bounds__(512, 1) void bottleneck56_kernel(BneckArgs a) {
     for (int s = 0; s < 5; ++s)
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[s][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    bf16x8 xf[2][5], wf[2][4];
-    auto ld1 = [&](int c, int b) __attribute__((always_inline)) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) wf[b][j] = ld_bf16x8(a.w1 + (j * 16 + fr) * CIN + c * 32 + fq * 8);
+    // the input fragments (HBM) run D k-steps ahead, conv1's weights (L2) one step
+    constexpr int D = NC < 4 ? NC : 4;
+    bf16x8 xf[D][5], wf[2][4];
+    auto ldx = [&](int c) __attribute__((always_inline)) {
 #pragma unroll
       for (int s = 0; s < 5; ++s)
-        if (s < 4 || t5) xf[b][s] = ld_bf16x8(xr[s] + c * 32);
+        if (s < 4 || t5) xf[c % D][s] = ld_bf16x8(xr[s] + c * 32);
     };
-    ld1(0, 0);
+    auto ldw = [&](int c) __attribute__((always_inline)) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        wf[c & 1][j] = ld_bf16x8(a.w1 + (j * 16 + fr) * CIN + c * 32 + fq * 8);
+    };
+    ldw(0);
+#pragma unroll
+    for (int c = 0; c < D - 1; ++c) ldx(c);
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
-      if (c + 1 < NC) ld1(c + 1, (c + 1) & 1);
+      if (c + D - 1 < NC) ldx(c + D - 1);
+      if (c + 1 < NC) ldw(c + 1);
       if (a.dbg & 1) continue;
 #pragma unroll
       for (int s = 0; s < 5; ++s)
         if (s < 4 || t5)
 #pragma unroll
           for (int j = 0; j < 4; ++j)
-            acc[s][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[c & 1][j], xf[c & 1][s],
+            acc[s][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[c & 1][j], xf[c % D][s],
                                                                 acc[s][j], 0, 0, 0);
     }
 #pragma unroll
@@ -244,7 +258,7 @@ __global__ __launch_bounds__(512, 1) void bottleneck56_kernel(BneckArgs a) {
   for (int j = 0; j < 4; ++j) {
     const int wi = wave * 4 + j;
     const int row = wi * 8 + (lane >> 3);
-    const int c = (lane & 7) ^ ((row >> 1) & 7);
+    const int c = (lane & 7) ^ rkey(row);
     glds16(a.w3 + row * kCM + c * 8, wreg + wi * 1024);
     if constexpr (DOWN) glds16(a.wd + row * kCM + c * 8, wreg + kCO * 128 + wi * 1024);
   }

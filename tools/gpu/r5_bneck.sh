@@ -10,7 +10,7 @@ timeout -k 10 300 python -u -m pytest tests/test_bottleneck_gpu.py -x -v --timeo
     --timeout-method thread > $d/pytest.log 2>&1 || { tail -40 $d/pytest.log; exit 1; }
 tail -5 $d/pytest.log
 for r in 1 2; do
-  for f in "--no-fuse-blocks" ""; do
+  for f in "--no-fuse-blocks" "" "--no-fuse-blocks --streams 2" "--streams 2"; do
     timeout -k 10 200 python tools/bench_forward.py --model resnet50 --batches 256 --iters 30 $f \
         >> $d/ab.jsonl 2> $d/ab.err || { tail -20 $d/ab.err; exit 1; }
   done
