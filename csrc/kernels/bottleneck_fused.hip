@@ -56,6 +56,7 @@ constexpr int kStrips = kH / kTR;                // 7
 static_assert(kR1 * kW % 16 == 0 && kTR * kW % (16 * 4) == 0, "tile geometry");
 static_assert(2 * kCO * 128 <= kW2Bytes, "W3 + Wd must fit the W2 region");
 static_assert(kTR * kW * 128 + 8 * 2048 <= kH1Bytes, "output stages must fit past H2");
+static_assert(kCO * 128 + 8 * 4096 <= kW2Bytes, "two-tile output stages must fit past W3");
 
 struct BneckArgs {
   const bf16* x;   // [B][56][56][CIN]
@@ -100,21 +101,28 @@ __global__ __launch_bounds__(512, 1) void bottleneck56_kernel(BneckArgs a) {
   const int rid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
   const int n = rid / kStrips, y0 = (rid - n * kStrips) * kTR;
 
-  // ---- W2 -> LDS (lands during phase 1): 576 rows of 128 B = 72 wave-instructions ----
+  // ---- W1 -> the H1 region (free until conv1's outputs are written): CIN / 64 blocks of 64
+  // rows x 128 B, row = k-block * 64 + output channel ----
+  constexpr int W1I = CIN / 64;  // wave-instructions per wave (64 * CIN / 64 rows / 8 / 8 waves)
 #pragma unroll
-  for (int j = 0; j < 9; ++j) {
-    const int wi = wave * 9 + j;
-    const int rg = wi * 8 + (lane >> 3);  // tap * 64 + output channel
-    const int tap = rg >> 6, row = rg & 63;
+  for (int j = 0; j < W1I; ++j) {
+    const int wi = wave * W1I + j;
+    const int row = wi * 8 + (lane >> 3);
+    const int kb = row >> 6, ch = row & 63;
     const int c = (lane & 7) ^ rkey(row);
-    glds16(a.w2 + row * (9 * kCM) + tap * kCM + c * 8, wreg + wi * 1024);
+    glds16(a.w1 + ch * CIN + kb * 64 + c * 8, h1 + wi * 1024);
   }
-  // zero padding columns of the patch (slots r * 58 and r * 58 + 57)
-  if (tid < kR1 * 2 * 8) {
-    const int s = tid >> 3, r = s >> 1;
-    *reinterpret_cast<uint4*>(h1 + (r * kPW + (s & 1) * (kPW - 1)) * 128 + (tid & 7) * 16) =
-        make_uint4(0, 0, 0, 0);
-  }
+  // W2 -> LDS (lands during phase 1): 576 rows of 128 B = 72 wave-instructions
+  auto stage_w2 = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < 9; ++j) {
+      const int wi = wave * 9 + j;
+      const int rg = wi * 8 + (lane >> 3);  // tap * 64 + output channel
+      const int tap = rg >> 6, row = rg & 63;
+      const int c = (lane & 7) ^ rkey(row);
+      glds16(a.w2 + row * (9 * kCM) + tap * kCM + c * 8, wreg + wi * 1024);
+    }
+  };
 
   // ---- phase 1: conv1 over the halo rows y0-1 .. y0+8 -> H1 ----
   {
@@ -138,34 +146,44 @@ __global__ __launch_bounds__(512, 1) void bottleneck56_kernel(BneckArgs a) {
     for (int s = 0; s < 5; ++s)
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[s][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    // the input fragments (HBM) run D k-steps ahead, conv1's weights (L2) one step
+    // the input fragments (HBM) run D k-steps ahead; conv1's weights come from LDS
     constexpr int D = NC < 4 ? NC : 4;
-    bf16x8 xf[D][5], wf[2][4];
+    bf16x8 xf[D][5];
     auto ldx = [&](int c) __attribute__((always_inline)) {
 #pragma unroll
       for (int s = 0; s < 5; ++s)
-        if (s < 4 || t5) xf[c % D][s] = ld_bf16x8(xr[s] + c * 32);
+        if (s < 4 || t5) xf[c % D][s] = ld_bf16x8(((a.dbg & 64) ? a.w1 : xr[s]) + c * 32);
     };
-    auto ldw = [&](int c) __attribute__((always_inline)) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        wf[c & 1][j] = ld_bf16x8(a.w1 + (j * 16 + fr) * CIN + c * 32 + fq * 8);
-    };
-    ldw(0);
 #pragma unroll
     for (int c = 0; c < D - 1; ++c) ldx(c);
+    // W1 landed in every wave (its DMA was issued before these >= 4 (D - 1) input loads;
+    // vector-memory loads complete in order), then the workgroup barrier
+    if constexpr (D - 1 >= 3)
+      asm volatile("s_waitcnt vmcnt(12)\n\ts_barrier" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(4)\n\ts_barrier" ::: "memory");
+    stage_w2();
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
       if (c + D - 1 < NC) ldx(c + D - 1);
-      if (c + 1 < NC) ldw(c + 1);
       if (a.dbg & 1) continue;
+      bf16x8 wf[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) wf[j] = lds16(h1, swz((c >> 1) * 64 + j * 16 + fr, (c & 1) * 4 + fq));
 #pragma unroll
       for (int s = 0; s < 5; ++s)
         if (s < 4 || t5)
 #pragma unroll
           for (int j = 0; j < 4; ++j)
-            acc[s][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[c & 1][j], xf[c % D][s],
-                                                                acc[s][j], 0, 0, 0);
+            acc[s][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], xf[c % D][s], acc[s][j],
+                                                                0, 0, 0);
+    }
+    __syncthreads();  // every wave is done with W1: its region becomes H1
+    // zero padding columns of the patch (slots r * 58 and r * 58 + 57)
+    if (tid < kR1 * 2 * 8) {
+      const int s = tid >> 3, r = s >> 1;
+      *reinterpret_cast<uint4*>(h1 + (r * kPW + (s & 1) * (kPW - 1)) * 128 + (tid & 7) * 16) =
+          make_uint4(0, 0, 0, 0);
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -215,7 +233,7 @@ __global__ __launch_bounds__(512, 1) void bottleneck56_kernel(BneckArgs a) {
 #pragma unroll
         for (int t = 0; t < 4; ++t)
           res[ps][i][t] = *reinterpret_cast<const uint2*>(
-              a.x + (size_t)gp[i] * kCO + wn * 128 + ps * 64 + t * 16 + fq * 4);
+              a.x + ((a.dbg & 32) ? 0 : (size_t)gp[i] * kCO) + wn * 128 + ps * 64 + t * 16 + fq * 4);
   }
 
   // ---- phase 2: conv2 (3x3) from H1 -> registers ----
@@ -283,7 +301,10 @@ __global__ __launch_bounds__(512, 1) void bottleneck56_kernel(BneckArgs a) {
   // Each tile's 16 x 128-B output lines go through a wave-private 2 KB LDS stage (the H1 bytes
   // past H2) so that every global store is 16 B per lane and whole lines per instruction: the
   // MFMA layout's 8-byte pieces of 16 pixels cost ~40 % of the kernel in partial-line writes.
-  uint8_t* const stg = h1 + kTR * kW * 128 + wave * 2048;
+  // Stage: block 0, one 2 KB tile per wave past H2; identity, two tiles per wave (4 KB) in the
+  // weight region past W3 (fewer serialised LDS round trips)
+  constexpr int TPS = DOWN ? 1 : 2;
+  uint8_t* const stg = DOWN ? h1 + kTR * kW * 128 + wave * 2048 : wreg + kCO * 128 + wave * 4096;
   // (identity: unrolled, so res[ps] indexes registers statically; block 0: one pass at a time)
   constexpr int kPassUnroll = DOWN ? 1 : 2;
 #pragma unroll kPassUnroll
@@ -300,8 +321,10 @@ __global__ __launch_bounds__(512, 1) void bottleneck56_kernel(BneckArgs a) {
       b3v[t] = *reinterpret_cast<const float4*>(a.b3 + ch0 + t * 16 + fq * 4);
       if constexpr (DOWN) bdv[t] = *reinterpret_cast<const float4*>(a.bd + ch0 + t * 16 + fq * 4);
     }
-#pragma unroll
-    for (int i = 0; i < 7; ++i) {
+    // one tile: conv3 (+ projection), bias + shortcut + ReLU in fp32, one bf16 rounding (as
+    // the layered conv3); lane: 4 channels of pixel fr per channel tile -> 8 B into row fr of
+    // stage slot `sl`
+    auto tile = [&](int i, uint8_t* st) __attribute__((always_inline)) {
       f32x4 acc3[4], accd[DOWN ? 4 : 1];
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
@@ -322,8 +345,6 @@ __global__ __launch_bounds__(512, 1) void bottleneck56_kernel(BneckArgs a) {
           }
         }
       }
-      // bias + shortcut + ReLU in fp32, one bf16 rounding (as the layered conv3); lane: 4
-      // channels of pixel fr per channel tile -> 8 B into row fr of the stage
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
         float sc[4];
@@ -342,21 +363,32 @@ __global__ __launch_bounds__(512, 1) void bottleneck56_kernel(BneckArgs a) {
         o[1] = (bf16)fmaxf(acc3[t][1] + b3v[t].y + sc[1], 0.f);
         o[2] = (bf16)fmaxf(acc3[t][2] + b3v[t].z + sc[2], 0.f);
         o[3] = (bf16)fmaxf(acc3[t][3] + b3v[t].w + sc[3], 0.f);
-        *reinterpret_cast<uint2*>(stg + swz(fr, t * 2 + (fq >> 1)) + (fq & 1) * 8) =
+        *reinterpret_cast<uint2*>(st + swz(fr, t * 2 + (fq >> 1)) + (fq & 1) * 8) =
             __builtin_bit_cast(uint2, o);
       }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // (wave-private stage)
-      // read back 8 pixels x 128 B per instruction: lane -> pixel (lane >> 3) + 8h, chunk lane & 7
+    };
+    // read back 8 pixels x 128 B per instruction: lane -> pixel (lane >> 3) + 8h, chunk lane & 7
+    auto flush = [&](int i, const uint8_t* st) __attribute__((always_inline)) {
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         const int px = h * 8 + (lane >> 3), c = lane & 7;
-        const uint4 v = *reinterpret_cast<const uint4*>(stg + swz(px, c));
+        const uint4 v = *reinterpret_cast<const uint4*>(st + swz(px, c));
         const int p = (wm * 7 + i) * 16 + px;
         const int r = p / kW, cc = p - r * kW;
         if (!(a.dbg & 16))
           *reinterpret_cast<uint4*>(a.y + (size_t)((n * kH + y0 + r) * kW + cc) * kCO + ch0 + c * 8) = v;
       }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // stage free for the next tile
+    };
+#pragma unroll
+    for (int i0 = 0; i0 < 7; i0 += TPS) {
+#pragma unroll
+      for (int u = 0; u < TPS; ++u)
+        if (i0 + u < 7) tile(i0 + u, stg + u * 2048);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // (wave-private stage)
+#pragma unroll
+      for (int u = 0; u < TPS; ++u)
+        if (i0 + u < 7) flush(i0 + u, stg + u * 2048);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // stage free for the next round
     }
     __builtin_amdgcn_sched_barrier(0);
   }
