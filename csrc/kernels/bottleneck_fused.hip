@@ -81,6 +81,13 @@ __device__ __forceinline__ int rkey(int row) { return ((row >> 1) & 3) << 1; }
 // byte offset of 16-B chunk c of 128-B LDS row `row`
 __device__ __forceinline__ int swz(int row, int c) { return row * 128 + ((c ^ rkey(row)) << 4); }
 
+// conv3 / projection output channel held by LDS weight row R: within each 64-channel group,
+// MFMA tile t row m <- channel (m >> 2) * 16 + t * 4 + (m & 3), so a lane's four channel tiles
+// hold 16 CONSECUTIVE channels (fq * 16 ..) of its pixel: 16-byte residual loads and stage stores
+__device__ __forceinline__ int perm3(int R) {
+  return (R & ~63) | (((R & 15) >> 2) << 4) | (((R >> 4) & 3) << 2) | (R & 3);
+}
+
 __device__ __forceinline__ bf16x8 lds16(const uint8_t* lds, int off) {
   return *reinterpret_cast<const bf16x8*>(lds + off);
 }
@@ -215,10 +222,9 @@ __global__ __launch_bounds__(512, 1) void bottleneck56_kernel(BneckArgs a) {
     pr[i] = p;
     gp[i] = (n * kH + y0 + r) * kW + cc;
   }
-  // identity: the residual in MFMA-output layout, 2 passes x 7 tiles x 4 channel tiles of 4
-  // channels (8 B each); block 0: the input pixels' 64 channels for the projection (7 tiles x 2
-  // k-halves)
-  uint2 res[DOWN ? 1 : 2][7][4];
+  // identity: the residual in (perm3) MFMA-output layout, 2 passes x 7 tiles x 16 channels;
+  // block 0: the input pixels' 64 channels for the projection (7 tiles x 2 k-halves)
+  uint4 res[DOWN ? 1 : 2][7][2];
   bf16x8 xc[DOWN ? 7 : 1][2];
   if constexpr (DOWN) {
 #pragma unroll
@@ -226,14 +232,15 @@ __global__ __launch_bounds__(512, 1) void bottleneck56_kernel(BneckArgs a) {
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) xc[i][kk] = ld_bf16x8(a.x + (size_t)gp[i] * CIN + kk * 32 + fq * 8);
   } else {
+    // (perm3 layout: 16 consecutive channels of the pixel per lane and 64-channel group)
 #pragma unroll
     for (int ps = 0; ps < 2; ++ps)
 #pragma unroll
       for (int i = 0; i < 7; ++i)
 #pragma unroll
-        for (int t = 0; t < 4; ++t)
-          res[ps][i][t] = *reinterpret_cast<const uint2*>(
-              a.x + ((a.dbg & 32) ? 0 : (size_t)gp[i] * kCO) + wn * 128 + ps * 64 + t * 16 + fq * 4);
+        for (int h = 0; h < 2; ++h)
+          res[ps][i][h] = *reinterpret_cast<const uint4*>(
+              a.x + ((a.dbg & 32) ? 0 : (size_t)gp[i] * kCO) + wn * 128 + ps * 64 + fq * 16 + h * 8);
   }
 
   // ---- phase 2: conv2 (3x3) from H1 -> registers ----
@@ -277,8 +284,9 @@ __global__ __launch_bounds__(512, 1) void bottleneck56_kernel(BneckArgs a) {
     const int wi = wave * 4 + j;
     const int row = wi * 8 + (lane >> 3);
     const int c = (lane & 7) ^ rkey(row);
-    glds16(a.w3 + row * kCM + c * 8, wreg + wi * 1024);
-    if constexpr (DOWN) glds16(a.wd + row * kCM + c * 8, wreg + kCO * 128 + wi * 1024);
+    const int g = perm3(row);
+    glds16(a.w3 + g * kCM + c * 8, wreg + wi * 1024);
+    if constexpr (DOWN) glds16(a.wd + g * kCM + c * 8, wreg + kCO * 128 + wi * 1024);
   }
   // H2 = bf16(relu(conv2 + b2)) over H1
 #pragma unroll
@@ -318,12 +326,11 @@ __global__ __launch_bounds__(512, 1) void bottleneck56_kernel(BneckArgs a) {
     float4 b3v[4], bdv[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-      b3v[t] = *reinterpret_cast<const float4*>(a.b3 + ch0 + t * 16 + fq * 4);
-      if constexpr (DOWN) bdv[t] = *reinterpret_cast<const float4*>(a.bd + ch0 + t * 16 + fq * 4);
+      b3v[t] = *reinterpret_cast<const float4*>(a.b3 + ch0 + fq * 16 + t * 4);
+      if constexpr (DOWN) bdv[t] = *reinterpret_cast<const float4*>(a.bd + ch0 + fq * 16 + t * 4);
     }
     // one tile: conv3 (+ projection), bias + shortcut + ReLU in fp32, one bf16 rounding (as
-    // the layered conv3); lane: 4 channels of pixel fr per channel tile -> 8 B into row fr of
-    // stage slot `sl`
+    // the layered conv3); lane: 16 consecutive channels of pixel fr -> 32 B of stage row fr
     auto tile = [&](int i, uint8_t* st) __attribute__((always_inline)) {
       f32x4 acc3[4], accd[DOWN ? 4 : 1];
 #pragma unroll
@@ -345,6 +352,7 @@ __global__ __launch_bounds__(512, 1) void bottleneck56_kernel(BneckArgs a) {
           }
         }
       }
+      bf16x4 o[4];  // channels fq * 16 + t * 4 .. + 4 (perm3)
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
         float sc[4];
@@ -355,16 +363,24 @@ __global__ __launch_bounds__(512, 1) void bottleneck56_kernel(BneckArgs a) {
           sc[2] = (float)(bf16)(accd[t][2] + bdv[t].z);
           sc[3] = (float)(bf16)(accd[t][3] + bdv[t].w);
         } else {
-          const bf16x4 rr = __builtin_bit_cast(bf16x4, res[ps][i][t]);
-          sc[0] = (float)rr[0]; sc[1] = (float)rr[1]; sc[2] = (float)rr[2]; sc[3] = (float)rr[3];
+          const bf16x8 rr = __builtin_bit_cast(bf16x8, res[ps][i][t >> 1]);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) sc[e] = (float)rr[(t & 1) * 4 + e];
         }
-        bf16x4 o;
-        o[0] = (bf16)fmaxf(acc3[t][0] + b3v[t].x + sc[0], 0.f);
-        o[1] = (bf16)fmaxf(acc3[t][1] + b3v[t].y + sc[1], 0.f);
-        o[2] = (bf16)fmaxf(acc3[t][2] + b3v[t].z + sc[2], 0.f);
-        o[3] = (bf16)fmaxf(acc3[t][3] + b3v[t].w + sc[3], 0.f);
-        *reinterpret_cast<uint2*>(st + swz(fr, t * 2 + (fq >> 1)) + (fq & 1) * 8) =
-            __builtin_bit_cast(uint2, o);
+        o[t][0] = (bf16)fmaxf(acc3[t][0] + b3v[t].x + sc[0], 0.f);
+        o[t][1] = (bf16)fmaxf(acc3[t][1] + b3v[t].y + sc[1], 0.f);
+        o[t][2] = (bf16)fmaxf(acc3[t][2] + b3v[t].z + sc[2], 0.f);
+        o[t][3] = (bf16)fmaxf(acc3[t][3] + b3v[t].w + sc[3], 0.f);
+      }
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        bf16x8 v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[e] = o[2 * h][e];
+          v[4 + e] = o[2 * h + 1][e];
+        }
+        *reinterpret_cast<uint4*>(st + swz(fr, 2 * fq + h)) = __builtin_bit_cast(uint4, v);
       }
     };
     // read back 8 pixels x 128 B per instruction: lane -> pixel (lane >> 3) + 8h, chunk lane & 7
