@@ -54,8 +54,7 @@ constexpr int kLdsBytes = kH1Bytes + kW2Bytes;   // 147,968
 constexpr int kT1 = kR1 * kW / 16;               // 35 phase-1 pixel tiles
 constexpr int kStrips = kH / kTR;                // 7
 static_assert(kR1 * kW % 16 == 0 && kTR * kW % (16 * 4) == 0, "tile geometry");
-static_assert(2 * kCO * 128 <= kW2Bytes, "W3 + Wd must fit the W2 region");
-static_assert(kTR * kW * 128 + 8 * 2048 <= kH1Bytes, "output stages must fit past H2");
+static_assert(kCO * 128 <= kW2Bytes, "W3 must fit the W2 region");
 static_assert(kCO * 128 + 8 * 4096 <= kW2Bytes, "two-tile output stages must fit past W3");
 
 struct BneckArgs {
@@ -278,7 +277,8 @@ __global__ __launch_bounds__(512, 1) void bottleneck56_kernel(BneckArgs a) {
   }
   __syncthreads();  // every wave is done with H1 and W2
 
-  // W3 (and Wd) -> the W2 region: 256 rows of 128 B each = 32 wave-instructions
+  // W3 -> the W2 region: 256 rows of 128 B each = 32 wave-instructions (block 0's projection
+  // weights come from L2 into registers, one 64-channel group per pass)
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int wi = wave * 4 + j;
@@ -286,7 +286,6 @@ __global__ __launch_bounds__(512, 1) void bottleneck56_kernel(BneckArgs a) {
     const int c = (lane & 7) ^ rkey(row);
     const int g = perm3(row);
     glds16(a.w3 + g * kCM + c * 8, wreg + wi * 1024);
-    if constexpr (DOWN) glds16(a.wd + g * kCM + c * 8, wreg + kCO * 128 + wi * 1024);
   }
   // H2 = bf16(relu(conv2 + b2)) over H1
 #pragma unroll
@@ -309,20 +308,24 @@ __global__ __launch_bounds__(512, 1) void bottleneck56_kernel(BneckArgs a) {
   // Each tile's 16 x 128-B output lines go through a wave-private 2 KB LDS stage (the H1 bytes
   // past H2) so that every global store is 16 B per lane and whole lines per instruction: the
   // MFMA layout's 8-byte pieces of 16 pixels cost ~40 % of the kernel in partial-line writes.
-  // Stage: block 0, one 2 KB tile per wave past H2; identity, two tiles per wave (4 KB) in the
-  // weight region past W3 (fewer serialised LDS round trips)
-  constexpr int TPS = DOWN ? 1 : 2;
-  uint8_t* const stg = DOWN ? h1 + kTR * kW * 128 + wave * 2048 : wreg + kCO * 128 + wave * 4096;
+  // Stage: two tiles per wave (4 KB) in the weight region past W3 (fewer serialised LDS round
+  // trips than one)
+  constexpr int TPS = 2;
+  uint8_t* const stg = wreg + kCO * 128 + wave * 4096;
   // (identity: unrolled, so res[ps] indexes registers statically; block 0: one pass at a time)
   constexpr int kPassUnroll = DOWN ? 1 : 2;
 #pragma unroll kPassUnroll
   for (int ps = 0; ps < 2; ++ps) {
     const int ch0 = wn * 128 + ps * 64;
-    bf16x8 af[4][2];  // W3 fragments, reused by the 7 tiles (Wd's are re-read per tile)
+    bf16x8 af[4][2], df[DOWN ? 4 : 1][2];  // W3 (and Wd) fragments, reused by the 7 tiles
 #pragma unroll
     for (int t = 0; t < 4; ++t)
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk) af[t][kk] = lds16(wreg, swz(ch0 + t * 16 + fr, kk * 4 + fq));
+      for (int kk = 0; kk < 2; ++kk) {
+        af[t][kk] = lds16(wreg, swz(ch0 + t * 16 + fr, kk * 4 + fq));
+        if constexpr (DOWN)
+          df[t][kk] = ld_bf16x8(a.wd + perm3(ch0 + t * 16 + fr) * kCM + kk * 32 + fq * 8);
+      }
     float4 b3v[4], bdv[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
@@ -346,9 +349,8 @@ __global__ __launch_bounds__(512, 1) void bottleneck56_kernel(BneckArgs a) {
           for (int t = 0; t < 4; ++t) {
             acc3[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[t][kk], bfr, acc3[t], 0, 0, 0);
             if constexpr (DOWN)
-              accd[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                  lds16(wreg, kCO * 128 + swz(ch0 + t * 16 + fr, kk * 4 + fq)), xc[i][kk], accd[t],
-                  0, 0, 0);
+              accd[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(df[t][kk], xc[i][kk], accd[t],
+                                                                0, 0, 0);
           }
         }
       }
