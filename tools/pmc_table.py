@@ -29,16 +29,14 @@ def layer_labels(model: str, batch: int):
 
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     from gale.models import get_model
-    from gale.models.graph import Conv, build_plan, stored_channels
+    from gale.models.graph import build_plan
 
     net = get_model(model)
     ops, _ = build_plan(net, 0, "bf16", fused=True)
-    convs = [L for L in net.layers if isinstance(L, Conv)]
-    out, ci = [], 0
+    out = []
     for op in ops:
         if op["kind"] == 0:
-            L = convs[ci]
-            ci += 1
+            L = net.layers[op["layer"]]
             d = op["conv"]
             m = batch * d["Ho"] * d["Wo"]
             fl = 2.0 * m * d["Cout"] * d["K"]
@@ -47,6 +45,13 @@ def layer_labels(model: str, batch: int):
             by += d["Npad"] * d["Kpad"] * 2
             out.append((f"{L.name} {d['KH']}x{d['KW']}/{d['stride']} {d['Cin']}->{d['Cout']} "
                         f"@{d['Ho']}x{d['Wo']}", fl, by))
+        elif op["kind"] == 9:  # OP_BOTTLENECK: a whole 56x56 block (bottleneck_fused.hip)
+            cin, down = op["p"][0], op["p"][1]
+            blk = net.layers[op["layer"]].name.rsplit(".", 1)[0]
+            m = batch * 56 * 56
+            fl = 2.0 * m * (cin * 64 + 576 * 64 + 64 * 256 + (64 * 256 if down else 0))
+            by = 2.0 * m * (cin + 256 + (0 if down else 256))
+            out.append((f"{blk} fused bottleneck {cin}->256{' +proj' if down else ''}", fl, by))
         else:
             out.append((f"op{op['kind']}", 0.0, 0.0))
     return out
