@@ -160,6 +160,14 @@ PYBIND11_MODULE(_C, m) {
         py::arg("cin"), py::arg("down"), py::arg("stream"));
   m.def("bottleneck56_supported", &gale::bottleneck56_supported, py::arg("H"), py::arg("W"),
         py::arg("cin"), py::arg("cmid"), py::arg("cout"), py::arg("down"));
+  m.def("stem_pool",
+        [](int batch, uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t y, uintptr_t stream) {
+          chk(gale::stem_pool(batch, P(x), P(w), static_cast<const float*>(P(bias)), P(y),
+                              S(stream)),
+              "stem_pool");
+        },
+        py::arg("batch"), py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("y"),
+        py::arg("stream"));
   m.def("stem_pack",
         [](int batch, int H, int W, int C, int Wp, int lp, uintptr_t x, uintptr_t y,
            uintptr_t stream) {

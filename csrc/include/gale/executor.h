@@ -32,6 +32,8 @@ enum OpKind : int {
   OP_LENET5 = 8,    // whole-network fused MNIST LeNet-5; ptrs = w1 b1 w2 b2 w3 b3 w4 b4 w5 b5
   OP_BOTTLENECK = 9,  // one whole ResNet-50 56x56 bottleneck (bottleneck56); ptrs = w1 b1 w2 b2
                       // w3 b3 [wd bd]; p[0] = cin, p[1] = down (projection shortcut)
+  OP_STEM_POOL = 10,  // ResNet-50 stem conv + max-pool (stem_pool); conv = the stem's desc,
+                      // w / bias = its weights; p[0..7] = the max-pool's H W C k s pad Ho Wo
 };
 
 // Buffer ids: 0 = network input (fp32 NHWC), 1 = network output (fp32 [B, classes]),

@@ -95,6 +95,14 @@ bool bottleneck56_supported(int H, int W, int cin, int cmid, int cout, int down)
 hipError_t bottleneck56(const BottleneckParams& p, int batch, const void* x, void* y,
                         hipStream_t stream);
 
+// ResNet-50 ImageNet stem conv (packed-stem ConvDesc, ReLU) + 3x3/2 max-pool in one launch
+// (stem_pool.hip): x = stem_pack() image bf16 [B][224][230][4], w [64][256], y bf16
+// [B][56][56][64]. stem_pool_supported: the conv desc + the maxpool op's geometry.
+bool stem_pool_supported(const ConvDesc& d, int H, int W, int C, int k, int s, int p, int Ho,
+                         int Wo);
+hipError_t stem_pool(int batch, const void* x, const void* w, const float* bias, void* y,
+                     hipStream_t stream);
+
 // fp32 NHWC [B][H][W][C<=4] -> bf16 [B][H][Wp][4] with `lp` zero columns on the left (and zeros
 // up to Wp on the right, channels >= C zero): the input of a packed-stem conv (ConvDesc::stem).
 hipError_t stem_pack(int batch, int H, int W, int C, int Wp, int lp, const float* x, void* y,

@@ -203,6 +203,12 @@ void Executor::launch_ops(size_t begin, size_t end, int batch, void* const* bufs
         e = bottleneck56(bp, batch, in, out, stream);
         break;
       }
+      case OP_STEM_POOL:
+        if (!stem_pool_supported(op.conv, op.p[0], op.p[1], op.p[2], op.p[3], op.p[4], op.p[5],
+                                 op.p[6], op.p[7]))
+          throw std::invalid_argument("stem_pool op: unsupported geometry");
+        e = stem_pool(batch, in, op.w, op.bias, out, stream);
+        break;
       default:
         throw std::invalid_argument("unknown plan op kind");
     }

@@ -393,7 +393,7 @@ def act_scales_from_packed(net: Network, packed: torch.Tensor) -> Dict[str, floa
 # --------------------------------------------------------------------------------------------
 
 (OP_CONV, OP_MAXPOOL, OP_AVGPOOL, OP_HEAD, OP_SOFTMAX, OP_RESNET20, OP_STEM_PACK, OP_BN_ACT,
- OP_LENET5, OP_BOTTLENECK) = range(10)
+ OP_LENET5, OP_BOTTLENECK, OP_STEM_POOL) = range(11)
 
 
 def is_cifar_resnet20(net: Network) -> bool:
@@ -460,6 +460,41 @@ def _is_conv(op: dict, kh: int, cin: int, cout: int, relu: int, res: bool, hw: i
             and (kh == 1 or d["pad"] == 1))
 
 
+def fuse_stem_pool(ops: List[dict]) -> List[dict]:
+    """The ResNet-50 packed stem conv followed by its 3x3/2 max-pool becomes ONE
+    ``OP_STEM_POOL`` (csrc/kernels/stem_pool.hip: the 112x112x64 stem output stays in LDS), when
+    nothing else reads the stem output."""
+    out: List[dict] = []
+    i = 0
+    while i < len(ops):
+        c = ops[i]
+        if (i + 1 < len(ops) and c["kind"] == OP_CONV and c["conv"].get("stem")
+                and ops[i + 1]["kind"] == OP_MAXPOOL and ops[i + 1]["in"] == c["out"]):
+            m, d = ops[i + 1], c["conv"]
+            H, W, C, k, s_, p, Ho, Wo = m["p"]
+            if (d["H"] == 224 and d["W"] == 230 and d["Ho"] == 112 and d["Wo"] == 112
+                    and d["Cout"] == 64 and d["Npad"] == 64 and d["K"] == 256 and d["relu"]
+                    and not d.get("has_res") and not d.get("fp8") and not d.get("f32")
+                    and (H, W, C, k, s_, p, Ho, Wo) == (112, 112, 64, 3, 2, 1, 56, 56)
+                    and m.get("et", 0) == 0):
+                live = False
+                for o in ops[i + 2:]:  # the stem output's buffer, read before it is rewritten?
+                    if o.get("in") == c["out"] or o.get("res", -1) == c["out"]:
+                        live = True
+                        break
+                    if o.get("out") == c["out"]:
+                        break
+                if not live:
+                    out.append(dict(kind=OP_STEM_POOL, conv=d, **{"in": c["in"]}, out=m["out"],
+                                    res=-1, w=c["w"], bias=c["bias"], p=list(m["p"]),
+                                    bpi=[c["bpi"][0], m["bpi"][1], 0], layer=m.get("layer", 0)))
+                    i += 2
+                    continue
+        out.append(c)
+        i += 1
+    return out
+
+
 def fuse_bottlenecks(ops: List[dict]) -> List[dict]:
     """Replace every ResNet-50 56x56 bottleneck of a bf16 plan - conv1 / conv2 / conv3 (+ the
     block-0 projection before them) - by ONE ``OP_BOTTLENECK`` (csrc/kernels/bottleneck_fused.hip:
@@ -521,7 +556,8 @@ def build_plan(net: Network, base_ptr: int, wdtype: str = "bf16",
     fold_bn=False)``): every BatchNorm conv is followed by a standalone ``bn_act`` kernel that
     applies the BN affine, the residual and the ReLU in place (the debugging / parity plan).
     ``fuse_blocks`` (bf16, folded BN, no chunking; default on, ``GALE_FUSE_BLOCKS=0`` off): the
-    ResNet-50 56x56 bottlenecks run as one kernel each (``fuse_bottlenecks``).
+    ResNet-50 stem + max-pool (``fuse_stem_pool``) and each 56x56 bottleneck
+    (``fuse_bottlenecks``) run as one kernel.
     ``chunk_layers``: the first ``chunk_layers`` layers may run per batch chunk (the executor's
     PlanSpec::chunk_ops; every op carries ``layer``, its layer index): each tensor they produce
     that is still read after them gets a buffer of its own, so a later chunk cannot overwrite an
@@ -661,5 +697,5 @@ def build_plan(net: Network, base_ptr: int, wdtype: str = "bf16",
     if fuse_blocks is None:
         fuse_blocks = os.environ.get("GALE_FUSE_BLOCKS", "1") != "0"
     if fuse_blocks and fused and wdtype == "bf16" and fold_bn and chunk_layers == 0:
-        ops = fuse_bottlenecks(ops)
+        ops = fuse_bottlenecks(fuse_stem_pool(ops))
     return ops, buf_bytes

@@ -1,6 +1,7 @@
-"""The fused ResNet-50 56x56 bottleneck kernel (csrc/kernels/bottleneck_fused.hip) against the
-layered conv kernels it replaces and against a PyTorch fp32 oracle of the same block, plus the
-whole ResNet-50 forward with and without the fusion (gale.models.graph.fuse_bottlenecks)."""
+"""The fused ResNet-50 kernels against the layered kernels they replace: the 56x56 bottleneck
+(csrc/kernels/bottleneck_fused.hip; also against a PyTorch fp32 oracle of the block), the stem +
+max-pool (csrc/kernels/stem_pool.hip), and the whole ResNet-50 forward with and without the
+fusions (gale.models.graph.fuse_stem_pool / fuse_bottlenecks)."""
 
 import pytest
 import torch
@@ -111,3 +112,38 @@ def test_resnet50_fused_blocks_match_layered_plan():
     assert torch.allclose(pf.sum(1), torch.ones(3), atol=1e-4)
     assert (pf - pl).abs().max().item() < 2e-3
     assert torch.equal(pf.argmax(1), pl.argmax(1))
+
+
+def test_stem_pool_matches_layered_stem_and_maxpool():
+    """stem_pool.hip (ResNet-50 stem conv + 3x3/2 max-pool in one kernel) against the layered
+    packed-stem conv_gemm + maxpool kernels on the model's own packed weights: the same fp32
+    accumulation order, so the pooled tensors agree bit for bit (up to a stray rounding)."""
+    from gale._native import native
+    from gale.models import get_model
+    from gale.models.graph import OP_CONV, OP_MAXPOOL, OP_STEM_PACK, build_plan
+    from gale.parallel.weights import materialize_weights
+
+    C = native()
+    net = get_model("resnet50")
+    packed = materialize_weights(net, DEV, wdtype="bf16")
+    ops, _ = build_plan(net, packed.data_ptr(), "bf16", fuse_blocks=False)
+    pk, st, mp = ops[0], ops[1], ops[2]
+    assert (pk["kind"], st["kind"], mp["kind"]) == (OP_STEM_PACK, OP_CONV, OP_MAXPOOL)
+    B = 3
+    g = torch.Generator().manual_seed(3)
+    x = torch.rand(B, 224, 224, 3, generator=g).to(DEV)
+    s = torch.cuda.current_stream().cuda_stream
+    H, W, Cc, Wp, lp = pk["p"][:5]
+    xp = torch.empty(B, 224, Wp, 4, device=DEV, dtype=torch.bfloat16)
+    C.stem_pack(B, H, W, Cc, Wp, lp, x.data_ptr(), xp.data_ptr(), s)
+    s0 = torch.empty(B, 112, 112, 64, device=DEV, dtype=torch.bfloat16)
+    C.conv2d(st["conv"], B, xp.data_ptr(), st["w"], st["bias"], 0, 0, s0.data_ptr(), s)
+    ref = torch.empty(B, 56, 56, 64, device=DEV, dtype=torch.bfloat16)
+    C.maxpool2d(B, *mp["p"], s0.data_ptr(), ref.data_ptr(), s)
+    got = torch.full_like(ref, float("nan"))
+    C.stem_pool(B, xp.data_ptr(), st["w"], st["bias"], got.data_ptr(), s)
+    torch.cuda.synchronize()
+    assert torch.isfinite(got.float()).all()
+    d = (got.float() - ref.float()).abs()
+    assert (d > 0).float().mean().item() < 1e-3
+    assert d.max().item() <= 2 ** -7 * max(ref.float().abs().max().item(), 1.0)

@@ -185,10 +185,11 @@ def test_chunked_plan_keeps_live_out_tensors(end):
 
 
 def test_resnet50_plan_fuses_56x56_bottlenecks():
-    """fuse_bottlenecks: the three 56x56 blocks (block 0 with its projection) become one
+    """fuse_stem_pool / fuse_bottlenecks: stem conv + max-pool become one OP_STEM_POOL, and the
+    three 56x56 blocks (block 0 with its projection) become one
     OP_BOTTLENECK each, wired from the block input to the block output buffer; other stages,
     fp8 and the unfused switch keep the layered ops."""
-    from gale.models.graph import OP_BOTTLENECK, OP_CONV
+    from gale.models.graph import OP_BOTTLENECK, OP_CONV, OP_STEM_POOL
 
     net = get_model("resnet50")
     layered, bufs = build_plan(net, 1 << 20, fuse_blocks=False)
@@ -196,7 +197,11 @@ def test_resnet50_plan_fuses_56x56_bottlenecks():
     assert bufs == bufs2
     bn = [op for op in fused if op["kind"] == OP_BOTTLENECK]
     assert [op["p"][:2] for op in bn] == [[64, 1], [256, 0], [256, 0]]
-    assert len(fused) == len(layered) - 4 - 3 - 3 + 3
+    assert len(fused) == len(layered) - 4 - 3 - 3 + 3 - 1  # (- 1: stem + max-pool fused)
+    sp = [op for op in fused if op["kind"] == OP_STEM_POOL]
+    assert len(sp) == 1 and fused[1] is sp[0]
+    assert sp[0]["in"] == layered[1]["in"] and sp[0]["out"] == layered[2]["out"]
+    assert sp[0]["w"] == layered[1]["w"] and sp[0]["p"] == layered[2]["p"]
     # block 0 reads the max-pool output and writes what l1.1 reads; each block feeds the next
     assert bn[0]["in"] == layered[2]["out"]  # stem_pack, stem, maxpool -> p0
     assert bn[1]["in"] == bn[0]["out"] and bn[2]["in"] == bn[1]["out"]
