@@ -52,6 +52,14 @@ def layer_labels(model: str, batch: int):
             fl = 2.0 * m * (cin * 64 + 576 * 64 + 64 * 256 + (64 * 256 if down else 0))
             by = 2.0 * m * (cin + 256 + (0 if down else 256))
             out.append((f"{blk} fused bottleneck {cin}->256{' +proj' if down else ''}", fl, by))
+        elif op["kind"] == 10:  # OP_STEM_POOL: stem conv + max-pool (stem_pool.hip)
+            d = op["conv"]
+            m = batch * d["Ho"] * d["Wo"]
+            fl = 2.0 * m * d["Cout"] * d["K"] * 9 / 8  # (+1 recomputed window row in 8)
+            by = 2.0 * (batch * d["H"] * d["W"] * 4 + batch * 56 * 56 * d["Cout"])
+            out.append(("stem 7x7/2 + maxpool 3x3/2 (fused) @56x56", fl, by))
+        elif op["kind"] == 6:
+            out.append(("stem_pack (fp32 -> bf16 [224][230][4])", 0.0, 0.0))
         else:
             out.append((f"op{op['kind']}", 0.0, 0.0))
     return out
