@@ -18,7 +18,10 @@ from gale._native import native  # noqa: E402
 
 C = native()
 REC = np.dtype([("off", "<i8"), ("len", "<i4"), ("slot", "<i4"), ("images", "<i4"),
-                ("status", "<i4"), ("tile0", "<i4"), ("pad", "<i4")])
+                ("status", "<i4"), ("tile0", "<i4"), ("has_cnt", "<i4"), ("cnt_off", "<i8"),
+                ("pad", "<i8")])
+assert REC.itemsize == C.JSON_RECORD_BYTES, "JsonRecord layout changed (gale/kernels.h)"
+
 
 
 def staged_batch(batch, H, W, Cc, distinct=64, seed=0):
@@ -34,7 +37,7 @@ def staged_batch(batch, H, W, Cc, distinct=64, seed=0):
     tiles = 0
     for i in range(batch):
         t = texts[i % len(texts)]
-        recs[i] = (len(buf), len(t), i, 1, 0, tiles, 0)
+        recs[i] = (len(buf), len(t), i, 1, 0, tiles, 0, 0, 0)
         tiles += C.json_tile_count(len(buf), len(t))
         buf += t + b" " * ((-len(t)) % 16)
     buf += b" " * 16
@@ -62,10 +65,10 @@ def main():
         d_counts = torch.zeros(tiles, dtype=torch.int32, device="cuda")
         out = torch.empty((b, H, W, Cc), device="cuda")
 
-        def run():
+        def run(count_pass=True):
             C.json_parse_instances(b, tiles, d_recs.data_ptr(), d_tile_rec.data_ptr(),
                                    d_raw.data_ptr(), H, W, Cc, d_counts.data_ptr(),
-                                   out.data_ptr(), s.cuda_stream)
+                                   out.data_ptr(), s.cuda_stream, count_pass)
 
         for _ in range(3):
             run()
@@ -79,8 +82,15 @@ def main():
         e1.record()
         torch.cuda.synchronize()
         us = e0.elapsed_time(e1) * 1e3 / a.iters
+        # the parse alone, from the counts (the serving step: the ingest pass counted them)
+        e0.record()
+        for _ in range(a.iters):
+            run(False)
+        e1.record()
+        torch.cuda.synchronize()
+        us_parse = e0.elapsed_time(e1) * 1e3 / a.iters
         print(json.dumps(dict(kernel="json_parse_instances", batch=b, tiles=tiles,
-                              bytes=int(raw.size), us=round(us, 2),
+                              bytes=int(raw.size), us=round(us, 2), parse_only_us=round(us_parse, 2),
                               gb_s=round(raw.size / us / 1e3, 1),
                               img_s=round(b / us * 1e6))), flush=True)
 
