@@ -158,6 +158,9 @@ class GaleConfig:
     rank_max_restarts: int = 10
     rank_restart_backoff_ms: int = 1000
     rank_start_timeout_s: float = 300.0
+    # more ranks than GPUs (a 1-GPU rehearsal of the multi-rank path): rank r serves GPU
+    # r % device_count and the process group is gloo (RCCL refuses two ranks on one device)
+    shared_gpu_rehearsal: bool = False
     fault: str = ""                    # replica_crash@N,parse_error@P,producer_fail@P
     trace: bool = False                # roctx ranges around pipeline stages (rocprofv3)
     profile: str = ""                  # run under rocprofv3 --kernel-trace --marker-trace --stats

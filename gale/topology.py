@@ -177,11 +177,16 @@ def run_topology(cfg: GaleConfig, stop_event: Optional[threading.Event] = None,
         incarnation = int(os.environ.get("GALE_RANK_INCARNATION", "0"))
         supervised = bool(os.environ.get("GALE_SUPERVISED"))
         if world > 1 and not cfg.stub:
-            devices = [local_rank]
+            dev = local_rank
+            if cfg.shared_gpu_rehearsal:
+                import torch
+
+                dev = local_rank % max(1, torch.cuda.device_count())
+            devices = [dev]
             if incarnation == 0:
                 from gale.parallel.group import init_rank_group
 
-                init_rank_group(local_rank, use_gpu=True)
+                init_rank_group(dev, use_gpu=True, shared_gpu=cfg.shared_gpu_rehearsal)
             # a respawned rank (incarnation > 0) has no group to join: it materialises the
             # weights itself from the same seed / --weights file (Storm's prepare() reload)
         if world > 1 and not cfg.partitions and not cfg.group_membership:
