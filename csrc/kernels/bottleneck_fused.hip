@@ -30,8 +30,6 @@
 // Rounding matches the layered plan: H1, H2 and the block-0 projection are rounded to bf16
 // exactly where the layered kernels store them.
 // Grid: batch x 7 strips, XCD-contiguous (neighbouring strips share 2 halo rows in one L2).
-#include <stdlib.h>
-
 #include "common.cuh"
 #include "gale/kernels.h"
 
@@ -69,7 +67,6 @@ struct BneckArgs {
   const float* bd;
   bf16* y;         // [B][56][56][256]
   int nwg;
-  int dbg;         // timing experiments only (GALE_BNECK_DBG): bits skip work, output invalid
 };
 
 // XOR key of 128-B LDS row `row`: even values only, so a ds_read_b128 lane group - which mixes
@@ -158,7 +155,7 @@ __global__ __launch_bounds__(512, 1) void bottleneck56_kernel(BneckArgs a) {
     auto ldx = [&](int c) __attribute__((always_inline)) {
 #pragma unroll
       for (int s = 0; s < 5; ++s)
-        if (s < 4 || t5) xf[c % D][s] = ld_bf16x8(((a.dbg & 64) ? a.w1 : xr[s]) + c * 32);
+        if (s < 4 || t5) xf[c % D][s] = ld_bf16x8(xr[s] + c * 32);
     };
 #pragma unroll
     for (int c = 0; c < D - 1; ++c) ldx(c);
@@ -172,7 +169,6 @@ __global__ __launch_bounds__(512, 1) void bottleneck56_kernel(BneckArgs a) {
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
       if (c + D - 1 < NC) ldx(c + D - 1);
-      if (a.dbg & 1) continue;
       bf16x8 wf[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) wf[j] = lds16(h1, swz((c >> 1) * 64 + j * 16 + fr, (c & 1) * 4 + fq));
@@ -239,7 +235,7 @@ __global__ __launch_bounds__(512, 1) void bottleneck56_kernel(BneckArgs a) {
 #pragma unroll
         for (int h = 0; h < 2; ++h)
           res[ps][i][h] = *reinterpret_cast<const uint4*>(
-              a.x + ((a.dbg & 32) ? 0 : (size_t)gp[i] * kCO) + wn * 128 + ps * 64 + fq * 16 + h * 8);
+              a.x + (size_t)gp[i] * kCO + wn * 128 + ps * 64 + fq * 16 + h * 8);
   }
 
   // ---- phase 2: conv2 (3x3) from H1 -> registers ----
@@ -256,7 +252,7 @@ __global__ __launch_bounds__(512, 1) void bottleneck56_kernel(BneckArgs a) {
       pb[i] = r * kPW + (pr[i] - r * kW);  // patch slot of the pixel at tap (0, 0)
     }
 #pragma unroll 1
-    for (int tap = 0; tap < ((a.dbg & 2) ? 0 : 9); ++tap) {
+    for (int tap = 0; tap < 9; ++tap) {
       const int kh = tap / 3;
       const int toff = kh * kPW + (tap - kh * 3);
 #pragma unroll
@@ -341,17 +337,15 @@ __global__ __launch_bounds__(512, 1) void bottleneck56_kernel(BneckArgs a) {
         acc3[t] = f32x4{0.f, 0.f, 0.f, 0.f};
         if constexpr (DOWN) accd[t] = f32x4{0.f, 0.f, 0.f, 0.f};
       }
-      if (!(a.dbg & 4)) {
 #pragma unroll
-        for (int kk = 0; kk < 2; ++kk) {
-          const bf16x8 bfr = lds16(h1, swz(pr[i], kk * 4 + fq));
+      for (int kk = 0; kk < 2; ++kk) {
+        const bf16x8 bfr = lds16(h1, swz(pr[i], kk * 4 + fq));
 #pragma unroll
-          for (int t = 0; t < 4; ++t) {
-            acc3[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[t][kk], bfr, acc3[t], 0, 0, 0);
-            if constexpr (DOWN)
-              accd[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(df[t][kk], xc[i][kk], accd[t],
-                                                                0, 0, 0);
-          }
+        for (int t = 0; t < 4; ++t) {
+          acc3[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[t][kk], bfr, acc3[t], 0, 0, 0);
+          if constexpr (DOWN)
+            accd[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(df[t][kk], xc[i][kk], accd[t], 0,
+                                                              0, 0);
         }
       }
       bf16x4 o[4];  // channels fq * 16 + t * 4 .. + 4 (perm3)
@@ -393,8 +387,7 @@ __global__ __launch_bounds__(512, 1) void bottleneck56_kernel(BneckArgs a) {
         const uint4 v = *reinterpret_cast<const uint4*>(st + swz(px, c));
         const int p = (wm * 7 + i) * 16 + px;
         const int r = p / kW, cc = p - r * kW;
-        if (!(a.dbg & 16))
-          *reinterpret_cast<uint4*>(a.y + (size_t)((n * kH + y0 + r) * kW + cc) * kCO + ch0 + c * 8) = v;
+        *reinterpret_cast<uint4*>(a.y + (size_t)((n * kH + y0 + r) * kW + cc) * kCO + ch0 + c * 8) = v;
       }
     };
 #pragma unroll
@@ -435,11 +428,6 @@ hipError_t bottleneck56(const BottleneckParams& p, int batch, const void* x, voi
   a.b1 = p.b1; a.b2 = p.b2; a.b3 = p.b3; a.bd = p.bd;
   a.y = static_cast<bf16*>(y);
   a.nwg = batch * kStrips;
-  static const int dbg = [] {
-    const char* e = getenv("GALE_BNECK_DBG");
-    return e ? atoi(e) : 0;
-  }();
-  a.dbg = dbg;
   if (p.down)
     hipLaunchKernelGGL((bottleneck56_kernel<64, true>), dim3(a.nwg), dim3(512), 0, stream, a);
   else

@@ -1,6 +1,5 @@
 """Time the fused 56x56 bottleneck kernel alone (bottleneck_fused.hip) at ResNet-50 batch 256,
-identity and projection forms, against the layered kernels it replaces. One JSON line per form.
-GALE_BNECK_DBG (kernel timing experiments) is read once per process."""
+identity and projection forms, against the layered kernels it replaces. One JSON line per form."""
 
 import argparse
 import json
@@ -55,7 +54,7 @@ def main():
             torch.cuda.synchronize()
             us = e0.elapsed_time(e1) / a.iters * 1e3
             print(json.dumps(dict(form="down" if down else "identity", impl=name, batch=a.batch,
-                                  us=round(us, 1), dbg=int(os.environ.get("GALE_BNECK_DBG", "0")))),
+                                  us=round(us, 1))),
                   flush=True)
 
 
