@@ -418,21 +418,29 @@ hipError_t bottleneck56(const BottleneckParams& p, int batch, const void* x, voi
   if (!p.w1 || !p.w2 || !p.w3 || !p.b1 || !p.b2 || !p.b3 || !x || !y) return hipErrorInvalidValue;
   if (p.down && (!p.wd || !p.bd || p.cin != 64)) return hipErrorInvalidValue;
   if (!p.down && p.cin != kCO) return hipErrorInvalidValue;
-  if ((long long)batch * kH * kW * kCO >= (1ll << 31)) return hipErrorInvalidValue;
-  BneckArgs a;
-  a.x = static_cast<const bf16*>(x);
-  a.w1 = static_cast<const bf16*>(p.w1);
-  a.w2 = static_cast<const bf16*>(p.w2);
-  a.w3 = static_cast<const bf16*>(p.w3);
-  a.wd = static_cast<const bf16*>(p.wd);
-  a.b1 = p.b1; a.b2 = p.b2; a.b3 = p.b3; a.bd = p.bd;
-  a.y = static_cast<bf16*>(y);
-  a.nwg = batch * kStrips;
-  if (p.down)
-    hipLaunchKernelGGL((bottleneck56_kernel<64, true>), dim3(a.nwg), dim3(512), 0, stream, a);
-  else
-    hipLaunchKernelGGL((bottleneck56_kernel<256, false>), dim3(a.nwg), dim3(512), 0, stream, a);
-  return hipGetLastError();
+  // the kernel's element offsets are 32-bit: launch chunks of <= 2048 images (any max_batch)
+  constexpr int kChunk = 2048;
+  static_assert((long long)kChunk * kH * kW * kCO < (1ll << 31), "chunk offsets");
+  for (int c0 = 0; c0 < batch; c0 += kChunk) {
+    const int nb = batch - c0 < kChunk ? batch - c0 : kChunk;
+    BneckArgs a;
+    a.x = static_cast<const bf16*>(x) + (size_t)c0 * kH * kW * p.cin;
+    a.w1 = static_cast<const bf16*>(p.w1);
+    a.w2 = static_cast<const bf16*>(p.w2);
+    a.w3 = static_cast<const bf16*>(p.w3);
+    a.wd = static_cast<const bf16*>(p.wd);
+    a.b1 = p.b1; a.b2 = p.b2; a.b3 = p.b3; a.bd = p.bd;
+    a.y = static_cast<bf16*>(y) + (size_t)c0 * kH * kW * kCO;
+    a.nwg = nb * kStrips;
+    if (p.down)
+      hipLaunchKernelGGL((bottleneck56_kernel<64, true>), dim3(a.nwg), dim3(512), 0, stream, a);
+    else
+      hipLaunchKernelGGL((bottleneck56_kernel<256, false>), dim3(a.nwg), dim3(512), 0, stream,
+                         a);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
 }
 
 }  // namespace gale

@@ -193,15 +193,22 @@ hipError_t stem_pool(int batch, const void* x, const void* w, const float* bias,
                      hipStream_t stream) {
   if (batch <= 0) return hipSuccess;
   if (!x || !w || !bias || !y) return hipErrorInvalidValue;
-  if ((long long)batch * kIH * kIW * 4 >= (1ll << 31)) return hipErrorInvalidValue;
-  StemPoolArgs a;
-  a.x = static_cast<const bf16*>(x);
-  a.w = static_cast<const bf16*>(w);
-  a.b = bias;
-  a.y = static_cast<bf16*>(y);
-  a.nwg = batch * kStrips;
-  hipLaunchKernelGGL(stem_pool_kernel, dim3(a.nwg), dim3(512), 0, stream, a);
-  return hipGetLastError();
+  // 32-bit element offsets in the kernel: launch chunks of <= 4096 images (any max_batch)
+  constexpr int kChunk = 4096;
+  static_assert((long long)kChunk * kIH * kIW * 4 < (1ll << 31), "chunk offsets");
+  for (int c0 = 0; c0 < batch; c0 += kChunk) {
+    const int nb = batch - c0 < kChunk ? batch - c0 : kChunk;
+    StemPoolArgs a;
+    a.x = static_cast<const bf16*>(x) + (size_t)c0 * kIH * kIW * 4;
+    a.w = static_cast<const bf16*>(w);
+    a.b = bias;
+    a.y = static_cast<bf16*>(y) + (size_t)c0 * kPO * kPO * kC;
+    a.nwg = nb * kStrips;
+    hipLaunchKernelGGL(stem_pool_kernel, dim3(a.nwg), dim3(512), 0, stream, a);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
 }
 
 }  // namespace gale
