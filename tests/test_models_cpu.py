@@ -217,3 +217,26 @@ def test_resnet50_plan_fuses_56x56_bottlenecks():
     # other models / dtypes untouched
     r20 = build_plan(get_model("resnet20"), 1 << 20, fused=False, fuse_blocks=True)[0]
     assert not any(op["kind"] == OP_BOTTLENECK for op in r20)
+
+
+def test_stem_pool_not_fused_when_the_stem_output_is_read_again():
+    """fuse_stem_pool only fuses when nothing else reads the stem output (it never reaches memory
+    in the fused kernel)."""
+    from gale.models.graph import (OP_STEM_POOL, AvgPool, Conv, Head, MaxPool, Network,
+                                   build_plan)
+
+    def net(extra_reader):
+        L = [Conv("stem", "input", "s0", 3, 64, 7, stride=2, pad=3),
+             MaxPool("pool", "s0", "p0", 3, 2, 1)]
+        if extra_reader:  # a 1x1 conv on the stem output itself
+            L.append(Conv("side", "s0", "sd", 64, 64, 1))
+            L.append(AvgPool("gp", "sd", "g"))
+        else:
+            L.append(AvgPool("gp", "p0", "g"))
+        L.append(Head("fc", "g", 10))
+        return Network("stemtest", (224, 224, 3), 10, L, dataset="imagenet")
+
+    fused = build_plan(net(False), 1 << 20, fuse_blocks=True)[0]
+    kept = build_plan(net(True), 1 << 20, fuse_blocks=True)[0]
+    assert sum(op["kind"] == OP_STEM_POOL for op in fused) == 1
+    assert not any(op["kind"] == OP_STEM_POOL for op in kept)
