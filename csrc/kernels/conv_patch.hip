@@ -14,7 +14,10 @@
 // channels drop from 9 x 112 to 180 rows.
 //
 // Pipeline: weights double-buffered per step; the patch is double-buffered per input block, and
-// the next block's patch is issued with the last tap's weights. Both go by LDS-DMA
+// the next block's patch is issued with the last tap's weights. The taps of a block share its
+// patch, so the next tap's X fragments are read at the end of a step, before the barrier (3x3
+// layers 2-5 % faster; a 3-stage weight ring with counted vmcnt was slower,
+// profiles/r5_conv_patch_ab.jsonl). Both go by LDS-DMA
 // (global_load_lds_dwordx4), with the same source-side XOR bank swizzle as conv_gemm (slot s of
 // LDS row r holds 16-byte chunk s ^ ((r >> 1) & 7)). Fragment rows map pixel p of the tile to
 // patch row (p / W + kh) * (W + 2) + p % W + kw; rows past the tile's pixels read a zero row.
@@ -61,7 +64,7 @@ struct PatchArgs {
 template <int BN, int PRR>
 __global__ __launch_bounds__(256, 2)
 void conv_patch_kernel(PatchArgs a) {
-  constexpr int WM = 2, PB = 2, TPS = 1;  // waves along the pixels, patch buffers, taps per step
+  constexpr int WM = 2;              // waves along the pixels
   constexpr int kBM = WM * 64;       // MFMA rows per tile (pixels P <= kBM; the rest read zeros)
   constexpr int WN = 2, NW = WM * WN;
   constexpr int TM = kBM / WM / 16;  // 16-pixel tiles per wave
@@ -69,8 +72,8 @@ void conv_patch_kernel(PatchArgs a) {
   constexpr int WI = BN / (8 * NW);  // weight wave-instructions per wave per step
   constexpr int NPJ = PRR / 8;       // patch wave-instructions
   constexpr int PJ = (NPJ + NW - 1) / NW;  // ... per wave
-  constexpr int SPB = (9 + TPS - 1) / TPS;  // k-steps per 64-channel input block
-  constexpr int WST = TPS * BN * 128;  // bytes per weight stage
+  constexpr int SPB = 9;             // k-steps (taps) per 64-channel input block
+  constexpr int WST = BN * 128;      // bytes per weight stage
   constexpr int PST = PRR * 128;     // bytes per patch stage
   constexpr int CW = BN / WN;        // epilogue geometry (as conv_gemm)
   constexpr int EPS = CW + 4;
@@ -78,14 +81,15 @@ void conv_patch_kernel(PatchArgs a) {
   constexpr int RPI = 64 / LPR;
   constexpr int HALF = TM / 2 * 16;
   constexpr int NRI = HALF / RPI;
-  constexpr int LDS_BYTES = 2 * WST + PB * PST;
+  constexpr int LDS_BYTES = 2 * WST + 2 * PST;
   static_assert(NW * HALF * EPS * 4 <= LDS_BYTES, "epilogue staging exceeds the LDS allocation");
   static_assert(WI >= 1, "tile too small for the workgroup");
   __shared__ __attribute__((aligned(1024))) uint8_t lds[LDS_BYTES];
   uint8_t* const wbuf = lds;
   uint8_t* const pbuf = lds + 2 * WST;
 
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  // (wave index in an SGPR: the LDS-DMA destinations (M0) are then scalar arithmetic)
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wave >> 1, wn = wave & 1;
 
   // XCD-contiguous tile order (bijective for any nwg): the channel tiles of one row block, which
@@ -116,12 +120,15 @@ void conv_patch_kernel(PatchArgs a) {
         poff[j] = (((img + ii) * a.H + yy) * a.W + xx) * a.Cin + chunk * 8;
     }
   }
-  const bf16* wsrc[WI];
+  // weight rows: a scalar base per step plus a 32-bit per-lane byte offset (the saddr form of
+  // the LDS-DMA load: no 64-bit vector address arithmetic in the loop)
+  const char* const wtile = reinterpret_cast<const char*>(a.w + (size_t)nt * BN * a.Kpad);
+  int wlo[WI];
 #pragma unroll
   for (int j = 0; j < WI; ++j) {
     const int row = (wave * WI + j) * 8 + srow;
     const int chunk = slot ^ ((row >> 1) & 7);
-    wsrc[j] = a.w + (size_t)(nt * BN + row) * a.Kpad + chunk * 8;
+    wlo[j] = (row * a.Kpad + chunk * 8) * 2;
   }
   auto stage_patch = [&](int cb, uint8_t* buf) __attribute__((always_inline)) {
 #pragma unroll
@@ -134,19 +141,12 @@ void conv_patch_kernel(PatchArgs a) {
       }
     }
   };
-  // step s = cb * SPB + taps [TPS*(s % SPB), +TPS): weight columns k = tap * Cin + cb * 64
-  // (k = (kh*3 + kw)*Cin + ci)
+  // step s = cb * SPB + tap: weight columns k = tap * Cin + cb * 64 (k = (kh*3 + kw)*Cin + ci)
   auto stage_w = [&](int s, uint8_t* buf) __attribute__((always_inline)) {
-    const int cb = s / SPB, t0 = (s - cb * SPB) * TPS;
+    const int cb = s / SPB, tap = s - cb * SPB;
+    const char* const wk = wtile + (size_t)(tap * a.Cin + cb * 64) * 2;
 #pragma unroll
-    for (int tt = 0; tt < TPS; ++tt) {
-      if (t0 + tt < 9) {
-        const int k0 = (t0 + tt) * a.Cin + cb * 64;
-#pragma unroll
-        for (int j = 0; j < WI; ++j)
-          glds16(wsrc[j] + k0, buf + tt * BN * 128 + (wave * WI + j) * 1024);
-      }
-    }
+    for (int j = 0; j < WI; ++j) glds16(wk + wlo[j], buf + (wave * WI + j) * 1024);
   };
 
   // ---- fragment geometry ----
@@ -177,51 +177,63 @@ void conv_patch_kernel(PatchArgs a) {
 #pragma unroll
     for (int t = 0; t < TN; ++t) acc[i][t] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  stage_patch(0, pbuf);
-  stage_w(0, wbuf);
-  for (int s = 0; s < a.nsteps; ++s) {
+  // X (patch) fragments of tap `tap` from patch buffer pc
+  auto read_x = [&](const uint8_t* pc, int tap, bf16x8 (&bx)[2][TM])
+      __attribute__((always_inline)) {
+    const int kh = tap / 3;
+    const int toff = kh * a.PW + (tap - kh * 3);
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int row = pbase[i] >= 0 ? pbase[i] + toff : a.PR;  // (row PR: zeros)
+      const int xo = row * 128, xs = (row >> 1) & 7;
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+        bx[kk][i] = *reinterpret_cast<const bf16x8*>(pc + xo + (((kk * 4 + fq) ^ xs) << 4));
+    }
+  };
+  // One k-step (one tap of 64 input channels). The taps of one input block share its patch,
+  // so the next tap's X fragments are read at the end of this step, before the barrier, and
+  // only the weight fragments wait for the step's DMA; the next step's DMA is issued right
+  // after those reads.
+  auto step = [&](int s, bf16x8 (&bx)[2][TM], bf16x8 (&bn)[2][TM])
+      __attribute__((always_inline)) {
     // step s has landed (vmcnt(0)); every wave is done with step s-1, whose weight buffer (and,
     // on a block's last tap, the previous block's patch buffer) is refilled below
     __syncthreads();
     const int cb = s / SPB, sl = s - cb * SPB;
     const uint8_t* wcur = wbuf + (s & 1) * WST;
-    const uint8_t* pcur = pbuf + (PB == 2 ? (cb & 1) * PST : 0);
+    const uint8_t* pcur = pbuf + (cb & 1) * PST;
+    if (sl == 0) read_x(pcur, 0, bx);  // a block's first tap: its patch has just landed
+    bf16x8 af[2][TN];
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int t = 0; t < TN; ++t)
+        af[kk][t] = *reinterpret_cast<const bf16x8*>(wcur + wrow_off[t] +
+                                                     (((kk * 4 + fq) ^ wsw[t]) << 4));
     if (s + 1 < a.nsteps) {
       stage_w(s + 1, wbuf + ((s + 1) & 1) * WST);
-      if (PB == 2 && sl == SPB - 1) stage_patch(cb + 1, pbuf + ((cb + 1) & 1) * PST);
+      if (sl == SPB - 1) stage_patch(cb + 1, pbuf + ((cb + 1) & 1) * PST);
     }
 #pragma unroll
-    for (int tt = 0; tt < TPS; ++tt) {
-      const int tap = sl * TPS + tt;
-      const uint8_t* wtap = wcur + tt * BN * 128;
-      const int kh = tap / 3;
-      const int toff = kh * a.PW + (tap - kh * 3);
-      int xoff[TM], xsw[TM];
+    for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        const int row = pbase[i] >= 0 ? pbase[i] + toff : a.PR;  // (row PR: zeros)
-        xoff[i] = row * 128;
-        xsw[i] = (row >> 1) & 7;
-      }
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        const int chunk = kk * 4 + fq;
-        bf16x8 af[TN], bfr[TM];
+      for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int t = 0; t < TN; ++t)
-          af[t] = *reinterpret_cast<const bf16x8*>(wtap + wrow_off[t] + ((chunk ^ wsw[t]) << 4));
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-          bfr[i] = *reinterpret_cast<const bf16x8*>(pcur + xoff[i] + ((chunk ^ xsw[i]) << 4));
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-          for (int t = 0; t < TN; ++t)
-            acc[i][t] =
-                __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[t], bfr[i], acc[i][t], 0, 0, 0);
-      }
-    }
+          acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[kk][t], bx[kk][i], acc[i][t],
+                                                              0, 0, 0);
+    if (sl + 1 < SPB) read_x(pcur, sl + 1, bn);
+  };
+  bf16x8 xa[2][TM], xb[2][TM];
+  stage_patch(0, pbuf);
+  stage_w(0, wbuf);
+  int s = 0;
+  for (; s + 1 < a.nsteps; s += 2) {  // (two steps per iteration: the fragment sets alternate)
+    step(s, xa, xb);
+    step(s + 1, xb, xa);
   }
+  if (s < a.nsteps) step(s, xa, xb);
 
   // ---- epilogue through LDS (as conv_gemm): fp32 (acc + bias) per wave, read back 8 channels
   // per lane, residual / ReLU, 16-byte bf16 stores of whole 128-byte rows ----
