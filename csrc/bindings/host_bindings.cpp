@@ -12,6 +12,7 @@
 #include <thread>
 
 #include "../codec/json_codec.h"
+#include "gale/llc_pair.h"
 #include "../codec/text_pack.h"
 #include "../kafka/broker.h"
 #include "../kafka/client.h"
@@ -435,6 +436,10 @@ void bind_host(py::module_& m) {
   }, py::arg("data"), py::arg("H"), py::arg("W"), py::arg("C"), py::arg("max_images") = -1);
   // ---- nibble transport (text_pack.h) ----
   m.def("text_pack_fast", &codec::text_pack_fast);
+  // L3-domain pairing (gale/llc_pair.h), for tests: each call acts on the calling thread
+  m.def("llc_pin_self_next_domain", &llc::pin_self_next_domain);
+  m.def("llc_register_local_port", &llc::register_local_port);
+  m.def("llc_pin_self_for_peer", &llc::pin_self_for_peer);
   m.def("set_pack_stream_stores", &codec::set_pack_stream_stores,
         "non-temporal stores for the packed stream (default on; A/B switch)");
   m.def("text_pack", [](py::bytes b, bool force_scalar) {

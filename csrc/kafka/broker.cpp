@@ -1,5 +1,6 @@
 // Embedded Kafka-protocol broker (see broker.h).
 #include "broker.h"
+#include "gale/llc_pair.h"
 #include "gale/thread_name.h"
 
 #include <arpa/inet.h>
@@ -489,9 +490,18 @@ void Broker::serve(int fd) {
   Conn c;
   c.fd = fd;
   std::string frame;
+  // L3 pairing with an in-process reader (gale/llc_pair.h): its registration may follow our
+  // accept, so look again before each of the first requests
+  int peer_port = -1, pair_tries = llc::enabled() ? 64 : 0;
+  {
+    sockaddr_in pa{};
+    socklen_t pl = sizeof(pa);
+    if (getpeername(fd, reinterpret_cast<sockaddr*>(&pa), &pl) == 0) peer_port = ntohs(pa.sin_port);
+  }
   while (running_) {
     char hdr[4];
     if (!read_exact(fd, hdr, 4)) break;
+    if (pair_tries > 0) pair_tries = llc::pin_self_for_peer(peer_port) ? 0 : pair_tries - 1;
     Reader hr(reinterpret_cast<const uint8_t*>(hdr), 4);
     const int32_t sz = hr.i32();
     if (sz < 0 || sz > (int32_t)std::min<int64_t>(cfg_.max_message_bytes + (16 << 20), 1 << 30))

@@ -1,5 +1,6 @@
 // Kafka-protocol client: connections, metadata, producer, consumer (see client.h).
 #include "client.h"
+#include "gale/llc_pair.h"
 #include "gale/thread_name.h"
 
 #include "compress.h"
@@ -103,6 +104,11 @@ Connection::Connection(const std::string& host, int port, const ClientConfig& cf
   timeval tv{cfg.request_timeout_ms / 1000, (cfg.request_timeout_ms % 1000) * 1000};
   setsockopt(fd_, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof(tv));
   setsockopt(fd_, SOL_SOCKET, SO_SNDTIMEO, &tv, sizeof(tv));
+  // an in-process broker pins the thread serving this connection to the reader's L3 domain
+  sockaddr_in la{};
+  socklen_t ll = sizeof(la);
+  if (getsockname(fd_, reinterpret_cast<sockaddr*>(&la), &ll) == 0)
+    llc::register_local_port(ntohs(la.sin_port));
 }
 
 Connection::~Connection() {

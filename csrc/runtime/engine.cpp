@@ -1,5 +1,6 @@
 // The gale serving engine (see engine.h).
 #include "engine.h"
+#include "gale/llc_pair.h"
 #include "gale/thread_name.h"
 
 #include <hip/hip_runtime.h>
@@ -337,6 +338,9 @@ void Engine::start() {
     sources_.emplace_back([this, i] {
       name_thread("gl-src", i);
       pin_thread(slot_dev_[(size_t)i % slot_dev_.size()]);
+      // one L3 domain of that set, shared with the in-process broker thread that serves this
+      // source's connection (gale/llc_pair.h)
+      llc::pin_self_next_domain();
       source_loop(i);
     });
   group_stop_ = false;

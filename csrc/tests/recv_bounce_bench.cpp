@@ -7,11 +7,15 @@
 //           --text-pack; a second pass over memory),
 //   bounce  recv() into a small per-thread bounce buffer (cache resident), pack each piece from
 //           there into the pool: only the packed half is written to memory.
-// Usage: recv_bounce_bench <mode> <pairs> <seconds> [piece_kb]
+// The sender either splices the stored pages (zero copy) or copies them with send() as the
+// broker's default writev path does; sender and receiver of a pair can be pinned to two cores of
+// one CCD (shared L3: the receive copy reads what the sender just wrote from L3) or of two CCDs.
+// Usage: recv_bounce_bench <mode> <pairs> <seconds> [piece_kb] [splice|copy] [none|same|cross]
 #include <fcntl.h>
 #include <netinet/in.h>
 #include <netinet/tcp.h>
 #include <pthread.h>
+#include <sched.h>
 #include <signal.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -60,7 +64,34 @@ std::vector<uint8_t> make_store(size_t n, unsigned seed) {
   return s;
 }
 
-void sender(int fd, unsigned seed) {
+void pin_to(int cpu) {
+  if (cpu < 0) return;
+  cpu_set_t set;
+  CPU_ZERO(&set);
+  CPU_SET(cpu, &set);
+  pthread_setaffinity_np(pthread_self(), sizeof(set), &set);
+}
+
+std::atomic<double> g_send_cpu{0};
+
+void sender_copy(int fd, unsigned seed, int cpu) {
+  pin_to(cpu);
+  std::vector<uint8_t> store = make_store(256u << 20, seed);
+  const double c0 = thread_cpu_s();
+  size_t pos = 0;
+  while (!g_stop) {
+    if (pos + (1u << 20) > store.size()) pos = 0;
+    const ssize_t k = send(fd, store.data() + pos, 1u << 20, 0);
+    if (k <= 0) break;
+    pos += (size_t)k;
+  }
+  double c = thread_cpu_s() - c0, cur = g_send_cpu.load();
+  while (!g_send_cpu.compare_exchange_weak(cur, cur + c)) {
+  }
+}
+
+void sender(int fd, unsigned seed, int cpu) {
+  pin_to(cpu);
   std::vector<uint8_t> store = make_store(256u << 20, seed);
   int p[2];
   if (pipe(p) != 0) return;
@@ -91,7 +122,8 @@ struct Result {
   double bytes = 0, cpu = 0;
 };
 
-void receiver(int fd, const char* mode, size_t piece, Result* res) {
+void receiver(int fd, const char* mode, size_t piece, Result* res, int cpu) {
+  pin_to(cpu);
   // pool: 64 chunks of (body + packed + tab), cycled, so writes stream to DRAM
   const size_t chunk = gale::codec::pack_layout_bytes(kBody) + 4096;
   const int nchunks = 64;
@@ -152,6 +184,15 @@ int main(int argc, char** argv) {
   const int pairs = atoi(argv[2]);
   const double secs = atof(argv[3]);
   const size_t piece = (size_t)(argc > 4 ? atoi(argv[4]) : 256) << 10;
+  const bool copy = argc > 5 && !strcmp(argv[5], "copy");
+  const char* pin = argc > 6 ? argv[6] : "none";
+  // receivers on the first core of every other CCD (8 cores per CCD, node 0 = CPUs 0-63);
+  // senders on the next core of the same CCD, or on the next CCD
+  auto rcpu = [&](int i) { return strcmp(pin, "none") ? (i * 16) % 64 : -1; };
+  auto scpu = [&](int i) {
+    return !strcmp(pin, "same") ? (i * 16) % 64 + 1 : !strcmp(pin, "cross") ? (i * 16) % 64 + 8
+                                                                            : -1;
+  };
   std::vector<std::thread> th;
   std::vector<Result> res((size_t)pairs);
   std::vector<int> fds;
@@ -175,8 +216,11 @@ int main(int argc, char** argv) {
     setsockopt(sv[1], SOL_SOCKET, SO_RCVBUF, &bufsz, sizeof(bufsz));
     fds.push_back(sv[0]);
     fds.push_back(sv[1]);
-    th.emplace_back(sender, sv[0], (unsigned)i + 1);
-    th.emplace_back(receiver, sv[1], mode, piece, &res[(size_t)i]);
+    if (copy)
+      th.emplace_back(sender_copy, sv[0], (unsigned)i + 1, scpu(i));
+    else
+      th.emplace_back(sender, sv[0], (unsigned)i + 1, scpu(i));
+    th.emplace_back(receiver, sv[1], mode, piece, &res[(size_t)i], rcpu(i));
   }
   const double t0 = now_s();
   std::this_thread::sleep_for(std::chrono::milliseconds((int)(secs * 1000)));
@@ -189,8 +233,10 @@ int main(int argc, char** argv) {
     bytes += r.bytes;
     cpu += r.cpu;
   }
-  printf("{\"mode\": \"%s\", \"pairs\": %d, \"piece_kb\": %zu, \"gb_s\": %.2f, "
-         "\"recv_cores\": %.2f, \"gb_per_recv_core_s\": %.2f}\n",
-         mode, pairs, piece >> 10, bytes / el / 1e9, cpu / el, bytes / 1e9 / cpu);
+  printf("{\"mode\": \"%s\", \"sender\": \"%s\", \"pin\": \"%s\", \"pairs\": %d, "
+         "\"piece_kb\": %zu, \"gb_s\": %.2f, \"recv_cores\": %.2f, "
+         "\"gb_per_recv_core_s\": %.2f, \"send_cores\": %.2f}\n",
+         mode, copy ? "copy" : "splice", pin, pairs, piece >> 10, bytes / el / 1e9, cpu / el,
+         bytes / 1e9 / cpu, g_send_cpu.load() / el);
   return 0;
 }
