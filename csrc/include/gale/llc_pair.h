@@ -6,9 +6,10 @@
 // that serves that connection looks its peer port up and pins itself to the same domain. The
 // broker's copy of a fetch response into the socket buffer then lands in the L3 that the
 // receive copy reads: 19.8 GB/s per receiving core with the pair on one CCD against 12.9 GB/s
-// across two (profiles/r5_llc_pair.jsonl, csrc/tests/recv_bounce_bench.cpp). In the whole
-// pipeline it measured no gain (same file: the scheduler already keeps most pairs close), so it
-// is opt-in.
+// across two (profiles/r5_llc_pair.jsonl, csrc/tests/recv_bounce_bench.cpp). That holds for a
+// copying sender only: bench.py's broker splices the stored batches (zero copy), so the receive
+// copy reads DRAM either way, and in the pipeline the pairing measured no gain (same file). It
+// is opt-in, for a broker that copies.
 //
 // Only meaningful when broker and consumers share a process (bench.py, the tests); a remote
 // broker simply never finds a registration. GALE_LLC_PAIR=1 turns it on.

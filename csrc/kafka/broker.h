@@ -47,8 +47,9 @@ struct BrokerConfig {
   // Fetch responses send stored record batches without a user->kernel copy (vmsplice the
   // immutable batch pages into a pipe, splice the pipe into the socket), as a Kafka broker's
   // sendfile() from the page cache does. Small/owned pieces (headers) are written normally.
-  // Measured on loopback (bench.py --broker-zero-copy): no gain, the splice page pinning costs
-  // about what the copy did; off by default.
+  // Off by default here; bench.py turns it on (profiles/archive/r3_broker_zero_copy_default.jsonl):
+  // with 11 loopback connections the transport costs 0.161 core-s per GB spliced against 0.206
+  // copied, sender and receiver together (profiles/r5_llc_pair.jsonl).
   bool zero_copy = false;
   // log.message.timestamp.type=LogAppendTime: every appended batch is stamped with the broker's
   // wall clock (attributes timestamp-type bit + maxTimestamp, CRC patched in O(log n) without

@@ -74,6 +74,8 @@ void pin_to(int cpu) {
 
 std::atomic<double> g_send_cpu{0};
 
+void add_send_cpu(double c);
+
 void sender_copy(int fd, unsigned seed, int cpu) {
   pin_to(cpu);
   std::vector<uint8_t> store = make_store(256u << 20, seed);
@@ -85,7 +87,11 @@ void sender_copy(int fd, unsigned seed, int cpu) {
     if (k <= 0) break;
     pos += (size_t)k;
   }
-  double c = thread_cpu_s() - c0, cur = g_send_cpu.load();
+  add_send_cpu(thread_cpu_s() - c0);
+}
+
+void add_send_cpu(double c) {
+  double cur = g_send_cpu.load();
   while (!g_send_cpu.compare_exchange_weak(cur, cur + c)) {
   }
 }
@@ -93,6 +99,11 @@ void sender_copy(int fd, unsigned seed, int cpu) {
 void sender(int fd, unsigned seed, int cpu) {
   pin_to(cpu);
   std::vector<uint8_t> store = make_store(256u << 20, seed);
+  const double c0 = thread_cpu_s();
+  struct Acc {
+    double c0;
+    ~Acc() { add_send_cpu(thread_cpu_s() - c0); }
+  } acc{c0};
   int p[2];
   if (pipe(p) != 0) return;
   fcntl(p[1], F_SETPIPE_SZ, 1 << 20);
