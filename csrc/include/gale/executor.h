@@ -34,6 +34,9 @@ enum OpKind : int {
                       // w3 b3 [wd bd]; p[0] = cin, p[1] = down (projection shortcut)
   OP_STEM_POOL = 10,  // ResNet-50 stem conv + max-pool (stem_pool); conv = the stem's desc,
                       // w / bias = its weights; p[0..7] = the max-pool's H W C k s pad Ho Wo
+  OP_CONV_PROJ = 11,  // bottleneck conv3 + projection shortcut as one GEMM (conv2d_gemm_proj):
+                      // conv = conv3's desc, in = its input, res = the block input (the
+                      // projection's source); ptrs = w3 b3 wd bd; p[0..4] = H2 W2 Cin2 stride2 Kpad2
 };
 
 // Buffer ids: 0 = network input (fp32 NHWC), 1 = network output (fp32 [B, classes]),

@@ -63,6 +63,16 @@ bool conv_gemm_supported(const ConvDesc& d, int batch, bool has_res);
 // conv path selection (tests / A-B benches): 0 auto, 1 never GEMM, 2 GEMM whenever the shape allows
 void set_conv_path(int mode);
 int conv_path();
+// conv3 of a ResNet bottleneck with its projection shortcut as ONE GEMM over the concatenated
+// reduction: y = act(conv1x1(x, w) + bias + conv1x1_stride2(x2, w2) + bias2). d: the 1x1
+// stride-1 conv on x (no residual); x2 [B][H2][W2][Cin2] bf16 sampled at stride2 onto d's output
+// grid, w2 [Npad][Kpad2]. The projection's output tensor never exists.
+bool conv_gemm_proj_supported(const ConvDesc& d, int batch, int H2, int W2, int Cin2,
+                              int stride2, int Kpad2);
+hipError_t conv2d_gemm_proj(const ConvDesc& d, int batch, const void* x, const void* w,
+                            const float* bias, const void* x2, int H2, int W2, int Cin2,
+                            int stride2, int Kpad2, const void* w2, const float* bias2, void* y,
+                            hipStream_t stream);
 hipError_t conv2d_gemm(const ConvDesc& d, int batch, const void* x, const void* w,
                        const float* bias, const void* res, void* y, hipStream_t stream);
 

@@ -49,6 +49,13 @@ struct GemmConvArgs {
   int cin_blocks;  // Cin / 64
   int relu, has_res, out_f32;
   int n_tiles, nwg;
+  // DUAL (conv2d_gemm_proj): k-steps [nkb1, nkb) read a second 1x1 source - the bottleneck's
+  // projection shortcut, x2 [B][H2][W2][Cin2] sampled at stride2, weights w2 [Npad][Kpad2] - so
+  // conv3 + projection is one GEMM over the concatenated K, with bias + bias2
+  const bf16* x2;
+  const bf16* w2;
+  const float* bias2;
+  int H2, W2, Cin2, stride2, Kpad2, nkb1;
 };
 
 __device__ __forceinline__ void glds16(const void* src, void* lds_base) {
@@ -65,7 +72,7 @@ __device__ __forceinline__ void glds16(const void* src, void* lds_base) {
 // (Variants measured and removed in round 3 - 256 x 128 tiles with 8 waves, a three-stage
 // 128 x 64 ring, register staging instead of LDS-DMA, the single-stage form for 2-4 k-steps: all
 // slower at ResNet-50 batch 256, profiles/archive/r2_resnet50_gemm_ab.txt.)
-template <int BM, int BN, bool STEM, int NST>
+template <int BM, int BN, bool STEM, int NST, bool DUAL = false>
 __global__ __launch_bounds__(256, NST == 1 ? 4 : 2)
 void conv_gemm_kernel(GemmConvArgs a) {
   constexpr int WM = BM / 64;                   // waves as WM (pixels) x 2 (channels)
@@ -126,9 +133,37 @@ void conv_gemm_kernel(GemmConvArgs a) {
     const int chunk = slot ^ ((row >> 1) & 7);
     wsrc[j] = a.w + (size_t)(nt * BN + row) * a.Kpad + chunk * 8;
   }
+  // DUAL: the second source's row of each staged output pixel (or -1 past M) and weight rows
+  int xoff2[DUAL ? XI : 1];
+  const bf16* wsrc2[DUAL ? WI : 1];
+  if (DUAL) {
+#pragma unroll
+    for (int j = 0; j < XI; ++j) {
+      const int row = (wave * XI + j) * 8 + srow;
+      const int m = mt * BM + row;
+      const int chunk = slot ^ ((row >> 1) & 7);
+      xoff2[j] = -1;
+      if (m < a.M) {
+        const int n = m / a.HWo;
+        const int rem = m - n * a.HWo;
+        const int ho = rem / a.Wo;
+        const int wo = rem - ho * a.Wo;
+        xoff2[j] = ((n * a.H2 + ho * a.stride2) * a.W2 + wo * a.stride2) * a.Cin2 + chunk * 8;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < WI; ++j) {
+      const int row = (wave * WI + j) * 8 + srow;
+      const int chunk = slot ^ ((row >> 1) & 7);
+      wsrc2[j] = a.w2 + (size_t)(nt * BN + row) * a.Kpad2 + chunk * 8;
+    }
+  }
 
   // source of im2col piece j (8 rows x 128 B per wave-instruction) of k-step kb
   auto xsrc = [&](int kb, int j) __attribute__((always_inline)) -> const void* {
+    if (DUAL && kb >= a.nkb1)
+      return xoff2[j] >= 0 ? (const void*)(a.x2 + xoff2[j] + (kb - a.nkb1) * 64)
+                           : (const void*)(g_zero_rows + 16 * (lane & 3));
     if (STEM) {
       const int hi = xh[j] + 2 * kb;
       return (unsigned)hi < (unsigned)a.H ? (const void*)(a.x + xoff[j] + hi * a.W * 4)
@@ -149,7 +184,8 @@ void conv_gemm_kernel(GemmConvArgs a) {
     for (int j = 0; j < XI; ++j) glds16(xsrc(kb, j), buf + (wave * XI + j) * 1024);
 #pragma unroll
     for (int j = 0; j < WI; ++j)
-      glds16(wsrc[j] + kb * 64, buf + BM * 128 + (wave * WI + j) * 1024);
+      glds16(DUAL && kb >= a.nkb1 ? wsrc2[j] + (kb - a.nkb1) * 64 : wsrc[j] + kb * 64,
+             buf + BM * 128 + (wave * WI + j) * 1024);
   };
   f32x4 acc[TM][TN];
 #pragma unroll
@@ -250,7 +286,11 @@ void conv_gemm_kernel(GemmConvArgs a) {
 #pragma unroll
     for (int t = 0; t < TN; ++t) {
       const int cl = t * 16 + fq * 4;
-      const float4 b = *reinterpret_cast<const float4*>(a.bias + c0 + cl);
+      float4 b = *reinterpret_cast<const float4*>(a.bias + c0 + cl);
+      if (DUAL) {
+        const float4 b2 = *reinterpret_cast<const float4*>(a.bias2 + c0 + cl);
+        b = make_float4(b.x + b2.x, b.y + b2.y, b.z + b2.z, b.w + b2.w);
+      }
 #pragma unroll
       for (int ii = 0; ii < TM / 2; ++ii) {
         const int i = h * (TM / 2) + ii;
@@ -335,6 +375,9 @@ hipError_t conv2d_gemm(const ConvDesc& d, int batch, const void* x, const void* 
   a.cin_blocks = d.stem ? 1 : d.Cin / 64;
   a.relu = d.relu;
   a.has_res = d.has_res && res != nullptr;
+  a.x2 = nullptr; a.w2 = nullptr; a.bias2 = nullptr;
+  a.H2 = a.W2 = a.Cin2 = a.stride2 = a.Kpad2 = 0;
+  a.nkb1 = a.nkb;
   // 64-channel tiles for the single-k-step (K = 64) 1x1 convs: these are bound by their
   // epilogue traffic, and half-width tiles (24 KB of LDS, 91 VGPRs) put 5 workgroups on a CU
   // instead of 4 (ResNet-50 batch 256: 4.87 -> 4.81 ms; at K = 128 / 256 / 512 the same change
@@ -372,6 +415,53 @@ hipError_t conv2d_gemm(const ConvDesc& d, int batch, const void* x, const void* 
       hipLaunchKernelGGL((conv_gemm_kernel<BM, 64, false, 2>), dim3(a.nwg), dim3(256), 0, stream,
                          a);
   }
+  return hipGetLastError();
+}
+
+bool conv_gemm_proj_supported(const ConvDesc& d, int batch, int H2, int W2, int Cin2,
+                              int stride2, int Kpad2) {
+  // (no conv_path switch: like the fused block kernels this op has no other implementation)
+  if (d.fp8 || d.in_f32 || d.f32 || d.out_f32 || d.stem || d.has_res) return false;
+  if (d.KH != 1 || d.KW != 1 || d.stride != 1 || d.pad != 0) return false;
+  if (d.Cin % 64 != 0 || d.K != d.Cin || d.Kpad != d.K || d.Ho != d.H || d.Wo != d.W) return false;
+  if (Cin2 % 64 != 0 || Kpad2 != Cin2 || stride2 < 1) return false;
+  if ((H2 - 1) / stride2 + 1 != d.Ho || (W2 - 1) / stride2 + 1 != d.Wo) return false;
+  if (d.Npad % 128 != 0 || d.Npad < d.Cout || d.Cout % 8 != 0) return false;
+  return (long long)batch * d.Ho * d.Wo < (1ll << 31) &&
+         (long long)batch * d.H * d.W * d.Cin < (1ll << 31) &&
+         (long long)batch * H2 * W2 * Cin2 < (1ll << 31);
+}
+
+hipError_t conv2d_gemm_proj(const ConvDesc& d, int batch, const void* x, const void* w,
+                            const float* bias, const void* x2, int H2, int W2, int Cin2,
+                            int stride2, int Kpad2, const void* w2, const float* bias2, void* y,
+                            hipStream_t stream) {
+  if (!conv_gemm_proj_supported(d, batch, H2, W2, Cin2, stride2, Kpad2))
+    return hipErrorInvalidValue;
+  GemmConvArgs a;
+  a.x = static_cast<const bf16*>(x);
+  a.w = static_cast<const bf16*>(w);
+  a.bias = bias;
+  a.res = nullptr;
+  a.y = y;
+  a.out_f32 = 0;
+  a.M = batch * d.Ho * d.Wo;
+  a.H = d.H; a.W = d.W; a.Cin = d.Cin; a.HWo = d.Ho * d.Wo; a.Wo = d.Wo; a.Cout = d.Cout;
+  a.KW = 1; a.stride = 1; a.pad = 0; a.Kpad = d.Kpad;
+  a.cin_blocks = d.Cin / 64;
+  a.nkb1 = d.Cin / 64;
+  a.nkb = a.nkb1 + Cin2 / 64;
+  a.relu = d.relu;
+  a.has_res = 0;
+  a.x2 = static_cast<const bf16*>(x2);
+  a.w2 = static_cast<const bf16*>(w2);
+  a.bias2 = bias2;
+  a.H2 = H2; a.W2 = W2; a.Cin2 = Cin2; a.stride2 = stride2; a.Kpad2 = Kpad2;
+  constexpr int BM = 128;
+  a.n_tiles = d.Npad / 128;
+  a.nwg = (a.M + BM - 1) / BM * a.n_tiles;
+  hipLaunchKernelGGL((conv_gemm_kernel<BM, 128, false, 2, true>), dim3(a.nwg), dim3(256), 0,
+                     stream, a);
   return hipGetLastError();
 }
 

@@ -203,6 +203,13 @@ void Executor::launch_ops(size_t begin, size_t end, int batch, void* const* bufs
         e = bottleneck56(bp, batch, in, out, stream);
         break;
       }
+      case OP_CONV_PROJ:
+        if (op.ptrs.size() != 4u || res == nullptr)
+          throw std::invalid_argument("conv_proj op: bad operands");
+        e = conv2d_gemm_proj(op.conv, batch, in, op.ptrs[0], static_cast<const float*>(op.ptrs[1]),
+                             res, op.p[0], op.p[1], op.p[2], op.p[3], op.p[4], op.ptrs[2],
+                             static_cast<const float*>(op.ptrs[3]), out, stream);
+        break;
       case OP_STEM_POOL:
         if (!stem_pool_supported(op.conv, op.p[0], op.p[1], op.p[2], op.p[3], op.p[4], op.p[5],
                                  op.p[6], op.p[7]))

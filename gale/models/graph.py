@@ -393,7 +393,7 @@ def act_scales_from_packed(net: Network, packed: torch.Tensor) -> Dict[str, floa
 # --------------------------------------------------------------------------------------------
 
 (OP_CONV, OP_MAXPOOL, OP_AVGPOOL, OP_HEAD, OP_SOFTMAX, OP_RESNET20, OP_STEM_PACK, OP_BN_ACT,
- OP_LENET5, OP_BOTTLENECK, OP_STEM_POOL) = range(11)
+ OP_LENET5, OP_BOTTLENECK, OP_STEM_POOL, OP_CONV_PROJ) = range(12)
 
 
 def is_cifar_resnet20(net: Network) -> bool:
@@ -541,6 +541,54 @@ def fuse_bottlenecks(ops: List[dict]) -> List[dict]:
     return out
 
 
+def projection_pairs(net: Network) -> Dict[str, str]:
+    """Bottleneck conv3 layers whose residual is a strided 1x1 projection read by nothing else:
+    {conv3 name: projection name}. Each pair can run as one GEMM over the concatenated
+    reduction (``fuse_projections``); stride-1 projections stay with the 56x56 block kernel."""
+    by_out = {L.out: L for L in net.layers if isinstance(L, Conv)}
+    readers: Dict[str, int] = {}
+    for L in net.layers:
+        readers[L.inp] = readers.get(L.inp, 0) + 1
+        if isinstance(L, Conv) and L.residual is not None:
+            readers[L.residual] = readers.get(L.residual, 0) + 1
+    pairs = {}
+    for L in net.layers:
+        if not (isinstance(L, Conv) and L.residual is not None and L.res_mode == "identity"
+                and L.k == 1 and L.stride == 1 and L.pad == 0 and not L.out_f32):
+            continue
+        D = by_out.get(L.residual)
+        if (D is not None and D.k == 1 and D.stride > 1 and D.pad == 0 and not D.relu
+                and D.residual is None and not D.out_f32 and D.cout == L.cout
+                and readers.get(D.out, 0) == 1 and D.cin % 64 == 0 and L.cin % 64 == 0):
+            pairs[L.name] = D.name
+    return pairs
+
+
+def fuse_projections(ops: List[dict], pairs: Dict[int, int]) -> List[dict]:
+    """Each (projection, conv3) op pair of ``pairs`` ({index of conv3: index of the projection},
+    op indices) becomes ONE ``OP_CONV_PROJ`` at conv3's place (csrc/kernels/conv_gemm.hip
+    conv2d_gemm_proj: the projection's output tensor never exists). build_plan keeps the block
+    input alive up to conv3 for these."""
+    drop = set(pairs.values())
+    out: List[dict] = []
+    for i, op in enumerate(ops):
+        if i in drop:
+            continue
+        if i in pairs:
+            dn = ops[pairs[i]]
+            dd, cd = dn["conv"], dict(op["conv"])
+            for k in ("has_res", "res_H", "res_W", "res_C", "res_stride"):
+                cd.pop(k, None)
+            out.append(dict(kind=OP_CONV_PROJ, conv=cd, **{"in": op["in"]}, out=op["out"],
+                            res=dn["in"], ptrs=[op["w"], op["bias"], dn["w"], dn["bias"]],
+                            p=[dd["H"], dd["W"], dd["Cin"], dd["stride"], dd["Kpad"]],
+                            bpi=[op["bpi"][0], op["bpi"][1], dn["bpi"][0]],
+                            layer=op.get("layer", 0)))
+            continue
+        out.append(op)
+    return out
+
+
 def build_plan(net: Network, base_ptr: int, wdtype: str = "bf16",
                act_scales: Optional[Dict[str, float]] = None,
                fused: bool = True, fold_bn: bool = True,
@@ -557,7 +605,8 @@ def build_plan(net: Network, base_ptr: int, wdtype: str = "bf16",
     applies the BN affine, the residual and the ReLU in place (the debugging / parity plan).
     ``fuse_blocks`` (bf16, folded BN, no chunking; default on, ``GALE_FUSE_BLOCKS=0`` off): the
     ResNet-50 stem + max-pool (``fuse_stem_pool``) and each 56x56 bottleneck
-    (``fuse_bottlenecks``) run as one kernel.
+    (``fuse_bottlenecks``) run as one kernel, and each strided projection shortcut runs inside
+    its block's conv3 (``fuse_projections``).
     ``chunk_layers``: the first ``chunk_layers`` layers may run per batch chunk (the executor's
     PlanSpec::chunk_ops; every op carries ``layer``, its layer index): each tensor they produce
     that is still read after them gets a buffer of its own, so a later chunk cannot overwrite an
@@ -573,12 +622,24 @@ def build_plan(net: Network, base_ptr: int, wdtype: str = "bf16",
     if fused and is_mnist_lenet5(net) and wdtype == "bf16":
         return _fused_lenet5_plan(net, base_ptr)
     layout, _ = param_layout(net, wdtype, fold_bn)
+    if fuse_blocks is None:
+        fuse_blocks = os.environ.get("GALE_FUSE_BLOCKS", "1") != "0"
+    fuse_blocks = bool(fuse_blocks and fused and wdtype == "bf16" and fold_bn and chunk_layers == 0)
+    # (GALE_FUSE_PROJ=0: the projections stay separate convs, for A/B runs)
+    proj = projection_pairs(net) if fuse_blocks and os.environ.get("GALE_FUSE_PROJ", "1") != "0" \
+        else {}
+    layer_index = {L.name: i for i, L in enumerate(net.layers)}
     # liveness: last layer index reading each tensor
     last_use: Dict[str, int] = {}
     for i, L in enumerate(net.layers):
         last_use[L.inp] = i
         if isinstance(L, Conv) and L.residual is not None:
             last_use[L.residual] = i
+    for c3, dn in proj.items():
+        # a fused projection reads the block input at conv3's place: keep it alive until then
+        x = net.layers[layer_index[dn]].inp
+        last_use[x] = max(last_use[x], layer_index[c3])
+    conv_op: Dict[str, int] = {}  # conv layer name -> index of its OP_CONV in ops
     buf_of: Dict[str, int] = {"input": 0}
     buf_bytes: List[int] = [_tensor_bytes(net, "input"), net.classes * 4]
     # bytes per image of a tensor as stored (every op also carries bpi = [in, out, res] for the
@@ -648,6 +709,7 @@ def build_plan(net: Network, base_ptr: int, wdtype: str = "bf16",
                       bpi=[in_bpi, tbytes[out_name], tbytes[L.residual] if res >= 0 else 0])
             if wdtype == "fp8":
                 op["wscale"] = base_ptr + layout[f"{L.name}.s"].offset
+            conv_op[L.name] = len(ops)
             ops.append(op)
             if unfold:
                 ho, wo, c = net.shapes[L.out]
@@ -694,8 +756,7 @@ def build_plan(net: Network, base_ptr: int, wdtype: str = "bf16",
             if lu == i and t in buf_of and buf_of[t] >= 2:
                 free.append(buf_of[t])
                 del last_use[t]
-    if fuse_blocks is None:
-        fuse_blocks = os.environ.get("GALE_FUSE_BLOCKS", "1") != "0"
-    if fuse_blocks and fused and wdtype == "bf16" and fold_bn and chunk_layers == 0:
+    if fuse_blocks:
+        ops = fuse_projections(ops, {conv_op[c3]: conv_op[dn] for c3, dn in proj.items()})
         ops = fuse_bottlenecks(fuse_stem_pool(ops))
     return ops, buf_bytes
