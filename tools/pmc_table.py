@@ -58,8 +58,22 @@ def layer_labels(model: str, batch: int):
             fl = 2.0 * m * d["Cout"] * d["K"] * 9 / 8  # (+1 recomputed window row in 8)
             by = 2.0 * (batch * d["H"] * d["W"] * 4 + batch * 56 * 56 * d["Cout"])
             out.append(("stem 7x7/2 + maxpool 3x3/2 (fused) @56x56", fl, by))
+        elif op["kind"] == 11:  # OP_CONV_PROJ: conv3 + strided projection (conv2d_gemm_proj)
+            d = op["conv"]
+            H2, W2, Cin2 = op["p"][:3]
+            m = batch * d["Ho"] * d["Wo"]
+            fl = 2.0 * m * d["Cout"] * (d["K"] + Cin2)
+            by = 2.0 * (batch * d["H"] * d["W"] * d["Cin"] + m * Cin2 + m * d["Cout"])
+            by += d["Npad"] * (d["Kpad"] + op["p"][4]) * 2
+            blk = net.layers[op["layer"]].name.rsplit(".", 1)[0]
+            out.append((f"{blk} conv3 1x1 {d['Cin']}->{d['Cout']} + proj 1x1/2 {Cin2} @"
+                        f"{d['Ho']}x{d['Wo']}", fl, by))
         elif op["kind"] == 6:
             out.append(("stem_pack (fp32 -> bf16 [224][230][4])", 0.0, 0.0))
+        elif op["kind"] == 2:
+            out.append(("avgpool 7x7 (global)", 0.0, 0.0))
+        elif op["kind"] == 4:
+            out.append(("softmax 1000", 0.0, 0.0))
         else:
             out.append((f"op{op['kind']}", 0.0, 0.0))
     return out
