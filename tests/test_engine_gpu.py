@@ -574,7 +574,7 @@ def test_gpu_locality_split_steals_parse_from_host_pinned():
         rng = np.random.default_rng(7)
         distinct = rng.random((48,) + net.input_shape, dtype=np.float32)
         enc = [C.encode_instances(distinct[i:i + 1]) for i in range(len(distinct))]
-        n = 1500
+        n = 3000  # (a deep backlog in slot 0's partition: slot 1 steals whenever it idles)
         for s in range(0, n, 50):
             b.append("in", 0, [enc[i % len(enc)] for i in range(s, s + 50)],
                      [f"k{i}".encode() for i in range(s, s + 50)])
