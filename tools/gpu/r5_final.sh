@@ -5,6 +5,7 @@
 #           SMT siblings) x3 interleaved, world-2 shared-GPU rehearsal with and without
 #           per-rank slices x2
 #   PART=c  kernel trace of the default bench, forward-alone ResNet-50 / ResNet-20, ingest kernels
+#   PART=d  the last code: config 2 (headline) x3 and config 4 (ResNet-50) x3
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 out=gpurun_out/final
@@ -50,6 +51,9 @@ case ${PART:-a} in
       one w2_slices_$i 300 --gpus 2 --shared-gpu-rehearsal --steps 10 --warmup 3 || exit 1
       one w2_float_$i 300 --gpus 2 --shared-gpu-rehearsal --steps 10 --warmup 3 --no-rank-slices || exit 1
     done ;;
+  d)
+    for i in 1 2 3; do one c2_$i 240 --steps 20 --warmup 5 || exit 1; done
+    for i in 1 2 3; do one c4_resnet50_$i 300 --model resnet50 --steps 10 --warmup 3 || exit 1; done ;;
   c)
     export TMPDIR=/tmp
     # one hardware queue per HIP stream under the profiler (README "--profile")
