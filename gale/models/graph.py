@@ -559,7 +559,8 @@ def projection_pairs(net: Network) -> Dict[str, str]:
         D = by_out.get(L.residual)
         if (D is not None and D.k == 1 and D.stride > 1 and D.pad == 0 and not D.relu
                 and D.residual is None and not D.out_f32 and D.cout == L.cout
-                and readers.get(D.out, 0) == 1 and D.cin % 64 == 0 and L.cin % 64 == 0):
+                and readers.get(D.out, 0) == 1 and D.cin % 64 == 0 and L.cin % 64 == 0
+                and L.cout % 128 == 0):  # (conv2d_gemm_proj's 128-channel tiles)
             pairs[L.name] = D.name
     return pairs
 
