@@ -31,6 +31,7 @@ EngineConfig config_from_dict(const py::dict& d) {
   opt(d, "partitions", c.partitions);
   opt(d, "source_parallelism", c.source_parallelism);
   opt(d, "start_offset", c.start_offset);
+  opt(d, "auto_offset_reset", c.auto_offset_reset);
   opt(d, "fetch_max_wait_ms", c.fetch_max_wait_ms);
   opt(d, "fetch_min_bytes", c.fetch_min_bytes);
   opt(d, "fetch_max_bytes", c.fetch_max_bytes);
@@ -55,6 +56,10 @@ EngineConfig config_from_dict(const py::dict& d) {
   opt(d, "sink_parallelism", c.sink_parallelism);
   opt(d, "acks", c.acks);
   opt(d, "sink_mode", c.sink_mode);
+  opt(d, "delivery", c.delivery);
+  opt(d, "producer_retries", c.producer_retries);
+  opt(d, "retry_backoff_ms", c.retry_backoff_ms);
+  opt(d, "delivery_timeout_ms", c.delivery_timeout_ms);
   opt(d, "linger_ms", c.linger_ms);
   opt(d, "compression", c.compression);
   opt(d, "batch_size", c.batch_size);

@@ -798,6 +798,8 @@ void bind_host(py::module_& m) {
         return py::make_tuple(first, recs);
       }, py::arg("topic"), py::arg("partition"), py::arg("batches"), py::arg("n_batches"),
          py::arg("start") = 0)
+      .def("fail_produce", &Broker::fail_produce, py::arg("topic"), py::arg("n"),
+           py::arg("error") = (int16_t)NOT_LEADER_FOR_PARTITION)
       .def("describe_group", [](Broker& b, const std::string& g) {
         const GroupInfo gi = b.describe_group(g);
         py::dict d;
@@ -863,8 +865,13 @@ void bind_host(py::module_& m) {
   py::class_<Producer, std::shared_ptr<Producer>>(k, "Producer")
       .def(py::init([](const std::string& bootstrap, int acks, int linger_ms, int batch_size,
                        const std::string& client_id, int request_timeout_ms, int max_in_flight,
-                       int max_request_size, const std::string& compression) {
+                       int max_request_size, const std::string& compression, int retries,
+                       int retry_backoff_ms, int delivery_timeout_ms, double fail_p) {
              ProducerConfig c;
+             c.retries = retries;
+             c.retry_backoff_ms = retry_backoff_ms;
+             c.delivery_timeout_ms = delivery_timeout_ms;
+             c.fail_p = fail_p;
              c.compression = codec_from_name(compression);
              c.max_request_size = max_request_size;
              c.bootstrap = bootstrap;
@@ -880,7 +887,9 @@ void bind_host(py::module_& m) {
            py::arg("bootstrap"), py::arg("acks") = 1, py::arg("linger_ms") = 0,
            py::arg("batch_size") = 16384, py::arg("client_id") = "gale-producer",
            py::arg("request_timeout_ms") = 30000, py::arg("max_in_flight") = 5,
-           py::arg("max_request_size") = 64 << 20, py::arg("compression") = "none")
+           py::arg("max_request_size") = 64 << 20, py::arg("compression") = "none",
+           py::arg("retries") = 0, py::arg("retry_backoff_ms") = 100,
+           py::arg("delivery_timeout_ms") = 120000, py::arg("fail_p") = 0.0)
       .def("send", [](Producer& p, const std::string& topic, py::object value, py::object key,
                       int partition, py::object headers, int64_t timestamp, py::object callback) {
         std::string v;
@@ -928,6 +937,8 @@ void bind_host(py::module_& m) {
         d["records_failed"] = s.records_failed;
         d["requests"] = s.requests;
         d["bytes"] = s.bytes;
+        d["records_retried"] = s.records_retried;
+        d["requests_failed"] = s.requests_failed;
         return d;
       });
 

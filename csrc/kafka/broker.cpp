@@ -407,6 +407,12 @@ int64_t Broker::committed(const std::string& group, const std::string& topic, in
   return it == offsets_.end() ? -1 : it->second;
 }
 
+void Broker::fail_produce(const std::string& topic, int64_t n, int16_t error) {
+  std::lock_guard<std::mutex> lk(mu_);
+  if (n <= 0) produce_faults_.erase(topic);
+  else produce_faults_[topic] = {n, error};
+}
+
 BrokerStats Broker::stats() const {
   std::lock_guard<std::mutex> lk(mu_);
   return stats_;
@@ -790,8 +796,12 @@ bool Broker::handle_request(Conn& c, const uint8_t* p, size_t n) {
             ProducePartitionResponse pr;
             pr.index = pp.index;
             PartitionLog* log = find_log(t.name, pp.index);
+            auto fault = produce_faults_.find(t.name);
             if (ack_err) {
               pr.error = ack_err;
+            } else if (fault != produce_faults_.end() && fault->second.first > 0) {
+              pr.error = fault->second.second;
+              if (--fault->second.first == 0) produce_faults_.erase(fault);
             } else if (!log) {
               pr.error = UNKNOWN_TOPIC_OR_PARTITION;
             } else if (leader_of(pp.index) != cfg_.node_id) {

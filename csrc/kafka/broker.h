@@ -115,6 +115,10 @@ class Broker {
   BrokerStats stats() const;
   BrokerProbes take_probes();
   GroupInfo describe_group(const std::string& group) { return coord_.describe(group); }
+  // Fault injection (tests): the next `n` partition appends of Produce requests to `topic` are
+  // rejected with `error` (nothing is appended) - a broker that truly refuses produces, e.g.
+  // NOT_LEADER_FOR_PARTITION during a leader move. n = 0 clears it.
+  void fail_produce(const std::string& topic, int64_t n, int16_t error);
 
  public:
   struct Chunk;  // one piece of a response (owned bytes or a zero-copy slice of a stored batch)
@@ -189,6 +193,7 @@ class Broker {
   mutable std::mutex mu_;  // topics_, offsets_, cluster_, stats_
   std::map<std::string, std::vector<PartitionLog>> topics_;
   std::map<std::string, int64_t> offsets_;  // "group\0topic\0partition" -> offset
+  std::map<std::string, std::pair<int64_t, int16_t>> produce_faults_;  // topic -> (left, error)
   std::vector<BrokerNode> cluster_;
   BrokerStats stats_;
   GroupCoordinator coord_;

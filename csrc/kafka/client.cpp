@@ -373,9 +373,12 @@ int32_t murmur2(const uint8_t* data, size_t n) {
 }
 
 Producer::Producer(ProducerConfig cfg)
-    : cfg_(std::move(cfg)), cluster_(cfg_), meta_(cfg_) {
+    : cfg_(std::move(cfg)), cluster_(cfg_), meta_(cfg_),
+      fault_state_(cfg_.fail_seed * 0x9e3779b97f4a7c15ull + 1) {
   if (cfg_.acks != 0 && cfg_.acks != 1 && cfg_.acks != -1)
     throw std::invalid_argument("acks must be 0, 1 or -1");
+  if (cfg_.retries < 0 || cfg_.retry_backoff_ms < 0 || cfg_.delivery_timeout_ms <= 0)
+    throw std::invalid_argument("retries / retry_backoff_ms must be >= 0, delivery_timeout_ms > 0");
   thread_ = std::thread([this] {
     name_thread("gl-sink");
     run();
@@ -446,6 +449,7 @@ void Producer::send(const std::string& topic, int partition, const std::string* 
   p.headers = std::move(headers);
   p.ts = timestamp >= 0 ? timestamp : wall_ms();
   p.cb = std::move(cb);
+  p.enq_ms = mono_ms();
   const size_t sz = record_bound(p.key, p.value, p.headers);
   PartBatch& b = acc_[{topic, partition}];
   if (b.recs.empty()) b.first_ms = mono_ms();
@@ -540,6 +544,7 @@ void Producer::send_group(const std::string& topic, int partition, RecordGroup g
   p.ts = g.ts >= 0 ? g.ts : wall_ms();
   p.group = std::make_unique<RecordGroup>(std::move(g));
   p.gcb = std::move(cb);
+  p.enq_ms = mono_ms();
   PartBatch& b = acc_[{topic, partition}];
   if (b.recs.empty()) b.first_ms = mono_ms();
   b.bytes += sz;
@@ -594,21 +599,46 @@ ProducerStats Producer::stats() const {
 
 void Producer::run() {
   std::deque<InFlight> inflight;
-  auto complete = [&](std::vector<Pending>& recs, int16_t err, int part, int64_t base) {
+  using TP = std::pair<std::string, int>;
+  // a request's outcome for one partition's chunk: retriable failures of records that still have
+  // attempts and time left wait in retry_ for their backoff; everything else is final
+  auto complete = [&](const TP& tp, std::vector<Pending>& recs, int16_t err, int64_t base) {
+    if (err != NONE && error_retriable(err) && cfg_.retries > 0) {
+      const int64_t now = mono_ms();
+      std::vector<Pending> again, last;
+      int64_t n_again = 0;
+      for (auto& p : recs) {
+        if (p.attempts < cfg_.retries && now - p.enq_ms < cfg_.delivery_timeout_ms) {
+          ++p.attempts;
+          n_again += (int64_t)p.records();
+          again.push_back(std::move(p));
+        } else {
+          last.push_back(std::move(p));
+        }
+      }
+      if (!again.empty()) {
+        retry_.push_back(Retry{tp, std::move(again), now + cfg_.retry_backoff_ms});
+        std::lock_guard<std::mutex> lk(mu_);
+        stats_.records_retried += n_again;
+        ++stats_.requests_failed;
+      }
+      if (last.empty()) return;
+      recs = std::move(last);
+    }
     int64_t idx = 0;
     for (size_t i = 0; i < recs.size(); ++i) {
       const int64_t off = (err == NONE && base >= 0) ? base + idx : -1;
       if (recs[i].group) {
         if (recs[i].gcb) {
           try {
-            recs[i].gcb(err, part, off, recs[i].group->size());
+            recs[i].gcb(err, tp.second, off, recs[i].group->size());
           } catch (...) {
           }
         }
       } else if (recs[i].cb) {
         SendResult r;
         r.error = err;
-        r.partition = part;
+        r.partition = tp.second;
         r.offset = off;
         try {
           recs[i].cb(r);
@@ -623,6 +653,20 @@ void Producer::run() {
     else stats_.records_failed += idx;
     done_cv_.notify_all();
   };
+  // a node's connection broke (or is mid-response): every request still in flight on it is
+  // lost with it; the next request to the node reconnects
+  auto lose_node = [&](int32_t node) {
+    for (auto it = inflight.begin(); it != inflight.end();) {
+      if (it->node == node) {
+        for (auto& b : it->batches) complete(b.first, b.second, NETWORK_EXCEPTION, -1);
+        it = inflight.erase(it);
+      } else {
+        ++it;
+      }
+    }
+    cluster_.drop(node);
+    cluster_.invalidate();
+  };
   auto read_one = [&]() {
     InFlight f = std::move(inflight.front());
     inflight.pop_front();
@@ -631,8 +675,8 @@ void Producer::run() {
     try {
       buf = cluster_.node(f.node).recv(f.corr, &n, heap_alloc);
     } catch (const std::exception&) {
-      for (auto& b : f.batches) complete(b.second, REQUEST_TIMED_OUT, b.first.second, -1);
-      cluster_.invalidate();
+      for (auto& b : f.batches) complete(b.first, b.second, REQUEST_TIMED_OUT, -1);
+      lose_node(f.node);
       return;
     }
     Reader r(buf.get(), n);
@@ -648,7 +692,7 @@ void Producer::run() {
               base = p.base_offset;
             }
       if (err != NONE) cluster_.invalidate();
-      complete(b.second, err, b.first.second, base);
+      complete(b.first, b.second, err, base);
     }
   };
 
@@ -660,6 +704,16 @@ void Producer::run() {
       for (;;) {
         const int64_t now = mono_ms();
         int64_t next = INT64_MAX;
+        // retries whose backoff ended go first (ahead of newer records of their partition)
+        for (auto it = retry_.begin(); it != retry_.end();) {
+          if (it->due_ms <= now) {
+            ready.push_back({it->tp, std::move(it->recs)});
+            it = retry_.erase(it);
+          } else {
+            next = std::min(next, it->due_ms);
+            ++it;
+          }
+        }
         for (auto it = acc_.begin(); it != acc_.end();) {
           PartBatch& b = it->second;
           if (b.recs.empty()) {
@@ -703,7 +757,7 @@ void Producer::run() {
           break;
         }
         if (!inflight.empty()) break;
-        if (closing_) {
+        if (closing_ && retry_.empty()) {
           stop = true;
           break;
         }
@@ -718,7 +772,7 @@ void Producer::run() {
       try {
         by_node[cluster_.leader(ready[i].first.first, ready[i].first.second)].push_back(i);
       } catch (const KafkaError& e) {
-        complete(ready[i].second, (int16_t)e.code, ready[i].first.second, -1);
+        complete(ready[i].first, ready[i].second, (int16_t)e.code, -1);
         cluster_.invalidate();
       }
     }
@@ -787,6 +841,15 @@ void Producer::run() {
         }
         Writer w;
         encode_produce_request(w, req);
+        if (cfg_.fail_p > 0) {  // injected loss of the request (never reaches the broker)
+          fault_state_ ^= fault_state_ << 13;
+          fault_state_ ^= fault_state_ >> 7;
+          fault_state_ ^= fault_state_ << 17;
+          if ((double)(fault_state_ >> 11) * 0x1.0p-53 < cfg_.fail_p) {
+            for (auto& b : f.batches) complete(b.first, b.second, NETWORK_EXCEPTION, -1);
+            continue;
+          }
+        }
         try {
           Connection& c = cluster_.node(kv.first);
           f.corr = c.send(PRODUCE, w);
@@ -796,12 +859,12 @@ void Producer::run() {
             stats_.bytes += (int64_t)w.size();
           }
         } catch (const std::exception&) {
-          for (auto& b : f.batches) complete(b.second, REQUEST_TIMED_OUT, b.first.second, -1);
-          cluster_.invalidate();
+          for (auto& b : f.batches) complete(b.first, b.second, NETWORK_EXCEPTION, -1);
+          lose_node(kv.first);
           continue;
         }
         if (cfg_.acks == 0) {
-          for (auto& b : f.batches) complete(b.second, NONE, b.first.second, -1);
+          for (auto& b : f.batches) complete(b.first, b.second, NONE, -1);
         } else {
           inflight.push_back(std::move(f));
           if ((int)inflight.size() >= cfg_.max_in_flight) read_one();

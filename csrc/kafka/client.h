@@ -149,6 +149,19 @@ struct ProducerConfig : ClientConfig {
   int max_in_flight = 5;
   int64_t buffer_memory = 1ll << 30;  // send() blocks while more than this is unsent
   int compression = 0;  // compression.type (compress.h Codec; kafka-clients default none)
+  // kafka-clients `retries` / `retry.backoff.ms` / `delivery.timeout.ms`: a request that failed
+  // with a retriable error (protocol.h error_retriable: leader moved, timeout, connection lost)
+  // is sent again after the backoff, at most `retries` times and while the record is younger
+  // than the delivery timeout; only then does its callback see the error. As in kafka-clients,
+  // a retried batch can land behind batches of the same partition that were sent after it
+  // while it waited (max_in_flight > 1).
+  int retries = 0;
+  int retry_backoff_ms = 100;
+  int delivery_timeout_ms = 120000;
+  // fault injection (tests, GALE_FAULT producer_fail@P): each produce request is dropped before
+  // it is sent with probability fail_p and completes with NETWORK_EXCEPTION (then retried)
+  double fail_p = 0;
+  uint64_t fail_seed = 0;
 };
 
 struct SendResult {
@@ -178,6 +191,7 @@ using GroupCallback = std::function<void(int16_t, int32_t, int64_t, size_t)>;
 
 struct ProducerStats {
   int64_t records_sent = 0, records_acked = 0, records_failed = 0, requests = 0, bytes = 0;
+  int64_t records_retried = 0, requests_failed = 0;  // re-sent records; requests that failed
 };
 
 class Producer {
@@ -210,6 +224,8 @@ class Producer {
     SendCallback cb;
     std::unique_ptr<RecordGroup> group;  // set: this entry is a whole group of records
     GroupCallback gcb;
+    int attempts = 0;    // sends that failed with a retriable error so far
+    int64_t enq_ms = 0;  // when it was handed to send() / send_group() (delivery timeout)
     size_t records() const { return group ? group->size() : 1; }
   };
   struct PartBatch {
@@ -221,6 +237,11 @@ class Producer {
     int32_t corr;
     int32_t node;
     std::vector<std::pair<std::pair<std::string, int>, std::vector<Pending>>> batches;
+  };
+  struct Retry {  // a failed chunk waiting for its backoff (sender thread only)
+    std::pair<std::string, int> tp;
+    std::vector<Pending> recs;
+    int64_t due_ms;
   };
   void run();
   int choose_partition(const std::string& topic, const std::string* key);
@@ -238,6 +259,8 @@ class Producer {
   uint32_t rr_ = 0;
   std::thread thread_;
   ProducerStats stats_;
+  std::deque<Retry> retry_;  // sender thread only
+  uint64_t fault_state_;     // fail_p's generator (sender thread only)
 };
 
 struct ConsumerConfig : ClientConfig {

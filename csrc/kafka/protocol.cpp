@@ -15,6 +15,9 @@ const char* error_name(int code) {
     case NOT_LEADER_FOR_PARTITION: return "NOT_LEADER_FOR_PARTITION";
     case REQUEST_TIMED_OUT: return "REQUEST_TIMED_OUT";
     case MESSAGE_TOO_LARGE: return "MESSAGE_TOO_LARGE";
+    case NETWORK_EXCEPTION: return "NETWORK_EXCEPTION";
+    case NOT_ENOUGH_REPLICAS: return "NOT_ENOUGH_REPLICAS";
+    case NOT_ENOUGH_REPLICAS_AFTER_APPEND: return "NOT_ENOUGH_REPLICAS_AFTER_APPEND";
     case COORDINATOR_NOT_AVAILABLE: return "COORDINATOR_NOT_AVAILABLE";
     case NOT_COORDINATOR: return "NOT_COORDINATOR";
     case INVALID_TOPIC_EXCEPTION: return "INVALID_TOPIC_EXCEPTION";
@@ -30,6 +33,22 @@ const char* error_name(int code) {
     case INVALID_PARTITIONS: return "INVALID_PARTITIONS";
     case INVALID_REQUEST: return "INVALID_REQUEST";
     default: return "ERROR";
+  }
+}
+
+bool error_retriable(int code) {
+  switch (code) {
+    case CORRUPT_MESSAGE:
+    case UNKNOWN_TOPIC_OR_PARTITION:
+    case LEADER_NOT_AVAILABLE:
+    case NOT_LEADER_FOR_PARTITION:
+    case REQUEST_TIMED_OUT:
+    case NETWORK_EXCEPTION:
+    case NOT_ENOUGH_REPLICAS:
+    case NOT_ENOUGH_REPLICAS_AFTER_APPEND:
+      return true;
+    default:
+      return false;
   }
 }
 

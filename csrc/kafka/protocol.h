@@ -57,10 +57,13 @@ enum ErrorCode : int16_t {
   NOT_LEADER_FOR_PARTITION = 6,
   REQUEST_TIMED_OUT = 7,
   MESSAGE_TOO_LARGE = 10,
+  NETWORK_EXCEPTION = 13,
   COORDINATOR_NOT_AVAILABLE = 15,
   NOT_COORDINATOR = 16,
   INVALID_TOPIC_EXCEPTION = 17,
   RECORD_LIST_TOO_LARGE = 18,
+  NOT_ENOUGH_REPLICAS = 19,
+  NOT_ENOUGH_REPLICAS_AFTER_APPEND = 20,
   INVALID_REQUIRED_ACKS = 21,
   ILLEGAL_GENERATION = 22,
   INCONSISTENT_GROUP_PROTOCOL = 23,
@@ -74,6 +77,9 @@ enum ErrorCode : int16_t {
 };
 
 const char* error_name(int code);
+// Kafka's RetriableException family (kafka-clients Errors): a produce that failed with one of
+// these may succeed when sent again (leader moved, broker busy, connection lost)
+bool error_retriable(int code);
 
 // ListOffsets special timestamps
 constexpr int64_t kLatest = -1;

@@ -5,6 +5,7 @@
 
 #include <hip/hip_runtime.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 #include <sched.h>
 #include <sys/prctl.h>
@@ -171,6 +172,13 @@ Engine::Engine(EngineConfig cfg) : cfg_(std::move(cfg)), rng_(cfg_.seed) {
     throw std::invalid_argument("engine: value_format must be json|json-string");
   if (cfg_.output_key != "none" && cfg_.output_key != "input")
     throw std::invalid_argument("engine: output_key must be none|input");
+  if (cfg_.delivery != "at-most-once" && cfg_.delivery != "at-least-once")
+    throw std::invalid_argument("engine: delivery must be at-most-once|at-least-once");
+  if (cfg_.auto_offset_reset != "latest" && cfg_.auto_offset_reset != "earliest")
+    throw std::invalid_argument("engine: auto_offset_reset must be latest|earliest");
+  if (cfg_.delivery == "at-least-once" && cfg_.sink_mode == "fire-and-forget")
+    throw std::invalid_argument("engine: at-least-once delivery needs acknowledged sends "
+                                "(sink_mode async or sync)");
   if (cfg_.max_batch <= 0 || cfg_.source_parallelism <= 0 || cfg_.sink_parallelism <= 0)
     throw std::invalid_argument("engine: max_batch / parallelism must be positive");
   // fault injection spec: comma separated kind@value
@@ -254,7 +262,14 @@ void Engine::start() {
     pc.buffer_memory = cfg_.producer_buffer_bytes;
     pc.max_request_size = (int)cfg_.producer_request_bytes;
     pc.compression = kafka::codec_from_name(cfg_.compression);
-    producers_.push_back(std::make_unique<kafka::Producer>(pc));
+    pc.retries = cfg_.producer_retries;
+    pc.retry_backoff_ms = cfg_.retry_backoff_ms;
+    pc.delivery_timeout_ms = cfg_.delivery_timeout_ms;
+    pc.fail_p = producer_fail_p_;
+    pc.fail_seed = cfg_.seed + (uint64_t)i + 1;
+    auto prod = std::make_unique<kafka::Producer>(pc);
+    std::lock_guard<std::mutex> lk(prod_mu_);
+    producers_.push_back(std::move(prod));
   }
   // static mode: resolve the input partitions and split them over the source threads now;
   // group mode: the sources start idle and the group thread hands them the assignment
@@ -396,7 +411,15 @@ void Engine::stop() {
   done_cv_.notify_all();
   if (watchdog_.joinable()) watchdog_.join();
   for (auto& p : producers_) p->close();
-  producers_.clear();
+  {
+    std::lock_guard<std::mutex> lk(prod_mu_);
+    for (const auto& p : producers_) {
+      const kafka::ProducerStats ps = p->stats();
+      prod_retried_ += ps.records_retried;
+      prod_req_failed_ += ps.requests_failed;
+    }
+    producers_.clear();
+  }
 }
 
 bool Engine::wait(int64_t timeout_ms) {
@@ -425,11 +448,23 @@ void Engine::commit(kafka::Consumer& c, const std::vector<int>& parts) {
       else if (next_fetch_.count(p)) offs[p] = next_fetch_[p];
     }
   }
+  // GALE_LOG_COMMITS=1: one stderr line per commit (delivery diagnostics in the fault tests)
+  static const bool log_commits = [] {
+    const char* e = getenv("GALE_LOG_COMMITS");
+    return e && *e && *e != '0';
+  }();
+  std::string what;
+  if (log_commits)
+    for (const auto& kv : offs)
+      what += " p" + std::to_string(kv.first) + "=" + std::to_string(kv.second);
   try {
     c.commit(offs);
     ++commits_;
+    if (log_commits)
+      fprintf(stderr, "[gale commit] generation %d ok:%s\n", (int)generation_, what.c_str());
   } catch (const std::exception& e) {
-    fprintf(stderr, "[gale source] offset commit failed: %s\n", e.what());
+    fprintf(stderr, "[gale source] offset commit failed (generation %d:%s): %s\n",
+            (int)generation_, what.c_str(), e.what());
   }
 }
 
@@ -667,7 +702,7 @@ void Engine::source_loop(int idx) {
   cc.recv_lowat = cfg_.recv_lowat >= 0 ? cfg_.recv_lowat : bounce ? (int)window : 0;
   // with decode workers the CRC32C check moves off this thread (decode_fetch)
   cc.check_crcs = cfg_.check_crcs && cfg_.decode_threads <= 0;
-  cc.auto_offset_reset = cfg_.start_offset == "earliest" ? "earliest" : "latest";
+  cc.auto_offset_reset = cfg_.start_offset == "earliest" ? "earliest" : cfg_.auto_offset_reset;
   Batcher& batcher = *batchers_[(size_t)slot];
   kafka::BufferAlloc alloc = kafka::heap_alloc;
   if (pinned) {
@@ -1382,40 +1417,49 @@ void Engine::finish_batch(ReplicaSlot* rs, Batch& b) {
 
 // A record group's acknowledgement: one pending-window update for all of its records.
 void Engine::complete_records(const std::vector<InRecord>& rs, bool ok) {
-  std::vector<char> good(rs.size());
-  for (size_t i = 0; i < rs.size(); ++i) good[i] = ok && !fault_hit(producer_fail_p_);
-  {
+  const int64_t now = mono_ns();
+  if (!ok && cfg_.delivery == "at-least-once") {
+    undelivered(rs);
+  } else {
     std::lock_guard<std::mutex> lk(pend_mu_);
     for (const InRecord& r : rs) {
       auto it = pending_.find(r.partition);
       if (it != pending_.end()) it->second.done(r.offset);
     }
   }
-  const int64_t now = mono_ns();
   const int64_t wall = wall_ms_now();
-  int64_t nok = 0, imgs = 0;
-  for (size_t i = 0; i < rs.size(); ++i) {
-    const InRecord& r = rs[i];
-    if (good[i]) {
-      ++nok;
+  int64_t imgs = 0;
+  if (ok) {
+    for (const InRecord& r : rs) {
       imgs += r.images;
       h_engine_e2e_us_.add((now - r.t_fetch_ns) / 1000);
       if (cfg_.slo_p99_ms > 0) h_slo_win_us_.add((now - r.t_fetch_ns) / 1000);
       if (r.timestamp_ms > 0) h_record_e2e_ms_.add(wall - r.timestamp_ms);
     }
+    records_out_ += (int64_t)rs.size();
+    images_out_ += imgs;
+  } else {
+    produce_failures_ += (int64_t)rs.size();
   }
-  records_out_ += nok;
-  images_out_ += imgs;
-  produce_failures_ += (int64_t)rs.size() - nok;
   t_last_ns_ = now;
-  if (ack_log_on_.load(std::memory_order_relaxed)) {
+  if (ok && ack_log_on_.load(std::memory_order_relaxed)) {
     std::lock_guard<std::mutex> lk(ack_mu_);
     for (size_t i = 0; i < rs.size() && ack_n_ < ack_cap_; ++i)
-      if (good[i])
-        ack_push({rs[i].partition, rs[i].offset, now, rs[i].t_fetch_ns, rs[i].t_take_ns,
-                  rs[i].t_done_ns});
+      ack_push({rs[i].partition, rs[i].offset, now, rs[i].t_fetch_ns, rs[i].t_take_ns,
+                rs[i].t_done_ns});
   }
   note_completed(completed_ += (int64_t)rs.size(), now);
+}
+
+void Engine::undelivered(const std::vector<InRecord>& rs) {
+  if (rs.empty()) return;
+  undelivered_ += (int64_t)rs.size();
+  if (!delivery_failed_.exchange(true))
+    fprintf(stderr, "[gale sink] at-least-once: %zu output(s) not acknowledged after %d "
+            "retr%s (first: input partition %d offset %lld); their offsets stay uncommitted, "
+            "delivery_failed raised\n", rs.size(), cfg_.producer_retries,
+            cfg_.producer_retries == 1 ? "y" : "ies", rs[0].partition,
+            (long long)rs[0].offset);
 }
 
 void Engine::note_completed(int64_t c, int64_t now) {
@@ -1432,7 +1476,9 @@ void Engine::note_completed(int64_t c, int64_t now) {
 }
 
 void Engine::complete_record(const InRecord& r, bool ok) {
-  {
+  if (!ok && cfg_.delivery == "at-least-once") {
+    undelivered({r});
+  } else {
     std::lock_guard<std::mutex> lk(pend_mu_);
     auto it = pending_.find(r.partition);
     if (it != pending_.end()) it->second.done(r.offset);
@@ -1517,8 +1563,7 @@ void Engine::emit(InRecord& r, std::string value, bool null_value, kafka::Produc
   kafka::SendCallback cb;
   if (!ff) {
     cb = [this, meta](const kafka::SendResult& res) {
-      const bool ok = res.error == 0 && !fault_hit(producer_fail_p_);
-      complete_record(meta, ok);
+      complete_record(meta, res.error == 0);
     };
   }
   try {
@@ -1652,6 +1697,19 @@ std::map<std::string, double> Engine::stats() const {
   s["completed"] = (double)completed_;
   s["errors"] = (double)errors_;
   s["produce_failures"] = (double)produce_failures_;
+  s["undelivered"] = (double)undelivered_;
+  s["delivery_failed"] = delivery_failed_ ? 1.0 : 0.0;
+  {
+    std::lock_guard<std::mutex> lk(prod_mu_);
+    int64_t retried = prod_retried_, req_failed = prod_req_failed_;
+    for (const auto& p : producers_) {
+      const kafka::ProducerStats ps = p->stats();
+      retried += ps.records_retried;
+      req_failed += ps.requests_failed;
+    }
+    s["produce_retried_records"] = (double)retried;
+    s["produce_failed_requests"] = (double)req_failed;
+  }
   s["dropped"] = (double)dropped_;
   s["requeued"] = (double)requeued_;
   s["replica_failures"] = (double)replica_failures_;

@@ -15,8 +15,13 @@
 //      Producer.send async | sync | fire-and-forget (KafkaBolt.java:129-155), acks (:113)
 //
 // Delivery: offsets of a partition are committed up to the first record whose output has not
-// been acknowledged (at-least-once when start_offset=committed). The reference is at-most-once,
-// latest-only; start_offset=latest reproduces that default.
+// been acknowledged. delivery = "at-most-once" (the reference, SURVEY.md §3.4: KafkaBolt fails
+// an unanchored tuple and nothing replays it, KafkaBolt.java:133-137,160-162) completes a record
+// whose produce failed, so the commit moves past it. delivery = "at-least-once" never does: the
+// producer retries it (producer_retries, retry_backoff_ms, delivery_timeout_ms) and when the
+// retries are spent the record stays pending - the commit cannot pass it - and the engine reports
+// delivery_failed, on which the rank exits non-zero and is respawned from the committed offsets
+// (gale/topology.py, gale/supervisor.py).
 // Failure handling: a replica that throws or exceeds the watchdog deadline is
 // marked dead and its in-flight batches are re-queued to the surviving replicas; malformed input
 // follows on_error = null (reference: a null record, InferenceBolt.java:92-99) | error-json |
@@ -57,6 +62,9 @@ struct EngineConfig {
   std::vector<int> partitions;     // empty = every partition of input_topic
   int source_parallelism = 2;      // KAFKA_SPOUT_PARAL (MainTopology.java:26)
   std::string start_offset = "latest";  // latest | earliest | committed
+  // where start_offset=committed (and group-managed partitions) start when the group has no
+  // committed offset for a partition (Kafka auto.offset.reset): latest | earliest
+  std::string auto_offset_reset = "latest";
   int fetch_max_wait_ms = 20;
   int fetch_min_bytes = 1;         // Kafka fetch.min.bytes: a long-poll returns once this much
                                    // is available (or fetch_max_wait_ms passed)
@@ -98,6 +106,10 @@ struct EngineConfig {
   int sink_parallelism = 2;        // KAFKA_BOLT_PARAL (MainTopology.java:28)
   int acks = 1;                    // MainTopology.java:113
   std::string sink_mode = "async"; // async | sync | fire-and-forget (KafkaBolt.java:186-197)
+  std::string delivery = "at-most-once";  // at-most-once | at-least-once (header comment)
+  int producer_retries = 0;        // kafka-clients retries (0.11 default 0)
+  int retry_backoff_ms = 100;      // retry.backoff.ms
+  int delivery_timeout_ms = 120000;  // delivery.timeout.ms: bound on a record's retries
   int linger_ms = 0;
   int batch_size = 1 << 20;
   std::string compression = "none";  // sink compression.type (kafka/compress.h codecs)
@@ -323,6 +335,9 @@ class Engine {
   void emit_error(InRecord& r, int status, kafka::Producer* prod);
   void complete_record(const InRecord& r, bool ok);
   void complete_records(const std::vector<InRecord>& rs, bool ok);
+  // at-least-once: outputs that were never acknowledged stay pending (their offsets are never
+  // committed); the first one is logged and delivery_failed is raised
+  void undelivered(const std::vector<InRecord>& rs);
   void commit(kafka::Consumer& c, const std::vector<int>& parts);
   kafka::Producer* producer_for(int i);
   bool fault_hit(double p);
@@ -369,7 +384,11 @@ class Engine {
 
   // fault injection
   int64_t crash_at_batch_ = -1;
-  double parse_error_p_ = 0, producer_fail_p_ = 0;
+  double parse_error_p_ = 0, producer_fail_p_ = 0;  // (producer_fail: the sink producers')
+  std::atomic<int64_t> undelivered_{0};
+  mutable std::mutex prod_mu_;  // producers_ against stats() (stop() clears it)
+  int64_t prod_retried_ = 0, prod_req_failed_ = 0;  // of producers already closed
+  std::atomic<bool> delivery_failed_{false};
   std::atomic<int64_t> batches_total_{0};
   std::mutex rng_mu_;
   std::mt19937_64 rng_;

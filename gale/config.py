@@ -22,6 +22,8 @@ CHOICES = {
     "step_launch": ("graph", "direct"),
     "sink_mode": ("async", "sync", "fire-and-forget"),
     "start_offset": ("latest", "earliest", "committed"),
+    "auto_offset_reset": ("latest", "earliest"),
+    "delivery": ("auto", "at-most-once", "at-least-once"),
     "value_format": ("json", "json-string"),
     "on_error": ("null", "error-json", "drop"),
     "output_key": ("none", "input"),
@@ -49,6 +51,8 @@ class GaleConfig:
     group_id: str = ""                 # default: the topology name
     partitions: str = ""               # comma-separated input partitions (empty = all)
     start_offset: str = "latest"       # reference: LatestTime + ignoreZkOffsets (:101-102)
+    auto_offset_reset: str = "latest"  # start_offset=committed / group-managed partitions with no
+                                       # committed offset start here (Kafka auto.offset.reset)
     commit_interval_ms: int = 2000
     fetch_min_bytes: int = 1           # Kafka fetch.min.bytes of the consumers (long-poll size)
     fetch_max_wait_ms: int = 20        # Kafka fetch.max.wait.ms
@@ -99,6 +103,16 @@ class GaleConfig:
     # sink (R9, E7-E9)
     acks: int = 1                      # MainTopology.java:113
     sink_mode: str = "async"           # KafkaBolt async / sync / fire-and-forget
+    # delivery of outputs: at-most-once = the reference (a failed send fails the unanchored tuple,
+    # nothing replays it, KafkaBolt.java:133-137); at-least-once = an output that is never
+    # acknowledged keeps its input offset uncommitted and the rank exits non-zero to be respawned
+    # from the committed offsets; auto = at-least-once when offsets are resumed (start_offset
+    # committed or group membership), else at-most-once
+    delivery: str = "auto"
+    producer_retries: int = 3          # kafka-clients retries (0.11 default 0): retriable produce
+                                       # errors are re-sent after retry_backoff_ms
+    retry_backoff_ms: int = 100        # retry.backoff.ms
+    delivery_timeout_ms: int = 120000  # delivery.timeout.ms: no retry after this long
     value_format: str = "json"         # json-string = spring JsonSerializer double encoding
     type_id_header: bool = False       # add __TypeId__: java.lang.String (spring JsonSerializer)
     linger_ms: int = 0
@@ -198,6 +212,12 @@ class GaleConfig:
             raise ValueError("replicas/gpus must be >= 0")
         if self.ranks < 0 or self.rank_restart_backoff_ms < 0:
             raise ValueError("--ranks / --rank-restart-backoff-ms must be >= 0")
+        if self.producer_retries < 0 or self.retry_backoff_ms < 0 or self.delivery_timeout_ms < 1:
+            raise ValueError("--producer-retries / --retry-backoff-ms must be >= 0, "
+                             "--delivery-timeout-ms >= 1")
+        if self.effective_delivery == "at-least-once" and self.sink_mode == "fire-and-forget":
+            raise ValueError("at-least-once delivery needs acknowledged sends: --sink-mode "
+                             "async|sync (or --delivery at-most-once)")
         if self.locality_split < 1:
             raise ValueError("locality_split must be >= 1")
         if not self.topology_name:
@@ -210,6 +230,14 @@ class GaleConfig:
     def effective_group(self) -> str:
         return self.group_id or self.topology_name
 
+    @property
+    def effective_delivery(self) -> str:
+        if self.delivery != "auto":
+            return self.delivery
+        resumes = self.start_offset == "committed" or self.group_membership
+        return "at-least-once" if resumes and self.sink_mode != "fire-and-forget" \
+            else "at-most-once"
+
     def engine_dict(self, H: int, W: int, C: int, classes: int) -> Dict[str, Any]:
         """Keyword dict for the native ``gale._C.Engine``."""
         return dict(
@@ -217,6 +245,9 @@ class GaleConfig:
             group_id=self.effective_group, client_id=self.topology_name,
             partitions=[int(p) for p in self.partitions.split(",") if p.strip()],
             source_parallelism=self.source_parallelism, start_offset=self.start_offset,
+            auto_offset_reset=self.auto_offset_reset, delivery=self.effective_delivery,
+            producer_retries=self.producer_retries, retry_backoff_ms=self.retry_backoff_ms,
+            delivery_timeout_ms=self.delivery_timeout_ms,
             commit_interval_ms=self.commit_interval_ms, sink_parallelism=self.sink_parallelism,
             fetch_min_bytes=self.fetch_min_bytes, fetch_max_wait_ms=self.fetch_max_wait_ms,
             recv_lowat=self.recv_lowat_kb << 10 if self.recv_lowat_kb >= 0 else -1,

@@ -49,8 +49,9 @@ class InvalidTopologyError(TopologyError):
 
 
 class RankFailedError(TopologyError):
-    """Every replica of this rank is dead (e.g. a hung device the watchdog gave up on): the
-    process exits non-zero so the rank supervisor (--ranks) replaces it."""
+    """Every replica of this rank is dead (e.g. a hung device the watchdog gave up on), or an
+    output could not be delivered under at-least-once delivery: the process exits non-zero so
+    the rank supervisor (--ranks) replaces it, resuming from the committed offsets."""
 
 
 def _alive(pid: int) -> bool:
@@ -162,7 +163,9 @@ def run_topology(cfg: GaleConfig, stop_event: Optional[threading.Event] = None,
     from gale.metrics import MetricsServer, Reporter
 
     rank, world, local_rank = _dist_env()
-    name = cfg.topology_name if world == 1 else f"{cfg.topology_name}.r{rank}"
+    supervised = bool(os.environ.get("GALE_SUPERVISED"))
+    # a supervised rank registers as NAME.r<rank> even alone (--ranks 1): the supervisor holds NAME
+    name = cfg.topology_name if world == 1 and not supervised else f"{cfg.topology_name}.r{rank}"
     registry = Registry(cfg.registry_dir)
     registry.register(name, {"input_topic": cfg.input_topic, "output_topic": cfg.output_topic,
                              "bootstrap": cfg.bootstrap, "model": cfg.model, "rank": rank})
@@ -175,7 +178,13 @@ def run_topology(cfg: GaleConfig, stop_event: Optional[threading.Event] = None,
             broker = start_embedded_broker(cfg)
         devices = None
         incarnation = int(os.environ.get("GALE_RANK_INCARNATION", "0"))
-        supervised = bool(os.environ.get("GALE_SUPERVISED"))
+        if incarnation > 0 and cfg.start_offset != "committed":
+            # a respawned rank resumes where its predecessor's commits end (storm-kafka: a
+            # restarted worker of the same topology reads its ZK offsets; ignoreZkOffsets only
+            # applies to a new submission); "latest" would skip whatever was in flight
+            if cfg.start_offset == "earliest":
+                cfg.auto_offset_reset = "earliest"
+            cfg.start_offset = "committed"
         if world > 1 and not cfg.stub:
             dev = local_rank
             if cfg.shared_gpu_rehearsal:
@@ -234,7 +243,7 @@ def run_topology(cfg: GaleConfig, stop_event: Optional[threading.Event] = None,
         final = reporter.report()
         reporter.close()
         if failed:
-            raise RankFailedError(f"rank {rank}: every replica is dead ({failed})")
+            raise RankFailedError(f"rank {rank}: {failed}")
         return dict(engine.stats(), final=final)
     finally:
         if engine is not None and engine.running:
@@ -257,14 +266,19 @@ def _serve_until_done(engine, cfg: GaleConfig, stop_event: threading.Event) -> s
         wait = 0.25 if deadline is None else min(0.25, max(0.0, deadline - time.monotonic()))
         if stop_event.wait(wait) or (deadline is not None and time.monotonic() >= deadline):
             return ""
-        alive = engine.stats().get("replicas_alive", 1)
+        st = engine.stats()
+        if st.get("delivery_failed", 0):
+            return (f"at-least-once delivery failed: {int(st.get('undelivered', 0))} output(s) "
+                    f"not acknowledged after {cfg.producer_retries} retries; offsets stay "
+                    f"uncommitted from the first of them")
+        alive = st.get("replicas_alive", 1)
         if alive > 0:
             dead_since = None
             continue
         now = time.monotonic()
         dead_since = dead_since or now
         if now - dead_since >= grace:
-            return f"replicas_alive 0 for {now - dead_since:.1f} s"
+            return f"every replica is dead (replicas_alive 0 for {now - dead_since:.1f} s)"
 
 
 def rank_partitions(cfg: GaleConfig, rank: int, world: int) -> str:

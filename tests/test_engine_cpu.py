@@ -203,12 +203,90 @@ def test_latest_only_skips_backlog(broker):
 
 
 def test_parse_error_and_producer_fault_injection(broker):
+    """producer_fail@P drops produce requests before they reach the broker (a lost request);
+    the sink producers retry them, so every input still has exactly its output."""
     produce_images(broker, [1] * 60)
-    eng, out = run(broker, 60, fault="parse_error@0.5,producer_fail@0.2", seed=3)
+    eng, out = run(broker, 60, fault="parse_error@0.5,producer_fail@0.3", seed=3,
+                   producer_retries=10, retry_backoff_ms=5, max_batch=4)
     st = eng.stats()
     assert 10 < st["errors"] < 50
-    assert st["produce_failures"] > 0
+    assert st["produce_retried_records"] > 0 and st["produce_failed_requests"] > 0
+    assert st["produce_failures"] == 0 and st["undelivered"] == 0
     assert len(out) == 60
+
+
+def _keyed(broker, n, seed=0, tag="k"):
+    """n keyed one-image records over the 2 input partitions -> {key: (partition, offset)}."""
+    rng = np.random.default_rng(seed)
+    where = {}
+    for i in range(n):
+        k = f"{tag}{i}".encode()
+        p = i % 2
+        off = broker.log_end("in", p)
+        broker.append("in", p, [C.encode_instances(rng.random((1, H, W, CH), dtype=np.float32))],
+                      [k])
+        where[k] = (p, off)
+    return where
+
+
+def test_producer_retries_through_broker_rejections(broker):
+    """The broker truly refuses produces (NOT_LEADER_FOR_PARTITION for its next 3 appends to
+    the output topic): kafka-clients-style retries re-send them, every input gets exactly one
+    output and the commits reach the log ends."""
+    where = _keyed(broker, 30)
+    broker.fail_produce("out", 3)
+    eng, out = run(broker, 30, group_id="gr", output_key="input", producer_retries=3,
+                   retry_backoff_ms=5, max_batch=4)
+    st = eng.stats()
+    assert st["produce_retried_records"] > 0 and st["produce_failures"] == 0
+    assert sorted(r["key"] for r in out) == sorted(where)
+    assert broker.committed("gr", "in", 0) == 15 and broker.committed("gr", "in", 1) == 15
+
+
+def test_at_least_once_commit_never_passes_an_unproduced_record(broker):
+    """at-least-once (start_offset=committed): the broker rejects produces with retries
+    spent, so some outputs are never acknowledged. The committed offset of each partition stays
+    at or before its first record without an output, the engine raises delivery_failed (the
+    rank would exit non-zero and be respawned), and a restart from the committed offsets gives
+    every input key an output (duplicates allowed, no loss)."""
+    where = _keyed(broker, 40)
+    broker.fail_produce("out", 4)  # the first 4 partition appends fail; no retries below
+    eng, out = run(broker, 40, group_id="alo", start_offset="committed",
+                   auto_offset_reset="earliest", output_key="input", producer_retries=0,
+                   max_batch=4, sink_parallelism=1)
+    st = eng.stats()
+    assert st["delivery_failed"] == 1 and st["undelivered"] > 0
+    assert st["produce_failures"] == st["undelivered"]
+    got = {r["key"] for r in out}
+    missing = set(where) - got
+    assert missing, "the injected rejections left every output delivered"
+    for p in (0, 1):
+        first_missing = min([where[k][1] for k in missing if where[k][0] == p], default=None)
+        c = broker.committed("alo", "in", p)
+        if first_missing is not None:
+            assert c <= first_missing, (p, c, first_missing)
+    # the respawn: a fresh engine resumes from the committed offsets
+    eng2, out2 = run(broker, sum(20 - broker.committed("alo", "in", p) for p in (0, 1)),
+                     group_id="alo", start_offset="committed", output_key="input")
+    assert eng2.stats()["delivery_failed"] == 0
+    assert {r["key"] for r in out2} >= set(where)
+    assert broker.committed("alo", "in", 0) == 20 and broker.committed("alo", "in", 1) == 20
+
+
+def test_at_most_once_is_the_reference_semantics(broker):
+    """delivery=at-most-once (the reference: KafkaBolt fails the unanchored tuple and nothing
+    replays it): a failed output is completed and the commit moves past it."""
+    _keyed(broker, 10)
+    broker.fail_produce("out", 1000)
+    eng, out = run(broker, 10, group_id="amo", delivery="at-most-once", producer_retries=0,
+                   output_key="input")
+    st = eng.stats()
+    assert out == [] and st["produce_failures"] == 10 and st["delivery_failed"] == 0
+    assert broker.committed("amo", "in", 0) == 5 and broker.committed("amo", "in", 1) == 5
+    with pytest.raises(ValueError):
+        make_cfg(broker, delivery="at-least-once", sink_mode="fire-and-forget").validate()
+    assert make_cfg(broker, start_offset="committed").effective_delivery == "at-least-once"
+    assert make_cfg(broker, start_offset="latest").effective_delivery == "at-most-once"
 
 
 def test_backpressure_small_queue(broker):

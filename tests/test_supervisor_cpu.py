@@ -18,33 +18,14 @@ import pytest
 
 from gale._native import native
 from gale.supervisor import RankSupervisor, child_argv
+from supervised import diagnose, lines, ranks_serving, read_keys, start_job, wait_for
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 C = native()
 K = C.kafka
 
 
-def wait_for(pred, timeout=30.0):
-    t = time.time() + timeout
-    while time.time() < t:
-        if pred():
-            return True
-        time.sleep(0.05)
-    return False
-
-
-def _lines(path):
-    if not os.path.exists(path):
-        return []
-    out = []
-    for x in open(path):
-        x = x.strip()
-        if x:
-            try:
-                out.append(json.loads(x))
-            except json.JSONDecodeError:  # (a line being written)
-                pass
-    return out
+_lines = lines
 
 
 def test_child_argv_drops_ranks():
@@ -57,6 +38,7 @@ def test_supervised_rank_killed_is_respawned_and_rejoins(tmp_path):
     b = K.Broker()
     b.start()
     sup = None
+    log = tmp_path / "job.log"
     try:
         b.create_topic("in", 6)
         b.create_topic("out", 1)
@@ -64,30 +46,30 @@ def test_supervised_rank_killed_is_respawned_and_rejoins(tmp_path):
         payload = [C.encode_instances(rng.random((1, 32, 32, 3), dtype=np.float32))
                    for _ in range(16)]
         metrics = tmp_path / "m.jsonl"
-        cmd = [sys.executable, "-m", "gale", "sup", "in", "out", "--ranks", "3",
-               "--bootstrap", f"127.0.0.1:{b.port}", "--stub", "--group-membership",
-               "--group-id", "G", "--start-offset", "committed", "--output-key", "input",
-               "--session-timeout-ms", "1500", "--heartbeat-interval-ms", "100",
-               "--rebalance-timeout-ms", "3000", "--commit-interval-ms", "100",
-               "--rank-restart-backoff-ms", "300", "--rank-max-restarts", "2",
-               "--registry-dir", str(tmp_path / "reg"), "--metrics-file", str(metrics),
-               "--metrics-interval", "0.25", "--max-batch", "16", "--max-wait-us", "500",
-               "--source-parallelism", "1", "--duration", "120"]
-        sup = subprocess.Popen(cmd, cwd=ROOT, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
-                               text=True, env=dict(os.environ, OMP_NUM_THREADS="1"))
-        assert wait_for(lambda: len(b.describe_group("G")["members"]) == 3, 90), \
-            "three supervised ranks did not join the group"
         reg = tmp_path / "reg"
+        sup = start_job(["sup", "in", "out", "--ranks", "3",
+                         "--bootstrap", f"127.0.0.1:{b.port}", "--stub", "--group-membership",
+                         "--group-id", "G", "--start-offset", "committed",
+                         "--auto-offset-reset", "earliest", "--output-key", "input",
+                         "--session-timeout-ms", "1500", "--heartbeat-interval-ms", "100",
+                         "--rebalance-timeout-ms", "3000", "--commit-interval-ms", "100",
+                         "--rank-restart-backoff-ms", "300", "--rank-max-restarts", "2",
+                         "--registry-dir", str(reg), "--metrics-file", str(metrics),
+                         "--metrics-interval", "0.25", "--max-batch", "16", "--max-wait-us",
+                         "500", "--source-parallelism", "1", "--duration", "120"], log)
+        assert wait_for(lambda: ranks_serving(metrics, 3, 6), 90), \
+            "three supervised ranks did not take partitions\n" + \
+            diagnose(b, {}, [], "G", "in", 6, log, metrics)
         assert wait_for(lambda: (reg / "sup.json").exists() and (reg / "sup.r1.json").exists())
         victim = json.load(open(reg / "sup.r1.json"))["pid"]
-        keys = []
+        where = {}
         i = 0
         t0 = time.time()
         gen_at_kill = None
         while time.time() - t0 < 5.0:
             for _ in range(6):
                 k = f"s{i}".encode()
-                keys.append(k)
+                where[k] = (i % 6, b.log_end("in", i % 6))
                 b.append("in", i % 6, [payload[i % 16]], [k])
                 i += 1
             if gen_at_kill is None and time.time() - t0 > 1.5:
@@ -106,8 +88,14 @@ def test_supervised_rank_killed_is_respawned_and_rejoins(tmp_path):
         assert new_pid != victim
         assert wait_for(lambda: len(b.describe_group("G")["members"]) == 3, 30)
         # at-least-once across the kill: every input key has an output record
-        assert wait_for(lambda: set(keys) <= {r["key"] for r in b.read("out", 0)}, 60), \
-            "records were lost across the rank restart"
+        out = {}
+
+        def all_out():
+            out.update(read_keys(b, "out"))
+            return set(where) <= set(out)
+
+        assert wait_for(all_out, 60), "records were lost across the rank restart\n" + \
+            diagnose(b, where, out, "G", "in", 6, log, metrics)
         # the three members of the final generation cover every partition
         g = b.describe_group("G")["generation"]
 
@@ -122,7 +110,8 @@ def test_supervised_rank_killed_is_respawned_and_rejoins(tmp_path):
         kill = subprocess.run([sys.executable, "-m", "gale", "kill", "sup", "--wait-secs", "30",
                                "--registry-dir", str(reg)], cwd=ROOT, timeout=60)
         assert kill.returncode == 0
-        _, err = sup.communicate(timeout=60)
+        sup.wait(timeout=60)
+        err = open(log, errors="replace").read()
         assert sup.returncode == 0, err[-3000:]
         events = [json.loads(x) for x in err.splitlines() if x.startswith('{"ts"')]
         kinds = [(e["event"], e.get("rank")) for e in events]
@@ -130,6 +119,158 @@ def test_supervised_rank_killed_is_respawned_and_rejoins(tmp_path):
         ex = [e for e in events if e["event"] == "rank_exit" and e["rank"] == 1]
         assert ex[0]["rc"] == -signal.SIGKILL
         assert [e for e in events if e["event"] == "job_exit"][0]["restarts"] == [0, 1, 0]
+        sup = None
+    finally:
+        if sup is not None and sup.poll() is None:
+            sup.kill()
+            sup.wait()
+        b.stop()
+
+
+def _stop_job(sup, reg, name):
+    kill = subprocess.run([sys.executable, "-m", "gale", "kill", name, "--wait-secs", "30",
+                           "--registry-dir", str(reg)], cwd=ROOT, timeout=60)
+    assert kill.returncode == 0
+    sup.wait(timeout=60)
+
+
+def test_supervised_single_rank(tmp_path):
+    """--ranks 1: the supervisor holds NAME in the registry, the rank registers as
+    NAME.r0 and serves (it used to collide with its own supervisor and exit 1)."""
+    b = K.Broker()
+    b.start()
+    sup = None
+    log = tmp_path / "job.log"
+    try:
+        b.create_topic("in", 1)
+        b.create_topic("out", 1)
+        metrics = tmp_path / "m.jsonl"
+        reg = tmp_path / "reg"
+        sup = start_job(["one", "in", "out", "--ranks", "1", "--bootstrap",
+                         f"127.0.0.1:{b.port}", "--stub", "--start-offset", "earliest",
+                         "--registry-dir", str(reg), "--metrics-file", str(metrics),
+                         "--metrics-interval", "0.25", "--duration", "60"], log)
+        assert wait_for(lambda: ranks_serving(metrics, 1, 1, group=False), 60), \
+            open(log).read()[-3000:]
+        assert (reg / "one.json").exists() and (reg / "one.r0.json").exists()
+        rng = np.random.default_rng(1)
+        for i in range(10):
+            b.append("in", 0, [C.encode_instances(rng.random((1, 32, 32, 3), dtype=np.float32))],
+                     [b"k%d" % i])
+        assert wait_for(lambda: len(b.read("out", 0)) == 10, 30)
+        _stop_job(sup, reg, "one")
+        assert sup.returncode == 0, open(log).read()[-3000:]
+        sup = None
+    finally:
+        if sup is not None and sup.poll() is None:
+            sup.kill()
+            sup.wait()
+        b.stop()
+
+
+def test_static_partition_rank_respawn_resumes_from_committed(tmp_path):
+    """Static p % world partitions with the default --start-offset latest: a
+    respawned rank resumes from the committed offsets (storm-kafka's restarted worker reads its
+    ZK offsets), so the records in flight when it was SIGKILLed are served, not skipped."""
+    b = K.Broker()
+    b.start()
+    sup = None
+    log = tmp_path / "job.log"
+    try:
+        b.create_topic("in", 4)
+        b.create_topic("out", 1)
+        rng = np.random.default_rng(2)
+        payload = [C.encode_instances(rng.random((1, 32, 32, 3), dtype=np.float32))
+                   for _ in range(8)]
+        metrics = tmp_path / "m.jsonl"
+        reg = tmp_path / "reg"
+        sup = start_job(["st", "in", "out", "--ranks", "2", "--bootstrap",
+                         f"127.0.0.1:{b.port}", "--stub", "--output-key", "input",
+                         "--commit-interval-ms", "100", "--rank-restart-backoff-ms", "200",
+                         "--stub-delay-us", "2000", "--max-batch", "8",
+                         "--registry-dir", str(reg), "--metrics-file", str(metrics),
+                         "--metrics-interval", "0.25", "--duration", "120"], log)
+        assert wait_for(lambda: ranks_serving(metrics, 2, 4, group=False), 60), \
+            diagnose(b, {}, [], "st", "in", 4, log, metrics)
+        victim = json.load(open(reg / "st.r1.json"))["pid"]
+        where = {}
+        for i in range(400):
+            k = f"t{i}".encode()
+            where[k] = (i % 4, b.log_end("in", i % 4))
+            b.append("in", i % 4, [payload[i % 8]], [k])
+            if i == 200:
+                os.kill(victim, signal.SIGKILL)
+        out = {}
+
+        def all_out():
+            out.update(read_keys(b, "out"))
+            return set(where) <= set(out)
+
+        assert wait_for(all_out, 60), diagnose(b, where, out, "st", "in", 4, log, metrics)
+        _stop_job(sup, reg, "st")
+        sup = None
+    finally:
+        if sup is not None and sup.poll() is None:
+            sup.kill()
+            sup.wait()
+        b.stop()
+
+
+def test_delivery_failure_exits_rank_and_respawn_delivers(tmp_path):
+    """at-least-once end to end: the output topic rejects every produce for a while and the
+    producer's retries run out, so the rank raises delivery_failed, exits non-zero and is
+    respawned; the new incarnation resumes from the committed offsets (which never passed the
+    undelivered records) and, once the broker accepts produces again, every key has an
+    output."""
+    b = K.Broker()
+    b.start()
+    sup = None
+    log = tmp_path / "job.log"
+    try:
+        b.create_topic("in", 2)
+        b.create_topic("out", 1)
+        rng = np.random.default_rng(3)
+        metrics = tmp_path / "m.jsonl"
+        reg = tmp_path / "reg"
+        sup = start_job(["df", "in", "out", "--ranks", "1", "--bootstrap",
+                         f"127.0.0.1:{b.port}", "--stub", "--output-key", "input",
+                         "--start-offset", "committed", "--auto-offset-reset", "earliest",
+                         "--producer-retries", "2", "--retry-backoff-ms", "20",
+                         "--commit-interval-ms", "100", "--rank-restart-backoff-ms", "500",
+                         "--rank-max-restarts", "5",
+                         "--registry-dir", str(reg), "--metrics-file", str(metrics),
+                         "--metrics-interval", "0.25", "--duration", "120"], log)
+        assert wait_for(lambda: ranks_serving(metrics, 1, 2, group=False), 60), \
+            diagnose(b, {}, [], "df", "in", 2, log, metrics)
+        where = {}
+        for i in range(40):
+            k = f"d{i}".encode()
+            where[k] = (i % 2, b.log_end("in", i % 2))
+            if i == 20:
+                b.fail_produce("out", 1 << 30)  # the broker refuses every produce from here
+            b.append("in", i % 2, [C.encode_instances(rng.random((1, 32, 32, 3),
+                                                                 dtype=np.float32))], [k])
+            time.sleep(0.01)
+
+        def exited():
+            return '"rank_exit"' in open(log, errors="replace").read()
+
+        assert wait_for(exited, 60), diagnose(b, where, read_keys(b, "out"), "df", "in", 2, log,
+                                              metrics)
+        b.fail_produce("out", 0)  # accepting again
+        out = {}
+
+        def all_out():
+            out.update(read_keys(b, "out"))
+            return set(where) <= set(out)
+
+        assert wait_for(all_out, 60), diagnose(b, where, out, "df", "in", 2, log, metrics)
+        text = open(log, errors="replace").read()
+        assert "at-least-once delivery failed" in text
+        events = [json.loads(x) for x in text.splitlines() if x.startswith('{"ts"')]
+        assert any(e["event"] == "rank_exit" and e["rc"] == 3 for e in events)
+        assert any(e["event"] == "rank_respawn" for e in events)
+        _stop_job(sup, reg, "df")
         sup = None
     finally:
         if sup is not None and sup.poll() is None:
