@@ -6,8 +6,12 @@ What one rank (= one GPU, launched by torch.distributed.run for N > 1) does:
 
 * starts an embedded Kafka-protocol broker on 127.0.0.1. With N ranks the N brokers form ONE
   Kafka cluster: the input topic has N x P partitions, partition p led by rank p % N's broker,
-  and every rank consumes exactly the partitions it leads (one partition per replica, BASELINE
-  config 3) - so all ranks share one input topic, as the reference's spouts share INPUT_TOPIC;
+  and every rank consumes exactly the partitions it leads - so all ranks share one input topic,
+  as the reference's spouts share INPUT_TOPIC. P (--partitions) defaults to 11-12 per GPU, one
+  consumer thread each (more TCP connections than one core can receive on; size_pipeline).
+  ``--baseline-config 3`` runs BASELINE config 3 literally: ONE partition per GPU data-parallel
+  replica, consumed by one source thread (MainTopology.java:26-27,61-62 map 2 spouts to 4 bolts;
+  the replica's streams still share that partition's records);
 * feeds the input partitions with synthetic InstObj records ``{"instances": [[[[...]]]]}``
   (32x32x3 Java-formatted floats, ~35 KB of JSON per image) drawn from ``--distinct`` distinct
   images (default 65536, ~2.3 GB of JSON, so the host stages stream from DRAM, not from cache).
@@ -16,9 +20,12 @@ What one rank (= one GPU, launched by torch.distributed.run for N > 1) does:
   ack) is measured exactly;
 * initialises ResNet-20 weights on rank 0 (seeded random init) and RCCL-broadcasts the packed
   buffer over xGMI to every other rank;
-* runs the full gale engine: Kafka Fetch over TCP -> envelope scan + CRC32C -> micro-batcher ->
-  pinned H2D -> GPU JSON parse -> hipGraph ResNet-20 forward -> D2H softmax ->
-  {"predictions": ...} encode -> Kafka Produce (acks=1) -> ack.
+* runs the full gale engine: Kafka Fetch over TCP (each body received through a cache-resident
+  window and nibble-packed into pinned memory) -> GPU ingest (CRC32C + image counts, one kernel
+  per fetch) -> micro-batcher -> per batch step, launched kernel by kernel (--step-launch direct,
+  the default; a hipGraph replay is --step-launch graph): GPU JSON parse -> whole-network
+  ResNet-20 forward whose epilogue writes the softmax AND its {"predictions": ...} text into
+  host-mapped memory -> Kafka Produce (acks=1) -> ack.
 
 Steady state: warm-up is W steps AND at least ``--min-warmup-s`` seconds AND until the last
 four 500 ms rate windows (2 s) all lie within 5 % of their mean (capped at ``--max-warmup-s``). A step is
@@ -69,7 +76,11 @@ def parse_args(argv=None):
     ap.add_argument("--distinct", type=int, default=0,
                     help="distinct synthetic images (default 65536; 256 = 435 MB for resnet50)")
     ap.add_argument("--partitions", type=int, default=0,
-                    help="input partitions per GPU (default: one per replica, BASELINE config 3)")
+                    help="input partitions per GPU (default 11-12 with >= 16 host CPUs per GPU, "
+                         "see size_pipeline)")
+    ap.add_argument("--baseline-config", type=int, default=0, choices=[0, 3],
+                    help="3 = BASELINE config 3 as written: one input partition per GPU "
+                         "data-parallel replica, one source thread per partition")
     ap.add_argument("--source-parallelism", type=int, default=0,
                     help="consumer threads (default: one per partition)")
     ap.add_argument("--sink-parallelism", type=int, default=2)
@@ -483,15 +494,42 @@ def latency_phase(eng, broker, feeder, bset, parts, rate_img_s, a, ipr):
     app = rf.take_log()
     lat, when = append_to_ack_us(app, ack, with_ack_time=True)
     stages = latency_stages_us(app, ack)
+    # per stage: [p50, p99, p999] in ms and the records above 2 ms in that stage alone
     host["latency_stages_ms"] = {
-        k: [round(float(np.percentile(v, q)) / 1e3, 3) for q in (50, 99)] if len(v) else None
+        k: [round(float(np.percentile(v, q)) / 1e3, 3) for q in (50, 99, 99.9)] if len(v) else None
         for k, v in stages.items()}
+    host["latency_stage_over_2ms"] = {k: int((v > 2000).sum()) for k, v in stages.items()}
+    host["latency_outliers"] = outlier_attribution(stages)
     if a.latency_dump and int(os.environ.get("RANK", "0")) == 0:
         # every 4th record, float32 microseconds (a 2 s window at 1.25 M img/s is 2.5 M records)
         np.savez_compressed(a.latency_dump, latency_us=lat[::4].astype(np.float32),
                             ack_t_ns=when[::4],
                             **{k: v[::4].astype(np.float32) for k, v in stages.items()})
     return lat, achieved, int(len(ack[0]) - len(lat)), host
+
+
+def outlier_attribution(stages, over_us=2000.0, bucket_ms=10.0):
+    """Records whose stage sum (append -> ack) exceeds ``over_us``: how many, which stage held
+    the largest share of each (the stage to blame), and how they cluster in time (distinct
+    ``bucket_ms`` windows of their fetch time: a few windows = stalls of the whole pipeline, e.g.
+    a descheduled thread; many = a diffuse tail)."""
+    names = list(stages)
+    if not names or not len(stages[names[0]]):
+        return {}
+    m = np.stack([np.asarray(stages[k], dtype=np.float64) for k in names])
+    tot = m.sum(axis=0)
+    bad = tot > over_us
+    out = {"n": int(bad.sum()), "of": int(len(tot)), "over_us": over_us}
+    if bad.any():
+        dom = m[:, bad].argmax(axis=0)
+        out["dominant_stage"] = {names[i]: int((dom == i).sum()) for i in range(len(names))}
+        out["stage_mean_ms"] = {names[i]: round(float(m[i, bad].mean()) / 1e3, 3)
+                                for i in range(len(names))}
+        # the outliers' positions in the record stream (the stage arrays keep ack-log order,
+        # which is time order per sink): spread over the window or bunched?
+        pos = np.nonzero(bad)[0]
+        out["runs"] = int(1 + (np.diff(pos) > 64).sum())
+    return out
 
 
 def pipeline_path(a, st) -> str:
@@ -594,6 +632,8 @@ def size_pipeline(a, cpus: float) -> None:
             a.replicas_per_gpu = 2
         else:
             a.replicas_per_gpu = 6 if big else max(1, min(4, int(cpus // 4)))
+    if a.baseline_config == 3:
+        a.partitions, a.source_parallelism = 1, 1
     if a.partitions <= 0:
         if r50:
             a.partitions = 12 if big else 4
@@ -956,7 +996,10 @@ def main(argv=None) -> int:
                        "max_wait_us": a.max_wait_us, "replicas_per_gpu": a.replicas_per_gpu,
                        "decode_threads": a.decode_threads,
                        "locality_split": a.locality_split,
-                       "partitions": n_parts, "step_images_per_gpu": a.step_images,
+                       "partitions": n_parts,
+                       "source_threads_per_gpu": a.source_parallelism or a.partitions,
+                       "baseline_config": a.baseline_config or None,
+                       "step_images_per_gpu": a.step_images,
                        "path": pipeline_path(a, st)},
             "load": (f"offered {a.rate:.0f} images/s per GPU" if a.rate > 0
                      else "value: backlog kept ahead of the consumers (max throughput); "

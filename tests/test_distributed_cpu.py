@@ -117,7 +117,8 @@ def test_scaling_driver_stub_1_2():
     """tools/scaling.py: bench.py at N = 1 (plain process) and N = 2 (torch.distributed.run,
     gloo stub ranks), one JSON line per N and a summary with the weak-scaling efficiency."""
     cmd = [sys.executable, "tools/scaling.py", "--gpus", "1,2", "--stub", "--steps", "4",
-           "--warmup", "1", "--timeout", "240", "--", "--batch", "32", "--distinct", "64",
+           "--warmup", "1", "--timeout", "240", "--placements", "floating", "--",
+           "--batch", "32", "--distinct", "64",
            "--step-images", "512", "--min-warmup-s", "0.2",
            "--replicas-per-gpu", "2", "--stub-null", "--timeout", "120"]
     out = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=600,
@@ -125,8 +126,10 @@ def test_scaling_driver_stub_1_2():
     assert out.returncode == 0, out.stdout[-3000:] + out.stderr[-3000:]
     lines = [json.loads(x) for x in out.stdout.splitlines() if x.startswith("{")]
     assert [r["n_gpus"] for r in lines[:2]] == [1, 2]
-    sc = lines[-1]["scaling"]
+    sc = lines[-1]["scaling"]["floating"]
     assert set(sc) == {"1", "2"} and sc["1"]["efficiency"] == 1.0 and sc["2"]["efficiency"] > 0
+    assert [x["rank"] for x in sc["2"]["per_rank"]] == [0, 1]
+    assert all(x["cores"] is not None and x["img_s"] > 0 for x in sc["2"]["per_rank"])
 
 
 def test_scaling_driver_single_process_mode():
@@ -198,12 +201,33 @@ def test_scaling_dry_run_prints_per_n_config():
                          cwd=ROOT, capture_output=True, text=True, timeout=300)
     assert out.returncode == 0, out.stderr[-3000:]
     lines = [json.loads(x) for x in out.stdout.splitlines() if x.startswith("{")]
-    assert [r["n_gpus"] for r in lines] == [1, 2, 4, 8]
+    # N = 1 once, every N > 1 under both host placements (floating, then --rank-slices)
+    assert [(r["n_gpus"], r["placement"]) for r in lines] == [
+        (1, "floating"), (2, "floating"), (2, "slices"), (4, "floating"), (4, "slices"),
+        (8, "floating"), (8, "slices")]
     one = lines[0]["config"]
     for r in lines[1:]:
         assert f"--gpus {r['n_gpus']}" in r["cmd"]
+        assert ("--rank-slices" in r["cmd"]) == (r["placement"] == "slices")
         c = r["config"]
         assert c["processes"] == r["n_gpus"]
         for k in ("replicas_per_gpu", "partitions_per_gpu", "decode_threads",
                   "step_images_per_gpu"):
             assert c[k] == one[k], k
+
+
+def test_scaling_placement_verdict():
+    """The sweep's placement decision: --rank-slices becomes the default only when it beats the
+    floating placement by more than 2 % at the largest N both ran."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import scaling
+
+    assert scaling.plan([1, 2, 8], ["floating", "slices"]) == [
+        (1, "floating"), (2, "floating"), (2, "slices"), (8, "floating"), (8, "slices")]
+    res = {"floating": {1: {"value": 2.0}, 2: {"value": 4.0}, 8: {"value": 12.0}},
+           "slices": {1: {"value": 2.0}, 2: {"value": 3.9}, 8: {"value": 13.0}}}
+    v = scaling.placement_verdict(res)
+    assert v["n_gpus"] == 8 and v["faster"] == "slices" and v["default"] == "slices"
+    res["slices"][8]["value"] = 12.1  # < 2 %: keep floating
+    assert scaling.placement_verdict(res)["default"] == "floating"
+    assert scaling.placement_verdict({"floating": res["floating"]}) == {}
