@@ -78,3 +78,12 @@ build/host_bench: csrc/tests/host_bench.cpp csrc/codec/json_codec.cpp csrc/kafka
 	@mkdir -p build
 	$(CXX) -O3 -std=c++17 -mavx2 -mfma -msse4.2 -mpclmul -mbmi2 -Icsrc/include \
 	    csrc/tests/host_bench.cpp csrc/codec/json_codec.cpp csrc/kafka/wire.cpp -o $@
+
+# DRAM antagonist for the host-projection test (tools/dram_antagonist.cpp); outside build/ so it
+# travels to the GPU box (build/ is gpurun-ignored)
+tools/bin/dram_antagonist: tools/dram_antagonist.cpp
+	@mkdir -p tools/bin
+	$(CXX) -O2 -std=c++17 -mavx2 -pthread $< -o $@
+
+antagonist: tools/bin/dram_antagonist
+.PHONY: antagonist
