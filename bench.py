@@ -324,6 +324,10 @@ class Timeline:
                    "cores": {k: round((cpu[k] - prev_cpu.get(k, 0.0)) / dt, 2) for k in cpu},
                    "rss_mb": round(_rss_mb()),
                    "queue": int(st.get("queue_records", 0)),
+                   # sources waiting for a free pinned fetch chunk (ingest backpressure)
+                   "pinned_waits": int(st.get("pinned_waits", 0)),
+                   "pinned_wait_s": round(st.get("pinned_wait_s", 0.0), 4),
+                   "batches": int(st.get("batches", 0)),
                    "lag": int(st.get("lag_records", 0)),
                    "fetch_lag": int(st.get("fetch_lag_records", 0))}
             if cg:
