@@ -122,6 +122,9 @@ def parse_args(argv=None):
                     help="pinned fetch-buffer budget per GPU (doubled with --text-pack)")
     ap.add_argument("--text-pack-window-kb", type=int, default=256,
                     help="bounce receive window per source thread")
+    ap.add_argument("--ingest-parse", action=argparse.BooleanOptionalAction, default=True,
+                    help="the GPU ingest parses each fetch's records into an fp32 image arena, "
+                         "so the batch step runs the forward only (whole-network plans)")
     ap.add_argument("--text-pack-bounce", action=argparse.BooleanOptionalAction, default=True,
                     help="with --text-pack: receive through a cache-resident window, keep only "
                          "the packed text + a sparse framing copy in pinned memory")
@@ -517,7 +520,8 @@ def outlier_attribution(stages, over_us=2000.0, bucket_ms=10.0):
     the largest share of each (the stage to blame), and how they cluster in time (distinct
     ``bucket_ms`` windows of their fetch time: a few windows = stalls of the whole pipeline, e.g.
     a descheduled thread; many = a diffuse tail)."""
-    names = list(stages)
+    # (queue = ingest + batching when the log has the split: sum the parts, not both)
+    names = [k for k in stages if not (k == "queue" and "ingest" in stages)]
     if not names or not len(stages[names[0]]):
         return {}
     m = np.stack([np.asarray(stages[k], dtype=np.float64) for k in names])
@@ -541,17 +545,20 @@ def pipeline_path(a, st) -> str:
     if a.stub:
         return "kafka-fetch->host-scan->cpu-stub-replica->kafka-produce"
     hops = ["kafka-fetch"]
+    recs = max(1.0, st.get("ingested_records", 0))
+    pre = st.get("preparsed_records", 0) / recs > 0.5  # the ingest pass parsed the images
     if st.get("ingested_records", 0) > 0:
-        hops.append("gpu-ingest(crc32c+count%s)" % (",nibble-link" if a.text_pack else ""))
+        hops.append("gpu-ingest(crc32c+count%s%s)" % ("+json-parse" if pre else "",
+                                                      ",nibble-link" if a.text_pack else ""))
     else:
         hops.append("host-scan+crc32c")
     batches = max(1.0, st.get("batches", 0))
     step_g = st.get("graph_step_batches", 0) / batches
     fwd_g = st.get("graph_forward_batches", 0) / batches
     if step_g > 0.5:
-        hops.append("%s(json-parse+forward%s+status)" %
-                    ("hipgraph-step" if a.step_launch == "graph" else "step", "+format"
-                     if a.gpu_encode else ""))
+        hops.append("%s(%sforward%s+status)" %
+                    ("hipgraph-step" if a.step_launch == "graph" else "step",
+                     "" if pre else "json-parse+", "+format" if a.gpu_encode else ""))
     else:
         hops.append("gpu-json-parse")
         hops.append("hipgraph-forward" if fwd_g > 0.5 else "forward(direct-launch)")
@@ -816,7 +823,7 @@ def main(argv=None) -> int:
                      decode_threads=a.decode_threads, slo_p99_ms=a.slo_p99_ms,
                      gpu_wait_poll_us=a.gpu_wait_poll_us, gpu_ingest=a.gpu_ingest, gpu_encode=a.gpu_encode,
                      replica_priority=a.replica_priority, step_launch=a.step_launch,
-                     text_pack=a.text_pack, text_pack_bounce=a.text_pack_bounce,
+                     text_pack=a.text_pack, text_pack_bounce=a.text_pack_bounce, ingest_parse=a.ingest_parse,
                      text_pack_window_kb=a.text_pack_window_kb,
                      pinned_fetch_mb=a.pinned_fetch_mb,
                      stub=a.stub, stub_null=a.stub_null, commit_interval_ms=500,

@@ -32,6 +32,7 @@ EngineConfig config_from_dict(const py::dict& d) {
   opt(d, "source_parallelism", c.source_parallelism);
   opt(d, "start_offset", c.start_offset);
   opt(d, "auto_offset_reset", c.auto_offset_reset);
+  opt(d, "ingest_parse", c.ingest_parse);
   opt(d, "fetch_max_wait_ms", c.fetch_max_wait_ms);
   opt(d, "fetch_min_bytes", c.fetch_min_bytes);
   opt(d, "fetch_max_bytes", c.fetch_max_bytes);
@@ -148,13 +149,15 @@ void bind_engine(py::module_& m) {
       .def("take_ack_log", [](Engine& e) {
         const std::vector<AckSample> v = e.take_ack_log();
         py::array_t<int32_t> p(v.size());
-        py::array_t<int64_t> o(v.size()), t(v.size()), tf(v.size()), tt(v.size()), td(v.size());
+        py::array_t<int64_t> o(v.size()), t(v.size()), tf(v.size()), tt(v.size()), td(v.size()),
+            tr(v.size());
         auto pp = p.mutable_unchecked<1>();
         auto po = o.mutable_unchecked<1>();
         auto pt = t.mutable_unchecked<1>();
         auto pf = tf.mutable_unchecked<1>();
         auto pk = tt.mutable_unchecked<1>();
         auto pd = td.mutable_unchecked<1>();
+        auto pr = tr.mutable_unchecked<1>();
         for (size_t i = 0; i < v.size(); ++i) {
           const auto k = (py::ssize_t)i;
           pp(k) = v[i].partition;
@@ -163,9 +166,10 @@ void bind_engine(py::module_& m) {
           pf(k) = v[i].t_fetch_ns;
           pk(k) = v[i].t_take_ns;
           pd(k) = v[i].t_done_ns;
+          pr(k) = v[i].t_ready_ns;
         }
-        // (partition, offset, t_ack, t_fetch, t_take, t_done)
-        return py::make_tuple(p, o, t, tf, tt, td);
+        // (partition, offset, t_ack, t_fetch, t_take, t_done, t_ready)
+        return py::make_tuple(p, o, t, tf, tt, td, tr);
       })
       .def("replica_stats", [](Engine& e) {
         py::list out;

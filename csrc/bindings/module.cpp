@@ -378,7 +378,8 @@ PYBIND11_MODULE(_C, m) {
       .def_property_readonly("slots", &gale::Executor::slots)
       .def_property_readonly("device", &gale::Executor::device)
       .def_property_readonly("graphs_captured", &gale::Executor::graphs_captured)
-      .def_property_readonly("graph_pays", &gale::Executor::graph_pays);
+      .def_property_readonly("graph_pays", &gale::Executor::graph_pays)
+      .def_property_readonly("step_out_ok", &gale::Executor::step_out_ok);
 
   gale::bind_host(m);
 }

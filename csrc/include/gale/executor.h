@@ -113,15 +113,19 @@ class Executor {
   // text, parse verdicts; gale/kernels.h StepOut) - only when step_out_ok()
   bool device_batch_ok() const;
   bool step_out_ok() const { return device_batch_ok() && spec_.ops.size() == 1; }
+  // xs (optional, device memory): image i's fp32 input at xs[i] instead of the slot's input
+  // buffer - images the GPU ingest already parsed (whole-network plans: device_batch_ok())
   void launch_device_batch(int slot, const int* d_batch, hipStream_t stream,
-                           const StepOut* so = nullptr);
+                           const StepOut* so = nullptr, const float* const* xs = nullptr);
 
  private:
   void launch_all(int batch, void* const* bufs, hipStream_t stream,
-                  const int* d_batch = nullptr, const StepOut* so = nullptr);
+                  const int* d_batch = nullptr, const StepOut* so = nullptr,
+                  const float* const* xs = nullptr);
   // ops [begin, end) for images [c0, c0 + batch) of the buffers (c0 > 0: a chunk)
   void launch_ops(size_t begin, size_t end, int batch, void* const* bufs, hipStream_t stream,
-                  int c0 = 0, const int* d_batch = nullptr, const StepOut* so = nullptr);
+                  int c0 = 0, const int* d_batch = nullptr, const StepOut* so = nullptr,
+                  const float* const* xs = nullptr);
   int device_;
   PlanSpec spec_;
   std::vector<int> buckets_;

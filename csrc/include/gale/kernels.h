@@ -163,6 +163,9 @@ struct ResNet20Params {
   // the launch is sized for) - a captured step graph replays one launch for every batch size
   const int* batch_dev;
   StepOut so;  // (prediction text + verdict hand-off in the epilogue)
+  // non-null: image i's fp32 [32][32][3] input is at xs[i] (images the GPU ingest already parsed
+  // into its fetch arenas; device memory) instead of x + i * 3072
+  const float* const* xs;
 };
 hipError_t resnet20_fused_forward(const ResNet20Params& p, int batch, const float* x, float* out,
                                   hipStream_t stream);
@@ -184,6 +187,7 @@ struct LeNet5Params {
   const float* b5;
   const int* batch_dev;  // as ResNet20Params::batch_dev
   StepOut so;            // as ResNet20Params::so
+  const float* const* xs;  // as ResNet20Params::xs ([28][28][1] images)
 };
 hipError_t lenet5_fused_forward(const LeNet5Params& p, int batch, const float* x, float* out,
                                 hipStream_t stream);
@@ -239,10 +243,17 @@ int json_tile_count(int64_t off, int32_t len);
 // recs[record].status, and recs / tile_rec / d_ntiles are only read - they may then be
 // host-mapped pinned memory (the step graph reads the batch's metadata where the host wrote it,
 // with no copy node).
+// images < 0 (with has_cnt): the record's image count is taken from the group sums of its count
+// block on the device (the GPU ingest parses a fetch right behind its counting launch, before
+// the host has read the counts); a total that is not whole images expects nothing (status 1).
+// tile_bad non-null (count_pass false): each tile's verdict (0 / 1 / 2 / 3) goes to
+// tile_bad[tile] by a plain store instead of raising a record status, so it may be host-mapped
+// memory; a record's verdict is the max over its tiles.
 hipError_t json_parse_instances(int nrec, int ntiles, JsonRecord* recs, const int* tile_rec,
                                 const uint8_t* bytes, int H, int W, int C, int* tile_counts,
                                 float* out, hipStream_t stream, bool count_pass = true,
-                                const int* d_ntiles = nullptr, int* status = nullptr);
+                                const int* d_ntiles = nullptr, int* status = nullptr,
+                                int* tile_bad = nullptr);
 
 // Raw (zero initial state, no final inversion) CRC32C of byte windows [end - len, end) of a
 // device buffer, one wave per window (len <= kCrcChunkBytes): each lane folds 64 bytes with

@@ -800,7 +800,7 @@ __global__ __launch_bounds__(256) void json_parse_kernel(JsonRecord* recs, const
                                                          int ntiles, const uint8_t* bytes, int H,
                                                          int W, int C, const int* counts,
                                                          float* out, const int* d_ntiles,
-                                                         int* status) {
+                                                         int* status, int* tile_bad) {
   __shared__ __attribute__((aligned(16))) uint8_t lds_text[kWaves][kText];
   __shared__ uint16_t lds_tok[kWaves][kMaxTok];
   __shared__ uint32_t lds_cm[kWaves][kTile / 16 + 1];  // packed masks of the tile's chunks + 1
@@ -818,7 +818,21 @@ __global__ __launch_bounds__(256) void json_parse_kernel(JsonRecord* recs, const
   const int beg = (int)(r.off - abeg), end = beg + r.len;
   const int aend = (end + 15) & ~15;
   const int per_image = H * W * C;
-  const int expected = r.images * per_image;
+  int expected = r.images * per_image;
+  if (r.images < 0) {
+    // parse at ingest (has_cnt; the host has not read the counts yet): the record's image count
+    // from its group sums in the count block. A total that is not a whole number of images, or
+    // more images than the record's text can hold (>= 2 bytes per number: the arena reserves
+    // len / (2 * per_image) slots for it), expects nothing: no element is stored and the last
+    // tile reports the count mismatch.
+    const int* rc = reinterpret_cast<const int*>(bytes + r.cnt_off);
+    const int nt = record_tiles(r);
+    const int ng = (nt + kGroupTiles - 1) / kGroupTiles;
+    int s = 0;
+    for (int k = lane; k < ng; k += 64) s += rc[nt + k];
+    const int tot = wave_sum_i(s);
+    expected = (tot % per_image == 0 && tot / per_image <= r.len / (2 * per_image)) ? tot : 0;
+  }
   const int tl = t - r.tile0;
   const int t0 = tl * kTile;
   const bool last_tile = t0 + kTile >= end;
@@ -926,7 +940,14 @@ __global__ __launch_bounds__(256) void json_parse_kernel(JsonRecord* recs, const
     if (idx < expected) dst[idx] = val;
   }
   if (last_tile && lane == 0 && base + ntok != expected) bad = max(bad, 1);
-  if (bad) atomicMax(status ? &status[ri] : &recs[ri].status, bad);
+  if (tile_bad) {
+    // the tile's verdict by a plain store (host-mapped results: no atomics over the link)
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) bad = max(bad, __shfl_xor(bad, d, 64));
+    if (lane == 0) tile_bad[t] = bad;
+  } else if (bad) {
+    atomicMax(status ? &status[ri] : &recs[ri].status, bad);
+  }
 }
 
 }  // namespace
@@ -967,15 +988,17 @@ hipError_t ingest_crc_count(const uint8_t* bytes, const CrcChunk* chunks, int nc
 hipError_t json_parse_instances(int nrec, int ntiles, JsonRecord* recs, const int* tile_rec,
                                 const uint8_t* bytes, int H, int W, int C, int* tile_counts,
                                 float* out, hipStream_t stream, bool count_pass,
-                                const int* d_ntiles, int* status) {
+                                const int* d_ntiles, int* status, int* tile_bad) {
   if (nrec <= 0 || ntiles <= 0) return hipSuccess;
   if (H <= 0 || W <= 0 || C <= 0) return hipErrorInvalidValue;
+  if (tile_bad && count_pass) return hipErrorInvalidValue;  // (per-tile verdicts: counted records)
   const int blocks = (ntiles + kWaves - 1) / kWaves;
   if (count_pass)
     hipLaunchKernelGGL(json_count_kernel, dim3(blocks), dim3(64 * kWaves), 0, stream, recs,
                        tile_rec, ntiles, bytes, tile_counts, d_ntiles, status);
   hipLaunchKernelGGL(json_parse_kernel, dim3(blocks), dim3(64 * kWaves), 0, stream, recs,
-                     tile_rec, ntiles, bytes, H, W, C, tile_counts, out, d_ntiles, status);
+                     tile_rec, ntiles, bytes, H, W, C, tile_counts, out, d_ntiles, status,
+                     tile_bad);
   return hipGetLastError();
 }
 

@@ -66,7 +66,7 @@ __global__ __launch_bounds__(kT) void lenet5_fused_kernel(LeNet5Params p, int n,
     s_w2[i] = (float)w2[c * 224 + (r / 6) * 8 + r % 6];
   }
   if (t < 16) s_b2[t] = p.b2[t];
-  const float* xi = x + (size_t)img * 784;
+  const float* xi = p.xs ? p.xs[img] : x + (size_t)img * 784;
   for (int i = t; i < kImg; i += kT) {
     const int y = i / kPad - 2, xx = i % kPad - 2;
     s_img[i] = (y >= 0 && y < 28 && xx >= 0 && xx < 28) ? xi[y * 28 + xx] : 0.f;

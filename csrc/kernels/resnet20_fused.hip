@@ -490,7 +490,8 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void resnet20_fused_kernel(ResNet2
       if (h == 0 || h == 33 || w == 0 || w == 33) IN[i] = T::zero();
     }
     zero_border<F8, NW, 34, 34, 16, L1>(X1);
-    const float4* xi = reinterpret_cast<const float4*>(x + (size_t)img * 3072);
+    const float4* xi =
+        reinterpret_cast<const float4*>(p.xs ? p.xs[img] : x + (size_t)img * 3072);
     for (int i = threadIdx.x; i < 768; i += 64 * NW) {
       const float4 v = xi[i];
       const float e[4] = {v.x, v.y, v.z, v.w};

@@ -32,6 +32,8 @@ class Engine::Batcher {
   // Blocks while the queue is full (backpressure to the Kafka consumer). False once closed.
   bool push_many(std::vector<InRecord>& recs, const std::atomic<bool>& stop) {
     size_t i = 0;
+    const int64_t now = mono_ns();  // ready for batching (decode / ingest done)
+    for (InRecord& r : recs) r.t_ready_ns = now;
     std::unique_lock<std::mutex> lk(mu_);
     while (i < recs.size()) {
       while (q_.size() >= cap_ && !closed_ && !stop)
@@ -328,7 +330,13 @@ void Engine::start() {
     const size_t budget = (size_t)cfg_.pinned_fetch_bytes * (pack ? 2 : 1) / nslots;
     pools_[i] = std::make_shared<PinnedPool>(pack ? codec::pack_layout_bytes(body) + 4096 : body,
                                              budget);
-    if (ingest_for((int)i)) pools_[i]->set_mirror_device(slot_dev_[i]);
+    if (ingest_for((int)i)) {
+      // the image arena behind each mirror (ingest_parse): one fp32 image per 2 * H * W * C
+      // bytes of fetch body, the most images a body of that size can hold
+      const size_t per = (size_t)cfg_.H * cfg_.W * cfg_.C;
+      const size_t arena = cfg_.ingest_parse && per ? (body / (2 * per) + 2) * per * 4 : 0;
+      pools_[i]->set_mirror_device(slot_dev_[i], arena);
+    }
     pools_[i]->set_wait_ms(200);
   }
   running_ = true;
@@ -930,9 +938,13 @@ bool Engine::ingest_fetch(FetchItem& it, std::vector<InRecord>& good, int lane) 
     io.arr_off[i] = s.arr_off;
     io.arr_len[i] = s.arr_len;
   }
+  PinnedPool& pool = *pools_[(size_t)it.slot];
+  const size_t arena_bytes = pool.mirror_extra();
+  float* arena =
+      arena_bytes ? reinterpret_cast<float*>(dev + pool.mirror_extra_offset()) : nullptr;
   try {
-    ingest->run(lane, f, dev, pools_[(size_t)it.slot]->chunk_bytes(),
-                cfg_.check_crcs && !f.crc_checked, cfg_.H, cfg_.W, cfg_.C, io);
+    ingest->run(lane, f, dev, pool.chunk_bytes(), cfg_.check_crcs && !f.crc_checked, cfg_.H,
+                cfg_.W, cfg_.C, io, arena, arena_bytes);
   } catch (const std::exception& e) {
     if (!ingest_failed_.exchange(true))
       fprintf(stderr, "[gale decode] GPU ingest failed (%s): host decode from now on\n", e.what());
@@ -960,6 +972,8 @@ bool Engine::ingest_fetch(FetchItem& it, std::vector<InRecord>& good, int lane) 
     r.dev_value = dev + rr.value_off;
     r.dev_locality = slot_key_[(size_t)it.slot];
     if (io.cnt_off[i] >= 0) r.dev_counts = dev + io.cnt_off[i];
+    r.dev_image = io.img[i];
+    if (r.dev_image) ++ingest_parsed_;
     ++records_in_;
     if (r.len >= 0) bytes_in_ += r.len;
     r.status = corrupt[i] ? (int)codec::CORRUPT : io.status[i];
@@ -1355,6 +1369,7 @@ void Engine::finish_batch(ReplicaSlot* rs, Batch& b) {
     meta.timestamp_ms = r.timestamp_ms;
     meta.t_fetch_ns = r.t_fetch_ns;
     meta.t_take_ns = b.t_take_ns;
+    meta.t_ready_ns = r.t_ready_ns;
     meta.t_done_ns = b.t_done_ns;
     meta.images = r.status == codec::OK ? r.images : 0;
     bool null_value = false;
@@ -1446,7 +1461,7 @@ void Engine::complete_records(const std::vector<InRecord>& rs, bool ok) {
     std::lock_guard<std::mutex> lk(ack_mu_);
     for (size_t i = 0; i < rs.size() && ack_n_ < ack_cap_; ++i)
       ack_push({rs[i].partition, rs[i].offset, now, rs[i].t_fetch_ns, rs[i].t_take_ns,
-                rs[i].t_done_ns});
+                rs[i].t_done_ns, rs[i].t_ready_ns});
   }
   note_completed(completed_ += (int64_t)rs.size(), now);
 }
@@ -1497,7 +1512,8 @@ void Engine::complete_record(const InRecord& r, bool ok) {
   if (ack_log_on_.load(std::memory_order_relaxed) && ok) {
     std::lock_guard<std::mutex> lk(ack_mu_);
     if (ack_n_ < ack_cap_)
-      ack_push({r.partition, r.offset, now, r.t_fetch_ns, r.t_take_ns, r.t_done_ns});
+      ack_push({r.partition, r.offset, now, r.t_fetch_ns, r.t_take_ns, r.t_done_ns,
+                r.t_ready_ns});
   }
   note_completed(++completed_, now);
 }
@@ -1789,14 +1805,17 @@ std::map<std::string, double> Engine::stats() const {
   s["assigned_partitions"] = cfg_.group_membership ? (double)assigned_partitions_
                                                    : (double)partition_offsets().size();
   s["ingested_records"] = (double)ingested_records_;
+  s["ingest_parsed_records"] = (double)ingest_parsed_;
   {
-    int64_t step = 0, fwd = 0;
+    int64_t step = 0, fwd = 0, pre = 0;
     for (auto& r : replicas_) {
       step += r->rep->graph_step_batches();
       fwd += r->rep->graph_forward_batches();
+      pre += r->rep->preparsed_records();
     }
     s["graph_step_batches"] = (double)step;
     s["graph_forward_batches"] = (double)fwd;
+    s["preparsed_records"] = (double)pre;  // records the step took parsed from the ingest arena
   }
   {
     int64_t text = 0, link = 0;

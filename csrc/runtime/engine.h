@@ -80,6 +80,10 @@ struct EngineConfig {
   // packed text + a sparse framing copy in the pinned chunk (BouncePackTap, pack_tap.h); false:
   // the body lands in the chunk whole and is packed behind it (PackTap)
   bool text_pack_bounce = true;
+  // GPU ingest also parses each fetch's records into an fp32 image arena behind its device
+  // mirror (Ingest::run arena): the replicas' batch step then runs the forward only, reading
+  // the images through a pointer table (whole-network plans; others ignore the arena)
+  bool ingest_parse = false;
   int text_pack_window_kb = 256;   // the bounce receive window per source (L2 resident)
   // consumers' receive low-water mark (kafka::ClientConfig::recv_lowat), bytes; 0 = off,
   // < 0 = auto (the bounce window when the bounce receive is on, else off)
@@ -156,6 +160,7 @@ struct AckSample {
   int64_t offset;
   int64_t t_ns;
   int64_t t_fetch_ns, t_take_ns, t_done_ns;
+  int64_t t_ready_ns;  // decode / GPU ingest done: pushed to the batcher
 };
 
 struct ReplicaStats {
@@ -361,6 +366,7 @@ class Engine {
   std::atomic<int64_t> steals_{0};
   std::atomic<bool> ingest_failed_{false};
   std::atomic<int64_t> ingested_records_{0}, ingest_ns_{0};
+  std::atomic<int64_t> ingest_parsed_{0};  // records whose images the ingest pass parsed
   std::mutex dec_mu_;
   std::condition_variable dec_cv_, dec_space_cv_;
   std::deque<FetchItem> dec_q_;

@@ -73,7 +73,7 @@ int Executor::bucket_for(int batch) const {
 }
 
 void Executor::launch_all(int batch, void* const* bufs, hipStream_t stream, const int* d_batch,
-                          const StepOut* so) {
+                          const StepOut* so, const float* const* xs) {
   size_t begin = 0;
   const int ch = spec_.chunk_images;
   if (spec_.chunk_ops > 0 && ch > 0 && batch > ch) {
@@ -81,7 +81,7 @@ void Executor::launch_all(int batch, void* const* bufs, hipStream_t stream, cons
       launch_ops(0, spec_.chunk_ops, std::min(ch, batch - c0), bufs, stream, c0);
     begin = spec_.chunk_ops;
   }
-  launch_ops(begin, spec_.ops.size(), batch, bufs, stream, 0, d_batch, so);
+  launch_ops(begin, spec_.ops.size(), batch, bufs, stream, 0, d_batch, so, xs);
 }
 
 bool Executor::device_batch_ok() const {
@@ -92,15 +92,17 @@ bool Executor::device_batch_ok() const {
 }
 
 void Executor::launch_device_batch(int slot, const int* d_batch, hipStream_t stream,
-                                   const StepOut* so) {
+                                   const StepOut* so, const float* const* xs) {
   if (!device_batch_ok()) throw std::logic_error("plan does not take a device batch count");
   if (so && !step_out_ok()) throw std::logic_error("plan cannot write the step outputs");
+  if (xs && spec_.ops.size() != 1) throw std::logic_error("plan cannot read an input table");
   if (slot < 0 || slot >= spec_.slots) throw std::invalid_argument("bad slot");
-  launch_all(spec_.max_batch, bufs_[slot].data(), stream, d_batch, so);
+  launch_all(spec_.max_batch, bufs_[slot].data(), stream, d_batch, so, xs);
 }
 
 void Executor::launch_ops(size_t begin, size_t end, int batch, void* const* bufs,
-                          hipStream_t stream, int c0, const int* d_batch, const StepOut* so) {
+                          hipStream_t stream, int c0, const int* d_batch, const StepOut* so,
+                          const float* const* xs) {
   auto at = [&](int id, long long bpi) -> void* {
     return static_cast<char*>(bufs[id]) + (size_t)c0 * (size_t)bpi;
   };
@@ -152,6 +154,7 @@ void Executor::launch_ops(size_t begin, size_t end, int batch, void* const* bufs
         rp.fc_b = static_cast<const float*>(op.ptrs[39]);
         rp.fp8 = f8 ? 1 : 0;
         rp.batch_dev = d_batch;
+        rp.xs = xs;
         if (so) rp.so = *so;
         if (f8)
           for (int i = 0; i < 19; ++i) {
@@ -178,6 +181,7 @@ void Executor::launch_ops(size_t begin, size_t end, int batch, void* const* bufs
         lp.w5 = static_cast<const float*>(op.ptrs[8]);
         lp.b5 = static_cast<const float*>(op.ptrs[9]);
         lp.batch_dev = d_batch;
+        lp.xs = xs;
         if (so) lp.so = *so;
         e = lenet5_fused_forward(lp, batch, static_cast<const float*>(in),
                                  static_cast<float*>(out), stream);

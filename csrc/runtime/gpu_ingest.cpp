@@ -86,13 +86,15 @@ size_t align16(size_t n) { return (n + 15) & ~(size_t)15; }
 }  // namespace
 
 void GpuIngest::run(int lane, const kafka::Fetched& f, uint8_t* dev, size_t dev_cap,
-                    bool check_crcs, int H, int W, int C, IngestIO& io) {
+                    bool check_crcs, int H, int W, int C, IngestIO& io, float* arena,
+                    size_t arena_bytes) {
   Lane& L = *lanes_[(size_t)lane % lanes_.size()];
   std::lock_guard<std::mutex> lk(L.mu);
   const size_t nrec_all = f.records.size();
   io.images.assign(nrec_all, 0);
   io.cnt_off.assign(nrec_all, -1);
   io.batch_ok.assign(f.batches.size(), 1);
+  io.img.assign(nrec_all, nullptr);
   // ---- plan: CRC windows (aligned to each batch's end) and the records to count
   std::vector<CrcChunk> chunks;
   std::vector<std::pair<size_t, size_t>> batch_chunks;  // (first chunk, count) per batch
@@ -137,16 +139,47 @@ void GpuIngest::run(int lane, const kafka::Fetched& f, uint8_t* dev, size_t dev_
   lo &= ~(size_t)15;
   const size_t span = hi - lo;
   const size_t ng = packed ? codec::pack_groups(span) : 0;
+  const size_t link = packed ? (size_t)f.tap_result : span;
+  // the per-tile token counts stay with the fetch buffer: at the end of its device mirror when
+  // they fit behind the text (and the packed stream), so the parse - here or in the replica that
+  // later takes these records - reuses them instead of counting again
+  const size_t ncnt = (size_t)ntiles + (size_t)ngroups;  // per record: tile counts, group sums
+  int64_t cnt_base = -1;
+  if (ntiles > 0) {
+    const size_t used = packed ? codec::pack_offset(span) + link : hi;
+    const size_t cb = (ncnt * sizeof(int) + 255) & ~(size_t)255;
+    if (dev_cap > cb + 256 && ((dev_cap - cb) & ~(size_t)255) >= ((used + 64 + 255) & ~(size_t)255))
+      cnt_base = (int64_t)((dev_cap - cb) & ~(size_t)255);
+  }
+  // parse at ingest: every counted record whose arena slots fit, images taken from its counts on
+  // the device (JsonRecord::images = -1), verdicts per tile into host memory
+  const int64_t per = (int64_t)H * W * C;
+  const int64_t S = 2 * per;
+  const bool parse = arena && cnt_base >= 0 && per > 0;
+  std::vector<int> pjs;  // parse record p -> counting record j
+  int ptiles = 0;
+  if (parse) {
+    for (size_t j = 0; j < nr; ++j) {
+      const size_t i = (size_t)rec_of[j];
+      const int64_t off = f.records[i].value_off + io.arr_off[i];
+      const int64_t slot = (off + S - 1) / S, cap = io.arr_len[i] / S;
+      if (cap <= 0 || (slot + cap) * per * (int64_t)sizeof(float) > (int64_t)arena_bytes) continue;
+      pjs.push_back((int)j);
+      ptiles += json_tile_count(off, (int32_t)io.arr_len[i]);
+    }
+  }
+  const size_t np = pjs.size();
   const size_t o_chunks = align16(ng * 2 * sizeof(uint32_t));  // (the pack group table first)
   const size_t o_groups = o_chunks + align16(nc * sizeof(CrcChunk));
   const size_t o_recs = o_groups + align16((size_t)ngroups * sizeof(int2));
-  const size_t o_gsum = o_recs + nr * sizeof(JsonRecord);  // (JsonRecord is 48 bytes)
+  const size_t o_precs = o_recs + nr * sizeof(JsonRecord);  // (JsonRecord is 48 bytes)
+  const size_t o_ptr = o_precs + np * sizeof(JsonRecord);
+  const size_t o_gsum = o_ptr + align16((size_t)ptiles * sizeof(int));
   const size_t o_crc = o_gsum + align16((size_t)ngroups * 4);
   const size_t o_gbad = o_crc + align16(nc * 4);
-  const size_t io_bytes = o_gbad + align16((size_t)ngroups * 4);
+  const size_t o_pbad = o_gbad + align16((size_t)ngroups * 4);
+  const size_t io_bytes = o_pbad + align16((size_t)ptiles * 4);
   check_hip(hipSetDevice(device_), "ingest: hipSetDevice");
-  // count blocks: per record its tile counts then its group sums (ntiles + ngroups ints)
-  const size_t ncnt = (size_t)ntiles + (size_t)ngroups;
   grow(L, io_bytes + 16, ncnt + 1);
   CrcChunk* hc = reinterpret_cast<CrcChunk*>(L.h_io + o_chunks);
   int2* hg = reinterpret_cast<int2*>(L.h_io + o_groups);
@@ -173,18 +206,37 @@ void GpuIngest::run(int lane, const kafka::Fetched& f, uint8_t* dev, size_t dev_
     }
     tile += nt;
   }
+  JsonRecord* hp = reinterpret_cast<JsonRecord*>(L.h_io + o_precs);
+  int* hpt = reinterpret_cast<int*>(L.h_io + o_ptr);
+  {
+    int pt = 0;
+    for (size_t k = 0; k < np; ++k) {
+      const JsonRecord& jr = hr[pjs[k]];
+      JsonRecord& pr = hp[k];
+      pr = jr;
+      pr.slot = (int32_t)((jr.off + S - 1) / S);
+      pr.images = -1;  // from the counts, on the device
+      pr.status = 0;
+      pr.tile0 = pt;
+      pr.has_cnt = 1;
+      pr.cnt_off = cnt_base + (int64_t)(jr.tile0 + jr.grp0) * (int64_t)sizeof(int);
+      pr.grp0 = 0;
+      const int nt = json_tile_count(pr.off, pr.len);
+      for (int t = 0; t < nt; ++t) hpt[pt + t] = (int)k;
+      pt += nt;
+    }
+  }
   // ---- device: text span -> mirror (packed: ONE H2D of the packed stream, expanded in place),
-  // plan H2D, CRC windows, token counts; the kernel stores its results (window CRCs, group sums
-  // and verdicts) straight into the lane's host-mapped buffer, so no D2H copy follows. Both
-  // copies are DMAs (SDMA engines, no CU time). Kernel READS of host memory stay out of this
-  // path: under the serving load the link is busy with these DMAs and every read waits behind
-  // them - expanding the packed text straight from the host-mapped chunk made text_unpack 15x
-  // slower (device time per batch 0.34 -> 2.9 ms), and reading only the plan and the step's
-  // metadata that way still stretched every kernel by 25-40 % (profiles/r5_step_ab.txt).
+  // plan H2D, CRC windows, token counts [, parse]; the kernels store their results (window CRCs,
+  // group sums and verdicts, parse tile verdicts) straight into the lane's host-mapped buffer,
+  // so no D2H copy follows. Both copies are DMAs (SDMA engines, no CU time). Kernel READS of
+  // host memory stay out of this path: under the serving load the link is busy with these DMAs
+  // and every read waits behind them - expanding the packed text straight from the host-mapped
+  // chunk made text_unpack 15x slower (device time per batch 0.34 -> 2.9 ms), and reading only
+  // the plan and the step's metadata that way still stretched every kernel by 25-40 %
+  // (profiles/r5_step_ab.txt).
   hipStream_t st = L.stream;
-  size_t link = span;
   if (packed) {
-    link = (size_t)f.tap_result;
     memcpy(L.h_io, f.buf.get() + codec::tab_offset(span), ng * 2 * sizeof(uint32_t));
     const size_t po = codec::pack_offset(span);
     check_hip(hipMemcpyAsync(dev + po, f.buf.get() + po, link, hipMemcpyHostToDevice, st),
@@ -199,20 +251,9 @@ void GpuIngest::run(int lane, const kafka::Fetched& f, uint8_t* dev, size_t dev_
   uint32_t* d_crc = reinterpret_cast<uint32_t*>(L.h_io + o_crc);   // (host-mapped results)
   int* d_gsum = reinterpret_cast<int*>(L.h_io + o_gsum);
   int* d_gbad = reinterpret_cast<int*>(L.h_io + o_gbad);
+  int* d_pbad = reinterpret_cast<int*>(L.h_io + o_pbad);
   JsonRecord* d_rec = reinterpret_cast<JsonRecord*>(L.d_io + o_recs);
-  // the per-tile token counts stay with the fetch buffer: at the end of its device mirror when
-  // they fit behind the text (and the packed stream), so the replica that later parses these
-  // records reuses them instead of counting again
-  int* d_cnt = L.d_counts;
-  int64_t cnt_base = -1;
-  if (ntiles > 0) {
-    const size_t used = packed ? codec::pack_offset(span) + link : hi;
-    const size_t cb = (ncnt * sizeof(int) + 255) & ~(size_t)255;
-    if (dev_cap > cb + 256 && ((dev_cap - cb) & ~(size_t)255) >= ((used + 64 + 255) & ~(size_t)255)) {
-      cnt_base = (int64_t)((dev_cap - cb) & ~(size_t)255);
-      d_cnt = reinterpret_cast<int*>(dev + cnt_base);
-    }
-  }
+  int* d_cnt = cnt_base >= 0 ? reinterpret_cast<int*>(dev + cnt_base) : L.d_counts;
   // CRC windows and token counts: one launch, one pass of workgroups over the buffer. Packed,
   // the same launch expands the text: CRC and counting waves read the packed stream, and the
   // counting waves store each record's text into the mirror for the parse (r4 ran a separate
@@ -225,6 +266,14 @@ void GpuIngest::run(int lane, const kafka::Fetched& f, uint8_t* dev, size_t dev_
                              packed ? reinterpret_cast<const uint32_t*>(L.d_io) : nullptr,
                              packed ? dev : nullptr),
             "ingest: crc32c + count");
+  // the parse right behind it, same stream (the counts are in place when it starts): the text
+  // -> fp32 images in the fetch's arena, so the batch step later runs only the forward
+  if (np > 0)
+    check_hip(json_parse_instances((int)np, ptiles, reinterpret_cast<JsonRecord*>(L.d_io + o_precs),
+                                   reinterpret_cast<const int*>(L.d_io + o_ptr), dev, H, W, C,
+                                   L.d_counts, arena, st, /*count_pass=*/false, nullptr, nullptr,
+                                   d_pbad),
+              "ingest: parse");
   check_hip(hipEventRecord(L.done, st), "ingest: event");
   wait(L);
   // ---- host: join the windows of each batch and compare; images from the element counts
@@ -245,7 +294,9 @@ void GpuIngest::run(int lane, const kafka::Fetched& f, uint8_t* dev, size_t dev_
   // a record's tokens: the sums of its tile groups (and its verdict: the worst group's)
   const int* gsum = reinterpret_cast<const int*>(L.h_io + o_gsum);
   const int* gbad = reinterpret_cast<const int*>(L.h_io + o_gbad);
-  const int64_t per = (int64_t)H * W * C;
+  const int* pbad = reinterpret_cast<const int*>(L.h_io + o_pbad);
+  std::vector<int> parsed_as(nr, -1);
+  for (size_t k = 0; k < np; ++k) parsed_as[(size_t)pjs[k]] = (int)k;
   for (size_t j = 0; j < nr; ++j) {
     const size_t i = (size_t)rec_of[j];
     const int64_t g1 = j + 1 < nr ? hr[j + 1].grp0 : ngroups;
@@ -265,6 +316,18 @@ void GpuIngest::run(int lane, const kafka::Fetched& f, uint8_t* dev, size_t dev_
       io.images[i] = (int32_t)(tok / per);
       if (cnt_base >= 0)
         io.cnt_off[i] = cnt_base + (hr[j].tile0 + hr[j].grp0) * (int64_t)sizeof(int);
+      const int k = parsed_as[j];
+      if (k >= 0) {
+        // the parse's verdict (structure, element count, numbers): the worst of its tiles, in
+        // the replica's mapping (GpuReplica::wait)
+        const JsonRecord& pr = hp[k];
+        const int nt = json_tile_count(pr.off, pr.len);
+        int v = 0;
+        for (int t = 0; t < nt; ++t) v = std::max(v, pbad[pr.tile0 + t]);
+        if (v == 1 || v == 3) io.status[i] = codec::BAD_SHAPE;
+        else if (v == 2) io.status[i] = codec::BAD_NUMBER;
+        else io.img[i] = arena + (int64_t)pr.slot * per;
+      }
     }
   }
 }

@@ -21,7 +21,8 @@ class GpuIngest : public Ingest {
   ~GpuIngest() override;
   int device() const override { return device_; }
   void run(int lane, const kafka::Fetched& f, uint8_t* dev, size_t dev_cap, bool check_crcs,
-           int H, int W, int C, IngestIO& io) override;
+           int H, int W, int C, IngestIO& io, float* arena = nullptr,
+           size_t arena_bytes = 0) override;
   void link_bytes(int64_t& text, int64_t& link) const override {
     text = text_bytes_.load();
     link = link_bytes_.load();
@@ -34,7 +35,8 @@ class GpuIngest : public Ingest {
     hipEvent_t done = nullptr;
     // one host-mapped pinned buffer and a device image of its plan part:
     //   [pack tab u32 x 2 per 2 KiB group][CrcChunk x nc][int2 group x ng][JsonRecord x nr]
-    //   [group sum i32 x ng][crc u32 x nc][group verdict i32 x ng]
+    //   [parse JsonRecord x np][parse tile -> record i32 x npt]
+    //   [group sum i32 x ng][crc u32 x nc][group verdict i32 x ng][parse tile verdict i32 x npt]
     // the host writes the plan, ONE H2D copies it (up to the group sums) into d_io, and
     // ingest_crc_count stores the results (group sums and verdicts, window CRCs) straight into
     // the host buffer: no D2H copy

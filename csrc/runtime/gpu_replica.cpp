@@ -25,6 +25,7 @@ GpuReplica::GpuReplica(std::shared_ptr<Executor> exec, int H, int W, int C, int 
       wait_poll_us_(wait_poll_us), gpu_encode_(gpu_encode), locality_(locality),
       step_direct_(step_direct) {
   step_graph_ = step_graph && use_graph && exec_->device_batch_ok();
+  ptr_input_ = step_graph_ && gpu_encode_ && step_direct_ && exec_->step_out_ok();
   if (exec_->input_bytes_per_image() != (long long)H * W * C * 4)
     throw std::invalid_argument("GpuReplica: executor input is not fp32 [H, W, C]");
   if (exec_->output_bytes_per_image() != (long long)classes * 4)
@@ -115,13 +116,19 @@ void GpuReplica::drop_steps(Slot& s) {
   }
 }
 
-// Per-slot parser metadata: [header][JsonRecord x max_batch][tile -> record index x tiles_cap],
-// pinned on the host and mirrored on the device (one H2D per batch), plus the per-tile token
-// counts. Growing keeps the first `keep` records already written into the host copy.
+size_t GpuReplica::meta_rec_bytes() const {
+  return (sizeof(JsonRecord) + sizeof(float*)) * (size_t)exec_->max_batch();
+}
+
+// Per-slot parser metadata: [header][JsonRecord x max_batch][input pointer x max_batch]
+// [tile -> record index x tiles_cap], pinned on the host and mirrored on the device (one H2D per
+// batch), plus the per-tile token counts. Growing keeps the first `keep` records and the input
+// pointer table already written into the host copy.
 void GpuReplica::ensure_tiles(Slot& s, int ntiles, int keep) {
   if (ntiles <= s.tiles_cap) return;
   const int cap = std::max(ntiles, s.tiles_cap * 2);
-  const size_t rec_bytes = sizeof(JsonRecord) * (size_t)exec_->max_batch();
+  const size_t rec_bytes = meta_rec_bytes();
+  const size_t xs_off = sizeof(JsonRecord) * (size_t)exec_->max_batch();
   const size_t bytes = kMetaHdr + rec_bytes + sizeof(int) * (size_t)cap;
   if (s.h_hdr) check_hip(hipEventSynchronize(s.done), "hipEventSynchronize");
   // host-mapped: the copy-free step graph's kernels read the metadata from here
@@ -129,6 +136,7 @@ void GpuReplica::ensure_tiles(Slot& s, int ntiles, int keep) {
   memset(h, 0, kMetaHdr);
   if (s.h_hdr) {
     memcpy(h + kMetaHdr, s.h_recs, sizeof(JsonRecord) * (size_t)keep);
+    memcpy(h + kMetaHdr + xs_off, s.h_xs, sizeof(float*) * (size_t)exec_->max_batch());
     drop_steps(s);
     hipHostFree(s.h_hdr);
     hipFree(s.d_hdr);
@@ -140,6 +148,8 @@ void GpuReplica::ensure_tiles(Slot& s, int ntiles, int keep) {
   s.d_hdr = reinterpret_cast<int32_t*>(d);
   s.h_recs = reinterpret_cast<JsonRecord*>(h + kMetaHdr);
   s.d_recs = reinterpret_cast<JsonRecord*>(d + kMetaHdr);
+  s.h_xs = reinterpret_cast<const float**>(h + kMetaHdr + xs_off);
+  s.d_xs = reinterpret_cast<const float**>(d + kMetaHdr + xs_off);
   check_hip(hipMalloc(reinterpret_cast<void**>(&s.d_tiles), sizeof(int) * cap),
             "hipMalloc(tiles)");
   s.h_tile_rec = reinterpret_cast<int*>(reinterpret_cast<char*>(s.h_recs) + rec_bytes);
@@ -179,6 +189,8 @@ void GpuReplica::submit(Batch& b) {
   auto resident = [my_loc](const InRecord& r) {
     return r.dev_value != nullptr && r.dev_locality == my_loc;
   };
+  // images the GPU ingest already parsed (its arena is in this replica's device memory)
+  auto preparsed = [&](const InRecord& r) { return ptr_input_ && resident(r) && r.dev_image; };
   for (const InRecord& r : b.recs) {
     if (resident(r)) continue;  // already in device memory (GPU ingest): nothing to copy
     const uint8_t* base = r.buf.get();
@@ -216,9 +228,25 @@ void GpuReplica::submit(Batch& b) {
   }
   const size_t staged_dev = doff;
   size_t hoff = 0;
-  int nrec = 0, img = 0, ntiles = 0;
+  int nrec = 0, img = 0, ntiles = 0, npre = 0;
   bool count_pass = false;
-  for (const InRecord& r : b.recs) {
+  const int64_t per = (int64_t)H_ * W_ * C_;
+  const float* in = static_cast<const float*>(exec_->input(slot));
+  s.parse_idx.assign(b.recs.size(), -1);
+  if (ptr_input_) ensure_tiles(s, 1, 0);  // (the pointer table lives in the metadata)
+  for (size_t ri = 0; ri < b.recs.size(); ++ri) {
+    const InRecord& r = b.recs[ri];
+    if (img + r.images > exec_->max_batch())
+      throw std::logic_error("GpuReplica: batch exceeds max_batch");
+    if (preparsed(r)) {  // the forward reads its images where the ingest parsed them
+      for (int k = 0; k < r.images; ++k) s.h_xs[img + k] = r.dev_image + k * per;
+      img += r.images;
+      ++npre;
+      continue;
+    }
+    if (ptr_input_)
+      for (int k = 0; k < r.images; ++k) s.h_xs[img + k] = in + (int64_t)(img + k) * per;
+    s.parse_idx[ri] = nrec;
     JsonRecord& jr = s.h_recs[nrec++];
     const uint8_t* base = r.buf.get();
     const size_t lo = (size_t)(r.value + r.arr_off - base);
@@ -260,6 +288,7 @@ void GpuReplica::submit(Batch& b) {
     for (const InRecord& r : b.recs) res += resident(r) ? 1 : 0;
     resident_ += res;
     host_ += (int64_t)b.recs.size() - res;
+    preparsed_ += npre;
   }
   b.images = img;
   ensure_tiles(s, ntiles, nrec);
@@ -280,17 +309,19 @@ void GpuReplica::submit(Batch& b) {
     s.h_hdr[2] = img;
     hipGraphExec_t g = (gpu_encode_ && step_direct_) ? nullptr : step_for(s, slot, count_pass);
     if (gpu_encode_) {
-      // the metadata this batch uses (header, its records, its tile map) as one DMA
-      const size_t rec_bytes = sizeof(JsonRecord) * (size_t)exec_->max_batch();
+      // the metadata this batch uses (header, its records, the input pointer table, its tile
+      // map) as one DMA
+      const size_t rec_bytes = meta_rec_bytes();
       const size_t used = ntiles > 0 ? kMetaHdr + rec_bytes + sizeof(int) * (size_t)ntiles
-                                     : kMetaHdr + sizeof(JsonRecord) * (size_t)nrec;
+                          : ptr_input_ ? kMetaHdr + rec_bytes
+                                       : kMetaHdr + sizeof(JsonRecord) * (size_t)nrec;
       check_hip(hipMemcpyAsync(s.d_hdr, s.h_hdr, used, hipMemcpyHostToDevice, stream_),
                 "H2D step metadata");
     }
     if (g)
       check_hip(hipGraphLaunch(g, stream_), "hipGraphLaunch(step)");
     else  // (the same kernels launched directly: no graph-launch bookkeeping in the runtime)
-      check_hip(enqueue_step(s, slot, count_pass, stream_), "step launch");
+      check_hip(enqueue_step(s, slot, count_pass, stream_, nrec > 0, ptr_input_), "step launch");
     b.step_graph = true;
     ++step_batches_;
     check_hip(hipEventRecord(s.done, stream_), "hipEventRecord");
@@ -335,11 +366,14 @@ void GpuReplica::submit(Batch& b) {
 // under the serving load); reading the metadata from host memory instead stretched every kernel
 // by 25-40 % under the link's DMA load (profiles/r5_step_ab.txt). Captured once per slot into
 // the step graph, or enqueued directly (step_direct).
-hipError_t GpuReplica::enqueue_step(Slot& s, int slot, bool count_pass, hipStream_t st) {
+hipError_t GpuReplica::enqueue_step(Slot& s, int slot, bool count_pass, hipStream_t st,
+                                     bool parse, bool xs) {
   const int mb = exec_->max_batch();
-  hipError_t c = json_parse_instances(mb, s.tiles_cap, s.d_recs, s.d_tile_rec, s.d_bytes, H_, W_,
-                                      C_, s.d_tiles, static_cast<float*>(exec_->input(slot)), st,
-                                      count_pass, s.d_hdr + 1, s.d_status);
+  hipError_t c = hipSuccess;
+  if (parse)  // (a batch of records the ingest already parsed: the forward alone)
+    c = json_parse_instances(mb, s.tiles_cap, s.d_recs, s.d_tile_rec, s.d_bytes, H_, W_, C_,
+                             s.d_tiles, static_cast<float*>(exec_->input(slot)), st, count_pass,
+                             s.d_hdr + 1, s.d_status);
   const bool fused = exec_->step_out_ok();
   StepOut so;
   so.text = s.h_text;
@@ -348,7 +382,8 @@ hipError_t GpuReplica::enqueue_step(Slot& s, int slot, bool count_pass, hipStrea
   so.nrec = s.d_hdr;
   if (c == hipSuccess) {
     try {
-      exec_->launch_device_batch(slot, s.d_hdr + 2, st, fused ? &so : nullptr);
+      exec_->launch_device_batch(slot, s.d_hdr + 2, st, fused ? &so : nullptr,
+                                 xs ? s.d_xs : nullptr);
     } catch (const std::exception&) {
       c = hipErrorLaunchFailure;
     }
@@ -367,7 +402,7 @@ hipGraphExec_t GpuReplica::step_for(Slot& s, int slot, bool count_pass) {
   hipGraphExec_t& g = s.step[count_pass ? 1 : 0];
   if (g) return g;
   const int mb = exec_->max_batch();
-  const size_t meta = kMetaHdr + sizeof(JsonRecord) * (size_t)mb + sizeof(int) * s.tiles_cap;
+  const size_t meta = kMetaHdr + meta_rec_bytes() + sizeof(int) * s.tiles_cap;
   // capture on a private stream (as Executor::run does), replayed on the replica's stream
   hipStream_t cs = nullptr;
   check_hip(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking), "capture stream");
@@ -437,7 +472,9 @@ void GpuReplica::wait(Batch& b) {
   b.dev_status.assign(b.recs.size(), codec::OK);
   const bool copy_free = b.step_graph && gpu_encode_;
   for (size_t i = 0; i < b.recs.size(); ++i) {
-    const int st = copy_free ? s.h_status[i] : s.h_recs[i].status;
+    const int k = i < s.parse_idx.size() ? s.parse_idx[i] : (int)i;
+    if (k < 0) continue;  // parsed (and judged) by the ingest pass
+    const int st = copy_free ? s.h_status[k] : s.h_recs[k].status;
     if (st == 1 || st == 3) b.dev_status[i] = codec::BAD_SHAPE;
     else if (st == 2) b.dev_status[i] = codec::BAD_NUMBER;
   }

@@ -28,6 +28,9 @@ struct IngestIO {
   std::vector<int64_t> cnt_off;
   // out: per Fetched::batches entry, false when its CRC32C did not match (check_crcs)
   std::vector<char> batch_ok;
+  // out (run() with an image arena): per record, its first image already parsed into the arena
+  // as fp32 [H][W][C] (device pointer; its images follow contiguously), null: not parsed
+  std::vector<const float*> img;
 };
 
 class Ingest {
@@ -36,8 +39,14 @@ class Ingest {
   virtual int device() const = 0;
   // lane: the calling decode thread (each lane owns its stream and staging buffers).
   // dev: device mirror of f.buf (same offsets), dev_cap bytes. Throws on a device error.
+  // arena (optional, device memory, arena_bytes): the fetch's records are also parsed into it
+  // (io.img), right behind the counting launch - the batch step then runs the forward only.
+  // Record r's images take the arena slots from ceil(o / S) on, o = its instances array's
+  // offset in the fetch body and S = 2 * H * W * C (a number and its separator take >= 2 bytes,
+  // so the records' slot ranges never overlap and slots < f.size / S + 1).
   virtual void run(int lane, const kafka::Fetched& f, uint8_t* dev, size_t dev_cap,
-                   bool check_crcs, int H, int W, int C, IngestIO& io) = 0;
+                   bool check_crcs, int H, int W, int C, IngestIO& io, float* arena = nullptr,
+                   size_t arena_bytes = 0) = 0;
   // fetched text bytes staged so far, and the bytes that crossed the host link for them (less
   // when the text is nibble-packed, csrc/codec/text_pack.h)
   virtual void link_bytes(int64_t& text, int64_t& link) const { text = link = 0; }

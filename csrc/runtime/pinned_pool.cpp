@@ -20,6 +20,7 @@ struct PinnedPool::State {
   std::vector<uint8_t*> all;
   std::unordered_map<const uint8_t*, uint8_t*> mirrors;  // pinned chunk -> device mirror
   int mirror_device = -1;
+  size_t mirror_extra = 0;
   size_t chunk = 0, max_bytes = 0;
   bool closed = false;
   int64_t in_use = 0, in_use_max = 0, heap_too_large = 0, heap_budget = 0, no_mirror = 0;
@@ -35,9 +36,15 @@ void PinnedPool::set_wait_ms(int ms) {
   st_->wait_ms = ms;
 }
 
-void PinnedPool::set_mirror_device(int device) {
+void PinnedPool::set_mirror_device(int device, size_t extra) {
   std::lock_guard<std::mutex> lk(st_->mu);
   st_->mirror_device = device;
+  st_->mirror_extra = extra;
+}
+
+size_t PinnedPool::mirror_extra() const {
+  std::lock_guard<std::mutex> lk(st_->mu);
+  return st_->mirror_extra;
 }
 
 uint8_t* PinnedPool::mirror(const uint8_t* base) const {
@@ -115,7 +122,9 @@ std::shared_ptr<uint8_t> PinnedPool::alloc(size_t n, bool* pinned) {
           const bool same = hipHostGetDevicePointer(&dp, p, 0) == hipSuccess && dp == p;
           if (st_->mirror_device >= 0 && same &&
               hipSetDevice(st_->mirror_device) == hipSuccess &&
-              hipMalloc(reinterpret_cast<void**>(&d), st_->chunk) == hipSuccess)
+              hipMalloc(reinterpret_cast<void**>(&d),
+                        st_->mirror_extra ? mirror_extra_offset() + st_->mirror_extra
+                                          : st_->chunk) == hipSuccess)
             st_->mirrors[p] = d;  // (no mirror: this chunk's records take the host path)
           else if (st_->mirror_device >= 0)
             ++st_->no_mirror;

@@ -35,10 +35,14 @@ class PinnedPool {
     int64_t waits = 0, wait_us = 0;
   };
   Stats stats() const;
-  // Device mirrors (GPU ingest, ingest.h): every pinned chunk gets a same-size buffer on
-  // `device`, at the same offsets. Set before the first alloc. mirror(base) -> nullptr when base
-  // is not a pinned chunk of this pool (or mirrors are off).
-  void set_mirror_device(int device);
+  // Device mirrors (GPU ingest, ingest.h): every pinned chunk gets a buffer on `device` holding
+  // the chunk's bytes at the same offsets, plus `extra` bytes behind them (from offset
+  // mirror_extra_offset(): the image arena the GPU ingest parses the chunk's records into). Set
+  // before the first alloc. mirror(base) -> nullptr when base is not a pinned chunk of this pool
+  // (or mirrors are off).
+  void set_mirror_device(int device, size_t extra = 0);
+  size_t mirror_extra_offset() const { return (chunk_ + 255) & ~(size_t)255; }
+  size_t mirror_extra() const;
   // Backpressure: with the budget spent and no chunk free, alloc waits up to `ms` for one to be
   // released before it falls back to the heap (0 = fall back at once).
   void set_wait_ms(int ms);

@@ -37,6 +37,7 @@ struct InRecord {
   int64_t timestamp_ms = -1;     // Kafka record CreateTime
   int64_t t_fetch_ns = 0;        // host receive time
   int64_t t_take_ns = 0, t_done_ns = 0;  // its batch's dispatch / device-done time (sink metas)
+  int64_t t_ready_ns = 0;                // decoded / ingested: handed to the batcher
   int64_t arr_off = 0, arr_len = 0;  // instances array inside the value (scan result)
   int32_t images = 0;
   int32_t status = 0;            // codec::Status (scan, then device parse)
@@ -48,6 +49,9 @@ struct InRecord {
   int32_t dev_locality = -1;
   // its per-tile token counts, left on the device by the ingest pass (null: none)
   const uint8_t* dev_counts = nullptr;
+  // its images, already parsed by the ingest pass: fp32 [H][W][C] each, contiguous, in the
+  // fetch's device image arena (null: the replica parses the text)
+  const float* dev_image = nullptr;
   // fragment `split_index` of an oversized record (null for ordinary records)
   std::shared_ptr<SplitRecord> split;
   int32_t split_index = -1;
@@ -89,6 +93,8 @@ class Replica {
   // graph-captured forward only (the rest launched directly)
   virtual int64_t graph_step_batches() const { return 0; }
   virtual int64_t graph_forward_batches() const { return 0; }
+  // records whose images the GPU ingest had parsed (the step ran only the forward for them)
+  virtual int64_t preparsed_records() const { return 0; }
 };
 
 // CPU stub (SURVEY.md §4 "stub replica for plumbing tests on GPU-less hosts"): parses on the
@@ -151,6 +157,7 @@ class GpuReplica : public Replica {
   int64_t host_records() const override { return host_; }
   int64_t graph_step_batches() const override { return step_batches_; }
   int64_t graph_forward_batches() const override { return fwd_graph_batches_; }
+  int64_t preparsed_records() const override { return preparsed_; }
   bool step_graph() const { return step_graph_; }
 
  private:
@@ -174,6 +181,13 @@ class GpuReplica : public Replica {
     // and raise verdicts in d_status; the format node hands them to h_status (host-mapped)
     int* d_status = nullptr;
     int* h_status = nullptr;
+    // input pointer table (ptr_input_): per batch image, its fp32 input on the device (the
+    // ingest arena, or the slot's input buffer for records parsed in the step), in the metadata
+    // allocation behind the records
+    const float** h_xs = nullptr;
+    const float** d_xs = nullptr;
+    // per batch record: its index among the records the step parses (-1: parsed at ingest)
+    std::vector<int> parse_idx;
     hipEvent_t done = nullptr;
     int64_t t_submit_ns = 0;
   };
@@ -182,7 +196,9 @@ class GpuReplica : public Replica {
   void ensure_tiles(Slot& s, int ntiles, int keep);
   void drop_steps(Slot& s);  // (buffers moved: the captured steps point at the old ones)
   hipGraphExec_t step_for(Slot& s, int slot, bool count_pass);
-  hipError_t enqueue_step(Slot& s, int slot, bool count_pass, hipStream_t st);
+  hipError_t enqueue_step(Slot& s, int slot, bool count_pass, hipStream_t st, bool parse = true,
+                          bool xs = false);
+  size_t meta_rec_bytes() const;  // records + input pointer table of the metadata allocation
   static void* mapped_alloc(size_t bytes, const char* what);
   std::shared_ptr<Executor> exec_;
   int H_, W_, C_, classes_;
@@ -202,6 +218,11 @@ class GpuReplica : public Replica {
   std::atomic<int64_t> step_batches_{0}, fwd_graph_batches_{0};
   bool step_graph_ = false;
   bool step_direct_ = false;  // the kernels-only step launched directly, not as a graph replay
+  // batches whose records the GPU ingest already parsed (InRecord::dev_image) run the forward
+  // only, reading each image through the slot's input pointer table (direct-launch step of a
+  // whole-network plan with the epilogue outputs); records without parse as before
+  bool ptr_input_ = false;
+  std::atomic<int64_t> preparsed_{0};
   int64_t expect_ns_ = 0;  // running average of submit -> done (adaptive sleep-poll)
 };
 

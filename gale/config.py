@@ -87,6 +87,10 @@ class GaleConfig:
                                        # window; the pinned chunk gets the packed text and a
                                        # sparse framing copy only (csrc/runtime/pack_tap.h)
     text_pack_window_kb: int = 256     # that window, per source thread
+    ingest_parse: bool = True          # GPU ingest: parse each fetch's records into an fp32 image
+                                       # arena right behind its counting launch, so the batch
+                                       # step of a whole-network plan (LeNet-5, ResNet-20) runs
+                                       # the forward only (images through a pointer table)
     # parallelism (R3)
     workers: int = 8                   # NUM_WORKERS: placement only (one process per GPU here)
     source_parallelism: int = 2        # KAFKA_SPOUT_PARAL

@@ -69,6 +69,13 @@ class Engine:
             reps = self._build_gpu_replicas(devices, params)
         devs = sorted({r.device.index or 0 for r in reps}, key=[r.device.index or 0
                                                                 for r in reps].index)
+        # the GPU ingest parses each fetch into an image arena when every replica's batch step
+        # can take the images from there: the direct-launch step of a whole-network plan with
+        # the prediction text in its epilogue (GpuReplica ptr_input_)
+        d["ingest_parse"] = bool(
+            cfg.ingest_parse and cfg.gpu_ingest and cfg.use_graph and cfg.graph_step
+            and cfg.gpu_encode and cfg.float_format == "jdk19" and cfg.step_launch == "direct"
+            and reps and all(getattr(r.executor, "step_out_ok", False) for r in reps))
         if (len(devs) > 1 or cfg.locality_split > 1) and cfg.numa_pin:
             # single-process multi-GPU: each GPU's replica workers and sources run on the CPUs
             # of that GPU's NUMA node (its pinned fetch buffers are first-touched there)
@@ -180,6 +187,7 @@ class Engine:
         self._native.set_ack_log(on, capacity)
 
     def take_ack_log(self):
-        """(partition, offset, t_ack_ns, t_fetch_ns, t_take_ns, t_done_ns) numpy arrays of the
-        ack log (and clear it); all CLOCK_MONOTONIC."""
+        """(partition, offset, t_ack_ns, t_fetch_ns, t_take_ns, t_done_ns, t_ready_ns) numpy
+        arrays of the ack log (and clear it); all CLOCK_MONOTONIC. t_ready: decode / GPU ingest
+        done, the record handed to the batcher."""
         return self._native.take_ack_log()

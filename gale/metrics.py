@@ -245,12 +245,23 @@ def latency_stages_us(append_log, ack_log):
     broker_source = append -> fetch response received (broker residency, fetch wait, socket),
     queue = fetch -> batch dispatched (decode / GPU ingest and batching), replica = dispatch ->
     device done (H2D, parse, forward, D2H, completion wait), sink = done -> produce ack
-    (prediction text, produce request, broker ack). Records without stage times are skipped."""
+    (prediction text, produce request, broker ack). With a t_ready column (ack logs of round 6 on)
+    queue is also split into ingest = fetch -> handed to the batcher (CRC / count [/ parse] on
+    the GPU, or the host decode) and batching = handed -> dispatched; queue = ingest + batching.
+    Records without stage times are skipped."""
     import numpy as np
 
     idx, tapp = _match_appends(append_log, ack_log)
     tack, tf, tt, td = (np.asarray(ack_log[k])[idx] for k in (2, 3, 4, 5))
+    tr = np.asarray(ack_log[6])[idx] if len(ack_log) > 6 else None
     ok = (tf > 0) & (tt > 0) & (td > 0)
+    if tr is not None:
+        ok &= tr > 0
+        tr = tr[ok]
     tapp, tack, tf, tt, td = tapp[ok], tack[ok], tf[ok], tt[ok], td[ok]
-    return {"broker_source": (tf - tapp) / 1e3, "queue": (tt - tf) / 1e3,
-            "replica": (td - tt) / 1e3, "sink": (tack - td) / 1e3}
+    out = {"broker_source": (tf - tapp) / 1e3, "queue": (tt - tf) / 1e3,
+           "replica": (td - tt) / 1e3, "sink": (tack - td) / 1e3}
+    if tr is not None:
+        out["ingest"] = (tr - tf) / 1e3
+        out["batching"] = (tt - tr) / 1e3
+    return out

@@ -165,15 +165,18 @@ def centered_log(p):
 
 @pytest.mark.parametrize("model,ingest", [("resnet20", True), ("resnet20", False),
                                           ("lenet5", True), ("resnet20", "pack"),
-                                          ("resnet20", "pack-inplace"), ("lenet5", "pack")])
+                                          ("resnet20", "pack-inplace"), ("lenet5", "pack"),
+                                          ("resnet20", "pack-noparse")])
 def test_gpu_engine_matches_oracle(broker, model, ingest):
     """Every output record is matched to ITS input by key (output_key=input) and compared on
     logits (centered log-softmax) with a bf16-level relative tolerance: a misrouted batch split
     (image i's row under record j) or a wrong image count cannot pass. ingest=True: CRC32C and
     image counts on the GPU and the parser reading the device-resident fetch buffer; False: the
     host decode path with per-batch H2D staging; "pack": GPU ingest of nibble-packed fetch
-    bodies (the source's PackTap, expanded on the device before the CRC / count / parse)."""
-    pack = ingest in ("pack", "pack-inplace")
+    bodies (the source's PackTap, expanded on the device before the CRC / count / parse).
+    With GPU ingest the records are parsed into the fetch's image arena by the ingest pass and
+    the batch step runs the forward alone ("pack-noparse": the step parses, as in round 5)."""
+    pack = ingest in ("pack", "pack-inplace", "pack-noparse")
     if pack and not C.text_pack_fast():
         pytest.skip("no AVX-512 VBMI on this host")
     net = get_model(model)
@@ -190,7 +193,8 @@ def test_gpu_engine_matches_oracle(broker, model, ingest):
                      bootstrap=f"127.0.0.1:{broker.port}", start_offset="earliest",
                      max_batch=32, max_wait_us=500, output_key="input",
                      gpu_ingest=bool(ingest), text_pack=pack,
-                     text_pack_bounce=ingest != "pack-inplace")
+                     text_pack_bounce=ingest != "pack-inplace",
+                     ingest_parse=ingest != "pack-noparse")
     eng = Engine(cfg, devices=[0], max_records=len(counts) + 1, params=params)
     eng.start()
     assert eng.wait(120), eng.stats()
@@ -212,11 +216,62 @@ def test_gpu_engine_matches_oracle(broker, model, ingest):
     st = eng.stats()
     assert st["errors"] == 1 and st["images_out"] == sum(counts)
     assert (st["ingested_records"] > 0) == bool(ingest)
+    # every good record's images came parsed from the ingest arena (the step ran the forward
+    # alone), unless the ingest parse is off or there is no GPU ingest
+    want = len(counts) if ingest and ingest != "pack-noparse" else 0
+    assert st["ingest_parsed_records"] == want and st["preparsed_records"] == want, st
     if pack:  # the text crossed the link packed (~0.5 bytes per fetched byte)
         assert 0 < st["ingest_link_bytes"] < 0.6 * st["ingest_text_bytes"], st
         # the bounce receive left sparse host copies (nothing needed the text on the host)
-        assert (st["sparse_fetches"] > 0) == (ingest == "pack"), st
+        assert (st["sparse_fetches"] > 0) == (ingest != "pack-inplace"), st
         assert st["restored_fetches"] == 0, st
+
+
+@pytest.mark.parametrize("ingest_parse", [True, False])
+def test_gpu_ingest_parse_verdicts(broker, ingest_parse):
+    """Records the ingest pass parses are judged there: a ragged array whose element count is
+    right (one pixel with 2 values, the next with 4) is bad_shape, a malformed number is
+    bad_number, a wrong element count is bad_shape - the same verdicts as the step's parse
+    (ingest_parse=False), and the good records' predictions are identical either way."""
+    rng = np.random.default_rng(3)
+    good = {f"g{i}".encode(): rng.random((1 + i % 2, 32, 32, 3), dtype=np.float32)
+            for i in range(6)}
+    for k, x in good.items():
+        broker.append("in", 0, [C.encode_instances(x)], [k])
+    x = rng.random((1, 32, 32, 3), dtype=np.float32).tolist()
+    x[0][0][1] = x[0][0][1] + [x[0][0][0].pop()]  # pixel (0, 0): 2 values, pixel (0, 1): 4
+    ragged = json.dumps({"instances": x}).encode()
+    badnum = C.encode_instances(rng.random((1, 32, 32, 3), dtype=np.float32))
+    i = badnum.index(b",", 2000)
+    badnum = badnum[:i] + b".5.5" + badnum[i:]  # "0.123.5.5": a number with two points
+    short = C.encode_instances(rng.random((1, 32, 32, 3), dtype=np.float32))
+    short = short[:short.rindex(b",")] + b"]]]]}"  # 3071 elements
+    broker.append("in", 0, [ragged, badnum, short], [b"ragged", b"badnum", b"short"])
+    n = len(good) + 3
+    eng, out = run_engine(broker, n, output_key="input", on_error="error-json",
+                          ingest_parse=ingest_parse)
+    by_key = {r["key"]: r["value"] for r in out}
+    assert len(out) == n
+    assert json.loads(by_key[b"ragged"])["error"] == "bad_shape"
+    # (a malformed number: its own token fails as a number, and the parser's structural check of
+    # the elements around it may speak first - either verdict rejects the record)
+    assert json.loads(by_key[b"badnum"])["error"] in ("bad_number", "bad_shape")
+    assert json.loads(by_key[b"short"])["error"] == "bad_shape"
+    for k, x in good.items():
+        p = np.array(json.loads(by_key[k])["predictions"])
+        assert p.shape == (len(x), 10) and np.allclose(p.sum(-1), 1.0, atol=1e-4)
+    st = eng.stats()
+    assert st["errors"] == 3
+    assert st["preparsed_records"] == (len(good) if ingest_parse else 0), st
+    # identical outputs - predictions and verdicts - with and without the ingest parse (same
+    # kernels, same rounding)
+    key = "_ingest_parse_preds"
+    prev = getattr(test_gpu_ingest_parse_verdicts, key, None)
+    cur = dict(by_key)
+    if prev is None:
+        setattr(test_gpu_ingest_parse_verdicts, key, cur)
+    else:
+        assert prev == cur
 
 
 def test_gpu_engine_float_format_java8(broker):

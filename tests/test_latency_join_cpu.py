@@ -52,3 +52,12 @@ def test_join_is_vectorised_at_scale():
     lat = append_to_ack_us(app, ack)
     assert len(lat) == len(rec_b)
     assert np.allclose(np.sort(lat), np.sort(d / 1e3))
+
+
+def test_stage_split_with_ready_time():
+    """A 7-column ack log (t_ready: handed to the batcher) splits queue into ingest + batching."""
+    app, ack = _logs()
+    ack = ack + (np.array([3200, 4500, 2800, 0]),)
+    st = latency_stages_us(app, ack)
+    assert np.allclose(st["ingest"] + st["batching"], st["queue"])
+    assert sorted(st["ingest"].tolist()) == [0.2, 0.3, 0.5]
