@@ -837,6 +837,18 @@ std::string normalize_records(const uint8_t* p, size_t len, int64_t min_offset, 
   // converted; a batch that fails with budget already spent is retried there with the whole
   // budget before it can become poison.
   size_t spent = 0;
+  // `out` already holds a record at or past min_offset: only then may the budget stop the
+  // conversion, since the consumer advances its position from decoded records alone - a stop
+  // before any of them (e.g. a compacted batch whose surviving records all lie below min_offset
+  // came first) would refetch the same prefix forever. Until then a batch gets the
+  // whole budget, and one that still fails becomes poison.
+  bool served = false;
+  auto any_at_or_past = [&](const std::vector<Rec>& v) {
+    for (const Rec& r : v)
+      if (r.offset >= min_offset) return true;
+    return false;
+  };
+  auto room = [&]() -> size_t { return served ? (limit > spent ? limit - spent : 0) : limit; };
   // offset after the previous entry of this response (a failed legacy wrapper's inner records
   // are the offsets from here to the wrapper's own, its last inner record's)
   int64_t prev_end = min_offset;
@@ -844,6 +856,7 @@ std::string normalize_records(const uint8_t* p, size_t len, int64_t min_offset, 
     std::vector<Rec> keep;
     for (const Rec& r : legacy_run)
       if (r.offset >= min_offset) keep.push_back(r);
+    served |= !keep.empty();
     append_v2(out, keep, 0);
     legacy_run.clear();
     hold.clear();
@@ -873,7 +886,8 @@ std::string normalize_records(const uint8_t* p, size_t len, int64_t min_offset, 
           continue;
         }
         const bool control = (bi.attributes & 0x20) != 0;
-        if (compressed && !control && spent >= limit) break;  // (budget spent: next fetch)
+        // (budget spent: the next fetch resumes here)
+        if (compressed && !control && spent >= limit && served) break;
         if (!compressed || control) {
           // verify the records parse, then copy the batch through verbatim
           std::vector<Rec> probe;
@@ -882,12 +896,14 @@ std::string normalize_records(const uint8_t* p, size_t len, int64_t min_offset, 
                              bi.records, base, bi.base_timestamp, bi.max_timestamp,
                              (bi.attributes & kAttrLogAppendTime) != 0, probe);
           out.append(reinterpret_cast<const char*>(p + pos), (size_t)bi.length);
+          served |= any_at_or_past(probe);
         } else {
           std::string plain;
           std::string err;
           if (!decompress(bi.attributes & 7, p + pos + kBatchHeaderBytes,
-                          (size_t)bi.length - kBatchHeaderBytes, plain, limit - spent, &err)) {
-            if (spent > 0) break;  // (maybe only the remaining budget: retried next fetch)
+                          (size_t)bi.length - kBatchHeaderBytes, plain, room(), &err)) {
+            // (maybe only the remaining budget: retried next fetch with all of it)
+            if (spent > 0 && served) break;
             throw ProtocolError(err.empty() ? "corrupt compressed batch" : err);
           }
           spent += plain.size();
@@ -895,6 +911,7 @@ std::string normalize_records(const uint8_t* p, size_t len, int64_t min_offset, 
           parse_v2_records(reinterpret_cast<const uint8_t*>(plain.data()), plain.size(),
                            bi.records, base, bi.base_timestamp, bi.max_timestamp,
                            (bi.attributes & kAttrLogAppendTime) != 0, probe);
+          served |= any_at_or_past(probe);
           // header verbatim (attributes without the codec), decompressed records, new length/CRC
           std::string b(reinterpret_cast<const char*>(p + pos), (size_t)kBatchHeaderBytes);
           b += plain;
@@ -914,21 +931,32 @@ std::string normalize_records(const uint8_t* p, size_t len, int64_t min_offset, 
                         e.what());
         else
           append_poison(out, base, base, 1, min_offset, st, e.what());
+        served |= base + (have_hdr ? bi.last_offset_delta : 0) >= min_offset;
       }
       prev_end = base + (have_hdr ? bi.last_offset_delta : 0) + 1;
     } else if (magic == 0 || magic == 1) {
       const int attrs = (int8_t)p[pos + 17];
-      if ((attrs & 7) != 0 && spent >= limit) break;  // (budget spent: next fetch)
+      if (base < min_offset) {
+        // a legacy entry's offset is its last (inner) record's: all of it lies below the
+        // position, so it is skipped before any decompression
+        if (!legacy_run.empty()) flush_legacy();
+        prev_end = base + 1;
+        pos += entry;
+        continue;
+      }
+      if ((attrs & 7) != 0 && spent >= limit && served) break;  // (budget spent: next fetch)
       const size_t held = hold.size();
       try {
         std::vector<Rec> recs;
         size_t used = 0;
-        legacy_records(p + pos, len - pos, true, limit - spent, hold, recs, &used);
+        legacy_records(p + pos, len - pos, true, room(), hold, recs, &used);
         for (size_t h = held; h < hold.size(); ++h) spent += hold[h].size();
         legacy_run.insert(legacy_run.end(), recs.begin(), recs.end());
+        served |= any_at_or_past(recs);
         ++st.converted_batches;
       } catch (const ProtocolError& e) {
-        if (spent > 0 && (attrs & 7) != 0) break;  // (maybe only the remaining budget)
+        // (maybe only the remaining budget)
+        if (spent > 0 && (attrs & 7) != 0 && served) break;
         if (!legacy_run.empty()) flush_legacy();
         // the wrapper's offset is its LAST inner record's; the inner count is unreadable, so
         // every offset from the previous entry's end up to it becomes one poison record (for
@@ -942,6 +970,7 @@ std::string normalize_records(const uint8_t* p, size_t len, int64_t min_offset, 
         } else {
           append_poison(out, base, base, 1, min_offset, st, e.what());
         }
+        served = true;  // (base >= min_offset here)
       }
       prev_end = base + 1;
     } else {
@@ -959,6 +988,7 @@ std::string normalize_records(const uint8_t* p, size_t len, int64_t min_offset, 
       append_poison(out, first, last, (int32_t)std::min<int64_t>(last - first + 1, 1 << 20),
                     min_offset, st,
                     "unsupported message format (magic " + std::to_string(magic) + ")");
+      served = true;
       prev_end = last + 1;
     }
     pos += entry;

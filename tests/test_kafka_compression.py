@@ -405,3 +405,22 @@ def test_engine_sink_compression(broker):
         if len(got) >= 6:
             break
     assert cons.format_stats()["converted_batches"] >= 1  # it was compressed on the wire
+
+
+def test_budget_never_stops_before_a_record_past_the_position():
+    """the decompression budget may stop a fetch's conversion only once the output
+    holds a record at or past the fetch position - the consumer advances from decoded records
+    alone, so a stop before any would refetch the same prefix forever. Here the first entry (a
+    gzip legacy wrapper, offsets 10-13) lies wholly below the position 14 and is skipped before
+    decompression, so the next wrapper gets the budget and the fetch makes progress."""
+    vals = [b"7" * 2000] * 4
+    below = K.encode_message_set(1, vals, 10, "gzip")   # offsets 10-13
+    past = K.encode_message_set(1, vals, 14, "gzip")    # offsets 14-17
+    blob, st = K.normalize_records(below + past, 14, True, limit=9000)
+    assert [r["offset"] for r in K.decode_records(blob, 0, True)] == [14, 15, 16, 17]
+    assert st["poison_batches"] == 0
+    # v2: a first batch whose records all lie below the position still lets the next one through
+    z0 = K.compress_batch(K.encode_batch([(None, b"1" * 2000, 0, None)] * 4, 0, 0), "gzip")
+    z1 = K.compress_batch(K.encode_batch([(None, b"2" * 2000, 0, None)] * 4, 4, 0), "gzip")
+    blob, st = K.normalize_records(z0 + z1, 4, True, limit=9000)
+    assert [r["offset"] for r in K.decode_records(blob, 0, True)] == [4, 5, 6, 7]
