@@ -51,7 +51,12 @@ struct GemmConvArgs {
   int n_tiles, nwg;
   // DUAL (conv2d_gemm_proj): k-steps [nkb1, nkb) read a second 1x1 source - the bottleneck's
   // projection shortcut, x2 [B][H2][W2][Cin2] sampled at stride2, weights w2 [Npad][Kpad2] - so
-  // conv3 + projection is one GEMM over the concatenated K, with bias + bias2
+  // conv3 + projection is one GEMM over the concatenated K, with bias + bias2. Rounding: the
+  // projection term stays fp32 inside the accumulator (one bf16 rounding of the sum), while the
+  // layered plan (GALE_FUSE_PROJ=0) and bottleneck56's block 0 store the projection as bf16
+  // first: the two forms differ by up to one bf16 ulp of the shortcut before the final rounding
+  // (tests/test_models_gpu.py pins the fused plan against the fp32 oracle and the
+  // layered one). Rounding it here too would need a second accumulator set per tile.
   const bf16* x2;
   const bf16* w2;
   const float* bias2;
@@ -418,6 +423,17 @@ hipError_t conv2d_gemm(const ConvDesc& d, int batch, const void* x, const void* 
   return hipGetLastError();
 }
 
+// images per launch of the fused projection: every element offset of the launch's x, x2 and y
+// (and its pixel count) must stay below 2^31 (max_batch >= ~2675 overflowed the
+// stage-2 projection's input)
+static int proj_chunk_images(const ConvDesc& d, int H2, int W2, int Cin2) {
+  const long long lim = (1ll << 31) - 1;
+  long long per = (long long)d.Ho * d.Wo * std::max(d.Cout, 1);
+  per = std::max(per, (long long)d.H * d.W * d.Cin);
+  per = std::max(per, (long long)H2 * W2 * Cin2);
+  return per > 0 ? (int)std::min<long long>(lim / per, 1 << 20) : 0;
+}
+
 bool conv_gemm_proj_supported(const ConvDesc& d, int batch, int H2, int W2, int Cin2,
                               int stride2, int Kpad2) {
   // (no conv_path switch: like the fused block kernels this op has no other implementation)
@@ -427,9 +443,8 @@ bool conv_gemm_proj_supported(const ConvDesc& d, int batch, int H2, int W2, int 
   if (Cin2 % 64 != 0 || Kpad2 != Cin2 || stride2 < 1) return false;
   if ((H2 - 1) / stride2 + 1 != d.Ho || (W2 - 1) / stride2 + 1 != d.Wo) return false;
   if (d.Npad % 128 != 0 || d.Npad < d.Cout || d.Cout % 8 != 0) return false;
-  return (long long)batch * d.Ho * d.Wo < (1ll << 31) &&
-         (long long)batch * d.H * d.W * d.Cin < (1ll << 31) &&
-         (long long)batch * H2 * W2 * Cin2 < (1ll << 31);
+  // (any batch: conv2d_gemm_proj launches chunks whose 32-bit element offsets hold)
+  return batch >= 0 && proj_chunk_images(d, H2, W2, Cin2) > 0;
 }
 
 hipError_t conv2d_gemm_proj(const ConvDesc& d, int batch, const void* x, const void* w,
@@ -438,6 +453,18 @@ hipError_t conv2d_gemm_proj(const ConvDesc& d, int batch, const void* x, const v
                             hipStream_t stream) {
   if (!conv_gemm_proj_supported(d, batch, H2, W2, Cin2, stride2, Kpad2))
     return hipErrorInvalidValue;
+  const int chunk = proj_chunk_images(d, H2, W2, Cin2);
+  if (batch > chunk) {  // chunks of images, each with 32-bit offsets (bf16 in and out)
+    for (int c0 = 0; c0 < batch; c0 += chunk) {
+      const int nb = std::min(chunk, batch - c0);
+      const hipError_t e = conv2d_gemm_proj(
+          d, nb, static_cast<const bf16*>(x) + (size_t)c0 * d.H * d.W * d.Cin, w, bias,
+          static_cast<const bf16*>(x2) + (size_t)c0 * H2 * W2 * Cin2, H2, W2, Cin2, stride2,
+          Kpad2, w2, bias2, static_cast<bf16*>(y) + (size_t)c0 * d.Ho * d.Wo * d.Cout, stream);
+      if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+  }
   GemmConvArgs a;
   a.x = static_cast<const bf16*>(x);
   a.w = static_cast<const bf16*>(w);
