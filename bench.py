@@ -661,8 +661,10 @@ def size_pipeline(a, cpus: float) -> None:
     if a.decode_threads <= 0:
         # 6 GPU-ingest workers keep more H2D copies in flight on the host link than 4 (higher
         # throughput in 5 of 6 interleaved pairs on two boxes, p50 unchanged; see
-        # profiles/archive/r3_decode_threads_ab.txt)
-        a.decode_threads = 6 if big else 2
+        # profiles/archive/r3_decode_threads_ab.txt). With the parse at ingest (round 6) each
+        # fetch holds its lane ~30 us longer: 10 lanes keep the ingest stage's p99 at 0.28-0.34 ms
+        # against 0.42-0.92 ms with 6 (profiles/r6_ab_ingest_parse.jsonl); a lane mostly sleeps
+        a.decode_threads = (10 if a.ingest_parse else 6) if big else 2
 
 
 def print_config(a) -> int:

@@ -117,6 +117,10 @@ class Executor {
   // buffer - images the GPU ingest already parsed (whole-network plans: device_batch_ok())
   void launch_device_batch(int slot, const int* d_batch, hipStream_t stream,
                            const StepOut* so = nullptr, const float* const* xs = nullptr);
+  // The forward of `batch` images taken from an input table in the kernel arguments (images the
+  // GPU ingest parsed): no metadata in device memory, one launch (step_out_ok() plans)
+  void launch_table(int slot, int batch, const InputTable& tab, hipStream_t stream,
+                    const StepOut* so = nullptr);
 
  private:
   void launch_all(int batch, void* const* bufs, hipStream_t stream,
@@ -125,7 +129,7 @@ class Executor {
   // ops [begin, end) for images [c0, c0 + batch) of the buffers (c0 > 0: a chunk)
   void launch_ops(size_t begin, size_t end, int batch, void* const* bufs, hipStream_t stream,
                   int c0 = 0, const int* d_batch = nullptr, const StepOut* so = nullptr,
-                  const float* const* xs = nullptr);
+                  const float* const* xs = nullptr, const InputTable* tab = nullptr);
   int device_;
   PlanSpec spec_;
   std::vector<int> buckets_;

@@ -140,6 +140,16 @@ hipError_t head_pool_dense_softmax(int batch, int HW, int C, int N, const void* 
 // in text, and, by workgroup 0 before anything else, the batch's parse verdicts handed over:
 // status_out[i] = status[i], status[i] = 0 for i < *nrec (status: the parse's device array;
 // text and status_out: host-mapped). The replica's step is then parse -> forward, two nodes.
+// The inputs of a batch whose images the GPU ingest already parsed into fetch arenas, passed BY
+// VALUE in the forward's kernel arguments, so a batch step needs no metadata copy at all: image
+// i is at base[code[i] >> 24] + (code[i] & 0xffffff) * (H * W * C) floats. base[0] == null:
+// no table (the forward reads x or xs).
+constexpr int kInputTableImages = 512, kInputTableBases = 16;
+struct InputTable {
+  const float* base[kInputTableBases];
+  uint32_t code[kInputTableImages];
+};
+
 struct StepOut {
   void* text = nullptr;
   int* status = nullptr;
@@ -168,7 +178,7 @@ struct ResNet20Params {
   const float* const* xs;
 };
 hipError_t resnet20_fused_forward(const ResNet20Params& p, int batch, const float* x, float* out,
-                                  hipStream_t stream);
+                                  hipStream_t stream, const InputTable* tab = nullptr);
 
 // Whole-network MNIST LeNet-5 (csrc/kernels/lenet5_fused.hip): x fp32 [B,28,28,1] -> softmax
 // fp32 [B,10], one image per 256-thread workgroup (grid = batch) with every activation in LDS. Weights are the serving
@@ -190,7 +200,7 @@ struct LeNet5Params {
   const float* const* xs;  // as ResNet20Params::xs ([28][28][1] images)
 };
 hipError_t lenet5_fused_forward(const LeNet5Params& p, int batch, const float* x, float* out,
-                                hipStream_t stream);
+                                hipStream_t stream, const InputTable* tab = nullptr);
 
 // Row softmax, fp32 [B, ld] -> fp32 [B, N] (first N columns of each row).
 hipError_t softmax_rows(int batch, int N, int ld, const float* x, float* out, hipStream_t stream);

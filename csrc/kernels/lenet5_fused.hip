@@ -44,7 +44,8 @@ __device__ __forceinline__ float dot_bf16(const float* a, const bf16* row, int k
 
 __global__ __launch_bounds__(kT) void lenet5_fused_kernel(LeNet5Params p, int n,
                                                           const float* __restrict__ x,
-                                                          float* __restrict__ out) {
+                                                          float* __restrict__ out,
+                                                          InputTable tab) {
   __shared__ float s_img[kImg];
   __shared__ float s_a1[kA1];
   __shared__ float s_a2[kA2];
@@ -66,7 +67,10 @@ __global__ __launch_bounds__(kT) void lenet5_fused_kernel(LeNet5Params p, int n,
     s_w2[i] = (float)w2[c * 224 + (r / 6) * 8 + r % 6];
   }
   if (t < 16) s_b2[t] = p.b2[t];
-  const float* xi = p.xs ? p.xs[img] : x + (size_t)img * 784;
+  const float* xi =
+      tab.base[0] ? tab.base[tab.code[img] >> 24] + (size_t)(tab.code[img] & 0xffffffu) * 784
+      : p.xs      ? p.xs[img]
+                  : x + (size_t)img * 784;
   for (int i = t; i < kImg; i += kT) {
     const int y = i / kPad - 2, xx = i % kPad - 2;
     s_img[i] = (y >= 0 && y < 28 && xx >= 0 && xx < 28) ? xi[y * 28 + xx] : 0.f;
@@ -169,12 +173,14 @@ __global__ __launch_bounds__(kT) void lenet5_fused_kernel(LeNet5Params p, int n,
 }  // namespace
 
 hipError_t lenet5_fused_forward(const LeNet5Params& p, int batch, const float* x, float* out,
-                                hipStream_t stream) {
+                                hipStream_t stream, const InputTable* tab) {
   if (batch <= 0) return hipSuccess;
   if (!p.w1 || !p.b1 || !p.w2 || !p.b2 || !p.w3 || !p.b3 || !p.w4 || !p.b4 || !p.w5 || !p.b5)
     return hipErrorInvalidValue;
+  static const InputTable kNoTable{};
+  if (tab && (batch > kInputTableImages || !tab->base[0])) return hipErrorInvalidValue;
   hipLaunchKernelGGL(lenet5_fused_kernel, dim3((unsigned)batch), dim3(kT), 0, stream, p, batch,
-                     x, out);
+                     x, out, tab ? *tab : kNoTable);
   return hipGetLastError();
 }
 

@@ -449,7 +449,8 @@ __device__ __forceinline__ void stem(const void* wgv, const float* __restrict__ 
 template <bool F8, int NW>
 __global__ __launch_bounds__(64 * NW, 8 / NW) void resnet20_fused_kernel(ResNet20Params p,
                                                                          const float* x,
-                                                                         float* out, int batch) {
+                                                                         float* out, int batch,
+                                                                         InputTable tab) {
   typedef Ty<F8> T;
   typedef typename T::elem elem;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -490,8 +491,11 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void resnet20_fused_kernel(ResNet2
       if (h == 0 || h == 33 || w == 0 || w == 33) IN[i] = T::zero();
     }
     zero_border<F8, NW, 34, 34, 16, L1>(X1);
-    const float4* xi =
-        reinterpret_cast<const float4*>(p.xs ? p.xs[img] : x + (size_t)img * 3072);
+    const float* src =
+        tab.base[0] ? tab.base[tab.code[img] >> 24] + (size_t)(tab.code[img] & 0xffffffu) * 3072
+        : p.xs      ? p.xs[img]
+                    : x + (size_t)img * 3072;
+    const float4* xi = reinterpret_cast<const float4*>(src);
     for (int i = threadIdx.x; i < 768; i += 64 * NW) {
       const float4 v = xi[i];
       const float e[4] = {v.x, v.y, v.z, v.w};
@@ -602,8 +606,11 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void resnet20_fused_kernel(ResNet2
 }  // namespace
 
 hipError_t resnet20_fused_forward(const ResNet20Params& p, int batch, const float* x, float* out,
-                                  hipStream_t stream) {
+                                  hipStream_t stream, const InputTable* tab) {
   if (batch <= 0) return hipSuccess;
+  static const InputTable kNoTable{};
+  if (tab && (batch > kInputTableImages || !tab->base[0])) return hipErrorInvalidValue;
+  const InputTable& t = tab ? *tab : kNoTable;
   const bool f8 = p.fp8 != 0;
   if (f8) {
     for (int i = 0; i < 19; ++i)
@@ -631,13 +638,13 @@ hipError_t resnet20_fused_forward(const ResNet20Params& p, int batch, const floa
   const dim3 block(64 * nw);
   if (f8) {
     hipLaunchKernelGGL((resnet20_fused_kernel<true, 4>), dim3(grid), block, lds, stream, p, x,
-                       out, batch);
+                       out, batch, t);
   } else if (nw == 8) {
     hipLaunchKernelGGL((resnet20_fused_kernel<false, 8>), dim3(grid), block, lds, stream, p, x,
-                       out, batch);
+                       out, batch, t);
   } else {
     hipLaunchKernelGGL((resnet20_fused_kernel<false, 4>), dim3(grid), block, lds, stream, p, x,
-                       out, batch);
+                       out, batch, t);
   }
   return hipGetLastError();
 }

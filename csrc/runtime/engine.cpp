@@ -973,6 +973,7 @@ bool Engine::ingest_fetch(FetchItem& it, std::vector<InRecord>& good, int lane) 
     r.dev_locality = slot_key_[(size_t)it.slot];
     if (io.cnt_off[i] >= 0) r.dev_counts = dev + io.cnt_off[i];
     r.dev_image = io.img[i];
+    r.dev_arena = r.dev_image ? arena : nullptr;
     if (r.dev_image) ++ingest_parsed_;
     ++records_in_;
     if (r.len >= 0) bytes_in_ += r.len;
@@ -1807,12 +1808,14 @@ std::map<std::string, double> Engine::stats() const {
   s["ingested_records"] = (double)ingested_records_;
   s["ingest_parsed_records"] = (double)ingest_parsed_;
   {
-    int64_t step = 0, fwd = 0, pre = 0;
+    int64_t step = 0, fwd = 0, pre = 0, tab = 0;
     for (auto& r : replicas_) {
       step += r->rep->graph_step_batches();
       fwd += r->rep->graph_forward_batches();
       pre += r->rep->preparsed_records();
+      tab += r->rep->table_batches();
     }
+    s["table_batches"] = (double)tab;  // steps = one forward launch, inputs in kernel arguments
     s["graph_step_batches"] = (double)step;
     s["graph_forward_batches"] = (double)fwd;
     s["preparsed_records"] = (double)pre;  // records the step took parsed from the ingest arena

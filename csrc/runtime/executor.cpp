@@ -100,9 +100,18 @@ void Executor::launch_device_batch(int slot, const int* d_batch, hipStream_t str
   launch_all(spec_.max_batch, bufs_[slot].data(), stream, d_batch, so, xs);
 }
 
+void Executor::launch_table(int slot, int batch, const InputTable& tab, hipStream_t stream,
+                            const StepOut* so) {
+  if (!step_out_ok()) throw std::logic_error("plan cannot read an input table");
+  if (slot < 0 || slot >= spec_.slots) throw std::invalid_argument("bad slot");
+  if (batch <= 0 || batch > spec_.max_batch || batch > kInputTableImages)
+    throw std::invalid_argument("bad table batch");
+  launch_ops(0, 1, batch, bufs_[slot].data(), stream, 0, nullptr, so, nullptr, &tab);
+}
+
 void Executor::launch_ops(size_t begin, size_t end, int batch, void* const* bufs,
                           hipStream_t stream, int c0, const int* d_batch, const StepOut* so,
-                          const float* const* xs) {
+                          const float* const* xs, const InputTable* tab) {
   auto at = [&](int id, long long bpi) -> void* {
     return static_cast<char*>(bufs[id]) + (size_t)c0 * (size_t)bpi;
   };
@@ -164,7 +173,7 @@ void Executor::launch_ops(size_t begin, size_t end, int batch, void* const* bufs
             rp.s_res[i] = op.scales[38 + i];
           }
         e = resnet20_fused_forward(rp, batch, static_cast<const float*>(in),
-                                   static_cast<float*>(out), stream);
+                                   static_cast<float*>(out), stream, tab);
         break;
       }
       case OP_LENET5: {
@@ -184,7 +193,7 @@ void Executor::launch_ops(size_t begin, size_t end, int batch, void* const* bufs
         lp.xs = xs;
         if (so) lp.so = *so;
         e = lenet5_fused_forward(lp, batch, static_cast<const float*>(in),
-                                 static_cast<float*>(out), stream);
+                                 static_cast<float*>(out), stream, tab);
         break;
       }
       case OP_BOTTLENECK: {

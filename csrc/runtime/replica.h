@@ -52,6 +52,7 @@ struct InRecord {
   // its images, already parsed by the ingest pass: fp32 [H][W][C] each, contiguous, in the
   // fetch's device image arena (null: the replica parses the text)
   const float* dev_image = nullptr;
+  const float* dev_arena = nullptr;  // the arena dev_image lies in (its fetch's)
   // fragment `split_index` of an oversized record (null for ordinary records)
   std::shared_ptr<SplitRecord> split;
   int32_t split_index = -1;
@@ -95,6 +96,8 @@ class Replica {
   virtual int64_t graph_forward_batches() const { return 0; }
   // records whose images the GPU ingest had parsed (the step ran only the forward for them)
   virtual int64_t preparsed_records() const { return 0; }
+  // batches whose step was the forward alone with its inputs in the kernel arguments
+  virtual int64_t table_batches() const { return 0; }
 };
 
 // CPU stub (SURVEY.md §4 "stub replica for plumbing tests on GPU-less hosts"): parses on the
@@ -158,6 +161,7 @@ class GpuReplica : public Replica {
   int64_t graph_step_batches() const override { return step_batches_; }
   int64_t graph_forward_batches() const override { return fwd_graph_batches_; }
   int64_t preparsed_records() const override { return preparsed_; }
+  int64_t table_batches() const override { return table_batches_; }
   bool step_graph() const { return step_graph_; }
 
  private:
@@ -198,6 +202,8 @@ class GpuReplica : public Replica {
   hipGraphExec_t step_for(Slot& s, int slot, bool count_pass);
   hipError_t enqueue_step(Slot& s, int slot, bool count_pass, hipStream_t st, bool parse = true,
                           bool xs = false);
+  template <typename Pre>
+  bool try_table_step(Batch& b, Slot& s, int slot, const Pre& preparsed);
   size_t meta_rec_bytes() const;  // records + input pointer table of the metadata allocation
   static void* mapped_alloc(size_t bytes, const char* what);
   std::shared_ptr<Executor> exec_;
@@ -223,6 +229,7 @@ class GpuReplica : public Replica {
   // whole-network plan with the epilogue outputs); records without parse as before
   bool ptr_input_ = false;
   std::atomic<int64_t> preparsed_{0};
+  std::atomic<int64_t> table_batches_{0};  // batches launched with a kernel-argument input table
   int64_t expect_ns_ = 0;  // running average of submit -> done (adaptive sleep-poll)
 };
 

@@ -220,6 +220,8 @@ def test_gpu_engine_matches_oracle(broker, model, ingest):
     # alone), unless the ingest parse is off or there is no GPU ingest
     want = len(counts) if ingest and ingest != "pack-noparse" else 0
     assert st["ingest_parsed_records"] == want and st["preparsed_records"] == want, st
+    # such batches are one forward launch, their inputs in the kernel arguments
+    assert (st["table_batches"] > 0) == (want > 0), st
     if pack:  # the text crossed the link packed (~0.5 bytes per fetched byte)
         assert 0 < st["ingest_link_bytes"] < 0.6 * st["ingest_text_bytes"], st
         # the bounce receive left sparse host copies (nothing needed the text on the host)
