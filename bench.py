@@ -210,6 +210,9 @@ def parse_args(argv=None):
                          "wake-up per this many KB of a fetch response; 0 = per segment, -1 = "
                          "the bounce window with the bounce receive (profiles/"
                          "r4_ab_recv_lowat.jsonl)")
+    ap.add_argument("--partition-max-kb", type=int, default=8192,
+                    help="consumer max.partition.fetch.bytes (KB): the most one partition's fetch "
+                         "response carries - the records at its head wait for the whole of it")
     ap.add_argument("--fetch-max-wait-ms", type=int, default=20,
                     help="consumer fetch.max.wait.ms (long-poll bound when no data is there)")
     ap.add_argument("--latency-sweep", default="",
@@ -825,7 +828,8 @@ def main(argv=None) -> int:
                      decode_threads=a.decode_threads, slo_p99_ms=a.slo_p99_ms,
                      gpu_wait_poll_us=a.gpu_wait_poll_us, gpu_ingest=a.gpu_ingest, gpu_encode=a.gpu_encode,
                      replica_priority=a.replica_priority, step_launch=a.step_launch,
-                     text_pack=a.text_pack, text_pack_bounce=a.text_pack_bounce, ingest_parse=a.ingest_parse,
+                     text_pack=a.text_pack, text_pack_bounce=a.text_pack_bounce,
+                     ingest_parse=a.ingest_parse, partition_max_kb=a.partition_max_kb,
                      text_pack_window_kb=a.text_pack_window_kb,
                      pinned_fetch_mb=a.pinned_fetch_mb,
                      stub=a.stub, stub_null=a.stub_null, commit_interval_ms=500,
