@@ -71,7 +71,8 @@ def parse_args(argv=None):
     ap.add_argument("--min-warmup-s", type=float, default=2.0)
     ap.add_argument("--max-warmup-s", type=float, default=20.0)
     ap.add_argument("--model", default="resnet20", choices=["lenet5", "resnet20", "resnet50"])
-    ap.add_argument("--batch", type=int, default=256, help="images per micro-batch (max_batch)")
+    ap.add_argument("--batch", type=int, default=0,
+                    help="images per micro-batch (max_batch; default 256, 128 for resnet50)")
     ap.add_argument("--images-per-record", type=int, default=1)
     ap.add_argument("--distinct", type=int, default=0,
                     help="distinct synthetic images (default 65536; 256 = 435 MB for resnet50)")
@@ -638,6 +639,13 @@ def size_pipeline(a, cpus: float) -> None:
         a.step_images = 4096 if r50 else (1048576 if a.model == "lenet5" else 262144)
     if a.distinct <= 0:
         a.distinct = 256 if r50 else 65536
+    if a.batch <= 0:
+        # ResNet-50 (BASELINE config 4: dynamic batch <= 256): a 128-image cap halves the
+        # latency at the same throughput - the host binds the rate, and a 256-image batch spends
+        # ~4 ms filling and ~5.5 ms on the device (profiles/r6_ab_r50_batch.jsonl: 45.2 / 44.7 k
+        # img/s, p50 12.3 ms at 256; 46.2 / 42.0 k, p50 6.2 / 6.5 ms at 128; 42.3 / 41.8 k,
+        # p50 3.8 ms at 64)
+        a.batch = 128 if r50 else 256
     if a.max_wait_us < 0:
         a.max_wait_us = 20000 if r50 else 2000
     big = cpus >= 16
