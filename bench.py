@@ -204,6 +204,9 @@ def parse_args(argv=None):
                          "(BASELINE's latency half); 0 = skip (p50 is then fetch -> ack under "
                          "the backlog, i.e. mostly queueing)")
     ap.add_argument("--latency-warmup-s", type=float, default=1.0)
+    ap.add_argument("--latency-batch-records", type=int, default=0,
+                    help="records per producer batch in the latency phase (0 = the backlog's "
+                         "batches, 64 records)")
     ap.add_argument("--fetch-min-bytes", type=int, default=1,
                     help="consumer fetch.min.bytes (Kafka default 1)")
     ap.add_argument("--recv-lowat-kb", type=int, default=-1,
@@ -797,6 +800,14 @@ def main(argv=None) -> int:
     imgs = synthetic_images(distinct, net.input_shape, seed=1234 + rank)
     enc_threads = a.encode_threads or max(1, int(host_cpus_per_rank()))
     bset = K.synthetic_batches(imgs, ipr, rpb, enc_threads)
+    # the latency phase's producer batches (--latency-batch-records; 0 = the same batches as the
+    # backlog): smaller batches make arrivals less bursty, as a kafka-clients producer with its
+    # 16 KB batch.size sends one ~35 KB record per batch
+    lat_bset = bset
+    lrpb = min(a.latency_batch_records, rpb) if a.latency_batch_records > 0 else rpb
+    if lrpb != rpb:
+        lat_bset = K.synthetic_batches(imgs[:max(lrpb * ipr, len(imgs) // 4)], ipr, lrpb,
+                                       enc_threads)
     del imgs
     t_enc = time.perf_counter() - t_enc
 
@@ -941,7 +952,7 @@ def main(argv=None) -> int:
     def measure(load_img_s):
         if world > 1:
             dist.barrier()
-        lu, ach, unm, hst = latency_phase(eng, broker, feeder, bset, my_parts,
+        lu, ach, unm, hst = latency_phase(eng, broker, feeder, lat_bset, my_parts,
                                           load_img_s / world, a, ipr)
         if world > 1:
             # every rank's samples (subsampled to <= 200k) and achieved rate to rank 0
