@@ -487,8 +487,10 @@ def latency_phase(eng, broker, feeder, bset, parts, rate_img_s, a, ipr):
     broker.take_probes()  # (reset)
     eng.set_ack_log(True)
     c0, t0, cg0, tcp0 = eng.completed, time.perf_counter(), _cgroup_cpu_stat(), _tcp_counters()
+    st0 = eng.stats()
     time.sleep(a.latency_s)
     eng.set_ack_log(False)
+    st1 = eng.stats()
     dt = time.perf_counter() - t0
     probes = broker.take_probes()
     achieved = (eng.completed - c0) * ipr / dt
@@ -501,6 +503,17 @@ def latency_phase(eng, broker, feeder, bset, parts, rate_img_s, a, ipr):
                 "latency_cg_throttled_periods": int(d.get("nr_throttled", 0)),
                 "latency_cg_periods": int(d.get("nr_periods", 0))}
     host["latency_broker_probes"] = probes
+    # the GPU ingest's turn per fetch in this window (us): waiting for a lane, host work before
+    # the device, the device wait, host work after, and the lane's whole turn
+    nf = st1.get("ingest_fetches", 0) - st0.get("ingest_fetches", 0)
+    if nf > 0:
+        d = {k: (st1.get(k, 0.0) - st0.get(k, 0.0)) / nf * 1e6 for k in (
+            "ingest_lane_wait_s", "ingest_prep_s", "ingest_device_wait_s", "ingest_post_s")}
+        d["lane_turn"] = (st1["thread_s_ingest"] - st0["thread_s_ingest"]) / nf * 1e6
+        host["latency_ingest_us_per_fetch"] = {k.replace("ingest_", "").replace("_s", ""):
+                                               round(v, 1) for k, v in d.items()}
+        host["latency_ingest_us_per_fetch"]["records"] = round(
+            (st1["ingested_records"] - st0["ingested_records"]) / nf, 1)
     tcp1 = _tcp_counters()
     host["latency_tcp"] = {k: tcp1[k] - tcp0.get(k, 0) for k in tcp1 if tcp1[k] != tcp0.get(k, 0)}
     rf.stop()

@@ -348,6 +348,10 @@ void Engine::start() {
   for (int i = 0; i < cfg_.decode_threads; ++i)
     decoders_.emplace_back([this, i] {
       name_thread("gl-dec", i);
+      // 1 us timer slack: the GPU ingest sleep-polls its fetch's completion every 20 us, and
+      // the default 50 us slack stretched each sleep to ~70 us (the ingest stage is the largest
+      // device-side part of a record's latency)
+      prctl(PR_SET_TIMERSLACK, 1000UL, 0, 0, 0);
       decode_loop(i);
     });
   for (auto& rs : replicas_)
@@ -914,6 +918,7 @@ bool Engine::ingest_fetch(FetchItem& it, std::vector<InRecord>& good, int lane) 
   uint8_t* dev = pools_[(size_t)it.slot]->mirror(f.buf.get());
   if (!dev) return false;
   const int64_t t0 = mono_ns();
+  ns_lane_wait_ += t0 - it.t_fetch_ns;  // (fetch received -> an ingest lane took it)
   const size_t n = f.records.size();
   IngestIO io;
   io.status.assign(n, codec::OK);
@@ -1832,6 +1837,30 @@ std::map<std::string, double> Engine::stats() const {
     s["ingest_link_bytes"] = (double)link;
   }
   s["thread_s_ingest"] = ingest_ns_ * 1e-9;
+  {
+    Ingest::Timing t;
+    for (auto& kv : ingests_) {
+      const Ingest::Timing q = kv.second->timing();
+      t.runs += q.runs;
+      t.prep_ns += q.prep_ns;
+      t.wait_ns += q.wait_ns;
+      t.post_ns += q.post_ns;
+    }
+    // per fetch, microseconds: waiting for a lane, the lane's host work before / after the
+    // device, and the device wait itself
+    const double n = (double)std::max<int64_t>(1, t.runs);
+    s["ingest_fetches"] = (double)t.runs;
+    s["ingest_lane_wait_us"] = (double)ns_lane_wait_ / n / 1e3;
+    s["ingest_prep_us"] = (double)t.prep_ns / n / 1e3;
+    s["ingest_device_wait_us"] = (double)t.wait_ns / n / 1e3;
+    s["ingest_post_us"] = (double)t.post_ns / n / 1e3;
+    s["ingest_lane_us"] = (double)ingest_ns_ / n / 1e3;  // a lane's whole turn, scan to push
+    // the same as running totals (s), for per-window deltas
+    s["ingest_lane_wait_s"] = (double)ns_lane_wait_ * 1e-9;
+    s["ingest_prep_s"] = (double)t.prep_ns * 1e-9;
+    s["ingest_device_wait_s"] = (double)t.wait_ns * 1e-9;
+    s["ingest_post_s"] = (double)t.post_ns * 1e-9;
+  }
   s["eff_max_batch"] = (double)eff_batch_;
   s["eff_max_wait_us"] = (double)eff_wait_ns_ / 1000.0;
   s["slo_adjustments"] = (double)slo_adjustments_;

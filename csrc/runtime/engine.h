@@ -418,6 +418,7 @@ class Engine {
   std::atomic<int64_t> ns_poll_{0}, ns_decode_{0}, ns_take_{0}, ns_submit_{0}, ns_wait_{0},
       ns_finish_{0};
   std::atomic<int64_t> ns_handoff_{0};  // sources blocked on a full decode queue (backpressure)
+  std::atomic<int64_t> ns_lane_wait_{0};  // GPU-ingested fetches: received -> a lane took it
   int64_t replica_busy_ns() const;  // summed over replicas, up to now
   std::atomic<double> capacity_rps_{0.0};   // load-aware: measured capacity (images/s)
   std::atomic<int64_t> lag_rebalances_{0};  // rebalances this member triggered on its lag

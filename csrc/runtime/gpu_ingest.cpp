@@ -1,5 +1,6 @@
 // GpuIngest (see gpu_ingest.h / ingest.h).
 #include "gpu_ingest.h"
+#include "metrics.h"
 
 #include <string.h>
 
@@ -90,6 +91,7 @@ void GpuIngest::run(int lane, const kafka::Fetched& f, uint8_t* dev, size_t dev_
                     size_t arena_bytes) {
   Lane& L = *lanes_[(size_t)lane % lanes_.size()];
   std::lock_guard<std::mutex> lk(L.mu);
+  const int64_t t_start = mono_ns();
   const size_t nrec_all = f.records.size();
   io.images.assign(nrec_all, 0);
   io.cnt_off.assign(nrec_all, -1);
@@ -275,7 +277,12 @@ void GpuIngest::run(int lane, const kafka::Fetched& f, uint8_t* dev, size_t dev_
                                    d_pbad),
               "ingest: parse");
   check_hip(hipEventRecord(L.done, st), "ingest: event");
+  const int64_t t_wait = mono_ns();
   wait(L);
+  const int64_t t_post = mono_ns();
+  ++runs_;
+  prep_ns_ += t_wait - t_start;
+  wait_ns_ += t_post - t_wait;
   // ---- host: join the windows of each batch and compare; images from the element counts
   const uint32_t* crc = reinterpret_cast<const uint32_t*>(L.h_io + o_crc);
   for (size_t b = 0; b < batch_chunks.size(); ++b) {
@@ -330,6 +337,7 @@ void GpuIngest::run(int lane, const kafka::Fetched& f, uint8_t* dev, size_t dev_
       }
     }
   }
+  post_ns_ += mono_ns() - t_post;
 }
 
 }  // namespace gale

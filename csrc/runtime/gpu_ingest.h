@@ -27,6 +27,14 @@ class GpuIngest : public Ingest {
     text = text_bytes_.load();
     link = link_bytes_.load();
   }
+  Timing timing() const override {
+    Timing t;
+    t.runs = runs_.load();
+    t.prep_ns = prep_ns_.load();
+    t.wait_ns = wait_ns_.load();
+    t.post_ns = post_ns_.load();
+    return t;
+  }
 
  private:
   struct Lane {
@@ -50,6 +58,7 @@ class GpuIngest : public Ingest {
   void wait(Lane& L);
   int device_, poll_us_;
   std::atomic<int64_t> text_bytes_{0}, link_bytes_{0};
+  std::atomic<int64_t> runs_{0}, prep_ns_{0}, wait_ns_{0}, post_ns_{0};
   uint32_t* d_tables_ = nullptr;
   std::vector<std::unique_ptr<Lane>> lanes_;
   kafka::CrcShift shift_chunk_;

@@ -50,6 +50,12 @@ class Ingest {
   // fetched text bytes staged so far, and the bytes that crossed the host link for them (less
   // when the text is nibble-packed, csrc/codec/text_pack.h)
   virtual void link_bytes(int64_t& text, int64_t& link) const { text = link = 0; }
+  // per run(): host work before the device (plan), the wait for the device, host work after
+  // (verdicts), summed in ns over `runs` calls
+  struct Timing {
+    int64_t runs = 0, prep_ns = 0, wait_ns = 0, post_ns = 0;
+  };
+  virtual Timing timing() const { return Timing(); }
 };
 
 }  // namespace gale
