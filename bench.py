@@ -691,7 +691,10 @@ def size_pipeline(a, cpus: float) -> None:
         # profiles/archive/r3_decode_threads_ab.txt). With the parse at ingest (round 6) each
         # fetch holds its lane ~30 us longer: 10 lanes keep the ingest stage's p99 at 0.28-0.34 ms
         # against 0.42-0.92 ms with 6 (profiles/r6_ab_ingest_parse.jsonl); a lane mostly sleeps
-        a.decode_threads = (10 if a.ingest_parse else 6) if big else 2
+        # LeNet-5's fetches carry 4x the records per byte: its lanes queued (lane wait 0.5 ms
+        # per fetch in the latency window with 10, profiles/r6_ingest_breakdown.jsonl)
+        a.decode_threads = ((16 if a.model == "lenet5" else 10) if a.ingest_parse else 6) \
+            if big else 2
 
 
 def print_config(a) -> int:
