@@ -96,6 +96,34 @@ def test_resnet50_gemm_convs_match_conv_mfma_and_fp32():
     assert torch.allclose(a.sum(1), torch.ones(6), atol=1e-4)
 
 
+def test_resnet50_fused_projection_vs_layered(monkeypatch):
+    """OP_CONV_PROJ (conv3 + the strided projection shortcut as one GEMM, conv2d_gemm_proj)
+    against the layered plan (GALE_FUSE_PROJ=0: the projection is its own conv, stored as bf16,
+    and conv3 adds it). The fused epilogue adds the projection's fp32 accumulator unrounded
+    (conv_gemm.hip DUAL note), so the two agree to accumulation / one bf16 rounding of the
+    shortcut - well inside the bf16 budget - and both match the bf16 emulation."""
+    net = get_model("resnet50")
+    params = init_params(net, seed=31, calib_batch=4)
+    packed = materialize_weights(net, torch.device("cuda", 0), params=params)
+    x = torch.rand((5,) + net.input_shape, generator=torch.Generator().manual_seed(13))
+    monkeypatch.setenv("GALE_FUSE_PROJ", "1")
+    fused = ModelReplica(net, packed, max_batch=8, slots=1)
+    monkeypatch.setenv("GALE_FUSE_PROJ", "0")
+    layered = ModelReplica(net, packed, max_batch=8, slots=1)
+    assert sum(op["kind"] == 11 for op in fused.ops) == 3  # l2.0 / l3.0 / l4.0
+    assert not any(op["kind"] == 11 for op in layered.ops)
+    a = fused.infer_eager(x).cpu()
+    b = layered.infer_eager(x).cpu()
+    torch.cuda.synchronize()
+    folded = fold_params(net, params)
+    emu = forward(net, folded, x, bf16=True)
+    budget = rel_logit_err(emu, forward(net, folded, x)).max().item()
+    e_ab, e_emu = rel_logit_err(a, b).max().item(), rel_logit_err(a, emu).max().item()
+    print(f"\nresnet50 fused proj vs layered {e_ab:.2e}, vs bf16 emulation {e_emu:.2e} "
+          f"(budget {budget:.2e})")
+    assert e_ab < max(1e-2, 0.35 * budget) and e_emu < max(1e-2, 0.35 * budget)
+
+
 @pytest.mark.parametrize("end", ["l2.0.down", "l2.0.conv3"])
 def test_resnet50_batch_chunked_prefix_is_bit_identical(end, monkeypatch):
     """PlanSpec chunking (the leading layers run per chunk of images, the rest over the whole
