@@ -214,6 +214,9 @@ def parse_args(argv=None):
                          "wake-up per this many KB of a fetch response; 0 = per segment, -1 = "
                          "the bounce window with the bounce receive (profiles/"
                          "r4_ab_recv_lowat.jsonl)")
+    ap.add_argument("--ingest-dev-timing", type=int, default=16,
+                    help="time every N-th GPU ingest fetch of each lane on the device (events: "
+                         "H2D copies, count pass, parse; latency_ingest_device_us); 0 off")
     ap.add_argument("--partition-max-kb", type=int, default=8192,
                     help="consumer max.partition.fetch.bytes (KB): the most one partition's fetch "
                          "response carries - the records at its head wait for the whole of it")
@@ -514,6 +517,17 @@ def latency_phase(eng, broker, feeder, bset, parts, rate_img_s, a, ipr):
                                                round(v, 1) for k, v in d.items()}
         host["latency_ingest_us_per_fetch"]["records"] = round(
             (st1["ingested_records"] - st0["ingested_records"]) / nf, 1)
+        # device spans of a sample of the fetches (GALE_INGEST_DEV_TIMING): H2D copies, count
+        # pass, parse, and the rest of the same fetches' device wait (queueing behind other
+        # streams on the shared hardware queues + completion)
+        nd = st1.get("ingest_dev_runs", 0) - st0.get("ingest_dev_runs", 0)
+        if nd > 0:
+            dv = {k: (st1.get("ingest_dev_" + k + "_s", 0.0) - st0.get("ingest_dev_" + k + "_s", 0.0))
+                  / nd * 1e6 for k in ("copy", "count", "parse", "wait")}
+            host["latency_ingest_device_us"] = {
+                "sampled": int(nd), "copy": round(dv["copy"], 1), "count": round(dv["count"], 1),
+                "parse": round(dv["parse"], 1), "host_wait": round(dv["wait"], 1),
+                "other": round(dv["wait"] - dv["copy"] - dv["count"] - dv["parse"], 1)}
     tcp1 = _tcp_counters()
     host["latency_tcp"] = {k: tcp1[k] - tcp0.get(k, 0) for k in tcp1 if tcp1[k] != tcp0.get(k, 0)}
     rf.stop()
@@ -732,6 +746,8 @@ def main(argv=None) -> int:
         return print_config(a)
     if a.gpus > 1 and not a.single_process and "WORLD_SIZE" not in os.environ:
         return launch_ranks(a, argv)
+    if a.ingest_dev_timing > 0:
+        os.environ.setdefault("GALE_INGEST_DEV_TIMING", str(a.ingest_dev_timing))
     from gale.utils import (cpu_time_split, host_cpus_per_rank, thread_cpu_seconds,
                             thread_ctx_switches)
 
@@ -951,7 +967,7 @@ def main(argv=None) -> int:
         # every rank's own view, for the JSON line: its partitions, output partition, window,
         # images, host slice and busy cores (imbalance between ranks shows up here)
         mine = {"rank": rank, "partitions": my_parts, "output_partition": cfg.output_partition,
-                "timed_s": round(elapsed, 4), "images": int(images),
+                "timed_s": round(elapsed, 6), "images": int(images),
                 "img_s": round(images / max(elapsed, 1e-9), 1),
                 "cpus": _cpulist(pinned_cpus),
                 "cores": round(sum(cpu1[k] - cpu0[k] for k in cpu1) / max(elapsed, 1e-9), 2)}

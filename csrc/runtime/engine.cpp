@@ -1845,6 +1845,12 @@ std::map<std::string, double> Engine::stats() const {
       t.prep_ns += q.prep_ns;
       t.wait_ns += q.wait_ns;
       t.post_ns += q.post_ns;
+      t.dev_runs += q.dev_runs;
+      t.dev_copy_ns += q.dev_copy_ns;
+      t.dev_count_ns += q.dev_count_ns;
+      t.dev_parse_ns += q.dev_parse_ns;
+      t.dev_wait_ns += q.dev_wait_ns;
+      t.plan_in_chunk += q.plan_in_chunk;
     }
     // per fetch, microseconds: waiting for a lane, the lane's host work before / after the
     // device, and the device wait itself
@@ -1860,6 +1866,13 @@ std::map<std::string, double> Engine::stats() const {
     s["ingest_prep_s"] = (double)t.prep_ns * 1e-9;
     s["ingest_device_wait_s"] = (double)t.wait_ns * 1e-9;
     s["ingest_post_s"] = (double)t.post_ns * 1e-9;
+    // sampled device spans (GALE_INGEST_DEV_TIMING), running totals
+    s["ingest_plan_in_chunk"] = (double)t.plan_in_chunk;
+    s["ingest_dev_runs"] = (double)t.dev_runs;
+    s["ingest_dev_copy_s"] = (double)t.dev_copy_ns * 1e-9;
+    s["ingest_dev_count_s"] = (double)t.dev_count_ns * 1e-9;
+    s["ingest_dev_parse_s"] = (double)t.dev_parse_ns * 1e-9;
+    s["ingest_dev_wait_s"] = (double)t.dev_wait_ns * 1e-9;
   }
   s["eff_max_batch"] = (double)eff_batch_;
   s["eff_max_wait_us"] = (double)eff_wait_ns_ / 1000.0;

@@ -2,6 +2,7 @@
 #include "gpu_ingest.h"
 #include "metrics.h"
 
+#include <stdlib.h>
 #include <string.h>
 
 #include <chrono>
@@ -31,6 +32,10 @@ GpuIngest::GpuIngest(int device, int lanes, int poll_us)
     check_hip(hipEventCreateWithFlags(&L->done, hipEventDisableTiming), "ingest: event");
     lanes_.push_back(std::move(L));
   }
+  if (const char* e = getenv("GALE_INGEST_DEV_TIMING")) dev_every_ = std::max(0, atoi(e));
+  if (dev_every_ > 0)
+    for (auto& L : lanes_)
+      for (hipEvent_t& ev : L->tev) check_hip(hipEventCreate(&ev), "ingest: timing event");
 }
 
 GpuIngest::~GpuIngest() {
@@ -41,6 +46,8 @@ GpuIngest::~GpuIngest() {
     if (L->d_io) hipFree(L->d_io);
     if (L->d_counts) hipFree(L->d_counts);
     if (L->done) hipEventDestroy(L->done);
+    for (hipEvent_t ev : L->tev)
+      if (ev) hipEventDestroy(ev);
     if (L->stream) hipStreamDestroy(L->stream);
   }
   if (d_tables_) hipFree(d_tables_);
@@ -183,9 +190,21 @@ void GpuIngest::run(int lane, const kafka::Fetched& f, uint8_t* dev, size_t dev_
   const size_t io_bytes = o_pbad + align16((size_t)ptiles * 4);
   check_hip(hipSetDevice(device_), "ingest: hipSetDevice");
   grow(L, io_bytes + 16, ncnt + 1);
-  CrcChunk* hc = reinterpret_cast<CrcChunk*>(L.h_io + o_chunks);
-  int2* hg = reinterpret_cast<int2*>(L.h_io + o_groups);
-  JsonRecord* hr = reinterpret_cast<JsonRecord*>(L.h_io + o_recs);
+  // the plan part [0, o_gsum): written into the fetch's own pinned chunk, behind the bytes the
+  // copy moves anyway, when it fits before the counts (the chunk is pinned and mirrored at the
+  // same offsets), so ONE DMA carries text and plan; else into the lane's buffer, its own DMA.
+  // (Sampled device timing, GALE_INGEST_DEV_TIMING: the copies were the largest device span of
+  // a fetch, 40-60 us, mostly per-DMA latency - profiles/r6_ingest_device_split.jsonl)
+  // (past every byte of the fetch: host code may still read records this plan skips)
+  const size_t used = std::max((size_t)f.size, packed ? codec::pack_offset(span) + link : hi);
+  const size_t plan_off = (used + 255) & ~(size_t)255;
+  const size_t plan_lim = cnt_base >= 0 ? (size_t)cnt_base : dev_cap;
+  const bool plan_in_chunk = plan_off + o_gsum <= plan_lim;
+  uint8_t* hpl = plan_in_chunk ? f.buf.get() + plan_off : L.h_io;  // host view of the plan
+  uint8_t* dpl = plan_in_chunk ? dev + plan_off : L.d_io;          // device view
+  CrcChunk* hc = reinterpret_cast<CrcChunk*>(hpl + o_chunks);
+  int2* hg = reinterpret_cast<int2*>(hpl + o_groups);
+  JsonRecord* hr = reinterpret_cast<JsonRecord*>(hpl + o_recs);
   if (nc) memcpy(hc, chunks.data(), nc * sizeof(CrcChunk));
   int tile = 0, grp = 0;
   for (size_t j = 0; j < nr; ++j) {
@@ -208,8 +227,8 @@ void GpuIngest::run(int lane, const kafka::Fetched& f, uint8_t* dev, size_t dev_
     }
     tile += nt;
   }
-  JsonRecord* hp = reinterpret_cast<JsonRecord*>(L.h_io + o_precs);
-  int* hpt = reinterpret_cast<int*>(L.h_io + o_ptr);
+  JsonRecord* hp = reinterpret_cast<JsonRecord*>(hpl + o_precs);
+  int* hpt = reinterpret_cast<int*>(hpl + o_ptr);
   {
     int pt = 0;
     for (size_t k = 0; k < np; ++k) {
@@ -238,44 +257,53 @@ void GpuIngest::run(int lane, const kafka::Fetched& f, uint8_t* dev, size_t dev_
   // the plan and the step's metadata that way still stretched every kernel by 25-40 %
   // (profiles/r5_step_ab.txt).
   hipStream_t st = L.stream;
-  if (packed) {
-    memcpy(L.h_io, f.buf.get() + codec::tab_offset(span), ng * 2 * sizeof(uint32_t));
-    const size_t po = codec::pack_offset(span);
-    check_hip(hipMemcpyAsync(dev + po, f.buf.get() + po, link, hipMemcpyHostToDevice, st),
-              "ingest: H2D packed text");
+  const bool timed = dev_every_ > 0 && L.nrun++ % dev_every_ == 0;
+  if (timed) check_hip(hipEventRecord(L.tev[0], st), "ingest: timing event");
+  if (packed) memcpy(hpl, f.buf.get() + codec::tab_offset(span), ng * 2 * sizeof(uint32_t));
+  const size_t c_lo = packed ? codec::pack_offset(span) : lo;
+  const size_t c_len = packed ? link : span;
+  if (plan_in_chunk) {
+    check_hip(hipMemcpyAsync(dev + c_lo, f.buf.get() + c_lo, plan_off + o_gsum - c_lo,
+                             hipMemcpyHostToDevice, st),
+              "ingest: H2D text + plan");
   } else {
-    check_hip(hipMemcpyAsync(dev + lo, f.buf.get() + lo, span, hipMemcpyHostToDevice, st),
+    check_hip(hipMemcpyAsync(dev + c_lo, f.buf.get() + c_lo, c_len, hipMemcpyHostToDevice, st),
               "ingest: H2D text");
+    check_hip(hipMemcpyAsync(L.d_io, L.h_io, o_gsum, hipMemcpyHostToDevice, st),
+              "ingest: H2D plan");
   }
-  check_hip(hipMemcpyAsync(L.d_io, L.h_io, o_gsum, hipMemcpyHostToDevice, st), "ingest: H2D plan");
+  plan_in_chunk_ += plan_in_chunk;
+  if (timed) check_hip(hipEventRecord(L.tev[1], st), "ingest: timing event");
   text_bytes_ += (int64_t)span;
   link_bytes_ += (int64_t)link;
   uint32_t* d_crc = reinterpret_cast<uint32_t*>(L.h_io + o_crc);   // (host-mapped results)
   int* d_gsum = reinterpret_cast<int*>(L.h_io + o_gsum);
   int* d_gbad = reinterpret_cast<int*>(L.h_io + o_gbad);
   int* d_pbad = reinterpret_cast<int*>(L.h_io + o_pbad);
-  JsonRecord* d_rec = reinterpret_cast<JsonRecord*>(L.d_io + o_recs);
+  JsonRecord* d_rec = reinterpret_cast<JsonRecord*>(dpl + o_recs);
   int* d_cnt = cnt_base >= 0 ? reinterpret_cast<int*>(dev + cnt_base) : L.d_counts;
   // CRC windows and token counts: one launch, one pass of workgroups over the buffer. Packed,
   // the same launch expands the text: CRC and counting waves read the packed stream, and the
   // counting waves store each record's text into the mirror for the parse (r4 ran a separate
   // text_unpack pass over the whole body first: a third of the ingest launches, 16 % of the
   // GPU's busy time under the serving load, profiles/r5_step_ab.txt)
-  check_hip(ingest_crc_count(dev, reinterpret_cast<const CrcChunk*>(L.d_io + o_chunks), (int)nc,
+  check_hip(ingest_crc_count(dev, reinterpret_cast<const CrcChunk*>(dpl + o_chunks), (int)nc,
                              d_tables_, d_crc, (int)nr, ngroups, d_rec,
-                             reinterpret_cast<const int2*>(L.d_io + o_groups), d_cnt, d_gsum,
+                             reinterpret_cast<const int2*>(dpl + o_groups), d_cnt, d_gsum,
                              d_gbad, st, packed ? dev + codec::pack_offset(span) : nullptr,
-                             packed ? reinterpret_cast<const uint32_t*>(L.d_io) : nullptr,
+                             packed ? reinterpret_cast<const uint32_t*>(dpl) : nullptr,
                              packed ? dev : nullptr),
             "ingest: crc32c + count");
+  if (timed) check_hip(hipEventRecord(L.tev[2], st), "ingest: timing event");
   // the parse right behind it, same stream (the counts are in place when it starts): the text
   // -> fp32 images in the fetch's arena, so the batch step later runs only the forward
   if (np > 0)
-    check_hip(json_parse_instances((int)np, ptiles, reinterpret_cast<JsonRecord*>(L.d_io + o_precs),
-                                   reinterpret_cast<const int*>(L.d_io + o_ptr), dev, H, W, C,
+    check_hip(json_parse_instances((int)np, ptiles, reinterpret_cast<JsonRecord*>(dpl + o_precs),
+                                   reinterpret_cast<const int*>(dpl + o_ptr), dev, H, W, C,
                                    L.d_counts, arena, st, /*count_pass=*/false, nullptr, nullptr,
                                    d_pbad),
               "ingest: parse");
+  if (timed) check_hip(hipEventRecord(L.tev[3], st), "ingest: timing event");
   check_hip(hipEventRecord(L.done, st), "ingest: event");
   const int64_t t_wait = mono_ns();
   wait(L);
@@ -283,6 +311,16 @@ void GpuIngest::run(int lane, const kafka::Fetched& f, uint8_t* dev, size_t dev_
   ++runs_;
   prep_ns_ += t_wait - t_start;
   wait_ns_ += t_post - t_wait;
+  if (timed) {
+    float ms[3] = {0.f, 0.f, 0.f};
+    for (int k = 0; k < 3; ++k)
+      check_hip(hipEventElapsedTime(&ms[k], L.tev[k], L.tev[k + 1]), "ingest: event time");
+    ++dev_runs_;
+    dev_copy_ns_ += (int64_t)(ms[0] * 1e6);
+    dev_count_ns_ += (int64_t)(ms[1] * 1e6);
+    dev_parse_ns_ += (int64_t)(ms[2] * 1e6);
+    dev_wait_ns_ += t_post - t_wait;
+  }
   // ---- host: join the windows of each batch and compare; images from the element counts
   const uint32_t* crc = reinterpret_cast<const uint32_t*>(L.h_io + o_crc);
   for (size_t b = 0; b < batch_chunks.size(); ++b) {

@@ -33,6 +33,12 @@ class GpuIngest : public Ingest {
     t.prep_ns = prep_ns_.load();
     t.wait_ns = wait_ns_.load();
     t.post_ns = post_ns_.load();
+    t.dev_runs = dev_runs_.load();
+    t.dev_copy_ns = dev_copy_ns_.load();
+    t.dev_count_ns = dev_count_ns_.load();
+    t.dev_parse_ns = dev_parse_ns_.load();
+    t.dev_wait_ns = dev_wait_ns_.load();
+    t.plan_in_chunk = plan_in_chunk_.load();
     return t;
   }
 
@@ -53,12 +59,18 @@ class GpuIngest : public Ingest {
     size_t io_cap = 0;
     int* d_counts = nullptr;  // per-tile token counts (scratch)
     size_t counts_cap = 0;
+    hipEvent_t tev[4] = {nullptr, nullptr, nullptr, nullptr};  // sampled device timing
+    int64_t nrun = 0;
   };
   void grow(Lane& L, size_t io_bytes, size_t tiles);
   void wait(Lane& L);
   int device_, poll_us_;
   std::atomic<int64_t> text_bytes_{0}, link_bytes_{0};
   std::atomic<int64_t> runs_{0}, prep_ns_{0}, wait_ns_{0}, post_ns_{0};
+  std::atomic<int64_t> dev_runs_{0}, dev_copy_ns_{0}, dev_count_ns_{0}, dev_parse_ns_{0},
+      dev_wait_ns_{0};
+  int dev_every_ = 0;  // GALE_INGEST_DEV_TIMING
+  std::atomic<int64_t> plan_in_chunk_{0};
   uint32_t* d_tables_ = nullptr;
   std::vector<std::unique_ptr<Lane>> lanes_;
   kafka::CrcShift shift_chunk_;

@@ -52,8 +52,13 @@ class Ingest {
   virtual void link_bytes(int64_t& text, int64_t& link) const { text = link = 0; }
   // per run(): host work before the device (plan), the wait for the device, host work after
   // (verdicts), summed in ns over `runs` calls
+  // dev_*: a sample of the runs (GALE_INGEST_DEV_TIMING=N: every N-th run of a lane) timed on
+  // the device with events - the H2D copies, the count pass, the parse - and the host wait of
+  // the same runs, so (host wait - device spans) is queueing behind other streams + completion
   struct Timing {
     int64_t runs = 0, prep_ns = 0, wait_ns = 0, post_ns = 0;
+    int64_t dev_runs = 0, dev_copy_ns = 0, dev_count_ns = 0, dev_parse_ns = 0, dev_wait_ns = 0;
+    int64_t plan_in_chunk = 0;  // runs whose plan rode the text's DMA (one copy, not two)
   };
   virtual Timing timing() const { return Timing(); }
 };

@@ -216,6 +216,8 @@ def test_gpu_engine_matches_oracle(broker, model, ingest):
     st = eng.stats()
     assert st["errors"] == 1 and st["images_out"] == sum(counts)
     assert (st["ingested_records"] > 0) == bool(ingest)
+    # the ingest plan rides the text's DMA (written behind the fetch in its pinned chunk)
+    assert (st["ingest_plan_in_chunk"] > 0) == bool(ingest), st
     # every good record's images came parsed from the ingest arena (the step ran the forward
     # alone), unless the ingest parse is off or there is no GPU ingest
     want = len(counts) if ingest and ingest != "pack-noparse" else 0
