@@ -1,11 +1,13 @@
 // GpuReplica (see replica.h): staged JSON bytes -> GPU JSON parser -> hipGraph forward ->
 // softmax rows on the replica's own streams. Kept apart from the host-only replicas so the
 // sanitizer build of the host pipeline (make tsan / make asan) links no GPU code.
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
 #include <chrono>
 #include <thread>
+#include <vector>
 #include <stdexcept>
 
 #include "../codec/json_codec.h"
@@ -36,6 +38,16 @@ GpuReplica::GpuReplica(std::shared_ptr<Executor> exec, int H, int W, int C, int 
     check_hip(hipDeviceGetStreamPriorityRange(&least, &greatest), "stream priority range");
     check_hip(hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, greatest),
               "hipStreamCreateWithPriority");
+  } else if (const char* e = getenv("GALE_REPLICA_CU_RESERVE"); e && atoi(e) > 0) {
+    // (A/B) the replica's kernels kept off the last N CUs, which the GPU ingest's passes then
+    // find free instead of queueing behind whole-chip forward batches
+    hipDeviceProp_t prop;
+    check_hip(hipGetDeviceProperties(&prop, exec_->device()), "hipGetDeviceProperties");
+    const int cus = prop.multiProcessorCount, keep = std::max(1, cus - atoi(e));
+    std::vector<uint32_t> mask((size_t)(cus + 31) / 32, 0u);
+    for (int i = 0; i < keep; ++i) mask[(size_t)i / 32] |= 1u << (i % 32);
+    check_hip(hipExtStreamCreateWithCUMask(&stream_, (uint32_t)mask.size(), mask.data()),
+              "hipExtStreamCreateWithCUMask");
   } else {
     check_hip(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "hipStreamCreate");
   }

@@ -396,8 +396,11 @@ def test_load_aware_assignment_sheds_a_slow_members_partitions(tmp_path):
     fast_parts = sum(len(last[n]["partitions"]) for n in ("F1", "F2"))
     assert fast_parts >= 10, last
     total_lag_aware = sum(aware[n][-2]["lag_records"] for n in aware)
-    ctrl_s = ctrl["S"][-2]
-    assert len(ctrl_s["partitions"]) == 4
+    # (S's last line of the 3-member range assignment: on a loaded host the fast members can
+    # finish their --duration first, and S's final lines then hold all 12 partitions)
+    held4 = [ln for ln in ctrl["S"][:-1] if len(ln["partitions"]) == 4]
+    assert held4, ctrl["S"][-2]
+    ctrl_s = held4[-1]
     # static: the slow member falls behind by up to ~1000 records/s (less on a loaded host, where
     # the feeder and the stubs share the CPUs); load-aware: the group keeps up
     assert ctrl_s["lag_records"] > 3000, ctrl_s
