@@ -2,6 +2,8 @@
 # A/B: the ingest lane's completion wait - a first sleep of ~80 % of the lane's expected device
 # time, then 5 us polls (default) vs 20 us polls from the start (GALE_INGEST_POLL_PREDICT=0).
 # Config 2 and config 1, interleaved.
+# (The predictive wait was not kept: GALE_INGEST_POLL_PREDICT no longer exists, both arms now
+# run the same code. Results: profiles/r6_ab_ingest_poll.jsonl.)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 out=gpurun_out/r6w
