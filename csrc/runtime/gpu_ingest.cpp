@@ -33,6 +33,8 @@ GpuIngest::GpuIngest(int device, int lanes, int poll_us)
     lanes_.push_back(std::move(L));
   }
   if (const char* e = getenv("GALE_INGEST_DEV_TIMING")) dev_every_ = std::max(0, atoi(e));
+  // (tests: the plan's own DMA, the path of a fetch whose plan does not fit behind it)
+  if (const char* e = getenv("GALE_INGEST_PLAN_SEPARATE")) plan_separate_ = atoi(e) != 0;
   if (dev_every_ > 0)
     for (auto& L : lanes_)
       for (hipEvent_t& ev : L->tev) check_hip(hipEventCreate(&ev), "ingest: timing event");
@@ -199,7 +201,7 @@ void GpuIngest::run(int lane, const kafka::Fetched& f, uint8_t* dev, size_t dev_
   const size_t used = std::max((size_t)f.size, packed ? codec::pack_offset(span) + link : hi);
   const size_t plan_off = (used + 255) & ~(size_t)255;
   const size_t plan_lim = cnt_base >= 0 ? (size_t)cnt_base : dev_cap;
-  const bool plan_in_chunk = plan_off + o_gsum <= plan_lim;
+  const bool plan_in_chunk = !plan_separate_ && plan_off + o_gsum <= plan_lim;
   uint8_t* hpl = plan_in_chunk ? f.buf.get() + plan_off : L.h_io;  // host view of the plan
   uint8_t* dpl = plan_in_chunk ? dev + plan_off : L.d_io;          // device view
   CrcChunk* hc = reinterpret_cast<CrcChunk*>(hpl + o_chunks);

@@ -70,6 +70,7 @@ class GpuIngest : public Ingest {
   std::atomic<int64_t> dev_runs_{0}, dev_copy_ns_{0}, dev_count_ns_{0}, dev_parse_ns_{0},
       dev_wait_ns_{0};
   int dev_every_ = 0;  // GALE_INGEST_DEV_TIMING
+  bool plan_separate_ = false;  // GALE_INGEST_PLAN_SEPARATE
   std::atomic<int64_t> plan_in_chunk_{0};
   uint32_t* d_tables_ = nullptr;
   std::vector<std::unique_ptr<Lane>> lanes_;

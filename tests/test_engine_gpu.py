@@ -166,8 +166,9 @@ def centered_log(p):
 @pytest.mark.parametrize("model,ingest", [("resnet20", True), ("resnet20", False),
                                           ("lenet5", True), ("resnet20", "pack"),
                                           ("resnet20", "pack-inplace"), ("lenet5", "pack"),
-                                          ("resnet20", "pack-noparse")])
-def test_gpu_engine_matches_oracle(broker, model, ingest):
+                                          ("resnet20", "pack-noparse"),
+                                          ("resnet20", "pack-plan-dma")])
+def test_gpu_engine_matches_oracle(broker, model, ingest, monkeypatch):
     """Every output record is matched to ITS input by key (output_key=input) and compared on
     logits (centered log-softmax) with a bf16-level relative tolerance: a misrouted batch split
     (image i's row under record j) or a wrong image count cannot pass. ingest=True: CRC32C and
@@ -175,8 +176,12 @@ def test_gpu_engine_matches_oracle(broker, model, ingest):
     host decode path with per-batch H2D staging; "pack": GPU ingest of nibble-packed fetch
     bodies (the source's PackTap, expanded on the device before the CRC / count / parse).
     With GPU ingest the records are parsed into the fetch's image arena by the ingest pass and
-    the batch step runs the forward alone ("pack-noparse": the step parses, as in round 5)."""
-    pack = ingest in ("pack", "pack-inplace", "pack-noparse")
+    the batch step runs the forward alone ("pack-noparse": the step parses, as in round 5).
+    "pack-plan-dma": the ingest plan takes its own DMA instead of riding the text's (the path a
+    fetch takes when the plan does not fit behind it in its chunk)."""
+    pack = ingest in ("pack", "pack-inplace", "pack-noparse", "pack-plan-dma")
+    if ingest == "pack-plan-dma":
+        monkeypatch.setenv("GALE_INGEST_PLAN_SEPARATE", "1")
     if pack and not C.text_pack_fast():
         pytest.skip("no AVX-512 VBMI on this host")
     net = get_model(model)
@@ -217,7 +222,7 @@ def test_gpu_engine_matches_oracle(broker, model, ingest):
     assert st["errors"] == 1 and st["images_out"] == sum(counts)
     assert (st["ingested_records"] > 0) == bool(ingest)
     # the ingest plan rides the text's DMA (written behind the fetch in its pinned chunk)
-    assert (st["ingest_plan_in_chunk"] > 0) == bool(ingest), st
+    assert (st["ingest_plan_in_chunk"] > 0) == (bool(ingest) and ingest != "pack-plan-dma"), st
     # every good record's images came parsed from the ingest arena (the step ran the forward
     # alone), unless the ingest parse is off or there is no GPU ingest
     want = len(counts) if ingest and ingest != "pack-noparse" else 0
