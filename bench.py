@@ -511,7 +511,8 @@ def latency_phase(eng, broker, feeder, bset, parts, rate_img_s, a, ipr):
     nf = st1.get("ingest_fetches", 0) - st0.get("ingest_fetches", 0)
     if nf > 0:
         d = {k: (st1.get(k, 0.0) - st0.get(k, 0.0)) / nf * 1e6 for k in (
-            "ingest_lane_wait_s", "ingest_prep_s", "ingest_device_wait_s", "ingest_post_s")}
+            "ingest_lane_wait_s", "ingest_prep_s", "ingest_plan_s", "ingest_device_wait_s",
+            "ingest_post_s")}
         d["lane_turn"] = (st1["thread_s_ingest"] - st0["thread_s_ingest"]) / nf * 1e6
         host["latency_ingest_us_per_fetch"] = {k.replace("ingest_", "").replace("_s", ""):
                                                round(v, 1) for k, v in d.items()}
@@ -704,9 +705,10 @@ def size_pipeline(a, cpus: float) -> None:
         # throughput in 5 of 6 interleaved pairs on two boxes, p50 unchanged; see
         # profiles/archive/r3_decode_threads_ab.txt). With the parse at ingest (round 6) each
         # fetch holds its lane ~30 us longer: 10 lanes keep the ingest stage's p99 at 0.28-0.34 ms
-        # against 0.42-0.92 ms with 6 (profiles/r6_ab_ingest_parse.jsonl); a lane mostly sleeps
-        # LeNet-5's fetches carry 4x the records per byte: its lanes queued (lane wait 0.5 ms
-        # per fetch in the latency window with 10, profiles/r6_ingest_breakdown.jsonl)
+        # against 0.42-0.92 ms with 6 (profiles/r6_ab_ingest_parse.jsonl); a lane mostly sleeps.
+        # LeNet-5's fetches carry 4x the records per byte: its lanes queued (lane wait 0.34-0.74
+        # ms per fetch in the latency window with 10 against 0.01-0.16 ms with 16,
+        # profiles/r6_ingest_breakdown.jsonl)
         a.decode_threads = ((16 if a.model == "lenet5" else 10) if a.ingest_parse else 6) \
             if big else 2
 

@@ -1843,6 +1843,7 @@ std::map<std::string, double> Engine::stats() const {
       const Ingest::Timing q = kv.second->timing();
       t.runs += q.runs;
       t.prep_ns += q.prep_ns;
+      t.plan_ns += q.plan_ns;
       t.wait_ns += q.wait_ns;
       t.post_ns += q.post_ns;
       t.dev_runs += q.dev_runs;
@@ -1864,6 +1865,7 @@ std::map<std::string, double> Engine::stats() const {
     // the same as running totals (s), for per-window deltas
     s["ingest_lane_wait_s"] = (double)ns_lane_wait_ * 1e-9;
     s["ingest_prep_s"] = (double)t.prep_ns * 1e-9;
+    s["ingest_plan_s"] = (double)t.plan_ns * 1e-9;
     s["ingest_device_wait_s"] = (double)t.wait_ns * 1e-9;
     s["ingest_post_s"] = (double)t.post_ns * 1e-9;
     // sampled device spans (GALE_INGEST_DEV_TIMING), running totals

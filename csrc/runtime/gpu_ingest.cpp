@@ -259,6 +259,7 @@ void GpuIngest::run(int lane, const kafka::Fetched& f, uint8_t* dev, size_t dev_
   // the plan and the step's metadata that way still stretched every kernel by 25-40 %
   // (profiles/r5_step_ab.txt).
   hipStream_t st = L.stream;
+  const int64_t t_plan = mono_ns();  // plan built; the HIP calls follow
   const bool timed = dev_every_ > 0 && L.nrun++ % dev_every_ == 0;
   if (timed) check_hip(hipEventRecord(L.tev[0], st), "ingest: timing event");
   if (packed) memcpy(hpl, f.buf.get() + codec::tab_offset(span), ng * 2 * sizeof(uint32_t));
@@ -312,6 +313,7 @@ void GpuIngest::run(int lane, const kafka::Fetched& f, uint8_t* dev, size_t dev_
   const int64_t t_post = mono_ns();
   ++runs_;
   prep_ns_ += t_wait - t_start;
+  plan_ns_ += t_plan - t_start;
   wait_ns_ += t_post - t_wait;
   if (timed) {
     float ms[3] = {0.f, 0.f, 0.f};

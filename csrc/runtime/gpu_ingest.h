@@ -31,6 +31,7 @@ class GpuIngest : public Ingest {
     Timing t;
     t.runs = runs_.load();
     t.prep_ns = prep_ns_.load();
+    t.plan_ns = plan_ns_.load();
     t.wait_ns = wait_ns_.load();
     t.post_ns = post_ns_.load();
     t.dev_runs = dev_runs_.load();
@@ -66,7 +67,7 @@ class GpuIngest : public Ingest {
   void wait(Lane& L);
   int device_, poll_us_;
   std::atomic<int64_t> text_bytes_{0}, link_bytes_{0};
-  std::atomic<int64_t> runs_{0}, prep_ns_{0}, wait_ns_{0}, post_ns_{0};
+  std::atomic<int64_t> runs_{0}, prep_ns_{0}, plan_ns_{0}, wait_ns_{0}, post_ns_{0};
   std::atomic<int64_t> dev_runs_{0}, dev_copy_ns_{0}, dev_count_ns_{0}, dev_parse_ns_{0},
       dev_wait_ns_{0};
   int dev_every_ = 0;  // GALE_INGEST_DEV_TIMING

@@ -57,6 +57,7 @@ class Ingest {
   // the same runs, so (host wait - device spans) is queueing behind other streams + completion
   struct Timing {
     int64_t runs = 0, prep_ns = 0, wait_ns = 0, post_ns = 0;
+    int64_t plan_ns = 0;  // the part of prep_ns before the first HIP call (the rest: HIP API)
     int64_t dev_runs = 0, dev_copy_ns = 0, dev_count_ns = 0, dev_parse_ns = 0, dev_wait_ns = 0;
     int64_t plan_in_chunk = 0;  // runs whose plan rode the text's DMA (one copy, not two)
   };
