@@ -3,6 +3,8 @@
 # workgroup per CU) vs two (default): single-layer times (tools/bench_conv.py, batch 256 and
 # 128), the ResNet-50 forward (tools/bench_forward.py), and the model numerics under the
 # three-stage form.
+# (The three-stage form was not kept: GALE_CONV_STAGES no longer exists, both arms now run the
+# same code. Results: profiles/r6_conv_stages_ab.jsonl.)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 out=gpurun_out/r6s
