@@ -34,6 +34,8 @@
 // Reference parity: the model the reference serves is an opaque SavedModel fetched as
 // "output/Softmax:0" (InferenceBolt.java:81-86); numerics equal the layer-by-layer gale plan
 // (same rounding points) and are checked against the fp32 / fp8-emulation oracles in tests.
+#include <stdlib.h>
+
 #include "common.cuh"
 #include "gale/kernels.h"
 #include "java_float.cuh"
@@ -626,12 +628,19 @@ hipError_t resnet20_fused_forward(const ResNet20Params& p, int batch, const floa
   }();
   // resident workgroups per CU: 2 of 4 waves (bf16: LDS bound; fp8: register bound — its 39 KB
   // of LDS would allow 4, but the hoisted A fragments need more than 128 VGPRs per lane), or 1 of
-  // 8 waves. bf16 with no more images than CUs: the 8-wave form (each image gets twice the
-  // waves, weights prefetched into LDS; measured 62.3 -> 58.0 us at batch 1,
-  // profiles/archive/r1_resnet20_waves_ab.txt). fp8 stays on 4 waves (its 8-wave form measured slower in
-  // round 1 and equal after the round-3 LDS layout fix: 50.9 / 53.1 vs 50.7 / 52.7 us at batch
-  // 64 / 256, profiles/archive/r3_resnet20_fp8_lds.txt).
-  const int nw = !f8 && batch <= cus ? 8 : 4;
+  // 8 waves. The 4-wave form is the default for both: alone a bf16 batch of <= 256 images is
+  // ~8 % faster on 8 waves (52.6 vs 56.9 us at 256; weights prefetched into LDS), but that
+  // workgroup takes a CU's whole register file and ~150 KB of its LDS, so nothing else runs
+  // beside it. On 4 waves (one per SIMD, 77 KB) two batches share the CUs (2 in flight: 36.6 vs
+  // 52.6 us per batch) and the GPU ingest's passes run beside a forward (count / parse 18-21 /
+  // 22-25 us vs 25-30 / 27-31 us per fetch under load); config 2 end to end: img/s higher in 4
+  // of 6 interleaved pairs, p50 equal (profiles/r6_ab_r20_waves.jsonl). GALE_R20_WAVES=8 selects
+  // the 8-wave form for bf16 batches of at most one image per CU (A/B).
+  static const bool want8 = [] {
+    const char* e = getenv("GALE_R20_WAVES");
+    return e && atoi(e) == 8;
+  }();
+  const int nw = !f8 && batch <= cus && want8 ? 8 : 4;
   const int grid_cap = nw == 8 ? cus : 2 * cus;
   const int grid = batch < grid_cap ? batch : grid_cap;
   const size_t lds = (size_t)kElems * (f8 ? 1 : 2) + (nw == 8 ? (size_t)kWeightLdsBytes : 0);
