@@ -708,8 +708,10 @@ def size_pipeline(a, cpus: float) -> None:
         # against 0.42-0.92 ms with 6 (profiles/r6_ab_ingest_parse.jsonl); a lane mostly sleeps.
         # LeNet-5's fetches carry 4x the records per byte: its lanes queued (lane wait 0.34-0.74
         # ms per fetch in the latency window with 10 against 0.01-0.16 ms with 16,
-        # profiles/r6_ingest_breakdown.jsonl)
-        a.decode_threads = ((16 if a.model == "lenet5" else 10) if a.ingest_parse else 6) \
+        # profiles/r6_ingest_breakdown.jsonl). With the 4-wave ResNet-20 forward, 12 lanes
+        # beat 10 in 5 of 6 interleaved pairs on two boxes (median 2.24 vs 2.13 M img/s, p50
+        # equal; profiles/r6_ab_lanes.jsonl)
+        a.decode_threads = ((16 if a.model == "lenet5" else 12) if a.ingest_parse else 6) \
             if big else 2
 
 
