@@ -16,6 +16,7 @@ threads all run natively; Python only starts/stops the engine and reads its metr
 
 from __future__ import annotations
 
+import os
 from typing import Dict, List, Optional, Sequence
 
 from gale._native import native
@@ -102,8 +103,10 @@ class Engine:
             # one lane (stream + staging) per thread that runs the ingest: the decode workers,
             # or the sources themselves when there are none
             lanes = cfg.decode_threads if cfg.decode_threads > 0 else cfg.source_parallelism
+            # the lanes sleep-poll their fetch's completion every 20 us (GALE_INGEST_POLL_US, A/B)
+            poll_us = int(os.environ.get("GALE_INGEST_POLL_US", "20"))
             for dev in devs:
-                self._native.enable_gpu_ingest(dev, max(1, lanes), 20)
+                self._native.enable_gpu_ingest(dev, max(1, lanes), poll_us)
 
     def _build_gpu_replicas(self, devices: Optional[Sequence[int]], params: Optional[dict]):
         import torch
